@@ -1,0 +1,230 @@
+/*
+ * rs_capi.h — C-ABI of the MI355X-native CTR forward path (librs_hip.so).
+ *
+ * This is the drop-in boundary that replaces the TF/Keras ops used by the
+ * reference's embedding-lookup + feature-interaction forward path
+ * (Hcyand/recommender_system, algorithm/deep_learning/...).  Every entry point
+ * below cites the reference interface it replaces.  The Python host layer
+ * (recommender_system_amd/layers.py, models.py) mirrors the reference's Keras
+ * Layer/Model API on top of these functions; any other host (ctypes, cgo, JNI)
+ * binds the same symbols.
+ *
+ * Conventions
+ *  - All tensors are caller-owned DEVICE pointers (HBM), row-major, contiguous
+ *    unless a *_stride argument says otherwise (strides are in ELEMENTS).
+ *  - Sizes are int64_t; small shape parameters are int.
+ *  - Every function is stream-ordered on `stream` (a hipStream_t passed as
+ *    void*; NULL = the legacy default stream), never allocates, never
+ *    synchronises, and is safe to capture into a hipGraph.
+ *  - Return value: RS_OK (0) or a negative rs_status; the message for the last
+ *    failure on the calling thread is available from rs_last_error_string().
+ *  - Sparse ids: `id_kind` selects int32 / int64 / float32.  float32 ids follow
+ *    the reference's packed input X[B,39] (model/deepFM.py:24), where Keras'
+ *    Embedding casts float ids to int32 by truncation.  An id outside
+ *    [0, vocab_c) is an error in the reference (TF InvalidArgumentError on CPU);
+ *    here the kernel reads a zero row instead and sets *err_flag = 1 (if
+ *    err_flag != NULL), which the host layer turns into IndexError.
+ */
+#ifndef RS_CAPI_H
+#define RS_CAPI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* rs_stream_t; /* hipStream_t */
+
+enum rs_status {
+  RS_OK = 0,
+  RS_ERR_ARG = -1,         /* bad shape / null pointer / unsupported combination */
+  RS_ERR_HIP = -2,         /* HIP launch or runtime error */
+  RS_ERR_UNSUPPORTED = -3  /* valid request, no kernel for it in this build */
+};
+
+enum rs_id_kind { RS_ID_I32 = 0, RS_ID_I64 = 1, RS_ID_F32 = 2 };
+
+enum rs_act {
+  RS_ACT_NONE = 0,
+  RS_ACT_RELU = 1,
+  RS_ACT_PRELU = 2,   /* max(0,x) + alpha*min(0,x); alpha per output column  */
+  RS_ACT_SIGMOID = 3
+};
+
+/* ------------------------------------------------------------------ meta */
+const char* rs_version(void);
+const char* rs_last_error_string(void);
+
+/* --------------------------------------------------------- embedding (a3)
+ * Replaces EmbedLayer.call (layer/core.py:273-280) + the dense/sparse concat of
+ * DeepFM.call / DCN.call (model/deepFM.py:24-26, model/dcn.py:25-27):
+ *   out[b, 0:nd]               = dense[b, 0:nd]
+ *   out[b, nd + c*k + j]       = table[field_offsets[c] + id(b,c), j]
+ * One contiguous table holds every field's Keras `Embedding` matrix stacked
+ * (field c occupies rows [field_offsets[c], field_offsets[c]+field_vocab[c])).
+ * nd may be 0 (dense may then be NULL): the result is EmbedLayer's [B, F*k].
+ * field_offsets / field_vocab are device int64[F].                          */
+int rs_embed_gather(const void* ids, int id_kind, int64_t id_stride,
+                    const float* dense, int64_t dense_stride, int nd,
+                    const float* table, const int64_t* field_offsets,
+                    const int64_t* field_vocab, int n_fields, int k,
+                    float* out, int64_t out_stride, int64_t batch,
+                    int* err_flag, rs_stream_t stream);
+
+/* ---------------------------------------------------- FM second order (a5)
+ * FMLayer.call (layer/interaction.py:106-114) on x = [dense | emb] with
+ * d = nd + F*k, weights w0:(1,), w1:(d,1), v:(d,kfm):
+ *   y[b] = x@w1 + w0 + 0.5*sum_f((x@v)_f^2 - (x^2 @ v^2)_f)
+ * The kernels consume a packed weight image built once per weight set by
+ * rs_fm_prepare (MFMA operand order + per-row squared norms of v); query its
+ * size in floats with rs_fm_prepared_size.                                   */
+int64_t rs_fm_prepared_size(int nd, int n_fields, int k, int kfm);
+int rs_fm_prepare(const float* w1, const float* v, int nd, int n_fields, int k,
+                  int kfm, float* prepared, rs_stream_t stream);
+
+/* Fused EmbedLayer + concat + FMLayer (the headline kernel; DeepFM semantics,
+ * model/deepFM.py:24-28).  logit[b] = FMLayer(x)[b]; if x_out != NULL the
+ * concatenated x[B,d] (row stride d) is also written for the DNN tower.      */
+int rs_embed_fm_fwd(const void* ids, int id_kind, int64_t id_stride,
+                    const float* dense, int64_t dense_stride, int nd,
+                    const float* table, const int64_t* field_offsets,
+                    const int64_t* field_vocab, int n_fields, int k,
+                    const float* prepared, const float* w0, int kfm,
+                    float* logit, float* x_out, int64_t batch, int* err_flag,
+                    rs_stream_t stream);
+
+/* FMLayer on an arbitrary dense x[B,n] (layer/interaction.py:106-114), e.g.
+ * the FM model's one-hot input (model/fm.py:19-23).  `prepared` comes from
+ * rs_fm_prepare(w1, v, n, 0, 0, kfm, ...).                                   */
+int rs_fm_fwd(const float* x, int64_t x_stride, int n, const float* prepared,
+              const float* w0, int kfm, float* logit, int64_t batch,
+              rs_stream_t stream);
+
+/* FM model on the compact form of its one-hot input (model/fm.py:19-23 with
+ * utils/dataset.py:47-48): x = [dense(nd) | onehot], where the one-hot block
+ * has exactly one 1 per field at column nd + field_offsets[c] + id(b,c).
+ * Gathers rows of v and w1 instead of multiplying by zeros.                  */
+int rs_fm_onehot_fwd(const void* ids, int id_kind, int64_t id_stride,
+                     const float* dense, int64_t dense_stride, int nd,
+                     const int64_t* field_offsets, const int64_t* field_vocab,
+                     int n_fields, const float* w1, const float* w0,
+                     const float* v, int kfm, float* logit, int64_t batch,
+                     int* err_flag, rs_stream_t stream);
+
+/* ------------------------------------------------------ DCN CrossNet (a9)
+ * CrossLayer.call (layer/interaction.py:75-83):
+ *   x_{l+1} = x0 * (x_l^T w_l) + b_l + x_l,  l = 0..L-1,  out = x_L
+ * w, b: [L, d] (Keras shapes (d,1) each, stacked).  The L contractions
+ * x0^T w_l run on fp32 MFMA; `prepared` (rs_cross_prepared_size floats) holds
+ * the packed weights and the sample-independent bias terms.                  */
+int64_t rs_cross_prepared_size(int d, int n_layers);
+int rs_cross_prepare(const float* w, const float* b, int d, int n_layers,
+                     float* prepared, rs_stream_t stream);
+int rs_cross_fwd(const float* x0, int64_t x_stride, int d, int n_layers,
+                 const float* prepared, float* out, int64_t out_stride,
+                 int64_t batch, rs_stream_t stream);
+
+/* ----------------------------------------------- PNN inner product (a11)
+ * InnerProductLayer.call (layer/interaction.py:170-183) on e[B,F,k]:
+ *   out[b,p] = <e[b,i_p,:], e[b,j_p,:]>, pairs (i<j) in row-major order.
+ * out row stride is out_stride (>= F(F-1)/2).                               */
+int rs_inner_product_fwd(const float* emb, int n_fields, int k, float* out,
+                         int64_t out_stride, int64_t batch, rs_stream_t stream);
+
+/* Fused gather + flatten + inner product: writes the PNN DNN input
+ * out[b] = [flat_emb (F*k) | inner (F(F-1)/2)] (model/pnn.py:34-41).       */
+int rs_embed_inner_fwd(const void* ids, int id_kind, int64_t id_stride,
+                       const float* table, const int64_t* field_offsets,
+                       const int64_t* field_vocab, int n_fields, int k,
+                       float* out, int64_t out_stride, int64_t batch,
+                       int* err_flag, rs_stream_t stream);
+
+/* ---------------------------------------------- DIN attention unit (a13)
+ * Attention.call (layer/interaction.py:369-406), 'prelu' mode:
+ *   e_t   = [q, key_t, q-key_t, q*key_t]                         (4k)
+ *   h1_t  = PReLU_{alpha1[t]}(e_t @ W1 + b1)                     (H1)
+ *   h2_t  = PReLU_{alpha2[t]}(h1_t @ W2 + b2)                    (H2)
+ *   s_t   = h2_t @ w3 + b3;  s_t = -4294967296 where mask[b,t]==0
+ *   out   = softmax_t(s) @ value                                 (k)
+ * W1 [4k,H1], W2 [H1,H2], w3 [H2], alpha1 [T,H1], alpha2 [T,H2] (Keras
+ * PReLU inside Dense on a 3-D input: alpha shape input_shape[1:]).
+ * `mask` is float [B,T] (0 = padded).  Supported: k in {4,8,16,32},
+ * H1,H2 <= 128.                                                              */
+int rs_din_attention_fwd(const float* query, const float* keys,
+                         const float* values, const float* mask, int T, int k,
+                         const float* W1, const float* b1, const float* alpha1,
+                         int H1, const float* W2, const float* b2,
+                         const float* alpha2, int H2, const float* w3,
+                         const float* b3, float* out, int64_t batch,
+                         rs_stream_t stream);
+
+/* Attention.call 'dice' mode (layer/interaction.py:363-364, 410-425): the
+ * activation stack is n_dice Dice layers applied to e_t (no Dense), then
+ * Dense(1).  Dice at inference: xhat=(x-mean)/sqrt(var+eps), p=sigmoid(xhat),
+ * y = alpha*(1-p)*x + p*x; per-layer mean/var/alpha are [n_dice, 4k].        */
+int rs_din_attention_dice_fwd(const float* query, const float* keys,
+                              const float* values, const float* mask, int T,
+                              int k, int n_dice, const float* dice_alpha,
+                              const float* dice_mean, const float* dice_var,
+                              float dice_eps, const float* w_out,
+                              const float* b_out, float* out, int64_t batch,
+                              rs_stream_t stream);
+
+/* --------------------------------------------------- dense tower (a7, a15)
+ * Keras Dense: y = act(x @ W + bias), W:[K,N] (Keras (in,out) orientation),
+ * fp32 MFMA.  alpha: per-column PReLU slope (RS_ACT_PRELU only).            */
+int rs_dense_fwd(const float* x, int64_t x_stride, const float* W,
+                 const float* bias, const float* alpha, int act, float* y,
+                 int64_t y_stride, int64_t M, int K, int N, rs_stream_t stream);
+
+/* Per-column affine + activation, in place allowed: y = act(x*scale + shift).
+ * Used for BatchNormalization at inference (model/din.py:89).               */
+int rs_affine_act(const float* x, int64_t x_stride, const float* scale,
+                  const float* shift, const float* alpha, int act, float* y,
+                  int64_t y_stride, int64_t M, int N, rs_stream_t stream);
+
+/* Dice at inference on a 2-D input (layer/interaction.py:410-425), per column
+ * n: xhat = (x-mean[n])/sqrt(var[n]+eps), p = sigmoid(xhat),
+ *    y = alpha[n]*(1-p)*x + p*x.  Used for DIN's dnn_activation='dice'.     */
+int rs_dice_fwd(const float* x, int64_t x_stride, const float* mean,
+                const float* var, float eps, const float* alpha, float* y,
+                int64_t y_stride, int64_t M, int N, rs_stream_t stream);
+
+/* Model heads: out[b] = sigmoid(c0*a[b] + c1*b[b]) (b may be NULL).
+ * DeepFM: sigmoid(0.5*(fm+dnn)) (model/deepFM.py:30).                       */
+int rs_sigmoid_combine(const float* a, const float* b, float c0, float c1,
+                       float* out, int64_t n, rs_stream_t stream);
+
+/* -------------------------------------- row-sharded lookup (§8(e), cfg 5)
+ * Global row of (b,c) = field_offsets[c] + id(b,c).  Rows are split across
+ * `world` ranks in blocks of `rows_per_rank` (owner = row / rows_per_rank).
+ *  rs_shard_bucketize: counts[r] = #lookups owned by rank r; perm[i] = the
+ *   position of lookup i (= b*F + c) in owner-major order; send_rows[perm[i]]
+ *   = local row index on the owner.  Stable within each owner.
+ *   workspace: rs_shard_workspace_size(batch*n_fields, world) bytes, device.
+ *  rs_gather_rows: out[i] = table[rows[i]] (k floats), local shard.
+ *  rs_unpermute_rows: dst[i] = src[perm[i]] (k floats per row).            */
+int64_t rs_shard_workspace_size(int64_t n_lookups, int world);
+int rs_shard_bucketize(const void* ids, int id_kind, int64_t id_stride,
+                       const int64_t* field_offsets, const int64_t* field_vocab,
+                       int n_fields, int64_t batch, int64_t rows_per_rank,
+                       int world, int32_t* counts, int32_t* perm,
+                       int32_t* send_rows, void* workspace, int* err_flag,
+                       rs_stream_t stream);
+int rs_gather_rows(const float* table, int64_t n_rows, int k,
+                   const int32_t* rows, int64_t n, float* out, int* err_flag,
+                   rs_stream_t stream);
+int rs_unpermute_rows(const float* src, const int32_t* perm, int k, int64_t n,
+                      float* dst, rs_stream_t stream);
+
+/* FM over pre-gathered rows (sharded path): emb is [B, F*k] in x order.     */
+int rs_rows_fm_fwd(const float* emb, const float* dense, int64_t dense_stride,
+                   int nd, int n_fields, int k, const float* prepared,
+                   const float* w0, int kfm, float* logit, int64_t batch,
+                   rs_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RS_CAPI_H */

@@ -1,0 +1,324 @@
+"""CPU oracle for the CTR forward path — TEST INFRASTRUCTURE ONLY.
+
+This module is a numpy op-for-op restatement of the reference's TF2/Keras
+forward path (Hcyand/recommender_system, algorithm/deep_learning/...).  Only
+``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg
+may import it, and only as the checker / the timed CPU baseline.  The product
+path (``recommender_system_amd``) never imports it and has no CPU fallback.
+
+PARITY STATUS: the reference's layer/model arithmetic lives in TensorFlow/Keras
+(unpinned TF 2.x), which is not installed in this image (ImportError, no
+network).  The layer math below is therefore **parity unpinned** by the
+reference itself: it is pinned by known-answer tests (brute-force FM pairwise
+sum, explicit per-sample CrossNet loop, per-pair inner products, one-hot FM ==
+gather FM, attention with one / zero unmasked positions; see
+tests/test_oracle.py).  The input producer (utils/dataset.py) IS pinned against
+the reference itself: tests/golden/make_golden.py imports the reference's
+``utils/dataset.py`` in the build container and commits its outputs as
+fixtures.
+
+Keras semantics restated here (third-party behaviour the reference relies on):
+  * Model inputs are autocast to float32 (``cast_inputs``).
+  * ``Embedding`` casts float ids to int32 by truncation, raises on an id outside
+    [0, vocab) (TF CPU InvalidArgumentError -> IndexError here).
+  * ``Dense`` kernel is (in, out); a 3-D input is a tensordot over its last axis.
+  * ``PReLU()`` alpha has shape input_shape[1:] (shared_axes=None).
+  * ``BatchNormalization`` at inference: (x - moving_mean)/sqrt(moving_var+eps)
+    * gamma + beta (eps 1e-3 default; Dice uses eps 1e-9, center/scale off).
+  * ``Dropout`` is the identity at inference.
+  * ``-2**32 + 1`` is -4294967295, which rounds to -4294967296.0 in float32.
+
+All functions take a ``dt`` argument (np.float64 for golden vectors, np.float32
+for the timed CPU baseline) and compute in that dtype.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+MASK_FILL = -2 ** 32 + 1  # layer/interaction.py:399
+
+
+# ----------------------------------------------------------------- helpers
+def cast_inputs(x, dt=np.float32):
+    """Keras Model.__call__ autocast of floating inputs (float64 -> float32)."""
+    return np.asarray(x, dtype=np.float32).astype(dt)
+
+
+def cast_ids(ids):
+    """Keras Embedding: ``tf.cast(inputs, 'int32')`` for non-integer ids
+    (truncation toward zero); integer ids pass through unchanged."""
+    ids = np.asarray(ids)
+    if np.issubdtype(ids.dtype, np.floating):
+        with np.errstate(invalid="ignore"):
+            return np.trunc(ids.astype(np.float32)).astype(np.int64)
+    return ids.astype(np.int64)
+
+
+def embedding_lookup(table, ids):
+    """tf.gather(table, ids) with TF-CPU's out-of-range error."""
+    ids = cast_ids(ids)
+    if ids.size and (ids.min() < 0 or ids.max() >= table.shape[0]):
+        raise IndexError(f"embedding id out of range [0, {table.shape[0]})")
+    return table[ids]
+
+
+# ----------------------------------------------------- layers (a3 .. a14)
+def embed_layer(sparse, tables, dt=np.float64):
+    """EmbedLayer.call (layer/core.py:273-280): per-field Embedding, stack to
+    [F,B,k], transpose to [B,F,k], reshape to [B,F*k] (field-major)."""
+    sparse = np.asarray(sparse)
+    embs = [embedding_lookup(np.asarray(t, dt), sparse[:, i]) for i, t in enumerate(tables)]
+    emb = np.transpose(np.stack(embs, 0), (1, 0, 2))
+    return emb.reshape(emb.shape[0], emb.shape[1] * emb.shape[2])
+
+
+def fm_layer(x, w0, w1, v, dt=np.float64):
+    """FMLayer.call (layer/interaction.py:106-114), op for op."""
+    x = np.asarray(x, dt)
+    w0, w1, v = (np.asarray(a, dt) for a in (w0, w1, v))
+    linear = x @ w1.reshape(-1, 1) + w0.reshape(1)
+    p1 = np.power(x @ v, 2)
+    p2 = np.power(x, 2) @ np.power(v, 2)
+    inter = 0.5 * np.sum(p1 - p2, axis=-1, keepdims=True)
+    return linear + inter
+
+
+def fm_layer_pairwise(x, w0, w1, v, dt=np.float64):
+    """Known-answer form of the FM: w0 + x.w1 + sum_{i<j} <v_i,v_j> x_i x_j."""
+    x = np.asarray(x, dt)
+    v = np.asarray(v, dt)
+    gram = v @ v.T
+    iu = np.triu_indices(v.shape[0], 1)
+    w0 = np.asarray(w0, dt).reshape(-1)[0]
+    w1 = np.asarray(w1, dt).reshape(-1)
+    out = np.empty((x.shape[0], 1), dt)
+    for b in range(x.shape[0]):
+        xx = np.outer(x[b], x[b])
+        out[b, 0] = w0 + x[b] @ w1 + np.sum(gram[iu] * xx[iu])
+    return out
+
+
+def fm_onehot_gather(dense, ids, field_offsets, w0, w1, v, dt=np.float64):
+    """FM model on one-hot x, computed as a gather (model/fm.py + the identity
+    x[b, nd + off_c + id_c] = 1, utils/dataset.py:47-48)."""
+    dense = np.asarray(dense, dt)
+    ids = cast_ids(ids)
+    nd = dense.shape[1]
+    rows = nd + np.asarray(field_offsets)[None, :] + ids
+    v = np.asarray(v, dt)
+    w1 = np.asarray(w1, dt).reshape(-1)
+    s = dense @ v[:nd] + v[rows].sum(1)
+    q = (dense ** 2) @ (v[:nd] ** 2) + (v[rows] ** 2).sum(1)
+    lin = dense @ w1[:nd] + w1[rows].sum(1) + np.asarray(w0, dt).reshape(1)
+    return (lin + 0.5 * np.sum(s * s - q, axis=1)).reshape(-1, 1)
+
+
+def activation(x, act, alpha=None):
+    if act is None or act == "linear":
+        return x
+    if act == "relu":
+        return np.maximum(x, 0)
+    if act == "sigmoid":
+        return 1.0 / (1.0 + np.exp(-x))
+    if act == "prelu":
+        return prelu(x, alpha)
+    raise ValueError(act)
+
+
+def prelu(x, alpha):
+    """Keras PReLU: max(0,x) + alpha * min(0,x) (alpha broadcast from the
+    trailing dims, shape input_shape[1:])."""
+    return np.maximum(x, 0) + alpha * np.minimum(x, 0)
+
+
+def dense(x, kernel, bias, act=None, alpha=None, dt=np.float64):
+    """Keras Dense: tensordot(x, kernel, [[-1],[0]]) + bias, then activation."""
+    x = np.asarray(x, dt)
+    y = np.tensordot(x, np.asarray(kernel, dt), axes=[[x.ndim - 1], [0]]) + np.asarray(bias, dt)
+    return activation(y, act, None if alpha is None else np.asarray(alpha, dt))
+
+
+def dnn_layer(x, hidden, out, act="relu", dt=np.float64):
+    """DNNLayer.call (layer/interaction.py:40-46); Dropout is inactive."""
+    for kern, bias in hidden:
+        x = dense(x, kern, bias, act, dt=dt)
+    return dense(x, out[0], out[1], None, dt=dt)
+
+
+def cross_layer(x, ws, bs, dt=np.float64):
+    """CrossLayer.call (layer/interaction.py:75-83), op for op on [B,d,1]."""
+    x0 = np.asarray(x, dt)[:, :, None]
+    x1 = x0
+    for w, b in zip(ws, bs):
+        w = np.asarray(w, dt).reshape(-1, 1)
+        b = np.asarray(b, dt).reshape(-1, 1)
+        x1_w = np.matmul(np.transpose(x1, (0, 2, 1)), w)  # [B,1,1]
+        x1 = np.matmul(x0, x1_w) + b + x1
+    return x1[:, :, 0]
+
+
+def cross_layer_loop(x, ws, bs, dt=np.float64):
+    """Known-answer form: explicit per-sample loop of x_{l+1}=x0 (x_l.w)+b+x_l."""
+    x = np.asarray(x, dt)
+    out = np.empty_like(x)
+    for n in range(x.shape[0]):
+        x0 = x[n]
+        xl = x0.copy()
+        for w, b in zip(ws, bs):
+            xl = x0 * float(xl @ np.asarray(w, dt).reshape(-1)) + np.asarray(b, dt).reshape(-1) + xl
+        out[n] = xl
+    return out
+
+
+def pair_indices(F):
+    """Row-major (i<j) pair order of InnerProductLayer (layer/interaction.py:172-177)."""
+    row, col = [], []
+    for i in range(F - 1):
+        for j in range(i + 1, F):
+            row.append(i)
+            col.append(j)
+    return np.array(row), np.array(col)
+
+
+def inner_product_layer(e, dt=np.float64):
+    """InnerProductLayer.call (layer/interaction.py:170-183) on [B,F,k]."""
+    e = np.asarray(e, dt)
+    row, col = pair_indices(e.shape[1])
+    p = e[:, row, :]
+    q = e[:, col, :]
+    return np.sum(p * q, axis=-1)
+
+
+def inner_product_loop(e, dt=np.float64):
+    e = np.asarray(e, dt)
+    B, F, _ = e.shape
+    out = []
+    for i in range(F - 1):
+        for j in range(i + 1, F):
+            out.append([float(e[b, i] @ e[b, j]) for b in range(B)])
+    return np.asarray(out, dt).T.reshape(B, -1)
+
+
+def batchnorm_inference(x, mean, var, gamma=None, beta=None, eps=1e-3, dt=np.float64):
+    x = np.asarray(x, dt)
+    y = (x - np.asarray(mean, dt)) / np.sqrt(np.asarray(var, dt) + dt(eps))
+    if gamma is not None:
+        y = y * np.asarray(gamma, dt)
+    if beta is not None:
+        y = y + np.asarray(beta, dt)
+    return y
+
+
+def dice(x, alpha, mean, var, eps=1e-9, dt=np.float64):
+    """Dice.call at inference (layer/interaction.py:421-425)."""
+    x = np.asarray(x, dt)
+    xn = batchnorm_inference(x, mean, var, eps=eps, dt=dt)
+    xp = 1.0 / (1.0 + np.exp(-xn))
+    return np.asarray(alpha, dt) * (1.0 - xp) * x + xp * x
+
+
+def attention(query, key, value, mask, params, act="prelu", dt=np.float64):
+    """Attention.call (layer/interaction.py:369-406).
+
+    params['prelu'] = [(kernel, bias, alpha[T,h]), ...] ; params['dice'] =
+    [(alpha[4k], mean[4k], var[4k], eps), ...] ; params['out'] = (kernel, bias).
+    """
+    q = np.asarray(query, dt)[:, None, :]
+    key = np.asarray(key, dt)
+    value = np.asarray(value, dt)
+    q = np.tile(q, (1, key.shape[1], 1))
+    emb = np.concatenate([q, key, q - key, q * key], axis=-1)
+    if act == "prelu":
+        for kern, bias, alpha in params["prelu"]:
+            emb = dense(emb, kern, bias, "prelu", alpha, dt=dt)
+    elif act == "dice":
+        for alpha, mean, var, eps in params["dice"]:
+            emb = dice(emb, alpha, mean, var, eps, dt=dt)
+    else:
+        raise ValueError(act)
+    score = dense(emb, params["out"][0], params["out"][1], None, dt=dt)[..., 0]
+    padding = np.ones_like(score) * dt(np.float32(MASK_FILL))
+    score = np.where(np.asarray(mask) == 0, padding, score)
+    score = score - score.max(-1, keepdims=True)
+    e = np.exp(score)
+    score = e / e.sum(-1, keepdims=True)
+    return np.matmul(score[:, None, :], value)[:, 0, :]
+
+
+def sigmoid(x):
+    return 1.0 / (1.0 + np.exp(-x))
+
+
+# ------------------------------------------------------------- models
+def fm_model(x, p, dt=np.float64):
+    """FM.call (model/fm.py:19-23): sigmoid(FMLayer(x))."""
+    return sigmoid(fm_layer(cast_inputs(x, dt), p["w0"], p["w1"], p["v"], dt=dt))
+
+
+def _split_dense_sparse(X, nd, dt):
+    Xc = cast_inputs(X, dt)
+    Xf = np.asarray(X, np.float32)  # ids go through the float32 autocast
+    return Xc[:, :nd], Xf[:, nd:]
+
+
+def deepfm(X, p, nd=13, dt=np.float64, inputs=None):
+    """DeepFM.call (model/deepFM.py:23-31).  X: packed [B, nd+F] or
+    inputs=(dense, ids)."""
+    dense_in, sparse = inputs if inputs is not None else _split_dense_sparse(X, nd, dt)
+    x = np.concatenate([np.asarray(dense_in, dt), embed_layer(sparse, p["tables"], dt)], axis=-1)
+    fm = fm_layer(x, p["w0"], p["w1"], p["v"], dt=dt)
+    dnn = dnn_layer(x, p["dnn_hidden"], p["dnn_out"], p.get("act", "relu"), dt=dt)
+    return sigmoid(0.5 * (fm + dnn)), fm, x
+
+
+def dcn(X, p, nd=13, dt=np.float64, inputs=None):
+    """DCN.call (model/dcn.py:24-34)."""
+    dense_in, sparse = inputs if inputs is not None else _split_dense_sparse(X, nd, dt)
+    x = np.concatenate([np.asarray(dense_in, dt), embed_layer(sparse, p["tables"], dt)], axis=1)
+    cross = cross_layer(x, p["cross_w"], p["cross_b"], dt=dt)
+    dnn = dnn_layer(x, p["dnn_hidden"], p["dnn_out"], p.get("act", "relu"), dt=dt)
+    z = np.concatenate([cross, dnn], axis=1)
+    return sigmoid(dense(z, p["out_kernel"], p["out_bias"], dt=dt)), cross
+
+
+def pnn_inner(X, p, nd=13, dt=np.float64, inputs=None):
+    """PNN.call mode='inner' (model/pnn.py:28-53) with 3-D embeddings [B,F,k]
+    (documented deviation: the reference's rank-2 EmbedLayer crashes at
+    model/pnn.py:38).  Returns the DNN logit (no sigmoid, as the reference)."""
+    _, sparse = inputs if inputs is not None else _split_dense_sparse(X, nd, dt)
+    flat = embed_layer(sparse, p["tables"], dt)
+    k = np.asarray(p["tables"][0]).shape[1]
+    z = flat.reshape(flat.shape[0], -1, k)
+    inner = inner_product_layer(z, dt=dt)
+    x = np.concatenate([flat, inner], axis=1)
+    return dnn_layer(x, p["dnn_hidden"], p["dnn_out"], p.get("act", "relu"), dt=dt), x
+
+
+def din(inputs, p, dense_feats, sparse_feats, behavior_feats, dt=np.float64,
+        att_act="prelu"):
+    """DIN.call (model/din.py:56-95).
+
+    p: 'sparse_tables' {feat: table} for non-behaviour sparse feats,
+       'seq_tables' {feat: table} for behaviour feats, 'att' attention params,
+       'bn' (gamma, beta, mean, var, eps), 'dnn' [(kernel, bias, alpha)],
+       'out' (kernel, bias)."""
+    dense_in = np.concatenate([cast_inputs(inputs[f], dt).reshape(-1, 1) for f in dense_feats], -1)
+    other_sparse = [f for f in sparse_feats if f not in behavior_feats]
+    sp = np.concatenate([np.asarray(inputs[f]).reshape(-1, 1) for f in other_sparse], -1)
+    other = np.concatenate([embedding_lookup(np.asarray(p["sparse_tables"][f], dt), sp[:, i])
+                            for i, f in enumerate(other_sparse)], -1)
+    other = np.concatenate([other, dense_in], -1)
+    hist = np.stack([np.asarray(inputs[f]) for f in behavior_feats], -1)  # [B,T,nb]
+    cand = np.asarray(inputs["movie_id"]).reshape(-1, 1)
+    seq = np.concatenate([embedding_lookup(np.asarray(p["seq_tables"][f], dt), hist[:, :, i])
+                          for i, f in enumerate(behavior_feats)], -1)
+    item = np.concatenate([embedding_lookup(np.asarray(p["seq_tables"][f], dt), cand[:, i])
+                           for i, f in enumerate(behavior_feats)], -1)
+    mask = (hist[:, :, 0] != 0).astype(dt)
+    att = attention(item, seq, seq, mask, p["att"], att_act, dt=dt)
+    emb = np.concatenate([att, item, other], -1)
+    g, bt, mu, var, eps = p["bn"]
+    emb = batchnorm_inference(emb, mu, var, g, bt, eps, dt=dt)
+    for kern, bias, alpha in p["dnn"]:
+        emb = dense(emb, kern, bias, "prelu", alpha, dt=dt)
+    return sigmoid(dense(emb, p["out"][0], p["out"][1], dt=dt)), att

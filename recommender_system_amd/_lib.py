@@ -1,0 +1,117 @@
+"""ctypes binding of librs_hip.so (the C-ABI declared in include/rs_capi.h).
+
+``import torch`` happens first so that the process has exactly one HIP runtime
+(torch's bundled libamdhip64.so.7, which the .so then binds to by SONAME).
+There is no fallback: if the library is missing or a call fails, this module
+raises.  Device tensors are passed as raw pointers; streams as
+``torch.cuda.current_stream().cuda_stream``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import threading
+from pathlib import Path
+
+import torch  # noqa: F401  (loads the HIP runtime before the extension)
+
+_LIB_PATH = Path(__file__).resolve().parent / "librs_hip.so"
+
+P = C.c_void_p
+I = C.c_int
+L = C.c_int64
+F = C.c_float
+
+# name -> (restype, argtypes); must match include/rs_capi.h
+SIGNATURES = {
+    "rs_version": (C.c_char_p, []),
+    "rs_last_error_string": (C.c_char_p, []),
+    "rs_embed_gather": (I, [P, I, L, P, L, I, P, P, P, I, I, P, L, L, P, P]),
+    "rs_fm_prepared_size": (L, [I, I, I, I]),
+    "rs_fm_prepare": (I, [P, P, I, I, I, I, P, P]),
+    "rs_embed_fm_fwd": (I, [P, I, L, P, L, I, P, P, P, I, I, P, P, I, P, P, L, P, P]),
+    "rs_fm_fwd": (I, [P, L, I, P, P, I, P, L, P]),
+    "rs_fm_onehot_fwd": (I, [P, I, L, P, L, I, P, P, I, P, P, P, I, P, L, P, P]),
+    "rs_cross_prepared_size": (L, [I, I]),
+    "rs_cross_prepare": (I, [P, P, I, I, P, P]),
+    "rs_cross_fwd": (I, [P, L, I, I, P, P, L, L, P]),
+    "rs_inner_product_fwd": (I, [P, I, I, P, L, L, P]),
+    "rs_embed_inner_fwd": (I, [P, I, L, P, P, P, I, I, P, L, L, P, P]),
+    "rs_din_attention_fwd": (I, [P, P, P, P, I, I, P, P, P, I, P, P, P, I, P, P, P, L, P]),
+    "rs_din_attention_dice_fwd": (I, [P, P, P, P, I, I, I, P, P, P, F, P, P, P, L, P]),
+    "rs_dense_fwd": (I, [P, L, P, P, P, I, P, L, L, I, I, P]),
+    "rs_affine_act": (I, [P, L, P, P, P, I, P, L, L, I, P]),
+    "rs_sigmoid_combine": (I, [P, P, F, F, P, L, P]),
+    "rs_dice_fwd": (I, [P, L, P, P, F, P, P, L, L, I, P]),
+    "rs_shard_workspace_size": (L, [L, I]),
+    "rs_shard_bucketize": (I, [P, I, L, P, P, I, L, L, I, P, P, P, P, P, P]),
+    "rs_gather_rows": (I, [P, L, I, P, L, P, P]),
+    "rs_unpermute_rows": (I, [P, P, I, L, P, P]),
+    "rs_rows_fm_fwd": (I, [P, P, L, I, I, I, P, P, I, P, L, P]),
+}
+
+ID_I32, ID_I64, ID_F32 = 0, 1, 2
+ACT = {None: 0, "linear": 0, "relu": 1, "prelu": 2, "sigmoid": 3}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class RSError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the bound library; raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not _LIB_PATH.exists():
+                raise ImportError(
+                    f"{_LIB_PATH} is missing: build the HIP extension first "
+                    "(python -c 'import __graft_entry__ as g; g.build()')")
+            h = C.CDLL(str(_LIB_PATH))
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(h, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = h
+    return _lib
+
+
+def library_path() -> Path:
+    return _LIB_PATH
+
+
+def check(status: int, what: str = "") -> None:
+    if status != 0:
+        msg = lib().rs_last_error_string().decode()
+        raise RSError(f"{what or 'librs_hip'} failed ({status}): {msg}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args), name)
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None for None)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RSError("librs_hip kernels need device (HIP) tensors; got a CPU tensor")
+    return t.data_ptr()
+
+
+def stream(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def id_kind(t) -> int:
+    if t.dtype == torch.int32:
+        return ID_I32
+    if t.dtype == torch.int64:
+        return ID_I64
+    if t.dtype == torch.float32:
+        return ID_F32
+    raise TypeError(f"unsupported sparse id dtype {t.dtype} (int32, int64 or float32)")

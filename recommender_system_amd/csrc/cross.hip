@@ -1,0 +1,211 @@
+// cross.hip — DCN CrossNet forward (CrossLayer, layer/interaction.py:49-83).
+//
+// Reference: x_{l+1} = x0 * (x_l^T w_l) + b_l + x_l for l < L, out = x_L.
+// Every x_l is affine in x0 per sample: x_l = alpha_l * x0 + beta_l with
+//   beta_l  = sum_{j<l} b_j               (sample-independent vector)
+//   alpha_0 = 1, alpha_{l+1} = alpha_l * (1 + g_l) + h_l,
+//   g_l = x0^T w_l (per sample),  h_l = beta_l^T w_l (sample-independent).
+// So the whole stack is one contraction G = X0 @ [w_0 .. w_{L-1}] — the
+// x0 x_l^T w contraction of the north star — done on v_mfma_f32_16x16x4_f32
+// with all L weight vectors as B columns, a 16-sample scalar recurrence, and
+// one fused-multiply-add pass out = alpha_L * x0 + beta_L.  x0 is read from
+// HBM once (staged in LDS), out is written once: the kernel is HBM-bound at
+// 2*d*4 bytes per sample; MFMA utilisation is at most L/16 by construction.
+#include "rs_common.hpp"
+
+namespace rs {
+
+struct CrossGeom {
+  int d, L, NT, DB;
+  int64_t b_img, h_off, beta_off, size;
+};
+
+static CrossGeom cross_geom(int d, int L) {
+  CrossGeom g{};
+  g.d = d;
+  g.L = L;
+  g.NT = (L + 15) / 16;
+  g.DB = (d + 3) / 4;
+  g.b_img = (int64_t)g.DB * g.NT * 64;
+  g.h_off = g.b_img;
+  g.beta_off = g.h_off + ((L + 3) / 4) * 4;
+  g.size = g.beta_off + ((d + 3) / 4) * 4;
+  return g;
+}
+
+// B image: rec[t][nt][lane] = w[col][4t + kk] (col = nt*16 + (lane&15), kk = lane>>4)
+__global__ void cross_prepare_img(const float* __restrict__ w, int d, int L, int NT, int64_t n,
+                                  float* __restrict__ out) {
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int t = (int)(idx / (NT * 64));
+    const int r = (int)(idx % (NT * 64));
+    const int nt = r / 64, lane = r % 64;
+    const int e = 4 * t + (lane >> 4), col = nt * 16 + (lane & 15);
+    out[idx] = (e < d && col < L) ? w[(int64_t)col * d + e] : 0.f;
+  }
+}
+
+// h_l = beta_l . w_l and beta_L = sum_l b_l (one workgroup, sequential over l).
+__global__ void cross_prepare_bias(const float* __restrict__ w, const float* __restrict__ b, int d, int L,
+                                   float* __restrict__ h, float* __restrict__ beta) {
+  __shared__ float red[16];
+  for (int j = threadIdx.x; j < d; j += blockDim.x) beta[j] = 0.f;
+  __syncthreads();
+  for (int l = 0; l < L; ++l) {
+    float p = 0.f;
+    for (int j = threadIdx.x; j < d; j += blockDim.x) p = fmaf(beta[j], w[(int64_t)l * d + j], p);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = p;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float s = 0.f;
+      for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+      h[l] = s;
+    }
+    for (int j = threadIdx.x; j < d; j += blockDim.x) beta[j] += b[(int64_t)l * d + j];
+    __syncthreads();
+  }
+}
+
+struct CrossArgs {
+  const float* x0;
+  int64_t x_stride;
+  int d, L, DB;
+  const float* img;
+  const float* h;
+  const float* beta;
+  float* out;
+  int64_t out_stride;
+  int64_t batch;
+};
+
+template <int NT, int NW>
+__global__ __launch_bounds__(NW * 64) void cross_mfma(CrossArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* tile = smem;                                       // [16][d]
+  float* cs = smem + ((16 * a.d + 3) / 4) * 4;              // [NW][16][NT*16+1]
+  float* alpha = cs + NW * 16 * (NT * 16 + 1);              // [16]
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int s = lane & 15, kk = lane >> 4;
+  const int64_t b0 = (int64_t)blockIdx.x * 16;
+  const int rows = (int)((a.batch - b0) < 16 ? (a.batch - b0) : 16);
+
+  // (1) stage the 16 x d tile of x0 (coalesced)
+  const int n = rows * a.d;
+  if (a.x_stride == a.d && ((uintptr_t)(a.x0 + b0 * a.d) % 16 == 0)) {
+    const float* src = a.x0 + b0 * a.d;
+    const int n4 = n / 4;
+    for (int i = threadIdx.x; i < n4; i += blockDim.x)
+      reinterpret_cast<floatx4*>(tile)[i] = reinterpret_cast<const floatx4*>(src)[i];
+    for (int i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) tile[i] = src[i];
+  } else {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const int r = i / a.d, j = i - r * a.d;
+      tile[i] = a.x0[(b0 + r) * a.x_stride + j];
+    }
+  }
+  for (int i = n + threadIdx.x; i < 16 * a.d; i += blockDim.x) tile[i] = 0.f;
+  __syncthreads();
+
+  // (2) G = X0 @ W on MFMA, K split across the NW waves
+  floatx4 acc[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int t = w; t < a.DB; t += NW) {
+    const int e = 4 * t + kk;
+    const float xv = e < a.d ? tile[s * a.d + e] : 0.f;
+    const float* rec = a.img + (int64_t)t * NT * 64;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(xv, rec[nt * 64 + lane], acc[nt]);
+  }
+  constexpr int CW = NT * 16 + 1;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cs[(w * 16 + kk * 4 + r) * CW + nt * 16 + s] = acc[nt][r];
+  __syncthreads();
+
+  // (3) per-sample recurrence alpha_{l+1} = alpha_l (1 + g_l) + h_l
+  if (threadIdx.x < 16) {
+    float al = 1.f;
+    for (int l = 0; l < a.L; ++l) {
+      float g = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) g += cs[(ww * 16 + threadIdx.x) * CW + l];
+      al = fmaf(al, 1.f + g, a.h[l]);
+    }
+    alpha[threadIdx.x] = al;
+  }
+  __syncthreads();
+
+  // (4) out = alpha * x0 + beta_L (coalesced)
+  if (a.out_stride == a.d && ((uintptr_t)(a.out + b0 * a.d) % 16 == 0) && (a.d % 4 == 0)) {
+    floatx4* dst = reinterpret_cast<floatx4*>(a.out + b0 * a.d);
+    const int n4 = n / 4;
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) {
+      const int r = (4 * i) / a.d, j = 4 * i - r * a.d;
+      const floatx4 x = reinterpret_cast<const floatx4*>(tile)[i];
+      const float al = alpha[r];
+      dst[i] = floatx4{fmaf(al, x[0], a.beta[j]), fmaf(al, x[1], a.beta[j + 1]), fmaf(al, x[2], a.beta[j + 2]),
+                       fmaf(al, x[3], a.beta[j + 3])};
+    }
+  } else {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const int r = i / a.d, j = i - r * a.d;
+      a.out[(b0 + r) * a.out_stride + j] = fmaf(alpha[r], tile[i], a.beta[j]);
+    }
+  }
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" int64_t rs_cross_prepared_size(int d, int n_layers) {
+  if (d < 1 || n_layers < 0) return -1;
+  return cross_geom(d, n_layers < 1 ? 1 : n_layers).size;
+}
+
+extern "C" int rs_cross_prepare(const float* w, const float* b, int d, int n_layers, float* prepared,
+                                rs_stream_t stream) {
+  RS_REQUIRE(d >= 1 && n_layers >= 0 && n_layers <= 32, "rs_cross_prepare: bad shape (d>=1, 0<=L<=32)");
+  RS_REQUIRE(prepared && (n_layers == 0 || (w && b)), "rs_cross_prepare: null pointer");
+  const int L = n_layers;
+  const CrossGeom g = cross_geom(d, L < 1 ? 1 : L);
+  hipStream_t st = as_stream(stream);
+  (void)hipMemsetAsync(prepared, 0, g.size * sizeof(float), st);
+  if (L > 0) {
+    int64_t grid = (g.b_img + 255) / 256;
+    if (grid > 4096) grid = 4096;
+    cross_prepare_img<<<(unsigned)grid, 256, 0, st>>>(w, d, L, g.NT, g.b_img, prepared);
+    cross_prepare_bias<<<1, 1024, 0, st>>>(w, b, d, L, prepared + g.h_off, prepared + g.beta_off);
+  }
+  return launch_status("rs_cross_prepare");
+}
+
+extern "C" int rs_cross_fwd(const float* x0, int64_t x_stride, int d, int n_layers, const float* prepared,
+                            float* out, int64_t out_stride, int64_t batch, rs_stream_t stream) {
+  RS_REQUIRE(x0 && prepared && out, "rs_cross_fwd: null pointer");
+  RS_REQUIRE(d >= 1 && n_layers >= 0 && n_layers <= 32 && batch >= 0, "rs_cross_fwd: bad shape");
+  RS_REQUIRE(x_stride >= d && out_stride >= d, "rs_cross_fwd: stride < d");
+  RS_REQUIRE(d <= 2304, "rs_cross_fwd: d > 2304 not supported (LDS tile)");
+  if (batch == 0) return RS_OK;
+  const int L = n_layers;
+  const CrossGeom g = cross_geom(d, L < 1 ? 1 : L);
+  CrossArgs a{x0, x_stride, d, L, g.DB, prepared, prepared + g.h_off, prepared + g.beta_off, out, out_stride, batch};
+  constexpr int NW = 8;
+  const size_t lds = (size_t)(((16 * d + 3) / 4) * 4 + NW * 16 * (g.NT * 16 + 1) + 16) * sizeof(float);
+  const unsigned grid = (unsigned)((batch + 15) / 16);
+  hipStream_t st = as_stream(stream);
+  if (g.NT == 1) {
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)cross_mfma<1, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    cross_mfma<1, NW><<<grid, NW * 64, lds, st>>>(a);
+  } else {
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)cross_mfma<2, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    cross_mfma<2, NW><<<grid, NW * 64, lds, st>>>(a);
+  }
+  return launch_status("rs_cross_fwd");
+}

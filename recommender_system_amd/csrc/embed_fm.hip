@@ -1,0 +1,685 @@
+// embed_fm.hip — embedding lookup (EmbedLayer) and FM second-order kernels.
+//
+// Reference semantics:
+//   EmbedLayer.call            algorithm/deep_learning/layer/core.py:273-280
+//   DeepFM x = [dense | emb]   algorithm/deep_learning/model/deepFM.py:24-26
+//   FMLayer.call               algorithm/deep_learning/layer/interaction.py:106-114
+//   FM model (one-hot input)   algorithm/deep_learning/model/fm.py:19-23,
+//                              utils/dataset.py:47-48 (get_dummies layout)
+//
+// Headline kernel: embed_fm_mfma — one launch does ids -> rows -> FM logit.
+//   * A workgroup owns 16 samples (one MFMA row tile) and NW waves split the
+//     contraction dimension d = nd + F*k round-robin by field (K-split).
+//   * Lane l of a wave is sample s = l&15 and k-slot kk = l>>4: for field c it
+//     loads k/4 consecutive floats of the sample's row (k=16: one float4, so a
+//     wave-instruction reads 16 whole 64-B rows), which are its A-operand
+//     values for the field's k/4 MFMA k-steps (k order permuted per field;
+//     the packed B image from rs_fm_prepare uses the same permutation).
+//   * s = x@v and the linear term x@w1 come out of v_mfma_f32_16x16x4_f32
+//     (B columns 0..kfm-1 = v, column kfm = w1); the second-order correction
+//     sum_f (x^2@v^2)_f = sum_i x_i^2 * |v_i|^2 is a per-lane FMA with the row
+//     norms packed beside B, reduced across the 4 k-slots by wave shuffles.
+//   * Partial tiles of the NW waves are summed through LDS; wave 0 finishes
+//     logit = (x@w1 + w0) + 0.5*(sum_f s_f^2 - sum_i x_i^2 |v_i|^2).
+#include <stdlib.h>
+
+#include "rs_common.hpp"
+
+namespace rs {
+
+// ----------------------------------------------------------- packed layout
+struct FmGeom {
+  int nd, F, k, kfm, d;
+  bool mfma;
+  int KV, NT, DB;
+  int64_t dense_rec, field_rec, field_base, size;
+};
+
+static FmGeom fm_geom(int nd, int F, int k, int kfm) {
+  FmGeom g{};
+  g.nd = nd;
+  g.F = F;
+  g.k = k;
+  g.kfm = kfm;
+  g.d = nd + F * k;
+  const bool kv_ok = (F == 0) || (k % 4 == 0 && (k == 4 || k == 8 || k == 16 || k == 32 || k == 64));
+  g.mfma = kv_ok && kfm >= 1 && kfm + 1 <= 32;
+  if (g.mfma) {
+    g.KV = (F == 0) ? 4 : k / 4;
+    g.NT = (kfm + 1 + 15) / 16;
+    g.DB = (nd + 3) / 4;
+    g.dense_rec = (int64_t)g.NT * 64 + 4;
+    g.field_rec = (int64_t)g.NT * 64 * g.KV + 4 * g.KV;
+    g.field_base = (int64_t)g.DB * g.dense_rec;
+    g.size = g.field_base + (int64_t)F * g.field_rec;
+  } else {
+    // generic path: [w1 (d) | v (d*kfm) | |v_i|^2 (d)]
+    g.size = (int64_t)g.d * (kfm + 2);
+  }
+  return g;
+}
+
+__device__ __forceinline__ float fm_bval(const float* w1, const float* v, int d, int kfm, int e, int colg) {
+  if (e >= d) return 0.f;
+  if (colg < kfm) return v[(int64_t)e * kfm + colg];
+  if (colg == kfm) return w1[e];
+  return 0.f;
+}
+
+__device__ __forceinline__ float fm_rownorm(const float* v, int d, int kfm, int e) {
+  if (e >= d) return 0.f;
+  float n = 0.f;
+  for (int f = 0; f < kfm; ++f) {
+    const float t = v[(int64_t)e * kfm + f];
+    n = fmaf(t, t, n);
+  }
+  return n;
+}
+
+__global__ void fm_prepare_mfma(const float* __restrict__ w1, const float* __restrict__ v, int nd, int F,
+                                int k, int kfm, int KV, int NT, int DB, int64_t dense_rec,
+                                int64_t field_rec, int64_t field_base, int64_t size,
+                                float* __restrict__ out) {
+  const int d = nd + F * k;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < size;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    float val;
+    if (idx < field_base) {
+      const int t = (int)(idx / dense_rec);
+      const int r = (int)(idx % dense_rec);
+      if (r < NT * 64) {
+        const int nt = r / 64, lane = r % 64;
+        const int e = 4 * t + (lane >> 4);
+        val = (e < nd) ? fm_bval(w1, v, d, kfm, e, nt * 16 + (lane & 15)) : 0.f;
+      } else {
+        const int e = 4 * t + (r - NT * 64);
+        val = (e < nd) ? fm_rownorm(v, d, kfm, e) : 0.f;
+      }
+    } else {
+      const int64_t j = idx - field_base;
+      const int c = (int)(j / field_rec);
+      const int r = (int)(j % field_rec);
+      if (r < NT * 64 * KV) {
+        const int nt = r / (64 * KV), rem = r % (64 * KV);
+        const int lane = rem / KV, tp = rem % KV;
+        const int e = nd + c * k + KV * (lane >> 4) + tp;
+        val = fm_bval(w1, v, d, kfm, e, nt * 16 + (lane & 15));
+      } else {
+        const int r2 = r - NT * 64 * KV;
+        const int e = nd + c * k + KV * (r2 / KV) + (r2 % KV);
+        val = fm_rownorm(v, d, kfm, e);
+      }
+    }
+    out[idx] = val;
+  }
+}
+
+__global__ void fm_prepare_generic(const float* __restrict__ w1, const float* __restrict__ v, int d, int kfm,
+                                   float* __restrict__ out) {
+  const int64_t n = (int64_t)d * (kfm + 2);
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    float val;
+    if (idx < d) val = w1[idx];
+    else if (idx < (int64_t)d * (kfm + 1)) val = v[idx - d];
+    else val = fm_rownorm(v, d, kfm, (int)(idx - (int64_t)d * (kfm + 1)));
+    out[idx] = val;
+  }
+}
+
+// ----------------------------------------------------------- id plumbing
+struct RawId {
+  int64_t bits;
+};
+
+__device__ __forceinline__ RawId raw_id(const void* ids, int kind, int64_t off) {
+  RawId r;
+  if (kind == RS_ID_I64) r.bits = static_cast<const int64_t*>(ids)[off];
+  else if (kind == RS_ID_I32) r.bits = static_cast<const int32_t*>(ids)[off];
+  else r.bits = static_cast<int64_t>(__float_as_uint(static_cast<const float*>(ids)[off]));
+  return r;
+}
+
+__device__ __forceinline__ bool decode_id(RawId r, int kind, int64_t vocab, int64_t& id) {
+  if (kind == RS_ID_F32) {
+    const float f = __uint_as_float(static_cast<uint32_t>(r.bits));
+    if (!(f > -1.0f && static_cast<double>(f) < static_cast<double>(vocab))) return false;
+    id = static_cast<int64_t>(f);
+    return true;
+  }
+  id = r.bits;
+  return id >= 0 && id < vocab;
+}
+
+struct EmbedFmArgs {
+  const void* ids;
+  int id_kind;
+  int64_t id_stride;
+  const float* dense;
+  int64_t dense_stride;
+  int nd;
+  const float* table;
+  const int64_t* offs;
+  const int64_t* vocab;
+  int F;
+  int k;
+  const float* prep;
+  const float* w0;
+  int kfm;
+  float* logit;
+  float* x_out;
+  int64_t batch;
+  int* err;
+  int DB;
+  int64_t dense_rec, field_rec, field_base;
+  int direct;  // rows already gathered: row(b,c) = b*F + c, no ids
+};
+
+template <int KV, int NT, int NW>
+__global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
+  constexpr int MAXC0 = 128 / (NW * KV);
+  constexpr int MAXC = MAXC0 < 1 ? 1 : (MAXC0 > 8 ? 8 : MAXC0);
+  __shared__ float cs[NW][16][NT * 16 + 1];
+  __shared__ float qs[NW][16];
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int s = lane & 15;   // A: sample row of the tile; B/C: column
+  const int kk = lane >> 4;  // k-slot
+  const int64_t b = (int64_t)blockIdx.x * 16 + s;
+  const bool valid = b < a.batch;
+  const int d = a.nd + a.F * a.k;
+
+  floatx4 acc[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float qn = 0.f;
+
+  // ---- dense block: k-steps t = w, w+NW, ... (4 dense features per k-step)
+  for (int t = w; t < a.DB; t += NW) {
+    const int e = 4 * t + kk;
+    float xv = 0.f;
+    if (valid && e < a.nd) xv = a.dense[b * a.dense_stride + e];
+    const float* rec = a.prep + (int64_t)t * a.dense_rec;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(xv, rec[nt * 64 + lane], acc[nt]);
+    qn = fmaf(xv * xv, rec[NT * 64 + kk], qn);
+    if (a.x_out && valid && e < a.nd) a.x_out[b * d + e] = xv;
+  }
+
+  // ---- fields: c = cg + j*NW + w
+  for (int cg = 0; cg < a.F; cg += NW * MAXC) {
+    RawId rid[MAXC];
+    // (1) ids first: the only loads the row gather depends on
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = cg + j * NW + w;
+      rid[j].bits = 0;
+      if (c < a.F && valid && !a.direct) rid[j] = raw_id(a.ids, a.id_kind, b * a.id_stride + c);
+    }
+    // (2) packed weights (independent of ids): in flight with the ids
+    Chunk<KV> bw[MAXC][NT], nw[MAXC];
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = cg + j * NW + w;
+      if (c < a.F) {
+        const float* rec = a.prep + a.field_base + (int64_t)c * a.field_rec;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) bw[j][nt].load(rec + (int64_t)(nt * 64 + lane) * KV);
+        nw[j].load(rec + NT * 64 * KV + kk * KV);
+      }
+    }
+    // (3) row gather: KV consecutive floats of the sample's row per lane
+    Chunk<KV> xs[MAXC];
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = cg + j * NW + w;
+      xs[j].zero();
+      if (c < a.F && valid) {
+        int64_t row = -1;
+        if (a.direct) {
+          row = b * a.F + c;
+        } else {
+          int64_t id;
+          if (decode_id(rid[j], a.id_kind, a.vocab[c], id)) row = a.offs[c] + id;
+          else flag_error(a.err);
+        }
+        if (row >= 0) xs[j].load(a.table + row * a.k + KV * kk);
+      }
+    }
+    // (4) MFMA over the field's KV k-steps + |v|^2 correction
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = cg + j * NW + w;
+      if (c < a.F) {
+#pragma unroll
+        for (int tp = 0; tp < KV; ++tp) {
+          const float xv = xs[j].v[tp];
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(xv, bw[j][nt].v[tp], acc[nt]);
+          qn = fmaf(xv * xv, nw[j].v[tp], qn);
+        }
+        if (a.x_out && valid) {
+          float* xo = a.x_out + b * d + a.nd + c * a.k + KV * kk;
+#pragma unroll
+          for (int tp = 0; tp < KV; ++tp) xo[tp] = xs[j].v[tp];
+        }
+      }
+    }
+  }
+
+  // ---- combine the NW partial tiles
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cs[w][kk * 4 + r][nt * 16 + s] = acc[nt][r];
+  qn += __shfl_xor(qn, 16);
+  qn += __shfl_xor(qn, 32);
+  if (lane < 16) qs[w][lane] = qn;
+  __syncthreads();
+  if (w == 0) {
+    const int smp = lane & 15, g = lane >> 4;
+    float ss = 0.f, lin = 0.f;
+#pragma unroll
+    for (int cc = g; cc < NT * 16; cc += 4) {
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) v += cs[ww][smp][cc];
+      if (cc < a.kfm) ss = fmaf(v, v, ss);
+      else if (cc == a.kfm) lin = v;
+    }
+    ss += __shfl_xor(ss, 16);
+    ss += __shfl_xor(ss, 32);
+    lin += __shfl_xor(lin, 16);
+    lin += __shfl_xor(lin, 32);
+    if (g == 0) {
+      float q = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) q += qs[ww][smp];
+      const int64_t bb = (int64_t)blockIdx.x * 16 + smp;
+      if (bb < a.batch) a.logit[bb] = (lin + a.w0[0]) + 0.5f * (ss - q);
+    }
+  }
+}
+
+// Generic fallback (any k / kfm): one 256-thread workgroup per sample.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+  return t;
+}
+
+__global__ __launch_bounds__(256) void embed_fm_generic(EmbedFmArgs a) {
+  __shared__ int64_t rows[1024];
+  __shared__ float red[4];
+  const int64_t b = blockIdx.x;
+  const int d = a.nd + a.F * a.k;
+  const float* w1 = a.prep;
+  const float* v = a.prep + d;
+  const float* nsq = a.prep + (int64_t)d * (a.kfm + 1);
+  for (int c = threadIdx.x; c < a.F; c += blockDim.x) {
+    int64_t row = -1;
+    if (a.direct) {
+      row = b * a.F + c;
+    } else {
+      int64_t id;
+      if (decode_id(raw_id(a.ids, a.id_kind, b * a.id_stride + c), a.id_kind, a.vocab[c], id))
+        row = a.offs[c] + id;
+      else
+        flag_error(a.err);
+    }
+    rows[c] = row;
+  }
+  __syncthreads();
+  auto xval = [&](int e) -> float {
+    if (e < a.nd) return a.dense[b * a.dense_stride + e];
+    const int c = (e - a.nd) / a.k, j = (e - a.nd) % a.k;
+    const int64_t r = rows[c];
+    return r >= 0 ? a.table[r * a.k + j] : 0.f;
+  };
+  float lin = 0.f, q = 0.f;
+  for (int e = threadIdx.x; e < d; e += blockDim.x) {
+    const float x = xval(e);
+    lin = fmaf(x, w1[e], lin);
+    q = fmaf(x * x, nsq[e], q);
+    if (a.x_out) a.x_out[b * d + e] = x;
+  }
+  lin = block_sum(lin, red);
+  q = block_sum(q, red);
+  float ss = 0.f;
+  for (int f = 0; f < a.kfm; ++f) {
+    float p = 0.f;
+    for (int e = threadIdx.x; e < d; e += blockDim.x) p = fmaf(xval(e), v[(int64_t)e * a.kfm + f], p);
+    p = block_sum(p, red);
+    ss = fmaf(p, p, ss);
+  }
+  if (threadIdx.x == 0) a.logit[b] = (lin + a.w0[0]) + 0.5f * (ss - q);
+}
+
+// -------------------------------------------------------------- gather
+struct GatherArgs {
+  const void* ids;
+  int id_kind;
+  int64_t id_stride;
+  const float* dense;
+  int64_t dense_stride;
+  int nd;
+  const float* table;
+  const int64_t* offs;
+  const int64_t* vocab;
+  int F, k;
+  float* out;
+  int64_t out_stride;
+  int64_t batch;
+  int* err;
+  int vec_store;
+};
+
+// Thread t handles chunk q of field c of sample b (VW floats), consecutive
+// threads walk a row then the next field, so 4 threads read one 64-B row.
+template <int VW>
+__global__ __launch_bounds__(256) void embed_gather_kernel(GatherArgs a) {
+  const uint32_t KQ = a.k / VW;
+  const uint32_t per_row = (uint32_t)a.F * KQ;
+  const uint32_t total = (uint32_t)a.batch * per_row;
+  for (uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const uint32_t bb = idx / per_row, r = idx - bb * per_row;
+    const uint32_t c = r / KQ, q = r - c * KQ;
+    const int64_t b = bb;
+    int64_t id;
+    Chunk<VW> x;
+    x.zero();
+    if (decode_id(raw_id(a.ids, a.id_kind, b * a.id_stride + c), a.id_kind, a.vocab[c], id))
+      x.load(a.table + (a.offs[c] + id) * a.k + q * VW);
+    else
+      flag_error(a.err);
+    float* dst = a.out + b * a.out_stride + a.nd + c * a.k + q * VW;
+    if constexpr (VW == 4) {
+      if (a.vec_store) {
+        *reinterpret_cast<floatx4*>(dst) = floatx4{x.v[0], x.v[1], x.v[2], x.v[3]};
+        continue;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < VW; ++t) dst[t] = x.v[t];
+  }
+  if (a.nd > 0) {
+    const uint32_t tot = (uint32_t)a.batch * a.nd;
+    for (uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += gridDim.x * blockDim.x) {
+      const uint32_t bb = idx / a.nd, e = idx - bb * a.nd;
+      a.out[(int64_t)bb * a.out_stride + e] = a.dense[(int64_t)bb * a.dense_stride + e];
+    }
+  }
+}
+
+// ------------------------------------------------------ FM one-hot gather
+struct OnehotArgs {
+  const void* ids;
+  int id_kind;
+  int64_t id_stride;
+  const float* dense;
+  int64_t dense_stride;
+  int nd;
+  const int64_t* offs;
+  const int64_t* vocab;
+  int F;
+  const float* w1;
+  const float* w0;
+  const float* v;
+  int kfm;
+  float* logit;
+  int64_t batch;
+  int* err;
+};
+
+// G lanes per sample (lane f owns latent factor f); 256/G samples per block.
+template <int G>
+__global__ __launch_bounds__(256) void fm_onehot_kernel(OnehotArgs a) {
+  const int f = threadIdx.x % G;
+  const int64_t b = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G;
+  const bool valid = b < a.batch;
+  float s = 0.f, q = 0.f, lin = 0.f;
+  if (valid) {
+    for (int i = 0; i < a.nd; ++i) {
+      const float x = a.dense[b * a.dense_stride + i];
+      const float vf = f < a.kfm ? a.v[(int64_t)i * a.kfm + f] : 0.f;
+      s = fmaf(x, vf, s);
+      q = fmaf(x * x, vf * vf, q);
+      if (f == 0) lin = fmaf(x, a.w1[i], lin);
+    }
+    for (int c = 0; c < a.F; ++c) {
+      int64_t id;
+      if (decode_id(raw_id(a.ids, a.id_kind, b * a.id_stride + c), a.id_kind, a.vocab[c], id)) {
+        const int64_t row = a.nd + a.offs[c] + id;
+        const float vf = f < a.kfm ? a.v[row * a.kfm + f] : 0.f;
+        s += vf;
+        q = fmaf(vf, vf, q);
+        if (f == 0) lin += a.w1[row];
+      } else if (f == 0) {
+        flag_error(a.err);
+      }
+    }
+  }
+  float term = (f < a.kfm) ? (s * s - q) : 0.f;
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) term += __shfl_xor(term, o, G);
+  if (valid && f == 0) a.logit[b] = (lin + a.w0[0]) + 0.5f * term;
+}
+
+// ------------------------------------------------------- launch helpers
+static int grid_for(int64_t work, int block, int cap = 2048) {
+  int64_t g = (work + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+static int fm_nw_default() {
+  static int nw = [] {
+    const char* e = getenv("RS_FM_NW");
+    int v = e ? atoi(e) : 8;
+    return (v == 4 || v == 8) ? v : 8;
+  }();
+  return nw;
+}
+
+template <int KV, int NT>
+static void launch_embed_fm_nw(const EmbedFmArgs& a, int nw, hipStream_t st) {
+  const int grid = (int)((a.batch + 15) / 16);
+  if (nw == 4) embed_fm_mfma<KV, NT, 4><<<grid, 256, 0, st>>>(a);
+  else embed_fm_mfma<KV, NT, 8><<<grid, 512, 0, st>>>(a);
+}
+
+template <int KV>
+static void launch_embed_fm_kv(const EmbedFmArgs& a, int NT, int nw, hipStream_t st) {
+  if (NT == 1) launch_embed_fm_nw<KV, 1>(a, nw, st);
+  else launch_embed_fm_nw<KV, 2>(a, nw, st);
+}
+
+static int run_embed_fm(EmbedFmArgs a, const FmGeom& g, hipStream_t st, const char* what) {
+  if (a.batch == 0) return RS_OK;
+  if (g.mfma) {
+    a.DB = g.DB;
+    a.dense_rec = g.dense_rec;
+    a.field_rec = g.field_rec;
+    a.field_base = g.field_base;
+    const int nw = fm_nw_default();
+    switch (g.KV) {
+      case 1: launch_embed_fm_kv<1>(a, g.NT, nw, st); break;
+      case 2: launch_embed_fm_kv<2>(a, g.NT, nw, st); break;
+      case 4: launch_embed_fm_kv<4>(a, g.NT, nw, st); break;
+      case 8: launch_embed_fm_kv<8>(a, g.NT, nw, st); break;
+      default: launch_embed_fm_kv<16>(a, g.NT, nw, st); break;
+    }
+  } else {
+    if (a.F > 1024) {
+      set_error("%s: generic FM path supports at most 1024 fields", what);
+      return RS_ERR_UNSUPPORTED;
+    }
+    embed_fm_generic<<<(unsigned)a.batch, 256, 0, st>>>(a);
+  }
+  return launch_status(what);
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" int64_t rs_fm_prepared_size(int nd, int n_fields, int k, int kfm) {
+  if (nd < 0 || n_fields < 0 || kfm < 1 || (n_fields > 0 && k < 1)) return -1;
+  return fm_geom(nd, n_fields, k, kfm).size;
+}
+
+extern "C" int rs_fm_prepare(const float* w1, const float* v, int nd, int n_fields, int k, int kfm,
+                             float* prepared, rs_stream_t stream) {
+  RS_REQUIRE(w1 && v && prepared, "rs_fm_prepare: null pointer");
+  RS_REQUIRE(nd >= 0 && n_fields >= 0 && kfm >= 1 && (n_fields == 0 || k >= 1), "rs_fm_prepare: bad shape");
+  const FmGeom g = fm_geom(nd, n_fields, k, kfm);
+  RS_REQUIRE(g.d > 0, "rs_fm_prepare: empty feature vector");
+  hipStream_t st = as_stream(stream);
+  if (g.mfma) {
+    fm_prepare_mfma<<<grid_for(g.size, 256), 256, 0, st>>>(w1, v, nd, n_fields, k, kfm, g.KV, g.NT, g.DB,
+                                                           g.dense_rec, g.field_rec, g.field_base, g.size,
+                                                           prepared);
+  } else {
+    fm_prepare_generic<<<grid_for(g.size, 256), 256, 0, st>>>(w1, v, g.d, kfm, prepared);
+  }
+  return launch_status("rs_fm_prepare");
+}
+
+extern "C" int rs_embed_fm_fwd(const void* ids, int id_kind, int64_t id_stride, const float* dense,
+                               int64_t dense_stride, int nd, const float* table, const int64_t* field_offsets,
+                               const int64_t* field_vocab, int n_fields, int k, const float* prepared,
+                               const float* w0, int kfm, float* logit, float* x_out, int64_t batch,
+                               int* err_flag, rs_stream_t stream) {
+  RS_REQUIRE(batch >= 0 && nd >= 0 && n_fields >= 0 && kfm >= 1, "rs_embed_fm_fwd: bad shape");
+  RS_REQUIRE(prepared && w0 && logit, "rs_embed_fm_fwd: null pointer");
+  RS_REQUIRE(nd == 0 || dense, "rs_embed_fm_fwd: dense is null");
+  RS_REQUIRE(n_fields == 0 || (ids && table && field_offsets && field_vocab && k >= 1),
+             "rs_embed_fm_fwd: sparse inputs missing");
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_embed_fm_fwd: bad id_kind");
+  const FmGeom g = fm_geom(nd, n_fields, k, kfm);
+  EmbedFmArgs a{};
+  a.ids = ids;
+  a.id_kind = id_kind;
+  a.id_stride = id_stride;
+  a.dense = dense;
+  a.dense_stride = dense_stride;
+  a.nd = nd;
+  a.table = table;
+  a.offs = field_offsets;
+  a.vocab = field_vocab;
+  a.F = n_fields;
+  a.k = k;
+  a.prep = prepared;
+  a.w0 = w0;
+  a.kfm = kfm;
+  a.logit = logit;
+  a.x_out = x_out;
+  a.batch = batch;
+  a.err = err_flag;
+  a.direct = 0;
+  return run_embed_fm(a, g, as_stream(stream), "rs_embed_fm_fwd");
+}
+
+extern "C" int rs_rows_fm_fwd(const float* emb, const float* dense, int64_t dense_stride, int nd, int n_fields,
+                              int k, const float* prepared, const float* w0, int kfm, float* logit, int64_t batch,
+                              rs_stream_t stream) {
+  RS_REQUIRE(batch >= 0 && nd >= 0 && n_fields >= 0 && kfm >= 1, "rs_rows_fm_fwd: bad shape");
+  RS_REQUIRE(prepared && w0 && logit && (n_fields == 0 || emb) && (nd == 0 || dense),
+             "rs_rows_fm_fwd: null pointer");
+  const FmGeom g = fm_geom(nd, n_fields, k, kfm);
+  EmbedFmArgs a{};
+  a.dense = dense;
+  a.dense_stride = dense_stride;
+  a.nd = nd;
+  a.table = emb;
+  a.F = n_fields;
+  a.k = k;
+  a.prep = prepared;
+  a.w0 = w0;
+  a.kfm = kfm;
+  a.logit = logit;
+  a.batch = batch;
+  a.direct = 1;
+  return run_embed_fm(a, g, as_stream(stream), "rs_rows_fm_fwd");
+}
+
+extern "C" int rs_fm_fwd(const float* x, int64_t x_stride, int n, const float* prepared, const float* w0, int kfm,
+                         float* logit, int64_t batch, rs_stream_t stream) {
+  RS_REQUIRE(x && prepared && w0 && logit, "rs_fm_fwd: null pointer");
+  RS_REQUIRE(n >= 1 && kfm >= 1 && batch >= 0, "rs_fm_fwd: bad shape");
+  const FmGeom g = fm_geom(n, 0, 0, kfm);
+  EmbedFmArgs a{};
+  a.dense = x;
+  a.dense_stride = x_stride;
+  a.nd = n;
+  a.F = 0;
+  a.k = 0;
+  a.prep = prepared;
+  a.w0 = w0;
+  a.kfm = kfm;
+  a.logit = logit;
+  a.batch = batch;
+  return run_embed_fm(a, g, as_stream(stream), "rs_fm_fwd");
+}
+
+extern "C" int rs_embed_gather(const void* ids, int id_kind, int64_t id_stride, const float* dense,
+                               int64_t dense_stride, int nd, const float* table, const int64_t* field_offsets,
+                               const int64_t* field_vocab, int n_fields, int k, float* out, int64_t out_stride,
+                               int64_t batch, int* err_flag, rs_stream_t stream) {
+  RS_REQUIRE(batch >= 0 && nd >= 0 && n_fields >= 0, "rs_embed_gather: bad shape");
+  RS_REQUIRE(out && (nd == 0 || dense), "rs_embed_gather: null pointer");
+  RS_REQUIRE(n_fields == 0 || (ids && table && field_offsets && field_vocab && k >= 1),
+             "rs_embed_gather: sparse inputs missing");
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_embed_gather: bad id_kind");
+  RS_REQUIRE(out_stride >= nd + (int64_t)n_fields * k, "rs_embed_gather: out_stride too small");
+  RS_REQUIRE(batch * (int64_t)(n_fields * (int64_t)k + nd) < (int64_t)1 << 31,
+             "rs_embed_gather: batch*row too large for one launch");
+  if (batch == 0) return RS_OK;
+  GatherArgs a{ids, id_kind, id_stride, dense, dense_stride, nd, table, field_offsets, field_vocab,
+               n_fields, k, out, out_stride, batch, err_flag, 0};
+  hipStream_t st = as_stream(stream);
+  const bool vec_src = (k % 4 == 0) && ((uintptr_t)table % 16 == 0);
+  if (vec_src) {
+    a.vec_store = ((uintptr_t)out % 16 == 0) && (out_stride % 4 == 0) && (nd % 4 == 0);
+    const int64_t work = batch * n_fields * (k / 4);
+    embed_gather_kernel<4><<<grid_for(work > batch * nd ? work : batch * nd, 256, 8192), 256, 0, st>>>(a);
+  } else {
+    const int64_t work = batch * n_fields * k;
+    embed_gather_kernel<1><<<grid_for(work > batch * nd ? work : batch * nd, 256, 8192), 256, 0, st>>>(a);
+  }
+  return launch_status("rs_embed_gather");
+}
+
+extern "C" int rs_fm_onehot_fwd(const void* ids, int id_kind, int64_t id_stride, const float* dense,
+                                int64_t dense_stride, int nd, const int64_t* field_offsets,
+                                const int64_t* field_vocab, int n_fields, const float* w1, const float* w0,
+                                const float* v, int kfm, float* logit, int64_t batch, int* err_flag,
+                                rs_stream_t stream) {
+  RS_REQUIRE(batch >= 0 && nd >= 0 && n_fields >= 0 && kfm >= 1 && kfm <= 64, "rs_fm_onehot_fwd: bad shape");
+  RS_REQUIRE(w1 && w0 && v && logit && (nd == 0 || dense), "rs_fm_onehot_fwd: null pointer");
+  RS_REQUIRE(n_fields == 0 || (ids && field_offsets && field_vocab), "rs_fm_onehot_fwd: sparse inputs missing");
+  if (batch == 0) return RS_OK;
+  OnehotArgs a{ids, id_kind, id_stride, dense, dense_stride, nd, field_offsets, field_vocab, n_fields,
+               w1, w0, v, kfm, logit, batch, err_flag};
+  hipStream_t st = as_stream(stream);
+  int G = 4;
+  while (G < kfm) G *= 2;
+  const int spb = 256 / G;
+  const unsigned grid = (unsigned)((batch + spb - 1) / spb);
+  switch (G) {
+    case 4: fm_onehot_kernel<4><<<grid, 256, 0, st>>>(a); break;
+    case 8: fm_onehot_kernel<8><<<grid, 256, 0, st>>>(a); break;
+    case 16: fm_onehot_kernel<16><<<grid, 256, 0, st>>>(a); break;
+    case 32: fm_onehot_kernel<32><<<grid, 256, 0, st>>>(a); break;
+    default: fm_onehot_kernel<64><<<grid, 256, 0, st>>>(a); break;
+  }
+  return launch_status("rs_fm_onehot_fwd");
+}

@@ -1,0 +1,106 @@
+// rs_common.hpp — shared device/host helpers for librs_hip.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rs_capi.h"
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+
+namespace rs {
+
+// Thread-local last-error message (rs_last_error_string).
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+
+// Map the status of the launch just issued to an rs_status.
+int launch_status(const char* what);
+
+inline hipStream_t as_stream(rs_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+#define RS_REQUIRE(cond, ...)            \
+  do {                                   \
+    if (!(cond)) {                       \
+      ::rs::set_error(__VA_ARGS__);      \
+      return RS_ERR_ARG;                 \
+    }                                    \
+  } while (0)
+
+// ------------------------------------------------------------ device side
+// Sparse id of (row b, field c) under the Keras Embedding cast semantics.
+// Returns false (and leaves `id` unspecified) when the id is outside
+// [0, vocab): float ids are truncated toward zero first (tf.cast to int32),
+// so e.g. -0.5 -> 0 is valid and -1.0 is not.
+__device__ __forceinline__ bool load_id(const void* ids, int kind, int64_t off,
+                                        int64_t vocab, int64_t& id) {
+  if (kind == RS_ID_I32) {
+    id = static_cast<const int32_t*>(ids)[off];
+  } else if (kind == RS_ID_I64) {
+    id = static_cast<const int64_t*>(ids)[off];
+  } else {
+    const float f = static_cast<const float*>(ids)[off];
+    if (!(f > -1.0f && static_cast<double>(f) < static_cast<double>(vocab))) return false;
+    id = static_cast<int64_t>(f);
+    return true;
+  }
+  return id >= 0 && id < vocab;
+}
+
+__device__ __forceinline__ void flag_error(int* err_flag) {
+  if (err_flag) __hip_atomic_store(err_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int N>
+struct VecF;
+template <>
+struct VecF<1> {
+  typedef float T;
+  static __device__ __forceinline__ float get(const T& v, int) { return v; }
+};
+template <>
+struct VecF<2> {
+  typedef floatx2 T;
+  static __device__ __forceinline__ float get(const T& v, int i) { return v[i]; }
+};
+template <>
+struct VecF<4> {
+  typedef floatx4 T;
+  static __device__ __forceinline__ float get(const T& v, int i) { return v[i]; }
+};
+
+// Load N consecutive floats (N in {1,2,4,8,16}) as vectors; p must be aligned
+// to min(16, 4N) bytes.
+template <int N>
+struct Chunk {
+  float v[N];
+  __device__ __forceinline__ void load(const float* p) {
+    if constexpr (N == 1) {
+      v[0] = p[0];
+    } else if constexpr (N == 2) {
+      floatx2 t = *reinterpret_cast<const floatx2*>(p);
+      v[0] = t[0];
+      v[1] = t[1];
+    } else {
+#pragma unroll
+      for (int q = 0; q < N / 4; ++q) {
+        floatx4 t = *reinterpret_cast<const floatx4*>(p + 4 * q);
+        v[4 * q + 0] = t[0];
+        v[4 * q + 1] = t[1];
+        v[4 * q + 2] = t[2];
+        v[4 * q + 3] = t[3];
+      }
+    }
+  }
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] = 0.f;
+  }
+};
+
+__device__ __forceinline__ floatx4 mfma16x16x4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+}  // namespace rs

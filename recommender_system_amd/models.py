@@ -1,0 +1,264 @@
+"""Keras-Model-compatible CTR models on the MI355X kernels.
+
+Same names, constructor arguments and forward semantics as the reference's
+models (Hcyand/recommender_system, algorithm/deep_learning/model/):
+
+  FM(k, w_reg=1e-4, v_reg=1e-4)                                   model/fm.py:14-23
+  DeepFM(feature_columns, k, w_reg, v_reg, hidden_units, output_dim, activation)
+                                                                  model/deepFM.py:15-31
+  DCN(feature_columns, hidden_units, output_dim, activation, layer_num, reg_w, reg_b)
+                                                                  model/dcn.py:15-34
+  PNN(feature_columns, mode, hidden_units, output_dim, activation='relu',
+      dropout=0.2, use_fgcnn=False)                               model/pnn.py:14-53
+  DIN(feature_columns, behavior_feature_list, att_hidden_units=(80, 40),
+      dnn_hidden_units=(256, 128, 64), att_attention='prelu',
+      dnn_activation='prelu', dnn_dropout=0.0)                    model/din.py:15-95
+
+Criteo-style models take the reference's packed input X[B, 13+F] (dense
+features followed by label-encoded sparse ids, as floats — Keras casts them to
+int32 inside Embedding, so ids are exact only below 2**24), or the pair
+``(dense[B,13] float, ids[B,F] int32/int64)`` which lifts that limit.
+
+Extra keyword ``embed_dim`` (default 8, the reference's EmbedLayer default)
+sets the embedding width: the reference ignores feat['embed_dim'] and always
+uses k=8 (layer/core.py:268-271), so 8 is the drop-in behaviour.
+
+PNN runs with 3-D embeddings [B,F,k] (documented deviation: the reference's
+rank-2 EmbedLayer makes PNN.call raise at model/pnn.py:38).  Modes 'outer' /
+'both' and use_fgcnn=True are outside this build's hot path and raise
+NotImplementedError; an unknown mode raises the reference's ValueError.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._lib import call, ptr
+from .layers import (Attention, BatchNormalization, CrossLayer, Dense, DNNLayer, EmbedLayer, FMLayer,
+                     KerasModule, sigmoid_combine, _ids_tensor, _to_device_f32, _ErrFlag)
+
+
+def _split_criteo(inputs, nd, device):
+    """(dense f32 [B,nd], ids [B,F]) from X[B,nd+F] or a (dense, ids) pair."""
+    if isinstance(inputs, (tuple, list)):
+        dense, ids = inputs
+        return _to_device_f32(dense, device), _ids_tensor(ids, device)
+    X = _to_device_f32(inputs, device)  # Keras autocast (float64 -> float32)
+    return X[:, :nd], X[:, nd:]
+
+
+def _subseed(gen):
+    return int(torch.randint(0, 2 ** 31, (1,), generator=gen))
+
+
+class FM(KerasModule):
+    """FM(k, w_reg, v_reg) — model/fm.py:14-23: sigmoid(FMLayer(x)).
+
+    ``forward(x[B,n])`` takes the reference's one-hot matrix (any dense x).
+    ``forward_onehot(dense, ids, field_offsets)`` takes its compact form and
+    gathers rows of v/w1 instead of multiplying by zeros (same result: the
+    one-hot block has exactly one 1 per field, utils/dataset.py:47-48)."""
+
+    def __init__(self, k, w_reg=1e-4, v_reg=1e-4, device=None, seed=None, print_shape=False):
+        super().__init__(device, seed)
+        self.fm = FMLayer(k, w_reg, v_reg, device=device, seed=_subseed(self._gen))
+        self.print_shape = print_shape  # the reference prints inputs.shape (model/fm.py:20)
+
+    def forward(self, inputs):
+        if self.print_shape:
+            print(tuple(inputs.shape))
+        logit = self.fm(inputs)
+        return sigmoid_combine(logit)
+
+    def forward_onehot(self, dense, ids, field_offsets, field_vocab, check_ids=True):
+        dense = _to_device_f32(dense, self._dev)
+        ids = _ids_tensor(ids, self._dev)
+        offs = torch.as_tensor(field_offsets, dtype=torch.int64, device=self._dev)
+        voc = torch.as_tensor(field_vocab, dtype=torch.int64, device=self._dev)
+        B, nd = dense.shape
+        n = nd + int(voc.sum())
+        if not self.fm.built:
+            self.fm.build(n)
+        logit = torch.empty(B, 1, dtype=torch.float32, device=self._dev)
+        err = _ErrFlag(self._dev)
+        call("rs_fm_onehot_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), nd,
+             ptr(offs), ptr(voc), ids.shape[1], ptr(self.fm.w1), ptr(self.fm.w0), ptr(self.fm.v), self.fm.k,
+             ptr(logit), B, ptr(err.t), _lib.stream())
+        if check_ids:
+            err.check("FM")
+        return sigmoid_combine(logit)
+
+
+class DeepFM(KerasModule):
+    """DeepFM — model/deepFM.py:15-31: x = [dense | EmbedLayer(sparse)],
+    sigmoid(0.5*(FMLayer(x) + DNNLayer(x))).  Embedding lookup + concat + FM
+    run as ONE fused kernel (rs_embed_fm_fwd) that also emits x for the DNN."""
+
+    def __init__(self, feature_columns, k, w_reg, v_reg, hidden_units, output_dim, activation,
+                 embed_dim=8, device=None, seed=None):
+        super().__init__(device, seed)
+        self.dense_feature_columns, self.sparse_feature_columns = feature_columns
+        self.nd = len(self.dense_feature_columns)
+        self.embed_layer = EmbedLayer(self.sparse_feature_columns, embed_dim, device=device, seed=_subseed(self._gen))
+        d = self.nd + self.embed_layer.n_fields * embed_dim
+        self.fm = FMLayer(k, w_reg, v_reg, device=device, seed=_subseed(self._gen), input_dim=d)
+        self.dnn = DNNLayer(hidden_units, output_dim, activation, device=device, seed=_subseed(self._gen))
+        self.dnn.build(d)
+        self._err = _ErrFlag(self._dev)
+
+    def fm_logit(self, inputs, x_out=None, check_ids=True):
+        """The north-star hot path: ids -> rows -> FM logit in one launch."""
+        dense, ids = _split_criteo(inputs, self.nd, self._dev)
+        B = ids.shape[0]
+        e = self.embed_layer
+        prep = self.fm.prepared(self.nd, e.n_fields, e.k)
+        logit = torch.empty(B, 1, dtype=torch.float32, device=self._dev)
+        call("rs_embed_fm_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), self.nd,
+             ptr(e.table), ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, e.k, ptr(prep), ptr(self.fm.w0),
+             self.fm.k, ptr(logit), ptr(x_out), B, ptr(self._err.t), _lib.stream())
+        if check_ids:
+            self._err.check("DeepFM")
+        return logit
+
+    def forward(self, inputs, check_ids=True):
+        dense, ids = _split_criteo(inputs, self.nd, self._dev)
+        B = ids.shape[0]
+        x = torch.empty(B, self.nd + self.embed_layer.n_fields * self.embed_layer.k, dtype=torch.float32,
+                        device=self._dev)
+        fm = self.fm_logit((dense, ids), x_out=x, check_ids=check_ids)
+        dnn = self.dnn(x)
+        return sigmoid_combine(fm, dnn, 0.5, 0.5)
+
+
+class DCN(KerasModule):
+    """DCN — model/dcn.py:15-34: sigmoid(Dense1([CrossLayer(x) | DNNLayer(x)]))."""
+
+    def __init__(self, feature_columns, hidden_units, output_dim, activation, layer_num, reg_w=1e-4, reg_b=1e-4,
+                 embed_dim=8, device=None, seed=None):
+        super().__init__(device, seed)
+        self.dense_feature_columns, self.sparse_feature_columns = feature_columns
+        self.nd = len(self.dense_feature_columns)
+        self.embed_layer = EmbedLayer(self.sparse_feature_columns, embed_dim, device=device, seed=_subseed(self._gen))
+        d = self.nd + self.embed_layer.n_fields * embed_dim
+        self.dense_layer = DNNLayer(hidden_units, output_dim, activation, device=device, seed=_subseed(self._gen))
+        self.dense_layer.build(d)
+        self.cross_layer = CrossLayer(layer_num, reg_w, reg_b, device=device, seed=_subseed(self._gen), input_dim=d)
+        # Dense(1) followed by tf.nn.sigmoid (model/dcn.py:33): the sigmoid is
+        # fused into the Dense epilogue; weights keep the Keras Dense names.
+        self.output_layer = Dense(1, "sigmoid", device=device, seed=_subseed(self._gen), input_dim=d + output_dim)
+        self.d = d
+
+    def forward(self, inputs, check_ids=True):
+        dense, ids = _split_criteo(inputs, self.nd, self._dev)
+        x = self.embed_layer.gather(ids, dense=dense, check_ids=check_ids)
+        B = x.shape[0]
+        z = torch.empty(B, self.d + self.dense_layer.output_layer.units, dtype=torch.float32, device=self._dev)
+        self.cross_layer(x, out=z[:, :self.d])
+        h = x
+        for layer in self.dense_layer.hidden_layer:
+            h = layer(h)
+        self.dense_layer.output_layer(h, out=z[:, self.d:])
+        return self.output_layer(z)
+
+
+class PNN(KerasModule):
+    """PNN(mode='inner') — model/pnn.py:14-53, with 3-D embeddings.
+    Returns the DNN logit (no sigmoid, as the reference)."""
+
+    def __init__(self, feature_columns, mode, hidden_units, output_dim, activation="relu", dropout=0.2,
+                 use_fgcnn=False, embed_dim=8, device=None, seed=None):
+        super().__init__(device, seed)
+        if mode not in ("inner", "outer", "both"):
+            raise ValueError("Please choice mode's value in 'inner', 'outer', 'both'.")
+        if mode != "inner":
+            raise NotImplementedError(f"PNN mode {mode!r}: OuterProductLayer is outside this build's hot path")
+        if use_fgcnn:
+            raise NotImplementedError("PNN use_fgcnn=True: FGCNNLayer is outside this build's hot path")
+        self.mode = mode
+        self.dense_feature_columns, self.sparse_feature_columns = feature_columns
+        self.nd = len(self.dense_feature_columns)
+        self.embed_layer = EmbedLayer(self.sparse_feature_columns, embed_dim, device=device, seed=_subseed(self._gen))
+        F = self.embed_layer.n_fields
+        self.width = F * embed_dim + F * (F - 1) // 2
+        self.dnn_layer = DNNLayer(hidden_units, output_dim, activation, dropout, device=device,
+                                  seed=_subseed(self._gen))
+        self.dnn_layer.build(self.width)
+        self._err = _ErrFlag(self._dev)
+
+    def product_inputs(self, inputs, check_ids=True):
+        """[flat_emb | inner products] in one fused launch (rs_embed_inner_fwd)."""
+        _, ids = _split_criteo(inputs, self.nd, self._dev)
+        e = self.embed_layer
+        B = ids.shape[0]
+        out = torch.empty(B, self.width, dtype=torch.float32, device=self._dev)
+        call("rs_embed_inner_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(e.table), ptr(e.field_offsets),
+             ptr(e.field_vocab), e.n_fields, e.k, ptr(out), out.stride(0), B, ptr(self._err.t), _lib.stream())
+        if check_ids:
+            self._err.check("PNN")
+        return out
+
+    def forward(self, inputs, check_ids=True):
+        return self.dnn_layer(self.product_inputs(inputs, check_ids))
+
+
+class DIN(KerasModule):
+    """DIN — model/din.py:15-95.  ``forward(inputs)`` takes the reference's
+    dict: each dense / non-behaviour sparse feature [B,1] (or [B]), each
+    behaviour feature [B,T] (0 = padding), and the candidate under the
+    hard-coded key 'movie_id' (model/din.py:74)."""
+
+    def __init__(self, feature_columns, behavior_feature_list, att_hidden_units=(80, 40),
+                 dnn_hidden_units=(256, 128, 64), att_attention="prelu", dnn_activation="prelu", dnn_dropout=0.0,
+                 device=None, seed=None):
+        super().__init__(device, seed)
+        self.dense_feature_columns, self.sparse_feature_columns = feature_columns
+        self.behavior_feature_list = list(behavior_feature_list)
+        self.other_sparse = [f for f in self.sparse_feature_columns if f["feat"] not in self.behavior_feature_list]
+        self.seq_feats = [f for f in self.sparse_feature_columns if f["feat"] in self.behavior_feature_list]
+        if len(self.seq_feats) != 1:
+            raise NotImplementedError("DIN: exactly one behaviour feature (the reference's use) is supported")
+        self.other_sparse_num = len(self.other_sparse)
+        self.dense_num = len(self.dense_feature_columns)
+        self.behavior_num = len(self.behavior_feature_list)
+        dev = device
+        self.embed_sparse_layers = torch.nn.ModuleList(
+            [EmbedLayer([f], k=f["embed_dim"], device=dev, seed=_subseed(self._gen)) for f in self.other_sparse])
+        self.embed_seq_layers = torch.nn.ModuleList(
+            [EmbedLayer([f], k=f["embed_dim"], device=dev, seed=_subseed(self._gen)) for f in self.seq_feats])
+        self.att_layer = Attention(att_hidden_units, att_attention, device=dev, seed=_subseed(self._gen))
+        self.bn_layer = BatchNormalization(device=dev)
+        act = "prelu" if dnn_activation == "prelu" else "dice"
+        self.dense_layer = torch.nn.ModuleList(
+            [Dense(u, activation=act, device=dev, seed=_subseed(self._gen)) for u in dnn_hidden_units])
+        self.dropout = dnn_dropout
+        self.out_layer = Dense(1, activation="sigmoid", device=dev, seed=_subseed(self._gen))
+        self._err = _ErrFlag(self._dev)
+
+    def forward(self, inputs, check_ids=True):
+        dev = self._dev
+        seq_layer = self.embed_seq_layers[0]
+        k = seq_layer.k
+        hist = _ids_tensor(inputs[self.seq_feats[0]["feat"]], dev)
+        B, T = hist.shape
+        cand = _ids_tensor(inputs["movie_id"], dev).reshape(B, 1)
+        seq_embed = seq_layer.gather(hist.reshape(B * T, 1), check_ids=check_ids).reshape(B, T, k)
+        item_embed = seq_layer.gather(cand, check_ids=check_ids)
+        mask = (hist != 0).to(torch.float32)
+        att_emb = self.att_layer([item_embed, seq_embed, seq_embed, mask])
+        other_k = sum(l.k for l in self.embed_sparse_layers)
+        width = 2 * k + other_k + self.dense_num
+        emb = torch.empty(B, width, dtype=torch.float32, device=dev)
+        emb[:, :k] = att_emb
+        emb[:, k:2 * k] = item_embed
+        col = 2 * k
+        for f, layer in zip(self.other_sparse, self.embed_sparse_layers):
+            ids = _ids_tensor(inputs[f["feat"]], dev).reshape(B, 1)
+            layer.gather(ids, out=emb[:, col:col + layer.k], check_ids=check_ids)
+            col += layer.k
+        for f in self.dense_feature_columns:
+            emb[:, col:col + 1] = _to_device_f32(inputs[f["feat"]], dev).reshape(B, 1)
+            col += 1
+        x = self.bn_layer(emb)
+        for layer in self.dense_layer:
+            x = layer(x)
+        return self.out_layer(x)

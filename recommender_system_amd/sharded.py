@@ -1,0 +1,147 @@
+"""Row-sharded embedding lookup + FM across the GPUs of one node.
+
+The reference has no distributed code.  This is the MI355X-native design for
+BASELINE config 5: ONE concatenated embedding table (global row of (b,c) =
+field_offsets[c] + id) split into contiguous row blocks, one per rank
+(owner = row // rows_per_rank); dense parameters (w0, w1, v) replicated.
+Per step and rank (B local samples, data parallel):
+
+  1. rs_shard_bucketize  -> per-owner counts, owner-major permutation, local
+                            row ids to request (stable, deterministic)
+  2. all_to_all(counts)  -> how many rows every peer asks of me   (RCCL)
+  3. all_to_all(rows ids)                                          (RCCL)
+  4. rs_gather_rows      -> serve the requested rows from my shard
+  5. all_to_all(rows)    -> my lookups' rows, owner-major          (RCCL)
+  6. rs_unpermute_rows   -> back to sample order [B*F, k]
+  7. rs_rows_fm_fwd      -> FM logit (the same MFMA kernel as the fused path)
+
+Collectives go through torch.distributed (backend "nccl" = RCCL over xGMI on
+ROCm; "gloo" in the CPU tests).  On an 8-GPU MI355X node every peer pair has
+its own xGMI link, so all-to-all is per-link bound: at B=4096, F=26, k=16,
+world=8 each peer exchange is ~13.3k ids (53 KB) and ~13.3k rows (852 KB).
+No all-reduce: forward only.  The local ops are pluggable (``ops``) so the
+exchange protocol is testable with world_size>1 on CPU (tests/test_sharded_gloo.py).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from ._lib import call, ptr
+
+
+class HipShardOps:
+    """Local per-rank steps on librs_hip.so kernels."""
+
+    def __init__(self, device):
+        self.device = device
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self._ws = None
+
+    def bucketize(self, ids, offsets, vocab, rows_per_rank, world):
+        B, F = ids.shape
+        n = B * F
+        counts = torch.empty(world, dtype=torch.int32, device=self.device)
+        perm = torch.empty(n, dtype=torch.int32, device=self.device)
+        send_rows = torch.empty(n, dtype=torch.int32, device=self.device)
+        wsz = _lib.lib().rs_shard_workspace_size(n, world)
+        if self._ws is None or self._ws.numel() < wsz:
+            self._ws = torch.empty(wsz, dtype=torch.uint8, device=self.device)
+        call("rs_shard_bucketize", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(offsets), ptr(vocab), F, B,
+             rows_per_rank, world, ptr(counts), ptr(perm), ptr(send_rows), ptr(self._ws), ptr(self.err),
+             _lib.stream())
+        return counts, perm, send_rows
+
+    def gather_rows(self, table, rows):
+        out = torch.empty(rows.numel(), table.shape[1], dtype=torch.float32, device=self.device)
+        call("rs_gather_rows", ptr(table), table.shape[0], table.shape[1], ptr(rows), rows.numel(), ptr(out),
+             ptr(self.err), _lib.stream())
+        return out
+
+    def unpermute(self, src, perm):
+        out = torch.empty(perm.numel(), src.shape[1], dtype=torch.float32, device=self.device)
+        call("rs_unpermute_rows", ptr(src), ptr(perm), src.shape[1], perm.numel(), ptr(out), _lib.stream())
+        return out
+
+    def rows_fm(self, emb, dense, n_fields, k, prepared, w0, kfm):
+        B = dense.shape[0]
+        logit = torch.empty(B, 1, dtype=torch.float32, device=self.device)
+        call("rs_rows_fm_fwd", ptr(emb), ptr(dense), dense.stride(0), dense.shape[1], n_fields, k, ptr(prepared),
+             ptr(w0), kfm, ptr(logit), B, _lib.stream())
+        return logit
+
+    def check(self):
+        if int(self.err.item()):
+            self.err.zero_()
+            raise IndexError("sharded lookup: embedding id out of range")
+
+
+class ShardedEmbeddingFM:
+    """DeepFM embedding lookup + FM with the table row-sharded over a process
+    group.  ``forward(dense[B,nd], ids[B,F]) -> logit[B,1]`` on every rank."""
+
+    def __init__(self, vocab_sizes, k, nd, kfm, group=None, device=None, seed=0, ops=None, table_init=True):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.vocab_sizes = [int(v) for v in vocab_sizes]
+        self.F, self.k, self.nd, self.kfm = len(self.vocab_sizes), int(k), int(nd), int(kfm)
+        offs = [0]
+        for v in self.vocab_sizes[:-1]:
+            offs.append(offs[-1] + v)
+        self.total_rows = sum(self.vocab_sizes)
+        self.rows_per_rank = math.ceil(self.total_rows / self.world)
+        lo = self.rank * self.rows_per_rank
+        hi = min(self.total_rows, lo + self.rows_per_rank)
+        self.row_range = (lo, hi)
+        self.offsets = torch.tensor(offs, dtype=torch.int64, device=self.device)
+        self.vocab = torch.tensor(self.vocab_sizes, dtype=torch.int64, device=self.device)
+        self.table_shard = torch.empty(max(hi - lo, 0), self.k, dtype=torch.float32, device=self.device)
+        if table_init:
+            g = torch.Generator(device=self.device)
+            g.manual_seed(seed * 1009 + self.rank)
+            self.table_shard.uniform_(-0.05, 0.05, generator=g)
+        d = self.nd + self.F * self.k
+        gen = torch.Generator(device="cpu")
+        gen.manual_seed(seed)  # replicated dense parameters: same on every rank
+        self.w0 = torch.zeros(1, device=self.device)
+        self.w1 = (torch.randn(d, 1, generator=gen) * 0.05).to(self.device)
+        self.v = (torch.randn(d, self.kfm, generator=gen) * 0.05).to(self.device)
+        self.ops = ops if ops is not None else HipShardOps(self.device)
+        self.prepared = None
+        if isinstance(self.ops, HipShardOps):
+            self.prepare()
+
+    def prepare(self):
+        n = _lib.lib().rs_fm_prepared_size(self.nd, self.F, self.k, self.kfm)
+        self.prepared = torch.empty(n, dtype=torch.float32, device=self.device)
+        call("rs_fm_prepare", ptr(self.w1), ptr(self.v), self.nd, self.F, self.k, self.kfm, ptr(self.prepared),
+             _lib.stream())
+
+    # -- the exchange
+    def lookup(self, ids):
+        """[B*F, k] embedding rows of the local batch in sample order."""
+        counts, perm, send_rows = self.ops.bucketize(ids, self.offsets, self.vocab, self.rows_per_rank, self.world)
+        if self.world == 1:
+            reply = self.ops.gather_rows(self.table_shard, send_rows)
+            return self.ops.unpermute(reply, perm)
+        recv_counts = torch.empty_like(counts)
+        dist.all_to_all_single(recv_counts, counts, group=self.group)
+        splits = torch.stack([counts, recv_counts]).cpu().tolist()  # one host sync per step
+        send_split, recv_split = splits[0], splits[1]
+        recv_rows = torch.empty(sum(recv_split), dtype=torch.int32, device=self.device)
+        dist.all_to_all_single(recv_rows, send_rows, recv_split, send_split, group=self.group)
+        reply = self.ops.gather_rows(self.table_shard, recv_rows)
+        got = torch.empty(sum(send_split), self.k, dtype=torch.float32, device=self.device)
+        dist.all_to_all_single(got, reply, send_split, recv_split, group=self.group)
+        return self.ops.unpermute(got, perm)
+
+    def forward(self, dense, ids):
+        emb = self.lookup(ids)
+        return self.ops.rows_fm(emb, dense, self.F, self.k, self.prepared, self.w0, self.kfm)
+
+    __call__ = forward

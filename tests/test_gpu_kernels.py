@@ -1,0 +1,310 @@
+"""GPU parity of every C-ABI kernel against the fp64 oracle (oracle/ctr_oracle.py).
+
+Runs on an MI355X through librs_hip.so (the HIP path is the only path).
+Sizes are small enough for the oracle to finish in seconds; edge cases follow
+what the reference's semantics allow: batch 1 / ragged tails (B not a multiple
+of the 16-sample tile), all id dtypes incl. the packed-float X, ids at 0 and
+vocab-1, out-of-range ids, fully masked DIN rows, L=0 CrossNet, F=2 PNN.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ctr_oracle as O
+from tests.helpers import assert_rel_close, assert_scaled_close, random_ids
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, dev, dtype=torch.float32):
+    return torch.as_tensor(np.asarray(a)).to(dtype).to(dev).contiguous()
+
+
+def _layout(vocabs, dev):
+    offs = np.concatenate([[0], np.cumsum(vocabs)[:-1]]).astype(np.int64)
+    return offs, _t(offs, dev, torch.int64), _t(vocabs, dev, torch.int64)
+
+
+# ------------------------------------------------------------------ gather
+@pytest.mark.parametrize("id_dtype", ["i32", "i64", "f32"])
+@pytest.mark.parametrize("k,nd,B", [(16, 13, 300), (8, 13, 1), (4, 0, 33), (6, 3, 17)])
+def test_embed_gather(gpu, id_dtype, k, nd, B):
+    from recommender_system_amd import _lib
+    rng = np.random.default_rng(k * 100 + B)
+    vocabs = rng.integers(1, 500, size=5).tolist() + [1]
+    offs, offs_d, voc_d = _layout(vocabs, gpu)
+    table = rng.uniform(-0.05, 0.05, size=(sum(vocabs), k)).astype(np.float32)
+    ids = random_ids(rng, B, vocabs)
+    ids[0, :] = np.array(vocabs) - 1
+    dense = rng.random((B, nd)).astype(np.float32)
+    if id_dtype == "f32":
+        ids_d = _t(ids, gpu, torch.float32)
+    else:
+        ids_d = _t(ids, gpu, torch.int32 if id_dtype == "i32" else torch.int64)
+    dense_d = _t(dense, gpu) if nd else None
+    F = len(vocabs)
+    out = torch.full((B, nd + F * k), -7.0, device=gpu)
+    err = torch.zeros(1, dtype=torch.int32, device=gpu)
+    tab_d = _t(table, gpu)
+    _lib.call("rs_embed_gather", ids_d.data_ptr(), _lib.id_kind(ids_d), ids_d.stride(0),
+              None if dense_d is None else dense_d.data_ptr(), nd, nd, tab_d.data_ptr(),
+              offs_d.data_ptr(), voc_d.data_ptr(), F, k, out.data_ptr(), out.stride(0), B, err.data_ptr(), 0)
+    torch.cuda.synchronize()
+    tables = [table[o:o + v] for o, v in zip(offs, vocabs)]
+    ref = np.concatenate([dense, O.embed_layer(ids, tables, np.float64)], 1)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref.astype(np.float32))
+    assert err.item() == 0
+
+
+# ------------------------------------------------------- fused gather + FM
+@pytest.mark.parametrize("k,kfm,F,nd,B", [
+    (16, 10, 26, 13, 300),   # headline shape (DeepFM, dim 16)
+    (8, 10, 26, 13, 65),     # reference default EmbedLayer k=8
+    (4, 8, 5, 3, 1),
+    (32, 15, 7, 13, 40),
+    (16, 16, 26, 13, 50),    # kfm+1 > 16 -> two MFMA column tiles
+    (8, 31, 9, 0, 31),
+    (64, 4, 3, 5, 20),
+    (6, 10, 4, 13, 19),      # k % 4 != 0 -> generic kernel
+    (16, 40, 4, 2, 9),       # kfm >= 32 -> generic kernel
+])
+def test_embed_fm_fused(gpu, k, kfm, F, nd, B):
+    from recommender_system_amd import _lib
+    rng = np.random.default_rng(7 + k + kfm + F)
+    vocabs = rng.integers(2, 300, size=F).tolist()
+    offs, offs_d, voc_d = _layout(vocabs, gpu)
+    d = nd + F * k
+    table = rng.uniform(-0.05, 0.05, size=(sum(vocabs), k)).astype(np.float32)
+    w1 = (rng.standard_normal((d, 1)) * 0.05).astype(np.float32)
+    v = (rng.standard_normal((d, kfm)) * 0.05).astype(np.float32)
+    w0 = np.array([0.0123], np.float32)
+    ids = random_ids(rng, B, vocabs).astype(np.int32)
+    dense = rng.random((B, nd)).astype(np.float32)
+    n = _lib.lib().rs_fm_prepared_size(nd, F, k, kfm)
+    prep = torch.empty(n, device=gpu)
+    w1_d, v_d, w0_d = _t(w1, gpu), _t(v, gpu), _t(w0, gpu)
+    _lib.call("rs_fm_prepare", w1_d.data_ptr(), v_d.data_ptr(), nd, F, k, kfm, prep.data_ptr(), 0)
+    ids_d, dense_d, tab_d = _t(ids, gpu, torch.int32), _t(dense, gpu), _t(table, gpu)
+    logit = torch.full((B,), 99.0, device=gpu)
+    x_out = torch.full((B, d), 99.0, device=gpu)
+    err = torch.zeros(1, dtype=torch.int32, device=gpu)
+    _lib.call("rs_embed_fm_fwd", ids_d.data_ptr(), 0, ids_d.stride(0), dense_d.data_ptr() if nd else None, nd, nd,
+              tab_d.data_ptr(), offs_d.data_ptr(), voc_d.data_ptr(), F, k, prep.data_ptr(), w0_d.data_ptr(),
+              kfm, logit.data_ptr(), x_out.data_ptr(), B, err.data_ptr(), 0)
+    torch.cuda.synchronize()
+    tables = [table[o:o + vv] for o, vv in zip(offs, vocabs)]
+    x = np.concatenate([dense, O.embed_layer(ids, tables, np.float64)], 1)
+    ref = O.fm_layer(x, w0, w1, v)[:, 0]
+    np.testing.assert_array_equal(x_out.cpu().numpy(), x.astype(np.float32))
+    assert_scaled_close(logit, ref, what="embed_fm logit")
+    assert err.item() == 0
+
+
+def test_embed_fm_packed_float_X_and_oor(gpu):
+    """Packed X[B,39] float ids (Keras int32 truncation) and the OOR flag."""
+    from recommender_system_amd import DeepFM
+    from tests.helpers import criteo_columns
+    rng = np.random.default_rng(3)
+    vocabs = rng.integers(2, 200, size=26)
+    cols = criteo_columns(vocabs)
+    m = DeepFM(cols, 10, 1e-4, 1e-4, [32, 16], 1, "relu", embed_dim=16, seed=1)
+    ids = random_ids(rng, 70, vocabs)
+    dense = rng.random((70, 13))
+    X = np.concatenate([dense, ids + 0.25], 1)  # fractional ids truncate
+    a = m.fm_logit(X).cpu().numpy()
+    b = m.fm_logit((dense, ids)).cpu().numpy()
+    np.testing.assert_array_equal(a, b)
+    X[5, 13 + 3] = vocabs[3]  # == vocab -> out of range
+    with pytest.raises(IndexError):
+        m.fm_logit(X)
+    X[5, 13 + 3] = -1.0
+    with pytest.raises(IndexError):
+        m.fm_logit(X)
+    X[5, 13 + 3] = -0.5  # truncates to 0: valid in Keras
+    m.fm_logit(X)
+
+
+# ------------------------------------------------------------- FMLayer dense
+@pytest.mark.parametrize("n,kfm,B", [(429, 10, 257), (43, 8, 5), (5000, 8, 33), (7, 20, 16)])
+def test_fm_layer_dense(gpu, n, kfm, B):
+    from recommender_system_amd import FMLayer
+    rng = np.random.default_rng(n)
+    x = rng.random((B, n)).astype(np.float32)
+    layer = FMLayer(kfm, seed=5)
+    y = layer(x)
+    w = {k: p.detach().cpu().numpy() for k, p in layer.keras_weights().items()}
+    ref = O.fm_layer(x, w["w0"], w["w1"], w["v"])
+    assert_scaled_close(y, ref, what="FMLayer")
+
+
+def test_fm_model_onehot(gpu):
+    """FM model: dense one-hot input == compact gather input == oracle."""
+    from recommender_system_amd import FM
+    rng = np.random.default_rng(11)
+    vocabs = rng.integers(2, 60, size=26)
+    offs = np.concatenate([[0], np.cumsum(vocabs)[:-1]])
+    B, nd = 48, 13
+    ids = random_ids(rng, B, vocabs)
+    dense = rng.random((B, nd))
+    n = nd + int(vocabs.sum())
+    onehot = np.zeros((B, n))
+    onehot[:, :nd] = dense
+    onehot[np.arange(B)[:, None], nd + offs[None, :] + ids] = 1.0
+    m = FM(8, seed=2)
+    y_dense = m(onehot).cpu().numpy()
+    y_gather = m.forward_onehot(dense, ids, offs, vocabs).cpu().numpy()
+    p = {k: v.detach().cpu().numpy() for k, v in m.fm.keras_weights().items()}
+    ref = O.fm_model(onehot, p)
+    assert_rel_close(y_dense, ref, what="FM dense")
+    assert_rel_close(y_gather, ref, what="FM gather")
+
+
+# ---------------------------------------------------------------- CrossNet
+@pytest.mark.parametrize("d,L,B", [(429, 3, 300), (221, 6, 17), (37, 1, 1), (64, 0, 20), (429, 20, 33)])
+def test_cross_layer(gpu, d, L, B):
+    from recommender_system_amd import CrossLayer
+    rng = np.random.default_rng(d + L)
+    x = (rng.standard_normal((B, d)) * 0.3).astype(np.float32)
+    layer = CrossLayer(L, seed=3)
+    y = layer(x)
+    ws = [w.detach().cpu().numpy() for w in layer.cross_weight]
+    bs = [b.detach().cpu().numpy() for b in layer.cross_bias]
+    ref = O.cross_layer(x, ws, bs)
+    assert_scaled_close(y, ref, what="CrossLayer")
+
+
+def test_cross_layer_strided_out(gpu):
+    from recommender_system_amd import CrossLayer
+    rng = np.random.default_rng(1)
+    x = (rng.standard_normal((50, 429)) * 0.3).astype(np.float32)
+    layer = CrossLayer(3, seed=3)
+    z = torch.zeros(50, 431, device=gpu)
+    layer(x, out=z[:, 1:430])
+    ws = [w.detach().cpu().numpy() for w in layer.cross_weight]
+    bs = [b.detach().cpu().numpy() for b in layer.cross_bias]
+    assert_scaled_close(z[:, 1:430], O.cross_layer(x, ws, bs), what="CrossLayer strided")
+    assert float(z[:, 0].abs().max()) == 0.0 and float(z[:, 430].abs().max()) == 0.0
+
+
+# ----------------------------------------------------------- inner product
+@pytest.mark.parametrize("F,k,B", [(26, 16, 100), (26, 8, 3), (2, 4, 10), (3, 5, 7), (39, 32, 9)])
+def test_inner_product(gpu, F, k, B):
+    from recommender_system_amd import InnerProductLayer
+    rng = np.random.default_rng(F * k)
+    e = rng.standard_normal((B, F, k)).astype(np.float32)
+    y = InnerProductLayer()(e)
+    assert_scaled_close(y, O.inner_product_layer(e), what="InnerProduct")
+
+
+def test_embed_inner_fused(gpu):
+    from recommender_system_amd import PNN
+    from tests.helpers import criteo_columns, dnn_params, tables_of
+    rng = np.random.default_rng(5)
+    vocabs = rng.integers(2, 300, size=26)
+    m = PNN(criteo_columns(vocabs), "inner", [64, 32], 1, embed_dim=16, seed=4)
+    ids = random_ids(rng, 77, vocabs)
+    X = np.concatenate([rng.random((77, 13)), ids], 1)
+    z = m.product_inputs(X).cpu().numpy()
+    y = m(X)
+    hidden, out = dnn_params(m.dnn_layer)
+    ref, ref_z = O.pnn_inner(X, {"tables": tables_of(m.embed_layer), "dnn_hidden": hidden, "dnn_out": out})
+    assert_scaled_close(z, ref_z, what="PNN inputs")
+    assert_scaled_close(y, ref, what="PNN logit")
+
+
+# -------------------------------------------------------------- DIN attention
+def _att_params(layer):
+    p = {}
+    if layer.activation == "prelu":
+        p["prelu"] = [(layer.kernels[i].detach().cpu().numpy(), layer.biases[i].detach().cpu().numpy(),
+                       layer.alphas[i].detach().cpu().numpy()) for i in range(len(layer.kernels))]
+    else:
+        p["dice"] = [(d.alphas.detach().cpu().numpy(), d.moving_mean.detach().cpu().numpy(),
+                      d.moving_variance.detach().cpu().numpy(), d.epsilon) for d in layer.dice]
+    p["out"] = (layer.out_kernel.detach().cpu().numpy(), layer.out_bias.detach().cpu().numpy())
+    return p
+
+
+@pytest.mark.parametrize("T,k,h,B", [(100, 8, (80, 40), 37), (10, 8, (80, 40), 5), (1, 4, (16, 16), 3),
+                                     (33, 16, (128, 100), 9), (20, 32, (64, 8), 4)])
+def test_din_attention_prelu(gpu, T, k, h, B):
+    from recommender_system_amd import Attention
+    rng = np.random.default_rng(T * k)
+    q = rng.standard_normal((B, k)).astype(np.float32)
+    key = rng.standard_normal((B, T, k)).astype(np.float32)
+    lens = rng.integers(0, T + 1, size=B)
+    lens[0] = 0  # fully masked row -> uniform average
+    mask = (np.arange(T)[None, :] < lens[:, None]).astype(np.float32)
+    layer = Attention(h, "prelu", seed=9)
+    layer.build(T, k)
+    with torch.no_grad():  # non-zero PReLU alphas and biases to exercise them
+        for a in layer.alphas:
+            a.copy_(torch.as_tensor(rng.uniform(-0.5, 0.5, size=tuple(a.shape)), dtype=torch.float32))
+        for b in layer.biases:
+            b.copy_(torch.as_tensor(rng.uniform(-0.1, 0.1, size=tuple(b.shape)), dtype=torch.float32))
+    y = layer([q, key, key, mask])
+    ref = O.attention(q, key, key, mask, _att_params(layer), "prelu")
+    assert_scaled_close(y, ref, what="Attention prelu")
+    np.testing.assert_allclose(y.cpu().numpy()[0], key[0].mean(0), rtol=1e-5, atol=1e-6)
+
+
+def test_din_attention_dice(gpu):
+    from recommender_system_amd import Attention
+    rng = np.random.default_rng(2)
+    B, T, k = 11, 50, 8
+    q = rng.standard_normal((B, k)).astype(np.float32)
+    key = rng.standard_normal((B, T, k)).astype(np.float32)
+    mask = (rng.random((B, T)) > 0.3).astype(np.float32)
+    layer = Attention((80, 40), "dice", seed=1)
+    layer.build(T, k)
+    with torch.no_grad():
+        for d in layer.dice:
+            d.alphas.uniform_(-0.5, 0.5)
+            d.moving_mean.uniform_(-0.1, 0.1)
+            d.moving_variance.uniform_(0.5, 1.5)
+    y = layer([q, key, key, mask])
+    assert_scaled_close(y, O.attention(q, key, key, mask, _att_params(layer), "dice"), what="Attention dice")
+
+
+# ---------------------------------------------------------------- Dense GEMM
+@pytest.mark.parametrize("M,K,N,act", [(4096, 429, 256, "relu"), (70, 13, 65, None), (33, 256, 128, "prelu"),
+                                       (5, 64, 1, None), (100, 66, 3, "sigmoid"), (1, 1, 7, "relu")])
+def test_dense(gpu, M, K, N, act):
+    from recommender_system_amd import Dense
+    rng = np.random.default_rng(M + K + N)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    layer = Dense(N, act, seed=2)
+    layer.build(K)
+    if act == "prelu":
+        with torch.no_grad():
+            layer.alpha.uniform_(-0.5, 0.5)
+            layer.bias.uniform_(-0.1, 0.1)
+    y = layer(x)
+    ref = O.dense(x, layer.kernel.cpu().numpy(), layer.bias.cpu().numpy(), act,
+                  None if layer.alpha is None else layer.alpha.cpu().numpy())
+    assert_scaled_close(y, ref, what=f"Dense {act}")
+
+
+def test_dice_2d_and_bn(gpu):
+    from recommender_system_amd import BatchNormalization, Dice
+    rng = np.random.default_rng(8)
+    x = rng.standard_normal((40, 66)).astype(np.float32)
+    dice = Dice()
+    dice.build(66)
+    bn = BatchNormalization()
+    bn.build(66)
+    with torch.no_grad():
+        dice.alphas.uniform_(-1, 1)
+        dice.moving_mean.uniform_(-0.2, 0.2)
+        dice.moving_variance.uniform_(0.5, 2.0)
+        for p in (bn.gamma, bn.moving_variance):
+            p.uniform_(0.5, 1.5)
+        for p in (bn.beta, bn.moving_mean):
+            p.uniform_(-0.2, 0.2)
+    xd = torch.as_tensor(x, device=gpu)
+    yd = dice(xd)
+    yb = bn(xd)
+    c = lambda t: t.detach().cpu().numpy()
+    assert_scaled_close(yd, O.dice(x, c(dice.alphas), c(dice.moving_mean), c(dice.moving_variance), 1e-9), what="Dice")
+    assert_scaled_close(yb, O.batchnorm_inference(x, c(bn.moving_mean), c(bn.moving_variance), c(bn.gamma),
+                                                  c(bn.beta), 1e-3), what="BN")
