@@ -127,33 +127,9 @@ __global__ void fm_prepare_generic(const float* __restrict__ w1, const float* __
   }
 }
 
-// ----------------------------------------------------------- id plumbing
-struct RawId {
-  int64_t bits;
-};
-
-__device__ __forceinline__ RawId raw_id(const void* ids, int kind, int64_t off) {
-  RawId r;
-  if (kind == RS_ID_I64) r.bits = static_cast<const int64_t*>(ids)[off];
-  else if (kind == RS_ID_I32) r.bits = static_cast<const int32_t*>(ids)[off];
-  else r.bits = static_cast<int64_t>(__float_as_uint(static_cast<const float*>(ids)[off]));
-  return r;
-}
-
-__device__ __forceinline__ bool decode_id(RawId r, int kind, int64_t vocab, int64_t& id) {
-  if (kind == RS_ID_F32) {
-    const float f = __uint_as_float(static_cast<uint32_t>(r.bits));
-    if (!(f > -1.0f && static_cast<double>(f) < static_cast<double>(vocab))) return false;
-    id = static_cast<int64_t>(f);
-    return true;
-  }
-  id = r.bits;
-  return id >= 0 && id < vocab;
-}
-
+// ----------------------------------------------------------- arguments
 struct EmbedFmArgs {
   const void* ids;
-  int id_kind;
   int64_t id_stride;
   const float* dense;
   int64_t dense_stride;
@@ -172,13 +148,14 @@ struct EmbedFmArgs {
   int* err;
   int DB;
   int64_t dense_rec, field_rec, field_base;
-  int direct;  // rows already gathered: row(b,c) = b*F + c, no ids
 };
 
-template <int KV, int NT, int NW>
+// KIND: 0 i32, 1 i64, 2 f32 ids; 3 = rows already gathered (row(b,c) = b*F+c).
+template <int KV, int NT, int NW, int KIND>
 __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
   constexpr int MAXC0 = 128 / (NW * KV);
   constexpr int MAXC = MAXC0 < 1 ? 1 : (MAXC0 > 8 ? 8 : MAXC0);
+  typedef Ids<KIND == 3 ? 0 : KIND> I;
   __shared__ float cs[NW][16][NT * 16 + 1];
   __shared__ float qs[NW][16];
 
@@ -186,87 +163,121 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int s = lane & 15;   // A: sample row of the tile; B/C: column
   const int kk = lane >> 4;  // k-slot
-  const int64_t b = (int64_t)blockIdx.x * 16 + s;
-  const bool valid = b < a.batch;
+  const int64_t bt = (int64_t)blockIdx.x * 16 + s;
+  const bool valid = bt < a.batch;
+  // Padded lanes of the last tile recompute the last sample: an MFMA output
+  // row depends only on its own A row, so they never touch valid outputs.
+  const int64_t b = valid ? bt : a.batch - 1;
   const int d = a.nd + a.F * a.k;
 
   floatx4 acc[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
   float qn = 0.f;
+  bool bad = false;
 
-  // ---- dense block: k-steps t = w, w+NW, ... (4 dense features per k-step)
-  for (int t = w; t < a.DB; t += NW) {
-    const int e = 4 * t + kk;
-    float xv = 0.f;
-    if (valid && e < a.nd) xv = a.dense[b * a.dense_stride + e];
-    const float* rec = a.prep + (int64_t)t * a.dense_rec;
+  // ---- prologue: everything that does not depend on the ids is issued first
+  // (dense features, packed weights, field offsets/vocab), so the kernel's
+  // critical path is exactly two dependent memory trips: ids -> rows.
+  // A dense block of at most NW k-steps (DeepFM: 13 features = 4 k-steps) is
+  // one k-step per wave; wider dense inputs (FMLayer on a plain x) stream.
+  const bool dense_small = a.DB <= NW;
+  const bool has_dense = dense_small && w < a.DB;  // wave-uniform
+  float dx = 0.f, dn = 0.f, drec[NT];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(xv, rec[nt * 64 + lane], acc[nt]);
-    qn = fmaf(xv * xv, rec[NT * 64 + kk], qn);
-    if (a.x_out && valid && e < a.nd) a.x_out[b * d + e] = xv;
+  for (int nt = 0; nt < NT; ++nt) drec[nt] = 0.f;
+  if (has_dense) {
+    const int e = 4 * w + kk;
+    dx = a.dense[b * a.dense_stride + (e < a.nd ? e : 0)];  // masked at use
+    const float* rec = a.prep + (int64_t)w * a.dense_rec;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) drec[nt] = rec[nt * 64 + lane];
+    dn = rec[NT * 64 + kk];
   }
 
-  // ---- fields: c = cg + j*NW + w
+  // ---- fields c = cg + j*NW + w; slots past F re-read field F-1 and add 0
   for (int cg = 0; cg < a.F; cg += NW * MAXC) {
-    RawId rid[MAXC];
-    // (1) ids first: the only loads the row gather depends on
+    int cj[MAXC];
+    int64_t offc[MAXC], vocc[MAXC];
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
       const int c = cg + j * NW + w;
-      rid[j].bits = 0;
-      if (c < a.F && valid && !a.direct) rid[j] = raw_id(a.ids, a.id_kind, b * a.id_stride + c);
+      cj[j] = c < a.F ? c : a.F - 1;
+      if constexpr (KIND != 3) {
+        offc[j] = a.offs[cj[j]];
+        vocc[j] = a.vocab[cj[j]];
+      }
     }
-    // (2) packed weights (independent of ids): in flight with the ids
+    typename I::raw_t rid[MAXC];
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j)
+      if constexpr (KIND != 3) rid[j] = I::load(a.ids, b * a.id_stride + cj[j]);
     Chunk<KV> bw[MAXC][NT], nw[MAXC];
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
-      const int c = cg + j * NW + w;
-      if (c < a.F) {
-        const float* rec = a.prep + a.field_base + (int64_t)c * a.field_rec;
+      const float* rec = a.prep + a.field_base + (int64_t)cj[j] * a.field_rec;
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) bw[j][nt].load(rec + (int64_t)(nt * 64 + lane) * KV);
-        nw[j].load(rec + NT * 64 * KV + kk * KV);
-      }
+      for (int nt = 0; nt < NT; ++nt) bw[j][nt].load(rec + (int64_t)(nt * 64 + lane) * KV);
+      nw[j].load(rec + NT * 64 * KV + kk * KV);
     }
-    // (3) row gather: KV consecutive floats of the sample's row per lane
+    // row gather: KV consecutive floats of the sample's row per lane
     Chunk<KV> xs[MAXC];
+    bool ok[MAXC];
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
-      const int c = cg + j * NW + w;
-      xs[j].zero();
-      if (c < a.F && valid) {
-        int64_t row = -1;
-        if (a.direct) {
-          row = b * a.F + c;
-        } else {
-          int64_t id;
-          if (decode_id(rid[j], a.id_kind, a.vocab[c], id)) row = a.offs[c] + id;
-          else flag_error(a.err);
-        }
-        if (row >= 0) xs[j].load(a.table + row * a.k + KV * kk);
+      int64_t row;
+      if constexpr (KIND == 3) {
+        row = b * a.F + cj[j];
+        ok[j] = true;
+      } else {
+        int64_t id;
+        ok[j] = I::decode(rid[j], vocc[j], id);
+        row = offc[j] + id;
       }
+      xs[j].load(a.table + row * a.k + KV * kk);
     }
-    // (4) MFMA over the field's KV k-steps + |v|^2 correction
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
-      const int c = cg + j * NW + w;
-      if (c < a.F) {
+      const bool live = cg + j * NW + w < a.F;
+      bad |= live && !ok[j];
+      const bool use = live && ok[j];
 #pragma unroll
-        for (int tp = 0; tp < KV; ++tp) {
-          const float xv = xs[j].v[tp];
+      for (int tp = 0; tp < KV; ++tp) {
+        const float xv = use ? xs[j].v[tp] : 0.f;
 #pragma unroll
-          for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(xv, bw[j][nt].v[tp], acc[nt]);
-          qn = fmaf(xv * xv, nw[j].v[tp], qn);
-        }
-        if (a.x_out && valid) {
-          float* xo = a.x_out + b * d + a.nd + c * a.k + KV * kk;
+        for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(xv, bw[j][nt].v[tp], acc[nt]);
+        qn = fmaf(xv * xv, nw[j].v[tp], qn);
+      }
+      if (a.x_out && live && valid) {
+        float* xo = a.x_out + b * d + a.nd + cj[j] * a.k + KV * kk;
 #pragma unroll
-          for (int tp = 0; tp < KV; ++tp) xo[tp] = xs[j].v[tp];
-        }
+        for (int tp = 0; tp < KV; ++tp) xo[tp] = ok[j] ? xs[j].v[tp] : 0.f;
       }
     }
   }
+
+  // ---- dense MFMAs (their loads were issued in the prologue)
+  if (has_dense) {
+    const int e = 4 * w + kk;
+    dx = e < a.nd ? dx : 0.f;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(dx, drec[nt], acc[nt]);
+    qn = fmaf(dx * dx, dn, qn);
+    if (a.x_out && valid && e < a.nd) a.x_out[b * d + e] = dx;
+  }
+  if (!dense_small) {
+    for (int t = w; t < a.DB; t += NW) {
+      const int e = 4 * t + kk;
+      const float xv = a.dense[b * a.dense_stride + (e < a.nd ? e : 0)];
+      const float x = e < a.nd ? xv : 0.f;
+      const float* rec = a.prep + (int64_t)t * a.dense_rec;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(x, rec[nt * 64 + lane], acc[nt]);
+      qn = fmaf(x * x, rec[NT * 64 + kk], qn);
+      if (a.x_out && valid && e < a.nd) a.x_out[b * d + e] = x;
+    }
+  }
+  if (__any(bad && valid) && lane == 0) flag_error(a.err);
 
   // ---- combine the NW partial tiles
 #pragma unroll
@@ -315,7 +326,9 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
+template <int KIND>
 __global__ __launch_bounds__(256) void embed_fm_generic(EmbedFmArgs a) {
+  typedef Ids<KIND == 3 ? 0 : KIND> I;
   __shared__ int64_t rows[1024];
   __shared__ float red[4];
   const int64_t b = blockIdx.x;
@@ -324,15 +337,11 @@ __global__ __launch_bounds__(256) void embed_fm_generic(EmbedFmArgs a) {
   const float* v = a.prep + d;
   const float* nsq = a.prep + (int64_t)d * (a.kfm + 1);
   for (int c = threadIdx.x; c < a.F; c += blockDim.x) {
-    int64_t row = -1;
-    if (a.direct) {
-      row = b * a.F + c;
-    } else {
+    int64_t row = b * a.F + c;
+    if constexpr (KIND != 3) {
       int64_t id;
-      if (decode_id(raw_id(a.ids, a.id_kind, b * a.id_stride + c), a.id_kind, a.vocab[c], id))
-        row = a.offs[c] + id;
-      else
-        flag_error(a.err);
+      if (I::decode(I::load(a.ids, b * a.id_stride + c), a.vocab[c], id)) row = a.offs[c] + id;
+      else { row = -1; flag_error(a.err); }
     }
     rows[c] = row;
   }
@@ -365,7 +374,6 @@ __global__ __launch_bounds__(256) void embed_fm_generic(EmbedFmArgs a) {
 // -------------------------------------------------------------- gather
 struct GatherArgs {
   const void* ids;
-  int id_kind;
   int64_t id_stride;
   const float* dense;
   int64_t dense_stride;
@@ -381,34 +389,36 @@ struct GatherArgs {
   int vec_store;
 };
 
-// Thread t handles chunk q of field c of sample b (VW floats), consecutive
+// Thread t handles chunk q of field c of sample b (VW floats); consecutive
 // threads walk a row then the next field, so 4 threads read one 64-B row.
-template <int VW>
+template <int VW, int KIND>
 __global__ __launch_bounds__(256) void embed_gather_kernel(GatherArgs a) {
+  typedef Ids<KIND> I;
   const uint32_t KQ = a.k / VW;
   const uint32_t per_row = (uint32_t)a.F * KQ;
   const uint32_t total = (uint32_t)a.batch * per_row;
+  bool bad = false;
   for (uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
     const uint32_t bb = idx / per_row, r = idx - bb * per_row;
     const uint32_t c = r / KQ, q = r - c * KQ;
     const int64_t b = bb;
     int64_t id;
+    const bool ok = I::decode(I::load(a.ids, b * a.id_stride + c), a.vocab[c], id);
+    bad |= !ok;
     Chunk<VW> x;
-    x.zero();
-    if (decode_id(raw_id(a.ids, a.id_kind, b * a.id_stride + c), a.id_kind, a.vocab[c], id))
-      x.load(a.table + (a.offs[c] + id) * a.k + q * VW);
-    else
-      flag_error(a.err);
+    x.load(a.table + (a.offs[c] + id) * a.k + q * VW);
     float* dst = a.out + b * a.out_stride + a.nd + c * a.k + q * VW;
     if constexpr (VW == 4) {
       if (a.vec_store) {
-        *reinterpret_cast<floatx4*>(dst) = floatx4{x.v[0], x.v[1], x.v[2], x.v[3]};
+        *reinterpret_cast<floatx4*>(dst) =
+            ok ? floatx4{x.v[0], x.v[1], x.v[2], x.v[3]} : floatx4{0.f, 0.f, 0.f, 0.f};
         continue;
       }
     }
 #pragma unroll
-    for (int t = 0; t < VW; ++t) dst[t] = x.v[t];
+    for (int t = 0; t < VW; ++t) dst[t] = ok ? x.v[t] : 0.f;
   }
+  if (bad) flag_error(a.err);
   if (a.nd > 0) {
     const uint32_t tot = (uint32_t)a.batch * a.nd;
     for (uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += gridDim.x * blockDim.x) {
@@ -421,7 +431,6 @@ __global__ __launch_bounds__(256) void embed_gather_kernel(GatherArgs a) {
 // ------------------------------------------------------ FM one-hot gather
 struct OnehotArgs {
   const void* ids;
-  int id_kind;
   int64_t id_stride;
   const float* dense;
   int64_t dense_stride;
@@ -439,36 +448,39 @@ struct OnehotArgs {
 };
 
 // G lanes per sample (lane f owns latent factor f); 256/G samples per block.
-template <int G>
+template <int G, int KIND>
 __global__ __launch_bounds__(256) void fm_onehot_kernel(OnehotArgs a) {
+  typedef Ids<KIND> I;
   const int f = threadIdx.x % G;
-  const int64_t b = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G;
-  const bool valid = b < a.batch;
+  const int64_t bt = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G;
+  const bool valid = bt < a.batch;
+  const int64_t b = valid ? bt : a.batch - 1;
+  const int fc = f < a.kfm ? f : 0;
   float s = 0.f, q = 0.f, lin = 0.f;
-  if (valid) {
-    for (int i = 0; i < a.nd; ++i) {
-      const float x = a.dense[b * a.dense_stride + i];
-      const float vf = f < a.kfm ? a.v[(int64_t)i * a.kfm + f] : 0.f;
-      s = fmaf(x, vf, s);
-      q = fmaf(x * x, vf * vf, q);
-      if (f == 0) lin = fmaf(x, a.w1[i], lin);
-    }
-    for (int c = 0; c < a.F; ++c) {
-      int64_t id;
-      if (decode_id(raw_id(a.ids, a.id_kind, b * a.id_stride + c), a.id_kind, a.vocab[c], id)) {
-        const int64_t row = a.nd + a.offs[c] + id;
-        const float vf = f < a.kfm ? a.v[row * a.kfm + f] : 0.f;
-        s += vf;
-        q = fmaf(vf, vf, q);
-        if (f == 0) lin += a.w1[row];
-      } else if (f == 0) {
-        flag_error(a.err);
-      }
-    }
+  bool bad = false;
+  for (int i = 0; i < a.nd; ++i) {
+    const float x = a.dense[b * a.dense_stride + i];
+    const float vf = f < a.kfm ? a.v[(int64_t)i * a.kfm + fc] : 0.f;
+    s = fmaf(x, vf, s);
+    q = fmaf(x * x, vf * vf, q);
+    lin = fmaf(x, a.w1[i], lin);
+  }
+  for (int c = 0; c < a.F; ++c) {
+    int64_t id;
+    const bool ok = I::decode(I::load(a.ids, b * a.id_stride + c), a.vocab[c], id);
+    bad |= !ok;
+    const int64_t row = a.nd + a.offs[c] + id;
+    const float vr = a.v[row * a.kfm + fc];
+    const float wr = a.w1[row];
+    const float vf = (ok && f < a.kfm) ? vr : 0.f;
+    s += vf;
+    q = fmaf(vf, vf, q);
+    lin += ok ? wr : 0.f;
   }
   float term = (f < a.kfm) ? (s * s - q) : 0.f;
 #pragma unroll
   for (int o = G / 2; o > 0; o >>= 1) term += __shfl_xor(term, o, G);
+  if (bad && valid && f == 0) flag_error(a.err);
   if (valid && f == 0) a.logit[b] = (lin + a.w0[0]) + 0.5f * term;
 }
 
@@ -480,49 +492,59 @@ static int grid_for(int64_t work, int block, int cap = 2048) {
   return (int)g;
 }
 
-static int fm_nw_default() {
-  static int nw = [] {
-    const char* e = getenv("RS_FM_NW");
-    int v = e ? atoi(e) : 8;
-    return (v == 4 || v == 8) ? v : 8;
-  }();
-  return nw;
-}
-
-template <int KV, int NT>
-static void launch_embed_fm_nw(const EmbedFmArgs& a, int nw, hipStream_t st) {
+template <int KV, int NT, int KIND>
+static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st) {
+  constexpr int NW = 16;
   const int grid = (int)((a.batch + 15) / 16);
-  if (nw == 4) embed_fm_mfma<KV, NT, 4><<<grid, 256, 0, st>>>(a);
-  else embed_fm_mfma<KV, NT, 8><<<grid, 512, 0, st>>>(a);
+  embed_fm_mfma<KV, NT, NW, KIND><<<grid, NW * 64, 0, st>>>(a);
 }
 
-template <int KV>
-static void launch_embed_fm_kv(const EmbedFmArgs& a, int NT, int nw, hipStream_t st) {
-  if (NT == 1) launch_embed_fm_nw<KV, 1>(a, nw, st);
-  else launch_embed_fm_nw<KV, 2>(a, nw, st);
+template <int KIND>
+static void launch_embed_fm_k(const EmbedFmArgs& a, int KV, int NT, hipStream_t st) {
+  if (NT == 1) {
+    switch (KV) {
+      case 1: launch_embed_fm3<1, 1, KIND>(a, st); break;
+      case 2: launch_embed_fm3<2, 1, KIND>(a, st); break;
+      case 4: launch_embed_fm3<4, 1, KIND>(a, st); break;
+      case 8: launch_embed_fm3<8, 1, KIND>(a, st); break;
+      default: launch_embed_fm3<16, 1, KIND>(a, st); break;
+    }
+  } else {
+    switch (KV) {
+      case 1: launch_embed_fm3<1, 2, KIND>(a, st); break;
+      case 2: launch_embed_fm3<2, 2, KIND>(a, st); break;
+      case 4: launch_embed_fm3<4, 2, KIND>(a, st); break;
+      case 8: launch_embed_fm3<8, 2, KIND>(a, st); break;
+      default: launch_embed_fm3<16, 2, KIND>(a, st); break;
+    }
+  }
 }
 
-static int run_embed_fm(EmbedFmArgs a, const FmGeom& g, hipStream_t st, const char* what) {
+// kind: RS_ID_* or 3 (rows already gathered)
+static int run_embed_fm(EmbedFmArgs a, const FmGeom& g, int kind, hipStream_t st, const char* what) {
   if (a.batch == 0) return RS_OK;
   if (g.mfma) {
     a.DB = g.DB;
     a.dense_rec = g.dense_rec;
     a.field_rec = g.field_rec;
     a.field_base = g.field_base;
-    const int nw = fm_nw_default();
-    switch (g.KV) {
-      case 1: launch_embed_fm_kv<1>(a, g.NT, nw, st); break;
-      case 2: launch_embed_fm_kv<2>(a, g.NT, nw, st); break;
-      case 4: launch_embed_fm_kv<4>(a, g.NT, nw, st); break;
-      case 8: launch_embed_fm_kv<8>(a, g.NT, nw, st); break;
-      default: launch_embed_fm_kv<16>(a, g.NT, nw, st); break;
+    if (a.F == 0) {
+      // dense-only (FMLayer on x): no field loop runs, any instantiation works
+      launch_embed_fm_k<3>(a, 4, g.NT, st);
+    } else if (kind == 3) {
+      launch_embed_fm_k<3>(a, g.KV, g.NT, st);
+    } else {
+      with_id_kind(kind, [&](auto K) { launch_embed_fm_k<decltype(K)::value>(a, g.KV, g.NT, st); });
     }
   } else {
     if (a.F > 1024) {
       set_error("%s: generic FM path supports at most 1024 fields", what);
       return RS_ERR_UNSUPPORTED;
     }
-    embed_fm_generic<<<(unsigned)a.batch, 256, 0, st>>>(a);
+    if (kind == 3 || a.F == 0) embed_fm_generic<3><<<(unsigned)a.batch, 256, 0, st>>>(a);
+    else with_id_kind(kind, [&](auto K) {
+      embed_fm_generic<decltype(K)::value><<<(unsigned)a.batch, 256, 0, st>>>(a);
+    });
   }
   return launch_status(what);
 }
@@ -564,10 +586,10 @@ extern "C" int rs_embed_fm_fwd(const void* ids, int id_kind, int64_t id_stride, 
   RS_REQUIRE(n_fields == 0 || (ids && table && field_offsets && field_vocab && k >= 1),
              "rs_embed_fm_fwd: sparse inputs missing");
   RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_embed_fm_fwd: bad id_kind");
+  RS_REQUIRE(k % 4 != 0 || (uintptr_t)table % 16 == 0, "rs_embed_fm_fwd: table must be 16-B aligned");
   const FmGeom g = fm_geom(nd, n_fields, k, kfm);
   EmbedFmArgs a{};
   a.ids = ids;
-  a.id_kind = id_kind;
   a.id_stride = id_stride;
   a.dense = dense;
   a.dense_stride = dense_stride;
@@ -584,8 +606,7 @@ extern "C" int rs_embed_fm_fwd(const void* ids, int id_kind, int64_t id_stride, 
   a.x_out = x_out;
   a.batch = batch;
   a.err = err_flag;
-  a.direct = 0;
-  return run_embed_fm(a, g, as_stream(stream), "rs_embed_fm_fwd");
+  return run_embed_fm(a, g, id_kind, as_stream(stream), "rs_embed_fm_fwd");
 }
 
 extern "C" int rs_rows_fm_fwd(const float* emb, const float* dense, int64_t dense_stride, int nd, int n_fields,
@@ -594,6 +615,7 @@ extern "C" int rs_rows_fm_fwd(const float* emb, const float* dense, int64_t dens
   RS_REQUIRE(batch >= 0 && nd >= 0 && n_fields >= 0 && kfm >= 1, "rs_rows_fm_fwd: bad shape");
   RS_REQUIRE(prepared && w0 && logit && (n_fields == 0 || emb) && (nd == 0 || dense),
              "rs_rows_fm_fwd: null pointer");
+  RS_REQUIRE(k % 4 != 0 || (uintptr_t)emb % 16 == 0, "rs_rows_fm_fwd: emb must be 16-B aligned");
   const FmGeom g = fm_geom(nd, n_fields, k, kfm);
   EmbedFmArgs a{};
   a.dense = dense;
@@ -607,8 +629,7 @@ extern "C" int rs_rows_fm_fwd(const float* emb, const float* dense, int64_t dens
   a.kfm = kfm;
   a.logit = logit;
   a.batch = batch;
-  a.direct = 1;
-  return run_embed_fm(a, g, as_stream(stream), "rs_rows_fm_fwd");
+  return run_embed_fm(a, g, 3, as_stream(stream), "rs_rows_fm_fwd");
 }
 
 extern "C" int rs_fm_fwd(const float* x, int64_t x_stride, int n, const float* prepared, const float* w0, int kfm,
@@ -627,7 +648,7 @@ extern "C" int rs_fm_fwd(const float* x, int64_t x_stride, int n, const float* p
   a.kfm = kfm;
   a.logit = logit;
   a.batch = batch;
-  return run_embed_fm(a, g, as_stream(stream), "rs_fm_fwd");
+  return run_embed_fm(a, g, 3, as_stream(stream), "rs_fm_fwd");
 }
 
 extern "C" int rs_embed_gather(const void* ids, int id_kind, int64_t id_stride, const float* dense,
@@ -643,17 +664,27 @@ extern "C" int rs_embed_gather(const void* ids, int id_kind, int64_t id_stride, 
   RS_REQUIRE(batch * (int64_t)(n_fields * (int64_t)k + nd) < (int64_t)1 << 31,
              "rs_embed_gather: batch*row too large for one launch");
   if (batch == 0) return RS_OK;
-  GatherArgs a{ids, id_kind, id_stride, dense, dense_stride, nd, table, field_offsets, field_vocab,
+  GatherArgs a{ids, id_stride, dense, dense_stride, nd, table, field_offsets, field_vocab,
                n_fields, k, out, out_stride, batch, err_flag, 0};
   hipStream_t st = as_stream(stream);
   const bool vec_src = (k % 4 == 0) && ((uintptr_t)table % 16 == 0);
-  if (vec_src) {
+  if (n_fields == 0) {
+    a.F = 0;
+    a.k = 4;
+    embed_gather_kernel<4, 0><<<grid_for(batch * nd, 256, 8192), 256, 0, st>>>(a);
+  } else if (vec_src) {
     a.vec_store = ((uintptr_t)out % 16 == 0) && (out_stride % 4 == 0) && (nd % 4 == 0);
     const int64_t work = batch * n_fields * (k / 4);
-    embed_gather_kernel<4><<<grid_for(work > batch * nd ? work : batch * nd, 256, 8192), 256, 0, st>>>(a);
+    with_id_kind(id_kind, [&](auto K) {
+      embed_gather_kernel<4, decltype(K)::value>
+          <<<grid_for(work > batch * nd ? work : batch * nd, 256, 8192), 256, 0, st>>>(a);
+    });
   } else {
     const int64_t work = batch * n_fields * k;
-    embed_gather_kernel<1><<<grid_for(work > batch * nd ? work : batch * nd, 256, 8192), 256, 0, st>>>(a);
+    with_id_kind(id_kind, [&](auto K) {
+      embed_gather_kernel<1, decltype(K)::value>
+          <<<grid_for(work > batch * nd ? work : batch * nd, 256, 8192), 256, 0, st>>>(a);
+    });
   }
   return launch_status("rs_embed_gather");
 }
@@ -666,20 +697,24 @@ extern "C" int rs_fm_onehot_fwd(const void* ids, int id_kind, int64_t id_stride,
   RS_REQUIRE(batch >= 0 && nd >= 0 && n_fields >= 0 && kfm >= 1 && kfm <= 64, "rs_fm_onehot_fwd: bad shape");
   RS_REQUIRE(w1 && w0 && v && logit && (nd == 0 || dense), "rs_fm_onehot_fwd: null pointer");
   RS_REQUIRE(n_fields == 0 || (ids && field_offsets && field_vocab), "rs_fm_onehot_fwd: sparse inputs missing");
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_fm_onehot_fwd: bad id_kind");
   if (batch == 0) return RS_OK;
-  OnehotArgs a{ids, id_kind, id_stride, dense, dense_stride, nd, field_offsets, field_vocab, n_fields,
+  OnehotArgs a{ids, id_stride, dense, dense_stride, nd, field_offsets, field_vocab, n_fields,
                w1, w0, v, kfm, logit, batch, err_flag};
   hipStream_t st = as_stream(stream);
   int G = 4;
   while (G < kfm) G *= 2;
   const int spb = 256 / G;
   const unsigned grid = (unsigned)((batch + spb - 1) / spb);
-  switch (G) {
-    case 4: fm_onehot_kernel<4><<<grid, 256, 0, st>>>(a); break;
-    case 8: fm_onehot_kernel<8><<<grid, 256, 0, st>>>(a); break;
-    case 16: fm_onehot_kernel<16><<<grid, 256, 0, st>>>(a); break;
-    case 32: fm_onehot_kernel<32><<<grid, 256, 0, st>>>(a); break;
-    default: fm_onehot_kernel<64><<<grid, 256, 0, st>>>(a); break;
-  }
+  with_id_kind(id_kind, [&](auto K) {
+    constexpr int KI = decltype(K)::value;
+    switch (G) {
+      case 4: fm_onehot_kernel<4, KI><<<grid, 256, 0, st>>>(a); break;
+      case 8: fm_onehot_kernel<8, KI><<<grid, 256, 0, st>>>(a); break;
+      case 16: fm_onehot_kernel<16, KI><<<grid, 256, 0, st>>>(a); break;
+      case 32: fm_onehot_kernel<32, KI><<<grid, 256, 0, st>>>(a); break;
+      default: fm_onehot_kernel<64, KI><<<grid, 256, 0, st>>>(a); break;
+    }
+  });
   return launch_status("rs_fm_onehot_fwd");
 }

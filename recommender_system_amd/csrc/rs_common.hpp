@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "rs_capi.h"
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -44,6 +46,41 @@ __device__ __forceinline__ bool load_id(const void* ids, int kind, int64_t off,
     return true;
   }
   return id >= 0 && id < vocab;
+}
+
+// Compile-time id plumbing for the hot kernels (no per-lane branches):
+// KIND 0 = int32, 1 = int64, 2 = float32 (Keras int32 truncation), 3 = no ids
+// (rows already gathered).  decode() returns validity and a clamped id (0 when
+// invalid) so the caller can issue the row load unconditionally and zero it.
+template <int KIND>
+struct Ids {
+  typedef typename std::conditional<KIND == 1, int64_t,
+                                    typename std::conditional<KIND == 2, float, int32_t>::type>::type raw_t;
+  static __device__ __forceinline__ raw_t load(const void* p, int64_t off) {
+    return static_cast<const raw_t*>(p)[off];
+  }
+  static __device__ __forceinline__ bool decode(raw_t r, int64_t vocab, int64_t& id) {
+    if constexpr (KIND == 2) {
+      const bool ok = (r > -1.0f) && (static_cast<double>(r) < static_cast<double>(vocab));
+      id = ok ? static_cast<int64_t>(r) : 0;
+      return ok;
+    } else {
+      const int64_t v = static_cast<int64_t>(r);
+      const bool ok = (v >= 0) && (v < vocab);
+      id = ok ? v : 0;
+      return ok;
+    }
+  }
+};
+
+// Host helper: call f(std::integral_constant<int, KIND>) for a runtime id kind.
+template <class Fn>
+inline void with_id_kind(int kind, Fn&& f) {
+  switch (kind) {
+    case RS_ID_I32: f(std::integral_constant<int, 0>()); break;
+    case RS_ID_I64: f(std::integral_constant<int, 1>()); break;
+    default: f(std::integral_constant<int, 2>()); break;
+  }
 }
 
 __device__ __forceinline__ void flag_error(int* err_flag) {

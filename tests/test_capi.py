@@ -1,0 +1,61 @@
+"""CPU: librs_hip.so loads, exports every symbol include/rs_capi.h declares,
+matches the ctypes signature table, and rejects bad arguments before any
+device work (these calls launch nothing)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from recommender_system_amd import _lib
+
+HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "rs_capi.h")
+
+
+def declared():
+    txt = open(HDR).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(rs_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_symbols_exported_and_bound():
+    lib = _lib.lib()
+    names = declared()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in rs_capi.h but not exported"
+    assert set(names) == set(_lib.SIGNATURES), "ctypes table out of sync with rs_capi.h"
+
+
+def test_version_and_sizes():
+    lib = _lib.lib()
+    assert b"gfx950" in lib.rs_version()
+    n = lib.rs_fm_prepared_size(13, 26, 16, 10)
+    assert n == 4 * (64 + 4) + 26 * (64 * 4 + 16)  # dense records + field records
+    assert lib.rs_fm_prepared_size(-1, 26, 16, 10) == -1
+    assert lib.rs_cross_prepared_size(429, 3) > 108 * 64
+    assert lib.rs_shard_workspace_size(4096 * 26, 8) > 0
+    assert lib.rs_shard_workspace_size(10, 65) == -1
+
+
+def test_argument_validation_without_device():
+    lib = _lib.lib()
+    st = lib.rs_embed_fm_fwd(None, 0, 26, None, 13, 13, None, None, None, 26, 16, None, None, 10, None, None, 4096,
+                             None, None)
+    assert st == -1 and b"null" in lib.rs_last_error_string()
+    assert lib.rs_dense_fwd(None, 4, None, None, None, 0, None, 4, 4, 4, 4, None) == -1
+    assert lib.rs_din_attention_fwd(*([C.c_void_p(1)] * 4), 100, 12, *([C.c_void_p(1)] * 3), 80,
+                                    *([C.c_void_p(1)] * 3), 40, C.c_void_p(1), C.c_void_p(1), C.c_void_p(1), 8,
+                                    None) == -1
+    assert b"k must be" in lib.rs_last_error_string()
+    assert lib.rs_cross_fwd(C.c_void_p(1), 10, 10, 40, C.c_void_p(1), C.c_void_p(1), 10, 4, None) == -1
+    with pytest.raises(_lib.RSError):
+        _lib.call("rs_sigmoid_combine", None, None, 1.0, 1.0, None, 4, None)
+
+
+def test_product_path_has_no_cpu_fallback():
+    import torch
+    from recommender_system_amd import FMLayer
+    layer = FMLayer(4, device="cpu", input_dim=8)
+    with pytest.raises(_lib.RSError, match="device"):
+        layer(torch.zeros(2, 8))

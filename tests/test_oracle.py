@@ -1,0 +1,132 @@
+"""CPU: known-answer tests that pin the oracle (the reference has no tests and
+its TF/Keras arithmetic cannot run here), plus the oracle's Keras semantics."""
+import numpy as np
+import pytest
+
+from oracle import ctr_oracle as O
+
+
+def test_fm_trick_equals_pairwise():
+    rng = np.random.default_rng(0)
+    x = rng.random((20, 37))
+    v = rng.standard_normal((37, 6)) * 0.05
+    w1 = rng.standard_normal((37, 1)) * 0.05
+    w0 = np.array([0.3])
+    a = O.fm_layer(x, w0, w1, v)
+    b = O.fm_layer_pairwise(x, w0, w1, v)
+    np.testing.assert_allclose(a, b, rtol=0, atol=1e-13)
+
+
+def test_fm_onehot_equals_gather():
+    rng = np.random.default_rng(1)
+    vocabs = rng.integers(2, 30, 26)
+    offs = np.concatenate([[0], np.cumsum(vocabs)[:-1]])
+    B, nd = 17, 13
+    ids = np.stack([rng.integers(0, v, B) for v in vocabs], 1)
+    dense = rng.random((B, nd))
+    n = nd + vocabs.sum()
+    x = np.zeros((B, n))
+    x[:, :nd] = dense
+    x[np.arange(B)[:, None], nd + offs[None] + ids] = 1
+    v = rng.standard_normal((n, 8)) * 0.05
+    w1 = rng.standard_normal((n, 1)) * 0.05
+    w0 = np.array([0.1])
+    np.testing.assert_allclose(O.fm_onehot_gather(dense, ids, offs, w0, w1, v), O.fm_layer(x, w0, w1, v),
+                               rtol=0, atol=1e-13)
+
+
+def test_cross_layer_equals_loop():
+    rng = np.random.default_rng(2)
+    x = rng.standard_normal((9, 21))
+    ws = [rng.standard_normal(21) * 0.05 for _ in range(4)]
+    bs = [rng.standard_normal(21) * 0.05 for _ in range(4)]
+    np.testing.assert_allclose(O.cross_layer(x, ws, bs), O.cross_layer_loop(x, ws, bs), rtol=1e-13, atol=1e-13)
+
+
+def test_cross_affine_closed_form():
+    """x_L = alpha_L x0 + beta_L — the identity the MFMA CrossNet kernel uses."""
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((5, 30))
+    ws = [rng.standard_normal(30) * 0.1 for _ in range(3)]
+    bs = [rng.standard_normal(30) * 0.1 for _ in range(3)]
+    beta = np.zeros(30)
+    alpha = np.ones(5)
+    for w, b in zip(ws, bs):
+        g = x @ w
+        h = beta @ w
+        alpha = alpha * (1 + g) + h
+        beta = beta + b
+    np.testing.assert_allclose(alpha[:, None] * x + beta, O.cross_layer(x, ws, bs), rtol=1e-12, atol=1e-12)
+
+
+def test_inner_product_equals_loop_and_order():
+    rng = np.random.default_rng(4)
+    e = rng.standard_normal((3, 6, 5))
+    np.testing.assert_allclose(O.inner_product_layer(e), O.inner_product_loop(e), rtol=1e-13)
+    row, col = O.pair_indices(4)
+    assert list(zip(row, col)) == [(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)]
+
+
+def _att_params(rng, k, T, h=(8, 4)):
+    W1 = rng.uniform(-0.3, 0.3, (4 * k, h[0]))
+    W2 = rng.uniform(-0.3, 0.3, (h[0], h[1]))
+    return {"prelu": [(W1, np.zeros(h[0]), rng.uniform(-.5, .5, (T, h[0]))),
+                      (W2, np.zeros(h[1]), rng.uniform(-.5, .5, (T, h[1])))],
+            "out": (rng.uniform(-0.3, 0.3, (h[1], 1)), np.zeros(1))}
+
+
+def test_attention_single_unmasked_and_all_masked():
+    rng = np.random.default_rng(5)
+    B, T, k = 3, 7, 4
+    q = rng.standard_normal((B, k))
+    key = rng.standard_normal((B, T, k))
+    mask = np.zeros((B, T))
+    mask[0, 3] = 1  # one valid position -> that value row
+    p = _att_params(rng, k, T)
+    out = O.attention(q, key, key, mask, p)
+    np.testing.assert_allclose(out[0], key[0, 3], rtol=1e-12)
+    np.testing.assert_allclose(out[1], key[1].mean(0), rtol=1e-12)  # fully masked -> uniform
+
+
+def test_mask_fill_value_is_float32_rounded():
+    assert O.MASK_FILL == -4294967295
+    assert np.float32(O.MASK_FILL) == np.float32(-4294967296.0)
+
+
+def test_embedding_cast_and_range():
+    t = np.arange(12.0).reshape(6, 2)
+    ids = np.array([0.9, 5.99, -0.5])
+    np.testing.assert_array_equal(O.embedding_lookup(t, ids), t[[0, 5, 0]])  # truncation toward zero
+    with pytest.raises(IndexError):
+        O.embedding_lookup(t, np.array([6]))
+    with pytest.raises(IndexError):
+        O.embedding_lookup(t, np.array([-1.0]))
+
+
+def test_embed_layer_is_field_major_flat():
+    t0 = np.arange(6.0).reshape(3, 2)
+    t1 = 10 + np.arange(8.0).reshape(4, 2)
+    out = O.embed_layer(np.array([[1, 3], [0, 0]]), [t0, t1])
+    np.testing.assert_array_equal(out, [[2, 3, 16, 17], [0, 1, 10, 11]])
+
+
+def test_dice_and_bn_inference():
+    x = np.array([[0.5, -2.0]])
+    y = O.dice(x, alpha=np.array([0.25, 0.25]), mean=np.zeros(2), var=np.ones(2), eps=1e-9)
+    p = 1 / (1 + np.exp(-x / np.sqrt(1 + 1e-9)))
+    np.testing.assert_allclose(y, 0.25 * (1 - p) * x + p * x)
+    np.testing.assert_allclose(O.batchnorm_inference(x, 0, 1, eps=1e-3), x / np.sqrt(1.001))
+
+
+def test_deepfm_oracle_composition():
+    rng = np.random.default_rng(6)
+    vocabs = [5, 7, 3]
+    tables = [rng.uniform(-0.05, 0.05, (v, 4)) for v in vocabs]
+    d = 2 + 3 * 4
+    p = {"tables": tables, "w0": np.zeros(1), "w1": rng.standard_normal((d, 1)) * 0.05,
+         "v": rng.standard_normal((d, 3)) * 0.05,
+         "dnn_hidden": [(rng.uniform(-.1, .1, (d, 8)), np.zeros(8))], "dnn_out": (rng.uniform(-.1, .1, (8, 1)), np.zeros(1))}
+    X = np.concatenate([rng.random((4, 2)), np.stack([rng.integers(0, v, 4) for v in vocabs], 1)], 1)
+    y, fm, x = O.deepfm(X, p, nd=2)
+    dnn = O.dnn_layer(x, p["dnn_hidden"], p["dnn_out"])
+    np.testing.assert_allclose(y, 1 / (1 + np.exp(-0.5 * (fm + dnn))))
