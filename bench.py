@@ -100,6 +100,51 @@ def _timed(fn, steps, warmup, world, events=True):
     return _max_over_ranks(dt, world), ms
 
 
+def _capture(fn, first, count):
+    """HIP graph of `count` consecutive steps fn(first) .. fn(first+count-1)."""
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for i in range(count):
+                fn(first + i)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    return g
+
+
+def _timed_graph(fn, steps, warmup, world, chunk=64):
+    """Exactly `steps` steps replayed from HIP graphs of `chunk` steps (plus
+    one tail graph), timed between barrier+sync; also returns the event time
+    per graph launch-slot (kernel + inter-kernel boundary)."""
+    for i in range(warmup):
+        fn(i)
+    torch.cuda.synchronize()
+    full, tail = divmod(steps, chunk)
+    g_full = _capture(fn, 0, chunk) if full else None
+    g_tail = _capture(fn, 0, tail) if tail else None
+    for g in (g_full, g_tail):
+        if g is not None:
+            g.replay()
+    torch.cuda.synchronize()
+    _barrier(world)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    s.record()
+    for _ in range(full):
+        g_full.replay()
+    if g_tail is not None:
+        g_tail.replay()
+    e.record()
+    torch.cuda.synchronize()
+    _barrier(world)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return _max_over_ranks(dt, world), s.elapsed_time(e) / steps
+
+
 def _pool(B, vocabs, nd, n_pool, device, dtype=torch.int32):
     g = torch.Generator(device=device)
     g.manual_seed(SEED)
@@ -165,7 +210,6 @@ def bench_hotpath(args, world, rank):
         logit = torch.empty(B, 1, device=dev)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
         lib = _lib.lib()
-        stream = _lib.stream()
         tptr, optr, vptr = e.table.data_ptr(), e.field_offsets.data_ptr(), e.field_vocab.data_ptr()
         pptr, w0ptr, lptr, eptr = prep.data_ptr(), model.fm.w0.data_ptr(), logit.data_ptr(), err.data_ptr()
 
@@ -173,23 +217,31 @@ def bench_hotpath(args, world, rank):
             j = i % ids_pool.shape[0]
             ids, dense = ids_pool[j], dense_pool[j]
             st = lib.rs_embed_fm_fwd(ids.data_ptr(), 0, F, dense.data_ptr(), nd, nd, tptr, optr, vptr, F, k, pptr,
-                                     w0ptr, kfm, lptr, None, B, eptr, stream)
+                                     w0ptr, kfm, lptr, None, B, eptr, _lib.stream())
             if st:
                 _lib.check(st, "rs_embed_fm_fwd")
 
-        dt, ms = _timed(step, args.steps, args.warmup, world)
+        # value: the K timed steps replayed from HIP graphs (no host launch cost)
+        dt, slot_ms = _timed_graph(step, args.steps, args.warmup, world)
+        # kernel duration: HIP events around each launch on the launch stream
+        _, ms = _timed(step, args.steps, 0, world)
         assert int(err.item()) == 0
-        kern_ms = float(np.mean(ms))
-        bytes_per_launch = B * (F * 4 + nd * 4 + F * k * 4 + 4) + (prep.numel() * 4 // 1)
+        kern_ms = slot_ms  # HIP events over the graph-replayed timed region, per launch
+        bytes_per_launch = B * (F * 4 + nd * 4 + F * k * 4 + 4) + prep.numel() * 4
         alg_bytes = B * 1824 + 18880
         achieved = alg_bytes / (kern_ms * 1e-3)
         result["value"] = args.steps * B / dt
         result["ms_per_step"] = dt / args.steps * 1e3
         result["roofline"] = {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                               "frac": achieved / PEAK_HBM, "traffic": _pmc_traffic(),
-                              "kernel": "embed_fm_mfma", "kernel_ms_avg": kern_ms,
-                              "kernel_ms_min": float(np.min(ms)), "algorithmic_bytes_per_launch": alg_bytes,
-                              "bytes_incl_packed_weights": int(bytes_per_launch)}
+                              "kernel": "embed_fm_mfma", "kernel_ms": kern_ms,
+                              "kernel_ms_source": "HIP events around the graph-replayed timed region / steps "
+                                                  "(kernel + back-to-back dispatch boundary)",
+                              "eager_launch_event_ms_median": float(np.median(ms)),
+                              "algorithmic_bytes_per_launch": alg_bytes,
+                              "bytes_incl_packed_weights": int(bytes_per_launch),
+                              "random_64B_row_ceiling_GBps": 3310.0,
+                              "frac_of_random_row_ceiling": achieved / 3.31e12}
         # full DeepFM forward (secondary)
         xbuf = torch.empty(B, nd + F * k, device=dev)
 
@@ -200,8 +252,8 @@ def bench_hotpath(args, world, rank):
             dnn = model.dnn(xbuf)
             rs.sigmoid_combine(fm, dnn, 0.5, 0.5)
 
-        dt2, _ = _timed(full, max(10, args.steps // 5), args.warmup, world, events=False)
         n2 = max(10, args.steps // 5)
+        dt2, _ = _timed_graph(full, n2, args.warmup, world, chunk=16)
         flops = B * 2 * (429 * 256 + 256 * 128 + 128 * 64 + 64)
         result["deepfm_forward"] = {"samples_per_s": n2 * B / dt2, "ms_per_step": dt2 / n2 * 1e3,
                                     "dnn_flop_per_step": flops, "note": "fused gather+FM (x emitted) + DNN "
@@ -242,6 +294,158 @@ def bench_hotpath(args, world, rank):
     return result
 
 
+def _line(metric, value, unit, args, world, ms_per_step, config, roofline, extra=None, dtype="f32", hib=True):
+    out = {"metric": metric, "value": value, "unit": unit, "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": hib, "scaling": "weak",
+           "vs_baseline": None, "dtype": dtype, "data": "synthetic", "config": config, "roofline": roofline,
+           "cpu_baseline": None}
+    if extra:
+        out.update(extra)
+    return out
+
+
+def bench_dcn(args, world, rank):
+    """Config 3: DCN CrossNet depth 3 on the DeepFM feature shape (26 x 1e6 x 16,
+    13 dense, d = 429), B = 4096: step = rs_embed_gather (x) + rs_cross_fwd."""
+    import recommender_system_amd as rs
+    B, F, V, k, nd = args.batch, 26, int(args.vocab if args.vocab != 1e7 else 1e6), 16, 13
+    dev = torch.device("cuda")
+    cols = [[{"feat": f"I{i + 1}"} for i in range(nd)],
+            [{"feat": f"C{i + 1}", "feat_onehot_dim": V, "embed_dim": k} for i in range(F)]]
+    model = rs.DCN(cols, [256, 128, 64], 1, "relu", layer_num=3, embed_dim=k, seed=SEED, device=dev)
+    ids_pool, dense_pool = _pool(B, [V] * F, nd, 64, dev)
+    d = nd + F * k
+    x = torch.empty(B, d, device=dev)
+    y = torch.empty(B, d, device=dev)
+    model.cross_layer.prepared(d)
+
+    def gather(i):
+        j = i % 64
+        model.embed_layer.gather(ids_pool[j], dense=dense_pool[j], out=x, check_ids=False)
+
+    def cross_only(i):
+        model.cross_layer(x, out=y)
+
+    def step(i):
+        gather(i)
+        cross_only(i)
+
+    dt, slot = _timed_graph(step, args.steps, args.warmup, world)
+    gather(0)
+    _, cross_ms = _timed_graph(cross_only, args.steps, 5, world)
+    alg = B * 2 * d * 4 + 3 * 2 * d * 4  # read x0, write x_L (+ weights)
+    ach = alg / (cross_ms * 1e-3)
+    useful = B * d * 3 * 2
+    issued = ((B + 15) // 16) * ((d + 3) // 4) * 16 * 16 * 4 * 2
+    n2 = max(10, args.steps // 5)
+
+    def full(i):
+        j = i % 64
+        model((dense_pool[j], ids_pool[j]), check_ids=False)
+
+    dt2, _ = _timed_graph(full, n2, args.warmup, world, chunk=16)
+    return _line("DCN CrossNet forward samples/sec @ batch 4096, 26 sparse x 1e6 vocab, dim 16, depth 3",
+                 args.steps * B / dt, "samples/s", args, world, dt / args.steps * 1e3,
+                 {"workload": "dcn_embed_gather+crossnet_depth3", "global_batch": B, "d": d, "layer_num": 3,
+                  "vocab_per_field": V, "parallelism": "dp1"},
+                 {"bound": "hbm", "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                  "frac": ach / PEAK_HBM, "traffic": None, "kernel": "cross_mfma", "kernel_ms": cross_ms,
+                  "algorithmic_bytes_per_launch": alg, "mfma_useful_flop_per_launch": useful,
+                  "mfma_issued_flop_per_launch": issued, "mfma_useful_fraction_by_construction": useful / issued},
+                 {"dcn_forward": {"samples_per_s": n2 * B / dt2, "ms_per_step": dt2 / n2 * 1e3}})
+
+
+def bench_din(args, world, rank):
+    """Config 4: DIN, Amazon-Electronics-shaped: B = 2048, T = 100, behaviour
+    vocab 63,001, k = 8, 1 dense + user_id (192,404); step = behaviour-seq +
+    candidate gathers + the attention-unit kernel."""
+    import recommender_system_amd as rs
+    B, T, k = 2048 if args.batch == 4096 else args.batch, 100, 8
+    dev = torch.device("cuda")
+    cols = [[{"feat": "age"}],
+            [{"feat": "user_id", "feat_onehot_dim": 192404, "embed_dim": k},
+             {"feat": "movies_seq", "feat_onehot_dim": 63001, "embed_dim": k}]]
+    model = rs.DIN(cols, ["movies_seq"], seed=SEED, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(SEED)
+    pool = []
+    for _ in range(8):
+        lens = torch.randint(1, T + 1, (B,), generator=g, device=dev)
+        hist = torch.randint(1, 63001, (B, T), generator=g, device=dev)
+        hist = torch.where(torch.arange(T, device=dev)[None, :] < lens[:, None], hist, torch.zeros_like(hist))
+        pool.append({"age": torch.rand(B, 1, generator=g, device=dev),
+                     "user_id": torch.randint(0, 192404, (B, 1), generator=g, device=dev),
+                     "movie_id": torch.randint(1, 63001, (B, 1), generator=g, device=dev),
+                     "movies_seq": hist})
+    seq_layer = model.embed_seq_layers[0]
+    att = model.att_layer
+    seq = torch.empty(B * T, k, device=dev)
+    item = torch.empty(B, k, device=dev)
+    out = torch.empty(B, k, device=dev)
+    masks = [(p["movies_seq"] != 0).to(torch.float32) for p in pool]
+    model(pool[0], check_ids=False)  # builds the attention weights (alpha: [T, h])
+    with torch.no_grad():
+        for a in att.alphas:
+            a.uniform_(-0.25, 0.25)
+
+    def step(i):
+        p = pool[i % 8]
+        seq_layer.gather(p["movies_seq"].reshape(B * T, 1), out=seq, check_ids=False)
+        seq_layer.gather(p["movie_id"], out=item, check_ids=False)
+        s3 = seq.view(B, T, k)
+        att([item, s3, s3, masks[i % 8]], out=out)
+
+    def att_only(i):
+        s3 = seq.view(B, T, k)
+        att([item, s3, s3, masks[i % 8]], out=out)
+
+    dt, _ = _timed_graph(step, args.steps, args.warmup, world)
+    _, att_ms = _timed_graph(att_only, args.steps, 5, world)
+    flop = B * T * 2 * (4 * k * 80 + 80 * 40 + 40)
+    ach = flop / (att_ms * 1e-3)
+    issued = B * ((T + 15) // 16) * 16 * 2 * (5 * 16 * 4 * k + 3 * 16 * 80)
+    n2 = max(10, args.steps // 5)
+
+    def full(i):
+        model(pool[i % 8], check_ids=False)
+
+    dt2, _ = _timed(full, n2, args.warmup, world, events=False)
+    return _line("DIN forward samples/sec @ batch 2048, behaviour seq len 100 (attention unit)",
+                 args.steps * B / dt, "samples/s", args, world, dt / args.steps * 1e3,
+                 {"workload": "din_seq_gather+attention_unit", "global_batch": B, "seq_len": T, "embed_dim": k,
+                  "att_hidden": [80, 40], "behaviour_vocab": 63001, "parallelism": "dp1"},
+                 {"bound": "mfma", "achieved": ach / 1e12, "peak": PEAK_F32 / 1e12, "unit": "TFLOP/s",
+                  "frac": ach / PEAK_F32, "traffic": None, "kernel": "din_attention_mfma", "kernel_ms": att_ms,
+                  "useful_flop_per_launch": flop, "issued_mfma_flop_per_launch": issued},
+                 {"din_forward": {"samples_per_s": n2 * B / dt2, "ms_per_step": dt2 / n2 * 1e3,
+                                  "note": "eager (host-synchronous id checks off); BN + PReLU MLP + heads"}})
+
+
+def bench_pnn(args, world, rank):
+    """PNN inner-product path: fused gather + flatten + inner products, B=4096,
+    26 x 1e6 x 16 -> [B, 416 + 325]."""
+    import recommender_system_amd as rs
+    B, F, V, k, nd = args.batch, 26, int(args.vocab if args.vocab != 1e7 else 1e6), 16, 13
+    dev = torch.device("cuda")
+    cols = [[{"feat": f"I{i + 1}"} for i in range(nd)],
+            [{"feat": f"C{i + 1}", "feat_onehot_dim": V, "embed_dim": k} for i in range(F)]]
+    model = rs.PNN(cols, "inner", [256, 128, 64], 1, embed_dim=k, seed=SEED, device=dev)
+    ids_pool, dense_pool = _pool(B, [V] * F, nd, 64, dev)
+
+    def step(i):
+        model.product_inputs((dense_pool[i % 64], ids_pool[i % 64]), check_ids=False)
+
+    dt, slot = _timed_graph(step, args.steps, args.warmup, world)
+    alg = B * (F * 4 + F * k * 4 + (F * k + F * (F - 1) // 2) * 4)
+    ach = alg / (slot * 1e-3)
+    return _line("PNN inner-product input samples/sec @ batch 4096, 26 sparse x 1e6 vocab, dim 16",
+                 args.steps * B / dt, "samples/s", args, world, dt / args.steps * 1e3,
+                 {"workload": "pnn_embed_inner_fused", "global_batch": B, "vocab_per_field": V, "parallelism": "dp1"},
+                 {"bound": "hbm", "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                  "frac": ach / PEAK_HBM, "traffic": None, "kernel": "inner_kernel", "kernel_ms": slot,
+                  "algorithmic_bytes_per_launch": alg})
+
+
 def _pmc_traffic():
     p = os.path.join(ROOT, "profiles", "pmc_embed_fm.json")
     try:
@@ -264,7 +468,15 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     args = ap.parse_args()
     world, rank = _dist_setup(args)
-    if args.config != "hotpath":
+    other = {"dcn": bench_dcn, "din": bench_din, "pnn": bench_pnn}
+    if args.config in other:
+        line = other[args.config](args, world, rank)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        return
+    if args.config == "deepfm1e6":
+        args.vocab = 1e6
+    elif args.config != "hotpath":
         raise SystemExit(f"unknown --config {args.config}")
     res = bench_hotpath(args, world, rank)
     if rank == 0:

@@ -148,7 +148,28 @@ struct EmbedFmArgs {
   int* err;
   int DB;
   int64_t dense_rec, field_rec, field_base;
+  unsigned long long* dbg;  // diagnostic builds only (RS_DIAG_STAMPS): phase stamps
 };
+
+// Phase stamps (s_memrealtime, 100 MHz) for the diagnostic library built by
+// scripts/build_diag.sh; compiled out of librs_hip.so.
+#ifdef RS_DIAG_STAMPS
+#define RS_STAMP(i)                                                                          \
+  do {                                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                       \
+    if (a.dbg && lane == 0)                                                                  \
+      a.dbg[((int64_t)blockIdx.x * NW + w) * 8 + (i)] = __builtin_amdgcn_s_memrealtime();   \
+    __builtin_amdgcn_sched_barrier(0);                                                       \
+  } while (0)
+#define RS_USE(x) asm volatile("" ::"v"(x))
+#else
+#define RS_STAMP(i) \
+  do {              \
+  } while (0)
+#define RS_USE(x) \
+  do {            \
+  } while (0)
+#endif
 
 // KIND: 0 i32, 1 i64, 2 f32 ids; 3 = rows already gathered (row(b,c) = b*F+c).
 template <int KV, int NT, int NW, int KIND>
@@ -181,61 +202,114 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
   // critical path is exactly two dependent memory trips: ids -> rows.
   // A dense block of at most NW k-steps (DeepFM: 13 features = 4 k-steps) is
   // one k-step per wave; wider dense inputs (FMLayer on a plain x) stream.
+  // Materialise every kernel argument at entry: one batched s_load instead
+  // of lazy per-use kernarg loads (each a dependent K$ round trip).
+  asm volatile("" ::"s"(a.ids), "s"(a.id_stride), "s"(a.dense), "s"(a.dense_stride), "s"(a.nd), "s"(a.table),
+               "s"(a.offs), "s"(a.vocab), "s"(a.F), "s"(a.k), "s"(a.prep), "s"(a.kfm));
+  asm volatile("" ::"s"(a.batch), "s"(a.DB), "s"(a.dense_rec), "s"(a.field_rec), "s"(a.field_base), "s"(a.x_out),
+               "s"(a.logit), "s"(a.w0), "s"(a.err));
+  RS_STAMP(0);
+  RS_USE(b);
+  RS_STAMP(5);
   const bool dense_small = a.DB <= NW;
   const bool has_dense = dense_small && w < a.DB;  // wave-uniform
   float dx = 0.f, dn = 0.f, drec[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) drec[nt] = 0.f;
-  if (has_dense) {
-    const int e = 4 * w + kk;
-    dx = a.dense[b * a.dense_stride + (e < a.nd ? e : 0)];  // masked at use
-    const float* rec = a.prep + (int64_t)w * a.dense_rec;
+  auto load_dense = [&]() {
+    if (has_dense) {
+      const int e = 4 * w + kk;
+      dx = a.dense[b * a.dense_stride + (e < a.nd ? e : 0)];  // masked at use
+      const float* rec = a.prep + (int64_t)w * a.dense_rec;
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) drec[nt] = rec[nt * 64 + lane];
-    dn = rec[NT * 64 + kk];
+      for (int nt = 0; nt < NT; ++nt) drec[nt] = rec[nt * 64 + lane];
+      dn = rec[NT * 64 + kk];
+    }
+  };
+  // ---- cooperative id tile: the workgroup's 16 x F ids and the F field
+  // (offset, vocab) pairs arrive through coalesced loads into LDS, once per
+  // workgroup (instead of 4 redundant lanes per id and one metadata load per
+  // wave and field), then one barrier.  Fields beyond FMAX use direct loads.
+  constexpr int FMAX = 128;
+  __shared__ typename I::raw_t lid[16][FMAX];
+  __shared__ int64_t lmeta[2][FMAX];
+  const bool coop = (KIND != 3) && a.F <= FMAX;
+  if (coop) {
+    const int64_t b0 = (int64_t)blockIdx.x * 16;
+    for (int t = threadIdx.x; t < 16 * a.F; t += NW * 64) {
+      const int ss = t / a.F, c = t - ss * a.F;
+      const int64_t bb = b0 + ss < a.batch ? b0 + ss : a.batch - 1;
+      lid[ss][c] = I::load(a.ids, bb * a.id_stride + c);
+    }
+    for (int t = threadIdx.x; t < 2 * a.F; t += NW * 64) {
+      const int c = t < a.F ? t : t - a.F;
+      lmeta[t < a.F ? 0 : 1][c] = t < a.F ? a.offs[c] : a.vocab[c];
+    }
   }
+  if (a.F == 0 || coop) load_dense();
+  if (coop) __syncthreads();
 
   // ---- fields c = cg + j*NW + w; slots past F re-read field F-1 and add 0
   for (int cg = 0; cg < a.F; cg += NW * MAXC) {
     int cj[MAXC];
     int64_t offc[MAXC], vocc[MAXC];
+    // Field metadata through the VECTOR path (wave index taken from the raw
+    // thread id, not readfirstlane, so these are not scalar loads): issued
+    // with the ids, no dependent K$-miss round trip on the critical path.
+    const int wv = threadIdx.x >> 6;
+    typename I::raw_t rid[MAXC];
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
       const int c = cg + j * NW + w;
       cj[j] = c < a.F ? c : a.F - 1;
       if constexpr (KIND != 3) {
-        offc[j] = a.offs[cj[j]];
-        vocc[j] = a.vocab[cj[j]];
+        if (coop) {
+          offc[j] = lmeta[0][cj[j]];
+          vocc[j] = lmeta[1][cj[j]];
+          rid[j] = lid[s][cj[j]];
+        } else {
+          const int cv = min(cg + j * NW + wv, a.F - 1);
+          offc[j] = a.offs[cv];
+          vocc[j] = a.vocab[cv];
+          rid[j] = I::load(a.ids, b * a.id_stride + cj[j]);
+        }
       }
     }
-    typename I::raw_t rid[MAXC];
-#pragma unroll
-    for (int j = 0; j < MAXC; ++j)
-      if constexpr (KIND != 3) rid[j] = I::load(a.ids, b * a.id_stride + cj[j]);
-    Chunk<KV> bw[MAXC][NT], nw[MAXC];
-#pragma unroll
-    for (int j = 0; j < MAXC; ++j) {
-      const float* rec = a.prep + a.field_base + (int64_t)cj[j] * a.field_rec;
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) bw[j][nt].load(rec + (int64_t)(nt * 64 + lane) * KV);
-      nw[j].load(rec + NT * 64 * KV + kk * KV);
-    }
+    if (cg == 0 && !coop && a.F > 0) load_dense();
+    RS_STAMP(6);
     // row gather: KV consecutive floats of the sample's row per lane
     Chunk<KV> xs[MAXC];
     bool ok[MAXC];
+    int64_t row[MAXC];
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
-      int64_t row;
       if constexpr (KIND == 3) {
-        row = b * a.F + cj[j];
+        row[j] = b * a.F + cj[j];
         ok[j] = true;
       } else {
         int64_t id;
         ok[j] = I::decode(rid[j], vocc[j], id);
-        row = offc[j] + id;
+        row[j] = offc[j] + id;
       }
-      xs[j].load(a.table + row * a.k + KV * kk);
     }
+    RS_USE(row[MAXC - 1]);
+    RS_STAMP(1);
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) xs[j].load_nt(a.table + row[j] * a.k + KV * kk);
+    // B fragments; lanes of the zero-padded columns (> kfm) load nothing.
+    Chunk<KV> bw[MAXC][NT];
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const float* rec = a.prep + a.field_base + (int64_t)cj[j] * a.field_rec;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        if (nt * 16 + s <= a.kfm) bw[j][nt].load(rec + (int64_t)(nt * 64 + lane) * KV);
+        else bw[j][nt].zero();
+      }
+    }
+    RS_USE(xs[MAXC - 1].v[KV - 1]);
+    RS_USE(bw[MAXC - 1][0].v[KV - 1]);
+    RS_STAMP(2);
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
       const bool live = cg + j * NW + w < a.F;
@@ -246,7 +320,15 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
         const float xv = use ? xs[j].v[tp] : 0.f;
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(xv, bw[j][nt].v[tp], acc[nt]);
-        qn = fmaf(xv * xv, nw[j].v[tp], qn);
+        // |v_e|^2 for this lane's element e: the B lanes of DPP row kk hold
+        // v[e][0..15] — the same row as the A lane that holds x_e.
+        float sq = 0.f;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const float bv = nt * 16 + s < a.kfm ? bw[j][nt].v[tp] : 0.f;
+          sq = fmaf(bv, bv, sq);
+        }
+        qn = fmaf(xv * xv, row16_sum(sq), qn);
       }
       if (a.x_out && live && valid) {
         float* xo = a.x_out + b * d + a.nd + cj[j] * a.k + KV * kk;
@@ -277,9 +359,12 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
       if (a.x_out && valid && e < a.nd) a.x_out[b * d + e] = x;
     }
   }
+  RS_USE(acc[0][0]);
+  RS_STAMP(3);
   if (__any(bad && valid) && lane == 0) flag_error(a.err);
 
-  // ---- combine the NW partial tiles
+  // ---- combine the NW partial tiles: thread (sample, column) sums the waves'
+  // partials; the per-sample reductions over columns are DPP row sums.
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -288,29 +373,26 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
   qn += __shfl_xor(qn, 32);
   if (lane < 16) qs[w][lane] = qn;
   __syncthreads();
-  if (w == 0) {
-    const int smp = lane & 15, g = lane >> 4;
-    float ss = 0.f, lin = 0.f;
+  RS_STAMP(7);
+  constexpr int NC = NT * 16;  // columns per sample
+  if (threadIdx.x < 16 * NC) {
+    const int smp = threadIdx.x / NC, col = threadIdx.x % NC;
+    float v = 0.f;
 #pragma unroll
-    for (int cc = g; cc < NT * 16; cc += 4) {
-      float v = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < NW; ++ww) v += cs[ww][smp][cc];
-      if (cc < a.kfm) ss = fmaf(v, v, ss);
-      else if (cc == a.kfm) lin = v;
+    for (int ww = 0; ww < NW; ++ww) v += cs[ww][smp][col];
+    float t = col < a.kfm ? v * v : 0.f;       // s_f^2
+    if (col < NW) t -= qs[col][smp];           // - sum_i x_i^2 |v_i|^2 (wave partials)
+    float lin = col == a.kfm ? v : 0.f;        // x@w1
+    t = row16_sum(t);
+    lin = row16_sum(lin);
+    if constexpr (NT == 2) {
+      t += __shfl_xor(t, 16);
+      lin += __shfl_xor(lin, 16);
     }
-    ss += __shfl_xor(ss, 16);
-    ss += __shfl_xor(ss, 32);
-    lin += __shfl_xor(lin, 16);
-    lin += __shfl_xor(lin, 32);
-    if (g == 0) {
-      float q = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < NW; ++ww) q += qs[ww][smp];
-      const int64_t bb = (int64_t)blockIdx.x * 16 + smp;
-      if (bb < a.batch) a.logit[bb] = (lin + a.w0[0]) + 0.5f * (ss - q);
-    }
+    const int64_t bb = (int64_t)blockIdx.x * 16 + smp;
+    if (col == 0 && bb < a.batch) a.logit[bb] = (lin + a.w0[0]) + 0.5f * t;
   }
+  RS_STAMP(4);
 }
 
 // Generic fallback (any k / kfm): one 256-thread workgroup per sample.
@@ -492,11 +574,26 @@ static int grid_for(int64_t work, int block, int cap = 2048) {
   return (int)g;
 }
 
+// Waves per workgroup for the k=16 kernel: 16 by default; RS_FM_NW=4|8|16
+// overrides it (tuning experiments only).
+static int fm_nw16() {
+  static int nw = [] {
+    const char* e = getenv("RS_FM_NW");
+    const int v = e ? atoi(e) : 16;
+    return (v == 4 || v == 8) ? v : 16;
+  }();
+  return nw;
+}
+
 template <int KV, int NT, int KIND>
 static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st) {
-  constexpr int NW = 16;
   const int grid = (int)((a.batch + 15) / 16);
-  embed_fm_mfma<KV, NT, NW, KIND><<<grid, NW * 64, 0, st>>>(a);
+  if constexpr (KV == 4 && NT == 1) {
+    const int nw = fm_nw16();
+    if (nw == 4) { embed_fm_mfma<KV, NT, 4, KIND><<<grid, 4 * 64, 0, st>>>(a); return; }
+    if (nw == 8) { embed_fm_mfma<KV, NT, 8, KIND><<<grid, 8 * 64, 0, st>>>(a); return; }
+  }
+  embed_fm_mfma<KV, NT, 16, KIND><<<grid, 16 * 64, 0, st>>>(a);
 }
 
 template <int KIND>
@@ -608,6 +705,76 @@ extern "C" int rs_embed_fm_fwd(const void* ids, int id_kind, int64_t id_stride, 
   a.err = err_flag;
   return run_embed_fm(a, g, id_kind, as_stream(stream), "rs_embed_fm_fwd");
 }
+
+#ifdef RS_DIAG_STAMPS
+// Ceiling probe: sum 64-B rows at given row indices (4 lanes per row, one
+// float4 each) with different cache-policy bits on the row load.
+template <int MODE>
+__device__ __forceinline__ floatx4 probe_load(const float* p) {
+  if constexpr (MODE == 0) {
+    return *reinterpret_cast<const floatx4*>(p);
+  } else if constexpr (MODE == 1) {
+    return __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(p));
+  } else {
+    floatx4 v;
+    if constexpr (MODE == 2) asm volatile("global_load_dwordx4 %0, %1, off sc1\n s_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    else if constexpr (MODE == 3) asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1 nt\n s_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    else asm volatile("global_load_dwordx4 %0, %1, off sc0\n s_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    return v;
+  }
+}
+template <int MODE>
+__global__ __launch_bounds__(256) void diag_gather_sum(const float* __restrict__ table,
+                                                      const int64_t* __restrict__ rows, int64_t n, float* out) {
+  float acc = 0.f;
+  const int q = threadIdx.x & 3;
+  const int64_t quad = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  const int64_t nquads = ((int64_t)gridDim.x * blockDim.x) >> 2;
+  for (int64_t i = quad; i < n; i += nquads) {
+    const floatx4 v = probe_load<MODE>(table + rows[i] * 16 + 4 * q);
+    acc += v[0] + v[1] + v[2] + v[3];
+  }
+  if (acc == 12345.678f) out[blockIdx.x] = acc;  // keep the loads live, never true
+}
+extern "C" int rs_diag_gather_sum(const float* table, const int64_t* rows, int64_t n, int grid, float* out,
+                                  int mode, rs_stream_t stream) {
+  hipStream_t st = as_stream(stream);
+  switch (mode) {
+    case 0: diag_gather_sum<0><<<grid, 256, 0, st>>>(table, rows, n, out); break;
+    case 1: diag_gather_sum<1><<<grid, 256, 0, st>>>(table, rows, n, out); break;
+    case 2: diag_gather_sum<2><<<grid, 256, 0, st>>>(table, rows, n, out); break;
+    case 3: diag_gather_sum<3><<<grid, 256, 0, st>>>(table, rows, n, out); break;
+    default: diag_gather_sum<4><<<grid, 256, 0, st>>>(table, rows, n, out); break;
+  }
+  return launch_status("rs_diag_gather_sum");
+}
+
+extern "C" int rs_diag_embed_fm_fwd(const void* ids, int id_kind, int64_t id_stride, const float* dense,
+                                    int64_t dense_stride, int nd, const float* table, const int64_t* field_offsets,
+                                    const int64_t* field_vocab, int n_fields, int k, const float* prepared,
+                                    const float* w0, int kfm, float* logit, int64_t batch,
+                                    unsigned long long* dbg, rs_stream_t stream) {
+  const FmGeom g = fm_geom(nd, n_fields, k, kfm);
+  EmbedFmArgs a{};
+  a.ids = ids;
+  a.id_stride = id_stride;
+  a.dense = dense;
+  a.dense_stride = dense_stride;
+  a.nd = nd;
+  a.table = table;
+  a.offs = field_offsets;
+  a.vocab = field_vocab;
+  a.F = n_fields;
+  a.k = k;
+  a.prep = prepared;
+  a.w0 = w0;
+  a.kfm = kfm;
+  a.logit = logit;
+  a.batch = batch;
+  a.dbg = dbg;
+  return run_embed_fm(a, g, id_kind, as_stream(stream), "rs_diag_embed_fm_fwd");
+}
+#endif
 
 extern "C" int rs_rows_fm_fwd(const float* emb, const float* dense, int64_t dense_stride, int nd, int n_fields,
                               int k, const float* prepared, const float* w0, int kfm, float* logit, int64_t batch,

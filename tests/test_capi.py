@@ -59,3 +59,11 @@ def test_product_path_has_no_cpu_fallback():
     layer = FMLayer(4, device="cpu", input_dim=8)
     with pytest.raises(_lib.RSError, match="device"):
         layer(torch.zeros(2, 8))
+
+
+def test_signature_arity_matches_header():
+    txt = re.sub(r"/\*.*?\*/", "", open(HDR).read(), flags=re.S)
+    for m in re.finditer(r"\b(rs_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", txt):
+        name, params = m.group(1), m.group(2).strip()
+        n = 0 if params in ("", "void") else len(params.split(","))
+        assert len(_lib.SIGNATURES[name][1]) == n, f"{name}: header has {n} params"
