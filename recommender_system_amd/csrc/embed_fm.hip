@@ -149,6 +149,7 @@ struct EmbedFmArgs {
   int DB;
   int64_t dense_rec, field_rec, field_base;
   unsigned long long* dbg;  // diagnostic builds only (RS_DIAG_STAMPS): phase stamps
+  int ablate;               // diagnostic builds only: bit0 no MFMA, bit1 no B loads, bit2 no combine
 };
 
 // Phase stamps (s_memrealtime, 100 MHz) for the diagnostic library built by
@@ -303,6 +304,9 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
       const float* rec = a.prep + a.field_base + (int64_t)cj[j] * a.field_rec;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
+#ifdef RS_DIAG_STAMPS
+        if (a.ablate & 2) { bw[j][nt].zero(); bw[j][nt].v[0] = (float)cj[j]; continue; }
+#endif
         if (nt * 16 + s <= a.kfm) bw[j][nt].load(rec + (int64_t)(nt * 64 + lane) * KV);
         else bw[j][nt].zero();
       }
@@ -319,7 +323,12 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
       for (int tp = 0; tp < KV; ++tp) {
         const float xv = use ? xs[j].v[tp] : 0.f;
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(xv, bw[j][nt].v[tp], acc[nt]);
+        for (int nt = 0; nt < NT; ++nt) {
+#ifdef RS_DIAG_STAMPS
+          if (a.ablate & 1) { acc[nt][0] += xv * bw[j][nt].v[tp]; continue; }
+#endif
+          acc[nt] = mfma16x16x4(xv, bw[j][nt].v[tp], acc[nt]);
+        }
         // |v_e|^2 for this lane's element e: the B lanes of DPP row kk hold
         // v[e][0..15] — the same row as the A lane that holds x_e.
         float sq = 0.f;
@@ -363,6 +372,12 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
   RS_STAMP(3);
   if (__any(bad && valid) && lane == 0) flag_error(a.err);
 
+#ifdef RS_DIAG_STAMPS
+  if (a.ablate & 4) {
+    if (w == 0 && kk == 0 && b < a.batch) a.logit[b] = acc[0][0] + acc[0][1] + qn;
+    return;
+  }
+#endif
   // ---- combine the NW partial tiles: thread (sample, column) sums the waves'
   // partials; the per-sample reductions over columns are DPP row sums.
 #pragma unroll
@@ -772,6 +787,7 @@ extern "C" int rs_diag_embed_fm_fwd(const void* ids, int id_kind, int64_t id_str
   a.logit = logit;
   a.batch = batch;
   a.dbg = dbg;
+  a.ablate = getenv("RS_ABLATE") ? atoi(getenv("RS_ABLATE")) : 0;
   return run_embed_fm(a, g, id_kind, as_stream(stream), "rs_diag_embed_fm_fwd");
 }
 #endif

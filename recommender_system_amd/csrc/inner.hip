@@ -112,8 +112,155 @@ __global__ __launch_bounds__(256) void inner_kernel(InnerArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- fast path
+// k in {4,8,16,32,64}, F <= 64.  Up to 16 samples per 256-thread workgroup:
+//  1. the workgroup's S x F ids and the F (offset, vocab) pairs -> LDS
+//     (coalesced, once), barrier;
+//  2. every row chunk (float4) of the S x F x k tile is requested up front
+//     (8 in flight per thread, non-temporal), then stored to LDS, barrier;
+//  3. Gram rows: thread (s, g) owns rows g and F-2-g (balanced, ~F dot
+//     products) with e_i in registers, e_j as float4 LDS reads; results to an
+//     LDS output tile, barrier;
+//  4. the S output rows [flat | inner] (or [inner]) leave as one coalesced
+//     block of dword stores.
+constexpr int IP_SMAX = 16;
+constexpr int IP_FMAX = 64;
+
+template <int K, int KIND>
+__global__ __launch_bounds__(256) void inner_fast(InnerArgs a) {
+  constexpr int KQ = K / 4;
+  typedef Ids<KIND == 3 ? 0 : KIND> I;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ typename I::raw_t lid[IP_SMAX][IP_FMAX];
+  __shared__ int64_t lmeta[2][IP_FMAX];
+  const int F = a.F, P = F * (F - 1) / 2, S = a.S;
+  float* tile = smem;                          // [S][F][K]
+  float* gram = smem + S * F * K;              // [S][P]
+  const int tid = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * S;
+  const int nvalid = (int)(a.batch - b0 < S ? a.batch - b0 : S);
+
+  if constexpr (KIND != 3) {
+    for (int t = tid; t < S * F; t += 256) {
+      const int s = t / F, c = t - s * F;
+      const int64_t bb = b0 + (s < nvalid ? s : nvalid - 1);
+      lid[s][c] = I::load(a.ids, bb * a.id_stride + c);
+    }
+    for (int t = tid; t < 2 * F; t += 256) {
+      const int c = t < F ? t : t - F;
+      lmeta[t < F ? 0 : 1][c] = t < F ? a.offs[c] : a.vocab[c];
+    }
+    __syncthreads();
+  }
+
+  bool bad = false;
+  const float* src = KIND == 3 ? a.emb : a.table;  // embeddings given vs gathered
+  const int total = S * F * KQ;
+  for (int base = 0; base < total; base += 256 * 8) {
+    floatx4 v[8];
+    int dsti[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int idx = base + u * 256 + tid;
+      dsti[u] = -1;
+      v[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (idx < total) {
+        const int s = idx / (F * KQ), r = idx - s * (F * KQ);
+        const int c = r / KQ, q = r - c * KQ;
+        const int64_t bb = b0 + (s < nvalid ? s : nvalid - 1);
+        int64_t row;
+        bool ok = true;
+        if constexpr (KIND == 3) {
+          row = bb * F + c;
+        } else {
+          int64_t id;
+          ok = I::decode(lid[s][c], lmeta[1][c], id);
+          row = lmeta[0][c] + id;
+          bad |= !ok && s < nvalid;
+        }
+        const floatx4 t = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(src + row * K + 4 * q));
+        v[u] = ok ? t : floatx4{0.f, 0.f, 0.f, 0.f};
+        dsti[u] = (s * F + c) * K + 4 * q;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (dsti[u] >= 0) *reinterpret_cast<floatx4*>(tile + dsti[u]) = v[u];
+  }
+  if (bad) flag_error(a.err);
+  __syncthreads();
+
+  const int NG = F / 2 > 0 ? F / 2 : 1;  // balanced row pairs (g, F-2-g)
+  for (int t = tid; t < S * NG; t += 256) {
+    const int s = t / NG, g = t - s * NG;
+    const float* es = tile + s * F * K;
+    float* gs = gram + s * P;
+    for (int pass = 0; pass < 2; ++pass) {
+      const int i = pass == 0 ? g : F - 2 - g;
+      if (pass == 1 && i <= g) break;
+      if (i > F - 2) continue;
+      float ei[K];
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        const floatx4 x = *reinterpret_cast<const floatx4*>(es + i * K + 4 * q);
+        ei[4 * q] = x[0]; ei[4 * q + 1] = x[1]; ei[4 * q + 2] = x[2]; ei[4 * q + 3] = x[3];
+      }
+      const int p0 = i * (2 * F - i - 1) / 2 - i - 1;
+      for (int j = i + 1; j < F; ++j) {
+        float dot = 0.f;
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) {
+          const floatx4 y = *reinterpret_cast<const floatx4*>(es + j * K + 4 * q);
+          dot = fmaf(ei[4 * q], y[0], dot);
+          dot = fmaf(ei[4 * q + 1], y[1], dot);
+          dot = fmaf(ei[4 * q + 2], y[2], dot);
+          dot = fmaf(ei[4 * q + 3], y[3], dot);
+        }
+        gs[p0 + j] = dot;
+      }
+    }
+  }
+  __syncthreads();
+
+  const int FK = a.write_flat ? F * K : 0;
+  const int W = FK + P;
+  for (int e = tid; e < nvalid * W; e += 256) {
+    const int s = e / W, col = e - s * W;
+    const float val = col < FK ? tile[s * F * K + col] : gram[s * P + (col - FK)];
+    const int oc = col < FK ? col : a.inner_off + (col - FK);
+    a.out[(b0 + s) * a.out_stride + oc] = val;
+  }
+}
+
+template <int KIND>
+static void launch_inner_fast_k(const InnerArgs& a, size_t lds, unsigned grid, hipStream_t st) {
+  switch (a.k) {
+    case 4: inner_fast<4, KIND><<<grid, 256, lds, st>>>(a); break;
+    case 8: inner_fast<8, KIND><<<grid, 256, lds, st>>>(a); break;
+    case 16: inner_fast<16, KIND><<<grid, 256, lds, st>>>(a); break;
+    case 32: inner_fast<32, KIND><<<grid, 256, lds, st>>>(a); break;
+    default: inner_fast<64, KIND><<<grid, 256, lds, st>>>(a); break;
+  }
+}
+
 static int launch_inner(InnerArgs a, hipStream_t st, const char* what) {
   if (a.batch == 0) return RS_OK;
+  const bool fast_k = a.k == 4 || a.k == 8 || a.k == 16 || a.k == 32 || a.k == 64;
+  if (fast_k && a.F >= 2 && a.F <= IP_FMAX) {
+    const int P = a.F * (a.F - 1) / 2;
+    const int64_t per = ((int64_t)a.F * a.k + P) * sizeof(float);
+    int S = IP_SMAX;
+    while (S > 1 && S * per > 96 * 1024) --S;
+    a.S = S;
+    const size_t lds = (size_t)S * per;
+    const unsigned grid = (unsigned)((a.batch + S - 1) / S);
+    if (a.ids == nullptr) {
+      launch_inner_fast_k<3>(a, lds, grid, st);
+    } else {
+      with_id_kind(a.id_kind, [&](auto K) { launch_inner_fast_k<decltype(K)::value>(a, lds, grid, st); });
+    }
+    return launch_status(what);
+  }
   a.NG = a.F / 2 > 0 ? a.F / 2 : 1;
   int S = 256 / a.NG;
   const int64_t per = (int64_t)a.F * a.k * sizeof(float);
