@@ -178,6 +178,28 @@ int rs_dense_fwd(const float* x, int64_t x_stride, const float* W,
                  const float* bias, const float* alpha, int act, float* y,
                  int64_t y_stride, int64_t M, int K, int N, rs_stream_t stream);
 
+/* ------------------------------------------------ fused MLP tower (a7, §8f)
+ * The whole DNNLayer (layer/interaction.py:30-46: hidden Dense(h_i, act) then
+ * Dense(output_dim)) in one launch; activations stay in LDS.
+ * dims[0..n_layers]: input width then each layer's units (each <= 1024);
+ * W[l]: Keras kernel [dims[l], dims[l+1]]; bias[l], alpha[l] (PReLU) may be
+ * NULL.  in_rows (device int32 [roundup(dims[0],16)], may be NULL): LDS
+ * input column p reads Keras kernel row in_rows[p] (-1 = none), so a fused
+ * producer can keep its own column order.  rs_mlp_prepared_size returns
+ * floats (-1 on bad dims).                                                   */
+int64_t rs_mlp_prepared_size(int n_layers, const int* dims);
+int rs_mlp_prepare(int n_layers, const int* dims, const float* const* W,
+                   const float* const* bias, const float* const* alpha,
+                   const int32_t* in_rows, float* prepared, rs_stream_t stream);
+/* head 0: y[M, dims[n_layers]] = tower(x).  head 1 (dims[n_layers] == 1):
+ * y[m] = sigmoid(c0 * tower(x)[m] + c1 * extra[m]) — the DeepFM head
+ * model/deepFM.py:30 (extra = FM logit, c0 = c1 = 0.5); extra may be NULL.
+ * acts[l]: rs_act per layer (hidden: the DNNLayer activation; last: NONE).  */
+int rs_mlp_fwd(const float* x, int64_t x_stride, int n_layers, const int* dims,
+               const int* acts, const float* prepared, float* y,
+               int64_t y_stride, int head, const float* extra, float c0,
+               float c1, int64_t batch, rs_stream_t stream);
+
 /* Per-column affine + activation, in place allowed: y = act(x*scale + shift).
  * Used for BatchNormalization at inference (model/din.py:89).               */
 int rs_affine_act(const float* x, int64_t x_stride, const float* scale,

@@ -213,15 +213,18 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
   RS_USE(b);
   RS_STAMP(5);
   const bool dense_small = a.DB <= NW;
-  const bool has_dense = dense_small && w < a.DB;  // wave-uniform
+  // Dense k-steps go to the LAST waves: with F = 26 fields over 16 waves the
+  // first F - NW waves already carry two fields.
+  const int dw = NW - 1 - w;                        // dense k-step of this wave
+  const bool has_dense = dense_small && dw < a.DB;  // wave-uniform
   float dx = 0.f, dn = 0.f, drec[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) drec[nt] = 0.f;
   auto load_dense = [&]() {
     if (has_dense) {
-      const int e = 4 * w + kk;
+      const int e = 4 * dw + kk;
       dx = a.dense[b * a.dense_stride + (e < a.nd ? e : 0)];  // masked at use
-      const float* rec = a.prep + (int64_t)w * a.dense_rec;
+      const float* rec = a.prep + (int64_t)dw * a.dense_rec;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) drec[nt] = rec[nt * 64 + lane];
       dn = rec[NT * 64 + kk];
@@ -296,7 +299,12 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
     RS_USE(row[MAXC - 1]);
     RS_STAMP(1);
 #pragma unroll
-    for (int j = 0; j < MAXC; ++j) xs[j].load_nt(a.table + row[j] * a.k + KV * kk);
+    for (int j = 0; j < MAXC; ++j) {
+#ifdef RS_DIAG_STAMPS
+      if ((a.ablate & 8) && cg + j * NW + w >= a.F) { xs[j].zero(); continue; }
+#endif
+      xs[j].load_nt(a.table + row[j] * a.k + KV * kk);
+    }
     // B fragments; lanes of the zero-padded columns (> kfm) load nothing.
     Chunk<KV> bw[MAXC][NT];
 #pragma unroll
@@ -306,6 +314,7 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
       for (int nt = 0; nt < NT; ++nt) {
 #ifdef RS_DIAG_STAMPS
         if (a.ablate & 2) { bw[j][nt].zero(); bw[j][nt].v[0] = (float)cj[j]; continue; }
+        if ((a.ablate & 8) && cg + j * NW + w >= a.F) { bw[j][nt].zero(); continue; }
 #endif
         if (nt * 16 + s <= a.kfm) bw[j][nt].load(rec + (int64_t)(nt * 64 + lane) * KV);
         else bw[j][nt].zero();
@@ -349,7 +358,7 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
 
   // ---- dense MFMAs (their loads were issued in the prologue)
   if (has_dense) {
-    const int e = 4 * w + kk;
+    const int e = 4 * dw + kk;
     dx = e < a.nd ? dx : 0.f;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(dx, drec[nt], acc[nt]);
@@ -595,7 +604,7 @@ static int fm_nw16() {
   static int nw = [] {
     const char* e = getenv("RS_FM_NW");
     const int v = e ? atoi(e) : 16;
-    return (v == 4 || v == 8) ? v : 16;
+    return (v == 4 || v == 8 || v == 13) ? v : 16;
   }();
   return nw;
 }
@@ -607,6 +616,7 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st) {
     const int nw = fm_nw16();
     if (nw == 4) { embed_fm_mfma<KV, NT, 4, KIND><<<grid, 4 * 64, 0, st>>>(a); return; }
     if (nw == 8) { embed_fm_mfma<KV, NT, 8, KIND><<<grid, 8 * 64, 0, st>>>(a); return; }
+    if (nw == 13) { embed_fm_mfma<KV, NT, 13, KIND><<<grid, 13 * 64, 0, st>>>(a); return; }
   }
   embed_fm_mfma<KV, NT, 16, KIND><<<grid, 16 * 64, 0, st>>>(a);
 }

@@ -28,6 +28,7 @@ device sync; pass ``check_ids=False`` to skip the host-side raise).
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
 from typing import Sequence
 
@@ -341,6 +342,7 @@ class InnerProductLayer(KerasModule):
 
 
 # -------------------------------------------------------------- dense / MLP
+_MLP_MAXL, _MLP_MAXD = 8, 1024  # rs_mlp_fwd limits (mlp.hip)
 _ACTS = ("relu", "prelu", "sigmoid", "linear", None, "dice")
 
 
@@ -401,7 +403,64 @@ class Dense(KerasModule):
         return out
 
 
-class DNNLayer(KerasModule):
+class TowerMixin:
+    """A stack of Keras Dense layers run as ONE rs_mlp_fwd launch (mlp.hip):
+    activations stay in LDS, weights are packed once.  The host class
+    provides ``_layers()`` (the Dense layers in order) and ``_dev``."""
+
+    def tower_ok(self):
+        ls = self._layers()
+        if not (ls[0].kernel is not None and len(ls) <= _MLP_MAXL and all(l.activation != "dice" for l in ls)
+                and all(d <= _MLP_MAXD for d in self._dims())):
+            return False
+        dims = self._dims()
+        return _lib.lib().rs_mlp_prepared_size(len(ls), (C.c_int * len(dims))(*dims)) >= 0  # LDS budget
+
+    def _dims(self):
+        ls = self._layers()
+        return [ls[0].kernel.shape[0]] + [l.units for l in ls]
+
+    def prepared(self, in_rows=None):
+        """Weights packed in MFMA B-fragment order (rs_mlp_prepare), cached
+        until any weight changes (in-place updates bump tensor versions)."""
+        params = [p for l in self._layers() for p in (l.kernel, l.bias, l.alpha) if p is not None]
+        key = (tuple((p._version, p.data_ptr()) for p in params),
+               None if in_rows is None else in_rows._version)
+        cache = self.__dict__.setdefault("_tower_prep", {})
+        slot = None if in_rows is None else in_rows.data_ptr()
+        ent = cache.get(slot)
+        if ent is None or ent[0] != key:
+            ls = self._layers()
+            dims = self._dims()
+            n = len(ls)
+            ci = (C.c_int * (n + 1))(*dims)
+            pa = lambda ts: (C.c_void_p * n)(*[ptr(t) for t in ts])
+            size = _lib.lib().rs_mlp_prepared_size(n, ci)
+            if size < 0:
+                _lib.check(-1, "rs_mlp_prepared_size")
+            prep = torch.empty(size, dtype=torch.float32, device=self._dev)
+            call("rs_mlp_prepare", n, ci, pa([l.kernel for l in ls]), pa([l.bias for l in ls]),
+                 pa([l.alpha for l in ls]), ptr(in_rows), ptr(prep), _stream())
+            ent = cache[slot] = (key, prep, in_rows)  # in_rows kept alive with its packing
+        return ent[1]
+
+    def tower(self, x, extra=None, c0=1.0, c1=1.0, head=False, out=None):
+        """rs_mlp_fwd on x:[M, K] (device, row stride x.stride(0)).  head=True:
+        sigmoid(c0*dnn + c1*extra) (output_dim 1)."""
+        ls = self._layers()
+        n = len(ls)
+        dims = self._dims()
+        M = x.shape[0]
+        if out is None:
+            out = torch.empty(M, 1 if head else dims[-1], dtype=torch.float32, device=self._dev)
+        acts = [_lib.ACT[l.activation] for l in ls]
+        call("rs_mlp_fwd", ptr(x), x.stride(0), n, (C.c_int * (n + 1))(*dims), (C.c_int * n)(*acts),
+             ptr(self.prepared()), ptr(out), out.stride(0), 1 if head else 0, ptr(extra), float(c0), float(c1), M,
+             _stream())
+        return out
+
+
+class DNNLayer(TowerMixin, KerasModule):
     """DNNLayer(hidden_units, output_dim, activation='relu', dropout=0.2) —
     layer/interaction.py:30-46.  Dropout is inactive at inference."""
 
@@ -413,6 +472,9 @@ class DNNLayer(KerasModule):
              for u in hidden_units])
         self.output_layer = Dense(output_dim, activation=None, device=device,
                                   seed=int(torch.randint(0, 2 ** 31, (1,), generator=self._gen)))
+
+    def _layers(self):
+        return list(self.hidden_layer) + [self.output_layer]
 
     def keras_weights(self):
         out = {}
@@ -436,6 +498,9 @@ class DNNLayer(KerasModule):
 
     def forward(self, inputs):
         x = inputs
+        if torch.is_tensor(x) and x.is_cuda and x.dim() == 2 and x.stride(1) == 1 and self.output_layer.kernel is not None \
+                and self.tower_ok():
+            return self.tower(x)
         for layer in self.hidden_layer:
             x = layer(x)
         return self.output_layer(x)

@@ -35,7 +35,7 @@ import torch
 from . import _lib
 from ._lib import call, ptr
 from .layers import (Attention, BatchNormalization, CrossLayer, Dense, DNNLayer, EmbedLayer, FMLayer,
-                     KerasModule, sigmoid_combine, _ids_tensor, _to_device_f32, _ErrFlag)
+                     KerasModule, TowerMixin, sigmoid_combine, _ids_tensor, _to_device_f32, _ErrFlag)
 
 
 def _split_criteo(inputs, nd, device):
@@ -126,6 +126,9 @@ class DeepFM(KerasModule):
         x = torch.empty(B, self.nd + self.embed_layer.n_fields * self.embed_layer.k, dtype=torch.float32,
                         device=self._dev)
         fm = self.fm_logit((dense, ids), x_out=x, check_ids=check_ids)
+        if self.dnn.output_layer.units == 1 and self.dnn.tower_ok():
+            # DNN tower + sigmoid(0.5*fm + 0.5*dnn) head in one launch
+            return self.dnn.tower(x, extra=fm, c0=0.5, c1=0.5, head=True)
         dnn = self.dnn(x)
         return sigmoid_combine(fm, dnn, 0.5, 0.5)
 
@@ -154,10 +157,13 @@ class DCN(KerasModule):
         B = x.shape[0]
         z = torch.empty(B, self.d + self.dense_layer.output_layer.units, dtype=torch.float32, device=self._dev)
         self.cross_layer(x, out=z[:, :self.d])
-        h = x
-        for layer in self.dense_layer.hidden_layer:
-            h = layer(h)
-        self.dense_layer.output_layer(h, out=z[:, self.d:])
+        if self.dense_layer.tower_ok():
+            self.dense_layer.tower(x, out=z[:, self.d:])
+        else:
+            h = x
+            for layer in self.dense_layer.hidden_layer:
+                h = layer(h)
+            self.dense_layer.output_layer(h, out=z[:, self.d:])
         return self.output_layer(z)
 
 
@@ -201,7 +207,7 @@ class PNN(KerasModule):
         return self.dnn_layer(self.product_inputs(inputs, check_ids))
 
 
-class DIN(KerasModule):
+class DIN(TowerMixin, KerasModule):
     """DIN — model/din.py:15-95.  ``forward(inputs)`` takes the reference's
     dict: each dense / non-behaviour sparse feature [B,1] (or [B]), each
     behaviour feature [B,T] (0 = padding), and the candidate under the
@@ -259,6 +265,11 @@ class DIN(KerasModule):
             emb[:, col:col + 1] = _to_device_f32(inputs[f["feat"]], dev).reshape(B, 1)
             col += 1
         x = self.bn_layer(emb)
+        if self.out_layer.kernel is not None and self.tower_ok():
+            return self.tower(x)  # PReLU MLP + Dense(1, sigmoid) in one launch
         for layer in self.dense_layer:
             x = layer(x)
         return self.out_layer(x)
+
+    def _layers(self):
+        return list(self.dense_layer) + [self.out_layer]

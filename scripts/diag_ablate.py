@@ -77,8 +77,12 @@ if __name__ == "__main__":
     if len(sys.argv) > 1:
         run_one(int(sys.argv[1]))
     else:
-        for ab in (0, 1, 2, 4, 3, 7):
+        runs = [(a, None) for a in (0, 8)] + [(0, "13"), (8, "13"), (0, "8")]
+        for ab, nw in runs:
             env = dict(os.environ, RS_ABLATE=str(ab))
+            if nw:
+                env["RS_FM_NW"] = nw
+            print("RS_FM_NW", nw or 16, end=" ")
             r = subprocess.run([sys.executable, __file__, str(ab)], env=env, capture_output=True, text=True, timeout=120)
             print(r.stdout.strip() or r.stderr[-500:], flush=True)
             if r.returncode != 0:

@@ -12,7 +12,7 @@ for cfg in ${CONFIGS:-hotpath}; do
 import json,sys
 d=json.load(open('gpurun_out/q_$cfg.json'))
 r=d['roofline']
-print('$cfg', 'value=%.4g'%d['value'], 'ms=%.4f'%d['ms_per_step'], 'roof=%.3f'%r['frac'], 'kern_ms=%.4f'%r.get('kernel_ms',0), {k:v for k,v in d.items() if k in ('concurrent_batches',)})
+print('$cfg', 'value=%.4g'%d['value'], 'ms=%.4f'%d['ms_per_step'], 'roof=%.3f'%r['frac'], 'kern_ms=%.4f'%r.get('kernel_ms',0), {k:v for k,v in d.items() if k in ('concurrent_batches','deepfm_forward')})
 "
 done
 echo DONE

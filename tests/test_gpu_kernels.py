@@ -308,3 +308,75 @@ def test_dice_2d_and_bn(gpu):
     assert_scaled_close(yd, O.dice(x, c(dice.alphas), c(dice.moving_mean), c(dice.moving_variance), 1e-9), what="Dice")
     assert_scaled_close(yb, O.batchnorm_inference(x, c(bn.moving_mean), c(bn.moving_variance), c(bn.gamma),
                                                   c(bn.beta), 1e-3), what="BN")
+
+
+# ------------------------------------------------------- fused MLP tower (mlp.hip)
+def _tower_ref(x, layers):
+    for l in layers:
+        x = O.dense(x, l.kernel.cpu().numpy(), l.bias.cpu().numpy(), l.activation,
+                    None if l.alpha is None else l.alpha.cpu().numpy())
+    return x
+
+
+@pytest.mark.parametrize("M,K,hidden,out,act", [(4096, 429, [256, 128, 64], 1, "relu"),
+                                                (1000, 741, [256, 128, 64], 1, "relu"),
+                                                (37, 37, [50, 3], 7, "prelu"),
+                                                (1, 1024, [1024], 16, "relu"),
+                                                (130, 20, [16, 16, 16, 16, 16, 16, 16], 2, "sigmoid")])
+def test_dnn_tower(gpu, M, K, hidden, out, act):
+    from recommender_system_amd import DNNLayer
+    rng = np.random.default_rng(M + K)
+    x = torch.tensor(rng.standard_normal((M, K)).astype(np.float32), device="cuda")
+    dnn = DNNLayer(hidden, out, act, seed=5)
+    dnn.build(K)
+    with torch.no_grad():
+        for l in dnn._layers():
+            l.bias.uniform_(-0.1, 0.1)
+            if l.alpha is not None:
+                l.alpha.uniform_(-0.5, 0.5)
+    assert dnn.tower_ok()
+    y = dnn(x)
+    torch.cuda.synchronize()
+    assert_scaled_close(y, _tower_ref(x.cpu().numpy(), dnn._layers()), what=f"DNN tower {hidden}")
+    # the per-layer Dense path agrees with the fused tower
+    h = x
+    for l in dnn._layers():
+        h = l(h)
+    assert_scaled_close(y, h, what="tower vs per-layer")
+
+
+def test_dnn_tower_head_strided_and_permuted(gpu):
+    """head=1 (DeepFM sigmoid(0.5 fm + 0.5 dnn)), a strided input/output view
+    and an LDS column permutation (in_rows) give the same numbers."""
+    from recommender_system_amd import DNNLayer
+    rng = np.random.default_rng(3)
+    M, K = 300, 45
+    big = torch.tensor(rng.standard_normal((M, K + 7)).astype(np.float32), device="cuda")
+    x = big[:, 3:3 + K]
+    dnn = DNNLayer([64, 32], 1, "relu", seed=9)
+    dnn.build(K)
+    fm = torch.tensor(rng.standard_normal((M, 1)).astype(np.float32), device="cuda")
+    y = dnn.tower(x, extra=fm, c0=0.5, c1=0.5, head=True)
+    z = _tower_ref(x.cpu().numpy(), dnn._layers())
+    ref = 1.0 / (1.0 + np.exp(-(0.5 * z + 0.5 * fm.cpu().numpy().astype(np.float64))))
+    assert_rel_close(y, ref, what="tower head")
+    out = torch.zeros(M, 5, device="cuda")
+    dnn.tower(x, out=out[:, 2:3])
+    assert_scaled_close(out[:, 2:3], z, what="tower strided out")
+    assert float(out[:, :2].abs().sum() + out[:, 3:].abs().sum()) == 0.0
+    # permuted LDS columns: column p of the staged tile holds Keras row perm[p]
+    perm = rng.permutation(K)
+    Kp = (K + 15) // 16 * 16
+    in_rows = torch.full((Kp,), -1, dtype=torch.int32, device="cuda")
+    in_rows[:K] = torch.tensor(perm, dtype=torch.int32)
+    prep = dnn.prepared(in_rows)
+    from recommender_system_amd import _lib
+    import ctypes as C
+    dims = dnn._dims()
+    n = len(dims) - 1
+    xp = x[:, torch.tensor(perm, device="cuda")].contiguous()
+    y2 = torch.empty(M, 1, device="cuda")
+    _lib.call("rs_mlp_fwd", xp.data_ptr(), xp.stride(0), n, (C.c_int * (n + 1))(*dims),
+              (C.c_int * n)(*[_lib.ACT[l.activation] for l in dnn._layers()]), prep.data_ptr(), y2.data_ptr(), 1,
+              0, None, 1.0, 1.0, M, _lib.stream())
+    assert_scaled_close(y2, z, what="tower permuted input")
