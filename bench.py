@@ -19,8 +19,8 @@ Also measured (nested in the JSON line, not `value`):
     average launch duration from HIP events recorded around every timed launch
     on the launch stream; peak 8.0 TB/s.  `traffic` = PMC HBM bytes per launch
     from profiles/  or null.
-  * `deepfm_forward`: the full DeepFM forward (fused kernel emitting x, DNN
-    429-256-128-64-1 on fp32 MFMA, sigmoid head) samples/s.
+  * `deepfm_forward`: the full DeepFM forward as ONE kernel (gather + FM +
+    DNN 429-256-128-64-1 on fp32 MFMA + sigmoid head) samples/s.
   * `cpu_baseline`: the oracle's numpy fp32 restatement of the reference
     forward (TF unavailable) on the same table and batches, bounded sample.
 
@@ -291,22 +291,29 @@ def bench_hotpath(args, world, rank):
             t = _timed_graph_streams(step_s, n, ns, world)
             conc[f"{ns}_streams"] = {"samples_per_s": n * B / t, "us_per_batch": t / n * 1e6}
         result["concurrent_batches"] = conc
-        # full DeepFM forward (secondary)
+        # full DeepFM forward (secondary): one fused launch (gather + FM + DNN
+        # tower + head), and the two-launch path (gather+FM emitting x, tower)
         xbuf = torch.empty(B, nd + F * k, device=dev)
 
         def full(i):
             j = i % ids_pool.shape[0]
-            ids, dense = ids_pool[j], dense_pool[j]
-            fm = model.fm_logit((dense, ids), x_out=xbuf, check_ids=False)
-            dnn = model.dnn(xbuf)
-            rs.sigmoid_combine(fm, dnn, 0.5, 0.5)
+            model.forward_fused((dense_pool[j], ids_pool[j]), check_ids=False)
+
+        def two_launch(i):
+            j = i % ids_pool.shape[0]
+            fm = model.fm_logit((dense_pool[j], ids_pool[j]), x_out=xbuf, check_ids=False)
+            model.dnn.tower(xbuf, extra=fm, c0=0.5, c1=0.5, head=True)
 
         n2 = max(10, args.steps // 5)
         dt2, _ = _timed_graph(full, n2, args.warmup, world, chunk=16)
+        dt3, _ = _timed_graph(two_launch, n2, args.warmup, world, chunk=16)
         flops = B * 2 * (429 * 256 + 256 * 128 + 128 * 64 + 64)
-        result["deepfm_forward"] = {"samples_per_s": n2 * B / dt2, "ms_per_step": dt2 / n2 * 1e3,
-                                    "dnn_flop_per_step": flops, "note": "fused gather+FM (x emitted) + DNN "
-                                    "429-256-128-64-1 fp32 MFMA + sigmoid head"}
+        result["deepfm_forward"] = {
+            "samples_per_s": n2 * B / dt2, "ms_per_step": dt2 / n2 * 1e3, "dnn_flop_per_step": flops,
+            "dnn_tflops_incl_gather": flops / (dt2 / n2) / 1e12,
+            "two_launch_samples_per_s": n2 * B / dt3,
+            "note": "rs_deepfm_fwd: gather + FM + DNN 429-256-128-64-1 (fp32 MFMA, LDS-resident activations) + "
+                    "sigmoid head in one launch; two_launch = rs_embed_fm_fwd emitting x + rs_mlp_fwd"}
         if args.cpu_baseline and rank == 0:
             cb, chk = cpu_baseline_hotpath(model, ids_pool, dense_pool, args.cpu_budget)
             j = chk[0]

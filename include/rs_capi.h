@@ -200,6 +200,27 @@ int rs_mlp_fwd(const float* x, int64_t x_stride, int n_layers, const int* dims,
                int64_t y_stride, int head, const float* extra, float c0,
                float c1, int64_t batch, rs_stream_t stream);
 
+/* --------------------------------------------- fused DeepFM forward (a8)
+ * DeepFM.call (model/deepFM.py:23-31) in ONE launch: ids -> rows -> x (kept
+ * in LDS) -> FM logit and the DNN tower -> out[b] = sigmoid(c0*dnn + c1*fm)
+ * (reference: c0 = c1 = 0.5).  Arguments as rs_embed_fm_fwd plus the tower
+ * (rs_mlp_*).  mlp_prepared must be packed with in_rows mapping the LDS
+ * column order [emb F*k | dense nd] to Keras rows: p < F*k -> nd + p,
+ * F*k <= p < F*k+nd -> p - F*k, else -1.  fm_logit (optional) receives the
+ * FM logit.  rs_deepfm_fused_ok: 1 when the shape is supported (k 8 or 16,
+ * kfm <= 15, 1..128 fields, tower output 1, dims[0] = nd + F*k).            */
+int rs_deepfm_fused_ok(int nd, int n_fields, int k, int kfm, int n_layers,
+                       const int* dims);
+int rs_deepfm_fwd(const void* ids, int id_kind, int64_t id_stride,
+                  const float* dense, int64_t dense_stride, int nd,
+                  const float* table, const int64_t* field_offsets,
+                  const int64_t* field_vocab, int n_fields, int k,
+                  const float* fm_prepared, const float* w0, int kfm,
+                  int n_layers, const int* dims, const int* acts,
+                  const float* mlp_prepared, float c0, float c1, float* out,
+                  float* fm_logit, int64_t batch, int* err_flag,
+                  rs_stream_t stream);
+
 /* Per-column affine + activation, in place allowed: y = act(x*scale + shift).
  * Used for BatchNormalization at inference (model/din.py:89).               */
 int rs_affine_act(const float* x, int64_t x_stride, const float* scale,

@@ -23,6 +23,7 @@
 //     logit = (x@w1 + w0) + 0.5*(sum_f s_f^2 - sum_i x_i^2 |v_i|^2).
 #include <stdlib.h>
 
+#include "mlp_tower.hpp"
 #include "rs_common.hpp"
 
 namespace rs {
@@ -173,8 +174,11 @@ struct EmbedFmArgs {
 #endif
 
 // KIND: 0 i32, 1 i64, 2 f32 ids; 3 = rows already gathered (row(b,c) = b*F+c).
-template <int KV, int NT, int NW, int KIND>
-__global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
+// TW: fused DeepFM — x goes to an LDS tile ([emb F*k | dense nd | 0-pad],
+// row stride tw->rs) instead of x_out, and the DNN tower of mlp_tower.hpp runs
+// on it, closed by sigmoid(c0*dnn + c1*fm) (model/deepFM.py:24-30).
+template <int KV, int NT, int NW, int KIND, bool TW>
+__device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArgs* tw) {
   constexpr int MAXC0 = 128 / (NW * KV);
   constexpr int MAXC = MAXC0 < 1 ? 1 : (MAXC0 > 8 ? 8 : MAXC0);
   typedef Ids<KIND == 3 ? 0 : KIND> I;
@@ -212,6 +216,22 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
   RS_STAMP(0);
   RS_USE(b);
   RS_STAMP(5);
+  // fused tower: its layer-0 weights, the bias/alpha block and the x tile's
+  // zero padding do not depend on the ids; issue them first
+  extern __shared__ float tsm[];
+  __shared__ float fmlog[TW ? 16 : 1];
+  floatx4 ring[TW ? 4 : 1];
+  const int xrs = TW ? tw->rs : 0;
+  if constexpr (TW) {
+    mlp_first_fill<NW>(*tw, ring);
+    float* par = tsm + 32 * tw->rs + NW * 256;
+    for (int i = threadIdx.x; i < tw->ptot; i += NW * 64) par[i] = tw->prep[tw->wtot + i];
+    const int d0 = a.F * a.k + a.nd, padw = tw->Kp[0] - d0;
+    for (int i = threadIdx.x; i < 16 * padw; i += NW * 64) {
+      const int r = i / padw;
+      tsm[r * xrs + d0 + (i - r * padw)] = 0.f;
+    }
+  }
   const bool dense_small = a.DB <= NW;
   // Dense k-steps go to the LAST waves: with F = 26 fields over 16 waves the
   // first F - NW waves already carry two fields.
@@ -348,7 +368,13 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
         }
         qn = fmaf(xv * xv, row16_sum(sq), qn);
       }
-      if (a.x_out && live && valid) {
+      if constexpr (TW) {
+        if (live) {
+          float* xo = tsm + s * xrs + cj[j] * a.k + KV * kk;
+#pragma unroll
+          for (int tp = 0; tp < KV; ++tp) xo[tp] = ok[j] ? xs[j].v[tp] : 0.f;
+        }
+      } else if (a.x_out && live && valid) {
         float* xo = a.x_out + b * d + a.nd + cj[j] * a.k + KV * kk;
 #pragma unroll
         for (int tp = 0; tp < KV; ++tp) xo[tp] = ok[j] ? xs[j].v[tp] : 0.f;
@@ -363,7 +389,11 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(dx, drec[nt], acc[nt]);
     qn = fmaf(dx * dx, dn, qn);
-    if (a.x_out && valid && e < a.nd) a.x_out[b * d + e] = dx;
+    if constexpr (TW) {
+      if (e < a.nd) tsm[s * xrs + a.F * a.k + e] = dx;
+    } else if (a.x_out && valid && e < a.nd) {
+      a.x_out[b * d + e] = dx;
+    }
   }
   if (!dense_small) {
     for (int t = w; t < a.DB; t += NW) {
@@ -374,7 +404,11 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(x, rec[nt * 64 + lane], acc[nt]);
       qn = fmaf(x * x, rec[NT * 64 + kk], qn);
-      if (a.x_out && valid && e < a.nd) a.x_out[b * d + e] = x;
+      if constexpr (TW) {
+        if (e < a.nd) tsm[s * xrs + a.F * a.k + e] = x;
+      } else if (a.x_out && valid && e < a.nd) {
+        a.x_out[b * d + e] = x;
+      }
     }
   }
   RS_USE(acc[0][0]);
@@ -414,9 +448,25 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
       lin += __shfl_xor(lin, 16);
     }
     const int64_t bb = (int64_t)blockIdx.x * 16 + smp;
-    if (col == 0 && bb < a.batch) a.logit[bb] = (lin + a.w0[0]) + 0.5f * t;
+    const float fm = (lin + a.w0[0]) + 0.5f * t;
+    if (col == 0 && bb < a.batch && a.logit) a.logit[bb] = fm;
+    if constexpr (TW) {
+      if (col == 0) fmlog[smp] = fm;
+    }
   }
   RS_STAMP(4);
+  if constexpr (TW) mlp_tower_tile<NW>(*tw, tsm, (int64_t)blockIdx.x * 16, ring, fmlog);
+}
+
+template <int KV, int NT, int NW, int KIND>
+__global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
+  embed_fm_body<KV, NT, NW, KIND, false>(a, nullptr);
+}
+
+// Fused DeepFM forward: gather + FM + DNN tower + head, one launch.
+template <int KV, int KIND>
+__global__ __launch_bounds__(16 * 64) void deepfm_fused(EmbedFmArgs a, MlpArgs t) {
+  embed_fm_body<KV, 1, 16, KIND, true>(a, &t);
 }
 
 // Generic fallback (any k / kfm): one 256-thread workgroup per sample.
@@ -910,4 +960,89 @@ extern "C" int rs_fm_onehot_fwd(const void* ids, int id_kind, int64_t id_stride,
     }
   });
   return launch_status("rs_fm_onehot_fwd");
+}
+
+// ------------------------------------------------------- fused DeepFM forward
+namespace rs {
+static bool deepfm_geom(int nd, int n_fields, int k, int kfm, int n_layers, const int* dims, FmGeom& fg,
+                        MlpGeom& mg) {
+  if (nd < 0 || n_fields < 1 || n_fields > 128 || kfm < 1 || (k != 8 && k != 16)) return false;
+  fg = fm_geom(nd, n_fields, k, kfm);
+  if (!fg.mfma || fg.NT != 1) return false;
+  if (!mlp_geom(n_layers, dims, mg)) return false;
+  // static LDS of the embed part (<= 37 KB) + the tower's dynamic LDS
+  return dims[0] == nd + n_fields * k && dims[n_layers] == 1 && mg.lds <= 120 * 1024;
+}
+
+template <int KV, int KIND>
+static void launch_deepfm(const EmbedFmArgs& a, const MlpArgs& t, size_t lds, hipStream_t st) {
+  static size_t lds_set = 64 * 1024;  // opt in to exactly what is needed beyond the default
+  if (lds > lds_set) {
+    (void)hipFuncSetAttribute((const void*)deepfm_fused<KV, KIND>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    lds_set = lds;
+  }
+  deepfm_fused<KV, KIND><<<(unsigned)((a.batch + 15) / 16), 16 * 64, lds, st>>>(a, t);
+}
+}  // namespace rs
+
+extern "C" int rs_deepfm_fused_ok(int nd, int n_fields, int k, int kfm, int n_layers, const int* dims) {
+  FmGeom fg;
+  MlpGeom mg;
+  return dims && deepfm_geom(nd, n_fields, k, kfm, n_layers, dims, fg, mg) ? 1 : 0;
+}
+
+extern "C" int rs_deepfm_fwd(const void* ids, int id_kind, int64_t id_stride, const float* dense,
+                             int64_t dense_stride, int nd, const float* table, const int64_t* field_offsets,
+                             const int64_t* field_vocab, int n_fields, int k, const float* fm_prepared,
+                             const float* w0, int kfm, int n_layers, const int* dims, const int* acts,
+                             const float* mlp_prepared, float c0, float c1, float* out, float* fm_logit,
+                             int64_t batch, int* err_flag, rs_stream_t stream) {
+  FmGeom fg;
+  MlpGeom mg;
+  RS_REQUIRE(dims && acts, "rs_deepfm_fwd: null dims/acts");
+  RS_REQUIRE(deepfm_geom(nd, n_fields, k, kfm, n_layers, dims, fg, mg),
+             "rs_deepfm_fwd: unsupported shape (see rs_deepfm_fused_ok)");
+  RS_REQUIRE(batch >= 0 && ids && table && field_offsets && field_vocab && fm_prepared && w0 && mlp_prepared && out,
+             "rs_deepfm_fwd: null pointer");
+  RS_REQUIRE(nd == 0 || dense, "rs_deepfm_fwd: dense is null");
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_deepfm_fwd: bad id_kind");
+  RS_REQUIRE((uintptr_t)table % 16 == 0, "rs_deepfm_fwd: table must be 16-B aligned");
+  MlpArgs t{};
+  RS_REQUIRE(mlp_fill_args(mg, acts, mlp_prepared, t), "rs_deepfm_fwd: bad activation");
+  if (batch == 0) return RS_OK;
+  t.y = out;
+  t.ys = 1;
+  t.head = 1;
+  t.c0 = c0;
+  t.c1 = c1;
+  t.M = batch;
+  EmbedFmArgs a{};
+  a.ids = ids;
+  a.id_stride = id_stride;
+  a.dense = dense;
+  a.dense_stride = dense_stride;
+  a.nd = nd;
+  a.table = table;
+  a.offs = field_offsets;
+  a.vocab = field_vocab;
+  a.F = n_fields;
+  a.k = k;
+  a.prep = fm_prepared;
+  a.w0 = w0;
+  a.kfm = kfm;
+  a.logit = fm_logit;
+  a.batch = batch;
+  a.err = err_flag;
+  a.DB = fg.DB;
+  a.dense_rec = fg.dense_rec;
+  a.field_rec = fg.field_rec;
+  a.field_base = fg.field_base;
+  hipStream_t st = as_stream(stream);
+  with_id_kind(id_kind, [&](auto K) {
+    constexpr int KIND = decltype(K)::value;
+    if (fg.KV == 2) launch_deepfm<2, KIND>(a, t, mg.lds, st);
+    else launch_deepfm<4, KIND>(a, t, mg.lds, st);
+  });
+  return launch_status("rs_deepfm_fwd");
 }

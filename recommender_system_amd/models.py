@@ -30,6 +30,8 @@ NotImplementedError; an unknown mode raises the reference's ValueError.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import torch
 
 from . import _lib
@@ -120,7 +122,53 @@ class DeepFM(KerasModule):
             self._err.check("DeepFM")
         return logit
 
+    def _fused_rows(self):
+        """Tower input permutation for the fused kernel: its LDS tile holds
+        [emb F*k | dense nd]; Keras rows are [dense nd | emb F*k]."""
+        e = self.embed_layer
+        fk = e.n_fields * e.k
+        kp = (fk + self.nd + 15) // 16 * 16
+        if getattr(self, "_in_rows", None) is None:
+            rows = torch.full((kp,), -1, dtype=torch.int32)
+            rows[:fk] = torch.arange(fk, dtype=torch.int32) + self.nd
+            rows[fk:fk + self.nd] = torch.arange(self.nd, dtype=torch.int32)
+            self._in_rows = rows.to(self._dev)
+        return self._in_rows
+
+    def fused_ok(self):
+        e = self.embed_layer
+        if not self.dnn.tower_ok():
+            return False
+        dims = self.dnn._dims()
+        return bool(_lib.lib().rs_deepfm_fused_ok(self.nd, e.n_fields, e.k, self.fm.k, len(dims) - 1,
+                                                   (C.c_int * len(dims))(*dims)))
+
+    def forward_fused(self, inputs, check_ids=True, fm_logit=None):
+        """DeepFM.call as ONE kernel (rs_deepfm_fwd)."""
+        dense, ids = _split_criteo(inputs, self.nd, self._dev)
+        B = ids.shape[0]
+        e = self.embed_layer
+        prep = self.fm.prepared(self.nd, e.n_fields, e.k)
+        mlp = self.dnn.prepared(self._fused_rows())
+        dims = self.dnn._dims()
+        n = len(dims) - 1
+        acts = [_lib.ACT[l.activation] for l in self.dnn._layers()]
+        out = torch.empty(B, 1, dtype=torch.float32, device=self._dev)
+        call("rs_deepfm_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), self.nd,
+             ptr(e.table), ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, e.k, ptr(prep), ptr(self.fm.w0),
+             self.fm.k, n, (C.c_int * (n + 1))(*dims), (C.c_int * n)(*acts), ptr(mlp), 0.5, 0.5, ptr(out),
+             ptr(fm_logit), B, ptr(self._err.t), _lib.stream())
+        if check_ids:
+            self._err.check("DeepFM")
+        return out
+
     def forward(self, inputs, check_ids=True):
+        if self.fused_ok():
+            return self.forward_fused(inputs, check_ids)
+        return self.forward_unfused(inputs, check_ids)
+
+    def forward_unfused(self, inputs, check_ids=True):
+        """Fused gather+FM kernel emitting x, then the tower kernel."""
         dense, ids = _split_criteo(inputs, self.nd, self._dev)
         B = ids.shape[0]
         x = torch.empty(B, self.nd + self.embed_layer.n_fields * self.embed_layer.k, dtype=torch.float32,
