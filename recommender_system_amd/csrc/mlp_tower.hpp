@@ -87,8 +87,12 @@ __device__ __forceinline__ float mlp_act(float v, int act, float alpha) {
 struct MlpItem {
   int t, g0, g1;
 };
+// k-slices per output tile: layers with >= 4 tiles keep whole columns per
+// wave (no partial-sum exchange: measured faster than filling all 16 waves);
+// narrow layers (the 64->1 head) split K over the idle waves.
 __device__ __forceinline__ int mlp_slices(int T, int G, int NW) {
-  int S = NW / T;
+  if (T >= 4) return 1;
+  const int S = NW / T;
   return S < 1 ? 1 : (S > G ? G : S);
 }
 __device__ __forceinline__ MlpItem mlp_item(int item, int T, int G, int S) {
@@ -110,10 +114,15 @@ __device__ __forceinline__ void mlp_ring_fill(floatx4 (&ring)[4], const floatx4*
 template <int D>
 __device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[4], const float* __restrict__ ap,
                                           const floatx4* __restrict__ bp, int g0, int g1, floatx4& acc) {
+  // A fragments are read one group ahead so the LDS latency hides behind
+  // the previous group's MFMAs
+  floatx4 an = *reinterpret_cast<const floatx4*>(ap + 16 * g0);
   for (int g = g0; g < g1; g += D) {
 #pragma unroll
     for (int u = 0; u < D; ++u) {
-      const floatx4 av = *reinterpret_cast<const floatx4*>(ap + 16 * (g + u));
+      const floatx4 av = an;
+      an = *reinterpret_cast<const floatx4*>(ap + 16 * min(g + u + 1, g1 - 1));
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc = mfma16x16x4(av[j], ring[u][j], acc);
       // refill the slot in place right after its MFMAs and pin it there: left
