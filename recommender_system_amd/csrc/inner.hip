@@ -24,9 +24,16 @@ struct InnerArgs {
   int64_t out_stride;
   int inner_off;   // column of the first pair in out
   int write_flat;  // also write the flattened embeddings to out[:, 0:F*k]
+  int contig;      // fast path: out rows are [flat | inner] back to back, 16-B aligned blocks
   int64_t batch;
   int* err;
+  unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_inner_set_dbg)
 };
+#define IP_STAMP(i)                                                                                   \
+  do {                                                                                                \
+    if (a.dbg && (threadIdx.x & 63) == 0)                                                             \
+      a.dbg[((int64_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 
 __device__ __forceinline__ bool inner_decode(const void* ids, int kind, int64_t off, int64_t vocab, int64_t& id) {
   if (kind == RS_ID_F32) {
@@ -113,7 +120,7 @@ __global__ __launch_bounds__(256) void inner_kernel(InnerArgs a) {
 }
 
 // ---------------------------------------------------------------- fast path
-// k in {4,8,16,32,64}, F <= 64.  Up to 16 samples per 256-thread workgroup:
+// k in {4,8,16,32,64}, F <= 64.  Up to 16 samples per 1024-thread workgroup:
 //  1. the workgroup's S x F ids and the F (offset, vocab) pairs -> LDS
 //     (coalesced, once), barrier;
 //  2. every row chunk (float4) of the S x F x k tile is requested up front
@@ -124,29 +131,32 @@ __global__ __launch_bounds__(256) void inner_kernel(InnerArgs a) {
 //  4. the S output rows [flat | inner] (or [inner]) leave as one coalesced
 //     block of dword stores.
 constexpr int IP_SMAX = 16;
+constexpr int IP_NW = 16, IP_NT = IP_NW * 64;  // 16 waves: one sample per wave in the Gram phase
 constexpr int IP_FMAX = 64;
 
 template <int K, int KIND>
-__global__ __launch_bounds__(256) void inner_fast(InnerArgs a) {
+__global__ __launch_bounds__(IP_NT) void inner_fast(InnerArgs a) {
   constexpr int KQ = K / 4;
   typedef Ids<KIND == 3 ? 0 : KIND> I;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ typename I::raw_t lid[IP_SMAX][IP_FMAX];
   __shared__ int64_t lmeta[2][IP_FMAX];
   const int F = a.F, P = F * (F - 1) / 2, S = a.S;
-  float* tile = smem;                          // [S][F][K]
-  float* gram = smem + S * F * K;              // [S][P]
+  const int SS = F * K + 4;                    // sample stride: +4 dwords spreads the Gram reads over banks
+  float* tile = smem;                          // [S][SS]
+  float* gram = smem + S * SS;                 // [S][P]
   const int tid = threadIdx.x;
   const int64_t b0 = (int64_t)blockIdx.x * S;
   const int nvalid = (int)(a.batch - b0 < S ? a.batch - b0 : S);
+  IP_STAMP(0);
 
   if constexpr (KIND != 3) {
-    for (int t = tid; t < S * F; t += 256) {
+    for (int t = tid; t < S * F; t += IP_NT) {
       const int s = t / F, c = t - s * F;
       const int64_t bb = b0 + (s < nvalid ? s : nvalid - 1);
       lid[s][c] = I::load(a.ids, bb * a.id_stride + c);
     }
-    for (int t = tid; t < 2 * F; t += 256) {
+    for (int t = tid; t < 2 * F; t += IP_NT) {
       const int c = t < F ? t : t - F;
       lmeta[t < F ? 0 : 1][c] = t < F ? a.offs[c] : a.vocab[c];
     }
@@ -155,91 +165,167 @@ __global__ __launch_bounds__(256) void inner_fast(InnerArgs a) {
 
   bool bad = false;
   const float* src = KIND == 3 ? a.emb : a.table;  // embeddings given vs gathered
-  const int total = S * F * KQ;
-  for (int base = 0; base < total; base += 256 * 8) {
-    floatx4 v[8];
-    int dsti[8];
+  // Row gather: wave w takes samples w, w+4, ...; a sample's F*KQ float4
+  // chunks spread over the lanes (chunk = lane + 64*u: field chunk/KQ, quad
+  // chunk%KQ), all loads of a pass issued before the LDS stores.
+  {
+    const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int FKQ = F * KQ;
+    const int per_s = (FKQ + 63) / 64;     // chunks per lane per sample
+    const int nit = ((S + IP_NW - 1) / IP_NW) * per_s;  // (sample, chunk-block) steps of this wave
+    for (int base = 0; base < nit; base += 8) {
+      floatx4 v[8];
+      int dsti[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int idx = base + u * 256 + tid;
-      dsti[u] = -1;
-      v[u] = floatx4{0.f, 0.f, 0.f, 0.f};
-      if (idx < total) {
-        const int s = idx / (F * KQ), r = idx - s * (F * KQ);
-        const int c = r / KQ, q = r - c * KQ;
-        const int64_t bb = b0 + (s < nvalid ? s : nvalid - 1);
-        int64_t row;
-        bool ok = true;
-        if constexpr (KIND == 3) {
-          row = bb * F + c;
-        } else {
-          int64_t id;
-          ok = I::decode(lid[s][c], lmeta[1][c], id);
-          row = lmeta[0][c] + id;
-          bad |= !ok && s < nvalid;
+      for (int u = 0; u < 8; ++u) {
+        const int it = base + u;
+        const int si = it / per_s, cb = it - si * per_s;  // per_s is 1..2 for F<=64, K<=16
+        const int sidx = w + IP_NW * si;
+        const int ch = cb * 64 + lane;
+        dsti[u] = -1;
+        v[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (it < nit && sidx < S && ch < FKQ) {
+          const int c = ch / KQ, q = ch - c * KQ;
+          const int64_t bb = b0 + (sidx < nvalid ? sidx : nvalid - 1);
+          int64_t row;
+          bool ok = true;
+          if constexpr (KIND == 3) {
+            row = bb * F + c;
+          } else {
+            int64_t id;
+            ok = I::decode(lid[sidx][c], lmeta[1][c], id);
+            row = lmeta[0][c] + id;
+            bad |= !ok && sidx < nvalid;
+          }
+          const floatx4 t = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(src + row * K + 4 * q));
+          v[u] = ok ? t : floatx4{0.f, 0.f, 0.f, 0.f};
+          dsti[u] = sidx * SS + c * K + 4 * q;
         }
-        const floatx4 t = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(src + row * K + 4 * q));
-        v[u] = ok ? t : floatx4{0.f, 0.f, 0.f, 0.f};
-        dsti[u] = (s * F + c) * K + 4 * q;
       }
-    }
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (dsti[u] >= 0) *reinterpret_cast<floatx4*>(tile + dsti[u]) = v[u];
+      for (int u = 0; u < 8; ++u)
+        if (dsti[u] >= 0) *reinterpret_cast<floatx4*>(tile + dsti[u]) = v[u];
+    }
   }
+  IP_STAMP(1);
   if (bad) flag_error(a.err);
   __syncthreads();
+  IP_STAMP(2);
 
-  const int NG = F / 2 > 0 ? F / 2 : 1;  // balanced row pairs (g, F-2-g)
-  for (int t = tid; t < S * NG; t += 256) {
-    const int s = t / NG, g = t - s * NG;
-    const float* es = tile + s * F * K;
-    float* gs = gram + s * P;
-    for (int pass = 0; pass < 2; ++pass) {
-      const int i = pass == 0 ? g : F - 2 - g;
-      if (pass == 1 && i <= g) break;
-      if (i > F - 2) continue;
-      float ei[K];
+  // Gram matrix per sample on MFMA: G = E E^T with E [F x K] from the LDS
+  // tile, 16x16 blocks (bi <= bj) of v_mfma_f32_16x16x4_f32.  Lane l holds
+  // float4 E[16b + (l&15)][16grp + 4(l>>4) ..+3] — the A fragment of row block
+  // b and, identically, the B fragment of column block b; MFMA j of a group
+  // takes component j (k order permuted the same way on both sides).  Only
+  // the strict upper triangle i < j < F is stored, at the reference's pair
+  // index p(i,j) = i(2F-i-1)/2 + j-i-1 (layer/interaction.py:174-177).
+  {
+    constexpr int NGRP = (K + 15) / 16;
+    const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int NB = (F + 15) >> 4;
+    const int kof = 4 * (lane >> 4);
+    for (int si = w; si < S; si += IP_NW) {
+      const float* es = tile + si * SS;
+      float* gs = gram + si * P;
+      if (NB <= 2) {
+        // common case (F <= 32): both row-block fragments read once, the three
+        // blocks (0,0) (0,1) (1,1) as independent MFMA chains
+        floatx4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
 #pragma unroll
-      for (int q = 0; q < KQ; ++q) {
-        const floatx4 x = *reinterpret_cast<const floatx4*>(es + i * K + 4 * q);
-        ei[4 * q] = x[0]; ei[4 * q + 1] = x[1]; ei[4 * q + 2] = x[2]; ei[4 * q + 3] = x[3];
-      }
-      const int p0 = i * (2 * F - i - 1) / 2 - i - 1;
-      for (int j = i + 1; j < F; ++j) {
-        float dot = 0.f;
+        for (int grp = 0; grp < NGRP; ++grp) {
+          const int kk = 16 * grp + kof;
+          const int r0 = lane & 15, r1 = 16 + (lane & 15);
+          floatx4 f0 = {0.f, 0.f, 0.f, 0.f}, f1 = f0;
+          if (kk < K && r0 < F) f0 = *reinterpret_cast<const floatx4*>(es + r0 * K + kk);
+          if (kk < K && r1 < F) f1 = *reinterpret_cast<const floatx4*>(es + r1 * K + kk);
 #pragma unroll
-        for (int q = 0; q < KQ; ++q) {
-          const floatx4 y = *reinterpret_cast<const floatx4*>(es + j * K + 4 * q);
-          dot = fmaf(ei[4 * q], y[0], dot);
-          dot = fmaf(ei[4 * q + 1], y[1], dot);
-          dot = fmaf(ei[4 * q + 2], y[2], dot);
-          dot = fmaf(ei[4 * q + 3], y[3], dot);
+          for (int q = 0; q < 4; ++q) {
+            c00 = mfma16x16x4(f0[q], f0[q], c00);
+            c01 = mfma16x16x4(f0[q], f1[q], c01);
+            c11 = mfma16x16x4(f1[q], f1[q], c11);
+          }
         }
-        gs[p0 + j] = dot;
+        const int jj0 = lane & 15, jj1 = 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i0 = 4 * (lane >> 4) + r, i1 = 16 + i0;
+          if (i0 < jj0 && jj0 < F) gs[i0 * (2 * F - i0 - 1) / 2 + jj0 - i0 - 1] = c00[r];
+          if (jj1 < F) gs[i0 * (2 * F - i0 - 1) / 2 + jj1 - i0 - 1] = c01[r];
+          if (i1 < jj1 && jj1 < F) gs[i1 * (2 * F - i1 - 1) / 2 + jj1 - i1 - 1] = c11[r];
+        }
+        continue;
+      }
+      for (int bi = 0; bi < NB; ++bi) {
+        for (int bj = bi; bj < NB; ++bj) {
+          floatx4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int grp = 0; grp < NGRP; ++grp) {
+            const int kk = 16 * grp + kof;
+            const int ra = 16 * bi + (lane & 15), rb = 16 * bj + (lane & 15);
+            floatx4 fa = {0.f, 0.f, 0.f, 0.f}, fb = {0.f, 0.f, 0.f, 0.f};
+            if (kk < K && ra < F) fa = *reinterpret_cast<const floatx4*>(es + ra * K + kk);
+            if (kk < K && rb < F) fb = *reinterpret_cast<const floatx4*>(es + rb * K + kk);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) c = mfma16x16x4(fa[q], fb[q], c);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ii = 16 * bi + 4 * (lane >> 4) + r, jj = 16 * bj + (lane & 15);
+            if (ii < jj && jj < F) gs[ii * (2 * F - ii - 1) / 2 + jj - ii - 1] = c[r];
+          }
+        }
       }
     }
   }
   __syncthreads();
-
+  IP_STAMP(3);
+  // coalesced output rows [flat F*K | inner P]
   const int FK = a.write_flat ? F * K : 0;
   const int W = FK + P;
-  for (int e = tid; e < nvalid * W; e += 256) {
-    const int s = e / W, col = e - s * W;
-    const float val = col < FK ? tile[s * F * K + col] : gram[s * P + (col - FK)];
-    const int oc = col < FK ? col : a.inner_off + (col - FK);
-    a.out[(b0 + s) * a.out_stride + oc] = val;
+  if (a.contig) {
+    // the workgroup's rows are one contiguous, 16-B aligned block: float4
+    // stores (scalar stores are issue-bound at ~4 B/clk/CU)
+    float* ob = a.out + b0 * a.out_stride;
+    const int n = nvalid * W;
+    const int dq = 4 * IP_NT / W, dr = 4 * IP_NT - dq * W;
+    int f = 4 * tid, s0 = f / W, c0 = f - s0 * W;
+    for (; f < n; f += 4 * IP_NT) {
+      floatx4 v;
+      int ss = s0, cc = c0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[q] = cc < FK ? tile[ss * SS + cc] : gram[ss * P + (cc - FK)];
+        if (++cc == W) { cc = 0; ++ss; }
+      }
+      if (f + 4 <= n) {
+        *reinterpret_cast<floatx4*>(ob + f) = v;
+      } else {
+        for (int q = 0; q < n - f; ++q) ob[f + q] = v[q];
+      }
+      s0 += dq;
+      c0 += dr;
+      if (c0 >= W) { c0 -= W; ++s0; }
+    }
+  } else {
+  for (int s = 0; s < nvalid; ++s) {
+    float* orow = a.out + (b0 + s) * a.out_stride;
+    for (int col = tid; col < W; col += IP_NT) {
+      const float val = col < FK ? tile[s * SS + col] : gram[s * P + (col - FK)];
+      orow[col < FK ? col : a.inner_off + (col - FK)] = val;
+    }
   }
+  }
+  IP_STAMP(4);
 }
 
 template <int KIND>
 static void launch_inner_fast_k(const InnerArgs& a, size_t lds, unsigned grid, hipStream_t st) {
   switch (a.k) {
-    case 4: inner_fast<4, KIND><<<grid, 256, lds, st>>>(a); break;
-    case 8: inner_fast<8, KIND><<<grid, 256, lds, st>>>(a); break;
-    case 16: inner_fast<16, KIND><<<grid, 256, lds, st>>>(a); break;
-    case 32: inner_fast<32, KIND><<<grid, 256, lds, st>>>(a); break;
-    default: inner_fast<64, KIND><<<grid, 256, lds, st>>>(a); break;
+    case 4: inner_fast<4, KIND><<<grid, IP_NT, lds, st>>>(a); break;
+    case 8: inner_fast<8, KIND><<<grid, IP_NT, lds, st>>>(a); break;
+    case 16: inner_fast<16, KIND><<<grid, IP_NT, lds, st>>>(a); break;
+    case 32: inner_fast<32, KIND><<<grid, IP_NT, lds, st>>>(a); break;
+    default: inner_fast<64, KIND><<<grid, IP_NT, lds, st>>>(a); break;
   }
 }
 
@@ -248,10 +334,13 @@ static int launch_inner(InnerArgs a, hipStream_t st, const char* what) {
   const bool fast_k = a.k == 4 || a.k == 8 || a.k == 16 || a.k == 32 || a.k == 64;
   if (fast_k && a.F >= 2 && a.F <= IP_FMAX) {
     const int P = a.F * (a.F - 1) / 2;
-    const int64_t per = ((int64_t)a.F * a.k + P) * sizeof(float);
+    const int64_t per = ((int64_t)a.F * a.k + 4 + P) * sizeof(float);
     int S = IP_SMAX;
     while (S > 1 && S * per > 96 * 1024) --S;
     a.S = S;
+    const int W = (a.write_flat ? a.F * a.k : 0) + P;
+    a.contig = a.out_stride == W && a.inner_off == (a.write_flat ? a.F * a.k : 0) && (uintptr_t)a.out % 16 == 0 &&
+               ((int64_t)S * W) % 4 == 0;
     const size_t lds = (size_t)S * per;
     const unsigned grid = (unsigned)((a.batch + S - 1) / S);
     if (a.ids == nullptr) {
@@ -280,6 +369,9 @@ static int launch_inner(InnerArgs a, hipStream_t st, const char* what) {
 
 using namespace rs;
 
+static unsigned long long* g_inner_dbg = nullptr;
+extern "C" void rs_diag_inner_set_dbg(unsigned long long* p) { g_inner_dbg = p; }
+
 extern "C" int rs_inner_product_fwd(const float* emb, int n_fields, int k, float* out, int64_t out_stride,
                                     int64_t batch, rs_stream_t stream) {
   RS_REQUIRE(emb && out, "rs_inner_product_fwd: null pointer");
@@ -287,6 +379,7 @@ extern "C" int rs_inner_product_fwd(const float* emb, int n_fields, int k, float
   RS_REQUIRE(out_stride >= (int64_t)n_fields * (n_fields - 1) / 2, "rs_inner_product_fwd: out_stride too small");
   RS_REQUIRE(k % 4 != 0 || (uintptr_t)emb % 16 == 0, "rs_inner_product_fwd: emb must be 16-B aligned");
   InnerArgs a{};
+  a.dbg = g_inner_dbg;
   a.emb = emb;
   a.F = n_fields;
   a.k = k;
@@ -309,6 +402,7 @@ extern "C" int rs_embed_inner_fwd(const void* ids, int id_kind, int64_t id_strid
              "rs_embed_inner_fwd: out_stride too small");
   RS_REQUIRE(k % 4 != 0 || (uintptr_t)table % 16 == 0, "rs_embed_inner_fwd: table must be 16-B aligned");
   InnerArgs a{};
+  a.dbg = g_inner_dbg;
   a.ids = ids;
   a.id_kind = id_kind;
   a.id_stride = id_stride;
