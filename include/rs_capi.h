@@ -125,6 +125,19 @@ int rs_cross_fwd(const float* x0, int64_t x_stride, int d, int n_layers,
                  const float* prepared, float* out, int64_t out_stride,
                  int64_t batch, rs_stream_t stream);
 
+/* Fused DCN input + CrossNet: x0 = [dense | EmbedLayer(ids)] (model/dcn.py:
+ * 24-27, layer/core.py:273-280) is assembled in LDS — never written to HBM —
+ * and out = CrossLayer(x0) (layer/interaction.py:75-83).  Gather arguments as
+ * rs_embed_gather; prepared from rs_cross_prepare(d = nd + F*k).  k % 4 == 0,
+ * 1..128 fields, d <= 1600.  Out-of-range ids set *err_flag, rows read 0.    */
+int rs_embed_cross_fwd(const void* ids, int id_kind, int64_t id_stride,
+                       const float* dense, int64_t dense_stride, int nd,
+                       const float* table, const int64_t* field_offsets,
+                       const int64_t* field_vocab, int n_fields, int k,
+                       int n_layers, const float* prepared, float* out,
+                       int64_t out_stride, int64_t batch, int* err_flag,
+                       rs_stream_t stream);
+
 /* ----------------------------------------------- PNN inner product (a11)
  * InnerProductLayer.call (layer/interaction.py:170-183) on e[B,F,k]:
  *   out[b,p] = <e[b,i_p,:], e[b,j_p,:]>, pairs (i<j) in row-major order.

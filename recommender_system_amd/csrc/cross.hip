@@ -20,7 +20,7 @@ struct CrossGeom {
   int64_t b_img, h_off, beta_off, size;
 };
 
-static CrossGeom cross_geom(int d, int L) {
+static inline CrossGeom cross_geom(int d, int L) {
   CrossGeom g{};
   g.d = d;
   g.L = L;
@@ -81,35 +81,14 @@ struct CrossArgs {
   int64_t batch;
 };
 
+// Phases (2)-(4) on a staged 16 x d tile of x0 (rows >= `rows` zero).
 template <int NT, int NW>
-__global__ __launch_bounds__(NW * 64) void cross_mfma(CrossArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* tile = smem;                                       // [16][d]
-  float* cs = smem + ((16 * a.d + 3) / 4) * 4;              // [NW][16][NT*16+1]
-  float* alpha = cs + NW * 16 * (NT * 16 + 1);              // [16]
+__device__ __forceinline__ void cross_tile(const CrossArgs& a, float* tile, float* cs, float* alpha, int64_t b0,
+                                           int rows) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int s = lane & 15, kk = lane >> 4;
-  const int64_t b0 = (int64_t)blockIdx.x * 16;
-  const int rows = (int)((a.batch - b0) < 16 ? (a.batch - b0) : 16);
-
-  // (1) stage the 16 x d tile of x0 (coalesced)
   const int n = rows * a.d;
-  if (a.x_stride == a.d && ((uintptr_t)(a.x0 + b0 * a.d) % 16 == 0)) {
-    const float* src = a.x0 + b0 * a.d;
-    const int n4 = n / 4;
-    for (int i = threadIdx.x; i < n4; i += blockDim.x)
-      reinterpret_cast<floatx4*>(tile)[i] = reinterpret_cast<const floatx4*>(src)[i];
-    for (int i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) tile[i] = src[i];
-  } else {
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-      const int r = i / a.d, j = i - r * a.d;
-      tile[i] = a.x0[(b0 + r) * a.x_stride + j];
-    }
-  }
-  for (int i = n + threadIdx.x; i < 16 * a.d; i += blockDim.x) tile[i] = 0.f;
-  __syncthreads();
-
   // (2) G = X0 @ W on MFMA, K split across the NW waves
   floatx4 acc[NT];
 #pragma unroll
@@ -141,23 +120,141 @@ __global__ __launch_bounds__(NW * 64) void cross_mfma(CrossArgs a) {
   }
   __syncthreads();
 
-  // (4) out = alpha * x0 + beta_L (coalesced)
+  // (4) out = alpha * x0 + beta_L: float4 stores over the contiguous block
+  // (row/column tracked incrementally, no per-element division)
   if (a.out_stride == a.d && ((uintptr_t)(a.out + b0 * a.d) % 16 == 0) && (a.d % 4 == 0)) {
     floatx4* dst = reinterpret_cast<floatx4*>(a.out + b0 * a.d);
     const int n4 = n / 4;
-    for (int i = threadIdx.x; i < n4; i += blockDim.x) {
-      const int r = (4 * i) / a.d, j = 4 * i - r * a.d;
+    const int step = 4 * NW * 64, dq = step / a.d, dr = step - dq * a.d;
+    int i = threadIdx.x, r = (4 * i) / a.d, j = 4 * i - r * a.d;
+    for (; i < n4; i += NW * 64) {
       const floatx4 x = reinterpret_cast<const floatx4*>(tile)[i];
       const float al = alpha[r];
       dst[i] = floatx4{fmaf(al, x[0], a.beta[j]), fmaf(al, x[1], a.beta[j + 1]), fmaf(al, x[2], a.beta[j + 2]),
                        fmaf(al, x[3], a.beta[j + 3])};
+      r += dq;
+      j += dr;
+      if (j >= a.d) { j -= a.d; ++r; }
     }
   } else {
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-      const int r = i / a.d, j = i - r * a.d;
-      a.out[(b0 + r) * a.out_stride + j] = fmaf(alpha[r], tile[i], a.beta[j]);
+    for (int r = 0; r < rows; ++r) {
+      float* orow = a.out + (b0 + r) * a.out_stride;
+      const float al = alpha[r];
+      for (int j = threadIdx.x; j < a.d; j += NW * 64) orow[j] = fmaf(al, tile[r * a.d + j], a.beta[j]);
     }
   }
+}
+
+template <int NT, int NW>
+__global__ __launch_bounds__(NW * 64) void cross_mfma(CrossArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* tile = smem;                                       // [16][d]
+  float* cs = smem + ((16 * a.d + 3) / 4) * 4;              // [NW][16][NT*16+1]
+  float* alpha = cs + NW * 16 * (NT * 16 + 1);              // [16]
+  const int64_t b0 = (int64_t)blockIdx.x * 16;
+  const int rows = (int)((a.batch - b0) < 16 ? (a.batch - b0) : 16);
+
+  // (1) stage the 16 x d tile of x0 (coalesced)
+  const int n = rows * a.d;
+  if (a.x_stride == a.d && ((uintptr_t)(a.x0 + b0 * a.d) % 16 == 0)) {
+    const float* src = a.x0 + b0 * a.d;
+    const int n4 = n / 4;
+    for (int i = threadIdx.x; i < n4; i += blockDim.x)
+      reinterpret_cast<floatx4*>(tile)[i] = reinterpret_cast<const floatx4*>(src)[i];
+    for (int i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) tile[i] = src[i];
+  } else {
+    for (int r = 0; r < rows; ++r)
+      for (int j = threadIdx.x; j < a.d; j += blockDim.x) tile[r * a.d + j] = a.x0[(b0 + r) * a.x_stride + j];
+  }
+  for (int i = n + threadIdx.x; i < 16 * a.d; i += blockDim.x) tile[i] = 0.f;
+  __syncthreads();
+  cross_tile<NT, NW>(a, tile, cs, alpha, b0, rows);
+}
+
+// Fused DCN input + CrossNet (model/dcn.py:24-27 + CrossLayer): x0 = [dense |
+// EmbedLayer(ids)] is assembled straight into the LDS tile (cooperative id
+// tile, one sample per wave, every row chunk requested before any LDS store),
+// so x0 never round-trips through HBM; then phases (2)-(4).  k % 4 == 0.
+struct EmbedCrossArgs {
+  const void* ids;
+  int64_t id_stride;
+  const float* dense;
+  int64_t dense_stride;
+  int nd, F, k;
+  const float* table;
+  const int64_t* offs;
+  const int64_t* vocab;
+  int* err;
+};
+
+constexpr int EC_FMAX = 128;
+
+template <int NT, int KIND>
+__global__ __launch_bounds__(16 * 64) void embed_cross(CrossArgs a, EmbedCrossArgs e) {
+  constexpr int NW = 16;
+  typedef Ids<KIND> I;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ typename I::raw_t lid[16][EC_FMAX];
+  __shared__ int64_t lmeta[2][EC_FMAX];
+  float* tile = smem;
+  float* cs = smem + ((16 * a.d + 3) / 4) * 4;
+  float* alpha = cs + NW * 16 * (NT * 16 + 1);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t b0 = (int64_t)blockIdx.x * 16;
+  const int rows = (int)((a.batch - b0) < 16 ? (a.batch - b0) : 16);
+  const int F = e.F;
+
+  for (int t = tid; t < 16 * F; t += NW * 64) {
+    const int ss = t / F, c = t - ss * F;
+    lid[ss][c] = I::load(e.ids, (b0 + (ss < rows ? ss : rows - 1)) * e.id_stride + c);
+  }
+  for (int t = tid; t < 2 * F; t += NW * 64) {
+    const int c = t < F ? t : t - F;
+    lmeta[t < F ? 0 : 1][c] = t < F ? e.offs[c] : e.vocab[c];
+  }
+  // dense columns (wave w: sample w)
+  {
+    const int64_t bb = b0 + (w < rows ? w : rows - 1);
+    for (int j = lane; j < e.nd; j += 64) tile[w * a.d + j] = w < rows ? e.dense[bb * e.dense_stride + j] : 0.f;
+  }
+  __syncthreads();
+
+  // rows: wave w gathers sample w's F*k/4 float4 chunks
+  bool bad = false;
+  {
+    const int KQ = e.k >> 2, FKQ = F * KQ;
+    const int nit = (FKQ + 63) >> 6;
+    for (int base = 0; base < nit; base += 8) {
+      floatx4 v[8];
+      int dst[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int ch = (base + u) * 64 + lane;
+        dst[u] = -1;
+        v[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (base + u < nit && ch < FKQ) {
+          const int c = ch / KQ, q = ch - c * KQ;
+          int64_t id;
+          const bool ok = I::decode(lid[w][c], lmeta[1][c], id);
+          bad |= !ok && w < rows;
+          const floatx4 t =
+              __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(e.table + (lmeta[0][c] + id) * e.k + 4 * q));
+          v[u] = (ok && w < rows) ? t : floatx4{0.f, 0.f, 0.f, 0.f};
+          dst[u] = w * a.d + e.nd + c * e.k + 4 * q;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (dst[u] >= 0) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) tile[dst[u] + q] = v[u][q];
+        }
+    }
+  }
+  if (__any(bad) && lane == 0) flag_error(e.err);
+  __syncthreads();
+  cross_tile<NT, NW>(a, tile, cs, alpha, b0, rows);
 }
 
 }  // namespace rs
@@ -208,4 +305,51 @@ extern "C" int rs_cross_fwd(const float* x0, int64_t x_stride, int d, int n_laye
     cross_mfma<2, NW><<<grid, NW * 64, lds, st>>>(a);
   }
   return launch_status("rs_cross_fwd");
+}
+
+extern "C" int rs_embed_cross_fwd(const void* ids, int id_kind, int64_t id_stride, const float* dense,
+                                  int64_t dense_stride, int nd, const float* table, const int64_t* field_offsets,
+                                  const int64_t* field_vocab, int n_fields, int k, int n_layers,
+                                  const float* prepared, float* out, int64_t out_stride, int64_t batch,
+                                  int* err_flag, rs_stream_t stream) {
+  RS_REQUIRE(ids && table && field_offsets && field_vocab && prepared && out, "rs_embed_cross_fwd: null pointer");
+  RS_REQUIRE(nd == 0 || dense, "rs_embed_cross_fwd: dense is null");
+  RS_REQUIRE(n_fields >= 1 && n_fields <= EC_FMAX && nd >= 0 && k >= 4 && k % 4 == 0,
+             "rs_embed_cross_fwd: need 1..128 fields and k a multiple of 4");
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_embed_cross_fwd: bad id_kind");
+  RS_REQUIRE((uintptr_t)table % 16 == 0, "rs_embed_cross_fwd: table must be 16-B aligned");
+  const int d = nd + n_fields * k;
+  RS_REQUIRE(n_layers >= 0 && n_layers <= 32 && batch >= 0, "rs_embed_cross_fwd: bad shape");
+  RS_REQUIRE(out_stride >= d, "rs_embed_cross_fwd: out_stride < d");
+  RS_REQUIRE(d <= 1600, "rs_embed_cross_fwd: d > 1600 not supported (LDS tile)");
+  if (batch == 0) return RS_OK;
+  const int L = n_layers;
+  const CrossGeom g = cross_geom(d, L < 1 ? 1 : L);
+  CrossArgs a{nullptr, d, d, L, g.DB, prepared, prepared + g.h_off, prepared + g.beta_off, out, out_stride, batch};
+  EmbedCrossArgs e{ids, id_stride, dense, dense_stride, nd, n_fields, k, table, field_offsets, field_vocab, err_flag};
+  constexpr int NW = 16;
+  const size_t lds = (size_t)(((16 * d + 3) / 4) * 4 + NW * 16 * (g.NT * 16 + 1) + 16) * sizeof(float);
+  const unsigned grid = (unsigned)((batch + 15) / 16);
+  hipStream_t st = as_stream(stream);
+  with_id_kind(id_kind, [&](auto K) {
+    constexpr int KIND = decltype(K)::value;
+    if (g.NT == 1) {
+      static size_t set1 = 64 * 1024;
+      if (lds > set1) {
+        (void)hipFuncSetAttribute((const void*)embed_cross<1, KIND>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        set1 = lds;
+      }
+      embed_cross<1, KIND><<<grid, NW * 64, lds, st>>>(a, e);
+    } else {
+      static size_t set2 = 64 * 1024;
+      if (lds > set2) {
+        (void)hipFuncSetAttribute((const void*)embed_cross<2, KIND>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        set2 = lds;
+      }
+      embed_cross<2, KIND><<<grid, NW * 64, lds, st>>>(a, e);
+    }
+  });
+  return launch_status("rs_embed_cross_fwd");
 }

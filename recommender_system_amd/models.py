@@ -198,6 +198,23 @@ class DCN(KerasModule):
         # fused into the Dense epilogue; weights keep the Keras Dense names.
         self.output_layer = Dense(1, "sigmoid", device=device, seed=_subseed(self._gen), input_dim=d + output_dim)
         self.d = d
+        self._err = _ErrFlag(self._dev)
+
+    def cross_fused(self, inputs, out=None, check_ids=True):
+        """CrossLayer([dense | EmbedLayer(ids)]) in ONE launch (rs_embed_cross_fwd):
+        x0 is assembled in LDS and never written to HBM."""
+        dense, ids = _split_criteo(inputs, self.nd, self._dev)
+        B = ids.shape[0]
+        e = self.embed_layer
+        if out is None:
+            out = torch.empty(B, self.d, dtype=torch.float32, device=self._dev)
+        prep = self.cross_layer.prepared(self.d)
+        call("rs_embed_cross_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), self.nd,
+             ptr(e.table), ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, e.k, self.cross_layer.layer_num,
+             ptr(prep), ptr(out), out.stride(0), B, ptr(self._err.t), _lib.stream())
+        if check_ids:
+            self._err.check("DCN")
+        return out
 
     def forward(self, inputs, check_ids=True):
         dense, ids = _split_criteo(inputs, self.nd, self._dev)
