@@ -93,12 +93,26 @@ __device__ __forceinline__ void cross_tile(const CrossArgs& a, float* tile, floa
   floatx4 acc[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int t = w; t < a.DB; t += NW) {
-    const int e = 4 * t + kk;
-    const float xv = e < a.d ? tile[s * a.d + e] : 0.f;
-    const float* rec = a.img + (int64_t)t * NT * 64;
+  // the wave's k-steps are t = w + NW*i; their B fragments (L2-resident) are
+  // requested 8 steps at a time before any MFMA waits on them
+  for (int t0 = w; t0 < a.DB; t0 += 8 * NW) {
+    float bv[8][NT], xv[8];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(xv, rec[nt * 64 + lane], acc[nt]);
+    for (int u = 0; u < 8; ++u) {
+      const int t = min(t0 + u * NW, a.DB - 1);
+      const float* rec = a.img + (int64_t)t * NT * 64;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) bv[u][nt] = rec[nt * 64 + lane];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = 4 * (t0 + u * NW) + kk;
+      xv[u] = (t0 + u * NW < a.DB && e < a.d) ? tile[s * a.d + e] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(xv[u], bv[u][nt], acc[nt]);
   }
   constexpr int CW = NT * 16 + 1;
 #pragma unroll
@@ -157,10 +171,23 @@ __global__ __launch_bounds__(NW * 64) void cross_mfma(CrossArgs a) {
   // (1) stage the 16 x d tile of x0 (coalesced)
   const int n = rows * a.d;
   if (a.x_stride == a.d && ((uintptr_t)(a.x0 + b0 * a.d) % 16 == 0)) {
+    // all of a thread's float4 loads are issued before its LDS stores (a
+    // load->store loop would pay one HBM round trip per iteration)
     const float* src = a.x0 + b0 * a.d;
     const int n4 = n / 4;
-    for (int i = threadIdx.x; i < n4; i += blockDim.x)
-      reinterpret_cast<floatx4*>(tile)[i] = reinterpret_cast<const floatx4*>(src)[i];
+    for (int i0 = threadIdx.x; i0 < n4; i0 += 8 * NW * 64) {
+      floatx4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * NW * 64;
+        v[u] = i < n4 ? reinterpret_cast<const floatx4*>(src)[i] : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * NW * 64;
+        if (i < n4) reinterpret_cast<floatx4*>(tile)[i] = v[u];
+      }
+    }
     for (int i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) tile[i] = src[i];
   } else {
     for (int r = 0; r < rows; ++r)
