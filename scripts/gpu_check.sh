@@ -41,6 +41,18 @@ if [ "${SKIP_PROF:-0}" != 1 ]; then
         -- python3 "$R/scripts/pmc_driver.py" > "$R/gpurun_out/pmc$i.log" 2>&1
     rc=$?; [ $rc -eq 0 ] || { echo "pmc pass $i rc=$rc"; tail -5 "$R/gpurun_out/pmc$i.log"; exit $rc; }
   done
+  for cfg in dcn din pnn; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$cfg" -o run --output-format csv \
+        -- python3 "$R/bench.py" --config $cfg --steps 50 --warmup 5 --no-cpu-baseline > "$R/gpurun_out/prof_$cfg.json" 2> "$R/gpurun_out/prof_$cfg.err"
+    rc=$?; [ $rc -eq 0 ] || { echo "rocprof $cfg rc=$rc"; tail -5 "$R/gpurun_out/prof_$cfg.err"; exit $rc; }
+  done
+  # MFMA utilisation of the MFMA-shaped kernels (CrossNet, DIN attention, DNN tower in the fused DeepFM)
+  for cfg in dcn din hotpath; do
+    timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
+        -d "$R/gpurun_out/mfma_$cfg" -o pmc --output-format csv \
+        -- python3 "$R/bench.py" --config $cfg --steps 20 --warmup 2 --no-cpu-baseline > "$R/gpurun_out/mfma_$cfg.log" 2>&1
+    rc=$?; [ $rc -eq 0 ] || { echo "mfma pmc $cfg rc=$rc"; tail -5 "$R/gpurun_out/mfma_$cfg.log"; exit $rc; }
+  done
   cd "$R"
 fi
 echo DONE

@@ -83,6 +83,32 @@ def main(tag):
         out["probe_gather"] = {"rows_per_dispatch": 1703936, "index_lines_128B": 1703936 * 8 // 128,
                                "RDREQ_random_rows_dispatches": req[:5], "RDREQ_line_pair_dispatches": req[5:]}
     json.dump(out, open(os.path.join(P, f"{tag}_pmc.json"), "w"), indent=1)
+    # per-config kernel stats (rocprofv3 --kernel-trace --stats of bench.py --config X)
+    for cfg in ("dcn", "din", "pnn"):
+        src = os.path.join(G, f"prof_{cfg}", "run_kernel_stats.csv")
+        if os.path.exists(src):
+            shutil.copy(src, os.path.join(P, f"{tag}_rocprof_kernel_stats_{cfg}.csv"))
+    # MFMA utilisation: SQ_VALU_MFMA_BUSY_CYCLES summed over the 1024 SIMDs,
+    # against the dispatch's wall cycles (GRBM_GUI_ACTIVE is summed over 8 XCDs)
+    mf = {}
+    for cfg in ("dcn", "din", "hotpath"):
+        path = os.path.join(G, f"mfma_{cfg}", "pmc_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        per = defaultdict(lambda: defaultdict(list))
+        for r in csv.DictReader(open(path)):
+            per[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for kname, cs in per.items():
+            if "SQ_VALU_MFMA_BUSY_CYCLES" not in cs or not any(v > 0 for v in cs["SQ_VALU_MFMA_BUSY_CYCLES"]):
+                continue
+            busy = st.median(cs["SQ_VALU_MFMA_BUSY_CYCLES"])
+            wall = st.median(cs["GRBM_GUI_ACTIVE"]) / 8
+            mf[kname[:90]] = {"config": cfg, "dispatches": len(cs["SQ_VALU_MFMA_BUSY_CYCLES"]),
+                              "mfma_busy_cycles_median": busy, "wall_cycles_median": wall,
+                              "mfma_util": busy / (1024 * wall) if wall else None}
+    if mf:
+        json.dump({"formula": "mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs * GRBM_GUI_ACTIVE / 8)",
+                   "kernels": mf}, open(os.path.join(P, f"{tag}_mfma_util.json"), "w"), indent=1)
     for n in ("bench.json", "bench_configs.jsonl"):
         s = os.path.join(G, n)
         if os.path.exists(s):
