@@ -184,6 +184,26 @@ int rs_din_attention_dice_fwd(const float* query, const float* keys,
                               const float* b_out, float* out, int64_t batch,
                               rs_stream_t stream);
 
+/* DIN attention straight from behaviour ids (model/din.py:56-80 + Attention
+ * 'prelu', layer/interaction.py:355-406): key = value = table[hist[b,t]],
+ * query = table[cand[b]], mask = hist != 0.  Two launches: scores (MFMA, the
+ * tile's PReLU alphas and W2 staged once per workgroup, layer 1 regrouped per
+ * sample as q(Wq+Wd) + key(Wk-Wd+diag(q)Wp)) then the masked softmax pool.
+ * prepared: rs_din_prepare (k in {4,8,16}, H1 <= 128, H2 <= 64); scores: a
+ * caller-owned [B, T] fp32 workspace; out [B, k].  OOR ids set *err_flag.   */
+int64_t rs_din_prepared_size(int T, int k, int H1, int H2);
+int rs_din_prepare(const float* W1, const float* b1, const float* alpha1,
+                   int H1, const float* W2, const float* b2,
+                   const float* alpha2, int H2, const float* w3,
+                   const float* b3, int T, int k, float* prepared,
+                   rs_stream_t stream);
+int rs_din_attention_ids_fwd(const void* hist, int id_kind, int64_t hist_stride,
+                             const void* cand, int64_t cand_stride, int T,
+                             int k, const float* table, int64_t vocab, int H1,
+                             int H2, const float* prepared, float* scores,
+                             float* out, int64_t batch, int* err_flag,
+                             rs_stream_t stream);
+
 /* --------------------------------------------------- dense tower (a7, a15)
  * Keras Dense: y = act(x @ W + bias), W:[K,N] (Keras (in,out) orientation),
  * fp32 MFMA.  alpha: per-column PReLU slope (RS_ACT_PRELU only).            */

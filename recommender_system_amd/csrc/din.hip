@@ -1,0 +1,356 @@
+// din.hip — DIN attention unit straight from behaviour ids (model/din.py:
+// 56-80 + Attention, layer/interaction.py:355-406, 'prelu' mode):
+//   q   = E[cand]                    key_t = value_t = E[hist_t]
+//   e_t = [q, key_t, q-key_t, q*key_t]                 (:381-391)
+//   h1  = PReLU_{alpha1[t]}(e_t W1 + b1)               (:366,393-394)
+//   h2  = PReLU_{alpha2[t]}(h1 W2 + b2)
+//   s_t = h2 w3 + b3; s_t = -4294967296 where hist_t == 0 (:396-401, din.py mask)
+//   out = softmax_t(s) @ value                          (:403-405)
+//
+// MI355X design (two launches, weight-reuse first):
+//  * The behaviour table (63,001 x 8 fp32 = 2 MB in the config) is L2-resident:
+//    keys/values are read through the ids, never materialised as [B,T,k].
+//  * Layer 1 is regrouped per sample: with W1 = [Wq; Wk; Wd; Wp] (k rows each),
+//    e_t W1 = q (Wq + Wd) + key_t (Wk - Wd + diag(q) Wp).  The per-sample
+//    matrix W'_b = Wkd + diag(q) Wp is built in registers (one FMA per A
+//    value), so layer 1 costs k + k MAC rows per position instead of 4k:
+//    on v_mfma_f32_16x16x4_f32 (swapped orientation C^T = W^T e^T) the B
+//    operand is key_t for the W'_b steps and q (the same for every position
+//    column) for the Wqd steps — q(Wq+Wd) lands in every column for free.
+//  * din_scores: one workgroup per (16-position tile, 16 samples).  PReLU
+//    alphas depend on the position only, so the tile's alpha1/alpha2 slices
+//    (16 x 120 floats) and the W2^T image are staged in LDS once per
+//    workgroup and reused by all 16 samples; layer 1's accumulators are
+//    layer 2's B operand in registers (k order permuted to match).
+//  * din_pool: one wave per sample — masked softmax over the T scores and
+//    the weighted sum of the value rows (gathered through the ids again).
+#include "rs_common.hpp"
+
+namespace rs {
+
+struct DinGeom {
+  int k, KS, H1, H2, HT1, HT2, T, NTT;
+  int64_t wkd, wp, wqd, b1, a1, w2, b2, a2, w3, b3, size;
+};
+
+static inline DinGeom din_geom(int T, int k, int H1, int H2) {
+  DinGeom g{};
+  g.k = k;
+  g.KS = k / 4;
+  g.H1 = H1;
+  g.H2 = H2;
+  g.HT1 = (H1 + 15) / 16;
+  g.HT2 = (H2 + 15) / 16;
+  g.T = T;
+  g.NTT = (T + 15) / 16;
+  const int64_t img1 = (int64_t)g.HT1 * g.KS * 64;
+  int64_t o = 0;
+  g.wkd = o; o += img1;
+  g.wp = o; o += img1;
+  g.wqd = o; o += img1;
+  g.b1 = o; o += g.HT1 * 16;
+  g.a1 = o; o += (int64_t)g.NTT * 16 * g.HT1 * 16;  // [t (padded)][h1 (padded)]
+  g.w2 = o; o += (int64_t)g.HT2 * g.HT1 * 64 * 4;
+  g.b2 = o; o += g.HT2 * 16;
+  g.a2 = o; o += (int64_t)g.NTT * 16 * g.HT2 * 16;
+  g.w3 = o; o += g.HT2 * 16;
+  g.b3 = o; o += 4;
+  g.size = o;
+  return g;
+}
+
+struct DinPrepArgs {
+  const float *W1, *b1, *alpha1, *W2, *b2, *alpha2, *w3, *b3;
+  DinGeom g;
+  float* out;
+};
+
+// Packs every operand image; element i of the prepared buffer.
+__global__ void din_prepare_kernel(DinPrepArgs a) {
+  const DinGeom& g = a.g;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.size) return;
+  const int k = g.k, H1 = g.H1, H2 = g.H2;
+  float v = 0.f;
+  if (i < g.b1) {
+    // layer-1 A images [HT1][KS][64]: lane (h = 16ht + (l&15), kk = l>>4),
+    // step s <-> input row j = kk*KS + s of each k-row block
+    const int which = (int)(i / (g.wp - g.wkd));
+    const int64_t r = i - which * (g.wp - g.wkd);
+    const int lane = (int)(r & 63), st = (int)(r >> 6);
+    const int s = st % g.KS, ht = st / g.KS;
+    const int h = 16 * ht + (lane & 15), j = (lane >> 4) * g.KS + s;
+    if (h < H1) {
+      const float wq = a.W1[(int64_t)(0 * k + j) * H1 + h], wk = a.W1[(int64_t)(1 * k + j) * H1 + h];
+      const float wd = a.W1[(int64_t)(2 * k + j) * H1 + h], wpp = a.W1[(int64_t)(3 * k + j) * H1 + h];
+      v = which == 0 ? wk - wd : which == 1 ? wpp : wq + wd;
+    }
+  } else if (i < g.a1) {
+    const int h = (int)(i - g.b1);
+    v = h < H1 ? a.b1[h] : 0.f;
+  } else if (i < g.w2) {
+    const int64_t r = i - g.a1;
+    const int t = (int)(r / (g.HT1 * 16)), h = (int)(r % (g.HT1 * 16));
+    v = (t < g.T && h < H1) ? a.alpha1[(int64_t)t * H1 + h] : 0.f;
+  } else if (i < g.b2) {
+    // W2^T image [HT2][HT1][64][4]: lane (h2 = 16ht2 + (l&15), kk), r:
+    // W2[h1 = 16ht + 4kk + r][h2]
+    const int64_t r0 = i - g.w2;
+    const int r = (int)(r0 & 3), lane = (int)((r0 >> 2) & 63);
+    const int64_t st = r0 >> 8;
+    const int ht = (int)(st % g.HT1), ht2 = (int)(st / g.HT1);
+    const int h2 = 16 * ht2 + (lane & 15), h1 = 16 * ht + 4 * (lane >> 4) + r;
+    v = (h1 < H1 && h2 < H2) ? a.W2[(int64_t)h1 * H2 + h2] : 0.f;
+  } else if (i < g.a2) {
+    const int h = (int)(i - g.b2);
+    v = h < H2 ? a.b2[h] : 0.f;
+  } else if (i < g.w3) {
+    const int64_t r = i - g.a2;
+    const int t = (int)(r / (g.HT2 * 16)), h = (int)(r % (g.HT2 * 16));
+    v = (t < g.T && h < H2) ? a.alpha2[(int64_t)t * H2 + h] : 0.f;
+  } else if (i < g.b3) {
+    const int h = (int)(i - g.w3);
+    v = h < H2 ? a.w3[h] : 0.f;
+  } else {
+    v = i == g.b3 ? a.b3[0] : 0.f;
+  }
+  a.out[i] = v;
+}
+
+struct DinArgs {
+  const void* hist;
+  int64_t hist_stride;
+  const void* cand;
+  int64_t cand_stride;
+  const float* table;
+  int64_t vocab;
+  const float* prep;
+  DinGeom g;
+  float* scores;  // [B, T] workspace
+  float* out;     // [B, k]
+  int64_t batch;
+  int* err;
+};
+
+constexpr int DIN_SPW = 4;  // samples per wave in din_scores
+
+template <int KS>
+__device__ __forceinline__ void din_row(const float* table, int64_t row, int kk, float (&v)[KS]) {
+  const float* p = table + row * (4 * KS) + kk * KS;
+  if constexpr (KS == 4) {
+    const floatx4 x = *reinterpret_cast<const floatx4*>(p);
+    v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+  } else if constexpr (KS == 2) {
+    const floatx2 x = *reinterpret_cast<const floatx2*>(p);
+    v[0] = x[0]; v[1] = x[1];
+  } else {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) v[s] = p[s];
+  }
+}
+
+template <int KS, int HT1M, int HT2M, int KIND>
+__global__ __launch_bounds__(256) void din_scores(DinArgs a) {
+  typedef Ids<KIND> I;
+  const DinGeom& g = a.g;
+  __shared__ float a1s[16][HT1M * 16 + 4];
+  __shared__ float a2s[16][HT2M * 16 + 4];
+  __shared__ floatx4 w2s[HT2M * HT1M * 64];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = lane & 15, kg = lane >> 4;
+  const int t0 = blockIdx.x * 16;
+
+  // ---- stage the tile's alphas and the W2^T image (shared by 16 samples)
+  const float* pa1 = a.prep + g.a1 + (int64_t)t0 * (g.HT1 * 16);
+  const float* pa2 = a.prep + g.a2 + (int64_t)t0 * (g.HT2 * 16);
+  for (int i = threadIdx.x; i < 16 * g.HT1 * 16; i += 256) a1s[i / (g.HT1 * 16)][i % (g.HT1 * 16)] = pa1[i];
+  for (int i = threadIdx.x; i < 16 * g.HT2 * 16; i += 256) a2s[i / (g.HT2 * 16)][i % (g.HT2 * 16)] = pa2[i];
+  const floatx4* pw2 = reinterpret_cast<const floatx4*>(a.prep + g.w2);
+  for (int i = threadIdx.x; i < g.HT2 * g.HT1 * 64; i += 256) w2s[i] = pw2[i];
+
+  // ---- per-lane constants: layer-1 images, biases, w3
+  float wkd[HT1M][KS], wpv[HT1M][KS], wqd[HT1M][KS], b1v[HT1M][4], b2v[HT2M][4], w3v[HT2M][4];
+#pragma unroll
+  for (int ht = 0; ht < HT1M; ++ht) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int64_t o = (int64_t)(ht * KS + s) * 64 + lane;
+      const bool on = ht < g.HT1;
+      wkd[ht][s] = on ? a.prep[g.wkd + o] : 0.f;
+      wpv[ht][s] = on ? a.prep[g.wp + o] : 0.f;
+      wqd[ht][s] = on ? a.prep[g.wqd + o] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b1v[ht][r] = ht < g.HT1 ? a.prep[g.b1 + 16 * ht + 4 * kg + r] : 0.f;
+  }
+#pragma unroll
+  for (int ht = 0; ht < HT2M; ++ht)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool on = ht < g.HT2;
+      b2v[ht][r] = on ? a.prep[g.b2 + 16 * ht + 4 * kg + r] : 0.f;
+      w3v[ht][r] = on ? a.prep[g.w3 + 16 * ht + 4 * kg + r] : 0.f;
+    }
+  const float b3 = a.prep[g.b3];
+  __syncthreads();
+
+  const int t = t0 + col;
+  const bool tv = t < g.T;
+  bool bad = false;
+  for (int si = 0; si < DIN_SPW; ++si) {
+    const int64_t b = ((int64_t)blockIdx.y * 4 + w) * DIN_SPW + si;  // wave-uniform
+    if (b >= a.batch) break;
+    // candidate (query) row and this lane's behaviour row
+    int64_t cid, hid;
+    const typename I::raw_t craw = I::load(a.cand, b * a.cand_stride);
+    const bool cok = I::decode(craw, a.vocab, cid);
+    const typename I::raw_t hraw = I::load(a.hist, b * a.hist_stride + (tv ? t : 0));
+    const bool hok = I::decode(hraw, a.vocab, hid);
+    bad |= !cok || (tv && !hok);
+    float q[KS], kv[KS];
+    din_row<KS>(a.table, cid, kg, q);
+    din_row<KS>(a.table, hid, kg, kv);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      q[s] = cok ? q[s] : 0.f;
+      kv[s] = hok ? kv[s] : 0.f;
+    }
+    const bool masked = static_cast<float>(hraw) == 0.f;  // din.py: mask = hist != 0
+
+    // layer 1 (lane holds h = 16ht + 4kg + r of position t)
+    float y1[HT1M][4];
+#pragma unroll
+    for (int ht = 0; ht < HT1M; ++ht) {
+      if (ht < g.HT1) {
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) acc = mfma16x16x4(fmaf(q[s], wpv[ht][s], wkd[ht][s]), kv[s], acc);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) acc = mfma16x16x4(wqd[ht][s], q[s], acc);
+        const floatx4 al = *reinterpret_cast<const floatx4*>(&a1s[col][16 * ht + 4 * kg]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = acc[r] + b1v[ht][r];
+          y1[ht][r] = fmaxf(x, 0.f) + al[r] * fminf(x, 0.f);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y1[ht][r] = 0.f;
+      }
+    }
+    // layer 2 + score
+    float part = 0.f;
+#pragma unroll
+    for (int ht2 = 0; ht2 < HT2M; ++ht2) {
+      if (ht2 < g.HT2) {
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ht = 0; ht < HT1M; ++ht) {
+          if (ht < g.HT1) {
+            const floatx4 wa = w2s[(ht2 * g.HT1 + ht) * 64 + lane];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc = mfma16x16x4(wa[r], y1[ht][r], acc);
+          }
+        }
+        const floatx4 al = *reinterpret_cast<const floatx4*>(&a2s[col][16 * ht2 + 4 * kg]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = acc[r] + b2v[ht2][r];
+          part = fmaf(fmaxf(x, 0.f) + al[r] * fminf(x, 0.f), w3v[ht2][r], part);
+        }
+      }
+    }
+    part += __shfl_xor(part, 16);
+    part += __shfl_xor(part, 32);
+    if (kg == 0 && tv) a.scores[b * g.T + t] = masked ? -4294967296.0f : part + b3;
+  }
+  if (__any(bad) && lane == 0) flag_error(a.err);
+}
+
+// masked softmax over the T scores and out[b] = sum_t a_t * E[hist_t]
+template <int KIND>
+__global__ __launch_bounds__(256) void din_pool(DinArgs a) {
+  typedef Ids<KIND> I;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= a.batch) return;
+  const int T = a.g.T, k = a.g.k;
+  const float* sc = a.scores + b * T;
+  float mx = -INFINITY;
+  for (int t = lane; t < T; t += 64) mx = fmaxf(mx, sc[t]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  // lanes = (position group tg, channel j)
+  const int ntg = 64 / k, j = lane % k, tg = lane / k;
+  float sum = 0.f, acc = 0.f;
+  for (int t = tg; t < T; t += ntg) {
+    const float e = expf(sc[t] - mx);
+    int64_t id;
+    const bool ok = I::decode(I::load(a.hist, b * a.hist_stride + t), a.vocab, id);
+    const float v = ok ? a.table[id * k + j] : 0.f;
+    sum += e;
+    acc = fmaf(e, v, acc);
+  }
+  // reduce over the position groups (lanes j, j+k, j+2k, ...)
+  for (int o = k; o < 64; o <<= 1) {
+    sum += __shfl_xor(sum, o);
+    acc += __shfl_xor(acc, o);
+  }
+  if (lane < k) a.out[b * k + lane] = acc / sum;
+}
+
+template <int KS, int HT1M, int HT2M, int KIND>
+static void launch_din(const DinArgs& a, hipStream_t st) {
+  const dim3 grid(a.g.NTT, (unsigned)((a.batch + 4 * DIN_SPW - 1) / (4 * DIN_SPW)));
+  din_scores<KS, HT1M, HT2M, KIND><<<grid, 256, 0, st>>>(a);
+  din_pool<KIND><<<(unsigned)((a.batch + 3) / 4), 256, 0, st>>>(a);
+}
+
+template <int KS, int KIND>
+static void launch_din_h(const DinArgs& a, hipStream_t st) {
+  if (a.g.HT1 <= 5 && a.g.HT2 <= 3) launch_din<KS, 5, 3, KIND>(a, st);
+  else launch_din<KS, 8, 4, KIND>(a, st);
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" int64_t rs_din_prepared_size(int T, int k, int H1, int H2) {
+  if (T < 1 || (k != 4 && k != 8 && k != 16) || H1 < 1 || H1 > 128 || H2 < 1 || H2 > 64) return -1;
+  return din_geom(T, k, H1, H2).size;
+}
+
+extern "C" int rs_din_prepare(const float* W1, const float* b1, const float* alpha1, int H1, const float* W2,
+                              const float* b2, const float* alpha2, int H2, const float* w3, const float* b3, int T,
+                              int k, float* prepared, rs_stream_t stream) {
+  RS_REQUIRE(rs_din_prepared_size(T, k, H1, H2) > 0, "rs_din_prepare: need k in {4,8,16}, H1 <= 128, H2 <= 64");
+  RS_REQUIRE(W1 && b1 && alpha1 && W2 && b2 && alpha2 && w3 && b3 && prepared, "rs_din_prepare: null pointer");
+  DinPrepArgs a{W1, b1, alpha1, W2, b2, alpha2, w3, b3, din_geom(T, k, H1, H2), prepared};
+  din_prepare_kernel<<<(unsigned)((a.g.size + 255) / 256), 256, 0, as_stream(stream)>>>(a);
+  return launch_status("rs_din_prepare");
+}
+
+extern "C" int rs_din_attention_ids_fwd(const void* hist, int id_kind, int64_t hist_stride, const void* cand,
+                                        int64_t cand_stride, int T, int k, const float* table, int64_t vocab,
+                                        int H1, int H2, const float* prepared, float* scores, float* out,
+                                        int64_t batch, int* err_flag, rs_stream_t stream) {
+  RS_REQUIRE(rs_din_prepared_size(T, k, H1, H2) > 0,
+             "rs_din_attention_ids_fwd: need k in {4,8,16}, H1 <= 128, H2 <= 64");
+  RS_REQUIRE(hist && cand && table && prepared && scores && out, "rs_din_attention_ids_fwd: null pointer");
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32 && vocab >= 1 && batch >= 0 && hist_stride >= T,
+             "rs_din_attention_ids_fwd: bad ids / shape");
+  RS_REQUIRE((uintptr_t)table % 16 == 0, "rs_din_attention_ids_fwd: table must be 16-B aligned");
+  if (batch == 0) return RS_OK;
+  DinArgs a{hist, hist_stride, cand, cand_stride, table, vocab, prepared, din_geom(T, k, H1, H2),
+            scores, out, batch, err_flag};
+  hipStream_t st = as_stream(stream);
+  with_id_kind(id_kind, [&](auto K) {
+    constexpr int KIND = decltype(K)::value;
+    if (k == 4) launch_din_h<1, KIND>(a, st);
+    else if (k == 8) launch_din_h<2, KIND>(a, st);
+    else launch_din_h<4, KIND>(a, st);
+  });
+  return launch_status("rs_din_attention_ids_fwd");
+}

@@ -631,6 +631,45 @@ class Attention(KerasModule):
         self.out_kernel = nn.Parameter(_glorot_uniform(n, 1, self._gen, self._dev), requires_grad=False)
         self.out_bias = nn.Parameter(torch.zeros(1, device=self._dev), requires_grad=False)
 
+    def ids_ok(self, k):
+        """The id-driven fused path (rs_din_attention_ids_fwd) supports it."""
+        return (self.activation == "prelu" and self.out_kernel is not None and k in (4, 8, 16)
+                and self.hidden_units[0] <= 128 and self.hidden_units[1] <= 64)
+
+    def prepared_ids(self, k):
+        params = list(self.kernels) + list(self.biases) + list(self.alphas) + [self.out_kernel, self.out_bias]
+        key = (k, self.T) + tuple((p._version, p.data_ptr()) for p in params)
+        if getattr(self, "_ids_key", None) != key:
+            h1, h2 = self.hidden_units
+            n = _lib.lib().rs_din_prepared_size(self.T, k, h1, h2)
+            if n < 0:
+                _lib.check(-1, "rs_din_prepared_size")
+            prep = torch.empty(n, dtype=torch.float32, device=self._dev)
+            call("rs_din_prepare", ptr(self.kernels[0]), ptr(self.biases[0]), ptr(self.alphas[0]), h1,
+                 ptr(self.kernels[1]), ptr(self.biases[1]), ptr(self.alphas[1]), h2, ptr(self.out_kernel),
+                 ptr(self.out_bias), self.T, k, ptr(prep), _stream())
+            self._ids_prep, self._ids_key = prep, key
+        return self._ids_prep
+
+    def forward_ids(self, table, vocab, hist, cand, err=None, out=None, scores=None):
+        """Attention over key = value = table[hist], query = table[cand],
+        mask = hist != 0 (model/din.py:56-80) without materialising [B,T,k]."""
+        B, T = hist.shape
+        k = table.shape[1]
+        if self.out_kernel is None:
+            self.build(T, k)
+        if T != self.T:
+            raise ValueError(f"Attention built for T={self.T} (PReLU alpha is [T,h]); got T={T}")
+        if out is None:
+            out = torch.empty(B, k, dtype=torch.float32, device=self._dev)
+        if scores is None:
+            scores = torch.empty(B, T, dtype=torch.float32, device=self._dev)
+        h1, h2 = self.hidden_units
+        call("rs_din_attention_ids_fwd", ptr(hist), _lib.id_kind(hist), hist.stride(0), ptr(cand),
+             cand.stride(0), T, k, ptr(table), vocab, h1, h2, ptr(self.prepared_ids(k)), ptr(scores), ptr(out), B,
+             ptr(err), _stream())
+        return out
+
     def keras_weights(self):
         out = {}
         for i in range(len(self.kernels)):

@@ -312,10 +312,19 @@ class DIN(TowerMixin, KerasModule):
         hist = _ids_tensor(inputs[self.seq_feats[0]["feat"]], dev)
         B, T = hist.shape
         cand = _ids_tensor(inputs["movie_id"], dev).reshape(B, 1)
-        seq_embed = seq_layer.gather(hist.reshape(B * T, 1), check_ids=check_ids).reshape(B, T, k)
         item_embed = seq_layer.gather(cand, check_ids=check_ids)
-        mask = (hist != 0).to(torch.float32)
-        att_emb = self.att_layer([item_embed, seq_embed, seq_embed, mask])
+        if self.att_layer.out_kernel is None:
+            self.att_layer.build(T, k)
+        if self.att_layer.ids_ok(k):
+            # keys/values read through the ids from the (L2-resident) table
+            att_emb = self.att_layer.forward_ids(seq_layer.table, int(seq_layer.vocab_sizes[0]), hist, cand,
+                                                 err=self._err.t)
+            if check_ids:
+                self._err.check("DIN")
+        else:
+            seq_embed = seq_layer.gather(hist.reshape(B * T, 1), check_ids=check_ids).reshape(B, T, k)
+            mask = (hist != 0).to(torch.float32)
+            att_emb = self.att_layer([item_embed, seq_embed, seq_embed, mask])
         other_k = sum(l.k for l in self.embed_sparse_layers)
         width = 2 * k + other_k + self.dense_num
         emb = torch.empty(B, width, dtype=torch.float32, device=dev)

@@ -455,3 +455,45 @@ def test_embed_cross_fused(gpu, k, L, B, id_dtype):
     bad[B // 2, 4] = vocabs[4]
     with pytest.raises(IndexError):
         m.cross_fused((dense, bad))
+
+
+# ------------------------------------- DIN attention from ids (rs_din_attention_ids_fwd)
+@pytest.mark.parametrize("T,k,h,B,id_dtype", [(100, 8, (80, 40), 2048, np.int64), (10, 8, (80, 40), 5, np.int32),
+                                              (1, 4, (16, 16), 3, np.int64), (33, 16, (128, 64), 21, np.int32),
+                                              (17, 8, (20, 7), 40, np.int32)])
+def test_din_attention_ids(gpu, T, k, h, B, id_dtype):
+    """keys = values = table[hist], query = table[cand], mask = hist != 0;
+    padded positions keep their (id 0) rows in the pooled values, a fully
+    padded row averages them uniformly — as the reference."""
+    from recommender_system_amd import Attention
+    rng = np.random.default_rng(T * k + B)
+    V = 5000
+    table_np = rng.standard_normal((V, k)).astype(np.float32)
+    lens = rng.integers(0, T + 1, size=B)
+    lens[0] = 0
+    hist = rng.integers(1, V, size=(B, T))
+    hist = np.where(np.arange(T)[None, :] < lens[:, None], hist, 0).astype(id_dtype)
+    cand = rng.integers(0, V, size=(B, 1)).astype(id_dtype)
+    layer = Attention(h, "prelu", seed=4)
+    layer.build(T, k)
+    with torch.no_grad():
+        for a in layer.alphas:
+            a.copy_(torch.as_tensor(rng.uniform(-0.5, 0.5, size=tuple(a.shape)), dtype=torch.float32))
+        for b in layer.biases:
+            b.copy_(torch.as_tensor(rng.uniform(-0.1, 0.1, size=tuple(b.shape)), dtype=torch.float32))
+    assert layer.ids_ok(k)
+    table = torch.tensor(table_np, device="cuda")
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    y = layer.forward_ids(table, V, torch.tensor(hist, device="cuda"), torch.tensor(cand, device="cuda"), err=err)
+    torch.cuda.synchronize()
+    key = table_np[hist]
+    q = table_np[cand[:, 0]]
+    mask = (hist != 0).astype(np.float32)
+    ref = O.attention(q, key, key, mask, _att_params(layer), "prelu")
+    assert_scaled_close(y, ref, what="DIN attention from ids")
+    assert err.item() == 0
+    bad = hist.copy()
+    bad[B - 1, 0] = V
+    layer.forward_ids(table, V, torch.tensor(bad, device="cuda"), torch.tensor(cand, device="cuda"), err=err)
+    torch.cuda.synchronize()
+    assert err.item() != 0
