@@ -133,6 +133,7 @@ struct DinArgs {
 };
 
 constexpr int DIN_SPW = 4;  // samples per wave in din_scores
+constexpr int ATT_POOL_TMAX = 1024;
 
 template <int KS>
 __device__ __forceinline__ void din_row(const float* table, int64_t row, int kk, float (&v)[KS]) {
@@ -268,36 +269,48 @@ __global__ __launch_bounds__(256) void din_scores(DinArgs a) {
   if (__any(bad) && lane == 0) flag_error(a.err);
 }
 
-// masked softmax over the T scores and out[b] = sum_t a_t * E[hist_t]
+// masked softmax over the T scores and out[b] = sum_t a_t * E[hist_t].
+// One wave per sample: (1) lanes take positions t = lane + 64i: score, id
+// -> e_t = exp(s_t - max) and the row index into LDS; (2) lanes (position
+// group tg, channel j) sum e_t * E[id_t][j] with independent (L2) loads.
 template <int KIND>
 __global__ __launch_bounds__(256) void din_pool(DinArgs a) {
   typedef Ids<KIND> I;
-  const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= a.batch) return;
+  __shared__ float es[4][ATT_POOL_TMAX];
+  __shared__ int rs_[4][ATT_POOL_TMAX];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b = (int64_t)blockIdx.x * 4 + w;
+  if (b >= a.batch) return;  // wave-uniform; no block barrier below
   const int T = a.g.T, k = a.g.k;
   const float* sc = a.scores + b * T;
   float mx = -INFINITY;
   for (int t = lane; t < T; t += 64) mx = fmaxf(mx, sc[t]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-  // lanes = (position group tg, channel j)
-  const int ntg = 64 / k, j = lane % k, tg = lane / k;
-  float sum = 0.f, acc = 0.f;
-  for (int t = tg; t < T; t += ntg) {
+  float sum = 0.f;
+  for (int t = lane; t < T; t += 64) {
     const float e = expf(sc[t] - mx);
     int64_t id;
     const bool ok = I::decode(I::load(a.hist, b * a.hist_stride + t), a.vocab, id);
-    const float v = ok ? a.table[id * k + j] : 0.f;
+    es[w][t] = ok ? e : 0.f;  // an OOR id (flagged by din_scores) contributes a zero row
+    rs_[w][t] = ok ? (int)id : 0;
     sum += e;
-    acc = fmaf(e, v, acc);
   }
-  // reduce over the position groups (lanes j, j+k, j+2k, ...)
-  for (int o = k; o < 64; o <<= 1) {
-    sum += __shfl_xor(sum, o);
-    acc += __shfl_xor(acc, o);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const int ntg = 64 / k, j = lane % k, tg = lane / k;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int t = tg;
+  for (; t + 3 * ntg < T; t += 4 * ntg) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = fmaf(es[w][t + u * ntg], a.table[(int64_t)rs_[w][t + u * ntg] * k + j], acc[u]);
   }
-  if (lane < k) a.out[b * k + lane] = acc / sum;
+  for (; t < T; t += ntg) acc[0] = fmaf(es[w][t], a.table[(int64_t)rs_[w][t] * k + j], acc[0]);
+  float v = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  for (int o = k; o < 64; o <<= 1) v += __shfl_xor(v, o);
+  if (lane < k) a.out[b * k + lane] = v / sum;
 }
 
 template <int KS, int HT1M, int HT2M, int KIND>
@@ -339,6 +352,7 @@ extern "C" int rs_din_attention_ids_fwd(const void* hist, int id_kind, int64_t h
   RS_REQUIRE(rs_din_prepared_size(T, k, H1, H2) > 0,
              "rs_din_attention_ids_fwd: need k in {4,8,16}, H1 <= 128, H2 <= 64");
   RS_REQUIRE(hist && cand && table && prepared && scores && out, "rs_din_attention_ids_fwd: null pointer");
+  RS_REQUIRE(T <= ATT_POOL_TMAX && vocab < (1ll << 31), "rs_din_attention_ids_fwd: T > %d or vocab >= 2^31", ATT_POOL_TMAX);
   RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32 && vocab >= 1 && batch >= 0 && hist_stride >= T,
              "rs_din_attention_ids_fwd: bad ids / shape");
   RS_REQUIRE((uintptr_t)table % 16 == 0, "rs_din_attention_ids_fwd: table must be 16-B aligned");
