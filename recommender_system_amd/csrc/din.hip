@@ -126,13 +126,31 @@ struct DinArgs {
   int64_t vocab;
   const float* prep;
   DinGeom g;
+  int64_t spc;    // samples per workgroup (din_scores)
   float* scores;  // [B, T] workspace
   float* out;     // [B, k]
   int64_t batch;
   int* err;
+  unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_din_set_dbg)
 };
+#define DIN_STAMP(i)                                                                                   \
+  do {                                                                                                 \
+    if (a.dbg && (threadIdx.x & 63) == 0)                                                              \
+      a.dbg[(((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6)) * 8 + (i)] =     \
+          __builtin_amdgcn_s_memtime();                                                                \
+  } while (0)
 
-constexpr int DIN_SPW = 4;  // samples per wave in din_scores
+
+// Keras PReLU max(0,x) + alpha*min(0,x) == x * (x < 0 ? alpha : 1) (one
+// rounding either way).  The slope is chosen with the sign bit as a mask
+// (v_ashrrev + v_bfi), then one multiply: fmaxf/fminf would add a
+// NaN-canonicalising v_max per element, and a compare+select adds VCC-hazard
+// nops between the MFMAs.
+__device__ __forceinline__ float prelu(float x, float alpha) {
+  const int m = __float_as_int(x) >> 31;  // all ones when x < 0 (sign bit)
+  const int slope = (m & __float_as_int(alpha)) | (~m & 0x3f800000);
+  return x * __int_as_float(slope);
+}
 constexpr int ATT_POOL_TMAX = 1024;
 
 template <int KS>
@@ -150,10 +168,14 @@ __device__ __forceinline__ void din_row(const float* table, int64_t row, int kk,
   }
 }
 
-template <int KS, int HT1M, int HT2M, int KIND>
-__global__ __launch_bounds__(256) void din_scores(DinArgs a) {
+// HT1M/HT2M are the EXACT tile counts when EXACT (the reference's (80, 40) is
+// (5, 3)): every guard folds away and the body is one straight MFMA stream;
+// otherwise they are upper bounds checked at run time.
+template <int KS, int HT1M, int HT2M, int KIND, bool EXACT>
+__global__ __launch_bounds__(256, 4) void din_scores(DinArgs a) {  // 4 waves/SIMD: all 896 workgroups resident
   typedef Ids<KIND> I;
   const DinGeom& g = a.g;
+  const int HT1 = EXACT ? HT1M : g.HT1, HT2 = EXACT ? HT2M : g.HT2;
   __shared__ float a1s[16][HT1M * 16 + 4];
   __shared__ float a2s[16][HT2M * 16 + 4];
   __shared__ floatx4 w2s[HT2M * HT1M * 64];
@@ -161,47 +183,98 @@ __global__ __launch_bounds__(256) void din_scores(DinArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, kg = lane >> 4;
   const int t0 = blockIdx.x * 16;
+  DIN_STAMP(0);
+  if (a.dbg && (threadIdx.x & 63) == 0)
+    a.dbg[(((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6)) * 8 + 6] =
+        __builtin_amdgcn_s_memrealtime();
 
   // ---- stage the tile's alphas and the W2^T image (shared by 16 samples)
-  const float* pa1 = a.prep + g.a1 + (int64_t)t0 * (g.HT1 * 16);
-  const float* pa2 = a.prep + g.a2 + (int64_t)t0 * (g.HT2 * 16);
-  for (int i = threadIdx.x; i < 16 * g.HT1 * 16; i += 256) a1s[i / (g.HT1 * 16)][i % (g.HT1 * 16)] = pa1[i];
-  for (int i = threadIdx.x; i < 16 * g.HT2 * 16; i += 256) a2s[i / (g.HT2 * 16)][i % (g.HT2 * 16)] = pa2[i];
+  const float* pa1 = a.prep + g.a1 + (int64_t)t0 * (HT1 * 16);
+  const float* pa2 = a.prep + g.a2 + (int64_t)t0 * (HT2 * 16);
+  // all loads first, then the LDS stores (one L2 round trip, not one per
+  // iteration of a load->store loop)
   const floatx4* pw2 = reinterpret_cast<const floatx4*>(a.prep + g.w2);
-  for (int i = threadIdx.x; i < g.HT2 * g.HT1 * 64; i += 256) w2s[i] = pw2[i];
+  {
+    constexpr int N1 = (16 * HT1M * 16 + 255) / 256, N2 = (16 * HT2M * 16 + 255) / 256;
+    constexpr int NW2 = (HT2M * HT1M * 64 + 255) / 256;
+    float v1[N1], v2[N2];
+    floatx4 vw[NW2];
+#pragma unroll
+    for (int u = 0; u < N1; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      v1[u] = i < 16 * HT1 * 16 ? pa1[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < N2; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      v2[u] = i < 16 * HT2 * 16 ? pa2[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < NW2; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      vw[u] = i < HT2 * HT1 * 64 ? pw2[i] : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < N1; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      if (i < 16 * HT1 * 16) a1s[i / (HT1 * 16)][i % (HT1 * 16)] = v1[u];
+    }
+#pragma unroll
+    for (int u = 0; u < N2; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      if (i < 16 * HT2 * 16) a2s[i / (HT2 * 16)][i % (HT2 * 16)] = v2[u];
+    }
+#pragma unroll
+    for (int u = 0; u < NW2; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      if (i < HT2 * HT1 * 64) w2s[i] = vw[u];
+    }
+  }
 
-  // ---- per-lane constants: layer-1 images, biases, w3
-  float wkd[HT1M][KS], wpv[HT1M][KS], wqd[HT1M][KS], b1v[HT1M][4], b2v[HT2M][4], w3v[HT2M][4];
+  // biases and w3 in LDS (float4 per lane and tile at use): registers go to
+  // the per-lane layer-1 images instead, keeping 4 waves/SIMD
+  __shared__ floatx4 b1s[HT1M * 4], b2s[HT2M * 4], w3s[HT2M * 4];
+  if (threadIdx.x < HT1M * 16) reinterpret_cast<float*>(b1s)[threadIdx.x] = threadIdx.x < HT1 * 16 ? a.prep[g.b1 + threadIdx.x] : 0.f;
+  if (threadIdx.x < HT2M * 16) {
+    reinterpret_cast<float*>(b2s)[threadIdx.x] = threadIdx.x < HT2 * 16 ? a.prep[g.b2 + threadIdx.x] : 0.f;
+    reinterpret_cast<float*>(w3s)[threadIdx.x] = threadIdx.x < HT2 * 16 ? a.prep[g.w3 + threadIdx.x] : 0.f;
+  }
+  // ---- per-lane constants: layer-1 images
+  float wkd[HT1M][KS], wpv[HT1M][KS], wqd[HT1M][KS];
 #pragma unroll
   for (int ht = 0; ht < HT1M; ++ht) {
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int64_t o = (int64_t)(ht * KS + s) * 64 + lane;
-      const bool on = ht < g.HT1;
+      const bool on = ht < HT1;
       wkd[ht][s] = on ? a.prep[g.wkd + o] : 0.f;
       wpv[ht][s] = on ? a.prep[g.wp + o] : 0.f;
       wqd[ht][s] = on ? a.prep[g.wqd + o] : 0.f;
     }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) b1v[ht][r] = ht < g.HT1 ? a.prep[g.b1 + 16 * ht + 4 * kg + r] : 0.f;
   }
-#pragma unroll
-  for (int ht = 0; ht < HT2M; ++ht)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const bool on = ht < g.HT2;
-      b2v[ht][r] = on ? a.prep[g.b2 + 16 * ht + 4 * kg + r] : 0.f;
-      w3v[ht][r] = on ? a.prep[g.w3 + 16 * ht + 4 * kg + r] : 0.f;
-    }
   const float b3 = a.prep[g.b3];
   __syncthreads();
+  DIN_STAMP(1);
 
   const int t = t0 + col;
   const bool tv = t < g.T;
   bool bad = false;
-  for (int si = 0; si < DIN_SPW; ++si) {
-    const int64_t b = ((int64_t)blockIdx.y * 4 + w) * DIN_SPW + si;  // wave-uniform
-    if (b >= a.batch) break;
+  // The workgroup owns samples [c0, c1) of its tile; its 4 waves pull them
+  // from an LDS counter (the next index is claimed while the current sample
+  // is computed), so a wave that runs ahead takes more and the SIMDs of the
+  // CU finish together.
+  __shared__ int wctr;
+  const int64_t c0 = (int64_t)blockIdx.y * a.spc, c1 = min(c0 + a.spc, a.batch);
+  if (threadIdx.x == 0) wctr = 4;
+  __syncthreads();
+  int64_t nb = c0 + w;
+  int cnt = 0;
+  for (;;) {
+    const int64_t b = nb;  // wave-uniform
+    if (b >= c1) break;
+    int nxt = 0;
+    if (lane == 0) nxt = atomicAdd(&wctr, 1);
+    nb = c0 + __builtin_amdgcn_readfirstlane(nxt);
     // candidate (query) row and this lane's behaviour row
     int64_t cid, hid;
     const typename I::raw_t craw = I::load(a.cand, b * a.cand_stride);
@@ -223,8 +296,8 @@ __global__ __launch_bounds__(256) void din_scores(DinArgs a) {
     float y1[HT1M][4];
 #pragma unroll
     for (int ht = 0; ht < HT1M; ++ht) {
-      if (ht < g.HT1) {
-        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      if (ht < HT1) {
+        floatx4 acc = b1s[ht * 4 + kg];  // bias as the C input
 #pragma unroll
         for (int s = 0; s < KS; ++s) acc = mfma16x16x4(fmaf(q[s], wpv[ht][s], wkd[ht][s]), kv[s], acc);
 #pragma unroll
@@ -232,8 +305,7 @@ __global__ __launch_bounds__(256) void din_scores(DinArgs a) {
         const floatx4 al = *reinterpret_cast<const floatx4*>(&a1s[col][16 * ht + 4 * kg]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float x = acc[r] + b1v[ht][r];
-          y1[ht][r] = fmaxf(x, 0.f) + al[r] * fminf(x, 0.f);
+          y1[ht][r] = prelu(acc[r], al[r]);
         }
       } else {
 #pragma unroll
@@ -244,12 +316,13 @@ __global__ __launch_bounds__(256) void din_scores(DinArgs a) {
     float part = 0.f;
 #pragma unroll
     for (int ht2 = 0; ht2 < HT2M; ++ht2) {
-      if (ht2 < g.HT2) {
-        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      if (ht2 < HT2) {
+        floatx4 acc = b2s[ht2 * 4 + kg];
+        const floatx4 w3v = w3s[ht2 * 4 + kg];
 #pragma unroll
         for (int ht = 0; ht < HT1M; ++ht) {
-          if (ht < g.HT1) {
-            const floatx4 wa = w2s[(ht2 * g.HT1 + ht) * 64 + lane];
+          if (ht < HT1) {
+            const floatx4 wa = w2s[(ht2 * HT1 + ht) * 64 + lane];
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc = mfma16x16x4(wa[r], y1[ht][r], acc);
           }
@@ -257,16 +330,20 @@ __global__ __launch_bounds__(256) void din_scores(DinArgs a) {
         const floatx4 al = *reinterpret_cast<const floatx4*>(&a2s[col][16 * ht2 + 4 * kg]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float x = acc[r] + b2v[ht2][r];
-          part = fmaf(fmaxf(x, 0.f) + al[r] * fminf(x, 0.f), w3v[ht2][r], part);
+          part = fmaf(prelu(acc[r], al[r]), w3v[r], part);
         }
       }
     }
     part += __shfl_xor(part, 16);
     part += __shfl_xor(part, 32);
     if (kg == 0 && tv) a.scores[b * g.T + t] = masked ? -4294967296.0f : part + b3;
+    if (cnt < 4) DIN_STAMP(2 + cnt);
+    ++cnt;
   }
   if (__any(bad) && lane == 0) flag_error(a.err);
+  if (a.dbg && (threadIdx.x & 63) == 0)
+    a.dbg[(((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6)) * 8 + 7] =
+        __builtin_amdgcn_s_memrealtime();
 }
 
 // masked softmax over the T scores and out[b] = sum_t a_t * E[hist_t].
@@ -313,22 +390,36 @@ __global__ __launch_bounds__(256) void din_pool(DinArgs a) {
   if (lane < k) a.out[b * k + lane] = v / sum;
 }
 
-template <int KS, int HT1M, int HT2M, int KIND>
+template <int KS, int HT1M, int HT2M, int KIND, bool EXACT>
 static void launch_din(const DinArgs& a, hipStream_t st) {
-  const dim3 grid(a.g.NTT, (unsigned)((a.batch + 4 * DIN_SPW - 1) / (4 * DIN_SPW)));
-  din_scores<KS, HT1M, HT2M, KIND><<<grid, 256, 0, st>>>(a);
-  din_pool<KIND><<<(unsigned)((a.batch + 3) / 4), 256, 0, st>>>(a);
+  // One resident round: 4 workgroups per CU (4 waves/SIMD), the batch split
+  // evenly over (position tile, sample chunk).
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu < 1) n_cu = 256;
+  }
+  DinArgs b = a;
+  const int64_t per_tile = std::max<int64_t>(1, std::min<int64_t>((4 * n_cu) / a.g.NTT, (a.batch + 3) / 4));
+  b.spc = (a.batch + per_tile - 1) / per_tile;
+  const dim3 grid(a.g.NTT, (unsigned)((a.batch + b.spc - 1) / b.spc));
+  din_scores<KS, HT1M, HT2M, KIND, EXACT><<<grid, 256, 0, st>>>(b);
+  din_pool<KIND><<<(unsigned)((a.batch + 3) / 4), 256, 0, st>>>(b);
 }
 
 template <int KS, int KIND>
 static void launch_din_h(const DinArgs& a, hipStream_t st) {
-  if (a.g.HT1 <= 5 && a.g.HT2 <= 3) launch_din<KS, 5, 3, KIND>(a, st);
-  else launch_din<KS, 8, 4, KIND>(a, st);
+  if (a.g.HT1 == 5 && a.g.HT2 == 3) launch_din<KS, 5, 3, KIND, true>(a, st);  // reference (80, 40)
+  else launch_din<KS, 8, 4, KIND, false>(a, st);
 }
 
 }  // namespace rs
 
 using namespace rs;
+
+static unsigned long long* g_din_dbg = nullptr;
+extern "C" void rs_diag_din_set_dbg(unsigned long long* p) { g_din_dbg = p; }
 
 extern "C" int64_t rs_din_prepared_size(int T, int k, int H1, int H2) {
   if (T < 1 || (k != 4 && k != 8 && k != 16) || H1 < 1 || H1 > 128 || H2 < 1 || H2 > 64) return -1;
@@ -358,7 +449,7 @@ extern "C" int rs_din_attention_ids_fwd(const void* hist, int id_kind, int64_t h
   RS_REQUIRE((uintptr_t)table % 16 == 0, "rs_din_attention_ids_fwd: table must be 16-B aligned");
   if (batch == 0) return RS_OK;
   DinArgs a{hist, hist_stride, cand, cand_stride, table, vocab, prepared, din_geom(T, k, H1, H2),
-            scores, out, batch, err_flag};
+            0, scores, out, batch, err_flag, g_din_dbg};
   hipStream_t st = as_stream(stream);
   with_id_kind(id_kind, [&](auto K) {
     constexpr int KIND = decltype(K)::value;

@@ -664,6 +664,8 @@ class Attention(KerasModule):
             out = torch.empty(B, k, dtype=torch.float32, device=self._dev)
         if scores is None:
             scores = torch.empty(B, T, dtype=torch.float32, device=self._dev)
+        if scores.numel() < B * T:
+            raise ValueError("forward_ids: scores workspace needs B*T elements")
         h1, h2 = self.hidden_units
         call("rs_din_attention_ids_fwd", ptr(hist), _lib.id_kind(hist), hist.stride(0), ptr(cand),
              cand.stride(0), T, k, ptr(table), vocab, h1, h2, ptr(self.prepared_ids(k)), ptr(scores), ptr(out), B,
