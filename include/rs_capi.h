@@ -289,6 +289,25 @@ int rs_shard_bucketize(const void* ids, int id_kind, int64_t id_stride,
                        int world, int32_t* counts, int32_t* perm,
                        int32_t* send_rows, void* workspace, int* err_flag,
                        rs_stream_t stream);
+
+/* Fixed-capacity ("slotted") variant for a host-sync-free exchange: every
+ * (rank -> owner) message is exactly `cap` slots, so both all-to-alls have
+ * equal, host-known splits.  send_slots [world*cap]: slots not used by this
+ * step keep their previous content (fill the buffer with -1 once, when it is
+ * allocated: -1 is served as a zero row, a stale slot as a valid row of the
+ * owner's shard that no lookup reads); slot_of [B*F]: the slot of lookup
+ * b*F+c, or -1 when its owner's slots overflowed (*overflow_flag set; redo the
+ * step with the exact protocol) or its id is out of range (*err_flag set).
+ * The returned rows are then addressed by slot_of as int32 ids of a single
+ * [world*cap, k] table: rs_embed_fm_fwd(ids = slot_of, offsets 0, vocab
+ * world*cap) computes the FM straight from the exchange buffer.            */
+int rs_shard_slot_bucketize(const void* ids, int id_kind, int64_t id_stride,
+                            const int64_t* field_offsets,
+                            const int64_t* field_vocab, int n_fields,
+                            int64_t batch, int64_t rows_per_rank, int world,
+                            int cap, int32_t* counts, int32_t* slot_of,
+                            int32_t* send_slots, void* workspace, int* err_flag,
+                            int* overflow_flag, rs_stream_t stream);
 int rs_gather_rows(const float* table, int64_t n_rows, int k,
                    const int32_t* rows, int64_t n, float* out, int* err_flag,
                    rs_stream_t stream);

@@ -53,6 +53,7 @@ SIGNATURES = {
     "rs_dice_fwd": (I, [P, L, P, P, F, P, P, L, L, I, P]),
     "rs_shard_workspace_size": (L, [L, I]),
     "rs_shard_bucketize": (I, [P, I, L, P, P, I, L, L, I, P, P, P, P, P, P]),
+    "rs_shard_slot_bucketize": (I, [P, I, L, P, P, I, L, L, I, I, P, P, P, P, P, P, P]),
     "rs_gather_rows": (I, [P, L, I, P, L, P, P, P]),
     "rs_unpermute_rows": (I, [P, P, I, L, P, P]),
     "rs_rows_fm_fwd": (I, [P, P, L, I, I, I, P, P, I, P, L, P]),

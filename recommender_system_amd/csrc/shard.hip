@@ -13,7 +13,7 @@
 
 namespace rs {
 
-constexpr int SH_CHUNK = 1024;  // lookups per workgroup
+constexpr int SH_CHUNK = 256;  // lookups per workgroup (one per thread)
 constexpr int SH_THREADS = 256;
 constexpr int SH_MAXW = 64;
 
@@ -28,10 +28,11 @@ struct ShardArgs {
   int64_t rpr;
   int world;
   int* err;
+  double inv_rpr;
 };
 
 __device__ __forceinline__ int shard_owner(const ShardArgs& a, int64_t i, int64_t& local) {
-  const int64_t b = i / a.F;
+  const int64_t b = (int64_t)((uint32_t)i / (uint32_t)a.F);  // n < 2^31
   const int c = (int)(i - b * a.F);
   const int64_t off = b * a.id_stride + c;
   int64_t id;
@@ -51,7 +52,11 @@ __device__ __forceinline__ int shard_owner(const ShardArgs& a, int64_t i, int64_
     return 0;
   }
   const int64_t row = a.offs[c] + id;
-  int o = (int)(row / a.rpr);
+  // owner = row / rpr without a 64-bit integer division: an fp64 quotient
+  // (exact to < 1 for rows < 2^52) and a +-1 fix-up
+  int o = (int)((double)row * a.inv_rpr);
+  if ((int64_t)o * a.rpr > row) --o;
+  else if ((int64_t)(o + 1) * a.rpr <= row) ++o;
   if (o >= a.world) o = a.world - 1;
   local = row - (int64_t)o * a.rpr;
   return o;
@@ -74,29 +79,52 @@ __global__ __launch_bounds__(SH_THREADS) void shard_hist(ShardArgs a, int32_t* h
 }
 
 // counts[o] = sum_b hist[b][o]; hist[b][o] <- base(o) + sum_{b'<b} hist[b'][o]
-__global__ void shard_scan(int32_t* hist, int nblocks, int world, int32_t* counts) {
+// base(o) = sum_{p<o} counts[p] (packed) or o * cap (slotted, cap > 0).
+// One 256-thread workgroup: wave w owns owners w, w+4, ...; each owner's
+// column is reduced / scanned 64 blocks at a time (independent loads, a
+// wave-level inclusive scan, a running carry) — no serial per-block chain.
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(256) void shard_scan(int32_t* hist, int nblocks, int world, int32_t* counts, int cap) {
   __shared__ int tot[SH_MAXW];
-  const int o = threadIdx.x;
-  if (o < world) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int o = w; o < world; o += 4) {
     int s = 0;
-    for (int b = 0; b < nblocks; ++b) s += hist[(int64_t)b * world + o];
-    tot[o] = s;
-    counts[o] = s;
+    for (int b = lane; b < nblocks; b += 64) s += hist[(int64_t)b * world + o];
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d);
+    if (lane == 0) {
+      tot[o] = s;
+      counts[o] = s;
+    }
   }
   __syncthreads();
-  if (o < world) {
-    int base = 0;
-    for (int p = 0; p < o; ++p) base += tot[p];
-    for (int b = 0; b < nblocks; ++b) {
-      const int v = hist[(int64_t)b * world + o];
-      hist[(int64_t)b * world + o] = base;
-      base += v;
+  for (int o = w; o < world; o += 4) {
+    int carry = 0;
+    if (cap > 0) carry = o * cap;
+    else
+      for (int p = 0; p < o; ++p) carry += tot[p];
+    for (int b0 = 0; b0 < nblocks; b0 += 64) {
+      const int b = b0 + lane;
+      const int v = b < nblocks ? hist[(int64_t)b * world + o] : 0;
+      const int inc = wave_incl_scan(v, lane);
+      if (b < nblocks) hist[(int64_t)b * world + o] = carry + inc - v;
+      carry += __shfl(inc, 63);
     }
   }
 }
 
+// cap > 0 (slotted): lookup i goes to slot o*cap + rank-within-owner; ranks
+// >= cap (and out-of-range ids) get perm[i] = -1 and raise *overflow / *err.
 __global__ __launch_bounds__(SH_THREADS) void shard_place(ShardArgs a, const int32_t* hist, int32_t* perm,
-                                                          int32_t* send_rows) {
+                                                          int32_t* send_rows, int cap, int* overflow) {
   __shared__ int running[SH_MAXW];
   __shared__ int wcnt[SH_THREADS / 64][SH_MAXW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -124,8 +152,13 @@ __global__ __launch_bounds__(SH_THREADS) void shard_place(ShardArgs a, const int
     if (act) {
       int pos = running[o] + rank;
       for (int ww = 0; ww < w; ++ww) pos += wcnt[ww][o];
-      perm[i] = pos;
-      send_rows[pos] = (int32_t)local;
+      if (cap > 0 && (pos - o * cap >= cap || local < 0)) {
+        if (local >= 0) flag_error(overflow);
+        perm[i] = -1;
+      } else {
+        perm[i] = pos;
+        send_rows[pos] = (int32_t)local;
+      }
     }
     __syncthreads();
     for (int oo = threadIdx.x; oo < a.world; oo += blockDim.x) {
@@ -206,7 +239,7 @@ extern "C" int rs_shard_bucketize(const void* ids, int id_kind, int64_t id_strid
   RS_REQUIRE(rows_per_rank < ((int64_t)1 << 31), "rs_shard_bucketize: shard rows must fit int32");
   hipStream_t st = as_stream(stream);
   ShardArgs a{ids, id_kind, id_stride, field_offsets, field_vocab, n_fields, batch * n_fields, rows_per_rank, world,
-              err_flag};
+              err_flag, 1.0 / (double)rows_per_rank};
   const int nb = (int)((a.n + SH_CHUNK - 1) / SH_CHUNK);
   int32_t* hist = static_cast<int32_t*>(workspace);
   if (a.n == 0) {
@@ -214,9 +247,36 @@ extern "C" int rs_shard_bucketize(const void* ids, int id_kind, int64_t id_strid
     return launch_status("rs_shard_bucketize");
   }
   shard_hist<<<nb, SH_THREADS, 0, st>>>(a, hist);
-  shard_scan<<<1, SH_MAXW, 0, st>>>(hist, nb, world, counts);
-  shard_place<<<nb, SH_THREADS, 0, st>>>(a, hist, perm, send_rows);
+  shard_scan<<<1, 256, 0, st>>>(hist, nb, world, counts, 0);
+  shard_place<<<nb, SH_THREADS, 0, st>>>(a, hist, perm, send_rows, 0, nullptr);
   return launch_status("rs_shard_bucketize");
+}
+
+extern "C" int rs_shard_slot_bucketize(const void* ids, int id_kind, int64_t id_stride,
+                                       const int64_t* field_offsets, const int64_t* field_vocab, int n_fields,
+                                       int64_t batch, int64_t rows_per_rank, int world, int cap, int32_t* counts,
+                                       int32_t* slot_of, int32_t* send_slots, void* workspace, int* err_flag,
+                                       int* overflow_flag, rs_stream_t stream) {
+  RS_REQUIRE(ids && field_offsets && field_vocab && counts && slot_of && send_slots && workspace && overflow_flag,
+             "rs_shard_slot_bucketize: null pointer");
+  RS_REQUIRE(world >= 1 && world <= SH_MAXW && rows_per_rank >= 1 && n_fields >= 1 && batch >= 0 && cap >= 1,
+             "rs_shard_slot_bucketize: bad shape (1 <= world <= %d, cap >= 1)", SH_MAXW);
+  RS_REQUIRE(batch * n_fields < ((int64_t)1 << 31) && (int64_t)world * cap < ((int64_t)1 << 31),
+             "rs_shard_slot_bucketize: too many lookups / slots");
+  RS_REQUIRE(rows_per_rank < ((int64_t)1 << 31), "rs_shard_slot_bucketize: shard rows must fit int32");
+  hipStream_t st = as_stream(stream);
+  ShardArgs a{ids, id_kind, id_stride, field_offsets, field_vocab, n_fields, batch * n_fields, rows_per_rank, world,
+              err_flag, 1.0 / (double)rows_per_rank};
+  const int nb = (int)((a.n + SH_CHUNK - 1) / SH_CHUNK);
+  int32_t* hist = static_cast<int32_t*>(workspace);
+  if (a.n == 0) {
+    (void)hipMemsetAsync(counts, 0, world * sizeof(int32_t), st);
+    return launch_status("rs_shard_slot_bucketize");
+  }
+  shard_hist<<<nb, SH_THREADS, 0, st>>>(a, hist);
+  shard_scan<<<1, 256, 0, st>>>(hist, nb, world, counts, cap);
+  shard_place<<<nb, SH_THREADS, 0, st>>>(a, hist, slot_of, send_slots, cap, overflow_flag);
+  return launch_status("rs_shard_slot_bucketize");
 }
 
 extern "C" int rs_gather_rows(const float* table, int64_t n_rows, int k, const int32_t* rows, int64_t n, float* out,

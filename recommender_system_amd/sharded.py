@@ -6,14 +6,22 @@ field_offsets[c] + id) split into contiguous row blocks, one per rank
 (owner = row // rows_per_rank); dense parameters (w0, w1, v) replicated.
 Per step and rank (B local samples, data parallel):
 
-  1. rs_shard_bucketize  -> per-owner counts, owner-major permutation, local
-                            row ids to request (stable, deterministic)
-  2. all_to_all(counts)  -> how many rows every peer asks of me   (RCCL)
-  3. all_to_all(rows ids)                                          (RCCL)
-  4. rs_gather_rows      -> serve the requested rows from my shard
-  5. all_to_all(rows)    -> my lookups' rows, owner-major          (RCCL)
-  6. rs_unpermute_rows   -> back to sample order [B*F, k]
-  7. rs_rows_fm_fwd      -> FM logit (the same MFMA kernel as the fused path)
+  1. rs_shard_slot_bucketize -> every lookup gets a slot in a fixed-capacity
+                               per-owner message (cap = 1.15 n/world + 64,
+                               stable, deterministic); local row ids to request
+  2. all_to_all(slots)      -> the row ids every peer asks of me    (RCCL)
+  3. rs_gather_rows         -> serve them from my shard (-1 -> zero row)
+  4. all_to_all(rows)       -> my lookups' rows, slot-addressed     (RCCL)
+  5. rs_embed_fm_fwd        -> FM logit straight from the exchange buffer
+                               (ids = slot of each lookup: the headline kernel)
+
+Equal, host-known splits: no host synchronisation inside the step, so the
+whole step is enqueued asynchronously.  A slot overflow (an owner receiving
+more than cap lookups from one rank: ~20 sigma for uniform ids) raises a
+device flag; ``forward(check=True)`` then recomputes the step with the exact
+protocol (``lookup``: counts all-to-all, one host sync, variable splits,
+rs_shard_bucketize / rs_unpermute_rows / rs_rows_fm_fwd), so the result is
+always exact.
 
 Collectives go through torch.distributed (backend "nccl" = RCCL over xGMI on
 ROCm; "gloo" in the CPU tests).  On an 8-GPU MI355X node every peer pair has
@@ -54,6 +62,41 @@ class HipShardOps:
              rows_per_rank, world, ptr(counts), ptr(perm), ptr(send_rows), ptr(self._ws), ptr(self.err),
              _lib.stream())
         return counts, perm, send_rows
+
+    def slot_bucketize(self, ids, offsets, vocab, rows_per_rank, world, cap, bufs):
+        B, F = ids.shape
+        n = B * F
+        if bufs.get("ws_n") != (n, world):
+            wsz = _lib.lib().rs_shard_workspace_size(n, world)
+            if self._ws is None or self._ws.numel() < wsz:
+                self._ws = torch.empty(wsz, dtype=torch.uint8, device=self.device)
+            bufs["ws_n"] = (n, world)
+        call("rs_shard_slot_bucketize", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(offsets), ptr(vocab), F, B,
+             rows_per_rank, world, cap, ptr(bufs["counts"]), ptr(bufs["slot_of"]), ptr(bufs["send"]), ptr(self._ws),
+             ptr(self.err), ptr(bufs["overflow"]), _lib.stream())
+        return bufs["slot_of"], bufs["send"]
+
+    def gather_rows_into(self, table, rows, out):
+        call("rs_gather_rows", ptr(table), table.shape[0], table.shape[1], ptr(rows), rows.numel(), ptr(out),
+             ptr(self.err), _lib.stream())
+        return out
+
+    def slots_fm(self, got, slot_of, dense, n_fields, k, prepared, w0, kfm, bufs):
+        """FM logit with lookup (b, c)'s row at got[slot_of[b*F + c]]: the
+        headline kernel with ids = slots, zero field offsets, vocab = #slots."""
+        B = dense.shape[0]
+        logit = torch.empty(B, 1, dtype=torch.float32, device=self.device)
+        call("rs_embed_fm_fwd", ptr(slot_of), _lib.ID_I32, n_fields, ptr(dense), dense.stride(0), dense.shape[1],
+             ptr(got), ptr(bufs["zoff"]), ptr(bufs["nslots"]), n_fields, k, ptr(prepared), ptr(w0), kfm, ptr(logit),
+             None, B, ptr(bufs["overflow"]), _lib.stream())
+        return logit
+
+    def flags(self, bufs):
+        """[out-of-range id seen, slot overflow seen] (device tensor; resets)."""
+        v = torch.stack([self.err[0], bufs["overflow"][0]]).clamp_(max=1)
+        self.err.zero_()
+        bufs["overflow"].zero_()
+        return v
 
     def gather_rows(self, table, rows):
         out = torch.empty(rows.numel(), table.shape[1], dtype=torch.float32, device=self.device)
@@ -122,7 +165,53 @@ class ShardedEmbeddingFM:
         call("rs_fm_prepare", ptr(self.w1), ptr(self.v), self.nd, self.F, self.k, self.kfm, ptr(self.prepared),
              _lib.stream())
 
-    # -- the exchange
+    # -- the fixed-capacity exchange (default)
+    def capacity(self, n):
+        """Slots per (rank -> owner) message for n local lookups."""
+        if self.world == 1:
+            return max(n, 1)
+        return min(n, ((int(math.ceil(1.15 * n / self.world)) + 64 + 63) // 64) * 64)
+
+    def _bufs(self, B):
+        bufs = getattr(self, "_slot_bufs", None)
+        if bufs is None or bufs["B"] != B:
+            n = B * self.F
+            cap = self.capacity(n)
+            W, dev = self.world, self.device
+            bufs = {"B": B, "cap": cap,
+                    "counts": torch.empty(W, dtype=torch.int32, device=dev),
+                    "slot_of": torch.empty(n, dtype=torch.int32, device=dev),
+                    "send": torch.full((W * cap,), -1, dtype=torch.int32, device=dev),  # -1 once (rs_capi.h)
+                    "recv": torch.empty(W * cap, dtype=torch.int32, device=dev),
+                    "reply": torch.empty(W * cap, self.k, dtype=torch.float32, device=dev),
+                    "got": torch.empty(W * cap, self.k, dtype=torch.float32, device=dev),
+                    "overflow": torch.zeros(1, dtype=torch.int32, device=dev),
+                    "zoff": torch.zeros(self.F, dtype=torch.int64, device=dev),
+                    "nslots": torch.full((self.F,), W * cap, dtype=torch.int64, device=dev)}
+            self._slot_bufs = bufs
+        return bufs
+
+    def exchange_slots(self, ids):
+        """Steps 1-4: returns (got [world*cap, k], slot_of [B*F]); the row of
+        lookup j is got[slot_of[j]] (slot_of = -1: overflow / bad id)."""
+        B = ids.shape[0]
+        bufs = self._bufs(B)
+        slot_of, send = self.ops.slot_bucketize(ids, self.offsets, self.vocab, self.rows_per_rank, self.world,
+                                                bufs["cap"], bufs)
+        if self.world == 1:
+            recv = send
+        else:
+            recv = bufs["recv"]
+            dist.all_to_all_single(recv, send, group=self.group)
+        reply = self.ops.gather_rows_into(self.table_shard, recv, bufs["reply"])
+        if self.world == 1:
+            got = reply
+        else:
+            got = bufs["got"]
+            dist.all_to_all_single(got, reply, group=self.group)
+        return got, slot_of
+
+    # -- the exact exchange (fallback after an overflow, and the reference)
     def lookup(self, ids):
         """[B*F, k] embedding rows of the local batch in sample order."""
         counts, perm, send_rows = self.ops.bucketize(ids, self.offsets, self.vocab, self.rows_per_rank, self.world)
@@ -140,8 +229,27 @@ class ShardedEmbeddingFM:
         dist.all_to_all_single(got, reply, send_split, recv_split, group=self.group)
         return self.ops.unpermute(got, perm)
 
-    def forward(self, dense, ids):
+    def forward_exact(self, dense, ids):
         emb = self.lookup(ids)
         return self.ops.rows_fm(emb, dense, self.F, self.k, self.prepared, self.w0, self.kfm)
+
+    def forward(self, dense, ids, check=True):
+        """FM logit [B,1] of the local batch.  check=True: one host sync at the
+        end of the step; a slot overflow is redone exactly, a bad id raises."""
+        got, slot_of = self.exchange_slots(ids)
+        bufs = self._bufs(ids.shape[0])
+        logit = self.ops.slots_fm(got, slot_of, dense, self.F, self.k, self.prepared, self.w0, self.kfm, bufs)
+        if check:
+            # collective decision: every rank must take the same branch (the
+            # exact fallback runs collectives; a lone raise would strand peers)
+            f = self.ops.flags(bufs)
+            if self.world > 1:
+                dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
+            bad, overflow = (bool(x) for x in f.tolist())
+            if bad:
+                raise IndexError("sharded lookup: embedding id out of range")
+            if overflow:
+                return self.forward_exact(dense, ids)
+        return logit
 
     __call__ = forward
