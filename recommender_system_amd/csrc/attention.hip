@@ -307,6 +307,7 @@ extern "C" int rs_din_attention_fwd(const float* query, const float* keys, const
                                     int T, int k, const float* W1, const float* b1, const float* alpha1, int H1,
                                     const float* W2, const float* b2, const float* alpha2, int H2, const float* w3,
                                     const float* b3, float* out, int64_t batch, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(query && keys && values && mask && W1 && b1 && alpha1 && W2 && b2 && alpha2 && w3 && b3 && out,
              "rs_din_attention_fwd: null pointer");
   RS_REQUIRE(T >= 1 && T <= ATT_TMAX && batch >= 0, "rs_din_attention_fwd: need 1 <= T <= %d", ATT_TMAX);
@@ -329,6 +330,7 @@ extern "C" int rs_din_attention_dice_fwd(const float* query, const float* keys, 
                                          const float* dice_mean, const float* dice_var, float dice_eps,
                                          const float* w_out, const float* b_out, float* out, int64_t batch,
                                          rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(query && keys && values && mask && w_out && b_out && out, "rs_din_attention_dice_fwd: null pointer");
   RS_REQUIRE(n_dice == 0 || (dice_alpha && dice_mean && dice_var), "rs_din_attention_dice_fwd: null Dice params");
   RS_REQUIRE(T >= 1 && T <= ATT_TMAX && k >= 1 && k <= 64 && n_dice >= 0 && batch >= 0,

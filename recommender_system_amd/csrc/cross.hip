@@ -312,6 +312,7 @@ extern "C" int rs_cross_prepare(const float* w, const float* b, int d, int n_lay
 
 extern "C" int rs_cross_fwd(const float* x0, int64_t x_stride, int d, int n_layers, const float* prepared,
                             float* out, int64_t out_stride, int64_t batch, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(x0 && prepared && out, "rs_cross_fwd: null pointer");
   RS_REQUIRE(d >= 1 && n_layers >= 0 && n_layers <= 32 && batch >= 0, "rs_cross_fwd: bad shape");
   RS_REQUIRE(x_stride >= d && out_stride >= d, "rs_cross_fwd: stride < d");
@@ -339,6 +340,7 @@ extern "C" int rs_embed_cross_fwd(const void* ids, int id_kind, int64_t id_strid
                                   const int64_t* field_vocab, int n_fields, int k, int n_layers,
                                   const float* prepared, float* out, int64_t out_stride, int64_t batch,
                                   int* err_flag, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(ids && table && field_offsets && field_vocab && prepared && out, "rs_embed_cross_fwd: null pointer");
   RS_REQUIRE(nd == 0 || dense, "rs_embed_cross_fwd: dense is null");
   RS_REQUIRE(n_fields >= 1 && n_fields <= EC_FMAX && nd >= 0 && k >= 4 && k % 4 == 0,

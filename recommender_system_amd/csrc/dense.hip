@@ -159,6 +159,7 @@ using namespace rs;
 
 extern "C" int rs_dense_fwd(const float* x, int64_t x_stride, const float* W, const float* bias, const float* alpha,
                             int act, float* y, int64_t y_stride, int64_t M, int K, int N, rs_stream_t stream) {
+  if (M == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(x && W && y, "rs_dense_fwd: null pointer");
   RS_REQUIRE(M >= 0 && K >= 1 && N >= 1 && x_stride >= K && y_stride >= N, "rs_dense_fwd: bad shape");
   RS_REQUIRE(act >= RS_ACT_NONE && act <= RS_ACT_SIGMOID, "rs_dense_fwd: bad activation");
@@ -181,6 +182,7 @@ extern "C" int rs_dense_fwd(const float* x, int64_t x_stride, const float* W, co
 extern "C" int rs_affine_act(const float* x, int64_t x_stride, const float* scale, const float* shift,
                              const float* alpha, int act, float* y, int64_t y_stride, int64_t M, int N,
                              rs_stream_t stream) {
+  if (M == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(x && y && M >= 0 && N >= 1 && x_stride >= N && y_stride >= N, "rs_affine_act: bad arguments");
   RS_REQUIRE(act >= RS_ACT_NONE && act <= RS_ACT_SIGMOID && (act != RS_ACT_PRELU || alpha),
              "rs_affine_act: bad activation");
@@ -192,6 +194,7 @@ extern "C" int rs_affine_act(const float* x, int64_t x_stride, const float* scal
 
 extern "C" int rs_sigmoid_combine(const float* a, const float* b, float c0, float c1, float* out, int64_t n,
                                   rs_stream_t stream) {
+  if (n == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(a && out && n >= 0, "rs_sigmoid_combine: bad arguments");
   if (n == 0) return RS_OK;
   sigmoid_combine_kernel<<<ew_grid(n), 256, 0, as_stream(stream)>>>(a, b, c0, c1, out, n);
@@ -215,6 +218,7 @@ __global__ void dice_kernel(const float* __restrict__ x, int64_t xs, const float
 
 extern "C" int rs_dice_fwd(const float* x, int64_t x_stride, const float* mean, const float* var, float eps,
                            const float* alpha, float* y, int64_t y_stride, int64_t M, int N, rs_stream_t stream) {
+  if (M == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(x && mean && var && alpha && y && M >= 0 && N >= 1 && x_stride >= N && y_stride >= N,
              "rs_dice_fwd: bad arguments");
   if (M == 0) return RS_OK;

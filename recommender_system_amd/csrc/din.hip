@@ -440,6 +440,7 @@ extern "C" int rs_din_attention_ids_fwd(const void* hist, int id_kind, int64_t h
                                         int64_t cand_stride, int T, int k, const float* table, int64_t vocab,
                                         int H1, int H2, const float* prepared, float* scores, float* out,
                                         int64_t batch, int* err_flag, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(rs_din_prepared_size(T, k, H1, H2) > 0,
              "rs_din_attention_ids_fwd: need k in {4,8,16}, H1 <= 128, H2 <= 64");
   RS_REQUIRE(hist && cand && table && prepared && scores && out, "rs_din_attention_ids_fwd: null pointer");

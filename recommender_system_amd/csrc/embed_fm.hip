@@ -752,6 +752,7 @@ extern "C" int rs_embed_fm_fwd(const void* ids, int id_kind, int64_t id_stride, 
                                const int64_t* field_vocab, int n_fields, int k, const float* prepared,
                                const float* w0, int kfm, float* logit, float* x_out, int64_t batch,
                                int* err_flag, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(batch >= 0 && nd >= 0 && n_fields >= 0 && kfm >= 1, "rs_embed_fm_fwd: bad shape");
   RS_REQUIRE(prepared && w0 && logit, "rs_embed_fm_fwd: null pointer");
   RS_REQUIRE(nd == 0 || dense, "rs_embed_fm_fwd: dense is null");
@@ -855,6 +856,7 @@ extern "C" int rs_diag_embed_fm_fwd(const void* ids, int id_kind, int64_t id_str
 extern "C" int rs_rows_fm_fwd(const float* emb, const float* dense, int64_t dense_stride, int nd, int n_fields,
                               int k, const float* prepared, const float* w0, int kfm, float* logit, int64_t batch,
                               rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(batch >= 0 && nd >= 0 && n_fields >= 0 && kfm >= 1, "rs_rows_fm_fwd: bad shape");
   RS_REQUIRE(prepared && w0 && logit && (n_fields == 0 || emb) && (nd == 0 || dense),
              "rs_rows_fm_fwd: null pointer");
@@ -877,6 +879,7 @@ extern "C" int rs_rows_fm_fwd(const float* emb, const float* dense, int64_t dens
 
 extern "C" int rs_fm_fwd(const float* x, int64_t x_stride, int n, const float* prepared, const float* w0, int kfm,
                          float* logit, int64_t batch, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(x && prepared && w0 && logit, "rs_fm_fwd: null pointer");
   RS_REQUIRE(n >= 1 && kfm >= 1 && batch >= 0, "rs_fm_fwd: bad shape");
   const FmGeom g = fm_geom(n, 0, 0, kfm);
@@ -898,6 +901,7 @@ extern "C" int rs_embed_gather(const void* ids, int id_kind, int64_t id_stride, 
                                int64_t dense_stride, int nd, const float* table, const int64_t* field_offsets,
                                const int64_t* field_vocab, int n_fields, int k, float* out, int64_t out_stride,
                                int64_t batch, int* err_flag, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(batch >= 0 && nd >= 0 && n_fields >= 0, "rs_embed_gather: bad shape");
   RS_REQUIRE(out && (nd == 0 || dense), "rs_embed_gather: null pointer");
   RS_REQUIRE(n_fields == 0 || (ids && table && field_offsets && field_vocab && k >= 1),
@@ -937,6 +941,7 @@ extern "C" int rs_fm_onehot_fwd(const void* ids, int id_kind, int64_t id_stride,
                                 const int64_t* field_vocab, int n_fields, const float* w1, const float* w0,
                                 const float* v, int kfm, float* logit, int64_t batch, int* err_flag,
                                 rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(batch >= 0 && nd >= 0 && n_fields >= 0 && kfm >= 1 && kfm <= 64, "rs_fm_onehot_fwd: bad shape");
   RS_REQUIRE(w1 && w0 && v && logit && (nd == 0 || dense), "rs_fm_onehot_fwd: null pointer");
   RS_REQUIRE(n_fields == 0 || (ids && field_offsets && field_vocab), "rs_fm_onehot_fwd: sparse inputs missing");
@@ -998,6 +1003,7 @@ extern "C" int rs_deepfm_fwd(const void* ids, int id_kind, int64_t id_stride, co
                              const float* w0, int kfm, int n_layers, const int* dims, const int* acts,
                              const float* mlp_prepared, float c0, float c1, float* out, float* fm_logit,
                              int64_t batch, int* err_flag, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   FmGeom fg;
   MlpGeom mg;
   RS_REQUIRE(dims && acts, "rs_deepfm_fwd: null dims/acts");

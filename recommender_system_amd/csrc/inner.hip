@@ -374,6 +374,7 @@ extern "C" void rs_diag_inner_set_dbg(unsigned long long* p) { g_inner_dbg = p; 
 
 extern "C" int rs_inner_product_fwd(const float* emb, int n_fields, int k, float* out, int64_t out_stride,
                                     int64_t batch, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(emb && out, "rs_inner_product_fwd: null pointer");
   RS_REQUIRE(n_fields >= 1 && k >= 1 && k <= 64 && batch >= 0, "rs_inner_product_fwd: bad shape (k<=64)");
   RS_REQUIRE(out_stride >= (int64_t)n_fields * (n_fields - 1) / 2, "rs_inner_product_fwd: out_stride too small");
@@ -395,6 +396,7 @@ extern "C" int rs_embed_inner_fwd(const void* ids, int id_kind, int64_t id_strid
                                   const int64_t* field_offsets, const int64_t* field_vocab, int n_fields, int k,
                                   float* out, int64_t out_stride, int64_t batch, int* err_flag,
                                   rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(ids && table && field_offsets && field_vocab && out, "rs_embed_inner_fwd: null pointer");
   RS_REQUIRE(n_fields >= 1 && k >= 1 && k <= 64 && batch >= 0, "rs_embed_inner_fwd: bad shape (k<=64)");
   RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_embed_inner_fwd: bad id_kind");

@@ -139,6 +139,7 @@ extern "C" int rs_mlp_prepare(int n_layers, const int* dims, const float* const*
 extern "C" int rs_mlp_fwd(const float* x, int64_t x_stride, int n_layers, const int* dims, const int* acts,
                           const float* prepared, float* y, int64_t y_stride, int head, const float* extra, float c0,
                           float c1, int64_t batch, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   MlpGeom g;
   RS_REQUIRE(mlp_geom(n_layers, dims, g), "rs_mlp_fwd: need 1..%d layers with widths 1..%d", MLP_MAXL, MLP_MAXD);
   RS_REQUIRE(x && prepared && y && acts, "rs_mlp_fwd: null pointer");

@@ -281,6 +281,7 @@ extern "C" int rs_shard_slot_bucketize(const void* ids, int id_kind, int64_t id_
 
 extern "C" int rs_gather_rows(const float* table, int64_t n_rows, int k, const int32_t* rows, int64_t n, float* out,
                               int* err_flag, rs_stream_t stream) {
+  if (n == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(rows && out && (n == 0 || table || n_rows == 0), "rs_gather_rows: null pointer");
   RS_REQUIRE(k >= 1 && n >= 0 && n_rows >= 0, "rs_gather_rows: bad shape");
   if (n == 0) return RS_OK;
@@ -294,6 +295,7 @@ extern "C" int rs_gather_rows(const float* table, int64_t n_rows, int k, const i
 
 extern "C" int rs_unpermute_rows(const float* src, const int32_t* perm, int k, int64_t n, float* dst,
                                  rs_stream_t stream) {
+  if (n == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(src && perm && dst && k >= 1 && n >= 0, "rs_unpermute_rows: bad arguments");
   if (n == 0) return RS_OK;
   hipStream_t st = as_stream(stream);

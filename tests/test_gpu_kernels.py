@@ -497,3 +497,36 @@ def test_din_attention_ids(gpu, T, k, h, B, id_dtype):
     layer.forward_ids(table, V, torch.tensor(bad, device="cuda"), torch.tensor(cand, device="cuda"), err=err)
     torch.cuda.synchronize()
     assert err.item() != 0
+
+
+# ------------------------------------------------------------ empty batches
+def test_empty_batches_every_path(gpu):
+    """B = 0 through every C-ABI path: no launch, no error, empty outputs."""
+    from recommender_system_amd import DCN, DeepFM, DNNLayer, FM, PNN, Attention, InnerProductLayer
+    from tests.helpers import criteo_columns
+    vocabs = [30] * 26
+    cols = criteo_columns(vocabs, embed_dim=16)
+    ids = np.zeros((0, 26), np.int32)
+    dense = np.zeros((0, 13), np.float32)
+    m = DeepFM(cols, 10, 1e-4, 1e-4, [32, 16], 1, "relu", embed_dim=16, seed=1)
+    assert m((dense, ids)).shape == (0, 1)
+    assert m.forward_unfused((dense, ids)).shape == (0, 1)
+    assert m.fm_logit((dense, ids)).shape == (0, 1)
+    d = DCN(cols, [32], 1, "relu", layer_num=2, embed_dim=16, seed=1)
+    assert d((dense, ids)).shape == (0, 1)
+    assert d.cross_fused((dense, ids)).shape == (0, 13 + 26 * 16)
+    p = PNN(cols, "inner", [32], 1, embed_dim=16, seed=1)
+    assert p((dense, ids)).shape == (0, 1)
+    dnn = DNNLayer([32], 1, "relu", seed=1)
+    dnn.build(20)
+    assert dnn(torch.zeros(0, 20, device="cuda")).shape == (0, 1)
+    ip = InnerProductLayer()
+    assert ip(torch.zeros(0, 5, 8, device="cuda")).shape == (0, 10)
+    att = Attention((16, 8), "prelu", seed=1)
+    att.build(7, 8)
+    table = torch.randn(50, 8, device="cuda")
+    out = att.forward_ids(table, 50, torch.zeros(0, 7, dtype=torch.int32, device="cuda"),
+                          torch.zeros(0, 1, dtype=torch.int32, device="cuda"))
+    assert out.shape == (0, 8)
+    fm = FM(8, 1e-4, 1e-4, seed=1)
+    assert fm(np.zeros((0, 43), np.float32)).shape == (0, 1)
