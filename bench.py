@@ -528,12 +528,30 @@ def bench_pnn(args, world, rank):
     dt, slot = _timed_graph(step, args.steps, args.warmup, world)
     alg = B * (F * 4 + F * k * 4 + (F * k + F * (F - 1) // 2) * 4)
     ach = alg / (slot * 1e-3)
+    # mode 'both' (inner + OuterProductLayer, model/pnn.py:45-48) and the full PNN forward
+    both = rs.PNN(cols, "both", [256, 128, 64], 1, embed_dim=k, seed=SEED, device=dev)
+    P = F * (F - 1) // 2
+
+    def step_both(i):
+        both.product_inputs((dense_pool[i % 64], ids_pool[i % 64]), check_ids=False)
+
+    def full(i):
+        model((dense_pool[i % 64], ids_pool[i % 64]), check_ids=False)
+
+    n2 = max(10, args.steps // 5)
+    dtb, slotb = _timed_graph(step_both, n2, args.warmup, world)
+    dtf, _ = _timed_graph(full, n2, args.warmup, world, chunk=16)
     return _line("PNN inner-product input samples/sec @ batch 4096, 26 sparse x 1e6 vocab, dim 16",
                  args.steps * B / dt, "samples/s", args, world, dt / args.steps * 1e3,
                  {"workload": "pnn_embed_inner_fused", "global_batch": B, "vocab_per_field": V, "parallelism": "dp1"},
                  {"bound": "hbm", "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                  "frac": ach / PEAK_HBM, "traffic": None, "kernel": "inner_kernel", "kernel_ms": slot,
-                  "algorithmic_bytes_per_launch": alg})
+                  "frac": ach / PEAK_HBM, "traffic": None, "kernel": "inner_fast", "kernel_ms": slot,
+                  "algorithmic_bytes_per_launch": alg},
+                 {"mode_both": {"samples_per_s": n2 * B / dtb, "kernel_ms": slotb,
+                                "outer_mfma_tflops": B * P * k * k * 2 / (slotb * 1e-3) / 1e12,
+                                "note": "[flat | inner | outer] in one launch (rs_embed_product_fwd)"},
+                  "pnn_inner_forward": {"samples_per_s": n2 * B / dtf, "ms_per_step": dtf / n2 * 1e3,
+                                        "note": "product inputs + DNN tower (rs_mlp_fwd, K = 741)"}})
 
 
 def _pmc_traffic():

@@ -153,6 +153,27 @@ int rs_embed_inner_fwd(const void* ids, int id_kind, int64_t id_stride,
                        float* out, int64_t out_stride, int64_t batch,
                        int* err_flag, rs_stream_t stream);
 
+/* OuterProductLayer (layer/interaction.py:186-215): out[b,p] =
+ * sum_{a,j} e[b,row_p,j] W[a,p,j] e[b,col_p,a] with W the Keras weight
+ * [k, P, k], pairs in the reference's row-major i<j order.  rs_outer_prepare
+ * packs W into per-lane MFMA fragments (rs_outer_prepared_size floats; k in
+ * {4,8,16,32,64}, 2..64 fields).  rs_outer_product_fwd: emb [B,F,k] -> out
+ * [B,P].  rs_embed_product_fwd: PNN's DNN input (model/pnn.py:32-48) from ids
+ * in one launch — out[b] = [flat_emb (F*k) | inner (P, if inner) | outer (P,
+ * if outer_prepared)]; mode 'inner' / 'outer' / 'both'.                      */
+int64_t rs_outer_prepared_size(int n_fields, int k);
+int rs_outer_prepare(const float* W, int n_fields, int k, float* prepared,
+                     rs_stream_t stream);
+int rs_outer_product_fwd(const float* emb, int n_fields, int k,
+                         const float* outer_prepared, float* out,
+                         int64_t out_stride, int64_t batch, rs_stream_t stream);
+int rs_embed_product_fwd(const void* ids, int id_kind, int64_t id_stride,
+                         const float* table, const int64_t* field_offsets,
+                         const int64_t* field_vocab, int n_fields, int k,
+                         int inner, const float* outer_prepared, float* out,
+                         int64_t out_stride, int64_t batch, int* err_flag,
+                         rs_stream_t stream);
+
 /* ---------------------------------------------- DIN attention unit (a13)
  * Attention.call (layer/interaction.py:369-406), 'prelu' mode:
  *   e_t   = [q, key_t, q-key_t, q*key_t]                         (4k)

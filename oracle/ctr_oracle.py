@@ -281,6 +281,50 @@ def dcn(X, p, nd=13, dt=np.float64, inputs=None):
     return sigmoid(dense(z, p["out_kernel"], p["out_bias"], dt=dt)), cross
 
 
+def outer_product_layer(e, W, dt=np.float64):
+    """OuterProductLayer.call (layer/interaction.py:200-215) op for op:
+    p [B,1,P,k] * W [k,P,k] -> sum over the last axis -> [B,k,P] ->
+    transpose * q -> sum: out[b,p] = sum_a q[b,p,a] sum_j p[b,p,j] W[a,p,j]."""
+    e = np.asarray(e, dt)
+    W = np.asarray(W, dt)
+    row, col = pair_indices(e.shape[1])
+    pp = e[:, row, :][:, None, :, :]           # [B,1,P,k]
+    qq = e[:, col, :]                          # [B,P,k]
+    tmp = np.sum(pp * W[None], axis=-1)        # [B,k,P]
+    return np.sum(np.transpose(tmp, (0, 2, 1)) * qq, axis=-1)
+
+
+def outer_product_loop(e, W, dt=np.float64):
+    """Known-answer restatement: out[b,p] = e_row^T W_p^T e_col per pair."""
+    e = np.asarray(e, dt)
+    W = np.asarray(W, dt)
+    B, F, _ = e.shape
+    out = []
+    p = 0
+    for i in range(F - 1):
+        for j in range(i + 1, F):
+            Wp = W[:, p, :]                    # [a, j']
+            out.append([float(e[b, j] @ (Wp @ e[b, i])) for b in range(B)])
+            p += 1
+    return np.asarray(out, dt).T.reshape(B, -1)
+
+
+def pnn(X, p, mode="inner", nd=13, dt=np.float64, inputs=None):
+    """PNN.call (model/pnn.py:28-53), mode 'inner' / 'outer' / 'both', with
+    3-D embeddings.  p['outer_W'] is the OuterProductLayer weight [k,P,k]."""
+    _, sparse = inputs if inputs is not None else _split_dense_sparse(X, nd, dt)
+    flat = embed_layer(sparse, p["tables"], dt)
+    k = np.asarray(p["tables"][0]).shape[1]
+    z = flat.reshape(flat.shape[0], -1, k)
+    parts = [flat]
+    if mode in ("inner", "both"):
+        parts.append(inner_product_layer(z, dt=dt))
+    if mode in ("outer", "both"):
+        parts.append(outer_product_layer(z, p["outer_W"], dt=dt))
+    x = np.concatenate(parts, axis=1)
+    return dnn_layer(x, p["dnn_hidden"], p["dnn_out"], p.get("act", "relu"), dt=dt), x
+
+
 def pnn_inner(X, p, nd=13, dt=np.float64, inputs=None):
     """PNN.call mode='inner' (model/pnn.py:28-53) with 3-D embeddings [B,F,k]
     (documented deviation: the reference's rank-2 EmbedLayer crashes at

@@ -8,7 +8,7 @@ reference's Keras layer / model names and signatures.
 """
 from . import _lib  # noqa: F401
 from .layers import (Attention, BatchNormalization, CrossLayer, Dense, Dice, DNNLayer, EmbedLayer,  # noqa: F401
-                     FMLayer, InnerProductLayer, sigmoid_combine)
+                     FMLayer, InnerProductLayer, OuterProductLayer, sigmoid_combine)
 from .models import DCN, DIN, FM, PNN, DeepFM  # noqa: F401
 from .dataset import create_criteo_dataset, denseFeature, features_dict, sparseFeature  # noqa: F401
 

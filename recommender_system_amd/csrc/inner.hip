@@ -24,6 +24,9 @@ struct InnerArgs {
   int64_t out_stride;
   int inner_off;   // column of the first pair in out
   int write_flat;  // also write the flattened embeddings to out[:, 0:F*k]
+  int want_inner;  // write the inner products (fast path; the generic kernel always does)
+  const float* outer_img;  // OuterProductLayer weights packed by rs_outer_prepare (null: no outer)
+  int outer_off;   // column of the first outer product in out
   int contig;      // fast path: out rows are [flat | inner] back to back, 16-B aligned blocks
   int64_t batch;
   int* err;
@@ -143,8 +146,9 @@ __global__ __launch_bounds__(IP_NT) void inner_fast(InnerArgs a) {
   __shared__ int64_t lmeta[2][IP_FMAX];
   const int F = a.F, P = F * (F - 1) / 2, S = a.S;
   const int SS = F * K + 4;                    // sample stride: +4 dwords spreads the Gram reads over banks
+  const int Pi = a.want_inner ? P : 0, Po = a.outer_img ? P : 0, PP = Pi + Po;
   float* tile = smem;                          // [S][SS]
-  float* gram = smem + S * SS;                 // [S][P]
+  float* gram = smem + S * SS;                 // [S][PP]: inner pairs, then outer pairs
   const int tid = threadIdx.x;
   const int64_t b0 = (int64_t)blockIdx.x * S;
   const int nvalid = (int)(a.batch - b0 < S ? a.batch - b0 : S);
@@ -226,7 +230,8 @@ __global__ __launch_bounds__(IP_NT) void inner_fast(InnerArgs a) {
     const int kof = 4 * (lane >> 4);
     for (int si = w; si < S; si += IP_NW) {
       const float* es = tile + si * SS;
-      float* gs = gram + si * P;
+      float* gs = gram + si * PP;
+      if (!a.want_inner) continue;
       if (NB <= 2) {
         // common case (F <= 32): both row-block fragments read once, the three
         // blocks (0,0) (0,1) (1,1) as independent MFMA chains
@@ -277,11 +282,85 @@ __global__ __launch_bounds__(IP_NT) void inner_fast(InnerArgs a) {
       }
     }
   }
+  // OuterProductLayer (layer/interaction.py:186-215): out[b,p] =
+  // sum_{a,j} e_row[j] W[a,p,j] e_col[a] — per pair a [16 samples x k] x
+  // [k x k] MFMA tile (A = the samples' e_row from the LDS tile, B = W_p^T
+  // packed per lane as float4 over 4 k-steps), then the dot with e_col and a
+  // DPP row sum over a.  Wave w takes pairs w, w+16, ...
+  if (a.outer_img) {
+    constexpr int KB = (K + 15) / 16;
+    const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int sm = lane & 15, kq = lane >> 4;
+    const floatx4* img = reinterpret_cast<const floatx4*>(a.outer_img);
+    int i = 0, j = 1;  // (row, col) of the current pair
+    // pair index p -> (i, j) in the reference's row-major i<j order, closed
+    // form (start(i) = i(2F-i-1)/2) with an integer fix-up: no loops/branches
+    // between the pipelined loads
+    auto set_pair = [&](int p) {
+      const float tf = (float)(2 * F - 1);
+      int ii = (int)((tf - sqrtf(tf * tf - 8.f * (float)p)) * 0.5f);
+      ii = ii < 0 ? 0 : (ii > F - 2 ? F - 2 : ii);
+      if (ii * (2 * F - ii - 1) / 2 > p) --ii;
+      if ((ii + 1) * (2 * F - ii - 2) / 2 <= p && ii < F - 2) ++ii;
+      i = ii;
+      j = p - ii * (2 * F - ii - 1) / 2 + ii + 1;
+    };
+    // B fragments (L2) of the wave's next pair are requested while the
+    // current pair computes (two named register sets, no copies: a copy of
+    // an in-flight load makes the compiler drain vmcnt every iteration)
+    auto fetch_w = [&](floatx4 (&wv)[KB][KB], int p) {
+      const int pc = p < P ? p : P - 1;
+#pragma unroll
+      for (int ab = 0; ab < KB; ++ab)
+#pragma unroll
+        for (int jg = 0; jg < KB; ++jg) wv[ab][jg] = img[((int64_t)(pc * KB + ab) * KB + jg) * 64 + lane];
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto pair = [&](const floatx4 (&wv)[KB][KB], int p) {
+      set_pair(p);
+      floatx4 acc[KB];
+#pragma unroll
+      for (int ab = 0; ab < KB; ++ab) acc[ab] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int jg = 0; jg < KB; ++jg) {
+        const int kk = 16 * jg + 4 * kq;
+        floatx4 ea = {0.f, 0.f, 0.f, 0.f};
+        if (kk < K && sm < S) ea = *reinterpret_cast<const floatx4*>(tile + sm * SS + i * K + kk);
+#pragma unroll
+        for (int ab = 0; ab < KB; ++ab)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[ab] = mfma16x16x4(ea[q], wv[ab][jg][q], acc[ab]);
+      }
+      // C[s][a]: lane holds a = 16ab + (lane&15), s = 4kq + r
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ss = 4 * kq + r;
+        float v = 0.f;
+#pragma unroll
+        for (int ab = 0; ab < KB; ++ab) {
+          const int aa = 16 * ab + sm;
+          const float ec = (aa < K && ss < S) ? tile[ss * SS + j * K + aa] : 0.f;
+          v = fmaf(acc[ab][r], ec, v);
+        }
+        v = row16_sum(v);
+        if (sm == 0 && ss < S) gram[ss * PP + Pi + p] = v;
+      }
+    };
+    floatx4 wa[KB][KB], wb[KB][KB];
+    fetch_w(wa, w);
+    for (int p = w; p < P; p += 2 * IP_NW) {
+      fetch_w(wb, p + IP_NW);
+      pair(wa, p);
+      if (p + IP_NW >= P) break;
+      fetch_w(wa, p + 2 * IP_NW);
+      pair(wb, p + IP_NW);
+    }
+  }
   __syncthreads();
   IP_STAMP(3);
-  // coalesced output rows [flat F*K | inner P]
+  // coalesced output rows [flat F*K | inner P | outer P]
   const int FK = a.write_flat ? F * K : 0;
-  const int W = FK + P;
+  const int W = FK + PP;
   if (a.contig) {
     // the workgroup's rows are one contiguous, 16-B aligned block: float4
     // stores (scalar stores are issue-bound at ~4 B/clk/CU)
@@ -294,7 +373,7 @@ __global__ __launch_bounds__(IP_NT) void inner_fast(InnerArgs a) {
       int ss = s0, cc = c0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        v[q] = cc < FK ? tile[ss * SS + cc] : gram[ss * P + (cc - FK)];
+        v[q] = cc < FK ? tile[ss * SS + cc] : gram[ss * PP + (cc - FK)];
         if (++cc == W) { cc = 0; ++ss; }
       }
       if (f + 4 <= n) {
@@ -310,8 +389,9 @@ __global__ __launch_bounds__(IP_NT) void inner_fast(InnerArgs a) {
   for (int s = 0; s < nvalid; ++s) {
     float* orow = a.out + (b0 + s) * a.out_stride;
     for (int col = tid; col < W; col += IP_NT) {
-      const float val = col < FK ? tile[s * SS + col] : gram[s * P + (col - FK)];
-      orow[col < FK ? col : a.inner_off + (col - FK)] = val;
+      const float val = col < FK ? tile[s * SS + col] : gram[s * PP + (col - FK)];
+      const int cp = col - FK;
+      orow[col < FK ? col : (cp < Pi ? a.inner_off + cp : a.outer_off + (cp - Pi))] = val;
     }
   }
   }
@@ -334,12 +414,15 @@ static int launch_inner(InnerArgs a, hipStream_t st, const char* what) {
   const bool fast_k = a.k == 4 || a.k == 8 || a.k == 16 || a.k == 32 || a.k == 64;
   if (fast_k && a.F >= 2 && a.F <= IP_FMAX) {
     const int P = a.F * (a.F - 1) / 2;
-    const int64_t per = ((int64_t)a.F * a.k + 4 + P) * sizeof(float);
+    const int PP = (a.want_inner ? P : 0) + (a.outer_img ? P : 0);
+    const int64_t per = ((int64_t)a.F * a.k + 4 + PP) * sizeof(float);
     int S = IP_SMAX;
     while (S > 1 && S * per > 96 * 1024) --S;
     a.S = S;
-    const int W = (a.write_flat ? a.F * a.k : 0) + P;
-    a.contig = a.out_stride == W && a.inner_off == (a.write_flat ? a.F * a.k : 0) && (uintptr_t)a.out % 16 == 0 &&
+    const int FKw = a.write_flat ? a.F * a.k : 0;
+    const int W = FKw + PP;
+    a.contig = a.out_stride == W && (!a.want_inner || a.inner_off == FKw) &&
+               (!a.outer_img || a.outer_off == FKw + (a.want_inner ? P : 0)) && (uintptr_t)a.out % 16 == 0 &&
                ((int64_t)S * W) % 4 == 0;
     const size_t lds = (size_t)S * per;
     const unsigned grid = (unsigned)((a.batch + S - 1) / S);
@@ -365,9 +448,48 @@ static int launch_inner(InnerArgs a, hipStream_t st, const char* what) {
   return launch_status(what);
 }
 
+// OuterProductLayer weights W [k, P, k] (Keras add_weight shape) -> per-lane
+// MFMA B fragments: img[((p*KB + ab)*KB + jg)*64 + lane][q] =
+// W[a = 16ab + (lane&15)][p][j = 16jg + 4(lane>>4) + q], zero-padded.
+__global__ void outer_prepare_kernel(const float* __restrict__ W, int P, int k, int KB, int64_t n,
+                                     float* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(i & 3), lane = (int)((i >> 2) & 63);
+    int64_t r = i >> 8;
+    const int jg = (int)(r % KB);
+    r /= KB;
+    const int ab = (int)(r % KB);
+    const int p = (int)(r / KB);
+    const int aa = 16 * ab + (lane & 15), j = 16 * jg + 4 * (lane >> 4) + q;
+    out[i] = (aa < k && j < k) ? W[((int64_t)aa * P + p) * k + j] : 0.f;
+  }
+}
+
+static int64_t outer_size(int F, int k) {
+  const int64_t P = (int64_t)F * (F - 1) / 2, KB = (k + 15) / 16;
+  return P * KB * KB * 256;
+}
+
 }  // namespace rs
 
 using namespace rs;
+
+extern "C" int64_t rs_outer_prepared_size(int n_fields, int k) {
+  if (n_fields < 2 || n_fields > IP_FMAX || !(k == 4 || k == 8 || k == 16 || k == 32 || k == 64)) return -1;
+  return outer_size(n_fields, k);
+}
+
+extern "C" int rs_outer_prepare(const float* W, int n_fields, int k, float* prepared, rs_stream_t stream) {
+  RS_REQUIRE(rs_outer_prepared_size(n_fields, k) > 0, "rs_outer_prepare: need 2..%d fields, k in {4,8,16,32,64}",
+             IP_FMAX);
+  RS_REQUIRE(W && prepared, "rs_outer_prepare: null pointer");
+  const int64_t n = outer_size(n_fields, k);
+  int64_t g = (n + 255) / 256;
+  g = g > 8192 ? 8192 : g;
+  outer_prepare_kernel<<<(unsigned)g, 256, 0, as_stream(stream)>>>(W, n_fields * (n_fields - 1) / 2, k,
+                                                                    (k + 15) / 16, n, prepared);
+  return launch_status("rs_outer_prepare");
+}
 
 static unsigned long long* g_inner_dbg = nullptr;
 extern "C" void rs_diag_inner_set_dbg(unsigned long long* p) { g_inner_dbg = p; }
@@ -388,6 +510,7 @@ extern "C" int rs_inner_product_fwd(const float* emb, int n_fields, int k, float
   a.out_stride = out_stride;
   a.inner_off = 0;
   a.write_flat = 0;
+  a.want_inner = 1;
   a.batch = batch;
   return launch_inner(a, as_stream(stream), "rs_inner_product_fwd");
 }
@@ -417,7 +540,67 @@ extern "C" int rs_embed_inner_fwd(const void* ids, int id_kind, int64_t id_strid
   a.out_stride = out_stride;
   a.inner_off = n_fields * k;
   a.write_flat = 1;
+  a.want_inner = 1;
   a.batch = batch;
   a.err = err_flag;
   return launch_inner(a, as_stream(stream), "rs_embed_inner_fwd");
+}
+
+extern "C" int rs_embed_product_fwd(const void* ids, int id_kind, int64_t id_stride, const float* table,
+                                    const int64_t* field_offsets, const int64_t* field_vocab, int n_fields, int k,
+                                    int inner, const float* outer_prepared, float* out, int64_t out_stride,
+                                    int64_t batch, int* err_flag, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
+  RS_REQUIRE(ids && table && field_offsets && field_vocab && out, "rs_embed_product_fwd: null pointer");
+  RS_REQUIRE(inner || outer_prepared, "rs_embed_product_fwd: nothing to compute (inner=0, no outer weights)");
+  RS_REQUIRE(rs_outer_prepared_size(n_fields, k) > 0,
+             "rs_embed_product_fwd: need 2..%d fields and k in {4,8,16,32,64}", IP_FMAX);
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32 && batch >= 0, "rs_embed_product_fwd: bad ids");
+  const int P = n_fields * (n_fields - 1) / 2;
+  RS_REQUIRE(out_stride >= (int64_t)n_fields * k + (inner ? P : 0) + (outer_prepared ? P : 0),
+             "rs_embed_product_fwd: out_stride too small");
+  RS_REQUIRE((uintptr_t)table % 16 == 0, "rs_embed_product_fwd: table must be 16-B aligned");
+  InnerArgs a{};
+  a.dbg = g_inner_dbg;
+  a.ids = ids;
+  a.id_kind = id_kind;
+  a.id_stride = id_stride;
+  a.table = table;
+  a.offs = field_offsets;
+  a.vocab = field_vocab;
+  a.F = n_fields;
+  a.k = k;
+  a.out = out;
+  a.out_stride = out_stride;
+  a.write_flat = 1;
+  a.want_inner = inner ? 1 : 0;
+  a.inner_off = n_fields * k;
+  a.outer_img = outer_prepared;
+  a.outer_off = n_fields * k + (inner ? P : 0);
+  a.batch = batch;
+  a.err = err_flag;
+  return launch_inner(a, as_stream(stream), "rs_embed_product_fwd");
+}
+
+extern "C" int rs_outer_product_fwd(const float* emb, int n_fields, int k, const float* outer_prepared, float* out,
+                                    int64_t out_stride, int64_t batch, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
+  RS_REQUIRE(emb && outer_prepared && out, "rs_outer_product_fwd: null pointer");
+  RS_REQUIRE(rs_outer_prepared_size(n_fields, k) > 0,
+             "rs_outer_product_fwd: need 2..%d fields and k in {4,8,16,32,64}", IP_FMAX);
+  RS_REQUIRE(out_stride >= (int64_t)n_fields * (n_fields - 1) / 2 && batch >= 0,
+             "rs_outer_product_fwd: out_stride too small");
+  RS_REQUIRE((uintptr_t)emb % 16 == 0, "rs_outer_product_fwd: emb must be 16-B aligned");
+  InnerArgs a{};
+  a.dbg = g_inner_dbg;
+  a.emb = emb;
+  a.F = n_fields;
+  a.k = k;
+  a.out = out;
+  a.out_stride = out_stride;
+  a.want_inner = 0;
+  a.outer_img = outer_prepared;
+  a.outer_off = 0;
+  a.batch = batch;
+  return launch_inner(a, as_stream(stream), "rs_outer_product_fwd");
 }

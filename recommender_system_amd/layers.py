@@ -341,6 +341,56 @@ class InnerProductLayer(KerasModule):
         return out
 
 
+class OuterProductLayer(KerasModule):
+    """OuterProductLayer() — layer/interaction.py:186-215.  Weight W:
+    (k, P, k) ~ N(0, 0.05) (tf.random_normal_initializer()), built on the
+    first call.  ``forward(e[B,F,k]) -> [B,P]`` with
+    out[b,p] = sum_{a,j} e[b,row_p,j] W[a,p,j] e[b,col_p,a]."""
+
+    def __init__(self, device=None, seed=None):
+        super().__init__(device, seed)
+        self.W = None
+        self.field_num = self.k = None
+
+    def build(self, F, k):
+        self.field_num, self.k = int(F), int(k)
+        P = F * (F - 1) // 2
+        self.W = nn.Parameter(_normal((k, P, k), self._gen, self._dev), requires_grad=False)
+
+    def keras_weights(self):
+        return {"W": self.W}
+
+    def set_keras_weights(self, weights, strict=True):
+        with torch.no_grad():
+            self.W.copy_(torch.as_tensor(weights["W"], dtype=torch.float32).reshape(self.W.shape))
+
+    def prepared(self):
+        """W packed into per-lane MFMA fragments (rs_outer_prepare), cached."""
+        key = (self.W._version, self.W.data_ptr())
+        if getattr(self, "_prep_key", None) != key:
+            n = _lib.lib().rs_outer_prepared_size(self.field_num, self.k)
+            if n < 0:
+                _lib.check(-1, "rs_outer_prepared_size")
+            self._prep = torch.empty(n, dtype=torch.float32, device=self._dev)
+            call("rs_outer_prepare", ptr(self.W), self.field_num, self.k, ptr(self._prep), _stream())
+            self._prep_key = key
+        return self._prep
+
+    def forward(self, inputs, out=None):
+        e = _to_device_f32(inputs, self._dev)
+        B, F, k = e.shape
+        if self.W is None:
+            self.build(F, k)
+        if (F, k) != (self.field_num, self.k):
+            raise ValueError(f"OuterProductLayer built for F={self.field_num}, k={self.k}; got {F}, {k}")
+        P = F * (F - 1) // 2
+        if out is None:
+            out = torch.empty(B, P, dtype=torch.float32, device=self._dev)
+        call("rs_outer_product_fwd", ptr(e.contiguous()), F, k, ptr(self.prepared()), ptr(out), out.stride(0), B,
+             _stream())
+        return out
+
+
 # -------------------------------------------------------------- dense / MLP
 _MLP_MAXL, _MLP_MAXD = 8, 1024  # rs_mlp_fwd limits (mlp.hip)
 _ACTS = ("relu", "prelu", "sigmoid", "linear", None, "dice")

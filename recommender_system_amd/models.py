@@ -37,6 +37,7 @@ import torch
 from . import _lib
 from ._lib import call, ptr
 from .layers import (Attention, BatchNormalization, CrossLayer, Dense, DNNLayer, EmbedLayer, FMLayer,
+                     InnerProductLayer, OuterProductLayer,
                      KerasModule, TowerMixin, sigmoid_combine, _ids_tensor, _to_device_f32, _ErrFlag)
 
 
@@ -233,7 +234,10 @@ class DCN(KerasModule):
 
 
 class PNN(KerasModule):
-    """PNN(mode='inner') — model/pnn.py:14-53, with 3-D embeddings.
+    """PNN(feature_columns, mode, ...) — model/pnn.py:14-53, with 3-D
+    embeddings (the reference reshapes them to 2-D before the product layers
+    and crashes at :38).  mode 'inner' / 'outer' / 'both'; the DNN input
+    [flat_emb | inner | outer] comes out of ONE launch (rs_embed_product_fwd).
     Returns the DNN logit (no sigmoid, as the reference)."""
 
     def __init__(self, feature_columns, mode, hidden_units, output_dim, activation="relu", dropout=0.2,
@@ -241,8 +245,6 @@ class PNN(KerasModule):
         super().__init__(device, seed)
         if mode not in ("inner", "outer", "both"):
             raise ValueError("Please choice mode's value in 'inner', 'outer', 'both'.")
-        if mode != "inner":
-            raise NotImplementedError(f"PNN mode {mode!r}: OuterProductLayer is outside this build's hot path")
         if use_fgcnn:
             raise NotImplementedError("PNN use_fgcnn=True: FGCNNLayer is outside this build's hot path")
         self.mode = mode
@@ -250,20 +252,32 @@ class PNN(KerasModule):
         self.nd = len(self.dense_feature_columns)
         self.embed_layer = EmbedLayer(self.sparse_feature_columns, embed_dim, device=device, seed=_subseed(self._gen))
         F = self.embed_layer.n_fields
-        self.width = F * embed_dim + F * (F - 1) // 2
+        P = F * (F - 1) // 2
+        self.inner_product_layer = InnerProductLayer(device=device)
+        self.outer_product_layer = OuterProductLayer(device=device, seed=_subseed(self._gen))
+        if mode != "inner":
+            self.outer_product_layer.build(F, embed_dim)
+        self.width = F * embed_dim + P * (2 if mode == "both" else 1)
         self.dnn_layer = DNNLayer(hidden_units, output_dim, activation, dropout, device=device,
                                   seed=_subseed(self._gen))
         self.dnn_layer.build(self.width)
         self._err = _ErrFlag(self._dev)
 
     def product_inputs(self, inputs, check_ids=True):
-        """[flat_emb | inner products] in one fused launch (rs_embed_inner_fwd)."""
+        """[flat_emb | inner | outer] (model/pnn.py:37-48) in one launch."""
         _, ids = _split_criteo(inputs, self.nd, self._dev)
         e = self.embed_layer
         B = ids.shape[0]
         out = torch.empty(B, self.width, dtype=torch.float32, device=self._dev)
-        call("rs_embed_inner_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(e.table), ptr(e.field_offsets),
-             ptr(e.field_vocab), e.n_fields, e.k, ptr(out), out.stride(0), B, ptr(self._err.t), _lib.stream())
+        if self.mode == "inner":
+            call("rs_embed_inner_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(e.table),
+                 ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, e.k, ptr(out), out.stride(0), B,
+                 ptr(self._err.t), _lib.stream())
+        else:
+            call("rs_embed_product_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(e.table),
+                 ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, e.k, 1 if self.mode == "both" else 0,
+                 ptr(self.outer_product_layer.prepared()), ptr(out), out.stride(0), B, ptr(self._err.t),
+                 _lib.stream())
         if check_ids:
             self._err.check("PNN")
         return out

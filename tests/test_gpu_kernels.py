@@ -530,3 +530,35 @@ def test_empty_batches_every_path(gpu):
     assert out.shape == (0, 8)
     fm = FM(8, 1e-4, 1e-4, seed=1)
     assert fm(np.zeros((0, 43), np.float32)).shape == (0, 1)
+
+
+# ---------------------------------------------------- PNN outer / both modes
+@pytest.mark.parametrize("F,k,B", [(26, 16, 100), (26, 8, 3), (2, 4, 10), (39, 32, 9), (9, 64, 17)])
+def test_outer_product(gpu, F, k, B):
+    from recommender_system_amd import OuterProductLayer
+    rng = np.random.default_rng(F * k + B)
+    e = rng.standard_normal((B, F, k)).astype(np.float32)
+    layer = OuterProductLayer(seed=3)
+    y = layer(e)
+    ref = O.outer_product_layer(e, layer.W.cpu().numpy())
+    assert_scaled_close(y, ref, what=f"OuterProduct F={F} k={k}")
+
+
+@pytest.mark.parametrize("mode,k,B,id_dtype", [("outer", 16, 4096, np.int32), ("both", 16, 37, np.int64),
+                                               ("both", 8, 5, np.int32), ("outer", 4, 64, np.int64)])
+def test_pnn_modes_fused(gpu, mode, k, B, id_dtype):
+    from recommender_system_amd import PNN
+    from tests.helpers import criteo_columns, dnn_params, tables_of
+    rng = np.random.default_rng(B + k)
+    vocabs = rng.integers(2, 4000, size=26)
+    m = PNN(criteo_columns(vocabs, embed_dim=k), mode, [64, 32], 1, embed_dim=k, seed=5)
+    ids = random_ids(rng, B, vocabs, id_dtype)
+    dense = rng.random((B, 13)).astype(np.float32)
+    x = m.product_inputs((dense, ids))
+    y = m((dense, ids))
+    hidden, out = dnn_params(m.dnn_layer)
+    p = {"tables": tables_of(m.embed_layer), "outer_W": m.outer_product_layer.W.cpu().numpy(),
+         "dnn_hidden": hidden, "dnn_out": out}
+    ref_y, ref_x = O.pnn(None, p, mode=mode, inputs=(dense, ids))
+    assert_scaled_close(x, ref_x, what=f"PNN {mode} inputs")
+    assert_scaled_close(y, ref_y, what=f"PNN {mode} logit")

@@ -72,8 +72,8 @@ def test_pnn_mode_errors():
     cols = criteo_columns([5] * 4)
     with pytest.raises(ValueError, match="Please choice mode"):
         PNN(cols, "bogus", [8], 1, device=DEV)
-    with pytest.raises(NotImplementedError):
-        PNN(cols, "outer", [8], 1, device=DEV)
+    m = PNN(cols, "both", [8], 1, device=DEV, embed_dim=4)  # outer/both are built (OuterProductLayer)
+    assert m.width == 4 * 4 + 2 * 6 and tuple(m.outer_product_layer.W.shape) == (4, 6, 4)
     with pytest.raises(NotImplementedError):
         PNN(cols, "inner", [8], 1, use_fgcnn=True, device=DEV)
 

@@ -130,3 +130,14 @@ def test_deepfm_oracle_composition():
     y, fm, x = O.deepfm(X, p, nd=2)
     dnn = O.dnn_layer(x, p["dnn_hidden"], p["dnn_out"])
     np.testing.assert_allclose(y, 1 / (1 + np.exp(-0.5 * (fm + dnn))))
+
+
+def test_outer_product_equals_loop():
+    """OuterProductLayer op-for-op restatement == per-pair e_col . (W_p e_row)."""
+    rng = np.random.default_rng(5)
+    e = rng.standard_normal((3, 5, 4))
+    W = rng.standard_normal((4, 10, 4))
+    np.testing.assert_allclose(O.outer_product_layer(e, W), O.outer_product_loop(e, W), rtol=1e-12, atol=1e-12)
+    # identity W_p -> plain inner product
+    Wi = np.repeat(np.eye(4)[:, None, :], 10, axis=1)
+    np.testing.assert_allclose(O.outer_product_layer(e, Wi), O.inner_product_layer(e), rtol=1e-12, atol=1e-12)
