@@ -138,6 +138,25 @@ int rs_embed_cross_fwd(const void* ids, int id_kind, int64_t id_stride,
                        int64_t out_stride, int64_t batch, int* err_flag,
                        rs_stream_t stream);
 
+/* Fused DCN forward (model/dcn.py:24-34) in one launch: x0 in LDS, CrossNet
+ * folded into its contraction, the DNN tower on the same tile, head
+ * sigmoid(Dense1([x_L | dnn])).  cross_prepared: rs_cross_prepare over
+ * n_cross + 1 columns — w_0..w_{L-1} then the output Dense's cross half
+ * w_o[:d] (bias row 0) — so the cross branch's logit is alpha_L (x0.w_o) +
+ * beta_L.w_o without forming x_L.  mlp_prepared: rs_mlp_prepare of the DNN
+ * hidden layers plus ONE folded last layer (W_last w_o[d:], b_last w_o[d:] +
+ * b_o), dims[n_layers] == 1, no input permutation.  rs_dcn_fused_ok: shape
+ * supported (k % 4 == 0, 1..128 fields, n_cross <= 31).                    */
+int rs_dcn_fused_ok(int nd, int n_fields, int k, int n_cross, int n_layers,
+                    const int* dims);
+int rs_dcn_fwd(const void* ids, int id_kind, int64_t id_stride,
+               const float* dense, int64_t dense_stride, int nd,
+               const float* table, const int64_t* field_offsets,
+               const int64_t* field_vocab, int n_fields, int k, int n_cross,
+               const float* cross_prepared, int n_layers, const int* dims,
+               const int* acts, const float* mlp_prepared, float* out,
+               int64_t batch, int* err_flag, rs_stream_t stream);
+
 /* ----------------------------------------------- PNN inner product (a11)
  * InnerProductLayer.call (layer/interaction.py:170-183) on e[B,F,k]:
  *   out[b,p] = <e[b,i_p,:], e[b,j_p,:]>, pairs (i<j) in row-major order.

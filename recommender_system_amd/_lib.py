@@ -35,6 +35,8 @@ SIGNATURES = {
     "rs_cross_prepare": (I, [P, P, I, I, P, P]),
     "rs_cross_fwd": (I, [P, L, I, I, P, P, L, L, P]),
     "rs_embed_cross_fwd": (I, [P, I, L, P, L, I, P, P, P, I, I, I, P, P, L, L, P, P]),
+    "rs_dcn_fused_ok": (I, [I, I, I, I, I, P]),
+    "rs_dcn_fwd": (I, [P, I, L, P, L, I, P, P, P, I, I, I, P, I, P, P, P, P, L, P, P]),
     "rs_inner_product_fwd": (I, [P, I, I, P, L, L, P]),
     "rs_embed_inner_fwd": (I, [P, I, L, P, P, P, I, I, P, L, L, P, P]),
     "rs_outer_prepared_size": (L, [I, I]),

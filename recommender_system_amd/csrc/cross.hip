@@ -11,6 +11,7 @@
 // one fused-multiply-add pass out = alpha_L * x0 + beta_L.  x0 is read from
 // HBM once (staged in LDS), out is written once: the kernel is HBM-bound at
 // 2*d*4 bytes per sample; MFMA utilisation is at most L/16 by construction.
+#include "mlp_tower.hpp"
 #include "rs_common.hpp"
 
 namespace rs {
@@ -284,6 +285,129 @@ __global__ __launch_bounds__(16 * 64) void embed_cross(CrossArgs a, EmbedCrossAr
   cross_tile<NT, NW>(a, tile, cs, alpha, b0, rows);
 }
 
+// Fused DCN forward (model/dcn.py:24-34) in ONE launch: x0 = [dense |
+// EmbedLayer(ids)] assembled in the DNN tower's LDS tile (Keras column order,
+// row pitch t.rs); CrossNet as the usual G = X0 @ [w_0..w_{L-1}, w_o[:d]]
+// contraction (the output Dense's cross half is one more B column: the cross
+// branch's logit is alpha_L (x0.w_o) + beta_L.w_o = alpha_L g_L + h_L, x_L is
+// never formed); the DNN tower on the same tile with its last layer folded
+// with the output Dense's DNN half; head sigmoid(dnn + cross).
+template <int NT, int KIND>
+__global__ __launch_bounds__(16 * 64) void dcn_fused(CrossArgs a, EmbedCrossArgs e, MlpArgs t) {
+  constexpr int NW = 16;
+  typedef Ids<KIND> I;
+  extern __shared__ __attribute__((aligned(16))) float tsm[];
+  __shared__ typename I::raw_t lid[16][EC_FMAX];
+  __shared__ int64_t lmeta[2][EC_FMAX];
+  constexpr int CW = NT * 16 + 1;
+  __shared__ float cs[NW * 16 * CW];
+  __shared__ float xlog[16];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int s = lane & 15, kk = lane >> 4;
+  const int64_t b0 = (int64_t)blockIdx.x * 16;
+  const int rows = (int)((a.batch - b0) < 16 ? (a.batch - b0) : 16);
+  const int F = e.F, RS = t.rs, d = a.d;
+
+  // tower weights and biases first (independent of the ids)
+  floatx4 ring[4];
+  mlp_first_fill<NW>(t, ring);
+  float* par = tsm + 32 * RS + NW * 256;
+  for (int i = tid; i < t.ptot; i += NW * 64) par[i] = t.prep[t.wtot + i];
+  for (int t0 = tid; t0 < 16 * F; t0 += NW * 64) {
+    const int ss = t0 / F, c = t0 - ss * F;
+    lid[ss][c] = I::load(e.ids, (b0 + (ss < rows ? ss : rows - 1)) * e.id_stride + c);
+  }
+  for (int t0 = tid; t0 < 2 * F; t0 += NW * 64) {
+    const int c = t0 < F ? t0 : t0 - F;
+    lmeta[t0 < F ? 0 : 1][c] = t0 < F ? e.offs[c] : e.vocab[c];
+  }
+  {  // dense columns + zero padding of the tile row (wave w: sample w)
+    const int64_t bb = b0 + (w < rows ? w : rows - 1);
+    for (int j = lane; j < e.nd; j += 64) tsm[w * RS + j] = w < rows ? e.dense[bb * e.dense_stride + j] : 0.f;
+    for (int j = d + lane; j < t.Kp[0]; j += 64) tsm[w * RS + j] = 0.f;
+  }
+  __syncthreads();
+  bool bad = false;
+  {  // rows: wave w gathers sample w's F*k/4 float4 chunks into its tile row
+    const int KQ = e.k >> 2, FKQ = F * KQ;
+    const int nit = (FKQ + 63) >> 6;
+    for (int base = 0; base < nit; base += 8) {
+      floatx4 v[8];
+      int dst[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int ch = (base + u) * 64 + lane;
+        dst[u] = -1;
+        v[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (base + u < nit && ch < FKQ) {
+          const int c = ch / KQ, q = ch - c * KQ;
+          int64_t id;
+          const bool ok = I::decode(lid[w][c], lmeta[1][c], id);
+          bad |= !ok && w < rows;
+          const floatx4 x =
+              __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(e.table + (lmeta[0][c] + id) * e.k + 4 * q));
+          v[u] = (ok && w < rows) ? x : floatx4{0.f, 0.f, 0.f, 0.f};
+          dst[u] = w * RS + e.nd + c * e.k + 4 * q;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (dst[u] >= 0) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) tsm[dst[u] + q] = v[u][q];
+        }
+    }
+  }
+  if (__any(bad) && lane == 0) flag_error(e.err);
+  __syncthreads();
+
+  // CrossNet contraction G = X0 @ [w_0 .. w_{L-1}, w_o[:d]] (a.L = L + 1 columns)
+  floatx4 acc[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int t0 = w; t0 < a.DB; t0 += 8 * NW) {
+    float bv[8][NT], xv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int tt = min(t0 + u * NW, a.DB - 1);
+      const float* rec = a.img + (int64_t)tt * NT * 64;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) bv[u][nt] = rec[nt * 64 + lane];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int ee = 4 * (t0 + u * NW) + kk;
+      xv[u] = (t0 + u * NW < a.DB && ee < d) ? tsm[s * RS + ee] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(xv[u], bv[u][nt], acc[nt]);
+  }
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cs[(w * 16 + kk * 4 + r) * CW + nt * 16 + s] = acc[nt][r];
+  __syncthreads();
+  if (tid < 16) {  // alpha recurrence over the L real layers, then the cross logit
+    const int L = a.L - 1;
+    float al = 1.f;
+    for (int l = 0; l < L; ++l) {
+      float g = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) g += cs[(ww * 16 + tid) * CW + l];
+      al = fmaf(al, 1.f + g, a.h[l]);
+    }
+    float go = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) go += cs[(ww * 16 + tid) * CW + L];
+    xlog[tid] = fmaf(al, go, a.h[L]);
+  }
+  // (the tower's first barrier publishes xlog and the tile)
+  mlp_tower_tile<NW>(t, tsm, b0, ring, xlog);
+}
+
 }  // namespace rs
 
 using namespace rs;
@@ -381,4 +505,70 @@ extern "C" int rs_embed_cross_fwd(const void* ids, int id_kind, int64_t id_strid
     }
   });
   return launch_status("rs_embed_cross_fwd");
+}
+
+namespace rs {
+static bool dcn_geom(int nd, int n_fields, int k, int n_cross, int n_layers, const int* dims, MlpGeom& mg) {
+  if (nd < 0 || n_fields < 1 || n_fields > EC_FMAX || k < 4 || k % 4 != 0 || n_cross < 0 || n_cross > 31) return false;
+  if (!mlp_geom(n_layers, dims, mg)) return false;
+  const int d = nd + n_fields * k;
+  // static LDS: ids (<= 16 KB) + meta 2 KB + partials (<= 33.8 KB) + the tower's dynamic LDS
+  return dims[0] == d && dims[n_layers] == 1 && mg.lds <= 100 * 1024;
+}
+}  // namespace rs
+
+extern "C" int rs_dcn_fused_ok(int nd, int n_fields, int k, int n_cross, int n_layers, const int* dims) {
+  MlpGeom mg;
+  return dims && dcn_geom(nd, n_fields, k, n_cross, n_layers, dims, mg) ? 1 : 0;
+}
+
+extern "C" int rs_dcn_fwd(const void* ids, int id_kind, int64_t id_stride, const float* dense, int64_t dense_stride,
+                          int nd, const float* table, const int64_t* field_offsets, const int64_t* field_vocab,
+                          int n_fields, int k, int n_cross, const float* cross_prepared, int n_layers,
+                          const int* dims, const int* acts, const float* mlp_prepared, float* out, int64_t batch,
+                          int* err_flag, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
+  MlpGeom mg;
+  RS_REQUIRE(dims && acts, "rs_dcn_fwd: null dims/acts");
+  RS_REQUIRE(dcn_geom(nd, n_fields, k, n_cross, n_layers, dims, mg), "rs_dcn_fwd: unsupported shape (rs_dcn_fused_ok)");
+  RS_REQUIRE(ids && table && field_offsets && field_vocab && cross_prepared && mlp_prepared && out,
+             "rs_dcn_fwd: null pointer");
+  RS_REQUIRE(nd == 0 || dense, "rs_dcn_fwd: dense is null");
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32 && batch >= 0, "rs_dcn_fwd: bad ids");
+  RS_REQUIRE((uintptr_t)table % 16 == 0, "rs_dcn_fwd: table must be 16-B aligned");
+  MlpArgs t{};
+  RS_REQUIRE(mlp_fill_args(mg, acts, mlp_prepared, t), "rs_dcn_fwd: bad activation");
+  t.y = out;
+  t.ys = 1;
+  t.head = 1;
+  t.c0 = 1.f;
+  t.c1 = 1.f;
+  t.M = batch;
+  const int d = nd + n_fields * k, Lx = n_cross + 1;  // + the output Dense's cross column
+  const CrossGeom g = cross_geom(d, Lx);
+  CrossArgs a{nullptr, d, d, Lx, g.DB, cross_prepared, cross_prepared + g.h_off, cross_prepared + g.beta_off,
+              nullptr, 0, batch};
+  EmbedCrossArgs e{ids, id_stride, dense, dense_stride, nd, n_fields, k, table, field_offsets, field_vocab, err_flag};
+  const size_t lds = mg.lds;
+  const unsigned grid = (unsigned)((batch + 15) / 16);
+  hipStream_t st = as_stream(stream);
+  with_id_kind(id_kind, [&](auto K) {
+    constexpr int KIND = decltype(K)::value;
+    if (g.NT == 1) {
+      static size_t set1 = 64 * 1024;
+      if (lds > set1) {
+        (void)hipFuncSetAttribute((const void*)dcn_fused<1, KIND>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        set1 = lds;
+      }
+      dcn_fused<1, KIND><<<grid, 16 * 64, lds, st>>>(a, e, t);
+    } else {
+      static size_t set2 = 64 * 1024;
+      if (lds > set2) {
+        (void)hipFuncSetAttribute((const void*)dcn_fused<2, KIND>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        set2 = lds;
+      }
+      dcn_fused<2, KIND><<<grid, 16 * 64, lds, st>>>(a, e, t);
+    }
+  });
+  return launch_status("rs_dcn_fwd");
 }

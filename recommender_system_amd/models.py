@@ -217,7 +217,78 @@ class DCN(KerasModule):
             self._err.check("DCN")
         return out
 
+    # ---- one-launch forward (rs_dcn_fwd)
+    def _fused_layers(self):
+        dl = self.dense_layer
+        return list(dl.hidden_layer), dl.output_layer
+
+    def fused_ok(self):
+        hidden, last = self._fused_layers()
+        if any(l.activation not in (None, "linear", "relu", "prelu", "sigmoid") for l in hidden):
+            return False
+        dims = [self.d] + [l.units for l in hidden] + [1]
+        e = self.embed_layer
+        return bool(_lib.lib().rs_dcn_fused_ok(self.nd, e.n_fields, e.k, self.cross_layer.layer_num, len(dims) - 1,
+                                                (C.c_int * len(dims))(*dims)))
+
+    def _fused_params(self):
+        """Cross image over [w_0..w_{L-1}, w_o[:d]] and the DNN tower with its
+        last layer folded with the output Dense's DNN half (cached)."""
+        hidden, last = self._fused_layers()
+        out = self.output_layer
+        cl = self.cross_layer
+        params = list(cl.cross_weight) + list(cl.cross_bias) + [out.kernel, out.bias, last.kernel, last.bias] + \
+            [p for l in hidden for p in (l.kernel, l.bias, l.alpha) if p is not None]
+        key = tuple((p._version, p.data_ptr()) for p in params)
+        if getattr(self, "_fused_key", None) == key:
+            return self._fused
+        d = self.d
+        with torch.no_grad():
+            L = cl.layer_num
+            W = torch.cat([w.reshape(1, d) for w in cl.cross_weight] + [out.kernel[:d].reshape(1, d)]).contiguous()
+            Bb = torch.cat([b.reshape(1, d) for b in cl.cross_bias] + [torch.zeros(1, d, device=self._dev)]).contiguous()
+            n = _lib.lib().rs_cross_prepared_size(d, L + 1)
+            cross = torch.empty(n, dtype=torch.float32, device=self._dev)
+            call("rs_cross_prepare", ptr(W), ptr(Bb), d, L + 1, ptr(cross), _lib.stream())
+            wo2 = out.kernel[d:].reshape(-1, 1)                       # [out_dim, 1]
+            wf = (last.kernel @ wo2).contiguous()                     # [h_last, 1]
+            bf = (last.bias.reshape(1, -1) @ wo2).reshape(1) + out.bias.reshape(1)
+            ks = [l.kernel for l in hidden] + [wf]
+            bs = [l.bias for l in hidden] + [bf.contiguous()]
+            als = [l.alpha for l in hidden] + [None]
+            dims = [d] + [l.units for l in hidden] + [1]
+            nl = len(ks)
+            ci = (C.c_int * (nl + 1))(*dims)
+            pa = lambda ts: (C.c_void_p * nl)(*[ptr(t) for t in ts])
+            mlp = torch.empty(_lib.lib().rs_mlp_prepared_size(nl, ci), dtype=torch.float32, device=self._dev)
+            call("rs_mlp_prepare", nl, ci, pa(ks), pa(bs), pa(als), None, ptr(mlp), _lib.stream())
+            acts = [_lib.ACT[l.activation] for l in hidden] + [0]
+        self._fused = (cross, mlp, dims, acts, (W, Bb, wf, bf))
+        self._fused_key = key
+        return self._fused
+
+    def forward_fused(self, inputs, check_ids=True):
+        """DCN.call as ONE kernel (rs_dcn_fwd)."""
+        dense, ids = _split_criteo(inputs, self.nd, self._dev)
+        B = ids.shape[0]
+        e = self.embed_layer
+        cross, mlp, dims, acts, _ = self._fused_params()
+        n = len(dims) - 1
+        out = torch.empty(B, 1, dtype=torch.float32, device=self._dev)
+        call("rs_dcn_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), self.nd,
+             ptr(e.table), ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, e.k, self.cross_layer.layer_num,
+             ptr(cross), n, (C.c_int * (n + 1))(*dims), (C.c_int * n)(*acts), ptr(mlp), ptr(out), B,
+             ptr(self._err.t), _lib.stream())
+        if check_ids:
+            self._err.check("DCN")
+        return out
+
     def forward(self, inputs, check_ids=True):
+        if self.fused_ok():
+            return self.forward_fused(inputs, check_ids)
+        return self.forward_unfused(inputs, check_ids)
+
+    def forward_unfused(self, inputs, check_ids=True):
         dense, ids = _split_criteo(inputs, self.nd, self._dev)
         x = self.embed_layer.gather(ids, dense=dense, check_ids=check_ids)
         B = x.shape[0]

@@ -562,3 +562,40 @@ def test_pnn_modes_fused(gpu, mode, k, B, id_dtype):
     ref_y, ref_x = O.pnn(None, p, mode=mode, inputs=(dense, ids))
     assert_scaled_close(x, ref_x, what=f"PNN {mode} inputs")
     assert_scaled_close(y, ref_y, what=f"PNN {mode} logit")
+
+
+# ------------------------------------------------- fused DCN (rs_dcn_fwd)
+@pytest.mark.parametrize("k,L,hidden,out_dim,B,id_dtype", [(16, 3, [256, 128, 64], 1, 4096, np.int32),
+                                                           (8, 2, [40, 24], 3, 37, np.int64),
+                                                           (4, 0, [16], 1, 5, np.int32),
+                                                           (16, 20, [32], 2, 100, np.int64)])
+def test_dcn_fused(gpu, k, L, hidden, out_dim, B, id_dtype):
+    """One-launch DCN == the layer-by-layer path == the fp64 oracle."""
+    from recommender_system_amd import DCN
+    from tests.helpers import criteo_columns, dnn_params, tables_of
+    rng = np.random.default_rng(k + L + B)
+    vocabs = rng.integers(2, 3000, size=26)
+    m = DCN(criteo_columns(vocabs, embed_dim=k), hidden, out_dim, "relu", layer_num=L, embed_dim=k, seed=6)
+    with torch.no_grad():
+        for b in m.cross_layer.cross_bias:
+            b.uniform_(-0.1, 0.1)
+        for l in m.dense_layer._layers():
+            l.bias.uniform_(-0.1, 0.1)
+        m.output_layer.bias.uniform_(-0.1, 0.1)
+    assert m.fused_ok()
+    ids = random_ids(rng, B, vocabs, id_dtype)
+    dense = rng.random((B, 13)).astype(np.float32)
+    y = m.forward_fused((dense, ids))
+    y2 = m.forward_unfused((dense, ids))
+    torch.cuda.synchronize()
+    hidden_p, out_p = dnn_params(m.dense_layer)
+    p = {"tables": tables_of(m.embed_layer), "cross_w": [w.cpu().numpy() for w in m.cross_layer.cross_weight],
+         "cross_b": [b.cpu().numpy() for b in m.cross_layer.cross_bias], "dnn_hidden": hidden_p, "dnn_out": out_p,
+         "out_kernel": m.output_layer.kernel.cpu().numpy(), "out_bias": m.output_layer.bias.cpu().numpy()}
+    ref, _ = O.dcn(None, p, inputs=(dense, ids))
+    assert_rel_close(y, ref, what="fused DCN")
+    assert_rel_close(y2, ref, what="layer-by-layer DCN")
+    bad = ids.copy()
+    bad[0, 3] = vocabs[3]
+    with pytest.raises(IndexError):
+        m.forward_fused((dense, bad))
