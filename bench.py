@@ -493,7 +493,7 @@ def bench_din(args, world, rank):
     def full(i):
         model(pool[i % 8], check_ids=False)
 
-    dt2, _ = _timed(full, n2, args.warmup, world, events=False)
+    dt2, _ = _timed_graph(full, n2, args.warmup, world, chunk=8)
     return _line("DIN forward samples/sec @ batch 2048, behaviour seq len 100 (attention unit)",
                  args.steps * B / dt, "samples/s", args, world, att_ms,
                  {"workload": "din_attention_unit_from_ids", "global_batch": B, "seq_len": T, "embed_dim": k,
@@ -508,7 +508,8 @@ def bench_din(args, world, rank):
                  {"materialised_keys_path": {"samples_per_s": args.steps * B / dt_old,
                                              "ms_per_step": dt_old / args.steps * 1e3},
                   "din_forward": {"samples_per_s": n2 * B / dt2, "ms_per_step": dt2 / n2 * 1e3,
-                                  "note": "eager (host-synchronous id checks off); BN + PReLU MLP + heads"}})
+                                  "note": "graph-replayed full DIN.call (id checks off): gathers, attention "
+                                          "from ids, BN, PReLU MLP + sigmoid head"}})
 
 
 def bench_pnn(args, world, rank):
