@@ -648,26 +648,11 @@ static int grid_for(int64_t work, int block, int cap = 2048) {
   return (int)g;
 }
 
-// Waves per workgroup for the k=16 kernel: 16 by default; RS_FM_NW=4|8|16
-// overrides it (tuning experiments only).
-static int fm_nw16() {
-  static int nw = [] {
-    const char* e = getenv("RS_FM_NW");
-    const int v = e ? atoi(e) : 16;
-    return (v == 4 || v == 8 || v == 13) ? v : 16;
-  }();
-  return nw;
-}
-
 template <int KV, int NT, int KIND>
 static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st) {
+  // 16 waves per 16-sample tile (measured best at the headline shape against
+  // 4, 8 and 13 waves: every field slot has its own wave, max 2 fields/wave)
   const int grid = (int)((a.batch + 15) / 16);
-  if constexpr (KV == 4 && NT == 1) {
-    const int nw = fm_nw16();
-    if (nw == 4) { embed_fm_mfma<KV, NT, 4, KIND><<<grid, 4 * 64, 0, st>>>(a); return; }
-    if (nw == 8) { embed_fm_mfma<KV, NT, 8, KIND><<<grid, 8 * 64, 0, st>>>(a); return; }
-    if (nw == 13) { embed_fm_mfma<KV, NT, 13, KIND><<<grid, 13 * 64, 0, st>>>(a); return; }
-  }
   embed_fm_mfma<KV, NT, 16, KIND><<<grid, 16 * 64, 0, st>>>(a);
 }
 

@@ -29,25 +29,6 @@ inline hipStream_t as_stream(rs_stream_t s) { return reinterpret_cast<hipStream_
   } while (0)
 
 // ------------------------------------------------------------ device side
-// Sparse id of (row b, field c) under the Keras Embedding cast semantics.
-// Returns false (and leaves `id` unspecified) when the id is outside
-// [0, vocab): float ids are truncated toward zero first (tf.cast to int32),
-// so e.g. -0.5 -> 0 is valid and -1.0 is not.
-__device__ __forceinline__ bool load_id(const void* ids, int kind, int64_t off,
-                                        int64_t vocab, int64_t& id) {
-  if (kind == RS_ID_I32) {
-    id = static_cast<const int32_t*>(ids)[off];
-  } else if (kind == RS_ID_I64) {
-    id = static_cast<const int64_t*>(ids)[off];
-  } else {
-    const float f = static_cast<const float*>(ids)[off];
-    if (!(f > -1.0f && static_cast<double>(f) < static_cast<double>(vocab))) return false;
-    id = static_cast<int64_t>(f);
-    return true;
-  }
-  return id >= 0 && id < vocab;
-}
-
 // Compile-time id plumbing for the hot kernels (no per-lane branches):
 // KIND 0 = int32, 1 = int64, 2 = float32 (Keras int32 truncation), 3 = no ids
 // (rows already gathered).  decode() returns validity and a clamped id (0 when
