@@ -599,3 +599,51 @@ def test_dcn_fused(gpu, k, L, hidden, out_dim, B, id_dtype):
     bad[0, 3] = vocabs[3]
     with pytest.raises(IndexError):
         m.forward_fused((dense, bad))
+
+
+# --------------------------------------- full-size table: 64-bit addressing
+def test_full_size_table_addressing(gpu):
+    """The headline layout at full size — 26 x 1e7 rows x 16 fp32 = 16.6 GB,
+    byte offsets past 2^33 — through DeepFM (fused, FM logit, two-launch),
+    DCN (fused, cross) and PNN ('both').  Only the rows the batch touches are
+    written (ids drawn near the top of each field's range); the oracle works
+    on exactly those rows."""
+    from recommender_system_amd import DCN, PNN, DeepFM
+    from tests.helpers import criteo_columns, dnn_params
+    V, F, k, B = 10_000_000, 26, 16, 64
+    vocabs = [V] * F
+    rng = np.random.default_rng(99)
+    ids = np.stack([rng.integers(V - 1000, V, size=B) for _ in range(F)], 1).astype(np.int64)
+    ids[0] = V - 1
+    dense = rng.random((B, 13)).astype(np.float32)
+    cols = criteo_columns(vocabs, embed_dim=k)
+    m = DeepFM(cols, 10, 1e-4, 1e-4, [64, 32], 1, "relu", embed_dim=k, seed=1)
+    e = m.embed_layer
+    rows = (e.field_offsets.cpu().numpy()[None, :] + ids).reshape(-1)
+    assert rows.max() * k * 4 > 2 ** 33
+    vals = rng.uniform(-0.05, 0.05, size=(rows.size, k)).astype(np.float32)
+    with torch.no_grad():
+        e.table[torch.as_tensor(rows, device="cuda")] = torch.as_tensor(vals, device="cuda")
+    x_emb = e.table[torch.as_tensor(rows, device="cuda")].cpu().numpy().reshape(B, F * k)  # dup-safe
+    x = np.concatenate([dense, x_emb], 1)
+    hidden, out = dnn_params(m.dnn)
+    fm = O.fm_layer(x, m.fm.w0.cpu().numpy(), m.fm.w1.cpu().numpy(), m.fm.v.cpu().numpy())
+    ref = 1.0 / (1.0 + np.exp(-(0.5 * (fm + O.dnn_layer(x, hidden, out)))))
+    assert_rel_close(m((dense, ids)), ref, what="DeepFM fused @16.6 GB")
+    assert_rel_close(m.forward_unfused((dense, ids)), ref, what="DeepFM two-launch @16.6 GB")
+    assert_scaled_close(m.fm_logit((dense, ids)), fm, what="FM logit @16.6 GB")
+    d = DCN(cols, [32], 1, "relu", layer_num=2, embed_dim=k, seed=2)
+    d.embed_layer.table = e.table  # share the 16.6 GB table
+    ws = [w.cpu().numpy() for w in d.cross_layer.cross_weight]
+    bs = [b.cpu().numpy() for b in d.cross_layer.cross_bias]
+    assert_scaled_close(d.cross_fused((dense, ids)), O.cross_layer(x, ws, bs), what="embed+cross @16.6 GB")
+    h2, o2 = dnn_params(d.dense_layer)
+    z = np.concatenate([O.cross_layer(x, ws, bs), O.dnn_layer(x, h2, o2)], 1)
+    dref = O.dense(z, d.output_layer.kernel.cpu().numpy(), d.output_layer.bias.cpu().numpy(), "sigmoid")
+    assert_rel_close(d((dense, ids)), dref, what="DCN fused @16.6 GB")
+    p = PNN(cols, "both", [32], 1, embed_dim=k, seed=3)
+    p.embed_layer.table = e.table
+    xin = p.product_inputs((dense, ids))
+    zz = x_emb.reshape(B, F, k)
+    pref = np.concatenate([x_emb, O.inner_product_layer(zz), O.outer_product_layer(zz, p.outer_product_layer.W.cpu().numpy())], 1)
+    assert_scaled_close(xin, pref, what="PNN both @16.6 GB")
