@@ -49,9 +49,11 @@ def _dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or args.sharded:
         torch.cuda.set_device(local)
         import torch.distributed as dist
+        for key, val in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29533"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(key, val)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
@@ -59,9 +61,14 @@ def _dist_setup(args):
 
 
 def _barrier(world):
-    if world > 1:
+    if world > 1 or _dist_on():
         import torch.distributed as dist
         dist.barrier()
+
+
+def _dist_on():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
 
 
 def _max_over_ranks(x, world):
@@ -233,7 +240,7 @@ def bench_hotpath(args, world, rank):
             [{"feat": f"C{i + 1}", "feat_onehot_dim": V, "embed_dim": k} for i in range(F)]]
     ids_pool, dense_pool = _pool(B, vocabs, nd, 64, dev)
     result = {}
-    if world == 1:
+    if world == 1 and not args.sharded:
         model = rs.DeepFM(cols, kfm, 1e-4, 1e-4, [256, 128, 64], 1, "relu", embed_dim=k, seed=SEED, device=dev)
         e = model.embed_layer
         prep = model.fm.prepared(nd, F, k)
@@ -345,38 +352,82 @@ def bench_hotpath(args, world, rank):
         else:
             result["cpu_baseline"] = None
     else:
-        import torch.distributed as dist
-        from recommender_system_amd.sharded import ShardedEmbeddingFM
-        sh = ShardedEmbeddingFM(vocabs, k, nd, kfm, device=dev, seed=SEED)
-        g = torch.Generator(device=dev)
-        g.manual_seed(SEED + rank)
-        ids_pool = torch.stack([torch.randint(0, V, (B, F), generator=g, device=dev, dtype=torch.int32)
-                                for _ in range(16)])
-
-        def step(i):
-            # fixed-capacity exchange, no host sync inside the step
-            j = i % ids_pool.shape[0]
-            sh.forward(dense_pool[j], ids_pool[j], check=False)
-
-        dt, ms = _timed(step, args.steps, args.warmup, world)
-        f = sh.ops.flags(sh._bufs(B))  # any bad id / slot overflow during the timed steps?
-        dist.all_reduce(f, op=dist.ReduceOp.MAX)
-        bad, overflow = (bool(x) for x in f.tolist())
-        if bad or overflow:
-            raise RuntimeError(f"sharded bench: {'bad ids' if bad else 'slot overflow'} during timing")
-        result["exchange"] = {"protocol": "fixed-capacity slots, 2 RCCL all-to-all, no host sync",
-                              "slots_per_peer": sh._bufs(B)["cap"], "lookups_per_rank": B * F,
-                              "row_bytes_per_rank_each_way": world * sh._bufs(B)["cap"] * k * 4}
-        result["value"] = world * args.steps * B / dt
-        result["ms_per_step"] = dt / args.steps * 1e3
-        step_ms = _max_over_ranks(float(np.mean(ms)), world)
-        alg = B * 1824 + 18880
-        result["roofline"] = {"bound": "hbm", "achieved": alg / (step_ms * 1e-3) / 1e9, "peak": PEAK_HBM / 1e9,
-                              "unit": "GB/s", "frac": alg / (step_ms * 1e-3) / PEAK_HBM, "traffic": None,
-                              "kernel": "sharded step (slot bucketize + 2x RCCL all-to-all + gather + FM)",
-                              "kernel_ms_avg": step_ms}
-        result["cpu_baseline"] = None
+        result.update(bench_sharded(args, world, rank, vocabs, dense_pool))
     return result
+
+
+def _graph_capturable(fn, first):
+    """Capture (never replay) one step in a HIP graph on every rank, then agree
+    collectively: the RCCL all-to-alls are graph-captured only if every rank
+    captured cleanly, otherwise every rank times the eager step."""
+    import torch.distributed as dist
+    ok, why = 1, None
+    try:
+        _capture(fn, first, 1)
+    except Exception as e:  # noqa: BLE001 - any capture failure selects the eager path
+        ok, why = 0, f"{type(e).__name__}: {e}"[:200]
+    torch.cuda.synchronize()
+    t = torch.tensor([ok], dtype=torch.int32, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item()), why
+
+
+def bench_sharded(args, world, rank, vocabs, dense_pool):
+    """BASELINE config 5 shape: the table row-sharded over the ranks, each rank
+    B local samples (weak scaling), fixed-capacity slot exchange with two RCCL
+    all-to-alls (sharded.py).  The step (3 bucketize kernels, all-to-all,
+    gather, all-to-all, FM) is replayed from HIP graphs when RCCL capture works
+    on every rank (decided collectively), eager otherwise.  With --sharded at
+    world 1 the all-to-alls still run (RCCL self-exchange): the N=1 point of
+    the same curve."""
+    import torch.distributed as dist
+    from recommender_system_amd.sharded import ShardedEmbeddingFM
+    B, F, k, nd = args.batch, len(vocabs), 16, 13
+    dev = torch.device("cuda")
+    sh = ShardedEmbeddingFM(vocabs, k, nd, 10, device=dev, seed=SEED)
+    sh._force_exchange = True
+    g = torch.Generator(device=dev)
+    g.manual_seed(SEED + rank)
+    ids_pool = torch.stack([torch.randint(0, vocabs[0], (B, F), generator=g, device=dev, dtype=torch.int32)
+                            for _ in range(16)])
+    out = torch.empty(B, 1, device=dev)
+
+    def step(i):
+        # fixed-capacity exchange, no host sync inside the step
+        j = i % ids_pool.shape[0]
+        sh.forward(dense_pool[j], ids_pool[j], check=False, out=out)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    _barrier(world)
+    graphed, why = _graph_capturable(step, args.warmup)
+    if graphed:
+        dt, slot_ms = _timed_graph(step, args.steps, 0, world, chunk=16)
+        step_ms = _max_over_ranks(slot_ms, world)
+    else:
+        dt, ms = _timed(step, args.steps, 0, world)
+        step_ms = _max_over_ranks(float(np.mean(ms)), world)
+    f = sh.ops.flags(sh._bufs(B))  # any bad id / slot overflow during the timed steps?
+    dist.all_reduce(f, op=dist.ReduceOp.MAX)
+    bad, overflow = (bool(x) for x in f.tolist())
+    if bad or overflow:
+        raise RuntimeError(f"sharded bench: {'bad ids' if bad else 'slot overflow'} during timing")
+    bufs = sh._bufs(B)
+    res = {"exchange": {"protocol": "fixed-capacity slots, 2 RCCL all-to-all, no host sync",
+                        "timing": "HIP graph replay (RCCL captured)" if graphed else f"eager launches ({why})",
+                        "slots_per_peer": bufs["cap"], "lookups_per_rank": B * F,
+                        "row_bytes_per_rank_each_way": world * bufs["cap"] * k * 4,
+                        "rows_per_rank": sh.rows_per_rank}}
+    res["value"] = world * args.steps * B / dt
+    res["ms_per_step"] = dt / args.steps * 1e3
+    alg = B * 1824 + 18880
+    res["roofline"] = {"bound": "hbm", "achieved": alg / (step_ms * 1e-3) / 1e9, "peak": PEAK_HBM / 1e9,
+                       "unit": "GB/s", "frac": alg / (step_ms * 1e-3) / PEAK_HBM, "traffic": None,
+                       "kernel": "sharded step (slot bucketize + 2x RCCL all-to-all + gather + FM)",
+                       "kernel_ms_avg": step_ms}
+    res["cpu_baseline"] = None
+    return res
 
 
 def _line(metric, value, unit, args, world, ms_per_step, config, roofline, extra=None, dtype="f32", hib=True):
@@ -594,6 +645,8 @@ def main():
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--sharded", action="store_true",
+                    help="time the row-sharded exchange path even at world 1 (N=1 point of the sharded curve)")
     args = ap.parse_args()
     world, rank = _dist_setup(args)
     other = {"dcn": bench_dcn, "din": bench_din, "pnn": bench_pnn}
@@ -613,17 +666,17 @@ def main():
             "value": res["value"], "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": res["ms_per_step"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "deepfm_embed_fm_hotpath" if world == 1 else "deepfm_embed_fm_rowsharded",
+            "config": {"workload": "deepfm_embed_fm_hotpath" if world == 1 and not args.sharded else "deepfm_embed_fm_rowsharded",
                        "global_batch": args.batch * world, "batch_per_gpu": args.batch, "sparse_fields": 26,
                        "vocab_per_field": int(args.vocab), "embed_dim": 16, "fm_k": 10, "dense_features": 13,
-                       "ids": "int32 uniform per field", "parallelism": f"dp{world}" + ("+rowshard" if world > 1 else "")},
+                       "ids": "int32 uniform per field", "parallelism": f"dp{world}" + ("+rowshard" if world > 1 or args.sharded else "")},
             "roofline": res["roofline"], "cpu_baseline": res["cpu_baseline"],
         }
-        for key in ("concurrent_batches", "zipf_ids", "deepfm_forward"):
+        for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "exchange"):
             if key in res:
                 line[key] = res[key]
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if _dist_on():
         import torch.distributed as dist
         dist.destroy_process_group()
 

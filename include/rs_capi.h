@@ -319,7 +319,10 @@ int rs_sigmoid_combine(const float* a, const float* b, float c0, float c1,
  *  rs_shard_bucketize: counts[r] = #lookups owned by rank r; perm[i] = the
  *   position of lookup i (= b*F + c) in owner-major order; send_rows[perm[i]]
  *   = local row index on the owner.  Stable within each owner.
- *   workspace: rs_shard_workspace_size(batch*n_fields, world) bytes, device.
+ *   workspace: rs_shard_workspace_size(batch*n_fields, world) bytes, device,
+ *   zero-filled once when allocated (its tail holds the control words of the
+ *   one-pass slotted kernel, which leaves them ready for the next call); one
+ *   workspace per stream — concurrent calls must not share it.
  *  rs_gather_rows: out[i] = table[rows[i]] (k floats), local shard.
  *  rs_unpermute_rows: dst[i] = src[perm[i]] (k floats per row).            */
 int64_t rs_shard_workspace_size(int64_t n_lookups, int world);
@@ -340,7 +343,9 @@ int rs_shard_bucketize(const void* ids, int id_kind, int64_t id_stride,
  * step with the exact protocol) or its id is out of range (*err_flag set).
  * The returned rows are then addressed by slot_of as int32 ids of a single
  * [world*cap, k] table: rs_embed_fm_fwd(ids = slot_of, offsets 0, vocab
- * world*cap) computes the FM straight from the exchange buffer.            */
+ * world*cap) computes the FM straight from the exchange buffer.
+ * One launch: stable per-owner ranks in LDS + a decoupled look-back over the
+ * preceding blocks' per-owner totals (single-pass chained scan).            */
 int rs_shard_slot_bucketize(const void* ids, int id_kind, int64_t id_stride,
                             const int64_t* field_offsets,
                             const int64_t* field_vocab, int n_fields,

@@ -170,6 +170,133 @@ __global__ __launch_bounds__(SH_THREADS) void shard_place(ShardArgs a, const int
   }
 }
 
+// ---------------------------------------------------------------- one pass
+// Slotted bucketize in ONE launch (replaces hist -> scan -> place when cap > 0):
+// a workgroup takes SP_PER consecutive lookups (one per thread per round),
+// ranks them stably per owner in LDS (wave ballots), and gets the number of
+// earlier lookups of every owner by a decoupled look-back over its
+// predecessors' published per-owner totals (single-pass chained scan).  The
+// result is identical to the three-kernel form: stable slot order.
+//   status[b][o] (u64): [63:62] 1 = aggregate of block b, 2 = inclusive prefix
+//   through block b; [61:32] launch epoch; [31:0] value.
+//   ctrl (u64): [63:32] epoch, [31:0] block ticket.  Blocks take dynamic ids
+//   (a block only ever waits on blocks that have already started); the block
+//   that draws the launch's last ticket re-arms ctrl to (epoch + 1, 0) — every
+//   ticket of this launch is drawn by then — so the next launch needs no
+//   memset (graph-replay safe).  The ids of block blockIdx.x are loaded while
+//   the ticket is in flight and kept when the ticket matches (in-order
+//   dispatch, the common case).
+constexpr int SP_THREADS = 1024;
+constexpr int SP_PER = SP_THREADS;
+
+__device__ __forceinline__ uint64_t sp_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sp_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(SP_THREADS) void shard_slot_onepass(ShardArgs a, uint64_t* status, uint64_t* ctrl,
+                                                                 int nb, int32_t* counts, int32_t* slot_of,
+                                                                 int32_t* send, int cap, int* overflow, int mode) {
+  constexpr int NW = SP_THREADS / 64;
+  __shared__ int wcnt[NW][SH_MAXW];
+  __shared__ int excl[SH_MAXW];
+  __shared__ uint64_t sh_tk;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    if (mode & 1) {
+      sh_tk = blockIdx.x;
+    } else {
+      // relaxed: an agent-scope release/acquire would write back / invalidate L2
+      const uint64_t t = __hip_atomic_fetch_add(ctrl, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((uint32_t)t == (uint32_t)nb - 1)
+        __hip_atomic_store(ctrl, ((t >> 32) + 1) << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sh_tk = t;
+    }
+  }
+  for (int i = threadIdx.x; i < NW * SH_MAXW; i += SP_THREADS) (&wcnt[0][0])[i] = 0;
+  // speculative: this block's lookups as if the ticket equals blockIdx.x
+  int64_t i = (int64_t)blockIdx.x * SP_PER + threadIdx.x;
+  int64_t loc = -1;
+  int o = i < a.n ? shard_owner(a, i, loc) : -1;
+  __syncthreads();
+  const int bid = (int)(uint32_t)sh_tk;
+  const uint64_t ep = ((sh_tk >> 32) & 0x3fffffffull) << 32;
+  if (bid != (int)blockIdx.x) {  // out-of-order dispatch: redo for the ticket
+    i = (int64_t)bid * SP_PER + threadIdx.x;
+    loc = -1;
+    o = i < a.n ? shard_owner(a, i, loc) : -1;
+  }
+  // stable in-block rank: peel one owner at a time per wave
+  const bool act = o >= 0;
+  int rank = 0;
+  uint64_t todo = __ballot(act);
+  while (todo) {
+    const int leader = __ffsll((unsigned long long)todo) - 1;
+    const int lo = __shfl(o, leader);
+    const uint64_t m = __ballot(act && o == lo);
+    if (act && o == lo) rank = __popcll(m & ((1ull << lane) - 1));
+    if (lane == 0) wcnt[w][lo] = __popcll(m);
+    todo &= ~m;
+  }
+  __syncthreads();
+  // per owner (wave o, o + NW, ...): this block's total, published at once,
+  // then a look-back over 128 predecessors per step (two per lane) that stops
+  // at the nearest published inclusive prefix
+  for (int oo = w; oo < a.world; oo += NW) {
+    int agg = 0;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) agg += wcnt[ww][oo];
+    uint64_t* st_o = status + oo;
+    if (lane == 0) sp_store(st_o + (int64_t)bid * a.world, ((bid == 0 ? 2ull : 1ull) << 62) | ep | (uint32_t)agg);
+    int before = 0;
+    for (int hi = (mode & 2) ? -1 : bid - 1; hi >= 0; hi -= 128) {
+      const int p0 = hi - lane, p1 = hi - 64 - lane;
+      uint64_t v0 = 0, v1 = 0;
+      bool r0 = p0 < 0, r1 = p1 < 0;
+      while (!__all(r0 && r1)) {
+        if (!r0) v0 = sp_load(st_o + (int64_t)p0 * a.world);
+        if (!r1) v1 = sp_load(st_o + (int64_t)p1 * a.world);
+        r0 = r0 || ((v0 & 0x3fffffff00000000ull) == ep && (v0 >> 62) != 0);
+        r1 = r1 || ((v1 & 0x3fffffff00000000ull) == ep && (v1 >> 62) != 0);
+      }
+      const uint64_t pm0 = __ballot(p0 >= 0 && (v0 >> 62) == 2);
+      const uint64_t pm1 = __ballot(p1 >= 0 && (v1 >> 62) == 2);
+      // nearest inclusive prefix: lowest lane of window 0, else of window 1
+      const int stop = pm0 ? __ffsll((unsigned long long)pm0) - 1
+                           : (pm1 ? 64 + __ffsll((unsigned long long)pm1) - 1 : 127);
+      int val = (p0 >= 0 && lane <= stop ? (int)(uint32_t)v0 : 0) +
+                (p1 >= 0 && 64 + lane <= stop ? (int)(uint32_t)v1 : 0);
+#pragma unroll
+      for (int d = 32; d > 0; d >>= 1) val += __shfl_xor(val, d);
+      before += val;
+      if (pm0 | pm1) break;
+    }
+    if (lane == 0) {
+      if (bid > 0) sp_store(st_o + (int64_t)bid * a.world, (2ull << 62) | ep | (uint32_t)(before + agg));
+      excl[oo] = before;
+      if (bid == nb - 1) counts[oo] = before + agg;
+    }
+  }
+  __syncthreads();
+  if (i < a.n) {
+    if (o < 0 || loc < 0) {  // out-of-range id (shard_owner raised *err)
+      slot_of[i] = -1;
+    } else {
+      int pos = excl[o] + rank;
+      for (int ww = 0; ww < w; ++ww) pos += wcnt[ww][o];
+      if (pos >= cap) {
+        flag_error(overflow);
+        slot_of[i] = -1;
+      } else {
+        slot_of[i] = o * cap + pos;
+        send[(int64_t)o * cap + pos] = (int32_t)loc;
+      }
+    }
+  }
+}
+
 template <int VW>
 __global__ void gather_rows_kernel(const float* __restrict__ table, int64_t n_rows, int k,
                                    const int32_t* __restrict__ rows, int64_t n, float* __restrict__ out, int* err) {
@@ -211,6 +338,21 @@ __global__ void unpermute_rows_kernel(const float* __restrict__ src, const int32
   }
 }
 
+// k = 16 fast path (the configs' dim): 4 lanes per row, one float4 each,
+// 32-bit indexing, every load issued before any store
+__global__ __launch_bounds__(256) void gather_rows_k16(const float* __restrict__ table, int64_t n_rows,
+                                                       const int32_t* __restrict__ rows, int n,
+                                                       float* __restrict__ out, int* err) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  const int i = idx >> 2, q = idx & 3;
+  if (i >= n) return;
+  const int64_t r = rows[i];
+  floatx4 x = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (r >= 0 && r < n_rows) x = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(table + r * 16) + q);
+  else if (r != -1 && q == 0) flag_error(err);
+  reinterpret_cast<floatx4*>(out)[idx] = x;
+}
+
 static unsigned sh_grid(int64_t work) {
   int64_t g = (work + 255) / 256;
   if (g > 8192) g = 8192;
@@ -221,10 +363,22 @@ static unsigned sh_grid(int64_t work) {
 
 using namespace rs;
 
+// diagnostic timing modes of shard_slot_onepass (scripts only; 0 = product):
+// bit0 blockIdx instead of the ticket, bit1 no look-back (wrong slots: timing only)
+static int g_sp_mode = 0;
+extern "C" void rs_diag_shard_set_mode(int m) { g_sp_mode = m; }
+
+// workspace = [hist (int32 per 256-lookup block and owner) | status (u64 per
+// 1024-lookup block and owner) share one region][256 B control words]
+static int64_t sh_ctrl_offset(int64_t n_lookups, int world) {
+  const int64_t hist = (n_lookups + SH_CHUNK - 1) / SH_CHUNK * world * 4;
+  const int64_t stat = (n_lookups + SP_PER - 1) / SP_PER * world * 8;
+  return (((hist > stat ? hist : stat) + 255) / 256) * 256;
+}
+
 extern "C" int64_t rs_shard_workspace_size(int64_t n_lookups, int world) {
   if (n_lookups < 0 || world < 1 || world > SH_MAXW) return -1;
-  const int64_t nb = (n_lookups + SH_CHUNK - 1) / SH_CHUNK;
-  return ((nb * world * 4 + 255) / 256) * 256 + 256;
+  return sh_ctrl_offset(n_lookups, world) + 256;
 }
 
 extern "C" int rs_shard_bucketize(const void* ids, int id_kind, int64_t id_stride, const int64_t* field_offsets,
@@ -273,9 +427,12 @@ extern "C" int rs_shard_slot_bucketize(const void* ids, int id_kind, int64_t id_
     (void)hipMemsetAsync(counts, 0, world * sizeof(int32_t), st);
     return launch_status("rs_shard_slot_bucketize");
   }
-  shard_hist<<<nb, SH_THREADS, 0, st>>>(a, hist);
-  shard_scan<<<1, 256, 0, st>>>(hist, nb, world, counts, cap);
-  shard_place<<<nb, SH_THREADS, 0, st>>>(a, hist, slot_of, send_slots, cap, overflow_flag);
+  (void)hist;
+  const int nbp = (int)((a.n + SP_PER - 1) / SP_PER);
+  uint8_t* ws = static_cast<uint8_t*>(workspace);
+  shard_slot_onepass<<<nbp, SP_THREADS, 0, st>>>(a, reinterpret_cast<uint64_t*>(ws),
+                                                 reinterpret_cast<uint64_t*>(ws + sh_ctrl_offset(a.n, world)), nbp,
+                                                 counts, slot_of, send_slots, cap, overflow_flag, g_sp_mode);
   return launch_status("rs_shard_slot_bucketize");
 }
 
@@ -286,7 +443,9 @@ extern "C" int rs_gather_rows(const float* table, int64_t n_rows, int k, const i
   RS_REQUIRE(k >= 1 && n >= 0 && n_rows >= 0, "rs_gather_rows: bad shape");
   if (n == 0) return RS_OK;
   hipStream_t st = as_stream(stream);
-  if (k % 4 == 0 && (uintptr_t)table % 16 == 0 && (uintptr_t)out % 16 == 0)
+  if (k == 16 && n < (1 << 29) && (uintptr_t)table % 16 == 0 && (uintptr_t)out % 16 == 0)
+    gather_rows_k16<<<(unsigned)((n * 4 + 255) / 256), 256, 0, st>>>(table, n_rows, rows, (int)n, out, err_flag);
+  else if (k % 4 == 0 && (uintptr_t)table % 16 == 0 && (uintptr_t)out % 16 == 0)
     gather_rows_kernel<4><<<sh_grid(n * (k / 4)), 256, 0, st>>>(table, n_rows, k, rows, n, out, err_flag);
   else
     gather_rows_kernel<1><<<sh_grid(n * k), 256, 0, st>>>(table, n_rows, k, rows, n, out, err_flag);

@@ -57,7 +57,7 @@ class HipShardOps:
         send_rows = torch.empty(n, dtype=torch.int32, device=self.device)
         wsz = _lib.lib().rs_shard_workspace_size(n, world)
         if self._ws is None or self._ws.numel() < wsz:
-            self._ws = torch.empty(wsz, dtype=torch.uint8, device=self.device)
+            self._ws = torch.zeros(wsz, dtype=torch.uint8, device=self.device)  # zeroed once (rs_capi.h)
         call("rs_shard_bucketize", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(offsets), ptr(vocab), F, B,
              rows_per_rank, world, ptr(counts), ptr(perm), ptr(send_rows), ptr(self._ws), ptr(self.err),
              _lib.stream())
@@ -69,7 +69,7 @@ class HipShardOps:
         if bufs.get("ws_n") != (n, world):
             wsz = _lib.lib().rs_shard_workspace_size(n, world)
             if self._ws is None or self._ws.numel() < wsz:
-                self._ws = torch.empty(wsz, dtype=torch.uint8, device=self.device)
+                self._ws = torch.zeros(wsz, dtype=torch.uint8, device=self.device)  # zeroed once (rs_capi.h)
             bufs["ws_n"] = (n, world)
         call("rs_shard_slot_bucketize", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(offsets), ptr(vocab), F, B,
              rows_per_rank, world, cap, ptr(bufs["counts"]), ptr(bufs["slot_of"]), ptr(bufs["send"]), ptr(self._ws),
@@ -81,11 +81,11 @@ class HipShardOps:
              ptr(self.err), _lib.stream())
         return out
 
-    def slots_fm(self, got, slot_of, dense, n_fields, k, prepared, w0, kfm, bufs):
+    def slots_fm(self, got, slot_of, dense, n_fields, k, prepared, w0, kfm, bufs, out=None):
         """FM logit with lookup (b, c)'s row at got[slot_of[b*F + c]]: the
         headline kernel with ids = slots, zero field offsets, vocab = #slots."""
         B = dense.shape[0]
-        logit = torch.empty(B, 1, dtype=torch.float32, device=self.device)
+        logit = out if out is not None else torch.empty(B, 1, dtype=torch.float32, device=self.device)
         call("rs_embed_fm_fwd", ptr(slot_of), _lib.ID_I32, n_fields, ptr(dense), dense.stride(0), dense.shape[1],
              ptr(got), ptr(bufs["zoff"]), ptr(bufs["nslots"]), n_fields, k, ptr(prepared), ptr(w0), kfm, ptr(logit),
              None, B, ptr(bufs["overflow"]), _lib.stream())
@@ -156,6 +156,9 @@ class ShardedEmbeddingFM:
         self.v = (torch.randn(d, self.kfm, generator=gen) * 0.05).to(self.device)
         self.ops = ops if ops is not None else HipShardOps(self.device)
         self.prepared = None
+        # world 1 skips the all-to-alls (a self-exchange is a copy); the bench
+        # sets this to time the RCCL self-exchange as the N=1 point of its curve
+        self._force_exchange = False
         if isinstance(self.ops, HipShardOps):
             self.prepare()
 
@@ -198,13 +201,14 @@ class ShardedEmbeddingFM:
         bufs = self._bufs(B)
         slot_of, send = self.ops.slot_bucketize(ids, self.offsets, self.vocab, self.rows_per_rank, self.world,
                                                 bufs["cap"], bufs)
-        if self.world == 1:
+        exchange = self.world > 1 or self._force_exchange
+        if not exchange:
             recv = send
         else:
             recv = bufs["recv"]
             dist.all_to_all_single(recv, send, group=self.group)
         reply = self.ops.gather_rows_into(self.table_shard, recv, bufs["reply"])
-        if self.world == 1:
+        if not exchange:
             got = reply
         else:
             got = bufs["got"]
@@ -233,12 +237,14 @@ class ShardedEmbeddingFM:
         emb = self.lookup(ids)
         return self.ops.rows_fm(emb, dense, self.F, self.k, self.prepared, self.w0, self.kfm)
 
-    def forward(self, dense, ids, check=True):
-        """FM logit [B,1] of the local batch.  check=True: one host sync at the
-        end of the step; a slot overflow is redone exactly, a bad id raises."""
+    def forward(self, dense, ids, check=True, out=None):
+        """FM logit [B,1] of the local batch (into ``out`` if given).
+        check=True: one host sync at the end of the step; a slot overflow is
+        redone exactly, a bad id raises."""
         got, slot_of = self.exchange_slots(ids)
         bufs = self._bufs(ids.shape[0])
-        logit = self.ops.slots_fm(got, slot_of, dense, self.F, self.k, self.prepared, self.w0, self.kfm, bufs)
+        logit = self.ops.slots_fm(got, slot_of, dense, self.F, self.k, self.prepared, self.w0, self.kfm, bufs,
+                                  out=out)
         if check:
             # collective decision: every rank must take the same branch (the
             # exact fallback runs collectives; a lone raise would strand peers)

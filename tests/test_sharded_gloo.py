@@ -60,7 +60,7 @@ class CpuOps:
         got[r < 0] = 0
         return got
 
-    def slots_fm(self, got, slot_of, dense, F, k, prepared, w0, kfm, bufs=None):
+    def slots_fm(self, got, slot_of, dense, F, k, prepared, w0, kfm, bufs=None, out=None):
         self.last_emb = got[slot_of.long()]
         return None
 
