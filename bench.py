@@ -374,12 +374,17 @@ def _graph_capturable(fn, first):
 
 def bench_sharded(args, world, rank, vocabs, dense_pool):
     """BASELINE config 5 shape: the table row-sharded over the ranks, each rank
-    B local samples (weak scaling), fixed-capacity slot exchange with two RCCL
-    all-to-alls (sharded.py).  The step (3 bucketize kernels, all-to-all,
-    gather, all-to-all, FM) is replayed from HIP graphs when RCCL capture works
-    on every rank (decided collectively), eager otherwise.  With --sharded at
-    world 1 the all-to-alls still run (RCCL self-exchange): the N=1 point of
-    the same curve."""
+    B local samples (weak scaling).  Timed protocol (the value): owner-side FM
+    partials, pipelined (sharded.py ``pipe_step``): per batch t, field route
+    of t -> ONE RCCL all-to-all carrying [row ids of t | FM partials of t-1]
+    -> combine of t-1 -> owner FM partials of t over its field range (steady
+    state: every step does one batch's full work).  Also timed: the same
+    protocol unpipelined (``forward``: two all-to-alls per batch) and the
+    fixed-capacity ROW exchange (``forward_slots``), which returns every
+    lookup's 64-B row to the requester.  Steps are replayed from HIP graphs
+    when RCCL capture works on every rank (decided collectively), eager
+    otherwise.  With --sharded at world 1 the all-to-alls still run (RCCL
+    self-exchange): the N=1 point of the same curve."""
     import torch.distributed as dist
     from recommender_system_amd.sharded import ShardedEmbeddingFM
     B, F, k, nd = args.batch, len(vocabs), 16, 13
@@ -391,40 +396,68 @@ def bench_sharded(args, world, rank, vocabs, dense_pool):
     ids_pool = torch.stack([torch.randint(0, vocabs[0], (B, F), generator=g, device=dev, dtype=torch.int32)
                             for _ in range(16)])
     out = torch.empty(B, 1, device=dev)
+    outs = [torch.empty(B, 1, device=dev) for _ in range(2)]
+    npool = ids_pool.shape[0]
 
-    def step(i):
-        # fixed-capacity exchange, no host sync inside the step
-        j = i % ids_pool.shape[0]
-        sh.forward(dense_pool[j], ids_pool[j], check=False, out=out)
+    def pipelined(i):
+        j, jp = i % npool, (i - 1) % npool
+        sh.pipe_step(cur=(dense_pool[j], ids_pool[j]), prev=(dense_pool[jp], outs[(i - 1) % 2]))
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    _barrier(world)
-    graphed, why = _graph_capturable(step, args.warmup)
-    if graphed:
-        dt, slot_ms = _timed_graph(step, args.steps, 0, world, chunk=16)
-        step_ms = _max_over_ranks(slot_ms, world)
-    else:
-        dt, ms = _timed(step, args.steps, 0, world)
-        step_ms = _max_over_ranks(float(np.mean(ms)), world)
-    f = sh.ops.flags(sh._bufs(B))  # any bad id / slot overflow during the timed steps?
+    def per_batch(fwd):
+        def step(i):
+            # fixed-size exchange, no host sync inside the step
+            j = i % npool
+            fwd(dense_pool[j], ids_pool[j], check=False, out=out)
+        return step
+
+    def run(step):
+        for i in range(args.warmup):
+            step(i)
+        torch.cuda.synchronize()
+        _barrier(world)
+        graphed, why = _graph_capturable(step, args.warmup)
+        if graphed:
+            dt, slot_ms = _timed_graph(step, args.steps, 0, world, chunk=16)
+            step_ms = _max_over_ranks(slot_ms, world)
+        else:
+            dt, ms = _timed(step, args.steps, 0, world)
+            step_ms = _max_over_ranks(float(np.mean(ms)), world)
+        return dt, step_ms, ("HIP graph replay (RCCL captured)" if graphed else f"eager launches ({why})")
+
+    dt, step_ms, timing = run(pipelined)
+    udt, ustep_ms, utiming = run(per_batch(sh.forward))
+    f = sh.ops.bad_flag()  # any bad id during the timed steps?
     dist.all_reduce(f, op=dist.ReduceOp.MAX)
-    bad, overflow = (bool(x) for x in f.tolist())
-    if bad or overflow:
-        raise RuntimeError(f"sharded bench: {'bad ids' if bad else 'slot overflow'} during timing")
+    if bool(f.item()):
+        raise RuntimeError("sharded bench: bad ids during timing")
+    # reference point: the same step with the row exchange
+    rdt, rstep_ms, rtiming = run(per_batch(sh.forward_slots))
+    fl = sh.ops.flags(sh._bufs(B))
+    dist.all_reduce(fl, op=dist.ReduceOp.MAX)
     bufs = sh._bufs(B)
-    res = {"exchange": {"protocol": "fixed-capacity slots, 2 RCCL all-to-all, no host sync",
-                        "timing": "HIP graph replay (RCCL captured)" if graphed else f"eager launches ({why})",
-                        "slots_per_peer": bufs["cap"], "lookups_per_rank": B * F,
-                        "row_bytes_per_rank_each_way": world * bufs["cap"] * k * 4,
-                        "rows_per_rank": sh.rows_per_rank}}
+    S, P = sh.slot_stride, sh.partial_width
+    res = {"exchange": {
+        "protocol": "owner-side FM partials, pipelined: field route(t), ONE RCCL all-to-all of [row ids of t | "
+                    "FM partials of t-1] records, combine(t-1), owner FM partials(t) over its field range; fixed "
+                    "sizes, no host sync",
+        "timing": timing, "lookups_per_rank": B * F, "rows_per_rank": sh.rows_per_rank,
+        "owner_field_ranges": sh.owner_field_ranges,
+        "bytes_per_rank_each_way": world * B * (S + P) * 4,
+        "unpipelined": {"samples_per_s": world * args.steps * B / udt, "ms_per_step": udt / args.steps * 1e3,
+                        "timing": utiming, "id_bytes_per_rank_each_way": world * B * S * 4,
+                        "partial_bytes_per_rank_each_way": world * B * P * 4,
+                        "note": "forward(): route, all-to-all ids, owner partials, all-to-all partials, combine"},
+        "rows_protocol": {"samples_per_s": world * args.steps * B / rdt, "ms_per_step": rdt / args.steps * 1e3,
+                          "timing": rtiming, "slots_per_peer": bufs["cap"],
+                          "row_bytes_per_rank_each_way": world * bufs["cap"] * k * 4,
+                          "overflow_during_timing": bool(fl[1].item()),
+                          "note": "fixed-capacity row exchange (forward_slots): rows back to the requester"}}}
     res["value"] = world * args.steps * B / dt
     res["ms_per_step"] = dt / args.steps * 1e3
     alg = B * 1824 + 18880
     res["roofline"] = {"bound": "hbm", "achieved": alg / (step_ms * 1e-3) / 1e9, "peak": PEAK_HBM / 1e9,
                        "unit": "GB/s", "frac": alg / (step_ms * 1e-3) / PEAK_HBM, "traffic": None,
-                       "kernel": "sharded step (slot bucketize + 2x RCCL all-to-all + gather + FM)",
+                       "kernel": "sharded step (field route + RCCL all-to-all + owner FM partials + combine)",
                        "kernel_ms_avg": step_ms}
     res["cpu_baseline"] = None
     return res

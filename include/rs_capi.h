@@ -359,6 +359,55 @@ int rs_gather_rows(const float* table, int64_t n_rows, int k,
 int rs_unpermute_rows(const float* src, const int32_t* perm, int k, int64_t n,
                       float* dst, rs_stream_t stream);
 
+/* ------------------- row-sharded FM, partial protocol (§8(e), default)
+ * A block split of the concatenated table gives every owner o a contiguous
+ * FIELD range [field_lo(o), field_lo(o) + n_owned(o)).  Instead of returning
+ * 64-B rows, the owner returns per-sample FM partials over the fields it
+ * holds (the FM's first stage x@[v|w1] and x^2@|v|^2 is linear in the rows),
+ * and the requester finishes the FM (FMLayer.call, layer/interaction.py:
+ * 106-114; EmbedLayer.call, layer/core.py:273-280, for the lookup):
+ *  rs_fm_partial_width(kfm): floats per partial record, P = roundup(kfm+2, 4):
+ *   [s_0 .. s_{kfm-1}, x@w1, sum_i x_i^2 |v_i|^2, 0-pad].
+ *  rs_shard_field_route: owner_fields [world][2] int32 = (field_lo, n_owned)
+ *   per owner; send = world*batch records of rec_stride int32 words (owner-
+ *   major), word j < slot_stride (slot_stride >= every n_owned) of record
+ *   (o, b) = local row of lookup (b, field_lo(o)+j) when o owns it, else -1.
+ *   Those words are all written; words >= slot_stride are left untouched;
+ *   out-of-range id -> *err_flag.
+ *  rs_shard_owner_fm: local_rows = n_pairs records of rec_stride words (the
+ *   received messages, requester-major), the owner's shard [shard_rows, k]
+ *   and the packed FM image of the WHOLE model (rs_fm_prepare with nd,
+ *   n_fields) -> partial records (P floats, partial_stride floats apart) over
+ *   fields field_lo .. field_lo+n_owned-1 (-1 rows contribute 0; a local row
+ *   >= shard_rows sets *err_flag).
+ *  rs_shard_fm_combine: partial records [world][batch] (partial_stride floats
+ *   apart, one block per owner) + dense [batch, nd] -> logit[batch]; owners
+ *   summed in rank order.
+ *  A pipelined exchange interleaves both messages in ONE buffer: record
+ *   (peer, b) = [slot_stride row ids of batch t | P partial floats of batch
+ *   t-1], rec_stride = partial_stride = slot_stride + P, partials at +slot_stride
+ *   words: one all-to-all per batch (sharded.py forward_stream).            */
+int rs_fm_partial_width(int kfm);
+int rs_shard_field_route(const void* ids, int id_kind, int64_t id_stride,
+                         const int64_t* field_offsets,
+                         const int64_t* field_vocab, int n_fields,
+                         int64_t batch, int64_t rows_per_rank, int world,
+                         const int32_t* owner_fields, int slot_stride,
+                         int64_t rec_stride, int32_t* send, int* err_flag,
+                         rs_stream_t stream);
+int rs_shard_owner_fm(const int32_t* local_rows, int64_t rec_stride,
+                      int field_lo, int n_owned, const float* shard,
+                      int64_t shard_rows, int nd, int n_fields, int k,
+                      const float* prepared, int kfm, float* partial,
+                      int64_t partial_stride, int64_t n_pairs, int* err_flag,
+                      rs_stream_t stream);
+int rs_shard_fm_combine(const float* partials, int64_t partial_stride,
+                        int world, int64_t batch,
+                        const float* dense, int64_t dense_stride, int nd,
+                        int n_fields, int k, const float* prepared,
+                        const float* w0, int kfm, float* logit,
+                        rs_stream_t stream);
+
 /* FM over pre-gathered rows (sharded path): emb is [B, F*k] in x order.     */
 int rs_rows_fm_fwd(const float* emb, const float* dense, int64_t dense_stride,
                    int nd, int n_fields, int k, const float* prepared,

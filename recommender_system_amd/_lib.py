@@ -63,6 +63,10 @@ SIGNATURES = {
     "rs_gather_rows": (I, [P, L, I, P, L, P, P, P]),
     "rs_unpermute_rows": (I, [P, P, I, L, P, P]),
     "rs_rows_fm_fwd": (I, [P, P, L, I, I, I, P, P, I, P, L, P]),
+    "rs_fm_partial_width": (I, [I]),
+    "rs_shard_field_route": (I, [P, I, L, P, P, I, L, L, I, P, I, L, P, P, P]),
+    "rs_shard_owner_fm": (I, [P, L, I, I, P, L, I, I, I, P, I, P, L, L, P, P]),
+    "rs_shard_fm_combine": (I, [P, L, I, L, P, L, I, I, I, P, P, I, P, P]),
 }
 
 ID_I32, ID_I64, ID_F32 = 0, 1, 2

@@ -149,6 +149,9 @@ struct EmbedFmArgs {
   int* err;
   int DB;
   int64_t dense_rec, field_rec, field_base;
+  int64_t owner_rows;       // KIND 4: rows of the owner's shard (ids are local rows, -1 = absent)
+  int pw;                   // KIND 4: floats per partial record (logit -> partial records)
+  int64_t pstride;          // KIND 4: floats between consecutive samples' partial records
   unsigned long long* dbg;  // diagnostic builds only (RS_DIAG_STAMPS): phase stamps
   int ablate;               // diagnostic builds only: bit0 no MFMA, bit1 no B loads, bit2 no combine
 };
@@ -173,15 +176,23 @@ struct EmbedFmArgs {
   } while (0)
 #endif
 
-// KIND: 0 i32, 1 i64, 2 f32 ids; 3 = rows already gathered (row(b,c) = b*F+c).
+// KIND: 0 i32, 1 i64, 2 f32 ids; 3 = rows already gathered (row(b,c) = b*F+c);
+// 4 = owner side of the sharded FM (sharded.py, partial protocol): ids are
+// int32 LOCAL rows of the owner's shard (-1 = lookup not owned here: a zero
+// contribution, not an error), no dense block, and instead of the logit the
+// workgroup writes each sample's partial record
+//   [s_0 .. s_{kfm-1}, x@w1, sum_i x_i^2 |v_i|^2, 0-pad]   (a.pw floats)
+// over the fields it was given; rs_shard_fm_combine finishes the FM.
 // TW: fused DeepFM — x goes to an LDS tile ([emb F*k | dense nd | 0-pad],
 // row stride tw->rs) instead of x_out, and the DNN tower of mlp_tower.hpp runs
 // on it, closed by sigmoid(c0*dnn + c1*fm) (model/deepFM.py:24-30).
-template <int KV, int NT, int NW, int KIND, bool TW>
+template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0>
 __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArgs* tw) {
-  constexpr int MAXC0 = 128 / (NW * KV);
+  // MC > 0: field slots per wave and pass (owner kernels with few fields)
+  constexpr int MAXC0 = MC > 0 ? MC : 128 / (NW * KV);
   constexpr int MAXC = MAXC0 < 1 ? 1 : (MAXC0 > 8 ? 8 : MAXC0);
-  typedef Ids<KIND == 3 ? 0 : KIND> I;
+  typedef Ids<(KIND >= 3) ? 0 : KIND> I;
+  constexpr bool OWNER = KIND == 4;
   __shared__ float cs[NW][16][NT * 16 + 1];
   __shared__ float qs[NW][16];
 
@@ -265,9 +276,11 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       const int64_t bb = b0 + ss < a.batch ? b0 + ss : a.batch - 1;
       lid[ss][c] = I::load(a.ids, bb * a.id_stride + c);
     }
-    for (int t = threadIdx.x; t < 2 * a.F; t += NW * 64) {
-      const int c = t < a.F ? t : t - a.F;
-      lmeta[t < a.F ? 0 : 1][c] = t < a.F ? a.offs[c] : a.vocab[c];
+    if constexpr (!OWNER) {
+      for (int t = threadIdx.x; t < 2 * a.F; t += NW * 64) {
+        const int c = t < a.F ? t : t - a.F;
+        lmeta[t < a.F ? 0 : 1][c] = t < a.F ? a.offs[c] : a.vocab[c];
+      }
     }
   }
   if (a.F == 0 || coop) load_dense();
@@ -287,7 +300,11 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       const int c = cg + j * NW + w;
       cj[j] = c < a.F ? c : a.F - 1;
       if constexpr (KIND != 3) {
-        if (coop) {
+        if (OWNER) {
+          offc[j] = 0;
+          vocc[j] = a.owner_rows;
+          rid[j] = coop ? lid[s][cj[j]] : I::load(a.ids, b * a.id_stride + cj[j]);
+        } else if (coop) {
           offc[j] = lmeta[0][cj[j]];
           vocc[j] = lmeta[1][cj[j]];
           rid[j] = lid[s][cj[j]];
@@ -346,7 +363,8 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
       const bool live = cg + j * NW + w < a.F;
-      bad |= live && !ok[j];
+      if constexpr (OWNER) bad |= live && !ok[j] && rid[j] != -1;
+      else bad |= live && !ok[j];
       const bool use = live && ok[j];
 #pragma unroll
       for (int tp = 0; tp < KV; ++tp) {
@@ -448,6 +466,19 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       lin += __shfl_xor(lin, 16);
     }
     const int64_t bb = (int64_t)blockIdx.x * 16 + smp;
+    if constexpr (OWNER) {
+      // partial record: column sums as they stand, the q term row-summed
+      float q = col < NW ? qs[col][smp] : 0.f;
+      q = row16_sum(q);
+      if constexpr (NT == 2) q += __shfl_xor(q, 16);
+      if (bb < a.batch) {
+        float* rec = a.logit + bb * a.pstride;
+        if (col <= a.kfm) rec[col] = v;
+        if (col == 0) rec[a.kfm + 1] = q;
+        else if (a.kfm + 1 + col < a.pw) rec[a.kfm + 1 + col] = 0.f;
+      }
+      return;
+    }
     const float fm = (lin + a.w0[0]) + 0.5f * t;
     if (col == 0 && bb < a.batch && a.logit) a.logit[bb] = fm;
     if constexpr (TW) {
@@ -461,6 +492,12 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 template <int KV, int NT, int NW, int KIND>
 __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
   embed_fm_body<KV, NT, NW, KIND, false>(a, nullptr);
+}
+
+// Owner side of the sharded FM (KIND 4): NW waves, MC field slots per wave.
+template <int KV, int NT, int NW, int MC>
+__global__ __launch_bounds__(NW * 64) void shard_owner_fm(EmbedFmArgs a) {
+  embed_fm_body<KV, NT, NW, 4, false, MC>(a, nullptr);
 }
 
 // Fused DeepFM forward: gather + FM + DNN tower + head, one launch.
@@ -837,6 +874,131 @@ extern "C" int rs_diag_embed_fm_fwd(const void* ids, int id_kind, int64_t id_str
   return run_embed_fm(a, g, id_kind, as_stream(stream), "rs_diag_embed_fm_fwd");
 }
 #endif
+
+// ------------------------------------------------ sharded FM, partial protocol
+// Owner side: rs_shard_owner_fm runs embed_fm_body in KIND 4 on the local rows
+// every requester asked of this owner (pairs = requester-major samples), over
+// the owner's contiguous field range; requester side: rs_shard_fm_combine sums
+// the world partial records of each sample in owner order, adds the dense
+// block and finishes logit = (lin + w0) + 0.5 (sum_f S_f^2 - q)
+// (layer/interaction.py:106-114 regrouped; same reassociation as the headline).
+namespace rs {
+
+template <int KV>
+static void launch_owner_kv(const EmbedFmArgs& a, int NT, hipStream_t st) {
+  const int grid = (int)((a.batch + 15) / 16);
+  if (NT == 1 && a.F <= 4) shard_owner_fm<KV, 1, 4, 1><<<grid, 4 * 64, 0, st>>>(a);
+  else if (NT == 1 && a.F <= 16) shard_owner_fm<KV, 1, 16, 1><<<grid, 16 * 64, 0, st>>>(a);
+  else if (NT == 1) shard_owner_fm<KV, 1, 16, 0><<<grid, 16 * 64, 0, st>>>(a);
+  else if (a.F <= 16) shard_owner_fm<KV, 2, 16, 1><<<grid, 16 * 64, 0, st>>>(a);
+  else shard_owner_fm<KV, 2, 16, 0><<<grid, 16 * 64, 0, st>>>(a);
+}
+
+// 16 lanes per sample (lane = partial column, strided by 16), DPP row sums.
+__global__ __launch_bounds__(256) void shard_fm_combine_k(const float* __restrict__ part, int world, int64_t batch,
+                                                          int64_t pst, const float* __restrict__ dense, int64_t ds,
+                                                          int nd,
+                                                          const float* __restrict__ prep, int64_t dense_rec, int NT,
+                                                          const float* __restrict__ w0, int kfm,
+                                                          float* __restrict__ logit) {
+  const int64_t b = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+  const int cl = threadIdx.x & 15;
+  const bool valid = b < batch;
+  const int64_t bb = valid ? b : batch - 1;  // padded lanes recompute the last sample
+  float t = 0.f, lin = 0.f, q = 0.f;
+  for (int col = cl; col < kfm + 2; col += 16) {
+    float acc = 0.f;
+    for (int o = 0; o < world; ++o) acc += part[((int64_t)o * batch + bb) * pst + col];
+    for (int e = 0; e < nd; ++e) {
+      const float x = dense[bb * ds + e];
+      const float* rec = prep + (int64_t)(e >> 2) * dense_rec;
+      if (col <= kfm) acc = fmaf(x, rec[(col >> 4) * 64 + (e & 3) * 16 + (col & 15)], acc);
+      else acc = fmaf(x * x, rec[NT * 64 + (e & 3)], acc);
+    }
+    if (col < kfm) t = fmaf(acc, acc, t);
+    else if (col == kfm) lin = acc;
+    else q = acc;
+  }
+  t = row16_sum(t);
+  lin = row16_sum(lin);
+  q = row16_sum(q);
+  if (valid && cl == 0) logit[b] = (lin + w0[0]) + 0.5f * (t - q);
+}
+
+}  // namespace rs
+
+extern "C" int rs_fm_partial_width(int kfm) { return kfm < 1 ? -1 : (kfm + 2 + 3) / 4 * 4; }
+
+extern "C" int rs_shard_owner_fm(const int32_t* local_rows, int64_t slot_stride, int field_lo, int n_owned,
+                                 const float* shard, int64_t shard_rows, int nd, int n_fields, int k,
+                                 const float* prepared, int kfm, float* partial, int64_t partial_stride,
+                                 int64_t n_pairs, int* err_flag, rs_stream_t stream) {
+  if (n_pairs == 0) return RS_OK;  // empty batch: nothing to launch
+  RS_REQUIRE(n_pairs > 0 && kfm >= 1 && nd >= 0 && k >= 1 && field_lo >= 0 && n_owned >= 0 &&
+                 field_lo + n_owned <= n_fields && n_owned <= slot_stride && shard_rows >= 0,
+             "rs_shard_owner_fm: bad shape");
+  RS_REQUIRE(partial_stride >= (kfm + 2 + 3) / 4 * 4, "rs_shard_owner_fm: partial_stride < rs_fm_partial_width");
+  RS_REQUIRE(prepared && partial && (n_owned == 0 || (local_rows && (shard || shard_rows == 0))),
+             "rs_shard_owner_fm: null pointer");
+  RS_REQUIRE((uintptr_t)shard % 16 == 0, "rs_shard_owner_fm: shard must be 16-B aligned");
+  const FmGeom g = fm_geom(nd, n_fields, k, kfm);
+  if (!g.mfma) {
+    set_error("rs_shard_owner_fm: needs the packed FM image (k in {4,8,16,32,64}, kfm <= 31)");
+    return RS_ERR_UNSUPPORTED;
+  }
+  hipStream_t st = as_stream(stream);
+  const int pw = (kfm + 2 + 3) / 4 * 4;
+  if (n_owned == 0) {  // this owner holds no rows: every partial is zero
+    (void)hipMemset2DAsync(partial, partial_stride * sizeof(float), 0, pw * sizeof(float), n_pairs, st);
+    return launch_status("rs_shard_owner_fm");
+  }
+  EmbedFmArgs a{};
+  a.ids = local_rows;
+  a.id_stride = slot_stride;
+  a.nd = 0;
+  a.table = shard;
+  a.F = n_owned;
+  a.k = k;
+  a.prep = prepared + (int64_t)field_lo * g.field_rec;  // weights of the owner's first field
+  a.kfm = kfm;
+  a.logit = partial;
+  a.batch = n_pairs;
+  a.err = err_flag;
+  a.DB = 0;  // dense block: added by the requester (rs_shard_fm_combine)
+  a.dense_rec = g.dense_rec;
+  a.field_rec = g.field_rec;
+  a.field_base = g.field_base;
+  a.owner_rows = shard_rows;
+  a.pw = pw;
+  a.pstride = partial_stride;
+  switch (g.KV) {
+    case 1: launch_owner_kv<1>(a, g.NT, st); break;
+    case 2: launch_owner_kv<2>(a, g.NT, st); break;
+    case 4: launch_owner_kv<4>(a, g.NT, st); break;
+    case 8: launch_owner_kv<8>(a, g.NT, st); break;
+    default: launch_owner_kv<16>(a, g.NT, st); break;
+  }
+  return launch_status("rs_shard_owner_fm");
+}
+
+extern "C" int rs_shard_fm_combine(const float* partials, int64_t partial_stride, int world, int64_t batch,
+                                   const float* dense,
+                                   int64_t dense_stride, int nd, int n_fields, int k, const float* prepared,
+                                   const float* w0, int kfm, float* logit, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch
+  RS_REQUIRE(batch > 0 && world >= 1 && nd >= 0 && n_fields >= 0 && kfm >= 1, "rs_shard_fm_combine: bad shape");
+  RS_REQUIRE(partials && prepared && w0 && logit && (nd == 0 || dense), "rs_shard_fm_combine: null pointer");
+  const FmGeom g = fm_geom(nd, n_fields, k, kfm);
+  if (!g.mfma) {
+    set_error("rs_shard_fm_combine: needs the packed FM image (k in {4,8,16,32,64}, kfm <= 31)");
+    return RS_ERR_UNSUPPORTED;
+  }
+  RS_REQUIRE(partial_stride >= (kfm + 2 + 3) / 4 * 4, "rs_shard_fm_combine: partial_stride < rs_fm_partial_width");
+  const int64_t threads = batch * 16;
+  shard_fm_combine_k<<<(unsigned)((threads + 255) / 256), 256, 0, as_stream(stream)>>>(
+      partials, world, batch, partial_stride, dense, dense_stride, nd, prepared, g.dense_rec, g.NT, w0, kfm, logit);
+  return launch_status("rs_shard_fm_combine");
+}
 
 extern "C" int rs_rows_fm_fwd(const float* emb, const float* dense, int64_t dense_stride, int nd, int n_fields,
                               int k, const float* prepared, const float* w0, int kfm, float* logit, int64_t batch,

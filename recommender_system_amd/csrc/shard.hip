@@ -297,6 +297,50 @@ __global__ __launch_bounds__(SP_THREADS) void shard_slot_onepass(ShardArgs a, ui
   }
 }
 
+// ------------------------------------------------ field route (partial protocol)
+// Block split of the concatenated table => owner o holds a contiguous FIELD
+// range [field_lo(o), field_lo(o) + n_owned(o)) (the fields its row block
+// intersects).  Message to owner o: batch records of rec_stride int32 words,
+// word j < slot_stride of record b = the local row of lookup
+// (b, field_lo(o) + j) if o owns it, else -1 (words past slot_stride are left
+// alone: the pipelined exchange keeps FM partials there).  Pure
+// index arithmetic (no scan, no capacity, no overflow); every slot is written
+// every step, so the buffer needs no initialisation.
+__global__ __launch_bounds__(256) void shard_field_route(ShardArgs a, const int32_t* __restrict__ ofl, int stride,
+                                                         int batch, int64_t rec_stride, int32_t* __restrict__ send) {
+  const int total = a.world * batch * stride;
+  for (int idx = blockIdx.x * 256 + threadIdx.x; idx < total; idx += gridDim.x * 256) {
+    const int ob = idx / stride;
+    const int j = idx - ob * stride;
+    const int o = ob / batch;
+    const int b = ob - o * batch;
+    const int c0 = ofl[2 * o], nf = ofl[2 * o + 1];
+    int32_t out = -1;
+    if (j < nf) {
+      const int c = c0 + j;
+      const int64_t off = (int64_t)b * a.id_stride + c;
+      int64_t id;
+      bool ok;
+      if (a.id_kind == RS_ID_F32) {
+        const float f = static_cast<const float*>(a.ids)[off];
+        ok = f > -1.0f && static_cast<double>(f) < static_cast<double>(a.vocab[c]);
+        id = ok ? static_cast<int64_t>(f) : 0;
+      } else {
+        id = (a.id_kind == RS_ID_I64) ? static_cast<const int64_t*>(a.ids)[off]
+                                      : static_cast<const int32_t*>(a.ids)[off];
+        ok = id >= 0 && id < a.vocab[c];
+      }
+      if (!ok) {
+        flag_error(a.err);
+      } else {
+        const int64_t local = a.offs[c] + id - (int64_t)o * a.rpr;
+        if (local >= 0 && local < a.rpr) out = (int32_t)local;
+      }
+    }
+    send[(int64_t)ob * rec_stride + j] = out;
+  }
+}
+
 template <int VW>
 __global__ void gather_rows_kernel(const float* __restrict__ table, int64_t n_rows, int k,
                                    const int32_t* __restrict__ rows, int64_t n, float* __restrict__ out, int* err) {
@@ -434,6 +478,26 @@ extern "C" int rs_shard_slot_bucketize(const void* ids, int id_kind, int64_t id_
                                                  reinterpret_cast<uint64_t*>(ws + sh_ctrl_offset(a.n, world)), nbp,
                                                  counts, slot_of, send_slots, cap, overflow_flag, g_sp_mode);
   return launch_status("rs_shard_slot_bucketize");
+}
+
+extern "C" int rs_shard_field_route(const void* ids, int id_kind, int64_t id_stride, const int64_t* field_offsets,
+                                    const int64_t* field_vocab, int n_fields, int64_t batch, int64_t rows_per_rank,
+                                    int world, const int32_t* owner_fields, int slot_stride, int64_t rec_stride,
+                                    int32_t* send, int* err_flag, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
+  RS_REQUIRE(ids && field_offsets && field_vocab && owner_fields && send, "rs_shard_field_route: null pointer");
+  RS_REQUIRE(world >= 1 && world <= SH_MAXW && rows_per_rank >= 1 && n_fields >= 1 && batch > 0 &&
+                 slot_stride >= 1 && slot_stride <= n_fields && rec_stride >= slot_stride,
+             "rs_shard_field_route: bad shape (1 <= world <= %d, 1 <= slot_stride <= n_fields)", SH_MAXW);
+  RS_REQUIRE((int64_t)world * batch * slot_stride < ((int64_t)1 << 31) && rows_per_rank < ((int64_t)1 << 31),
+             "rs_shard_field_route: too many slots / shard rows must fit int32");
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_shard_field_route: bad id_kind");
+  ShardArgs a{ids, id_kind, id_stride, field_offsets, field_vocab, n_fields, batch * n_fields, rows_per_rank, world,
+              err_flag, 1.0 / (double)rows_per_rank};
+  const int64_t total = (int64_t)world * batch * slot_stride;
+  shard_field_route<<<sh_grid(total), 256, 0, as_stream(stream)>>>(a, owner_fields, slot_stride, (int)batch, rec_stride,
+                                                                     send);
+  return launch_status("rs_shard_field_route");
 }
 
 extern "C" int rs_gather_rows(const float* table, int64_t n_rows, int k, const int32_t* rows, int64_t n, float* out,

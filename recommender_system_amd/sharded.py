@@ -116,6 +116,38 @@ class HipShardOps:
              ptr(w0), kfm, ptr(logit), B, _lib.stream())
         return logit
 
+    # -- partial protocol (rs_shard_field_route / rs_shard_owner_fm / rs_shard_fm_combine)
+    # Record layouts (in 4-byte words): row-id records of `rec` words, slot j
+    # at word j; partial records `pst` words apart starting at word `poff` of
+    # the buffer (separate buffers: rec = S, poff = 0, pst = P; the pipelined
+    # fused buffer: rec = pst = S + P, poff = S).
+    def field_route(self, sh, ids, send, rec=None):
+        B, F = ids.shape
+        call("rs_shard_field_route", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(sh.offsets), ptr(sh.vocab), F, B,
+             sh.rows_per_rank, sh.world, ptr(sh.owner_fields), sh.slot_stride, rec or sh.slot_stride, ptr(send),
+             ptr(self.err), _lib.stream())
+        return send
+
+    def owner_partials(self, sh, recv, n_pairs, out, rec=None, poff=0, pst=None):
+        lo, n_own = sh.owner_field_ranges[sh.rank]
+        call("rs_shard_owner_fm", ptr(recv), rec or sh.slot_stride, lo, n_own, ptr(sh.table_shard),
+             sh.table_shard.shape[0], sh.nd, sh.F, sh.k, ptr(sh.prepared), sh.kfm, ptr(out) + 4 * poff,
+             pst or sh.partial_width, n_pairs, ptr(self.err), _lib.stream())
+        return out
+
+    def combine(self, sh, partials, dense, out, poff=0, pst=None):
+        B = dense.shape[0]
+        call("rs_shard_fm_combine", ptr(partials) + 4 * poff, pst or sh.partial_width, sh.world, B, ptr(dense),
+             dense.stride(0), dense.shape[1], sh.F, sh.k, ptr(sh.prepared), ptr(sh.w0), sh.kfm, ptr(out),
+             _lib.stream())
+        return out
+
+    def bad_flag(self):
+        """[out-of-range id seen] (device tensor; resets)."""
+        v = self.err.clamp(max=1)
+        self.err.zero_()
+        return v
+
     def check(self):
         if int(self.err.item()):
             self.err.zero_()
@@ -126,10 +158,14 @@ class ShardedEmbeddingFM:
     """DeepFM embedding lookup + FM with the table row-sharded over a process
     group.  ``forward(dense[B,nd], ids[B,F]) -> logit[B,1]`` on every rank."""
 
-    def __init__(self, vocab_sizes, k, nd, kfm, group=None, device=None, seed=0, ops=None, table_init=True):
+    def __init__(self, vocab_sizes, k, nd, kfm, group=None, device=None, seed=0, ops=None, table_init=True,
+                 world=None, rank=None):
+        """world/rank: explicit partition without a process group (a rank of
+        a simulated world in single-process tests); default: the group's."""
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        on = dist.is_initialized()
+        self.world = int(world) if world is not None else (dist.get_world_size(group) if on else 1)
+        self.rank = int(rank) if rank is not None else (dist.get_rank(group) if on else 0)
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         self.vocab_sizes = [int(v) for v in vocab_sizes]
         self.F, self.k, self.nd, self.kfm = len(self.vocab_sizes), int(k), int(nd), int(kfm)
@@ -154,6 +190,16 @@ class ShardedEmbeddingFM:
         self.w0 = torch.zeros(1, device=self.device)
         self.w1 = (torch.randn(d, 1, generator=gen) * 0.05).to(self.device)
         self.v = (torch.randn(d, self.kfm, generator=gen) * 0.05).to(self.device)
+        # partial protocol: owner o holds the contiguous field range its row
+        # block intersects; messages are [B][slot_stride] local rows
+        self.owner_field_ranges = []
+        for o in range(self.world):
+            lo_r, hi_r = o * self.rows_per_rank, min(self.total_rows, (o + 1) * self.rows_per_rank)
+            cs = [c for c in range(self.F) if offs[c] < hi_r and offs[c] + self.vocab_sizes[c] > lo_r]
+            self.owner_field_ranges.append((cs[0], len(cs)) if cs else (0, 0))
+        self.slot_stride = max(1, max(n for _, n in self.owner_field_ranges))
+        self.owner_fields = torch.tensor(self.owner_field_ranges, dtype=torch.int32, device=self.device)
+        self.partial_width = (self.kfm + 2 + 3) // 4 * 4  # rs_fm_partial_width
         self.ops = ops if ops is not None else HipShardOps(self.device)
         self.prepared = None
         # world 1 skips the all-to-alls (a self-exchange is a copy); the bench
@@ -168,7 +214,106 @@ class ShardedEmbeddingFM:
         call("rs_fm_prepare", ptr(self.w1), ptr(self.v), self.nd, self.F, self.k, self.kfm, ptr(self.prepared),
              _lib.stream())
 
-    # -- the fixed-capacity exchange (default)
+    # -- the partial protocol (default forward)
+    def _pbufs(self, B):
+        pb = getattr(self, "_part_bufs", None)
+        if pb is None or pb["B"] != B:
+            W, S, P, dev = self.world, self.slot_stride, self.partial_width, self.device
+            pb = {"B": B,
+                  "send": torch.empty(W * B * S, dtype=torch.int32, device=dev),
+                  "recv": torch.empty(W * B * S, dtype=torch.int32, device=dev),
+                  "pout": torch.empty(W * B * P, dtype=torch.float32, device=dev),
+                  "pin": torch.empty(W * B * P, dtype=torch.float32, device=dev)}
+            self._part_bufs = pb
+        return pb
+
+    def forward(self, dense, ids, check=True, out=None):
+        """FM logit [B,1] of the local batch (into ``out`` if given), partial
+        protocol:
+          1. rs_shard_field_route -> [world][B][S] local rows (-1 = not yours)
+          2. all_to_all(rows ids)  -> what every requester asks of me  (RCCL)
+          3. rs_shard_owner_fm     -> per (requester, sample) FM partials over
+                                      my fields, [world][B][P] fp32
+          4. all_to_all(partials)  -> every owner's partials of my samples (RCCL)
+          5. rs_shard_fm_combine   -> sum owners in rank order + dense, logit
+        Fixed, host-known message sizes (S*4 and P*4 bytes per sample and
+        peer), no overflow case, no host sync unless ``check``."""
+        B = ids.shape[0]
+        pb = self._pbufs(B)
+        exchange = self.world > 1 or self._force_exchange
+        send = self.ops.field_route(self, ids, pb["send"])
+        recv = send
+        if exchange:
+            recv = pb["recv"]
+            dist.all_to_all_single(recv, send, group=self.group)
+        part = self.ops.owner_partials(self, recv, self.world * B, pb["pout"])
+        if exchange:
+            dist.all_to_all_single(pb["pin"], part, group=self.group)
+            part = pb["pin"]
+        logit = out if out is not None else torch.empty(B, 1, dtype=torch.float32, device=self.device)
+        logit = self.ops.combine(self, part, dense, logit)
+        if check:
+            f = self.ops.bad_flag()
+            if self.world > 1:
+                dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
+            if bool(f.item()):
+                raise IndexError("sharded lookup: embedding id out of range")
+        return logit
+
+    # -- the pipelined partial protocol: one all-to-all per batch
+    def _sbufs(self, B):
+        sb = getattr(self, "_stream_bufs", None)
+        if sb is None or sb["B"] != B:
+            R = self.slot_stride + self.partial_width
+            n = self.world * B * R
+            sb = {"B": B, "R": R,
+                  "send": torch.zeros(n, dtype=torch.int32, device=self.device),
+                  "recv": torch.zeros(n, dtype=torch.int32, device=self.device)}
+            self._stream_bufs = sb
+        return sb
+
+    def pipe_step(self, cur=None, prev=None):
+        """One exchange of the pipelined partial protocol.  cur = (dense, ids)
+        of batch t (or None), prev = (dense, out) of batch t-1 (or None):
+          rs_shard_field_route(ids_t)   -> row-id words of the fused records
+          all_to_all                    -> ONE collective: [ids of t | partials of t-1]
+          rs_shard_fm_combine(t-1)      -> out_{t-1}
+          rs_shard_owner_fm(t)          -> partial words of the fused records
+        (stream-ordered: the owner's partials of t ride the next exchange)."""
+        B = (cur[1] if cur is not None else prev[0]).shape[0]
+        sb = self._sbufs(B)
+        S, R = self.slot_stride, sb["R"]
+        exchange = self.world > 1 or self._force_exchange
+        if cur is not None:
+            self.ops.field_route(self, cur[1], sb["send"], rec=R)
+        recv = sb["send"]
+        if exchange:
+            recv = sb["recv"]
+            dist.all_to_all_single(recv, sb["send"], group=self.group)
+        if prev is not None:
+            self.ops.combine(self, recv, prev[0], prev[1], poff=S, pst=R)
+        if cur is not None:
+            self.ops.owner_partials(self, recv, self.world * B, sb["send"], rec=R, poff=S, pst=R)
+
+    def forward_stream(self, batches, check=True):
+        """FM logits of a sequence of local batches [(dense, ids), ...] with the
+        pipelined partial protocol: batch t's row-id message and batch t-1's
+        partials share one all-to-all, so a stream of n batches costs n + 1
+        collectives instead of 2n.  Returns [logit [B,1] per batch]."""
+        outs = [torch.empty(ids.shape[0], 1, dtype=torch.float32, device=self.device) for _, ids in batches]
+        for t in range(len(batches) + 1):
+            cur = batches[t] if t < len(batches) else None
+            prev = (batches[t - 1][0], outs[t - 1]) if t > 0 else None
+            self.pipe_step(cur, prev)
+        if check:
+            f = self.ops.bad_flag()
+            if self.world > 1:
+                dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
+            if bool(f.item()):
+                raise IndexError("sharded lookup: embedding id out of range")
+        return outs
+
+    # -- the fixed-capacity row exchange (returns rows; forward_slots)
     def capacity(self, n):
         """Slots per (rank -> owner) message for n local lookups."""
         if self.world == 1:
@@ -237,8 +382,9 @@ class ShardedEmbeddingFM:
         emb = self.lookup(ids)
         return self.ops.rows_fm(emb, dense, self.F, self.k, self.prepared, self.w0, self.kfm)
 
-    def forward(self, dense, ids, check=True, out=None):
-        """FM logit [B,1] of the local batch (into ``out`` if given).
+    def forward_slots(self, dense, ids, check=True, out=None):
+        """FM logit [B,1] through the fixed-capacity ROW exchange (the rows of
+        every lookup come back to the requester: EmbedLayer semantics).
         check=True: one host sync at the end of the step; a slot overflow is
         redone exactly, a bad id raises."""
         got, slot_of = self.exchange_slots(ids)

@@ -1,6 +1,7 @@
-"""world=1 timing of the sharded step's local part (slot bucketize, gather,
-FM from the exchange buffer) — eager, no collectives; for the step-overhead
-estimate of the N>1 path (which adds the two RCCL all-to-alls)."""
+"""world=1 timing of the sharded step's local part — eager, no collectives:
+the partial protocol (field route, owner FM partials, combine) and the row
+exchange (slot bucketize, gather, FM from the exchange buffer); for the
+step-overhead estimate of the N>1 path (which adds two RCCL all-to-alls)."""
 import os
 import sys
 import time
@@ -23,7 +24,12 @@ for i in range(n):
     sh.forward(dense, ids[i % 8], check=False)
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / n
-print(f"world=1 sharded step (eager, no check): {dt * 1e6:.1f} us/step, slots {sh._bufs(B)['cap']}")
+print(f"world=1 partial-protocol step (eager, no check): {dt * 1e6:.1f} us/step")
+t0 = time.perf_counter()
+for i in range(n):
+    sh.forward_slots(dense, ids[i % 8], check=False)
+torch.cuda.synchronize()
+print(f"world=1 row-slot step (eager, no check): {(time.perf_counter() - t0) / n * 1e6:.1f} us/step")
 t0 = time.perf_counter()
 for i in range(50):
     sh.forward(dense, ids[i % 8], check=True)

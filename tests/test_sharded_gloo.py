@@ -79,6 +79,60 @@ class CpuOps:
         self.last_emb = emb
         return None
 
+    # partial protocol (fp64 inside, fp32 buffers like the device path)
+    @staticmethod
+    def _f32(t):
+        return t.view(torch.float32) if t.dtype == torch.int32 else t
+
+    def field_route(self, sh, ids, send, rec=None):
+        ids_n = ids.numpy().astype(np.int64)
+        B = ids_n.shape[0]
+        out = np.full((sh.world, B, sh.slot_stride), -1, np.int64)
+        rows = sh.offsets.numpy()[None, :] + ids_n
+        for o, (lo, n) in enumerate(sh.owner_field_ranges):
+            for j in range(n):
+                loc = rows[:, lo + j] - o * sh.rows_per_rank
+                m = (loc >= 0) & (loc < sh.rows_per_rank)
+                out[o, m, j] = loc[m]
+        R = rec or sh.slot_stride
+        send.view(-1, R)[:, :sh.slot_stride].copy_(torch.as_tensor(out.reshape(-1, sh.slot_stride), dtype=torch.int32))
+        return send
+
+    def owner_partials(self, sh, recv, n_pairs, out, rec=None, poff=0, pst=None):
+        lo, n = sh.owner_field_ranges[sh.rank]
+        r = recv.numpy().reshape(n_pairs, rec or sh.slot_stride)[:, :sh.slot_stride].astype(np.int64)
+        T = sh.table_shard.numpy().astype(np.float64)
+        v, w1 = sh.v.numpy().astype(np.float64), sh.w1.numpy().astype(np.float64)[:, 0]
+        res = np.zeros((n_pairs, sh.partial_width))
+        for j in range(n):
+            e = sh.nd + (lo + j) * sh.k + np.arange(sh.k)
+            loc = r[:, j]
+            x = np.zeros((n_pairs, sh.k))
+            x[loc >= 0] = T[loc[loc >= 0]]
+            res[:, :sh.kfm] += x @ v[e]
+            res[:, sh.kfm] += x @ w1[e]
+            res[:, sh.kfm + 1] += (x * x) @ (v[e] ** 2).sum(1)
+        P, pst = sh.partial_width, pst or sh.partial_width
+        self._f32(out)[poff:].as_strided((n_pairs, P), (pst, 1)).copy_(torch.as_tensor(res, dtype=torch.float32))
+        return out
+
+    def combine(self, sh, partials, dense, out, poff=0, pst=None):
+        B, nd, kfm = dense.shape[0], sh.nd, sh.kfm
+        P, pst = sh.partial_width, pst or sh.partial_width
+        flat = self._f32(partials)[poff:]
+        p = flat.as_strided((sh.world * B, P), (pst, 1)).numpy().reshape(sh.world, B, P).astype(np.float64).sum(0)
+        d = dense.numpy().astype(np.float64)
+        v, w1 = sh.v.numpy().astype(np.float64), sh.w1.numpy().astype(np.float64)[:, 0]
+        S = p[:, :kfm] + d @ v[:nd]
+        lin = p[:, kfm] + d @ w1[:nd]
+        q = p[:, kfm + 1] + (d * d) @ (v[:nd] ** 2).sum(1)
+        logit = lin + float(sh.w0[0]) + 0.5 * ((S ** 2).sum(1) - q)
+        out.copy_(torch.as_tensor(logit.reshape(B, 1), dtype=torch.float32))
+        return out
+
+    def bad_flag(self):
+        return torch.zeros(1, dtype=torch.int32)
+
 
 def _free_port():
     s = socket.socket()
@@ -113,7 +167,7 @@ def _worker(rank, world, port, vocabs, k, B, q):
         sh._slot_bufs = None
         sh.capacity = lambda n: 2
         dense0 = torch.zeros(B, 3)
-        sh.forward(dense0, ids)
+        sh.forward_slots(dense0, ids)
         ok_rows = ok_rows and np.array_equal(ops.last_emb.numpy(), expect)
         dense = rng.random((B, 3)).astype(np.float32)
         x = np.concatenate([dense, emb.numpy().reshape(B, -1)], 1)
@@ -122,7 +176,18 @@ def _worker(rank, world, port, vocabs, k, B, q):
         fm_ref = O.deepfm(None, {"tables": tables, "w0": sh.w0.numpy(), "w1": sh.w1.numpy(), "v": sh.v.numpy(),
                                  "dnn_hidden": [], "dnn_out": (np.zeros((x.shape[1], 1)), np.zeros(1))},
                           nd=3, inputs=(dense, ids.numpy()))[1]
-        q.put((rank, ok_rows, float(np.max(np.abs(fm_sh - fm_ref))), sh.row_range))
+        # partial protocol: owners return FM partials over their fields
+        part = sh.forward(torch.as_tensor(dense), ids).numpy()
+        rms = float(np.sqrt(np.mean(fm_ref ** 2)))
+        ok_part = bool(np.all(np.abs(part - fm_ref) <= 1e-5 * np.maximum(np.abs(fm_ref), rms)))
+        # pipelined: 3 batches, one all-to-all each (+1 to drain) == per-batch forward
+        d2 = [torch.as_tensor(rng.random((B, 3)).astype(np.float32)) for _ in range(3)]
+        i2 = [torch.as_tensor(np.stack([rng.integers(0, v, B) for v in vocabs], 1), dtype=torch.int32)
+              for _ in range(2)] + [ids]
+        outs = sh.forward_stream(list(zip(d2, i2)))
+        for d_, i_, o_ in zip(d2, i2, outs):
+            ok_part = ok_part and np.allclose(o_.numpy(), sh.forward(d_, i_).numpy(), rtol=1e-6, atol=1e-7)
+        q.put((rank, ok_rows and ok_part, float(np.max(np.abs(fm_sh - fm_ref))), sh.row_range))
     finally:
         dist.destroy_process_group()
 
@@ -186,11 +251,12 @@ def test_gpu_sharded_single_rank_equals_fused(gpu):
     B = 300
     ids = torch.as_tensor(np.stack([rng.integers(0, v, B) for v in vocabs], 1), dtype=torch.int32, device=gpu)
     dense = torch.rand(B, 13, device=gpu)
-    a = sh.forward(dense, ids)                 # fixed-capacity slots (default)
+    a = sh.forward_slots(dense, ids)           # fixed-capacity row slots
     e = sh.forward_exact(dense, ids)           # counts + variable splits
+    pp = sh.forward(dense, ids)                # owner FM partials (default)
     sh._slot_bufs = None
     sh.capacity = lambda n: 7                  # forced overflow -> exact fallback
-    f = sh.forward(dense, ids)
+    f = sh.forward_slots(dense, ids)
     b = torch.empty(B, 1, device=gpu)
     _lib.call("rs_embed_fm_fwd", ids.data_ptr(), 0, 26, dense.data_ptr(), 13, 13, sh.table_shard.data_ptr(),
               sh.offsets.data_ptr(), sh.vocab.data_ptr(), 26, 16, sh.prepared.data_ptr(), sh.w0.data_ptr(), 10,
@@ -198,12 +264,82 @@ def test_gpu_sharded_single_rank_equals_fused(gpu):
     np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-6, atol=1e-6)
     np.testing.assert_allclose(e.cpu().numpy(), b.cpu().numpy(), rtol=1e-6, atol=1e-6)
     np.testing.assert_allclose(f.cpu().numpy(), b.cpu().numpy(), rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(pp.cpu().numpy(), b.cpu().numpy(), rtol=1e-6, atol=1e-6)
     bad = ids.clone()
     bad[3, 5] = vocabs[5]
     sh.capacity = lambda n: max(n, 1)
     sh._slot_bufs = None
     with pytest.raises(IndexError):
+        sh.forward_slots(dense, bad)
+    with pytest.raises(IndexError):
         sh.forward(dense, bad)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("world,k,kfm", [(8, 16, 10), (3, 16, 10), (2, 8, 20), (5, 4, 3)])
+def test_gpu_partial_protocol_simulated_world(gpu, world, k, kfm, fused):
+    """The partial protocol's three kernels at world > 1 in ONE process: each
+    simulated rank routes its own batch, the all-to-all is done as a block
+    transpose, every owner runs rs_shard_owner_fm on its shard, and every
+    requester's rs_shard_fm_combine must equal the unsharded fused kernel
+    (rs_embed_fm_fwd over the concatenated table) and the fp64 oracle.
+    fused: the pipelined layout (row ids and partials interleaved in one
+    record per peer and sample, as forward_stream exchanges them)."""
+    from recommender_system_amd import _lib
+    from recommender_system_amd.sharded import ShardedEmbeddingFM
+    rng = np.random.default_rng(world * 100 + k)
+    vocabs = [int(v) for v in rng.integers(1, 4000, 26)]
+    vocabs[7] = 20000  # one field straddles several owners
+    B, nd = 257, 13
+    shs = [ShardedEmbeddingFM(vocabs, k, nd, kfm, device=gpu, seed=11, table_init=False, world=world, rank=r)
+           for r in range(world)]
+    full = torch.empty(shs[0].total_rows, k, device=gpu).uniform_(-0.05, 0.05)
+    for sh in shs:
+        lo, hi = sh.row_range
+        sh.table_shard = full[lo:hi].contiguous()
+    ids = [torch.as_tensor(np.stack([rng.integers(0, v, B) for v in vocabs], 1), dtype=torch.int32, device=gpu)
+           for _ in range(world)]
+    dense = [torch.rand(B, nd, device=gpu) for _ in range(world)]
+    S, P = shs[0].slot_stride, shs[0].partial_width
+    R = S + P if fused else S          # words per row-id record
+    poff, pst = (S, S + P) if fused else (0, P)
+    sends = [sh.ops.field_route(sh, ids[r], torch.full((world * B * R,), 7, dtype=torch.int32, device=gpu), rec=R)
+             for r, sh in enumerate(shs)]
+    id_words = [x.view(world * B, R)[:, :S].clone() for x in sends]
+    if fused:  # the route left the partial words alone
+        assert all(bool((x.view(world * B, R)[:, S:] == 7).all()) for x in sends)
+    # all-to-all #1: owner o receives block o of every requester, requester-major
+    recvs = [torch.cat([sends[r].view(world, B * R)[o] for r in range(world)]) for o in range(world)]
+    pouts = [sh.ops.owner_partials(sh, recvs[o], world * B, sends[o] if fused else
+                                   torch.empty(world * B * P, device=gpu), rec=R, poff=poff, pst=pst)
+             for o, sh in enumerate(shs)]
+    if fused:  # the owner wrote only the partial words: row-id words intact
+        for o in range(world):
+            assert torch.equal(pouts[o].view(world * B, R)[:, :S], id_words[o])
+    # all-to-all #2: requester r receives block r of every owner, owner-major
+    blk = B * (R if fused else P)
+    pins = [torch.cat([pouts[o].view(world, blk)[r] for o in range(world)]) for r in range(world)]
+    for r, sh in enumerate(shs):
+        got = sh.ops.combine(sh, pins[r], dense[r], torch.empty(B, 1, device=gpu), poff=poff, pst=pst)
+        ref = torch.empty(B, 1, device=gpu)
+        _lib.call("rs_embed_fm_fwd", ids[r].data_ptr(), 0, 26, dense[r].data_ptr(), nd, nd, full.data_ptr(),
+                  sh.offsets.data_ptr(), sh.vocab.data_ptr(), 26, k, sh.prepared.data_ptr(), sh.w0.data_ptr(), kfm,
+                  ref.data_ptr(), None, B, None, _lib.stream())
+        g, f = got.cpu().numpy(), ref.cpu().numpy()
+        rms = float(np.sqrt(np.mean(f ** 2)))
+        assert np.all(np.abs(g - f) <= 1e-5 * np.maximum(np.abs(f), rms)), (r, float(np.max(np.abs(g - f))))
+        T = full.cpu().numpy().astype(np.float64)
+        offs = sh.offsets.cpu().numpy()
+        tables = [T[o:o + v] for o, v in zip(offs, vocabs)]
+        oracle = O.deepfm(None, {"tables": tables, "w0": sh.w0.cpu().numpy(), "w1": sh.w1.cpu().numpy(),
+                                 "v": sh.v.cpu().numpy(), "dnn_hidden": [],
+                                 "dnn_out": (np.zeros((nd + 26 * k, 1)), np.zeros(1))},
+                          nd=nd, inputs=(dense[r].cpu().numpy(), ids[r].cpu().numpy()))[1]
+        rms = float(np.sqrt(np.mean(oracle ** 2)))
+        assert np.all(np.abs(g - oracle) <= 1e-5 * np.maximum(np.abs(oracle), rms))
+    for sh in shs:
+        sh.ops.check()
 
 
 @pytest.mark.gpu
