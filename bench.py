@@ -375,10 +375,11 @@ def _graph_capturable(fn, first):
 def bench_sharded(args, world, rank, vocabs, dense_pool):
     """BASELINE config 5 shape: the table row-sharded over the ranks, each rank
     B local samples (weak scaling).  Timed protocol (the value): owner-side FM
-    partials, pipelined (sharded.py ``pipe_step``): per batch t, field route
-    of t -> ONE RCCL all-to-all carrying [row ids of t | FM partials of t-1]
-    -> combine of t-1 -> owner FM partials of t over its field range (steady
-    state: every step does one batch's full work).  Also timed: the same
+    partials, pipelined (sharded.py ``pipe_step``): per batch t, ONE RCCL
+    all-to-all carrying [row ids of t | FM partials of t-1], then ONE launch
+    (rs_shard_fm_pipe) doing combine of t-1 | owner FM partials of t over its
+    field range | field route of t+1 (steady state: every step does one
+    batch's full work).  Also timed: the same
     protocol unpipelined (``forward``: two all-to-alls per batch) and the
     fixed-capacity ROW exchange (``forward_slots``), which returns every
     lookup's 64-B row to the requester.  Steps are replayed from HIP graphs
@@ -400,8 +401,8 @@ def bench_sharded(args, world, rank, vocabs, dense_pool):
     npool = ids_pool.shape[0]
 
     def pipelined(i):
-        j, jp = i % npool, (i - 1) % npool
-        sh.pipe_step(cur=(dense_pool[j], ids_pool[j]), prev=(dense_pool[jp], outs[(i - 1) % 2]))
+        j, jp, jn = i % npool, (i - 1) % npool, (i + 1) % npool
+        sh.pipe_step(prev=(dense_pool[jp], outs[(i - 1) % 2]), cur=ids_pool[j], nxt=(dense_pool[jn], ids_pool[jn]))
 
     def per_batch(fwd):
         def step(i):
@@ -424,6 +425,7 @@ def bench_sharded(args, world, rank, vocabs, dense_pool):
             step_ms = _max_over_ranks(float(np.mean(ms)), world)
         return dt, step_ms, ("HIP graph replay (RCCL captured)" if graphed else f"eager launches ({why})")
 
+    sh.pipe_route(ids_pool[0])  # prologue: batch 0's row ids
     dt, step_ms, timing = run(pipelined)
     udt, ustep_ms, utiming = run(per_batch(sh.forward))
     f = sh.ops.bad_flag()  # any bad id during the timed steps?
@@ -437,9 +439,9 @@ def bench_sharded(args, world, rank, vocabs, dense_pool):
     bufs = sh._bufs(B)
     S, P = sh.slot_stride, sh.partial_width
     res = {"exchange": {
-        "protocol": "owner-side FM partials, pipelined: field route(t), ONE RCCL all-to-all of [row ids of t | "
-                    "FM partials of t-1] records, combine(t-1), owner FM partials(t) over its field range; fixed "
-                    "sizes, no host sync",
+        "protocol": "owner-side FM partials, pipelined: ONE RCCL all-to-all of [row ids of t | FM partials of "
+                    "t-1] records + ONE launch (combine t-1 | owner FM partials of t over its field range | field "
+                    "route of t+1) per batch; fixed sizes, no host sync",
         "timing": timing, "lookups_per_rank": B * F, "rows_per_rank": sh.rows_per_rank,
         "owner_field_ranges": sh.owner_field_ranges,
         "bytes_per_rank_each_way": world * B * (S + P) * 4,
@@ -457,7 +459,7 @@ def bench_sharded(args, world, rank, vocabs, dense_pool):
     alg = B * 1824 + 18880
     res["roofline"] = {"bound": "hbm", "achieved": alg / (step_ms * 1e-3) / 1e9, "peak": PEAK_HBM / 1e9,
                        "unit": "GB/s", "frac": alg / (step_ms * 1e-3) / PEAK_HBM, "traffic": None,
-                       "kernel": "sharded step (field route + RCCL all-to-all + owner FM partials + combine)",
+                       "kernel": "sharded step (RCCL all-to-all + rs_shard_fm_pipe)",
                        "kernel_ms_avg": step_ms}
     res["cpu_baseline"] = None
     return res

@@ -408,6 +408,26 @@ int rs_shard_fm_combine(const float* partials, int64_t partial_stride,
                         const float* w0, int kfm, float* logit,
                         rs_stream_t stream);
 
+/* One launch per pipelined step (sharded.py pipe_step), run after the
+ * step's all-to-all: the owner part of batch t on recv's row-id words
+ * (partials -> send's partial words), batch t+1's field route (ids_next ->
+ * send's row-id words; ids_next NULL = none) and batch t-1's combine
+ * (recv's partial words + dense_prev -> logit_prev; logit_prev NULL = none).
+ * recv and send hold world*batch fused records of slot_stride + P words
+ * ([row ids | partial]).  The three parts are independent, so one pipelined
+ * step is exactly one kernel and one all-to-all.                           */
+int rs_shard_fm_pipe(const int32_t* recv, int field_lo, int n_owned,
+                     const float* shard, int64_t shard_rows,
+                     const float* dense_prev, int64_t dense_stride,
+                     float* logit_prev, const void* ids_next, int id_kind,
+                     int64_t id_stride, const int64_t* field_offsets,
+                     const int64_t* field_vocab, int64_t rows_per_rank,
+                     const int32_t* owner_fields, int slot_stride,
+                     int32_t* send, int world, int64_t batch, int nd,
+                     int n_fields, int k, const float* prepared,
+                     const float* w0, int kfm, int* err_flag,
+                     rs_stream_t stream);
+
 /* FM over pre-gathered rows (sharded path): emb is [B, F*k] in x order.     */
 int rs_rows_fm_fwd(const float* emb, const float* dense, int64_t dense_stride,
                    int nd, int n_fields, int k, const float* prepared,

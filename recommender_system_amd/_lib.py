@@ -67,6 +67,7 @@ SIGNATURES = {
     "rs_shard_field_route": (I, [P, I, L, P, P, I, L, L, I, P, I, L, P, P, P]),
     "rs_shard_owner_fm": (I, [P, L, I, I, P, L, I, I, I, P, I, P, L, L, P, P]),
     "rs_shard_fm_combine": (I, [P, L, I, L, P, L, I, I, I, P, P, I, P, P]),
+    "rs_shard_fm_pipe": (I, [P, I, I, P, L, P, L, P, P, I, L, P, P, L, P, I, P, I, L, I, I, I, P, P, I, P, P]),
 }
 
 ID_I32, ID_I64, ID_F32 = 0, 1, 2

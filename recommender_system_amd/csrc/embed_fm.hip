@@ -25,6 +25,7 @@
 
 #include "mlp_tower.hpp"
 #include "rs_common.hpp"
+#include "shard_route.hpp"
 
 namespace rs {
 
@@ -187,7 +188,7 @@ struct EmbedFmArgs {
 // row stride tw->rs) instead of x_out, and the DNN tower of mlp_tower.hpp runs
 // on it, closed by sigmoid(c0*dnn + c1*fm) (model/deepFM.py:24-30).
 template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0>
-__device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArgs* tw) {
+__device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArgs* tw, const int tile) {
   // MC > 0: field slots per wave and pass (owner kernels with few fields)
   constexpr int MAXC0 = MC > 0 ? MC : 128 / (NW * KV);
   constexpr int MAXC = MAXC0 < 1 ? 1 : (MAXC0 > 8 ? 8 : MAXC0);
@@ -200,7 +201,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int s = lane & 15;   // A: sample row of the tile; B/C: column
   const int kk = lane >> 4;  // k-slot
-  const int64_t bt = (int64_t)blockIdx.x * 16 + s;
+  const int64_t bt = (int64_t)tile * 16 + s;
   const bool valid = bt < a.batch;
   // Padded lanes of the last tile recompute the last sample: an MFMA output
   // row depends only on its own A row, so they never touch valid outputs.
@@ -270,7 +271,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   __shared__ int64_t lmeta[2][FMAX];
   const bool coop = (KIND != 3) && a.F <= FMAX;
   if (coop) {
-    const int64_t b0 = (int64_t)blockIdx.x * 16;
+    const int64_t b0 = (int64_t)tile * 16;
     for (int t = threadIdx.x; t < 16 * a.F; t += NW * 64) {
       const int ss = t / a.F, c = t - ss * a.F;
       const int64_t bb = b0 + ss < a.batch ? b0 + ss : a.batch - 1;
@@ -465,7 +466,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       t += __shfl_xor(t, 16);
       lin += __shfl_xor(lin, 16);
     }
-    const int64_t bb = (int64_t)blockIdx.x * 16 + smp;
+    const int64_t bb = (int64_t)tile * 16 + smp;
     if constexpr (OWNER) {
       // partial record: column sums as they stand, the q term row-summed
       float q = col < NW ? qs[col][smp] : 0.f;
@@ -486,24 +487,86 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     }
   }
   RS_STAMP(4);
-  if constexpr (TW) mlp_tower_tile<NW>(*tw, tsm, (int64_t)blockIdx.x * 16, ring, fmlog);
+  if constexpr (TW) mlp_tower_tile<NW>(*tw, tsm, (int64_t)tile * 16, ring, fmlog);
 }
 
 template <int KV, int NT, int NW, int KIND>
 __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
-  embed_fm_body<KV, NT, NW, KIND, false>(a, nullptr);
+  embed_fm_body<KV, NT, NW, KIND, false>(a, nullptr, blockIdx.x);
 }
 
-// Owner side of the sharded FM (KIND 4): NW waves, MC field slots per wave.
+// ---- sharded FM, partial protocol: combine (requester side) as a block part
+struct CombineArgs {
+  const float* part;  // partial records [world][batch], pst floats apart
+  int64_t pst;
+  int world;
+  int64_t batch;
+  const float* dense;
+  int64_t ds;
+  int nd;
+  const float* prep;  // the packed FM image (dense records at its start)
+  int64_t dense_rec;
+  int NT;
+  const float* w0;
+  int kfm;
+  float* logit;
+};
+
+// 16 lanes per sample (lane = partial column, strided by 16), DPP row sums;
+// blocks blk of nblk, NTH threads each, grid-stride over batch*16 lanes.
+template <int NTH>
+__device__ __forceinline__ void fm_combine_part(const CombineArgs& c, int blk, int nblk) {
+  for (int64_t idx = (int64_t)blk * NTH + threadIdx.x; idx < c.batch * 16; idx += (int64_t)nblk * NTH) {
+    const int64_t b = idx >> 4;
+    const int cl = threadIdx.x & 15;
+    float t = 0.f, lin = 0.f, q = 0.f;
+    for (int col = cl; col < c.kfm + 2; col += 16) {
+      float acc = 0.f;
+      for (int o = 0; o < c.world; ++o) acc += c.part[((int64_t)o * c.batch + b) * c.pst + col];
+      for (int e = 0; e < c.nd; ++e) {
+        const float x = c.dense[b * c.ds + e];
+        const float* rec = c.prep + (int64_t)(e >> 2) * c.dense_rec;
+        if (col <= c.kfm) acc = fmaf(x, rec[(col >> 4) * 64 + (e & 3) * 16 + (col & 15)], acc);
+        else acc = fmaf(x * x, rec[c.NT * 64 + (e & 3)], acc);
+      }
+      if (col < c.kfm) t = fmaf(acc, acc, t);
+      else if (col == c.kfm) lin = acc;
+      else q = acc;
+    }
+    t = row16_sum(t);
+    lin = row16_sum(lin);
+    q = row16_sum(q);
+    if (cl == 0) c.logit[b] = (lin + c.w0[0]) + 0.5f * (t - q);
+  }
+}
+
+// One launch per pipelined step (sharded.py pipe_step): blocks
+// [0, owner_blocks) are the owner side of batch t (KIND 4, 16 pairs each),
+// then route_blocks of batch t+1's field route, then combine_blocks of batch
+// t-1's combine — three independent parts, so a step is ONE kernel + ONE
+// all-to-all.  Any part may be empty.
+struct PipeArgs {
+  int owner_blocks, route_blocks, combine_blocks;
+  RouteArgs r;
+  CombineArgs c;
+};
+
 template <int KV, int NT, int NW, int MC>
-__global__ __launch_bounds__(NW * 64) void shard_owner_fm(EmbedFmArgs a) {
-  embed_fm_body<KV, NT, NW, 4, false, MC>(a, nullptr);
+__global__ __launch_bounds__(NW * 64) void shard_fm_pipe(EmbedFmArgs a, PipeArgs p) {
+  const int bid = blockIdx.x;
+  if (bid < p.owner_blocks) {
+    embed_fm_body<KV, NT, NW, 4, false, MC>(a, nullptr, bid);
+  } else if (bid < p.owner_blocks + p.route_blocks) {
+    field_route_part<NW * 64>(p.r, bid - p.owner_blocks, p.route_blocks);
+  } else {
+    fm_combine_part<NW * 64>(p.c, bid - p.owner_blocks - p.route_blocks, p.combine_blocks);
+  }
 }
 
 // Fused DeepFM forward: gather + FM + DNN tower + head, one launch.
 template <int KV, int KIND>
 __global__ __launch_bounds__(16 * 64) void deepfm_fused(EmbedFmArgs a, MlpArgs t) {
-  embed_fm_body<KV, 1, 16, KIND, true>(a, &t);
+  embed_fm_body<KV, 1, 16, KIND, true>(a, &t, blockIdx.x);
 }
 
 // Generic fallback (any k / kfm): one 256-thread workgroup per sample.
@@ -884,77 +947,49 @@ extern "C" int rs_diag_embed_fm_fwd(const void* ids, int id_kind, int64_t id_str
 // (layer/interaction.py:106-114 regrouped; same reassociation as the headline).
 namespace rs {
 
-template <int KV>
-static void launch_owner_kv(const EmbedFmArgs& a, int NT, hipStream_t st) {
-  const int grid = (int)((a.batch + 15) / 16);
-  if (NT == 1 && a.F <= 4) shard_owner_fm<KV, 1, 4, 1><<<grid, 4 * 64, 0, st>>>(a);
-  else if (NT == 1 && a.F <= 16) shard_owner_fm<KV, 1, 16, 1><<<grid, 16 * 64, 0, st>>>(a);
-  else if (NT == 1) shard_owner_fm<KV, 1, 16, 0><<<grid, 16 * 64, 0, st>>>(a);
-  else if (a.F <= 16) shard_owner_fm<KV, 2, 16, 1><<<grid, 16 * 64, 0, st>>>(a);
-  else shard_owner_fm<KV, 2, 16, 0><<<grid, 16 * 64, 0, st>>>(a);
+template <int KV, int NT, int NW, int MC>
+static void launch_pipe4(const EmbedFmArgs& a, PipeArgs p, hipStream_t st) {
+  const int T = NW * 64;
+  p.owner_blocks = a.F > 0 ? (int)((a.batch + 15) / 16) : 0;
+  if (p.route_blocks) p.route_blocks = (int)std::min<int64_t>((p.r.total + T - 1) / T, 4096);
+  if (p.combine_blocks) p.combine_blocks = (int)std::min<int64_t>((p.c.batch * 16 + T - 1) / T, 4096);
+  const int grid = p.owner_blocks + p.route_blocks + p.combine_blocks;
+  if (grid) shard_fm_pipe<KV, NT, NW, MC><<<grid, T, 0, st>>>(a, p);
 }
 
-// 16 lanes per sample (lane = partial column, strided by 16), DPP row sums.
-__global__ __launch_bounds__(256) void shard_fm_combine_k(const float* __restrict__ part, int world, int64_t batch,
-                                                          int64_t pst, const float* __restrict__ dense, int64_t ds,
-                                                          int nd,
-                                                          const float* __restrict__ prep, int64_t dense_rec, int NT,
-                                                          const float* __restrict__ w0, int kfm,
-                                                          float* __restrict__ logit) {
-  const int64_t b = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
-  const int cl = threadIdx.x & 15;
-  const bool valid = b < batch;
-  const int64_t bb = valid ? b : batch - 1;  // padded lanes recompute the last sample
-  float t = 0.f, lin = 0.f, q = 0.f;
-  for (int col = cl; col < kfm + 2; col += 16) {
-    float acc = 0.f;
-    for (int o = 0; o < world; ++o) acc += part[((int64_t)o * batch + bb) * pst + col];
-    for (int e = 0; e < nd; ++e) {
-      const float x = dense[bb * ds + e];
-      const float* rec = prep + (int64_t)(e >> 2) * dense_rec;
-      if (col <= kfm) acc = fmaf(x, rec[(col >> 4) * 64 + (e & 3) * 16 + (col & 15)], acc);
-      else acc = fmaf(x * x, rec[NT * 64 + (e & 3)], acc);
-    }
-    if (col < kfm) t = fmaf(acc, acc, t);
-    else if (col == kfm) lin = acc;
-    else q = acc;
+// NW / MC by the owner's field count: 4 waves x 1 slot for <= 4 fields (the
+// 8-rank shape), 16 waves for more; past 16 fields the default 2 slots.
+template <int KV>
+static void launch_pipe_kv(const EmbedFmArgs& a, const PipeArgs& p, int NT, hipStream_t st) {
+  if (NT == 1 && a.F <= 4) launch_pipe4<KV, 1, 4, 1>(a, p, st);
+  else if (NT == 1 && a.F <= 16) launch_pipe4<KV, 1, 16, 1>(a, p, st);
+  else if (NT == 1) launch_pipe4<KV, 1, 16, 0>(a, p, st);
+  else if (a.F <= 16) launch_pipe4<KV, 2, 16, 1>(a, p, st);
+  else launch_pipe4<KV, 2, 16, 0>(a, p, st);
+}
+
+static void launch_pipe(const EmbedFmArgs& a, const PipeArgs& p, const FmGeom& g, hipStream_t st) {
+  switch (g.KV) {
+    case 1: launch_pipe_kv<1>(a, p, g.NT, st); break;
+    case 2: launch_pipe_kv<2>(a, p, g.NT, st); break;
+    case 4: launch_pipe_kv<4>(a, p, g.NT, st); break;
+    case 8: launch_pipe_kv<8>(a, p, g.NT, st); break;
+    default: launch_pipe_kv<16>(a, p, g.NT, st); break;
   }
-  t = row16_sum(t);
-  lin = row16_sum(lin);
-  q = row16_sum(q);
-  if (valid && cl == 0) logit[b] = (lin + w0[0]) + 0.5f * (t - q);
 }
 
 }  // namespace rs
 
 extern "C" int rs_fm_partial_width(int kfm) { return kfm < 1 ? -1 : (kfm + 2 + 3) / 4 * 4; }
 
-extern "C" int rs_shard_owner_fm(const int32_t* local_rows, int64_t slot_stride, int field_lo, int n_owned,
-                                 const float* shard, int64_t shard_rows, int nd, int n_fields, int k,
-                                 const float* prepared, int kfm, float* partial, int64_t partial_stride,
-                                 int64_t n_pairs, int* err_flag, rs_stream_t stream) {
-  if (n_pairs == 0) return RS_OK;  // empty batch: nothing to launch
-  RS_REQUIRE(n_pairs > 0 && kfm >= 1 && nd >= 0 && k >= 1 && field_lo >= 0 && n_owned >= 0 &&
-                 field_lo + n_owned <= n_fields && n_owned <= slot_stride && shard_rows >= 0,
-             "rs_shard_owner_fm: bad shape");
-  RS_REQUIRE(partial_stride >= (kfm + 2 + 3) / 4 * 4, "rs_shard_owner_fm: partial_stride < rs_fm_partial_width");
-  RS_REQUIRE(prepared && partial && (n_owned == 0 || (local_rows && (shard || shard_rows == 0))),
-             "rs_shard_owner_fm: null pointer");
-  RS_REQUIRE((uintptr_t)shard % 16 == 0, "rs_shard_owner_fm: shard must be 16-B aligned");
-  const FmGeom g = fm_geom(nd, n_fields, k, kfm);
-  if (!g.mfma) {
-    set_error("rs_shard_owner_fm: needs the packed FM image (k in {4,8,16,32,64}, kfm <= 31)");
-    return RS_ERR_UNSUPPORTED;
-  }
-  hipStream_t st = as_stream(stream);
-  const int pw = (kfm + 2 + 3) / 4 * 4;
-  if (n_owned == 0) {  // this owner holds no rows: every partial is zero
-    (void)hipMemset2DAsync(partial, partial_stride * sizeof(float), 0, pw * sizeof(float), n_pairs, st);
-    return launch_status("rs_shard_owner_fm");
-  }
+namespace rs {
+// owner part (KIND 4) of a pipe launch over the received row-id records
+static EmbedFmArgs owner_args(const FmGeom& g, const int32_t* local_rows, int64_t rec_stride, int field_lo,
+                              int n_owned, const float* shard, int64_t shard_rows, int k, const float* prepared,
+                              int kfm, float* partial, int64_t partial_stride, int64_t n_pairs, int* err_flag) {
   EmbedFmArgs a{};
   a.ids = local_rows;
-  a.id_stride = slot_stride;
+  a.id_stride = rec_stride;
   a.nd = 0;
   a.table = shard;
   a.F = n_owned;
@@ -964,40 +999,114 @@ extern "C" int rs_shard_owner_fm(const int32_t* local_rows, int64_t slot_stride,
   a.logit = partial;
   a.batch = n_pairs;
   a.err = err_flag;
-  a.DB = 0;  // dense block: added by the requester (rs_shard_fm_combine)
+  a.DB = 0;  // dense block: added by the requester (combine part)
   a.dense_rec = g.dense_rec;
   a.field_rec = g.field_rec;
   a.field_base = g.field_base;
   a.owner_rows = shard_rows;
-  a.pw = pw;
+  a.pw = (kfm + 2 + 3) / 4 * 4;
   a.pstride = partial_stride;
-  switch (g.KV) {
-    case 1: launch_owner_kv<1>(a, g.NT, st); break;
-    case 2: launch_owner_kv<2>(a, g.NT, st); break;
-    case 4: launch_owner_kv<4>(a, g.NT, st); break;
-    case 8: launch_owner_kv<8>(a, g.NT, st); break;
-    default: launch_owner_kv<16>(a, g.NT, st); break;
+  return a;
+}
+}  // namespace rs
+
+#define RS_PIPE_GEOM(what)                                                                   \
+  const FmGeom g = fm_geom(nd, n_fields, k, kfm);                                            \
+  if (!g.mfma) {                                                                             \
+    set_error("%s: needs the packed FM image (k in {4,8,16,32,64}, kfm <= 31)", what);       \
+    return RS_ERR_UNSUPPORTED;                                                               \
+  }                                                                                          \
+  const int pw = (kfm + 2 + 3) / 4 * 4;                                                      \
+  (void)pw
+
+extern "C" int rs_shard_owner_fm(const int32_t* local_rows, int64_t rec_stride, int field_lo, int n_owned,
+                                 const float* shard, int64_t shard_rows, int nd, int n_fields, int k,
+                                 const float* prepared, int kfm, float* partial, int64_t partial_stride,
+                                 int64_t n_pairs, int* err_flag, rs_stream_t stream) {
+  if (n_pairs == 0) return RS_OK;  // empty batch: nothing to launch
+  RS_REQUIRE(n_pairs > 0 && kfm >= 1 && nd >= 0 && k >= 1 && field_lo >= 0 && n_owned >= 0 &&
+                 field_lo + n_owned <= n_fields && n_owned <= rec_stride && shard_rows >= 0,
+             "rs_shard_owner_fm: bad shape");
+  RS_REQUIRE(prepared && partial && (n_owned == 0 || (local_rows && (shard || shard_rows == 0))),
+             "rs_shard_owner_fm: null pointer");
+  RS_REQUIRE((uintptr_t)shard % 16 == 0, "rs_shard_owner_fm: shard must be 16-B aligned");
+  RS_PIPE_GEOM("rs_shard_owner_fm");
+  RS_REQUIRE(partial_stride >= pw, "rs_shard_owner_fm: partial_stride < rs_fm_partial_width");
+  hipStream_t st = as_stream(stream);
+  if (n_owned == 0) {  // this owner holds no rows: every partial is zero
+    (void)hipMemset2DAsync(partial, partial_stride * sizeof(float), 0, pw * sizeof(float), n_pairs, st);
+    return launch_status("rs_shard_owner_fm");
   }
+  PipeArgs p{};
+  launch_pipe(owner_args(g, local_rows, rec_stride, field_lo, n_owned, shard, shard_rows, k, prepared, kfm, partial,
+                         partial_stride, n_pairs, err_flag),
+              p, g, st);
   return launch_status("rs_shard_owner_fm");
 }
 
 extern "C" int rs_shard_fm_combine(const float* partials, int64_t partial_stride, int world, int64_t batch,
-                                   const float* dense,
-                                   int64_t dense_stride, int nd, int n_fields, int k, const float* prepared,
-                                   const float* w0, int kfm, float* logit, rs_stream_t stream) {
+                                   const float* dense, int64_t dense_stride, int nd, int n_fields, int k,
+                                   const float* prepared, const float* w0, int kfm, float* logit,
+                                   rs_stream_t stream) {
   if (batch == 0) return RS_OK;  // empty batch: nothing to launch
   RS_REQUIRE(batch > 0 && world >= 1 && nd >= 0 && n_fields >= 0 && kfm >= 1, "rs_shard_fm_combine: bad shape");
   RS_REQUIRE(partials && prepared && w0 && logit && (nd == 0 || dense), "rs_shard_fm_combine: null pointer");
-  const FmGeom g = fm_geom(nd, n_fields, k, kfm);
-  if (!g.mfma) {
-    set_error("rs_shard_fm_combine: needs the packed FM image (k in {4,8,16,32,64}, kfm <= 31)");
-    return RS_ERR_UNSUPPORTED;
-  }
-  RS_REQUIRE(partial_stride >= (kfm + 2 + 3) / 4 * 4, "rs_shard_fm_combine: partial_stride < rs_fm_partial_width");
-  const int64_t threads = batch * 16;
-  shard_fm_combine_k<<<(unsigned)((threads + 255) / 256), 256, 0, as_stream(stream)>>>(
-      partials, world, batch, partial_stride, dense, dense_stride, nd, prepared, g.dense_rec, g.NT, w0, kfm, logit);
+  RS_PIPE_GEOM("rs_shard_fm_combine");
+  RS_REQUIRE(partial_stride >= pw, "rs_shard_fm_combine: partial_stride < rs_fm_partial_width");
+  EmbedFmArgs a{};  // no owner part
+  PipeArgs p{};
+  p.combine_blocks = 1;
+  p.c = CombineArgs{partials, partial_stride, world, batch, dense, dense_stride, nd, prepared, g.dense_rec, g.NT,
+                    w0, kfm, logit};
+  launch_pipe(a, p, g, as_stream(stream));
   return launch_status("rs_shard_fm_combine");
+}
+
+extern "C" int rs_shard_fm_pipe(const int32_t* recv, int field_lo, int n_owned, const float* shard,
+                                int64_t shard_rows, const float* dense_prev, int64_t dense_stride, float* logit_prev,
+                                const void* ids_next, int id_kind, int64_t id_stride, const int64_t* field_offsets,
+                                const int64_t* field_vocab, int64_t rows_per_rank, const int32_t* owner_fields,
+                                int slot_stride, int32_t* send, int world, int64_t batch, int nd, int n_fields,
+                                int k, const float* prepared, const float* w0, int kfm, int* err_flag,
+                                rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch
+  RS_REQUIRE(batch > 0 && world >= 1 && world <= 64 && nd >= 0 && n_fields >= 1 && k >= 1 && kfm >= 1 &&
+                 slot_stride >= 1 && slot_stride <= n_fields && field_lo >= 0 && n_owned >= 0 &&
+                 field_lo + n_owned <= n_fields && n_owned <= slot_stride && shard_rows >= 0 && rows_per_rank >= 1,
+             "rs_shard_fm_pipe: bad shape");
+  RS_REQUIRE(recv && send && prepared && w0 && (n_owned == 0 || shard || shard_rows == 0),
+             "rs_shard_fm_pipe: null pointer");
+  RS_REQUIRE(!ids_next || (field_offsets && field_vocab && owner_fields), "rs_shard_fm_pipe: route inputs missing");
+  RS_REQUIRE(!logit_prev || nd == 0 || dense_prev, "rs_shard_fm_pipe: dense_prev is null");
+  RS_REQUIRE((uintptr_t)shard % 16 == 0, "rs_shard_fm_pipe: shard must be 16-B aligned");
+  RS_REQUIRE((int64_t)world * batch * (slot_stride + 32) < ((int64_t)1 << 31) && rows_per_rank < ((int64_t)1 << 31),
+             "rs_shard_fm_pipe: too many slots / shard rows must fit int32");
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_shard_fm_pipe: bad id_kind");
+  RS_PIPE_GEOM("rs_shard_fm_pipe");
+  const int64_t R = slot_stride + pw;  // words per fused record: [row ids | partial]
+  hipStream_t st = as_stream(stream);
+  const int64_t n_pairs = (int64_t)world * batch;
+  float* pout = reinterpret_cast<float*>(send + slot_stride);
+  const float* pin = reinterpret_cast<const float*>(recv + slot_stride);
+  EmbedFmArgs a{};
+  if (n_owned > 0) {
+    a = owner_args(g, recv, R, field_lo, n_owned, shard, shard_rows, k, prepared, kfm, pout, R, n_pairs, err_flag);
+  } else {  // no rows here: zero partials for every requester
+    (void)hipMemset2DAsync(pout, R * sizeof(float), 0, pw * sizeof(float), n_pairs, st);
+  }
+  PipeArgs p{};
+  if (ids_next) {
+    p.route_blocks = 1;
+    p.r = RouteArgs{ids_next, id_kind, id_stride, field_offsets, field_vocab, rows_per_rank, owner_fields,
+                    slot_stride, (int)batch, R, send, err_flag, (int64_t)world * batch * slot_stride};
+  }
+  if (logit_prev) {
+    p.combine_blocks = 1;
+    p.c = CombineArgs{pin, R, world, batch, dense_prev, dense_stride, nd, prepared, g.dense_rec, g.NT, w0, kfm,
+                      logit_prev};
+  }
+  launch_pipe(a, p, g, st);
+  return launch_status("rs_shard_fm_pipe");
 }
 
 extern "C" int rs_rows_fm_fwd(const float* emb, const float* dense, int64_t dense_stride, int nd, int n_fields,

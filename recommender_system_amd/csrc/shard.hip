@@ -10,6 +10,7 @@
 // rs_gather_rows serves the owner's rows; rs_unpermute_rows puts the returned
 // rows back in sample order for the FM kernel (rs_rows_fm_fwd).
 #include "rs_common.hpp"
+#include "shard_route.hpp"
 
 namespace rs {
 
@@ -297,48 +298,9 @@ __global__ __launch_bounds__(SP_THREADS) void shard_slot_onepass(ShardArgs a, ui
   }
 }
 
-// ------------------------------------------------ field route (partial protocol)
-// Block split of the concatenated table => owner o holds a contiguous FIELD
-// range [field_lo(o), field_lo(o) + n_owned(o)) (the fields its row block
-// intersects).  Message to owner o: batch records of rec_stride int32 words,
-// word j < slot_stride of record b = the local row of lookup
-// (b, field_lo(o) + j) if o owns it, else -1 (words past slot_stride are left
-// alone: the pipelined exchange keeps FM partials there).  Pure
-// index arithmetic (no scan, no capacity, no overflow); every slot is written
-// every step, so the buffer needs no initialisation.
-__global__ __launch_bounds__(256) void shard_field_route(ShardArgs a, const int32_t* __restrict__ ofl, int stride,
-                                                         int batch, int64_t rec_stride, int32_t* __restrict__ send) {
-  const int total = a.world * batch * stride;
-  for (int idx = blockIdx.x * 256 + threadIdx.x; idx < total; idx += gridDim.x * 256) {
-    const int ob = idx / stride;
-    const int j = idx - ob * stride;
-    const int o = ob / batch;
-    const int b = ob - o * batch;
-    const int c0 = ofl[2 * o], nf = ofl[2 * o + 1];
-    int32_t out = -1;
-    if (j < nf) {
-      const int c = c0 + j;
-      const int64_t off = (int64_t)b * a.id_stride + c;
-      int64_t id;
-      bool ok;
-      if (a.id_kind == RS_ID_F32) {
-        const float f = static_cast<const float*>(a.ids)[off];
-        ok = f > -1.0f && static_cast<double>(f) < static_cast<double>(a.vocab[c]);
-        id = ok ? static_cast<int64_t>(f) : 0;
-      } else {
-        id = (a.id_kind == RS_ID_I64) ? static_cast<const int64_t*>(a.ids)[off]
-                                      : static_cast<const int32_t*>(a.ids)[off];
-        ok = id >= 0 && id < a.vocab[c];
-      }
-      if (!ok) {
-        flag_error(a.err);
-      } else {
-        const int64_t local = a.offs[c] + id - (int64_t)o * a.rpr;
-        if (local >= 0 && local < a.rpr) out = (int32_t)local;
-      }
-    }
-    send[(int64_t)ob * rec_stride + j] = out;
-  }
+// field route of the partial protocol: shard_route.hpp
+__global__ __launch_bounds__(256) void shard_field_route(RouteArgs a) {
+  field_route_part<256>(a, blockIdx.x, gridDim.x);
 }
 
 template <int VW>
@@ -492,11 +454,10 @@ extern "C" int rs_shard_field_route(const void* ids, int id_kind, int64_t id_str
   RS_REQUIRE((int64_t)world * batch * slot_stride < ((int64_t)1 << 31) && rows_per_rank < ((int64_t)1 << 31),
              "rs_shard_field_route: too many slots / shard rows must fit int32");
   RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_shard_field_route: bad id_kind");
-  ShardArgs a{ids, id_kind, id_stride, field_offsets, field_vocab, n_fields, batch * n_fields, rows_per_rank, world,
-              err_flag, 1.0 / (double)rows_per_rank};
   const int64_t total = (int64_t)world * batch * slot_stride;
-  shard_field_route<<<sh_grid(total), 256, 0, as_stream(stream)>>>(a, owner_fields, slot_stride, (int)batch, rec_stride,
-                                                                     send);
+  RouteArgs a{ids, id_kind, id_stride, field_offsets, field_vocab, rows_per_rank, owner_fields, slot_stride,
+              (int)batch, rec_stride, send, err_flag, total};
+  shard_field_route<<<sh_grid(total), 256, 0, as_stream(stream)>>>(a);
   return launch_status("rs_shard_field_route");
 }
 

@@ -142,6 +142,21 @@ class HipShardOps:
              _lib.stream())
         return out
 
+    def pipe(self, sh, recv, send, prev=None, cur=None, nxt=None):
+        """rs_shard_fm_pipe: combine(prev) | owner(cur) | route(nxt) in ONE launch
+        on the fused records (sharded.py pipe_step)."""
+        lo, n_own = sh.owner_field_ranges[sh.rank]
+        B = (cur if cur is not None else (prev[0] if prev is not None else nxt[1])).shape[0]
+        if cur is None:
+            n_own = 0  # no owner part this step (its partial words are never read)
+        ids = nxt[1] if nxt is not None else None
+        call("rs_shard_fm_pipe", ptr(recv), lo, n_own, ptr(sh.table_shard), sh.table_shard.shape[0],
+             ptr(prev[0]) if prev is not None else None, prev[0].stride(0) if prev is not None else 0,
+             ptr(prev[1]) if prev is not None else None, ptr(ids), _lib.id_kind(ids) if ids is not None else 0,
+             ids.stride(0) if ids is not None else 0, ptr(sh.offsets), ptr(sh.vocab), sh.rows_per_rank,
+             ptr(sh.owner_fields), sh.slot_stride, ptr(send), sh.world, B, sh.nd, sh.F, sh.k, ptr(sh.prepared),
+             ptr(sh.w0), sh.kfm, ptr(self.err), _lib.stream())
+
     def bad_flag(self):
         """[out-of-range id seen] (device tensor; resets)."""
         v = self.err.clamp(max=1)
@@ -272,39 +287,46 @@ class ShardedEmbeddingFM:
             self._stream_bufs = sb
         return sb
 
-    def pipe_step(self, cur=None, prev=None):
-        """One exchange of the pipelined partial protocol.  cur = (dense, ids)
-        of batch t (or None), prev = (dense, out) of batch t-1 (or None):
-          rs_shard_field_route(ids_t)   -> row-id words of the fused records
-          all_to_all                    -> ONE collective: [ids of t | partials of t-1]
-          rs_shard_fm_combine(t-1)      -> out_{t-1}
-          rs_shard_owner_fm(t)          -> partial words of the fused records
-        (stream-ordered: the owner's partials of t ride the next exchange)."""
-        B = (cur[1] if cur is not None else prev[0]).shape[0]
+    def pipe_route(self, ids):
+        """Prologue of a stream: the first batch's row-id words."""
+        sb = self._sbufs(ids.shape[0])
+        self.ops.field_route(self, ids, sb["send"], rec=sb["R"])
+
+    def pipe_step(self, prev=None, cur=None, nxt=None):
+        """One step of the pipelined partial protocol, for batch t = cur:
+          all_to_all                  -> ONE collective: [row ids of t | partials of t-1]
+          rs_shard_fm_pipe (1 launch) -> combine(t-1) into prev's out
+                                         | owner partials of t  (ride the next exchange)
+                                         | field route of t+1   (ditto)
+        prev = (dense, out) of batch t-1, cur = ids of batch t (its row ids were
+        routed by the previous step or pipe_route), nxt = (dense, ids) of
+        batch t+1; any may be None."""
+        B = next(x for x in (cur, prev and prev[0], nxt and nxt[1]) if x is not None).shape[0]
         sb = self._sbufs(B)
-        S, R = self.slot_stride, sb["R"]
-        exchange = self.world > 1 or self._force_exchange
-        if cur is not None:
-            self.ops.field_route(self, cur[1], sb["send"], rec=R)
-        recv = sb["send"]
-        if exchange:
-            recv = sb["recv"]
-            dist.all_to_all_single(recv, sb["send"], group=self.group)
-        if prev is not None:
-            self.ops.combine(self, recv, prev[0], prev[1], poff=S, pst=R)
-        if cur is not None:
-            self.ops.owner_partials(self, recv, self.world * B, sb["send"], rec=R, poff=S, pst=R)
+        if self.world > 1 or self._force_exchange:
+            dist.all_to_all_single(sb["recv"], sb["send"], group=self.group)
+            self.ops.pipe(self, sb["recv"], sb["send"], prev=prev, cur=cur, nxt=nxt)
+        else:
+            # no exchange: the launch must not write the records it reads, so
+            # the two buffers alternate (read "send", write "recv", swap)
+            self.ops.pipe(self, sb["send"], sb["recv"], prev=prev, cur=cur, nxt=nxt)
+            sb["send"], sb["recv"] = sb["recv"], sb["send"]
 
     def forward_stream(self, batches, check=True):
         """FM logits of a sequence of local batches [(dense, ids), ...] with the
         pipelined partial protocol: batch t's row-id message and batch t-1's
-        partials share one all-to-all, so a stream of n batches costs n + 1
-        collectives instead of 2n.  Returns [logit [B,1] per batch]."""
+        partials share one all-to-all and one launch, so a stream of n batches
+        costs n + 1 collectives and n + 2 launches (vs 2n and 3n).  Returns
+        [logit [B,1] per batch]."""
+        n = len(batches)
         outs = [torch.empty(ids.shape[0], 1, dtype=torch.float32, device=self.device) for _, ids in batches]
-        for t in range(len(batches) + 1):
-            cur = batches[t] if t < len(batches) else None
+        if n:
+            self.pipe_route(batches[0][1])
+        for t in range(n + 1):
             prev = (batches[t - 1][0], outs[t - 1]) if t > 0 else None
-            self.pipe_step(cur, prev)
+            cur = batches[t][1] if t < n else None
+            nxt = batches[t + 1] if t + 1 < n else None
+            self.pipe_step(prev, cur, nxt)
         if check:
             f = self.ops.bad_flag()
             if self.world > 1:

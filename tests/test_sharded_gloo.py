@@ -130,6 +130,15 @@ class CpuOps:
         out.copy_(torch.as_tensor(logit.reshape(B, 1), dtype=torch.float32))
         return out
 
+    def pipe(self, sh, recv, send, prev=None, cur=None, nxt=None):
+        R = sh.slot_stride + sh.partial_width
+        if prev is not None:
+            self.combine(sh, recv, prev[0], prev[1], poff=sh.slot_stride, pst=R)
+        if cur is not None:
+            self.owner_partials(sh, recv, cur.shape[0] * sh.world, send, rec=R, poff=sh.slot_stride, pst=R)
+        if nxt is not None:
+            self.field_route(sh, nxt[1], send, rec=R)
+
     def bad_flag(self):
         return torch.zeros(1, dtype=torch.int32)
 
@@ -254,6 +263,10 @@ def test_gpu_sharded_single_rank_equals_fused(gpu):
     a = sh.forward_slots(dense, ids)           # fixed-capacity row slots
     e = sh.forward_exact(dense, ids)           # counts + variable splits
     pp = sh.forward(dense, ids)                # owner FM partials (default)
+    ids2 = torch.as_tensor(np.stack([rng.integers(0, v, B) for v in vocabs], 1), dtype=torch.int32, device=gpu)
+    dense2 = torch.rand(B, 13, device=gpu)
+    st = sh.forward_stream([(dense, ids), (dense2, ids2), (dense, ids)])  # pipelined, one launch per step
+    np.testing.assert_allclose(st[1].cpu().numpy(), sh.forward(dense2, ids2).cpu().numpy(), rtol=1e-6, atol=1e-7)
     sh._slot_bufs = None
     sh.capacity = lambda n: 7                  # forced overflow -> exact fallback
     f = sh.forward_slots(dense, ids)
@@ -265,6 +278,8 @@ def test_gpu_sharded_single_rank_equals_fused(gpu):
     np.testing.assert_allclose(e.cpu().numpy(), b.cpu().numpy(), rtol=1e-6, atol=1e-6)
     np.testing.assert_allclose(f.cpu().numpy(), b.cpu().numpy(), rtol=1e-6, atol=1e-6)
     np.testing.assert_allclose(pp.cpu().numpy(), b.cpu().numpy(), rtol=1e-6, atol=1e-6)
+    for o in (st[0], st[2]):
+        np.testing.assert_allclose(o.cpu().numpy(), b.cpu().numpy(), rtol=1e-6, atol=1e-6)
     bad = ids.clone()
     bad[3, 5] = vocabs[5]
     sh.capacity = lambda n: max(n, 1)
@@ -365,3 +380,49 @@ def test_gpu_slot_bucketize_matches_reference(gpu, world, cap):
     np.testing.assert_array_equal(so.cpu().numpy(), rso.numpy())
     np.testing.assert_array_equal(send.cpu().numpy(), rsend.numpy())
     assert bool(bufs["overflow"].item()) == ref.overflow
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_gpu_pipe_kernel_simulated_world(gpu, world):
+    """rs_shard_fm_pipe (combine t-1 | owner t | route t+1 in one launch) over
+    a stream of 3 batches per simulated rank, the all-to-all done as a block
+    transpose of the fused records: every batch's logit equals the unsharded
+    fused kernel."""
+    from recommender_system_amd import _lib
+    from recommender_system_amd.sharded import ShardedEmbeddingFM
+    rng = np.random.default_rng(world + 40)
+    vocabs = [int(v) for v in rng.integers(1, 3000, 26)]
+    B, nd, k, kfm, T = 300, 13, 16, 10, 3
+    shs = [ShardedEmbeddingFM(vocabs, k, nd, kfm, device=gpu, seed=5, table_init=False, world=world, rank=r)
+           for r in range(world)]
+    full = torch.empty(shs[0].total_rows, k, device=gpu).uniform_(-0.05, 0.05)
+    for sh in shs:
+        lo, hi = sh.row_range
+        sh.table_shard = full[lo:hi].contiguous()
+    batches = [[(torch.rand(B, nd, device=gpu),
+                 torch.as_tensor(np.stack([rng.integers(0, v, B) for v in vocabs], 1), dtype=torch.int32,
+                                 device=gpu)) for _ in range(T)] for _ in range(world)]
+    outs = [[torch.full((B, 1), float("nan"), device=gpu) for _ in range(T)] for _ in range(world)]
+    for r, sh in enumerate(shs):
+        sh.pipe_route(batches[r][0][1])
+    R = shs[0].slot_stride + shs[0].partial_width
+    for t in range(T + 1):
+        sends = [sh._sbufs(B)["send"] for sh in shs]
+        recvs = [torch.cat([sends[q].view(world, B * R)[o] for q in range(world)]) for o in range(world)]
+        for r, sh in enumerate(shs):
+            prev = (batches[r][t - 1][0], outs[r][t - 1]) if t > 0 else None
+            cur = batches[r][t][1] if t < T else None
+            nxt = batches[r][t + 1] if t + 1 < T else None
+            sh.ops.pipe(sh, recvs[r], sends[r], prev=prev, cur=cur, nxt=nxt)
+    for r, sh in enumerate(shs):
+        for t in range(T):
+            dense, ids = batches[r][t]
+            ref = torch.empty(B, 1, device=gpu)
+            _lib.call("rs_embed_fm_fwd", ids.data_ptr(), 0, 26, dense.data_ptr(), nd, nd, full.data_ptr(),
+                      sh.offsets.data_ptr(), sh.vocab.data_ptr(), 26, k, sh.prepared.data_ptr(), sh.w0.data_ptr(),
+                      kfm, ref.data_ptr(), None, B, None, _lib.stream())
+            g, f = outs[r][t].cpu().numpy(), ref.cpu().numpy()
+            rms = float(np.sqrt(np.mean(f ** 2)))
+            assert np.all(np.abs(g - f) <= 1e-5 * np.maximum(np.abs(f), rms)), (r, t)
+        sh.ops.check()
