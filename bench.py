@@ -24,7 +24,7 @@ Also measured (nested in the JSON line, not `value`):
   * `cpu_baseline`: the oracle's numpy fp32 restatement of the reference
     forward (TF unavailable) on the same table and batches, bounded sample.
 
-Other configs (own JSON line): --config deepfm1e6 | dcn | din | pnn.
+Other configs (own JSON line): --config deepfm1e6 | dcn | din | pnn | nfm | afm | ffm.
 """
 from __future__ import annotations
 
@@ -660,6 +660,92 @@ def bench_pnn(args, world, rank):
                                         "note": "product inputs + DNN tower (rs_mlp_fwd, K = 741)"}})
 
 
+def _rank3_setup(args, k, nd=13):
+    B, F = args.batch, 26
+    V = int(args.vocab if args.vocab != 1e7 else 1e6)
+    cols = [[{"feat": f"I{i + 1}"} for i in range(nd)],
+            [{"feat": f"C{i + 1}", "feat_onehot_dim": V, "embed_dim": k} for i in range(F)]]
+    ids_pool, dense_pool = _pool(B, [V] * F, nd, 64, torch.device("cuda"))
+    return B, F, V, cols, ids_pool, dense_pool
+
+
+def _hbm_line(metric, args, world, B, dt, slot, alg, workload, V, kernel, extra=None):
+    ach = alg / (slot * 1e-3)
+    return _line(metric, args.steps * B / dt, "samples/s", args, world, dt / args.steps * 1e3,
+                 {"workload": workload, "global_batch": B, "vocab_per_field": V, "parallelism": "dp1"},
+                 {"bound": "hbm", "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                  "frac": ach / PEAK_HBM, "traffic": None, "kernel": kernel, "kernel_ms": slot,
+                  "algorithmic_bytes_per_launch": alg}, extra)
+
+
+def bench_nfm(args, world, rank):
+    """NFM (model/nfm.py, 3-D embeddings): ids -> rows -> bi-interaction ->
+    [dense | pooled] in one launch (the headline), then BN + DNN tower."""
+    import recommender_system_amd as rs
+    k = 16
+    B, F, V, cols, ids_pool, dense_pool = _rank3_setup(args, k)
+    m = rs.NFM(cols, [256, 128, 64], 1, embed_dim=k, seed=SEED, device=torch.device("cuda"))
+
+    def step(i):
+        m.bi_interaction_input((dense_pool[i % 64], ids_pool[i % 64]), check_ids=False)
+
+    def full(i):
+        m((dense_pool[i % 64], ids_pool[i % 64]), check_ids=False)
+
+    dt, slot = _timed_graph(step, args.steps, args.warmup, world)
+    n2 = max(10, args.steps // 5)
+    dtf, _ = _timed_graph(full, n2, args.warmup, world, chunk=16)
+    alg = B * (F * 4 + F * k * 4 + 13 * 4 + (13 + k) * 4)
+    return _hbm_line("NFM bi-interaction input samples/sec @ batch 4096, 26 sparse x 1e6 vocab, dim 16", args,
+                     world, B, dt, slot, alg, "nfm_embed_bi_interaction_fused", V, "pair_pool_kernel (sum)",
+                     {"nfm_forward": {"samples_per_s": n2 * B / dtf, "ms_per_step": dtf / n2 * 1e3,
+                                      "note": "bi-interaction launch + BN + DNN 29-256-128-64-1 + Dense(1) tower"}})
+
+
+def bench_afm(args, world, rank):
+    """AFM (model/afm.py): ids -> rows -> pair pooling -> Dense(1) -> 2 sigmoids
+    in one launch; 'att' (== sum, the reference's size-1 softmax) and 'max'."""
+    import recommender_system_amd as rs
+    k = 16
+    B, F, V, cols, ids_pool, dense_pool = _rank3_setup(args, k)
+    dev = torch.device("cuda")
+    m = rs.AFM(cols, "att", seed=SEED, device=dev)
+    mx = rs.AFM(cols, "max", seed=SEED, device=dev)
+
+    def step(i):
+        m((dense_pool[i % 64], ids_pool[i % 64]), check_ids=False)
+
+    def step_max(i):
+        mx((dense_pool[i % 64], ids_pool[i % 64]), check_ids=False)
+
+    dt, slot = _timed_graph(step, args.steps, args.warmup, world)
+    dtm, slotm = _timed_graph(step_max, args.steps, args.warmup, world)
+    alg = B * (F * 4 + F * k * 4 + 4)
+    return _hbm_line("AFM forward samples/sec @ batch 4096, 26 sparse x 1e6 vocab, dim 16", args, world, B, dt,
+                     slot, alg, "afm_att_fused", V, "pair_pool_kernel (att == sum)",
+                     {"mode_max": {"samples_per_s": args.steps * B / dtm, "kernel_ms": slotm,
+                                   "note": "max over the 325 pair products per dim, in registers"}})
+
+
+def bench_ffm(args, world, rank):
+    """FFM (model/ffm.py): one wave per sample gathers 26 rows of the
+    [feature_num, 39, k] field-aware table (k = 8: 1,248-B rows)."""
+    import recommender_system_amd as rs
+    k = 8
+    B, F, V, cols, ids_pool, dense_pool = _rank3_setup(args, k)
+    m = rs.FFM(cols, k, seed=SEED, device=torch.device("cuda"))
+
+    def step(i):
+        m((dense_pool[i % 64], ids_pool[i % 64]))
+
+    dt, slot = _timed_graph(step, args.steps, args.warmup, world)
+    NF = 13 + F
+    alg = B * (F * 4 + 13 * 4 + F * NF * k * 4 + F * 4 + 4)
+    return _hbm_line("FFM forward samples/sec @ batch 4096, 26 sparse x 1e6 vocab, k 8", args, world, B, dt, slot,
+                     alg, "ffm_fused", V, "ffm_kernel",
+                     {"table_GB": (13 + F * V) * NF * k * 4 / 1e9})
+
+
 def _pmc_traffic():
     p = os.path.join(ROOT, "profiles", "pmc_embed_fm.json")
     try:
@@ -684,7 +770,8 @@ def main():
                     help="time the row-sharded exchange path even at world 1 (N=1 point of the sharded curve)")
     args = ap.parse_args()
     world, rank = _dist_setup(args)
-    other = {"dcn": bench_dcn, "din": bench_din, "pnn": bench_pnn}
+    other = {"dcn": bench_dcn, "din": bench_din, "pnn": bench_pnn, "nfm": bench_nfm, "afm": bench_afm,
+             "ffm": bench_ffm}
     if args.config in other:
         line = other[args.config](args, world, rank)
         if rank == 0:

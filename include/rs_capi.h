@@ -313,6 +313,47 @@ int rs_dice_fwd(const float* x, int64_t x_stride, const float* mean,
 int rs_sigmoid_combine(const float* a, const float* b, float c0, float c1,
                        float* out, int64_t n, rs_stream_t stream);
 
+/* ------------------------- other interactions on the gather (§8(f) rank 3)
+ * rs_embed_pair_pool_fwd: per sample, the F field rows e_c (one concatenated
+ *  table, per-field offsets) pooled over the P = F(F-1)/2 pair products
+ *  e_i*e_j (per dim): mode 0 = sum = 0.5((sum e)^2 - sum e^2) — NFM's
+ *  bi-interaction (model/nfm.py:28) and AFM 'att' (AttentionLayer's softmax
+ *  over a size-1 axis is 1, layer/interaction.py:313-318); mode 1 = mean
+ *  (AFM 'avg'); mode 2 = max (AFM 'max', F <= 64).  Outputs (any subset):
+ *  out[b*out_stride + out_col + j] = pooled_j and out[b*out_stride + i] =
+ *  dense[b, i] for i < nd (NFM's concat([dense, emb]), model/nfm.py:29);
+ *  head_out[b] = sigmoid^n_sigmoid(pooled @ head_w + head_b) (AFMLayer's
+ *  Dense(1) + sigmoid, then AFM.call's second sigmoid: n_sigmoid = 2).
+ * rs_pair_products_fwd: InteractionLayer (layer/interaction.py:280-297):
+ *  e [batch, F*k] (row stride e_stride) -> out [batch, P, k], pairs i<j
+ *  row-major.
+ * rs_ffm_fwd: FFMLayer.call + FFM.call (layer/interaction.py:134-163,
+ *  model/ffm.py:20-22) on label-encoded ids: x = [dense | one-hot], feature
+ *  f = nd + field_offsets[c] + id; v [feature_num, (nd+F)*k], w
+ *  [feature_num]; out[b] = sigmoid^n_sigmoid(w0 + x@w + sum_{f<g}
+ *  <field_f, field_g>), field = x @ v; k divides 64, (nd+F)*k <= 1024.      */
+int rs_embed_pair_pool_fwd(const void* ids, int id_kind, int64_t id_stride,
+                           const float* table, const int64_t* field_offsets,
+                           const int64_t* field_vocab, int n_fields, int k,
+                           int mode, const float* dense, int64_t dense_stride,
+                           int nd, float* out, int64_t out_stride, int out_col,
+                           const float* head_w, const float* head_b,
+                           int n_sigmoid, float* head_out, int64_t batch,
+                           int* err_flag, rs_stream_t stream);
+int rs_pair_products_fwd(const float* e, int64_t e_stride, int n_fields, int k,
+                         int64_t batch, float* out, rs_stream_t stream);
+/* AttentionLayer.call (layer/interaction.py:310-319) on x [batch, n_rows, k]
+ * (row stride x_stride): its softmax runs over a size-1 axis (every score is
+ * exactly 1), so out[b, j] = sum_p x[b, p, j].                             */
+int rs_attention_pool_fwd(const float* x, int64_t x_stride, int n_rows, int k,
+                          int64_t batch, float* out, rs_stream_t stream);
+int rs_ffm_fwd(const void* ids, int id_kind, int64_t id_stride,
+               const float* dense, int64_t dense_stride, int nd,
+               const float* v, const float* w, const float* w0,
+               const int64_t* field_offsets, const int64_t* field_vocab,
+               int n_fields, int k, int n_sigmoid, float* out, int64_t batch,
+               int* err_flag, rs_stream_t stream);
+
 /* -------------------------------------- row-sharded lookup (§8(e), cfg 5)
  * Global row of (b,c) = field_offsets[c] + id(b,c).  Rows are split across
  * `world` ranks in blocks of `rows_per_rank` (owner = row / rows_per_rank).

@@ -366,3 +366,100 @@ def din(inputs, p, dense_feats, sparse_feats, behavior_feats, dt=np.float64,
     for kern, bias, alpha in p["dnn"]:
         emb = dense(emb, kern, bias, "prelu", alpha, dt=dt)
     return sigmoid(dense(emb, p["out"][0], p["out"][1], dt=dt)), att
+
+
+# ------------------------------------ other interactions
+def interaction_layer(e, dt=np.float64):
+    """InteractionLayer.call (layer/interaction.py:286-297): [B,F,k] ->
+    [B,P,k] element-wise products of the (i<j) row-major pairs."""
+    e = np.asarray(e, dt)
+    prods = [e[:, i] * e[:, j] for i in range(e.shape[1]) for j in range(i + 1, e.shape[1])]
+    return np.transpose(np.asarray(prods), (1, 0, 2))
+
+
+def attention_layer(x, p, dt=np.float64):
+    """AttentionLayer.call (layer/interaction.py:310-319) op for op:
+    Dense(P, relu) -> Dense(1) -> tf.nn.softmax over the LAST axis (size 1:
+    every score is exactly 1) -> transpose -> matmul with the inputs."""
+    x = np.asarray(x, dt)
+    h = activation(np.tensordot(x, np.asarray(p["att_w_kernel"], dt), axes=1) + np.asarray(p["att_w_bias"], dt),
+                   "relu")
+    s = np.tensordot(h, np.asarray(p["att_h_kernel"], dt), axes=1) + np.asarray(p["att_h_bias"], dt)  # [B,P,1]
+    e = np.exp(s - s.max(axis=-1, keepdims=True))
+    a = e / e.sum(axis=-1, keepdims=True)                                     # softmax over axis -1
+    a = np.transpose(a, (0, 2, 1))                                            # [B,1,P]
+    return np.matmul(a, x).reshape(-1, x.shape[2])
+
+
+def afm(X, p, mode, nd=13, dt=np.float64, inputs=None):
+    """AFM.call (model/afm.py:15-19) over AFMLayer.call
+    (layer/interaction.py:333-351): per-field Embedding(feat_onehot_dim,
+    embed_dim) -> [B,F,k] -> InteractionLayer -> mean / max / attention over
+    the pairs -> Dense(1) -> sigmoid, then AFM's second sigmoid."""
+    _, sparse = inputs if inputs is not None else _split_dense_sparse(X, nd, dt)
+    sparse = np.asarray(sparse)
+    embed = np.transpose(np.stack([embedding_lookup(np.asarray(t, dt), sparse[:, i])
+                                   for i, t in enumerate(p["tables"])], 0), (1, 0, 2))
+    pairs = interaction_layer(embed, dt)
+    if mode == "avg":
+        x = np.mean(pairs, axis=1)
+    elif mode == "max":
+        x = np.max(pairs, axis=1)
+    else:
+        x = attention_layer(pairs, p, dt)
+    out = sigmoid(dense(x, p["out_kernel"], p["out_bias"], dt=dt))
+    return sigmoid(out), x
+
+
+def bi_interaction(e, dt=np.float64):
+    """NFM's Bi-Interaction (model/nfm.py:28) on a 3-D embedding [B,F,k]:
+    0.5 * (sum_f e)^2 - sum_f e^2, per dim -> [B,k]."""
+    e = np.asarray(e, dt)
+    return 0.5 * (np.power(np.sum(e, axis=1), 2) - np.sum(np.power(e, 2), axis=1))
+
+
+def nfm(X, p, nd=13, dt=np.float64, inputs=None):
+    """NFM.call (model/nfm.py:22-33) with 3-D embeddings (documented
+    deviation: on the reference's rank-2 EmbedLayer output the reduce_sum over
+    axis 1 yields [B] and the concat with the dense block fails):
+    x = BN(concat([dense, BiInteraction(emb)])) -> DNNLayer -> Dense(1) -> sigmoid."""
+    dense_in, sparse = inputs if inputs is not None else _split_dense_sparse(X, nd, dt)
+    flat = embed_layer(sparse, p["tables"], dt)
+    k = np.asarray(p["tables"][0]).shape[1]
+    emb = bi_interaction(flat.reshape(flat.shape[0], -1, k), dt)
+    x = np.concatenate([np.asarray(dense_in, dt), emb], axis=-1)
+    x = batchnorm_inference(x, p["bn_mean"], p["bn_var"], p.get("bn_gamma"), p.get("bn_beta"), dt=dt)
+    x = dnn_layer(x, p["dnn_hidden"], p["dnn_out"], p.get("act", "relu"), dt=dt)
+    return sigmoid(dense(x, p["out_kernel"], p["out_bias"], dt=dt)), emb
+
+
+def ffm_layer(dense_in, sparse, onehot_dims, w0, w, v, dt=np.float64):
+    """FFMLayer.call (layer/interaction.py:134-163) op for op: x = [dense |
+    one_hot(id_c, feat_onehot_dim_c) ...]; linear = w0 + x@w; field_f =
+    tensordot(x, v) [B, NF, k]; inter = sum_{i<j} sum(field_f[:,i] *
+    field_f[:,j]).  Builds the dense one-hot matrix: small vocabularies only."""
+    dense_in = np.asarray(dense_in, dt)
+    ids = cast_ids(sparse)
+    B = dense_in.shape[0]
+    parts = [dense_in]
+    for c, depth in enumerate(onehot_dims):
+        col = ids[:, c]
+        oh = np.zeros((B, depth), dt)
+        ok = (col >= 0) & (col < depth)  # tf.one_hot: out-of-range -> zero row
+        oh[np.nonzero(ok)[0], col[ok]] = 1.0
+        parts.append(oh)
+    x = np.concatenate(parts, axis=1)
+    linear = np.asarray(w0, dt) + x @ np.asarray(w, dt)
+    field_f = np.tensordot(x, np.asarray(v, dt), axes=1)
+    inter = np.zeros((B, 1), dt)
+    NF = field_f.shape[1]
+    for i in range(NF):
+        for j in range(i + 1, NF):
+            inter += np.sum(field_f[:, i] * field_f[:, j], axis=1, keepdims=True)
+    return linear + inter
+
+
+def ffm(X, p, onehot_dims, nd=13, dt=np.float64, inputs=None):
+    """FFM.call (model/ffm.py:20-22): sigmoid(FFMLayer(inputs))."""
+    dense_in, sparse = inputs if inputs is not None else _split_dense_sparse(X, nd, dt)
+    return sigmoid(ffm_layer(dense_in, sparse, onehot_dims, p["w0"], p["w"], p["v"], dt=dt))

@@ -7,9 +7,10 @@ DIN attention), as hand-written gfx950 HIP kernels behind a C-ABI
 reference's Keras layer / model names and signatures.
 """
 from . import _lib  # noqa: F401
-from .layers import (Attention, BatchNormalization, CrossLayer, Dense, Dice, DNNLayer, EmbedLayer,  # noqa: F401
-                     FMLayer, InnerProductLayer, OuterProductLayer, sigmoid_combine)
-from .models import DCN, DIN, FM, PNN, DeepFM  # noqa: F401
+from .layers import (AFMLayer, Attention, AttentionLayer, BatchNormalization, CrossLayer, Dense, Dice,  # noqa: F401
+                     DNNLayer, EmbedLayer, FFMLayer, FMLayer, InnerProductLayer, InteractionLayer,
+                     OuterProductLayer, sigmoid_combine)
+from .models import AFM, DCN, DIN, FFM, FM, NFM, PNN, DeepFM  # noqa: F401
 from .dataset import create_criteo_dataset, denseFeature, features_dict, sparseFeature  # noqa: F401
 
 __version__ = "0.1.0"

@@ -64,6 +64,10 @@ SIGNATURES = {
     "rs_unpermute_rows": (I, [P, P, I, L, P, P]),
     "rs_rows_fm_fwd": (I, [P, P, L, I, I, I, P, P, I, P, L, P]),
     "rs_fm_partial_width": (I, [I]),
+    "rs_embed_pair_pool_fwd": (I, [P, I, L, P, P, P, I, I, I, P, L, I, P, L, I, P, P, I, P, L, P, P]),
+    "rs_pair_products_fwd": (I, [P, L, I, I, L, P, P]),
+    "rs_attention_pool_fwd": (I, [P, L, I, I, L, P, P]),
+    "rs_ffm_fwd": (I, [P, I, L, P, L, I, P, P, P, P, P, I, I, I, P, L, P, P]),
     "rs_shard_field_route": (I, [P, I, L, P, P, I, L, L, I, P, I, L, P, P, P]),
     "rs_shard_owner_fm": (I, [P, L, I, I, P, L, I, I, I, P, I, P, L, L, P, P]),
     "rs_shard_fm_combine": (I, [P, L, I, L, P, L, I, I, I, P, P, I, P, P]),

@@ -783,3 +783,178 @@ def sigmoid_combine(a, b=None, c0=1.0, c1=1.0, out=None):
         out = torch.empty_like(a)
     call("rs_sigmoid_combine", ptr(a), ptr(b), float(c0), float(c1), ptr(out), a.numel(), _stream())
     return out
+
+
+# ------------------------------------ other interactions
+class InteractionLayer(KerasModule):
+    """InteractionLayer() — layer/interaction.py:280-297: [B,F,k] -> [B,P,k]
+    element-wise products of the (i<j) row-major field pairs
+    (rs_pair_products_fwd)."""
+
+    def __init__(self, device=None):
+        super().__init__(device)
+
+    def forward(self, inputs, out=None):
+        e = _to_device_f32(inputs, self._dev).contiguous()
+        B, F, k = e.shape
+        P = F * (F - 1) // 2
+        if out is None:
+            out = torch.empty(B, P, k, dtype=torch.float32, device=self._dev)
+        call("rs_pair_products_fwd", ptr(e), F * k, F, k, B, ptr(out), _stream())
+        return out
+
+
+class AttentionLayer(KerasModule):
+    """AttentionLayer() — layer/interaction.py:300-319.  Holds the reference's
+    weights (attention_w = Dense(n_rows, relu), attention_h = Dense(1)) for
+    Keras-name weight exchange; its softmax runs over a size-1 axis, so every
+    score is exactly 1 and the output is the sum over the rows
+    (rs_attention_pool_fwd) — the weights cannot change the result."""
+
+    def __init__(self, device=None, seed=None):
+        super().__init__(device, seed)
+        self.attention_w = self.attention_h = None
+
+    def build(self, n_rows, k):
+        self.attention_w = Dense(n_rows, activation="relu", device=self._dev, seed=_subseed(self._gen),
+                                 input_dim=k)
+        self.attention_h = Dense(1, device=self._dev, seed=_subseed(self._gen), input_dim=n_rows)
+
+    def keras_weights(self):
+        if self.attention_w is None:
+            return {}
+        out = {f"dense/{n}": v for n, v in self.attention_w.keras_weights().items()}
+        out.update({f"dense_1/{n}": v for n, v in self.attention_h.keras_weights().items()})
+        return out
+
+    def set_keras_weights(self, weights, strict=True):
+        self.attention_w.set_keras_weights({n[6:]: v for n, v in weights.items() if n.startswith("dense/")}, strict)
+        self.attention_h.set_keras_weights({n[8:]: v for n, v in weights.items() if n.startswith("dense_1/")},
+                                           strict)
+
+    def forward(self, inputs, out=None):
+        x = _to_device_f32(inputs, self._dev).contiguous()
+        B, P, k = x.shape
+        if self.attention_w is None:
+            self.build(P, k)
+        if out is None:
+            out = torch.empty(B, k, dtype=torch.float32, device=self._dev)
+        call("rs_attention_pool_fwd", ptr(x), P * k, P, k, B, ptr(out), _stream())
+        return out
+
+
+def _subseed(gen):
+    return int(torch.randint(0, 2 ** 31, (1,), generator=gen))
+
+
+_AFM_MODES = {"att": 0, "avg": 1, "max": 2}
+
+
+class AFMLayer(KerasModule):
+    """AFMLayer(feature_columns, mode) — layer/interaction.py:322-351:
+    per-field Embedding(feat_onehot_dim, embed_dim) -> InteractionLayer ->
+    'avg' mean / 'max' max / attention (== sum) over the pairs -> Dense(1) ->
+    sigmoid.  ids -> rows -> pooled pairs -> head in ONE launch
+    (rs_embed_pair_pool_fwd); the [B,P,k] pair tensor is never formed."""
+
+    def __init__(self, feature_columns, mode, device=None, seed=None):
+        super().__init__(device, seed)
+        self.dense_feature_columns, self.sparse_feature_columns = feature_columns
+        self.mode = mode
+        dims = {int(f["embed_dim"]) for f in self.sparse_feature_columns}
+        if len(dims) != 1:
+            raise ValueError("AFMLayer: every sparse feature needs the same embed_dim (the pairs are stacked)")
+        self.k = dims.pop()
+        self.nd = len(self.dense_feature_columns)
+        self.embed_layer = EmbedLayer(self.sparse_feature_columns, self.k, device=device, seed=_subseed(self._gen))
+        self.interaction_layer = InteractionLayer(device=device)
+        F = self.embed_layer.n_fields
+        self.attention_layer = None
+        if mode == "att":
+            self.attention_layer = AttentionLayer(device=device, seed=_subseed(self._gen))
+            self.attention_layer.build(F * (F - 1) // 2, self.k)
+        self.output_layer = Dense(1, device=device, seed=_subseed(self._gen), input_dim=self.k)
+        self._err = _ErrFlag(self._dev)
+
+    def pooled(self, inputs, check_ids=True, n_sigmoid=1):
+        """(pooled [B,k], head [B,1] = sigmoid^n_sigmoid(Dense(1)(pooled)))."""
+        if isinstance(inputs, (tuple, list)):
+            ids = _ids_tensor(inputs[1], self._dev)
+        else:
+            ids = _to_device_f32(inputs, self._dev)[:, self.nd:]
+        B = ids.shape[0]
+        e = self.embed_layer
+        pooled = torch.empty(B, self.k, dtype=torch.float32, device=self._dev)
+        head = torch.empty(B, 1, dtype=torch.float32, device=self._dev)
+        call("rs_embed_pair_pool_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(e.table),
+             ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, self.k, _AFM_MODES.get(self.mode, 0), None, 0, 0,
+             ptr(pooled), self.k, 0, ptr(self.output_layer.kernel), ptr(self.output_layer.bias), n_sigmoid,
+             ptr(head), B, ptr(self._err.t), _stream())
+        if check_ids:
+            self._err.check("AFMLayer")
+        return pooled, head
+
+    def forward(self, inputs, check_ids=True):
+        return self.pooled(inputs, check_ids, n_sigmoid=1)[1]
+
+
+class FFMLayer(KerasModule):
+    """FFMLayer(feature_columns, k, w_reg=1e-4, v_reg=1e-4) —
+    layer/interaction.py:117-163.  Weights in Keras shapes: w0 (1,), w
+    (feature_num, 1), v (feature_num, field_num, k), feature_num = nd +
+    sum(feat_onehot_dim), field_num = nd + F.  ``forward(X[B, nd+F])`` on
+    label-encoded ids: the one-hot x is never formed — row nd + offset_c + id
+    of w and v is gathered (rs_ffm_fwd, one wave per sample)."""
+
+    def __init__(self, feature_columns, k, w_reg=1e-4, v_reg=1e-4, device=None, seed=None):
+        super().__init__(device, seed)
+        self.dense_feature_columns, self.sparse_feature_columns = feature_columns
+        self.k = int(k)
+        self.w_reg, self.v_reg = w_reg, v_reg
+        self.nd = len(self.dense_feature_columns)
+        self.onehot_dims = [int(f["feat_onehot_dim"]) for f in self.sparse_feature_columns]
+        self.feature_num = sum(self.onehot_dims) + self.nd
+        self.field_num = self.nd + len(self.sparse_feature_columns)
+        offs = [0]
+        for v in self.onehot_dims[:-1]:
+            offs.append(offs[-1] + v)
+        dev = self._dev
+        self.register_buffer("field_offsets", torch.tensor(offs, dtype=torch.int64, device=dev))
+        self.register_buffer("field_vocab", torch.tensor(self.onehot_dims, dtype=torch.int64, device=dev))
+        self.w0 = nn.Parameter(torch.zeros(1, device=dev), requires_grad=False)
+        self.w = nn.Parameter(_normal((self.feature_num, 1), self._gen, dev), requires_grad=False)
+        v = torch.empty(self.feature_num, self.field_num, self.k, dtype=torch.float32, device=dev)
+        if v.is_cuda:
+            g = torch.Generator(device=v.device)
+            g.manual_seed(_subseed(self._gen))
+            v.normal_(0.0, 0.05, generator=g)
+        else:
+            v.normal_(0.0, 0.05, generator=self._gen)
+        self.v = nn.Parameter(v, requires_grad=False)
+        self._err = _ErrFlag(dev)
+
+    def keras_weights(self):
+        return {"w0": self.w0, "w": self.w, "v": self.v}
+
+    def set_keras_weights(self, weights, strict=True):
+        with torch.no_grad():
+            for name, p in self.keras_weights().items():
+                p.copy_(torch.as_tensor(weights[name], dtype=torch.float32).reshape(p.shape))
+
+    def logits(self, inputs, n_sigmoid=0):
+        if isinstance(inputs, (tuple, list)):
+            dense, ids = _to_device_f32(inputs[0], self._dev), _ids_tensor(inputs[1], self._dev)
+        else:
+            X = _to_device_f32(inputs, self._dev)
+            dense, ids = X[:, :self.nd], X[:, self.nd:]
+        B = ids.shape[0]
+        out = torch.empty(B, 1, dtype=torch.float32, device=self._dev)
+        # tf.one_hot (layer/interaction.py:145-146) maps an out-of-range id to
+        # a zero row without an error: the kernel does the same (no check)
+        call("rs_ffm_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), self.nd,
+             ptr(self.v), ptr(self.w), ptr(self.w0), ptr(self.field_offsets), ptr(self.field_vocab),
+             len(self.onehot_dims), self.k, n_sigmoid, ptr(out), B, None, _stream())
+        return out
+
+    def forward(self, inputs):
+        return self.logits(inputs, 0)

@@ -13,6 +13,10 @@ models (Hcyand/recommender_system, algorithm/deep_learning/model/):
   DIN(feature_columns, behavior_feature_list, att_hidden_units=(80, 40),
       dnn_hidden_units=(256, 128, 64), att_attention='prelu',
       dnn_activation='prelu', dnn_dropout=0.0)                    model/din.py:15-95
+  NFM(feature_columns, hidden_units, output_dim, activation='relu', dropout=0)
+                                                                  model/nfm.py:13-33
+  AFM(feature_columns, mode)                                      model/afm.py:11-19
+  FFM(feature_columns, k, w_reg=1e-4, v_reg=1e-4)                 model/ffm.py:10-22
 
 Criteo-style models take the reference's packed input X[B, 13+F] (dense
 features followed by label-encoded sparse ids, as floats — Keras casts them to
@@ -36,8 +40,8 @@ import torch
 
 from . import _lib
 from ._lib import call, ptr
-from .layers import (Attention, BatchNormalization, CrossLayer, Dense, DNNLayer, EmbedLayer, FMLayer,
-                     InnerProductLayer, OuterProductLayer,
+from .layers import (AFMLayer, Attention, BatchNormalization, CrossLayer, Dense, DNNLayer, EmbedLayer, FFMLayer,
+                     FMLayer, InnerProductLayer, OuterProductLayer,
                      KerasModule, TowerMixin, sigmoid_combine, _ids_tensor, _to_device_f32, _ErrFlag)
 
 
@@ -432,3 +436,79 @@ class DIN(TowerMixin, KerasModule):
 
     def _layers(self):
         return list(self.dense_layer) + [self.out_layer]
+
+
+# ------------------------------------ other CTR models
+class NFM(TowerMixin, KerasModule):
+    """NFM(feature_columns, hidden_units, output_dim, activation='relu',
+    dropout=0) — model/nfm.py:13-33, with 3-D embeddings (documented
+    deviation: on the reference's rank-2 EmbedLayer output the bi-interaction
+    reduce_sum collapses to [B] and the concat with the dense block fails):
+    x = BN(concat([dense, 0.5((sum_f e)^2 - sum_f e^2)])) -> DNNLayer ->
+    Dense(1) -> sigmoid.  ids -> rows -> bi-interaction -> [dense | pooled]
+    in one launch (rs_embed_pair_pool_fwd), BN (rs_affine_act), then the
+    DNNLayer + output Dense as ONE tower launch (rs_mlp_fwd)."""
+
+    def __init__(self, feature_columns, hidden_units, output_dim, activation="relu", dropout=0, embed_dim=8,
+                 device=None, seed=None):
+        super().__init__(device, seed)
+        self.dense_feature_columns, self.sparse_feature_columns = feature_columns
+        self.nd = len(self.dense_feature_columns)
+        self.dnn_layers = DNNLayer(hidden_units, output_dim, activation, dropout, device=device,
+                                   seed=_subseed(self._gen))
+        self.emb_layers = EmbedLayer(self.sparse_feature_columns, embed_dim, device=device, seed=_subseed(self._gen))
+        self.bn_layer = BatchNormalization(device=device)
+        self.output_layer = Dense(1, activation="sigmoid", device=device, seed=_subseed(self._gen))
+        d = self.nd + embed_dim
+        self.dnn_layers.build(d)
+        self.output_layer.build(int(output_dim))
+        self.bn_layer.build(d)
+        self._err = _ErrFlag(self._dev)
+
+    def _layers(self):
+        return list(self.dnn_layers.hidden_layer) + [self.dnn_layers.output_layer, self.output_layer]
+
+    def bi_interaction_input(self, inputs, check_ids=True):
+        """concat([dense, BiInteraction(emb)]) [B, nd+k] (model/nfm.py:26-29)."""
+        dense, ids = _split_criteo(inputs, self.nd, self._dev)
+        e = self.emb_layers
+        B = ids.shape[0]
+        x = torch.empty(B, self.nd + e.k, dtype=torch.float32, device=self._dev)
+        call("rs_embed_pair_pool_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(e.table),
+             ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, e.k, 0, ptr(dense), dense.stride(0), self.nd,
+             ptr(x), x.stride(0), self.nd, None, None, 0, None, B, ptr(self._err.t), _lib.stream())
+        if check_ids:
+            self._err.check("NFM")
+        return x
+
+    def forward(self, inputs, check_ids=True):
+        x = self.bn_layer(self.bi_interaction_input(inputs, check_ids))
+        if self.tower_ok():
+            return self.tower(x)  # DNNLayer + Dense(1, sigmoid) in one launch
+        return self.output_layer(self.dnn_layers(x))
+
+
+class AFM(KerasModule):
+    """AFM(feature_columns, mode) — model/afm.py:11-19: sigmoid(AFMLayer(x)),
+    i.e. sigmoid(sigmoid(Dense(1)(pool over pairs))) — both sigmoids in the
+    one rs_embed_pair_pool_fwd launch."""
+
+    def __init__(self, feature_columns, mode, device=None, seed=None):
+        super().__init__(device, seed)
+        self.afm_layer = AFMLayer(feature_columns, mode, device=device, seed=_subseed(self._gen))
+
+    def forward(self, inputs, check_ids=True):
+        return self.afm_layer.pooled(inputs, check_ids, n_sigmoid=2)[1]
+
+
+class FFM(KerasModule):
+    """FFM(feature_columns, k, w_reg=1e-4, v_reg=1e-4) — model/ffm.py:10-22:
+    sigmoid(FFMLayer(x)), one launch (rs_ffm_fwd)."""
+
+    def __init__(self, feature_columns, k, w_reg=1e-4, v_reg=1e-4, device=None, seed=None):
+        super().__init__(device, seed)
+        self.dense_feature_columns, self.sparse_feature_columns = feature_columns
+        self.ffm = FFMLayer(feature_columns, k, w_reg, v_reg, device=device, seed=_subseed(self._gen))
+
+    def forward(self, inputs):
+        return self.ffm.logits(inputs, n_sigmoid=1)
