@@ -21,7 +21,7 @@ I = C.c_int
 L = C.c_int64
 F = C.c_float
 
-# name -> (restype, argtypes); must match include/rs_capi.h
+# name -> (restype, argtypes); must match include/rs_capi.h and include/rs_batchio.h
 SIGNATURES = {
     "rs_version": (C.c_char_p, []),
     "rs_last_error_string": (C.c_char_p, []),
@@ -63,6 +63,11 @@ SIGNATURES = {
     "rs_gather_rows": (I, [P, L, I, P, L, P, P, P]),
     "rs_unpermute_rows": (I, [P, P, I, L, P, P]),
     "rs_rows_fm_fwd": (I, [P, P, L, I, I, I, P, P, I, P, L, P]),
+    "rs_cb_write": (I, [C.c_char_p, L, I, I, I, P, P, P, P, P]),
+    "rs_cb_open": (P, [C.c_char_p]),
+    "rs_cb_info": (I, [P, P, P, P, P, P, P]),
+    "rs_cb_read": (I, [P, L, L, P, P, P]),
+    "rs_cb_close": (None, [P]),
     "rs_fm_partial_width": (I, [I]),
     "rs_embed_pair_pool_fwd": (I, [P, I, L, P, P, P, I, I, I, P, L, I, P, L, I, P, P, I, P, L, P, P]),
     "rs_pair_products_fwd": (I, [P, L, I, I, L, P, P]),
