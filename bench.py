@@ -24,7 +24,7 @@ Also measured (nested in the JSON line, not `value`):
   * `cpu_baseline`: the oracle's numpy fp32 restatement of the reference
     forward (TF unavailable) on the same table and batches, bounded sample.
 
-Other configs (own JSON line): --config deepfm1e6 | dcn | din | pnn | nfm | afm | ffm | io.
+Other configs (own JSON line): --config deepfm1e6 | dcn | din | pnn | nfm | afm | ffm | io | fm_train.
 """
 from __future__ import annotations
 
@@ -807,6 +807,55 @@ def bench_io(args, world, rank):
                           "graphs on resident inputs"})
 
 
+def bench_fm_train(args, world, rank):
+    """FM training step (compile_fit's SGD on FM):
+    B = 4096 on 26 x 1e6 one-hot columns, k = 16 (config-2 shape), graph-
+    replayed.  Keras' l2 regularisers give every row of w1 / v a gradient, so
+    each step also rewrites the whole (n, 17) parameter block: that dense
+    decay pass is the HBM-bound part; the sparse rows go through a sort +
+    segmented sum.  Also timed: the reference's own scale (bundled-sample
+    width 43,604, k = 8, batch 32)."""
+    import recommender_system_amd as rs
+    dev = torch.device("cuda")
+    B, F, nd = args.batch, 26, 13
+    V = int(args.vocab if args.vocab != 1e7 else 1e6)
+
+    def setup(B, V, k, n_pool=16):
+        vocab = np.full(F, V, np.int64)
+        offs = np.concatenate([[0], np.cumsum(vocab)[:-1]])
+        m = rs.FM(k, 1e-4, 1e-4, seed=SEED, device=dev)
+        m.fm.build(nd + int(vocab.sum()))
+        ids_pool, dense_pool = _pool(B, [V] * F, nd, n_pool, dev)
+        labels = (torch.rand(n_pool, B, device=dev) < 0.25).to(torch.float32)
+        o = torch.as_tensor(offs, device=dev)
+        vo = torch.as_tensor(vocab, device=dev)
+
+        def step(i):
+            j = i % n_pool
+            m.train_step(dense_pool[j], ids_pool[j], labels[j], o, vo, lr=0.01, check_ids=False)
+        return m, step
+
+    k = 16
+    m, step = setup(B, V, k)
+    dt, slot = _timed_graph(step, args.steps, args.warmup, world, chunk=16)
+    n_rows = nd + F * V
+    decay = 2 * n_rows * (k + 1) * 4
+    ach = decay / (slot * 1e-3)
+    _, step_small = setup(32, 1677, 8)  # ~43,6xx one-hot columns, the bundled sample's width
+    dts, slots = _timed_graph(step_small, args.steps, args.warmup, world, chunk=16)
+    return _line("FM training samples/sec @ batch 4096, 26 x 1e6 one-hot columns, k 16 (SGD + l2, compile_fit)",
+                 args.steps * B / dt, "samples/s", args, world, dt / args.steps * 1e3,
+                 {"workload": "fm_train_step", "global_batch": B, "vocab_per_field": V, "k": k,
+                  "parallelism": "dp1"},
+                 {"bound": "hbm", "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                  "frac": ach / PEAK_HBM, "traffic": None,
+                  "kernel": "whole step; bytes = the l2 decay pass (read+write of w1 and v)", "kernel_ms": slot,
+                  "decay_bytes_per_step": decay},
+                 {"reference_scale": {"steps_per_s": args.steps / dts, "ms_per_step": dts / args.steps * 1e3,
+                                      "note": "batch 32, 26 x 1,677 + 13 = 43,615 columns, k 8 (compile_fit's "
+                                              "defaults on the bundled sample's width)"}})
+
+
 def _pmc_traffic():
     p = os.path.join(ROOT, "profiles", "pmc_embed_fm.json")
     try:
@@ -832,7 +881,7 @@ def main():
     args = ap.parse_args()
     world, rank = _dist_setup(args)
     other = {"dcn": bench_dcn, "din": bench_din, "pnn": bench_pnn, "nfm": bench_nfm, "afm": bench_afm,
-             "ffm": bench_ffm, "io": bench_io}
+             "ffm": bench_ffm, "io": bench_io, "fm_train": bench_fm_train}
     if args.config in other:
         line = other[args.config](args, world, rank)
         if rank == 0:

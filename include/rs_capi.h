@@ -354,6 +354,29 @@ int rs_ffm_fwd(const void* ids, int id_kind, int64_t id_stride,
                int n_fields, int k, int n_sigmoid, float* out, int64_t batch,
                int* err_flag, rs_stream_t stream);
 
+/* ------------------------------------------ training (§8(f) rank 4)
+ * rs_fm_train_step: one SGD step of the FM model (model/fm.py:14-23 +
+ * utils/compile_fit.py:9-15) on a batch in compact form — dense [B, nd] and
+ * label codes ids [B, F] standing for x = [dense | one-hot] (one-hot column
+ * nd + field_offsets[c] + id, utils/dataset.py:47-48) — with the FMLayer
+ * weights w0 (1), w1 (n_rows), v (n_rows, k) updated in place:
+ *   y = w0 + x@w1 + 0.5 sum_f [(x@v)_f^2 - (x^2@v^2)_f],
+ *   dL/dy_b = (sigmoid(y_b) - labels_b) / B   (Keras binary_crossentropy on
+ *   the sigmoid's logits, batch mean), l2 regularisers l2_w on w1 and l2_v
+ *   on v (FMLayer.build, layer/interaction.py:97-104), SGD with rate lr.
+ * Every row decays (the regulariser's dense gradient); the looked-up rows
+ * get their summed gradient through a deterministic sort + segmented sum.
+ * loss (optional, [B]): per-sample cross-entropy before the step.
+ * workspace: rs_fm_train_workspace_size(B, F, k, nd) bytes (device).       */
+int64_t rs_fm_train_workspace_size(int64_t batch, int n_fields, int k, int nd);
+int rs_fm_train_step(const void* ids, int id_kind, int64_t id_stride,
+                     const float* dense, int64_t dense_stride, int nd,
+                     const int64_t* field_offsets, const int64_t* field_vocab,
+                     int n_fields, int k, float* w0, float* w1, float* v,
+                     int64_t n_rows, const float* labels, int64_t batch,
+                     float lr, float l2_w, float l2_v, void* workspace,
+                     float* loss, int* err_flag, rs_stream_t stream);
+
 /* -------------------------------------- row-sharded lookup (§8(e), cfg 5)
  * Global row of (b,c) = field_offsets[c] + id(b,c).  Rows are split across
  * `world` ranks in blocks of `rows_per_rank` (owner = row / rows_per_rank).

@@ -463,3 +463,45 @@ def ffm(X, p, onehot_dims, nd=13, dt=np.float64, inputs=None):
     """FFM.call (model/ffm.py:20-22): sigmoid(FFMLayer(inputs))."""
     dense_in, sparse = inputs if inputs is not None else _split_dense_sparse(X, nd, dt)
     return sigmoid(ffm_layer(dense_in, sparse, onehot_dims, p["w0"], p["w"], p["v"], dt=dt))
+
+
+# --------------------------------------------- training (SURVEY §8(f) rank 4)
+def onehot_matrix(dense, ids, field_vocab, dt=np.float64):
+    """utils/dataset.py:47-48 (pd.get_dummies): x = [dense | one-hot per
+    field], field c's block starts at nd + sum(vocab[:c])."""
+    dense = np.asarray(dense, dt)
+    ids = cast_ids(ids)
+    offs = np.concatenate([[0], np.cumsum(field_vocab)[:-1]]).astype(np.int64)
+    B, nd = dense.shape
+    x = np.zeros((B, nd + int(np.sum(field_vocab))), dt)
+    x[:, :nd] = dense
+    x[np.arange(B)[:, None], nd + offs[None, :] + ids] = 1.0
+    return x
+
+
+def fm_loss(x, t, w0, w1, v, l2_w, l2_v, dt=np.float64):
+    """compile_fit's objective for FM (utils/compile_fit.py:9-15,
+    model/fm.py:19-23): mean binary cross-entropy of sigmoid(FMLayer(x))
+    (Keras takes the sigmoid's logits: softplus form) + l2_w |w1|^2 + l2_v |v|^2."""
+    y = fm_layer(x, w0, w1, v, dt)[:, 0]
+    t = np.asarray(t, dt)
+    ce = np.maximum(y, 0) - y * t + np.log1p(np.exp(-np.abs(y)))
+    return np.mean(ce) + l2_w * np.sum(np.asarray(w1, dt) ** 2) + l2_v * np.sum(np.asarray(v, dt) ** 2), ce
+
+
+def fm_train_step(x, t, w0, w1, v, lr, l2_w, l2_v, dt=np.float64):
+    """One SGD step (tf.keras SGD: w -= lr * dL/dw) of fm_loss, gradients in
+    closed form: g = (sigmoid(y) - t)/B, dL/dw0 = sum g, dL/dw1 = x^T g +
+    2 l2_w w1, dL/dv = x^T (g * s) - (x^2)^T g * v + 2 l2_v v, s = x @ v.
+    Returns (w0, w1, v) after the step and the per-sample losses before it."""
+    x = np.asarray(x, dt)
+    w0, w1, v = (np.asarray(a, dt) for a in (w0, w1, v))
+    y = fm_layer(x, w0, w1, v, dt)[:, 0]
+    t = np.asarray(t, dt)
+    g = (sigmoid(y) - t) / x.shape[0]
+    s = x @ v
+    g_w0 = np.sum(g, keepdims=True)
+    g_w1 = x.T @ g[:, None] + 2 * l2_w * w1
+    g_v = x.T @ (g[:, None] * s) - ((x * x).T @ g)[:, None] * v + 2 * l2_v * v
+    ce = np.maximum(y, 0) - y * t + np.log1p(np.exp(-np.abs(y)))
+    return w0 - lr * g_w0, w1 - lr * g_w1, v - lr * g_v, ce

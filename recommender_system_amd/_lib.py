@@ -68,6 +68,8 @@ SIGNATURES = {
     "rs_cb_info": (I, [P, P, P, P, P, P, P]),
     "rs_cb_read": (I, [P, L, L, P, P, P]),
     "rs_cb_close": (None, [P]),
+    "rs_fm_train_workspace_size": (L, [L, I, I, I]),
+    "rs_fm_train_step": (I, [P, I, L, P, L, I, P, P, I, I, P, P, P, L, P, L, F, F, F, P, P, P, P]),
     "rs_fm_partial_width": (I, [I]),
     "rs_embed_pair_pool_fwd": (I, [P, I, L, P, P, P, I, I, I, P, L, I, P, L, I, P, P, I, P, L, P, P]),
     "rs_pair_products_fwd": (I, [P, L, I, I, L, P, P]),

@@ -1,0 +1,306 @@
+// train.hip — the FM model's training step: forward,
+// binary cross-entropy gradient, L2 regularisers and SGD, with the sparse
+// rows updated by a deterministic scatter-add (row-sparse SGD).
+//
+// Reference semantics:
+//   FM.call / FMLayer.call   model/fm.py:19-23, layer/interaction.py:106-114
+//     y = w0 + x@w1 + 0.5 * sum_f [(x@v)_f^2 - (x^2 @ v^2)_f],  p = sigmoid(y)
+//   FMLayer.build            layer/interaction.py:94-104: w1 ~ l2(reg_w),
+//                            v ~ l2(reg_b) (Keras l2: loss += l * sum(w^2))
+//   compile_fit              utils/compile_fit.py:9-15: SGD(lr), loss
+//                            'binary_crossentropy' on a sigmoid output —
+//                            Keras takes the sigmoid's logits, so
+//                            dL/dy_b = (sigmoid(y_b) - t_b) / B (batch mean)
+// with x = [dense | one-hot] (utils/dataset.py:47-48): the one-hot block of
+// sample b has a single 1 at column nd + offset_c + id(b,c) per field.
+//
+// Gradients (x one-hot, so x = x^2 = 1 on the sparse rows):
+//   dy/dw0 = 1,  dy/dw1_i = x_i,  dy/dv_if = x_i s_f - x_i^2 v_if,
+//   s_f = (x@v)_f.
+// Update (one step, lr, l2 weights lw / lv; all from the OLD weights):
+//   w0  -= lr * sum_b g_b
+//   w1  -= lr * (G1 + 2 lw w1),   v -= lr * (Gv + 2 lv v)       (every row)
+// The decay touches every row (as Keras' dense regulariser gradient does);
+// G is non-zero only on the nd dense rows and the rows the batch looked up.
+// Sparse rows: per-lookup contributions are sorted by row (hipCUB radix sort,
+// stable) and each row's contributions are summed in lookup order by one
+// thread, so the result is bitwise reproducible.
+#include <hipcub/hipcub.hpp>
+
+#include "rs_common.hpp"
+
+namespace rs {
+
+struct FmTrainArgs {
+  const void* ids;
+  int64_t id_stride;
+  const float* dense;
+  int64_t dense_stride;
+  int nd;
+  const int64_t* offs;  // one-hot field offsets (without nd)
+  const int64_t* vocab;
+  int F, k;
+  float* w0;
+  float* w1;  // [n_rows]
+  float* v;   // [n_rows, k]
+  int64_t n_rows;
+  const float* labels;
+  int64_t batch;
+  float lr, l2_w, l2_v;
+  // workspace
+  float* g;        // [B]
+  float* s;        // [B, k]
+  float* contrib;  // [B*F, k+1]
+  uint32_t* key_in;
+  uint32_t* key_out;
+  uint32_t* val_in;
+  uint32_t* val_out;
+  float* gdense;  // [nd, k+1] + 1 (w0)
+  float* loss;    // [B] (optional)
+  int* err;
+};
+
+// One wave per sample, lane f < k: s_f and the (x^2 @ v^2)_f term; lane 0
+// also the linear part.  Rows in the reference's column order (dense, then
+// field by field).
+template <int KIND>
+__global__ __launch_bounds__(256) void fm_train_fwd(FmTrainArgs a) {
+  typedef Ids<KIND> I;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= a.batch) return;  // wave-uniform
+  const bool fl = lane < a.k;
+  const int f = fl ? lane : 0;
+  float s = 0.f, q = 0.f, lin = 0.f;
+  for (int i = 0; i < a.nd; ++i) {
+    const float x = a.dense[b * a.dense_stride + i];
+    const float vv = a.v[(int64_t)i * a.k + f];
+    s = fmaf(x, vv, s);
+    q = fmaf(x * x, vv * vv, q);
+    lin = fmaf(x, a.w1[i], lin);
+  }
+  bool bad = false;
+  for (int c = 0; c < a.F; ++c) {
+    int64_t id;
+    const bool ok = I::decode(I::load(a.ids, b * a.id_stride + c), a.vocab[c], id);
+    bad |= !ok;
+    const int64_t row = a.nd + a.offs[c] + id;
+    const float vv = ok ? a.v[row * a.k + f] : 0.f;
+    s += vv;
+    q = fmaf(vv, vv, q);
+    lin += ok ? a.w1[row] : 0.f;
+  }
+  if (bad && lane == 0) flag_error(a.err);
+  float t = fl ? s * s - q : 0.f;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+  const float y = (lin + a.w0[0]) + 0.5f * t;
+  const float p = sigmoidf_(y);
+  const float tb = a.labels[b];
+  const float g = (p - tb) / (float)a.batch;
+  if (fl) a.s[b * a.k + f] = s;
+  if (lane == 0) {
+    a.g[b] = g;
+    if (a.loss) a.loss[b] = fmaxf(y, 0.f) - y * tb + log1pf(expf(-fabsf(y)));
+  }
+}
+
+// Per lookup j = b*F + c: key = one-hot row, contribution
+// [g_b (s_bf - v_rf) for f < k | g_b]   (x = 1 on the sparse rows).
+template <int KIND>
+__global__ __launch_bounds__(256) void fm_train_lookup_grads(FmTrainArgs a) {
+  typedef Ids<KIND> I;
+  const int K1 = a.k + 1;
+  const int64_t total = a.batch * a.F * K1;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+    const int64_t j = idx / K1;
+    const int f = (int)(idx - j * K1);
+    const int64_t b = j / a.F;
+    const int c = (int)(j - b * a.F);
+    int64_t id;
+    const bool ok = I::decode(I::load(a.ids, b * a.id_stride + c), a.vocab[c], id);
+    const int64_t row = a.nd + a.offs[c] + id;
+    const float g = ok ? a.g[b] : 0.f;  // a bad id contributes nothing (its row is a valid one)
+    a.contrib[idx] = f < a.k ? g * (a.s[b * a.k + f] - a.v[row * a.k + f]) : g;
+    if (f == 0) {
+      a.key_in[j] = (uint32_t)row;
+      a.val_in[j] = (uint32_t)j;
+    }
+  }
+}
+
+// Dense rows i < nd: G[i][f] = sum_b g_b (x_bi s_bf - x_bi^2 v_if),
+// G[i][k] = sum_b g_b x_bi; G[nd*(k+1)] = sum_b g_b (w0).  One 256-thread
+// block per output: strided partial sums, then a fixed-shape tree in LDS —
+// the same order every run.
+__global__ __launch_bounds__(256) void fm_train_dense_grads(FmTrainArgs a) {
+  __shared__ float red[256];
+  const int K1 = a.k + 1;
+  const int idx = blockIdx.x;
+  const bool is_w0 = idx == a.nd * K1;
+  const int i = is_w0 ? 0 : idx / K1, f = is_w0 ? 0 : idx - i * K1;
+  const float vi = (!is_w0 && f < a.k) ? a.v[(int64_t)i * a.k + f] : 0.f;
+  float acc = 0.f;
+  for (int64_t b = threadIdx.x; b < a.batch; b += 256) {
+    const float g = a.g[b];
+    if (is_w0) {
+      acc += g;
+    } else {
+      const float x = a.dense[b * a.dense_stride + i];
+      acc += f < a.k ? g * (x * a.s[b * a.k + f] - x * x * vi) : g * x;
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+#pragma unroll
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.gdense[idx] = red[0];
+}
+
+// L2 decay of every row: w -= lr * 2 l w  (the regulariser's gradient);
+// float4 over v when it is 16-B aligned (k % 4 == 0), then w1.
+__global__ __launch_bounds__(256) void fm_train_decay(FmTrainArgs a) {
+  const int64_t nv = a.n_rows * a.k;
+  const float cv = a.lr * 2.f * a.l2_v, cw = a.lr * 2.f * a.l2_w;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int64_t done = 0;
+  if ((nv & 3) == 0 && ((uintptr_t)a.v & 15) == 0) {
+    floatx4* v4 = reinterpret_cast<floatx4*>(a.v);
+    for (int64_t q = t0; q < nv / 4; q += stride) {
+      floatx4 x = __builtin_nontemporal_load(v4 + q);
+      x -= cv * x;
+      __builtin_nontemporal_store(x, v4 + q);
+    }
+    done = nv;
+  }
+  for (int64_t idx = done + t0; idx < nv + a.n_rows; idx += stride) {
+    if (idx < nv) a.v[idx] -= cv * a.v[idx];
+    else a.w1[idx - nv] -= cw * a.w1[idx - nv];
+  }
+}
+
+// Sorted lookups: the first position of each row's segment sums the
+// segment's contributions in lookup order and applies them; then the dense
+// rows and w0.
+__global__ __launch_bounds__(256) void fm_train_apply(FmTrainArgs a) {
+  const int64_t n = a.batch * a.F;
+  const int K1 = a.k + 1;
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p < n) {
+    const uint32_t r = a.key_out[p];
+    if (p == 0 || a.key_out[p - 1] != r) {
+      int64_t e = p + 1;
+      while (e < n && a.key_out[e] == r) ++e;
+      for (int f = 0; f < K1; ++f) {
+        float acc = 0.f;
+        for (int64_t q = p; q < e; ++q) acc += a.contrib[(int64_t)a.val_out[q] * K1 + f];
+        if (f < a.k) a.v[(int64_t)r * a.k + f] -= a.lr * acc;
+        else a.w1[r] -= a.lr * acc;
+      }
+    }
+  } else if (p < n + a.nd * K1 + 1) {
+    const int idx = (int)(p - n);
+    const float gsum = a.gdense[idx];
+    if (idx == a.nd * K1) {
+      a.w0[0] -= a.lr * gsum;
+    } else {
+      const int i = idx / K1, f = idx - i * K1;
+      if (f < a.k) a.v[(int64_t)i * a.k + f] -= a.lr * gsum;
+      else a.w1[i] -= a.lr * gsum;
+    }
+  }
+}
+
+// workspace layout (all 256-B aligned)
+struct TrainWs {
+  int64_t g, s, contrib, key_in, key_out, val_in, val_out, gdense, sort, total;
+  size_t sort_bytes;
+};
+
+static int64_t al256(int64_t x) { return (x + 255) / 256 * 256; }
+
+static TrainWs train_ws(int64_t batch, int n_fields, int k, int nd) {
+  TrainWs w{};
+  const int64_t n = batch * n_fields;
+  size_t sb = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sb, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(n > 0 ? n : 1));
+  w.sort_bytes = sb;
+  int64_t o = 0;
+  w.g = o; o = al256(o + batch * 4);
+  w.s = o; o = al256(o + batch * k * 4);
+  w.contrib = o; o = al256(o + n * (k + 1) * 4);
+  w.key_in = o; o = al256(o + n * 4);
+  w.key_out = o; o = al256(o + n * 4);
+  w.val_in = o; o = al256(o + n * 4);
+  w.val_out = o; o = al256(o + n * 4);
+  w.gdense = o; o = al256(o + ((int64_t)nd * (k + 1) + 1) * 4);
+  w.sort = o; o = al256(o + (int64_t)sb);
+  w.total = o;
+  return w;
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" int64_t rs_fm_train_workspace_size(int64_t batch, int n_fields, int k, int nd) {
+  if (batch < 0 || n_fields < 0 || k < 1 || nd < 0) return -1;
+  return train_ws(batch, n_fields, k, nd).total;
+}
+
+extern "C" int rs_fm_train_step(const void* ids, int id_kind, int64_t id_stride, const float* dense,
+                                int64_t dense_stride, int nd, const int64_t* field_offsets,
+                                const int64_t* field_vocab, int n_fields, int k, float* w0, float* w1, float* v,
+                                int64_t n_rows, const float* labels, int64_t batch, float lr, float l2_w, float l2_v,
+                                void* workspace, float* loss, int* err_flag, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: no step (Keras runs no step either)
+  RS_REQUIRE(batch > 0 && nd >= 0 && n_fields >= 0 && k >= 1 && k <= 64 && n_rows >= nd,
+             "rs_fm_train_step: bad shape (1 <= k <= 64)");
+  RS_REQUIRE(n_rows < ((int64_t)1 << 32) && batch * n_fields < ((int64_t)1 << 31),
+             "rs_fm_train_step: rows must fit uint32, lookups int32");
+  RS_REQUIRE(w0 && w1 && v && labels && workspace && (nd == 0 || dense) &&
+                 (n_fields == 0 || (ids && field_offsets && field_vocab)),
+             "rs_fm_train_step: null pointer");
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_fm_train_step: bad id_kind");
+  const TrainWs w = train_ws(batch, n_fields, k, nd);
+  uint8_t* ws = static_cast<uint8_t*>(workspace);
+  FmTrainArgs a{ids, id_stride, dense, dense_stride, nd, field_offsets, field_vocab, n_fields, k, w0, w1, v, n_rows,
+                labels, batch, lr, l2_w, l2_v,
+                reinterpret_cast<float*>(ws + w.g), reinterpret_cast<float*>(ws + w.s),
+                reinterpret_cast<float*>(ws + w.contrib), reinterpret_cast<uint32_t*>(ws + w.key_in),
+                reinterpret_cast<uint32_t*>(ws + w.key_out), reinterpret_cast<uint32_t*>(ws + w.val_in),
+                reinterpret_cast<uint32_t*>(ws + w.val_out), reinterpret_cast<float*>(ws + w.gdense), loss,
+                err_flag};
+  hipStream_t st = as_stream(stream);
+  const int64_t n = batch * n_fields;
+  with_id_kind(id_kind, [&](auto K) {
+    constexpr int KD = decltype(K)::value;
+    fm_train_fwd<KD><<<(unsigned)((batch + 3) / 4), 256, 0, st>>>(a);
+    if (n > 0) {
+      const int64_t tot = n * (k + 1);
+      fm_train_lookup_grads<KD><<<(unsigned)std::min<int64_t>((tot + 255) / 256, 8192), 256, 0, st>>>(a);
+    }
+  });
+  fm_train_dense_grads<<<(unsigned)(nd * (k + 1) + 1), 256, 0, st>>>(a);
+  if (n > 0) {
+    int bits = 1;
+    while (bits < 32 && ((uint64_t)1 << bits) < (uint64_t)n_rows) ++bits;
+    size_t sb = w.sort_bytes;
+    const hipError_t e = hipcub::DeviceRadixSort::SortPairs(ws + w.sort, sb, a.key_in, a.key_out, a.val_in,
+                                                            a.val_out, (int)n, 0, bits, st);
+    if (e != hipSuccess) {
+      set_error("rs_fm_train_step: radix sort failed: %s", hipGetErrorString(e));
+      return RS_ERR_HIP;
+    }
+  }
+  const int64_t dn = n_rows * (int64_t)(k + 1);
+  fm_train_decay<<<(unsigned)std::min<int64_t>((dn / 4 + 255) / 256 + 1, 8192), 256, 0, st>>>(a);
+  const int64_t ap = n + nd * (k + 1) + 1;
+  fm_train_apply<<<(unsigned)((ap + 255) / 256), 256, 0, st>>>(a);
+  return launch_status("rs_fm_train_step");
+}

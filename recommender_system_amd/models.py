@@ -95,6 +95,38 @@ class FM(KerasModule):
             err.check("FM")
         return sigmoid_combine(logit)
 
+    def train_step(self, dense, ids, labels, field_offsets, field_vocab, lr=0.01, return_loss=False,
+                   check_ids=True):
+        """One step of compile_fit (utils/compile_fit.py:9-15: SGD(lr),
+        binary cross-entropy, FMLayer's l2 regularisers) on a compact batch
+        (dense [B,nd], label codes [B,F] of the one-hot x): one
+        rs_fm_train_step call updates w0 / w1 / v in place.  Returns the
+        per-sample losses before the step if ``return_loss``."""
+        dense = _to_device_f32(dense, self._dev)
+        ids = _ids_tensor(ids, self._dev)
+        labels = _to_device_f32(labels, self._dev).reshape(-1)
+        offs = torch.as_tensor(field_offsets, dtype=torch.int64, device=self._dev)
+        voc = torch.as_tensor(field_vocab, dtype=torch.int64, device=self._dev)
+        B, nd = dense.shape
+        F = ids.shape[1]
+        fm = self.fm
+        if not fm.built:  # (a host sum: not inside a graph capture)
+            fm.build(nd + int(voc.sum()))
+        n = fm.w1.shape[0]
+        ws_n = _lib.lib().rs_fm_train_workspace_size(B, F, fm.k, nd)
+        ws = self.__dict__.get("_train_ws")
+        if ws is None or ws.numel() < ws_n:
+            ws = self.__dict__["_train_ws"] = torch.empty(ws_n, dtype=torch.uint8, device=self._dev)
+        loss = torch.empty(B, dtype=torch.float32, device=self._dev) if return_loss else None
+        err = _ErrFlag(self._dev)
+        call("rs_fm_train_step", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), nd,
+             ptr(offs), ptr(voc), F, fm.k, ptr(fm.w0), ptr(fm.w1), ptr(fm.v), n, ptr(labels), B, float(lr),
+             float(fm.reg_w), float(fm.reg_b), ptr(ws), ptr(loss), ptr(err.t), _lib.stream())
+        fm._invalidate()  # packed operand images of the old weights are stale
+        if check_ids:
+            err.check("FM.train_step")
+        return loss
+
 
 class DeepFM(KerasModule):
     """DeepFM — model/deepFM.py:15-31: x = [dense | EmbedLayer(sparse)],

@@ -1,4 +1,4 @@
-"""CPU: librs_hip.so loads, exports every symbol include/rs_capi.h declares,
+"""CPU: librs_hip.so loads, exports every symbol include/*.h declares,
 matches the ctypes signature table, and rejects bad arguments before any
 device work (these calls launch nothing)."""
 import ctypes as C
@@ -9,13 +9,16 @@ import pytest
 
 from recommender_system_amd import _lib
 
-HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "rs_capi.h")
+INC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+HDRS = sorted(os.path.join(INC, f) for f in os.listdir(INC) if f.endswith(".h"))
+
+
+def _headers_text():
+    return re.sub(r"/\*.*?\*/", "", "".join(open(h).read() for h in HDRS), flags=re.S)
 
 
 def declared():
-    txt = open(HDR).read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(rs_[a-z0-9_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(rs_[a-z0-9_]+)\s*\(", _headers_text())))
 
 
 def test_header_symbols_exported_and_bound():
@@ -23,8 +26,8 @@ def test_header_symbols_exported_and_bound():
     names = declared()
     assert len(names) >= 20
     for n in names:
-        assert hasattr(lib, n), f"{n} declared in rs_capi.h but not exported"
-    assert set(names) == set(_lib.SIGNATURES), "ctypes table out of sync with rs_capi.h"
+        assert hasattr(lib, n), f"{n} declared in include/*.h but not exported"
+    assert set(names) == set(_lib.SIGNATURES), "ctypes table out of sync with include/*.h"
 
 
 def test_version_and_sizes():
@@ -62,7 +65,7 @@ def test_product_path_has_no_cpu_fallback():
 
 
 def test_signature_arity_matches_header():
-    txt = re.sub(r"/\*.*?\*/", "", open(HDR).read(), flags=re.S)
+    txt = _headers_text()
     for m in re.finditer(r"\b(rs_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", txt):
         name, params = m.group(1), m.group(2).strip()
         n = 0 if params in ("", "void") else len(params.split(","))

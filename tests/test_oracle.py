@@ -141,3 +141,29 @@ def test_outer_product_equals_loop():
     # identity W_p -> plain inner product
     Wi = np.repeat(np.eye(4)[:, None, :], 10, axis=1)
     np.testing.assert_allclose(O.outer_product_layer(e, Wi), O.inner_product_layer(e), rtol=1e-12, atol=1e-12)
+
+
+def test_fm_train_step_gradient_matches_finite_differences():
+    """The closed-form FM training gradient (oracle.fm_train_step, the
+    restatement of compile_fit's SGD on FM) == central differences of the
+    regularised loss, on a one-hot x with a repeated row."""
+    rng = np.random.default_rng(11)
+    vocab = [3, 4]
+    dense = rng.random((5, 2))
+    ids = np.array([[0, 1], [2, 1], [0, 3], [1, 1], [0, 0]])
+    x = O.onehot_matrix(dense, ids, vocab)
+    t = rng.integers(0, 2, 5).astype(float)
+    w0, w1, v = np.array([0.1]), rng.normal(size=(9, 1)), rng.normal(size=(9, 3))
+    lr, l2w, l2v = 1.0, 1e-2, 2e-2
+    n0, n1, nv, _ = O.fm_train_step(x, t, w0, w1, v, lr, l2w, l2v)
+    grads = [(w0 - n0), (w1 - n1), (v - nv)]
+    eps = 1e-6
+    for p, gp in zip((w0, w1, v), grads):
+        for idx in np.ndindex(p.shape):
+            keep = p[idx]
+            p[idx] = keep + eps
+            lp = O.fm_loss(x, t, w0, w1, v, l2w, l2v)[0]
+            p[idx] = keep - eps
+            lm = O.fm_loss(x, t, w0, w1, v, l2w, l2v)[0]
+            p[idx] = keep
+            assert abs((lp - lm) / (2 * eps) - gp[idx]) < 1e-7
