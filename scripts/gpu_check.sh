@@ -22,11 +22,14 @@ fi
 
 if [ "${SKIP_CONFIGS:-0}" != 1 ]; then
   : > gpurun_out/bench_configs.jsonl
-  for cfg in deepfm1e6 dcn din pnn; do
+  for cfg in deepfm1e6 dcn din pnn nfm afm ffm fm_train io; do
     timeout -k 10 300 python bench.py --config $cfg --steps 100 --warmup 10 >> gpurun_out/bench_configs.jsonl 2> gpurun_out/bench_$cfg.err
     rc=$?; [ $rc -eq 0 ] || { echo "bench $cfg rc=$rc"; tail -5 gpurun_out/bench_$cfg.err; exit $rc; }
   done
-  cat gpurun_out/bench_configs.jsonl
+  python scripts/fmt_lines.py gpurun_out/bench_configs.jsonl
+  timeout -k 10 300 python bench.py --sharded --steps $STEPS --warmup 20 --no-cpu-baseline > gpurun_out/bench_sharded.json 2> gpurun_out/bench_sharded.err
+  rc=$?; [ $rc -eq 0 ] || { echo "bench sharded rc=$rc"; tail -5 gpurun_out/bench_sharded.err; exit $rc; }
+  python scripts/fmt_lines.py gpurun_out/bench_sharded.json
 fi
 
 if [ "${SKIP_PROF:-0}" != 1 ]; then
@@ -41,7 +44,10 @@ if [ "${SKIP_PROF:-0}" != 1 ]; then
         -- python3 "$R/scripts/pmc_driver.py" > "$R/gpurun_out/pmc$i.log" 2>&1
     rc=$?; [ $rc -eq 0 ] || { echo "pmc pass $i rc=$rc"; tail -5 "$R/gpurun_out/pmc$i.log"; exit $rc; }
   done
-  for cfg in dcn din pnn; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_sharded" -o run --output-format csv \
+      -- python3 "$R/bench.py" --sharded --steps 100 --warmup 10 --no-cpu-baseline > "$R/gpurun_out/prof_sharded.json" 2> "$R/gpurun_out/prof_sharded.err"
+  rc=$?; [ $rc -eq 0 ] || { echo "rocprof sharded rc=$rc"; tail -5 "$R/gpurun_out/prof_sharded.err"; exit $rc; }
+  for cfg in dcn din pnn nfm afm ffm fm_train; do
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$cfg" -o run --output-format csv \
         -- python3 "$R/bench.py" --config $cfg --steps 50 --warmup 5 --no-cpu-baseline > "$R/gpurun_out/prof_$cfg.json" 2> "$R/gpurun_out/prof_$cfg.err"
     rc=$?; [ $rc -eq 0 ] || { echo "rocprof $cfg rc=$rc"; tail -5 "$R/gpurun_out/prof_$cfg.err"; exit $rc; }

@@ -84,7 +84,7 @@ def main(tag):
                                "RDREQ_random_rows_dispatches": req[:5], "RDREQ_line_pair_dispatches": req[5:]}
     json.dump(out, open(os.path.join(P, f"{tag}_pmc.json"), "w"), indent=1)
     # per-config kernel stats (rocprofv3 --kernel-trace --stats of bench.py --config X)
-    for cfg in ("dcn", "din", "pnn"):
+    for cfg in ("dcn", "din", "pnn", "nfm", "afm", "ffm", "fm_train", "sharded"):
         src = os.path.join(G, f"prof_{cfg}", "run_kernel_stats.csv")
         if os.path.exists(src):
             shutil.copy(src, os.path.join(P, f"{tag}_rocprof_kernel_stats_{cfg}.csv"))
