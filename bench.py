@@ -843,6 +843,18 @@ def bench_fm_train(args, world, rank):
     ach = decay / (slot * 1e-3)
     _, step_small = setup(32, 1677, 8)  # ~43,6xx one-hot columns, the bundled sample's width
     dts, slots = _timed_graph(step_small, args.steps, args.warmup, world, chunk=16)
+    # DeepFM training step (config-2 model: 26 x 1e6 x 16 tables, DNN 256-128-64)
+    cols = [[{"feat": f"I{i + 1}"} for i in range(nd)],
+            [{"feat": f"C{i + 1}", "feat_onehot_dim": V, "embed_dim": 16} for i in range(F)]]
+    dfm = rs.DeepFM(cols, 10, 1e-4, 1e-4, [256, 128, 64], 1, "relu", embed_dim=16, seed=SEED, device=dev)
+    ids_pool, dense_pool = _pool(B, [V] * F, nd, 16, dev)
+    lab = (torch.rand(16, B, device=dev) < 0.25).to(torch.float32)
+
+    def step_dfm(i):
+        dfm.train_step((dense_pool[i % 16], ids_pool[i % 16]), lab[i % 16], lr=0.01, check_ids=False)
+
+    n_d = max(10, args.steps // 5)
+    dtd, _ = _timed_graph(step_dfm, n_d, args.warmup, world, chunk=16)
     return _line("FM training samples/sec @ batch 4096, 26 x 1e6 one-hot columns, k 16 (SGD + l2, compile_fit)",
                  args.steps * B / dt, "samples/s", args, world, dt / args.steps * 1e3,
                  {"workload": "fm_train_step", "global_batch": B, "vocab_per_field": V, "k": k,
@@ -851,7 +863,10 @@ def bench_fm_train(args, world, rank):
                   "frac": ach / PEAK_HBM, "traffic": None,
                   "kernel": "whole step; bytes = the l2 decay pass (read+write of w1 and v)", "kernel_ms": slot,
                   "decay_bytes_per_step": decay},
-                 {"reference_scale": {"steps_per_s": args.steps / dts, "ms_per_step": dts / args.steps * 1e3,
+                 {"deepfm_train": {"samples_per_s": n_d * B / dtd, "ms_per_step": dtd / n_d * 1e3,
+                                   "note": "DeepFM.train_step: gather, DNN 429-256-128-64-1 fwd/bwd (rs_dense_fwd, "
+                                           "rs_gemm), FM grads, SGD + l2, row-sparse embedding SGD"},
+                  "reference_scale": {"steps_per_s": args.steps / dts, "ms_per_step": dts / args.steps * 1e3,
                                       "note": "batch 32, 26 x 1,677 + 13 = 43,615 columns, k 8 (compile_fit's "
                                               "defaults on the bundled sample's width)"}})
 

@@ -377,6 +377,54 @@ int rs_fm_train_step(const void* ids, int id_kind, int64_t id_stride,
                      float lr, float l2_w, float l2_v, void* workspace,
                      float* loss, int* err_flag, rs_stream_t stream);
 
+/* DeepFM training (model/deepFM.py + utils/compile_fit.py; the host layer
+ * DeepFM.train_step composes these with rs_embed_gather / rs_dense_fwd /
+ * rs_fm_fwd):
+ * rs_gemm: C[M,N] = alpha op(A)[M,K] op(B)[K,N] + beta C (row-major; op =
+ *  transpose when trans_*), then C *= (mask > 0) if mask (ReLU backward);
+ *  deterministic (each output's K sum in one fixed order).  With a
+ *  workspace of rs_gemm_workspace_size(M, N, K) bytes (0 = not needed) a
+ *  launch of few output tiles splits K into slices summed in slice order.
+ * rs_col_sum: out[n] = sum_m A[m,n] (bias gradients), fixed-order trees.
+ * rs_sgd_update: w -= lr (grad + 2 l2 w) (Keras SGD + l2 regulariser).
+ * rs_head_grad: z = c_fm fm + c_dnn dnn (DeepFM: 0.5, 0.5),
+ *  g = (sigmoid(z) - t)/B -> g_fm = c_fm g, g_dnn = c_dnn g, loss (optional).
+ * rs_fm_x_grad: dx[b,i] += g_b (w1_i + sum_f v_if s_bf - x_bi sum_f v_if^2)
+ *  (FMLayer w.r.t. its input; s = x @ v).
+ * rs_fm_param_grads: dw1 = x^T g, dv = x^T (g s) - (x^2)^T g * v, dw0 =
+ *  sum g (no l2 terms; kfm <= 32).
+ * rs_embedding_sgd: table[off_c + id(b,c)] -= lr * grad[b, c*k : c*k+k]
+ *  summed over duplicate rows in lookup order (stable sort + segmented sum:
+ *  Keras' IndexedSlices scatter-add); workspace:
+ *  rs_embedding_sgd_workspace_size(batch * n_fields) bytes.                 */
+int64_t rs_gemm_workspace_size(int64_t M, int64_t N, int64_t K);
+int rs_gemm(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+            float alpha, const float* A, int64_t lda, const float* B,
+            int64_t ldb, float beta, float* C, int64_t ldc, const float* mask,
+            int64_t ldm, void* workspace, int64_t workspace_bytes,
+            rs_stream_t stream);
+int rs_col_sum(const float* A, int64_t lda, int64_t M, int64_t N, float* out,
+               rs_stream_t stream);
+int rs_sgd_update(float* w, const float* grad, int64_t n, float lr, float l2,
+                  rs_stream_t stream);
+int rs_head_grad(const float* fm, const float* dnn, const float* labels,
+                 int64_t batch, float c_fm, float c_dnn, float* g_fm,
+                 float* g_dnn, float* loss, rs_stream_t stream);
+int rs_fm_x_grad(const float* x, int64_t ldx, const float* s, const float* w1,
+                 const float* v, int64_t batch, int d, int kfm, const float* g,
+                 float* dx, int64_t lddx, rs_stream_t stream);
+int rs_fm_param_grads(const float* x, int64_t ldx, const float* s,
+                      const float* v, int64_t batch, int d, int kfm,
+                      const float* g, float* dw1, float* dv, float* dw0,
+                      rs_stream_t stream);
+int64_t rs_embedding_sgd_workspace_size(int64_t n_lookups);
+int rs_embedding_sgd(float* table, int64_t n_rows, int k, const void* ids,
+                     int id_kind, int64_t id_stride,
+                     const int64_t* field_offsets, const int64_t* field_vocab,
+                     int n_fields, int64_t batch, const float* grad,
+                     int64_t grad_stride, float lr, void* workspace,
+                     int* err_flag, rs_stream_t stream);
+
 /* -------------------------------------- row-sharded lookup (§8(e), cfg 5)
  * Global row of (b,c) = field_offsets[c] + id(b,c).  Rows are split across
  * `world` ranks in blocks of `rows_per_rank` (owner = row / rows_per_rank).

@@ -505,3 +505,62 @@ def fm_train_step(x, t, w0, w1, v, lr, l2_w, l2_v, dt=np.float64):
     g_v = x.T @ (g[:, None] * s) - ((x * x).T @ g)[:, None] * v + 2 * l2_v * v
     ce = np.maximum(y, 0) - y * t + np.log1p(np.exp(-np.abs(y)))
     return w0 - lr * g_w0, w1 - lr * g_w1, v - lr * g_v, ce
+
+
+def deepfm_train_step(dense, ids, t, p, lr, l2_w, l2_v, nd=13, act="relu", dt=np.float64):
+    """One SGD step of compile_fit on DeepFM (model/deepFM.py:23-31,
+    utils/compile_fit.py:9-15), backpropagated by hand: z = 0.5 (fm + dnn),
+    g = (sigmoid(z) - t)/B; DNN layers by the chain rule (ReLU' = [a > 0]);
+    FM w.r.t. x: w1 + v s - x |v|^2 per feature; w1 / v with their l2
+    terms; embedding rows by scatter-add (np.add.at) of dL/dx's sparse block.
+    p: {"tables", "w0", "w1", "v", "dnn_hidden": [(W, b)], "dnn_out": (W, b)}.
+    Returns (new p, per-sample losses before the step)."""
+    dense = np.asarray(dense, dt)
+    ids = cast_ids(ids)
+    t = np.asarray(t, dt)
+    tables = [np.array(tb, dt) for tb in p["tables"]]
+    k = tables[0].shape[1]
+    x = np.concatenate([dense, embed_layer(ids, tables, dt)], axis=1)
+    w0, w1, v = (np.array(p[n], dt) for n in ("w0", "w1", "v"))
+    layers = [(np.array(W, dt), np.array(b, dt)) for W, b in p["dnn_hidden"]] + \
+             [(np.array(p["dnn_out"][0], dt), np.array(p["dnn_out"][1], dt))]
+    acts = [x]
+    for W, b in layers[:-1]:
+        acts.append(activation(acts[-1] @ W + b, act))
+    dnn = (acts[-1] @ layers[-1][0] + layers[-1][1])[:, 0]
+    fm = fm_layer(x, w0, w1, v, dt)[:, 0]
+    z = 0.5 * (fm + dnn)
+    g = (sigmoid(z) - t) / x.shape[0]
+    gf = gd = 0.5 * g
+    loss = np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z)))
+    delta = gd[:, None]
+    new_layers = [None] * len(layers)
+    for li in reversed(range(len(layers))):
+        W, b = layers[li]
+        dW, db = acts[li].T @ delta, delta.sum(0)
+        prev = delta @ W.T
+        if li > 0 and act == "relu":
+            prev = prev * (acts[li] > 0)
+        new_layers[li] = (W - lr * dW, b - lr * db)
+        delta = prev
+    s = x @ v
+    dx = delta + gf[:, None] * (w1[:, 0][None, :] + s @ v.T - x * np.sum(v * v, axis=1)[None, :])
+    dw1 = x.T @ gf[:, None]
+    dv = x.T @ (gf[:, None] * s) - ((x * x).T @ gf)[:, None] * v
+    out = {"w0": w0 - lr * gf.sum(keepdims=True), "w1": w1 - lr * (dw1 + 2 * l2_w * w1),
+           "v": v - lr * (dv + 2 * l2_v * v), "dnn_hidden": new_layers[:-1], "dnn_out": new_layers[-1]}
+    for c, tb in enumerate(tables):
+        np.add.at(tb, ids[:, c], -lr * dx[:, nd + c * k: nd + (c + 1) * k])
+    out["tables"] = tables
+    return out, loss
+
+
+def deepfm_loss(dense, ids, t, p, l2_w, l2_v, nd=13, dt=np.float64):
+    """compile_fit's objective on DeepFM: mean BCE(t, sigmoid(0.5(fm+dnn)))
+    + l2_w |w1|^2 + l2_v |v|^2."""
+    _, fm, x = deepfm(None, p, nd, dt, inputs=(dense, ids))
+    dnn = dnn_layer(x, p["dnn_hidden"], p["dnn_out"], "relu", dt)
+    z = 0.5 * (fm + dnn)[:, 0]
+    t = np.asarray(t, dt)
+    ce = np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z)))
+    return np.mean(ce) + l2_w * np.sum(np.asarray(p["w1"], dt) ** 2) + l2_v * np.sum(np.asarray(p["v"], dt) ** 2)

@@ -70,6 +70,15 @@ SIGNATURES = {
     "rs_cb_close": (None, [P]),
     "rs_fm_train_workspace_size": (L, [L, I, I, I]),
     "rs_fm_train_step": (I, [P, I, L, P, L, I, P, P, I, I, P, P, P, L, P, L, F, F, F, P, P, P, P]),
+    "rs_gemm_workspace_size": (L, [L, L, L]),
+    "rs_gemm": (I, [I, I, L, L, L, F, P, L, P, L, F, P, L, P, L, P, L, P]),
+    "rs_col_sum": (I, [P, L, L, L, P, P]),
+    "rs_sgd_update": (I, [P, P, L, F, F, P]),
+    "rs_head_grad": (I, [P, P, P, L, F, F, P, P, P, P]),
+    "rs_fm_x_grad": (I, [P, L, P, P, P, L, I, I, P, P, L, P]),
+    "rs_fm_param_grads": (I, [P, L, P, P, L, I, I, P, P, P, P, P]),
+    "rs_embedding_sgd_workspace_size": (L, [L]),
+    "rs_embedding_sgd": (I, [P, L, I, P, I, L, P, P, I, L, P, L, F, P, P, P]),
     "rs_fm_partial_width": (I, [I]),
     "rs_embed_pair_pool_fwd": (I, [P, I, L, P, P, P, I, I, I, P, L, I, P, L, I, P, P, I, P, L, P, P]),
     "rs_pair_products_fwd": (I, [P, L, I, I, L, P, P]),

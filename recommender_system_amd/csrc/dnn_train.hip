@@ -1,0 +1,386 @@
+// dnn_train.hip — building blocks of the DeepFM training step (SURVEY §8(f)
+// rank 4: compile_fit on model/deepFM.py): a deterministic fp32 GEMM for the
+// DNN backward, column sums, SGD updates, the DeepFM head gradient, the FM
+// gradients w.r.t. x and (w0, w1, v), and the row-sparse SGD of the
+// embedding tables (EmbedLayer's Embedding, layer/core.py:271 — Keras applies
+// its IndexedSlices gradient with a scatter-add; here a stable sort by row
+// plus an in-order segmented sum, bitwise reproducible).
+//
+// Reference semantics (utils/compile_fit.py:9-15, model/deepFM.py:23-31):
+//   z = 0.5 (FM(x) + DNN(x)),  p = sigmoid(z),  L = mean_b BCE(t_b, p_b)
+//   + l2(reg_w) |w1|^2 + l2(reg_b) |v|^2 (FMLayer.build); Dense layers and
+//   embeddings carry no regulariser; SGD(lr): w -= lr dL/dw.
+#include <hipcub/hipcub.hpp>
+
+#include "rs_common.hpp"
+
+namespace rs {
+
+// ------------------------------------------------------------------ GEMM
+// C[M,N] = alpha * op(A)[M,K] op(B)[K,N] + beta * C, row-major, optionally
+// masked: C[m,n] *= (mask[m,n] > 0) (ReLU backward: a = relu(z) > 0 <=> z > 0).
+// 64x64 tiles, 256 threads, 4x4 outputs per thread, K in steps of 16 through
+// LDS; each output's K sum runs in one fixed order.
+constexpr int GT = 64, GK = 16;
+
+// Split-K (part != nullptr): block z of gridDim.z covers K range
+// [z*kslice, (z+1)*kslice) and stores its raw partial tile to part[z][M][N];
+// gemm_reduce sums the slices in z order (deterministic).
+__global__ __launch_bounds__(256) void gemm_kernel(int ta, int tb, int M, int N, int K, float alpha,
+                                                   const float* __restrict__ A, int64_t lda,
+                                                   const float* __restrict__ B, int64_t ldb, float beta,
+                                                   float* __restrict__ C, int64_t ldc,
+                                                   const float* __restrict__ mask, int64_t ldm, int kslice,
+                                                   float* __restrict__ part) {
+  __shared__ float As[GK][GT + 4];
+  __shared__ float Bs[GK][GT + 4];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
+  float acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  const int kb = part ? blockIdx.z * kslice : 0;
+  const int ke = part ? min(K, kb + kslice) : K;
+  for (int k0 = kb; k0 < ke; k0 += GK) {
+    // stage op(A)[m0:m0+64, k0:k0+16] as As[k][m] and op(B)[k0:k0+16, n0:n0+64] as Bs[k][n]
+    for (int e = threadIdx.x; e < GK * GT; e += 256) {
+      const int kk = e / GT, mm = e % GT;
+      const int m = m0 + mm, k = k0 + kk;
+      float av = 0.f;
+      if (m < M && k < ke) av = ta ? A[(int64_t)k * lda + m] : A[(int64_t)m * lda + k];
+      As[kk][mm] = av;
+      const int n = n0 + mm;
+      float bv = 0.f;
+      if (n < N && k < ke) bv = tb ? B[(int64_t)n * ldb + k] : B[(int64_t)k * ldb + n];
+      Bs[kk][mm] = bv;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < GK; ++kk) {
+      float a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty * 4 + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx * 4 + j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + ty * 4 + i;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + tx * 4 + j;
+      if (n >= N) continue;
+      if (part) {
+        part[((int64_t)blockIdx.z * M + m) * N + n] = acc[i][j];
+        continue;
+      }
+      float v = alpha * acc[i][j];
+      if (beta != 0.f) v += beta * C[(int64_t)m * ldc + n];
+      if (mask && !(mask[(int64_t)m * ldm + n] > 0.f)) v = 0.f;
+      C[(int64_t)m * ldc + n] = v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void gemm_reduce(int M, int N, int S, float alpha, const float* __restrict__ part,
+                                                   float beta, float* __restrict__ C, int64_t ldc,
+                                                   const float* __restrict__ mask, int64_t ldm) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)M * N) return;
+  const int m = (int)(idx / N), n = (int)(idx - (int64_t)m * N);
+  float acc = 0.f;
+  for (int z = 0; z < S; ++z) acc += part[(int64_t)z * M * N + idx];
+  float v = alpha * acc;
+  if (beta != 0.f) v += beta * C[(int64_t)m * ldc + n];
+  if (mask && !(mask[(int64_t)m * ldm + n] > 0.f)) v = 0.f;
+  C[(int64_t)m * ldc + n] = v;
+}
+
+// out[n] = sum_m A[m, n] (fixed-shape tree per column; one block per column)
+__global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ A, int64_t lda, int M, int N,
+                                                      float* __restrict__ out) {
+  __shared__ float red[256];
+  const int n = blockIdx.x;
+  float acc = 0.f;
+  for (int m = threadIdx.x; m < M; m += 256) acc += A[(int64_t)m * lda + n];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[n] = red[0];
+}
+
+// w -= lr * (g + 2 l2 w)
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ w, const float* __restrict__ g, int64_t n,
+                                                  float lr, float l2) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    w[i] -= lr * (g[i] + 2.f * l2 * w[i]);
+}
+
+// DeepFM head: z = c_fm*fm + c_dnn*dnn, g = (sigmoid(z) - t)/B, outputs
+// g_fm = c_fm*g, g_dnn = c_dnn*g (dL/dfm, dL/ddnn) and the BCE loss.
+__global__ __launch_bounds__(256) void head_grad_kernel(const float* __restrict__ fm, const float* __restrict__ dnn,
+                                                        const float* __restrict__ t, int64_t B, float c_fm,
+                                                        float c_dnn, float* __restrict__ g_fm,
+                                                        float* __restrict__ g_dnn, float* __restrict__ loss) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  const float z = c_fm * fm[b] + c_dnn * dnn[b];
+  const float g = (sigmoidf_(z) - t[b]) / (float)B;
+  g_fm[b] = c_fm * g;
+  g_dnn[b] = c_dnn * g;
+  if (loss) loss[b] = fmaxf(z, 0.f) - z * t[b] + log1pf(expf(-fabsf(z)));
+}
+
+// FM gradient w.r.t. x, accumulated: dx[b,i] += g_b (w1_i + sum_f v_if s_bf
+// - x_bi sum_f v_if^2); one thread per (b, i).
+__global__ __launch_bounds__(256) void fm_x_grad_kernel(const float* __restrict__ x, int64_t ldx,
+                                                        const float* __restrict__ s, const float* __restrict__ w1,
+                                                        const float* __restrict__ v, int64_t B, int d, int kfm,
+                                                        const float* __restrict__ g, float* __restrict__ dx,
+                                                        int64_t lddx) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= B * d) return;
+  const int64_t b = idx / d;
+  const int i = (int)(idx - b * d);
+  float vs = 0.f, vv = 0.f;
+  for (int f = 0; f < kfm; ++f) {
+    const float vf = v[(int64_t)i * kfm + f];
+    vs = fmaf(vf, s[b * kfm + f], vs);
+    vv = fmaf(vf, vf, vv);
+  }
+  dx[b * lddx + i] += g[b] * ((w1[i] + vs) - x[b * ldx + i] * vv);
+}
+
+// FM parameter gradients (without the l2 terms): one block per feature i,
+// fixed-shape trees over the batch:
+//   dw1_i = sum_b g_b x_bi,  dv_if = sum_b g_b x_bi s_bf - (sum_b g_b x_bi^2) v_if;
+// block d computes dw0 = sum_b g_b.
+__global__ __launch_bounds__(256) void fm_param_grad_kernel(const float* __restrict__ x, int64_t ldx,
+                                                            const float* __restrict__ s,
+                                                            const float* __restrict__ v, int64_t B, int d, int kfm,
+                                                            const float* __restrict__ g, float* __restrict__ dw1,
+                                                            float* __restrict__ dv, float* __restrict__ dw0) {
+  __shared__ float red[34][256];
+  const int i = blockIdx.x;
+  const int NQ = kfm + 2;  // [x s_0 .. x s_{kfm-1} | x | x^2] weighted by g
+  float acc[34];
+  for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
+  for (int64_t b = threadIdx.x; b < B; b += 256) {
+    const float gb = g[b];
+    if (i == d) {
+      acc[0] += gb;
+      continue;
+    }
+    const float xg = gb * x[b * ldx + i];
+    for (int f = 0; f < kfm; ++f) acc[f] = fmaf(xg, s[b * kfm + f], acc[f]);
+    acc[kfm] += xg;
+    acc[kfm + 1] = fmaf(xg, x[b * ldx + i], acc[kfm + 1]);
+  }
+  for (int q = 0; q < NQ; ++q) red[q][threadIdx.x] = acc[q];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+      for (int q = 0; q < NQ; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (i == d) {
+    if (threadIdx.x == 0) dw0[0] = red[0][0];
+    return;
+  }
+  if ((int)threadIdx.x < kfm) {
+    const int f = threadIdx.x;
+    dv[(int64_t)i * kfm + f] = red[f][0] - red[kfm + 1][0] * v[(int64_t)i * kfm + f];
+  }
+  if (threadIdx.x == 0) dw1[i] = red[kfm][0];
+}
+
+// ------------------------------------------- row-sparse SGD of the tables
+template <int KIND>
+__global__ __launch_bounds__(256) void emb_keys_kernel(const void* ids, int64_t id_stride,
+                                                       const int64_t* __restrict__ offs,
+                                                       const int64_t* __restrict__ vocab, int F, int64_t B,
+                                                       uint32_t* __restrict__ key, uint32_t* __restrict__ val,
+                                                       int* err) {
+  typedef Ids<KIND> I;
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= B * F) return;
+  const int64_t b = j / F;
+  const int c = (int)(j - b * F);
+  int64_t id;
+  const bool ok = I::decode(I::load(ids, b * id_stride + c), vocab[c], id);
+  if (!ok) flag_error(err);
+  key[j] = ok ? (uint32_t)(offs[c] + id) : 0xffffffffu;  // bad ids sort last and are skipped
+  val[j] = (uint32_t)j;
+}
+
+// Sorted lookups: the first position of each row's segment sums the
+// segment's gradient rows (grad row of lookup j = b*F + c at
+// grad[b*ldg + c*k]) in lookup order and applies table[r] -= lr * G.
+__global__ __launch_bounds__(256) void emb_apply_kernel(const uint32_t* __restrict__ key,
+                                                        const uint32_t* __restrict__ val, int64_t n, int F, int k,
+                                                        const float* __restrict__ grad, int64_t ldg, float lr,
+                                                        float* __restrict__ table) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= n) return;
+  const uint32_t r = key[p];
+  if (r == 0xffffffffu || (p > 0 && key[p - 1] == r)) return;
+  int64_t e = p + 1;
+  while (e < n && key[e] == r) ++e;
+  for (int f = 0; f < k; ++f) {
+    float acc = 0.f;
+    for (int64_t q = p; q < e; ++q) {
+      const int64_t j = val[q];
+      const int64_t b = j / F;
+      const int c = (int)(j - b * F);
+      acc += grad[b * ldg + (int64_t)c * k + f];
+    }
+    table[(int64_t)r * k + f] -= lr * acc;
+  }
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+// K slices for a launch of few output tiles (the weight gradients x^T delta:
+// M x N small, K = batch): aim for ~512 workgroups, slices of >= 64.
+static int gemm_splits(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = ((M + GT - 1) / GT) * ((N + GT - 1) / GT);
+  int64_t s = 512 / (tiles > 0 ? tiles : 1);
+  s = std::min<int64_t>(s, K / 64);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 256));
+}
+
+extern "C" int64_t rs_gemm_workspace_size(int64_t M, int64_t N, int64_t K) {
+  if (M < 0 || N < 0 || K < 0) return -1;
+  const int s = gemm_splits(M, N, K);
+  return s > 1 ? (int64_t)s * M * N * 4 : 0;
+}
+
+extern "C" int rs_gemm(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
+                       int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc,
+                       const float* mask, int64_t ldm, void* workspace, int64_t workspace_bytes,
+                       rs_stream_t stream) {
+  if (M == 0 || N == 0) return RS_OK;
+  RS_REQUIRE(M > 0 && N > 0 && K >= 0 && M < (1 << 30) && N < (1 << 30) && K < (1 << 30), "rs_gemm: bad shape");
+  RS_REQUIRE(C && (K == 0 || (A && B)), "rs_gemm: null pointer");
+  RS_REQUIRE(lda >= (trans_a ? M : K) && ldb >= (trans_b ? K : N) && ldc >= N && (!mask || ldm >= N),
+             "rs_gemm: leading dimension too small");
+  hipStream_t st = as_stream(stream);
+  int S = gemm_splits(M, N, K);
+  if (S > 1 && (!workspace || workspace_bytes < (int64_t)S * M * N * 4)) S = 1;  // no room: one pass over K
+  dim3 grid((unsigned)((N + GT - 1) / GT), (unsigned)((M + GT - 1) / GT), (unsigned)S);
+  const int kslice = (int)((K + S - 1) / S + GK - 1) / GK * GK;
+  float* part = S > 1 ? static_cast<float*>(workspace) : nullptr;
+  gemm_kernel<<<grid, 256, 0, st>>>(trans_a, trans_b, (int)M, (int)N, (int)K, alpha, A, lda, B, ldb, beta, C, ldc,
+                                    mask, ldm, kslice, part);
+  if (part)
+    gemm_reduce<<<(unsigned)((M * N + 255) / 256), 256, 0, st>>>((int)M, (int)N, S, alpha, part, beta, C, ldc, mask,
+                                                                 ldm);
+  return launch_status("rs_gemm");
+}
+
+extern "C" int rs_col_sum(const float* A, int64_t lda, int64_t M, int64_t N, float* out, rs_stream_t stream) {
+  if (N == 0) return RS_OK;
+  RS_REQUIRE(A && out && M >= 0 && N > 0 && M < (1ll << 31) && lda >= N, "rs_col_sum: bad arguments");
+  col_sum_kernel<<<(unsigned)N, 256, 0, as_stream(stream)>>>(A, lda, (int)M, (int)N, out);
+  return launch_status("rs_col_sum");
+}
+
+extern "C" int rs_sgd_update(float* w, const float* grad, int64_t n, float lr, float l2, rs_stream_t stream) {
+  if (n == 0) return RS_OK;
+  RS_REQUIRE(w && grad && n > 0, "rs_sgd_update: bad arguments");
+  sgd_kernel<<<(unsigned)std::min<int64_t>((n + 255) / 256, 8192), 256, 0, as_stream(stream)>>>(w, grad, n, lr, l2);
+  return launch_status("rs_sgd_update");
+}
+
+extern "C" int rs_head_grad(const float* fm, const float* dnn, const float* labels, int64_t batch, float c_fm,
+                            float c_dnn, float* g_fm, float* g_dnn, float* loss, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(fm && dnn && labels && g_fm && g_dnn && batch > 0, "rs_head_grad: bad arguments");
+  head_grad_kernel<<<(unsigned)((batch + 255) / 256), 256, 0, as_stream(stream)>>>(fm, dnn, labels, batch, c_fm,
+                                                                                   c_dnn, g_fm, g_dnn, loss);
+  return launch_status("rs_head_grad");
+}
+
+extern "C" int rs_fm_x_grad(const float* x, int64_t ldx, const float* s, const float* w1, const float* v,
+                            int64_t batch, int d, int kfm, const float* g, float* dx, int64_t lddx,
+                            rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(x && s && w1 && v && g && dx && batch > 0 && d > 0 && kfm >= 1 && ldx >= d && lddx >= d,
+             "rs_fm_x_grad: bad arguments");
+  fm_x_grad_kernel<<<(unsigned)((batch * d + 255) / 256), 256, 0, as_stream(stream)>>>(x, ldx, s, w1, v, batch, d,
+                                                                                       kfm, g, dx, lddx);
+  return launch_status("rs_fm_x_grad");
+}
+
+extern "C" int rs_fm_param_grads(const float* x, int64_t ldx, const float* s, const float* v, int64_t batch, int d,
+                                 int kfm, const float* g, float* dw1, float* dv, float* dw0, rs_stream_t stream) {
+  RS_REQUIRE(x && s && v && g && dw1 && dv && dw0 && batch >= 0 && d > 0 && kfm >= 1 && kfm <= 32 && ldx >= d,
+             "rs_fm_param_grads: bad arguments (kfm <= 32)");
+  fm_param_grad_kernel<<<(unsigned)(d + 1), 256, 0, as_stream(stream)>>>(x, ldx, s, v, batch, d, kfm, g, dw1, dv,
+                                                                          dw0);
+  return launch_status("rs_fm_param_grads");
+}
+
+static int64_t emb_sort_bytes(int64_t n) {
+  size_t sb = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sb, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (int)(n > 0 ? n : 1));
+  return (int64_t)sb;
+}
+
+extern "C" int64_t rs_embedding_sgd_workspace_size(int64_t n_lookups) {
+  if (n_lookups < 0) return -1;
+  return 4 * ((n_lookups * 4 + 255) / 256 * 256) + (emb_sort_bytes(n_lookups) + 255) / 256 * 256;
+}
+
+extern "C" int rs_embedding_sgd(float* table, int64_t n_rows, int k, const void* ids, int id_kind, int64_t id_stride,
+                                const int64_t* field_offsets, const int64_t* field_vocab, int n_fields,
+                                int64_t batch, const float* grad, int64_t grad_stride, float lr, void* workspace,
+                                int* err_flag, rs_stream_t stream) {
+  const int64_t n = batch * n_fields;
+  if (n == 0) return RS_OK;
+  RS_REQUIRE(table && ids && field_offsets && field_vocab && grad && workspace && k >= 1 && batch > 0 &&
+                 grad_stride >= (int64_t)n_fields * k,
+             "rs_embedding_sgd: bad arguments");
+  RS_REQUIRE(n_rows < 0xffffffffll && n < (1ll << 31), "rs_embedding_sgd: rows must fit uint32, lookups int32");
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_embedding_sgd: bad id_kind");
+  const int64_t slab = (n * 4 + 255) / 256 * 256;
+  uint8_t* ws = static_cast<uint8_t*>(workspace);
+  uint32_t* key_in = reinterpret_cast<uint32_t*>(ws);
+  uint32_t* key_out = reinterpret_cast<uint32_t*>(ws + slab);
+  uint32_t* val_in = reinterpret_cast<uint32_t*>(ws + 2 * slab);
+  uint32_t* val_out = reinterpret_cast<uint32_t*>(ws + 3 * slab);
+  hipStream_t st = as_stream(stream);
+  with_id_kind(id_kind, [&](auto K) {
+    emb_keys_kernel<decltype(K)::value><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
+        ids, id_stride, field_offsets, field_vocab, n_fields, batch, key_in, val_in, err_flag);
+  });
+  // 2^bits > n_rows: a bad id's key 0xffffffff keeps its low bits all set,
+  // so it still sorts after every valid row
+  int bits = 1;
+  while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)n_rows) ++bits;
+  size_t sb = (size_t)emb_sort_bytes(n);
+  const hipError_t e = hipcub::DeviceRadixSort::SortPairs(ws + 4 * slab, sb, key_in, key_out, val_in, val_out, (int)n,
+                                                          0, bits, st);
+  if (e != hipSuccess) {
+    set_error("rs_embedding_sgd: radix sort failed: %s", hipGetErrorString(e));
+    return RS_ERR_HIP;
+  }
+  emb_apply_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(key_out, val_out, n, n_fields, k, grad, grad_stride,
+                                                               lr, table);
+  return launch_status("rs_embedding_sgd");
+}

@@ -269,7 +269,11 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   constexpr int FMAX = 128;
   __shared__ typename I::raw_t lid[16][FMAX];
   __shared__ int64_t lmeta[2][FMAX];
+#ifdef RS_DIAG_STAMPS
+  const bool coop = (KIND != 3) && a.F <= FMAX && !(a.ablate & 16);  // bit 16: per-wave id loads
+#else
   const bool coop = (KIND != 3) && a.F <= FMAX;
+#endif
   if (coop) {
     const int64_t b0 = (int64_t)tile * 16;
     for (int t = threadIdx.x; t < 16 * a.F; t += NW * 64) {

@@ -458,6 +458,11 @@ class TowerMixin:
     activations stay in LDS, weights are packed once.  The host class
     provides ``_layers()`` (the Dense layers in order) and ``_dev``."""
 
+    def _invalidate(self):
+        # packed images keyed on tensor versions miss in-place kernel updates
+        # (training steps): drop them
+        self.__dict__.pop("_tower_prep", None)
+
     def tower_ok(self):
         ls = self._layers()
         if not (ls[0].kernel is not None and len(ls) <= _MLP_MAXL and all(l.activation != "dice" for l in ls)

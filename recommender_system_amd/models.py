@@ -159,6 +159,86 @@ class DeepFM(KerasModule):
             self._err.check("DeepFM")
         return logit
 
+    def train_step(self, inputs, labels, lr=0.01, return_loss=False, check_ids=True):
+        """One step of compile_fit (utils/compile_fit.py:9-15: SGD(lr),
+        binary cross-entropy on sigmoid(0.5 (FM + DNN)), FMLayer's l2
+        regularisers) on a batch, every weight updated in place: the DNN's
+        kernels/biases, w0 / w1 / v, and the looked-up embedding rows
+        (row-sparse, duplicates summed in lookup order — rs_embedding_sgd).
+        Forward with saved activations (rs_embed_gather, rs_dense_fwd,
+        rs_fm_fwd), backward through rs_gemm / rs_col_sum / rs_fm_x_grad /
+        rs_fm_param_grads, all gradients from the pre-step weights, then the
+        updates.  Supports output_dim 1 and 'relu' / linear hidden layers."""
+        dense, ids = _split_criteo(inputs, self.nd, self._dev)
+        labels = _to_device_f32(labels, self._dev).reshape(-1)
+        e, fm, dnn = self.embed_layer, self.fm, self.dnn
+        layers = list(dnn.hidden_layer) + [dnn.output_layer]
+        if dnn.output_layer.units != 1:
+            raise NotImplementedError("DeepFM.train_step: output_dim 1 only")
+        if any(l.activation not in (None, "linear", "relu") for l in dnn.hidden_layer):
+            raise NotImplementedError("DeepFM.train_step: 'relu' or linear hidden layers only")
+        B, dev, st = ids.shape[0], self._dev, _lib.stream()
+        d, kfm = self.nd + e.n_fields * e.k, fm.k
+        emp = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=dev)
+        # forward, keeping what the backward needs
+        x = e.gather(ids, dense, check_ids=check_ids)
+        acts = [x]
+        for layer in dnn.hidden_layer:
+            acts.append(layer(acts[-1]))
+        dnn_out = dnn.output_layer(acts[-1])
+        fm_out = fm(x)
+        s = emp(B, kfm)
+        gws = self._gemm_ws(max(_lib.lib().rs_gemm_workspace_size(L.kernel.shape[0], L.kernel.shape[1], B)
+                                for L in layers))
+        gw = (ptr(gws), gws.numel())
+        call("rs_gemm", 0, 0, B, kfm, d, 1.0, ptr(x), d, ptr(fm.v), kfm, 0.0, ptr(s), kfm, None, 0, *gw, st)
+        g_fm, g_dnn = emp(B), emp(B)
+        loss = emp(B) if return_loss else None
+        call("rs_head_grad", ptr(fm_out), ptr(dnn_out), ptr(labels), B, 0.5, 0.5, ptr(g_fm), ptr(g_dnn), ptr(loss), st)
+        # DNN backward: delta = dL/d(pre-activation) of each layer, top down
+        grads = []
+        delta = g_dnn.view(B, 1)
+        for li in reversed(range(len(layers))):
+            L, a_in = layers[li], acts[li]
+            K_in, N_out = L.kernel.shape
+            dW, db = emp(K_in, N_out), emp(N_out)
+            call("rs_gemm", 1, 0, K_in, N_out, B, 1.0, ptr(a_in), a_in.stride(0), ptr(delta), delta.stride(0), 0.0,
+                 ptr(dW), N_out, None, 0, *gw, st)
+            call("rs_col_sum", ptr(delta), delta.stride(0), B, N_out, ptr(db), st)
+            grads.append((L, dW, db))
+            relu_below = li > 0 and layers[li - 1].activation == "relu"
+            prev = emp(B, K_in)
+            call("rs_gemm", 0, 1, B, K_in, N_out, 1.0, ptr(delta), delta.stride(0), ptr(L.kernel), N_out, 0.0,
+                 ptr(prev), K_in, ptr(a_in) if relu_below else None, a_in.stride(0), *gw, st)
+            delta = prev
+        dx = delta  # [B, d]: the DNN's gradient w.r.t. x; the FM's is added next
+        call("rs_fm_x_grad", ptr(x), d, ptr(s), ptr(fm.w1), ptr(fm.v), B, d, kfm, ptr(g_fm), ptr(dx), d, st)
+        dw1, dv, dw0 = emp(d), emp(d, kfm), emp(1)
+        call("rs_fm_param_grads", ptr(x), d, ptr(s), ptr(fm.v), B, d, kfm, ptr(g_fm), ptr(dw1), ptr(dv), ptr(dw0), st)
+        # updates (every gradient above used the pre-step weights)
+        for L, dW, db in grads:
+            call("rs_sgd_update", ptr(L.kernel), ptr(dW), dW.numel(), float(lr), 0.0, st)
+            call("rs_sgd_update", ptr(L.bias), ptr(db), db.numel(), float(lr), 0.0, st)
+        call("rs_sgd_update", ptr(fm.w1), ptr(dw1), d, float(lr), float(fm.reg_w), st)
+        call("rs_sgd_update", ptr(fm.v), ptr(dv), d * kfm, float(lr), float(fm.reg_b), st)
+        call("rs_sgd_update", ptr(fm.w0), ptr(dw0), 1, float(lr), 0.0, st)
+        n = B * e.n_fields
+        ws_n = _lib.lib().rs_embedding_sgd_workspace_size(n)
+        ws = self.__dict__.get("_emb_ws")
+        if ws is None or ws.numel() < ws_n:
+            ws = self.__dict__["_emb_ws"] = torch.empty(ws_n, dtype=torch.uint8, device=dev)
+        call("rs_embedding_sgd", ptr(e.table), e.total_rows, e.k, ptr(ids), _lib.id_kind(ids), ids.stride(0),
+             ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, B, ptr(dx) + 4 * self.nd, d, float(lr), ptr(ws),
+             None, st)
+        self._weights_changed()  # packed operand images of the old weights are stale
+        return loss
+
+    def _gemm_ws(self, nbytes):
+        ws = self.__dict__.get("_gemm_wsbuf")
+        if ws is None or ws.numel() < max(nbytes, 1):
+            ws = self.__dict__["_gemm_wsbuf"] = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self._dev)
+        return ws
+
     def _fused_rows(self):
         """Tower input permutation for the fused kernel: its LDS tile holds
         [emb F*k | dense nd]; Keras rows are [dense nd | emb F*k]."""

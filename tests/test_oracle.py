@@ -167,3 +167,48 @@ def test_fm_train_step_gradient_matches_finite_differences():
             lm = O.fm_loss(x, t, w0, w1, v, l2w, l2v)[0]
             p[idx] = keep
             assert abs((lp - lm) / (2 * eps) - gp[idx]) < 1e-7
+
+
+def test_deepfm_train_step_gradient_matches_finite_differences():
+    """oracle.deepfm_train_step's hand backprop == central differences of
+    compile_fit's DeepFM objective, for embedding rows (one repeated in the
+    batch), DNN weights of every layer, FM w0 / w1 / v."""
+    rng = np.random.default_rng(12)
+    nd, k, kfm = 2, 3, 2
+    vocab = [3, 2]
+    tables = [rng.normal(size=(v_, k)) * 0.5 for v_ in vocab]
+    d = nd + len(vocab) * k
+    p = {"tables": tables, "w0": np.array([0.1]), "w1": rng.normal(size=(d, 1)), "v": rng.normal(size=(d, kfm)),
+         "dnn_hidden": [(rng.normal(size=(d, 5)), rng.normal(size=5) * 0.1),
+                        (rng.normal(size=(5, 3)), rng.normal(size=3) * 0.1)],
+         "dnn_out": (rng.normal(size=(3, 1)), np.array([0.05]))}
+    dense = rng.random((4, nd))
+    ids = np.array([[0, 1], [2, 1], [0, 0], [1, 1]])
+    t = np.array([1.0, 0.0, 1.0, 0.0])
+    lr, l2w, l2v = 1.0, 1e-2, 3e-2
+    new, _ = O.deepfm_train_step(dense, ids, t, p, lr, l2w, l2v, nd=nd)
+    eps = 1e-6
+
+    def check(arr, new_arr, idx):
+        keep = arr[idx]
+        arr[idx] = keep + eps
+        lp = O.deepfm_loss(dense, ids, t, p, l2w, l2v, nd=nd)
+        arr[idx] = keep - eps
+        lm = O.deepfm_loss(dense, ids, t, p, l2w, l2v, nd=nd)
+        arr[idx] = keep
+        assert abs((lp - lm) / (2 * eps) - (arr[idx] - new_arr[idx]) / lr) < 1e-6, idx
+
+    for idx in [(0, 0), (0, 2), (2, 1), (1, 0)]:
+        check(p["tables"][0], new["tables"][0], idx)
+    check(p["tables"][1], new["tables"][1], (1, 2))
+    check(p["w0"], new["w0"], (0,))
+    for idx in [(0, 0), (5, 0), (7, 0)]:
+        check(p["w1"], new["w1"], idx)
+    for idx in [(1, 1), (6, 0)]:
+        check(p["v"], new["v"], idx)
+    for li in range(2):
+        for idx in [(0, 0), (2, 1)]:
+            check(p["dnn_hidden"][li][0], new["dnn_hidden"][li][0], idx)
+        check(p["dnn_hidden"][li][1], new["dnn_hidden"][li][1], (1,))
+    check(p["dnn_out"][0], new["dnn_out"][0], (2, 0))
+    check(p["dnn_out"][1], new["dnn_out"][1], (0,))
