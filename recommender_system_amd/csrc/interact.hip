@@ -170,6 +170,89 @@ __global__ __launch_bounds__(256) void pair_pool_kernel(PoolArgs a) {
   }
 }
 
+// Sum / mean pooling, k % 4 == 0: 4 waves per workgroup split the fields
+// (wave w takes fields w, w+4, ...: its <= 8 ids first, then all its rows in
+// flight), each lane keeps float4 partials of sum e and sum e^2 for its 4
+// dims, and wave 0 adds the four partials in wave order (LDS) and finishes.
+// 64/G samples per workgroup (16 at k = 16 -> 256 workgroups at B = 4096).
+template <int G, int KIND>
+__global__ __launch_bounds__(256) void pair_pool_ksplit(PoolArgs a) {
+  typedef Ids<KIND> I;
+  constexpr int CH = 8;  // fields per wave and pass
+  __shared__ floatx4 sp[4][64], qp[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b = (int64_t)blockIdx.x * (64 / G) + lane / G;
+  const int l = lane & (G - 1);
+  const bool valid = b < a.batch;
+  const int64_t bb = valid ? b : a.batch - 1;
+  const bool lane_ok = 4 * l < a.k;
+  const int jj = lane_ok ? 4 * l : 0;
+  floatx4 s = {0.f, 0.f, 0.f, 0.f}, q = {0.f, 0.f, 0.f, 0.f};
+  bool bad = false;
+  for (int c0 = w; c0 < a.F; c0 += 4 * CH) {
+    int64_t row[CH];
+    bool okc[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const int cu = c0 + 4 * u;
+      const int c = cu < a.F ? cu : a.F - 1;
+      int64_t id;
+      okc[u] = I::decode(I::load(a.ids, bb * a.id_stride + c), a.vocab[c], id) && cu < a.F;
+      bad |= cu < a.F && !okc[u];
+      row[u] = a.offs[c] + id;
+    }
+    floatx4 v[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+      v[u] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(a.table + row[u] * a.k + jj));
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const floatx4 x = okc[u] ? v[u] : floatx4{0.f, 0.f, 0.f, 0.f};
+      s += x;
+      q += x * x;
+    }
+  }
+  if (bad && valid && lane_ok) flag_error(a.err);
+  sp[w][lane] = s;
+  qp[w][lane] = q;
+  __syncthreads();
+  if (w != 0) return;
+  s = sp[0][lane];
+  q = qp[0][lane];
+#pragma unroll
+  for (int ww = 1; ww < 4; ++ww) {
+    s += sp[ww][lane];
+    q += qp[ww][lane];
+  }
+  floatx4 pooled = 0.5f * (s * s - q);
+  if (a.mode == 1) pooled = a.F >= 2 ? pooled * (1.0f / (0.5f * (float)a.F * (float)(a.F - 1))) : floatx4{0.f, 0.f, 0.f, 0.f};
+  if (valid && a.out) {
+    float* o = a.out + b * a.out_stride;
+    if (lane_ok) {
+      if (((a.out_col | (int)a.out_stride) & 3) == 0) {
+        *reinterpret_cast<floatx4*>(o + a.out_col + jj) = pooled;
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) o[a.out_col + jj + t] = pooled[t];
+      }
+    }
+    for (int d = l; d < a.nd; d += G) o[d] = a.dense[b * a.dense_stride + d];
+  }
+  if (a.head_w) {
+    float y = 0.f;
+    if (lane_ok) {
+      const floatx4 hw = *reinterpret_cast<const floatx4*>(a.head_w + jj);
+      const floatx4 p = pooled * hw;
+      y = (p[0] + p[1]) + (p[2] + p[3]);
+    }
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) y += __shfl_xor(y, o, G);
+    y += a.head_b ? a.head_b[0] : 0.f;
+    for (int t = 0; t < a.n_sig; ++t) y = sigmoidf_(y);
+    if (valid && l == 0) a.head_out[b] = y;
+  }
+}
+
 // InteractionLayer: out[b, p, j] = e[b, i_p, j] * e[b, j_p, j], pairs row-major.
 __global__ __launch_bounds__(256) void pair_products_kernel(const float* __restrict__ e, int64_t e_stride, int F,
                                                             int k, int64_t batch, float* __restrict__ out) {
@@ -446,8 +529,20 @@ extern "C" int rs_embed_pair_pool_fwd(const void* ids, int id_kind, int64_t id_s
         }
       }
     };
-    if (mode != 2) go(std::integral_constant<int, 0>());
-    else go(std::integral_constant<int, PMAXF>());
+    if (mode != 2 && v4) {
+      const unsigned g2 = (unsigned)((batch + 64 / G - 1) / (64 / G));
+      switch (G) {
+        case 1: pair_pool_ksplit<1, KD><<<g2, 256, 0, st>>>(a); break;
+        case 2: pair_pool_ksplit<2, KD><<<g2, 256, 0, st>>>(a); break;
+        case 4: pair_pool_ksplit<4, KD><<<g2, 256, 0, st>>>(a); break;
+        case 8: pair_pool_ksplit<8, KD><<<g2, 256, 0, st>>>(a); break;
+        default: pair_pool_ksplit<16, KD><<<g2, 256, 0, st>>>(a); break;
+      }
+    } else if (mode != 2) {
+      go(std::integral_constant<int, 0>());
+    } else {
+      go(std::integral_constant<int, PMAXF>());
+    }
   });
   return launch_status("rs_embed_pair_pool_fwd");
 }
