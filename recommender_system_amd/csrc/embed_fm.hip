@@ -494,9 +494,9 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   if constexpr (TW) mlp_tower_tile<NW>(*tw, tsm, (int64_t)tile * 16, ring, fmlog);
 }
 
-template <int KV, int NT, int NW, int KIND>
+template <int KV, int NT, int NW, int KIND, int MC>
 __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
-  embed_fm_body<KV, NT, NW, KIND, false>(a, nullptr, blockIdx.x);
+  embed_fm_body<KV, NT, NW, KIND, false, MC>(a, nullptr, blockIdx.x);
 }
 
 // ---- sharded FM, partial protocol: combine (requester side) as a block part
@@ -570,7 +570,7 @@ __global__ __launch_bounds__(NW * 64) void shard_fm_pipe(EmbedFmArgs a, PipeArgs
 // Fused DeepFM forward: gather + FM + DNN tower + head, one launch.
 template <int KV, int KIND>
 __global__ __launch_bounds__(16 * 64) void deepfm_fused(EmbedFmArgs a, MlpArgs t) {
-  embed_fm_body<KV, 1, 16, KIND, true>(a, &t, blockIdx.x);
+  embed_fm_body<KV, 1, 16, KIND, true, 1>(a, &t, blockIdx.x);
 }
 
 // Generic fallback (any k / kfm): one 256-thread workgroup per sample.
@@ -754,10 +754,14 @@ static int grid_for(int64_t work, int block, int cap = 2048) {
 
 template <int KV, int NT, int KIND>
 static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st) {
-  // 16 waves per 16-sample tile (measured best at the headline shape against
-  // 4, 8 and 13 waves: every field slot has its own wave, max 2 fields/wave)
+  // 16 waves per 16-sample tile (measured against 4, 8 and 13 waves), one
+  // field slot per wave and pass: the headline's 26 fields take two passes
+  // (16 + 10), 6.05 us per launch against 6.54 with both in one pass (2 slots
+  // per wave) — the second pass's row requests queue behind a shorter first
+  // wave of 256 rows per CU.  More than 32 fields: 2 slots per pass.
   const int grid = (int)((a.batch + 15) / 16);
-  embed_fm_mfma<KV, NT, 16, KIND><<<grid, 16 * 64, 0, st>>>(a);
+  if (a.F <= 32) embed_fm_mfma<KV, NT, 16, KIND, 1><<<grid, 16 * 64, 0, st>>>(a);
+  else embed_fm_mfma<KV, NT, 16, KIND, 0><<<grid, 16 * 64, 0, st>>>(a);
 }
 
 template <int KIND>
@@ -962,13 +966,14 @@ static void launch_pipe4(const EmbedFmArgs& a, PipeArgs p, hipStream_t st) {
 }
 
 // NW / MC by the owner's field count: 4 waves x 1 slot for <= 4 fields (the
-// 8-rank shape), 16 waves for more; past 16 fields the default 2 slots.
+// 8-rank shape), 16 waves x 1 slot per pass up to 32 fields (as the headline
+// kernel), 2 slots per pass beyond.
 template <int KV>
 static void launch_pipe_kv(const EmbedFmArgs& a, const PipeArgs& p, int NT, hipStream_t st) {
   if (NT == 1 && a.F <= 4) launch_pipe4<KV, 1, 4, 1>(a, p, st);
-  else if (NT == 1 && a.F <= 16) launch_pipe4<KV, 1, 16, 1>(a, p, st);
+  else if (NT == 1 && a.F <= 32) launch_pipe4<KV, 1, 16, 1>(a, p, st);
   else if (NT == 1) launch_pipe4<KV, 1, 16, 0>(a, p, st);
-  else if (a.F <= 16) launch_pipe4<KV, 2, 16, 1>(a, p, st);
+  else if (a.F <= 32) launch_pipe4<KV, 2, 16, 1>(a, p, st);
   else launch_pipe4<KV, 2, 16, 0>(a, p, st);
 }
 
