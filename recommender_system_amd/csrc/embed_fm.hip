@@ -293,6 +293,9 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 
   // ---- fields c = cg + j*NW + w; slots past F re-read field F-1 and add 0
   for (int cg = 0; cg < a.F; cg += NW * MAXC) {
+    // one slot per wave: a wave with no field left in this pass stops (a
+    // wave-uniform exit; nothing after the loop needs its slot)
+    if (MAXC == 1 && cg + w >= a.F) break;
     int cj[MAXC];
     int64_t offc[MAXC], vocc[MAXC];
     // Field metadata through the VECTOR path (wave index taken from the raw
