@@ -253,11 +253,14 @@ __global__ __launch_bounds__(16 * 64) void embed_cross(CrossArgs a, EmbedCrossAr
   {
     const int KQ = e.k >> 2, FKQ = F * KQ;
     const int nit = (FKQ + 63) >> 6;
-    for (int base = 0; base < nit; base += 8) {
-      floatx4 v[8];
-      int dst[8];
+    // one 64-chunk slice per pass (26 fields x 4 chunks: 2 passes) — as in
+    // the headline kernel, requesting the rows in two waves beats one burst
+    constexpr int CP = 1;
+    for (int base = 0; base < nit; base += CP) {
+      floatx4 v[CP];
+      int dst[CP];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < CP; ++u) {
         const int ch = (base + u) * 64 + lane;
         dst[u] = -1;
         v[u] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -273,7 +276,7 @@ __global__ __launch_bounds__(16 * 64) void embed_cross(CrossArgs a, EmbedCrossAr
         }
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < CP; ++u)
         if (dst[u] >= 0) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) tile[dst[u] + q] = v[u][q];
@@ -332,11 +335,14 @@ __global__ __launch_bounds__(16 * 64) void dcn_fused(CrossArgs a, EmbedCrossArgs
   {  // rows: wave w gathers sample w's F*k/4 float4 chunks into its tile row
     const int KQ = e.k >> 2, FKQ = F * KQ;
     const int nit = (FKQ + 63) >> 6;
-    for (int base = 0; base < nit; base += 8) {
-      floatx4 v[8];
-      int dst[8];
+    // one 64-chunk slice per pass (26 fields x 4 chunks: 2 passes) — as in
+    // the headline kernel, requesting the rows in two waves beats one burst
+    constexpr int CP = 1;
+    for (int base = 0; base < nit; base += CP) {
+      floatx4 v[CP];
+      int dst[CP];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < CP; ++u) {
         const int ch = (base + u) * 64 + lane;
         dst[u] = -1;
         v[u] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -352,7 +358,7 @@ __global__ __launch_bounds__(16 * 64) void dcn_fused(CrossArgs a, EmbedCrossArgs
         }
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < CP; ++u)
         if (dst[u] >= 0) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) tsm[dst[u] + q] = v[u][q];
