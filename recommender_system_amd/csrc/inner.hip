@@ -177,11 +177,14 @@ __global__ __launch_bounds__(IP_NT) void inner_fast(InnerArgs a) {
     const int FKQ = F * KQ;
     const int per_s = (FKQ + 63) / 64;     // chunks per lane per sample
     const int nit = ((S + IP_NW - 1) / IP_NW) * per_s;  // (sample, chunk-block) steps of this wave
-    for (int base = 0; base < nit; base += 8) {
-      floatx4 v[8];
-      int dsti[8];
+    // one (sample, 64-chunk block) step per pass: the rows go out in two
+    // waves at F = 26, k = 16 (as in the headline kernel)
+    constexpr int CP = 1;
+    for (int base = 0; base < nit; base += CP) {
+      floatx4 v[CP];
+      int dsti[CP];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < CP; ++u) {
         const int it = base + u;
         const int si = it / per_s, cb = it - si * per_s;  // per_s is 1..2 for F<=64, K<=16
         const int sidx = w + IP_NW * si;
@@ -207,7 +210,7 @@ __global__ __launch_bounds__(IP_NT) void inner_fast(InnerArgs a) {
         }
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < CP; ++u)
         if (dsti[u] >= 0) *reinterpret_cast<floatx4*>(tile + dsti[u]) = v[u];
     }
   }
