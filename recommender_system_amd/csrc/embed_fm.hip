@@ -969,11 +969,12 @@ static void launch_pipe4(const EmbedFmArgs& a, PipeArgs p, hipStream_t st) {
 }
 
 // NW / MC by the owner's field count: 4 waves x 1 slot for <= 4 fields (the
-// 8-rank shape), 16 waves x 1 slot per pass up to 32 fields (as the headline
-// kernel), 2 slots per pass beyond.
+// 8-rank shape), 8 waves for <= 8 (4 ranks), 16 waves x 1 slot per pass up
+// to 32 fields (as the headline kernel), 2 slots per pass beyond.
 template <int KV>
 static void launch_pipe_kv(const EmbedFmArgs& a, const PipeArgs& p, int NT, hipStream_t st) {
   if (NT == 1 && a.F <= 4) launch_pipe4<KV, 1, 4, 1>(a, p, st);
+  else if (NT == 1 && a.F <= 8) launch_pipe4<KV, 1, 8, 1>(a, p, st);
   else if (NT == 1 && a.F <= 32) launch_pipe4<KV, 1, 16, 1>(a, p, st);
   else if (NT == 1) launch_pipe4<KV, 1, 16, 0>(a, p, st);
   else if (a.F <= 32) launch_pipe4<KV, 2, 16, 1>(a, p, st);
