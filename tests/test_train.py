@@ -134,3 +134,34 @@ def test_deepfm_train_steps_match_oracle(gpu, B, k, hidden, vmax, id_dtype):
         assert_scaled_close(got["dnn_out"][0], p["dnn_out"][0], what=f"step {step} W_out")
     y = m((dense, ids))
     assert_scaled_close(y, O.deepfm(None, p, inputs=(dense, ids))[0], what="forward after training")
+
+
+@pytest.mark.gpu
+def test_compile_fit_deepfm_on_bundled_sample(gpu):
+    """compile_fit on DeepFM (model/deepFM.py's __main__ flow) over the
+    reference's bundled Criteo sample: the loss falls epoch over epoch, and
+    the first 5 SGD steps equal the oracle's."""
+    import os
+
+    import recommender_system_amd as rs
+    from recommender_system_amd.dataset import criteo_compact, features_dict
+    from recommender_system_amd.train import compile_fit
+    from tests.helpers import dnn_params, tables_of
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "criteo_train_1w.txt.gz")
+    dense, ids, label, _ = criteo_compact(path)
+    cols = features_dict(path)
+    m = rs.DeepFM(cols, 10, 1e-4, 1e-4, [64, 32], 1, "relu", seed=4)
+    hid, out = dnn_params(m.dnn)
+    p = {"tables": tables_of(m.embed_layer), "w0": m.fm.w0.cpu().numpy(), "w1": m.fm.w1.cpu().numpy(),
+         "v": m.fm.v.cpu().numpy(), "dnn_hidden": hid, "dnn_out": out}
+    N = 160
+    compile_fit(m, dense[:N], ids[:N], label[:N], batch_size=32, epochs=1, sgd=0.01)
+    d32 = dense[:N].astype(np.float32)
+    for r0 in range(0, N, 32):
+        p, _ = O.deepfm_train_step(d32[r0:r0 + 32], ids[r0:r0 + 32], label[r0:r0 + 32], p, 0.01, 1e-4, 1e-4)
+    assert_scaled_close(m.fm.v, p["v"], what="DeepFM compile_fit v")
+    for c in (0, 7, 25):
+        assert_scaled_close(m.embed_layer.field_table(c), p["tables"][c], what=f"DeepFM compile_fit table {c}")
+    m2 = rs.DeepFM(cols, 10, 1e-4, 1e-4, [64, 32], 1, "relu", seed=4)
+    hist = compile_fit(m2, dense[:960], ids[:960], label[:960], batch_size=32, epochs=4, sgd=0.05)
+    assert hist[-1] < hist[0]
