@@ -855,6 +855,14 @@ def bench_fm_train(args, world, rank):
 
     n_d = max(10, args.steps // 5)
     dtd, _ = _timed_graph(step_dfm, n_d, args.warmup, world, chunk=16)
+    del dfm
+    # DCN training step (config-2 model: CrossNet 3 layers over d = 429, DNN 256-128-64 -> 1)
+    dcn = rs.DCN(cols, [256, 128, 64], 1, "relu", 3, embed_dim=16, seed=SEED, device=dev)
+
+    def step_dcn(i):
+        dcn.train_step((dense_pool[i % 16], ids_pool[i % 16]), lab[i % 16], lr=0.01, check_ids=False)
+
+    dtc, _ = _timed_graph(step_dcn, n_d, args.warmup, world, chunk=16)
     return _line("FM training samples/sec @ batch 4096, 26 x 1e6 one-hot columns, k 16 (SGD + l2, compile_fit)",
                  args.steps * B / dt, "samples/s", args, world, dt / args.steps * 1e3,
                  {"workload": "fm_train_step", "global_batch": B, "vocab_per_field": V, "k": k,
@@ -866,6 +874,9 @@ def bench_fm_train(args, world, rank):
                  {"deepfm_train": {"samples_per_s": n_d * B / dtd, "ms_per_step": dtd / n_d * 1e3,
                                    "note": "DeepFM.train_step: gather, DNN 429-256-128-64-1 fwd/bwd (rs_dense_fwd, "
                                            "rs_gemm), FM grads, SGD + l2, row-sparse embedding SGD"},
+                  "dcn_train": {"samples_per_s": n_d * B / dtc, "ms_per_step": dtc / n_d * 1e3,
+                                "note": "DCN.train_step: gather, CrossNet x3 fwd/bwd (rs_cross_train_fwd/_bwd), DNN "
+                                        "429-256-128-64-1, output Dense, SGD + l2, row-sparse embedding SGD"},
                   "reference_scale": {"steps_per_s": args.steps / dts, "ms_per_step": dts / args.steps * 1e3,
                                       "note": "batch 32, 26 x 1,677 + 13 = 43,615 columns, k 8 (compile_fit's "
                                               "defaults on the bundled sample's width)"}})

@@ -417,6 +417,23 @@ int rs_fm_param_grads(const float* x, int64_t ldx, const float* s,
                       const float* v, int64_t batch, int d, int kfm,
                       const float* g, float* dw1, float* dv, float* dw0,
                       rs_stream_t stream);
+/* CrossNet training (layer/interaction.py:75-83, DCN.train_step):
+ * rs_cross_train_fwd: x_{l+1} = x0 (x_l . w_l) + b_l + x_l for l < L;
+ *  W, b [L, d] (row l = w_l, b_l); keeps xs [L, B, d] (x_1 .. x_L) and
+ *  g [L, B] (g_l = x_l . w_l); x_L also to xl_out (row stride ldo; may be
+ *  NULL).  d <= 2048.
+ * rs_cross_train_bwd: from dxl = dL/dx_L: deltas [L, B, d] (delta_{l+1} for
+ *  db_l = sum_b delta_{l+1}), s [L, B] (s_l = x0 . delta_{l+1}, for dw_l =
+ *  sum_b s_l x_l), and dx += delta_0 + sum_l g_l delta_{l+1} (dL/dx0).      */
+int rs_cross_train_fwd(const float* x0, int64_t ldx, int d, int n_layers,
+                       const float* W, const float* b, int64_t batch,
+                       float* xs, float* g, float* xl_out, int64_t ldo,
+                       rs_stream_t stream);
+int rs_cross_train_bwd(const float* x0, int64_t ldx, int d, int n_layers,
+                       const float* W, int64_t batch, const float* g,
+                       const float* dxl, int64_t lddxl, float* deltas,
+                       float* s, float* dx, int64_t lddx,
+                       rs_stream_t stream);
 int64_t rs_embedding_sgd_workspace_size(int64_t n_lookups);
 int rs_embedding_sgd(float* table, int64_t n_rows, int k, const void* ids,
                      int id_kind, int64_t id_stride,

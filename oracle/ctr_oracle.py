@@ -564,3 +564,80 @@ def deepfm_loss(dense, ids, t, p, l2_w, l2_v, nd=13, dt=np.float64):
     t = np.asarray(t, dt)
     ce = np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z)))
     return np.mean(ce) + l2_w * np.sum(np.asarray(p["w1"], dt) ** 2) + l2_v * np.sum(np.asarray(p["v"], dt) ** 2)
+
+
+def dcn_train_step(dense, ids, t, p, lr, reg_w, reg_b, nd=13, act="relu", dt=np.float64):
+    """One SGD step of compile_fit on DCN (model/dcn.py:24-34,
+    utils/compile_fit.py:9-15), backpropagated by hand.  logit = [x_L | dnn]
+    Wo + bo, g = (sigmoid(logit) - t)/B; CrossNet (layer/interaction.py:75-83)
+    x_{l+1} = x0 g_l + b_l + x_l with g_l = x_l . w_l, backward
+    delta_L = dL/dx_L, s_l = x0 . delta_{l+1}, dw_l = sum_b s_l x_l,
+    db_l = sum_b delta_{l+1}, delta_l = delta_{l+1} + s_l w_l, dL/dx0 +=
+    delta_0 + sum_l g_l delta_{l+1}; l2(reg) adds 2 reg w.  DNNLayer's
+    Dropout is taken as the identity.  Returns (new p, losses before the step)."""
+    dense = np.asarray(dense, dt)
+    ids = cast_ids(ids)
+    t = np.asarray(t, dt)
+    tables = [np.array(tb, dt) for tb in p["tables"]]
+    k = tables[0].shape[1]
+    x = np.concatenate([dense, embed_layer(ids, tables, dt)], axis=1)
+    B, d = x.shape
+    ws = [np.array(w, dt).reshape(-1) for w in p["cross_w"]]
+    bs = [np.array(b, dt).reshape(-1) for b in p["cross_b"]]
+    xl, xs, gl = x, [x], []
+    for w, b in zip(ws, bs):
+        gl.append(xl @ w)
+        xl = x * gl[-1][:, None] + b[None, :] + xl
+        xs.append(xl)
+    layers = [(np.array(W, dt), np.array(b, dt)) for W, b in p["dnn_hidden"]] + \
+             [(np.array(p["dnn_out"][0], dt), np.array(p["dnn_out"][1], dt))]
+    acts = [x]
+    for W, b in layers[:-1]:
+        acts.append(activation(acts[-1] @ W + b, act))
+    dnn = acts[-1] @ layers[-1][0] + layers[-1][1]
+    z = np.concatenate([xl, dnn], axis=1)
+    Wo, bo = np.array(p["out_kernel"], dt), np.array(p["out_bias"], dt)
+    logit = (z @ Wo + bo)[:, 0]
+    loss = np.maximum(logit, 0) - logit * t + np.log1p(np.exp(-np.abs(logit)))
+    g = (sigmoid(logit) - t) / B
+    dz = g[:, None] @ Wo.T
+    out = {"out_kernel": Wo - lr * (z.T @ g[:, None]), "out_bias": bo - lr * g.sum(keepdims=True)}
+    delta = dz[:, d:]
+    new_layers = [None] * len(layers)
+    for li in reversed(range(len(layers))):
+        W, b = layers[li]
+        dW, db = acts[li].T @ delta, delta.sum(0)
+        prev = delta @ W.T
+        if li > 0 and act == "relu":
+            prev = prev * (acts[li] > 0)
+        new_layers[li] = (W - lr * dW, b - lr * db)
+        delta = prev
+    dx = delta
+    dc = dz[:, :d]
+    new_w, new_b = [None] * len(ws), [None] * len(ws)
+    for l in reversed(range(len(ws))):
+        s_l = np.sum(x * dc, axis=1)
+        new_w[l] = (ws[l] - lr * (xs[l].T @ s_l + 2 * reg_w * ws[l])).reshape(-1, 1)
+        new_b[l] = (bs[l] - lr * (dc.sum(0) + 2 * reg_b * bs[l])).reshape(-1, 1)
+        dx = dx + gl[l][:, None] * dc
+        dc = dc + s_l[:, None] * ws[l][None, :]
+    dx = dx + dc
+    out.update({"cross_w": new_w, "cross_b": new_b, "dnn_hidden": new_layers[:-1], "dnn_out": new_layers[-1]})
+    for c, tb in enumerate(tables):
+        np.add.at(tb, ids[:, c], -lr * dx[:, nd + c * k: nd + (c + 1) * k])
+    out["tables"] = tables
+    return out, loss
+
+
+def dcn_loss(dense, ids, t, p, reg_w, reg_b, nd=13, dt=np.float64):
+    """compile_fit's objective on DCN: mean BCE(t, DCN.call) + reg_w sum |w_l|^2
+    + reg_b sum |b_l|^2 (the Keras l2 regularisers)."""
+    q = dict(p, act=p.get("act", "relu"))
+    x = np.concatenate([np.asarray(dense, dt), embed_layer(ids, p["tables"], dt)], axis=1)
+    z = np.concatenate([cross_layer(x, p["cross_w"], p["cross_b"], dt),
+                        dnn_layer(x, p["dnn_hidden"], p["dnn_out"], q["act"], dt)], axis=1)
+    logit = (z @ np.asarray(p["out_kernel"], dt) + np.asarray(p["out_bias"], dt))[:, 0]
+    t = np.asarray(t, dt)
+    ce = np.maximum(logit, 0) - logit * t + np.log1p(np.exp(-np.abs(logit)))
+    return np.mean(ce) + reg_w * sum(np.sum(np.asarray(w, dt) ** 2) for w in p["cross_w"]) + \
+        reg_b * sum(np.sum(np.asarray(b, dt) ** 2) for b in p["cross_b"])

@@ -77,6 +77,8 @@ SIGNATURES = {
     "rs_head_grad": (I, [P, P, P, L, F, F, P, P, P, P]),
     "rs_fm_x_grad": (I, [P, L, P, P, P, L, I, I, P, P, L, P]),
     "rs_fm_param_grads": (I, [P, L, P, P, L, I, I, P, P, P, P, P]),
+    "rs_cross_train_fwd": (I, [P, L, I, I, P, P, L, P, P, P, L, P]),
+    "rs_cross_train_bwd": (I, [P, L, I, I, P, L, P, P, L, P, P, P, L, P]),
     "rs_embedding_sgd_workspace_size": (L, [L]),
     "rs_embedding_sgd": (I, [P, L, I, P, I, L, P, P, I, L, P, L, F, P, P, P]),
     "rs_fm_partial_width": (I, [I]),

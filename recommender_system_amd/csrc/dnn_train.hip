@@ -250,6 +250,116 @@ __global__ __launch_bounds__(256) void emb_apply_kernel(const uint32_t* __restri
   }
 }
 
+// ------------------------------------------------------ CrossNet training
+// layer/interaction.py:75-83: x_{l+1} = x0 (x_l . w_l) + b_l + x_l.
+// Forward, one wave per sample: every x_l (l = 1..L; x_0 = x0 itself) and
+// g_l = x_l . w_l are kept for the backward; x_L also goes to xl_out (the
+// output Dense's input, row stride ldo).
+constexpr int CR_MAXE = 32;  // d <= 64 * CR_MAXE
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void cross_train_fwd(const float* __restrict__ x0, int64_t ldx, int d, int L,
+                                                       const float* __restrict__ W, const float* __restrict__ Bv,
+                                                       int64_t B, float* __restrict__ xs, float* __restrict__ gl,
+                                                       float* __restrict__ xl_out, int64_t ldo) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;  // wave-uniform
+  const int ne = (d + 63) / 64;
+  float x0r[CR_MAXE], xr[CR_MAXE];
+#pragma unroll
+  for (int t = 0; t < CR_MAXE; ++t) {
+    const int e = lane + 64 * t;
+    x0r[t] = (t < ne && e < d) ? x0[b * ldx + e] : 0.f;
+    xr[t] = x0r[t];
+  }
+  for (int l = 0; l < L; ++l) {
+    float dot = 0.f;
+#pragma unroll
+    for (int t = 0; t < CR_MAXE; ++t) {
+      const int e = lane + 64 * t;
+      if (t < ne && e < d) dot = fmaf(xr[t], W[(int64_t)l * d + e], dot);
+    }
+    const float g = wave_sum(dot);
+    if (lane == 0) gl[(int64_t)l * B + b] = g;
+    float* xo = xs + ((int64_t)l * B + b) * d;  // x_{l+1}
+#pragma unroll
+    for (int t = 0; t < CR_MAXE; ++t) {
+      const int e = lane + 64 * t;
+      if (t < ne && e < d) {
+        xr[t] = fmaf(x0r[t], g, Bv[(int64_t)l * d + e]) + xr[t];
+        xo[e] = xr[t];
+      }
+    }
+  }
+  if (xl_out) {
+#pragma unroll
+    for (int t = 0; t < CR_MAXE; ++t) {
+      const int e = lane + 64 * t;
+      if (t < ne && e < d) xl_out[b * ldo + e] = xr[t];
+    }
+  }
+}
+
+// Backward, one wave per sample, from delta_L = dL/dx_L (row stride ldd):
+// for l = L-1 .. 0:  keep delta_{l+1} (db_l = sum_b delta_{l+1}) and
+// s_l = x0 . delta_{l+1} (dw_l = sum_b s_l x_l); dL/dx0 += g_l delta_{l+1};
+// delta_l = delta_{l+1} + s_l w_l.  Finally dx (row stride lddx) += delta_0
+// + sum_l g_l delta_{l+1}.
+__global__ __launch_bounds__(256) void cross_train_bwd(const float* __restrict__ x0, int64_t ldx, int d, int L,
+                                                       const float* __restrict__ W, int64_t B,
+                                                       const float* __restrict__ gl, const float* __restrict__ dL,
+                                                       int64_t ldd, float* __restrict__ deltas,
+                                                       float* __restrict__ sl, float* __restrict__ dx,
+                                                       int64_t lddx) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int ne = (d + 63) / 64;
+  float x0r[CR_MAXE], dr[CR_MAXE], acc[CR_MAXE];
+#pragma unroll
+  for (int t = 0; t < CR_MAXE; ++t) {
+    const int e = lane + 64 * t;
+    const bool in = t < ne && e < d;
+    x0r[t] = in ? x0[b * ldx + e] : 0.f;
+    dr[t] = in ? dL[b * ldd + e] : 0.f;
+    acc[t] = 0.f;
+  }
+  for (int l = L - 1; l >= 0; --l) {
+    float* dout = deltas + ((int64_t)l * B + b) * d;  // delta_{l+1}
+    float dot = 0.f;
+#pragma unroll
+    for (int t = 0; t < CR_MAXE; ++t) {
+      const int e = lane + 64 * t;
+      if (t < ne && e < d) {
+        dout[e] = dr[t];
+        dot = fmaf(x0r[t], dr[t], dot);
+      }
+    }
+    const float s = wave_sum(dot);
+    const float g = gl[(int64_t)l * B + b];
+    if (lane == 0) sl[(int64_t)l * B + b] = s;
+#pragma unroll
+    for (int t = 0; t < CR_MAXE; ++t) {
+      const int e = lane + 64 * t;
+      if (t < ne && e < d) {
+        acc[t] = fmaf(g, dr[t], acc[t]);
+        dr[t] = fmaf(s, W[(int64_t)l * d + e], dr[t]);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < CR_MAXE; ++t) {
+    const int e = lane + 64 * t;
+    if (t < ne && e < d) dx[b * lddx + e] += dr[t] + acc[t];
+  }
+}
+
 }  // namespace rs
 
 using namespace rs;
@@ -383,4 +493,28 @@ extern "C" int rs_embedding_sgd(float* table, int64_t n_rows, int k, const void*
   emb_apply_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(key_out, val_out, n, n_fields, k, grad, grad_stride,
                                                                lr, table);
   return launch_status("rs_embedding_sgd");
+}
+
+extern "C" int rs_cross_train_fwd(const float* x0, int64_t ldx, int d, int n_layers, const float* W, const float* b,
+                                  int64_t batch, float* xs, float* g, float* xl_out, int64_t ldo,
+                                  rs_stream_t stream) {
+  if (batch == 0 || n_layers == 0) return RS_OK;
+  RS_REQUIRE(x0 && W && b && xs && g && batch > 0 && d >= 1 && d <= 64 * CR_MAXE && n_layers > 0 && ldx >= d &&
+                 (!xl_out || ldo >= d),
+             "rs_cross_train_fwd: bad arguments (d <= %d)", 64 * CR_MAXE);
+  cross_train_fwd<<<(unsigned)((batch + 3) / 4), 256, 0, as_stream(stream)>>>(x0, ldx, d, n_layers, W, b, batch, xs,
+                                                                              g, xl_out, ldo);
+  return launch_status("rs_cross_train_fwd");
+}
+
+extern "C" int rs_cross_train_bwd(const float* x0, int64_t ldx, int d, int n_layers, const float* W, int64_t batch,
+                                  const float* g, const float* dxl, int64_t lddxl, float* deltas, float* s,
+                                  float* dx, int64_t lddx, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(x0 && dxl && dx && batch > 0 && d >= 1 && d <= 64 * CR_MAXE && n_layers >= 0 && ldx >= d &&
+                 lddxl >= d && lddx >= d && (n_layers == 0 || (W && g && deltas && s)),
+             "rs_cross_train_bwd: bad arguments (d <= %d)", 64 * CR_MAXE);
+  cross_train_bwd<<<(unsigned)((batch + 3) / 4), 256, 0, as_stream(stream)>>>(x0, ldx, d, n_layers, W, batch, g, dxl,
+                                                                              lddxl, deltas, s, dx, lddx);
+  return launch_status("rs_cross_train_bwd");
 }

@@ -58,6 +58,62 @@ def _subseed(gen):
     return int(torch.randint(0, 2 ** 31, (1,), generator=gen))
 
 
+def _dnn_backward(layers, acts, delta, gw, emp, st):
+    """Backward through Dense layers (relu or linear hidden activations):
+    delta = dL/d(pre-activation) of the top layer; returns the (layer, dW, db)
+    gradients and dL/d(acts[0]).  dW = a_in^T delta (split-K rs_gemm), db =
+    column sums, delta_below = (delta W^T) [a_in > 0] (mask epilogue)."""
+    B = acts[0].shape[0]
+    grads = []
+    for li in reversed(range(len(layers))):
+        L, a_in = layers[li], acts[li]
+        K_in, N_out = L.kernel.shape
+        dW, db = emp(K_in, N_out), emp(N_out)
+        call("rs_gemm", 1, 0, K_in, N_out, B, 1.0, ptr(a_in), a_in.stride(0), ptr(delta), delta.stride(0), 0.0,
+             ptr(dW), N_out, None, 0, *gw, st)
+        call("rs_col_sum", ptr(delta), delta.stride(0), B, N_out, ptr(db), st)
+        grads.append((L, dW, db))
+        relu_below = li > 0 and layers[li - 1].activation == "relu"
+        prev = emp(B, K_in)
+        call("rs_gemm", 0, 1, B, K_in, N_out, 1.0, ptr(delta), delta.stride(0), ptr(L.kernel), N_out, 0.0,
+             ptr(prev), K_in, ptr(a_in) if relu_below else None, a_in.stride(0), *gw, st)
+        delta = prev
+    return grads, delta
+
+
+def _dnn_apply(grads, lr, st, l2=0.0):
+    for L, dW, db in grads:
+        call("rs_sgd_update", ptr(L.kernel), ptr(dW), dW.numel(), float(lr), float(l2), st)
+        call("rs_sgd_update", ptr(L.bias), ptr(db), db.numel(), float(lr), float(l2), st)
+
+
+def _embedding_sgd(model, ids, dx, ldx, lr, st):
+    """Row-sparse SGD of the looked-up rows from dL/dx's embedding block
+    (columns nd.., row stride ldx): rs_embedding_sgd, duplicates summed in
+    lookup order."""
+    e = model.embed_layer
+    B = ids.shape[0]
+    ws_n = _lib.lib().rs_embedding_sgd_workspace_size(B * e.n_fields)
+    ws = model.__dict__.get("_emb_ws")
+    if ws is None or ws.numel() < ws_n:
+        ws = model.__dict__["_emb_ws"] = torch.empty(ws_n, dtype=torch.uint8, device=model._dev)
+    call("rs_embedding_sgd", ptr(e.table), e.total_rows, e.k, ptr(ids), _lib.id_kind(ids), ids.stride(0),
+         ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, B, ptr(dx) + 4 * model.nd, ldx, float(lr), ptr(ws),
+         None, st)
+
+
+def _check_train_tower(name, dnn):
+    if any(l.activation not in (None, "linear", "relu") for l in dnn.hidden_layer):
+        raise NotImplementedError(f"{name}.train_step: 'relu' or linear hidden layers only")
+
+
+def _gemm_ws(model, nbytes):
+    ws = model.__dict__.get("_gemm_wsbuf")
+    if ws is None or ws.numel() < max(nbytes, 1):
+        ws = model.__dict__["_gemm_wsbuf"] = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=model._dev)
+    return ws
+
+
 class FM(KerasModule):
     """FM(k, w_reg, v_reg) — model/fm.py:14-23: sigmoid(FMLayer(x)).
 
@@ -175,8 +231,7 @@ class DeepFM(KerasModule):
         layers = list(dnn.hidden_layer) + [dnn.output_layer]
         if dnn.output_layer.units != 1:
             raise NotImplementedError("DeepFM.train_step: output_dim 1 only")
-        if any(l.activation not in (None, "linear", "relu") for l in dnn.hidden_layer):
-            raise NotImplementedError("DeepFM.train_step: 'relu' or linear hidden layers only")
+        _check_train_tower("DeepFM", dnn)
         B, dev, st = ids.shape[0], self._dev, _lib.stream()
         d, kfm = self.nd + e.n_fields * e.k, fm.k
         emp = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=dev)
@@ -195,49 +250,22 @@ class DeepFM(KerasModule):
         g_fm, g_dnn = emp(B), emp(B)
         loss = emp(B) if return_loss else None
         call("rs_head_grad", ptr(fm_out), ptr(dnn_out), ptr(labels), B, 0.5, 0.5, ptr(g_fm), ptr(g_dnn), ptr(loss), st)
-        # DNN backward: delta = dL/d(pre-activation) of each layer, top down
-        grads = []
-        delta = g_dnn.view(B, 1)
-        for li in reversed(range(len(layers))):
-            L, a_in = layers[li], acts[li]
-            K_in, N_out = L.kernel.shape
-            dW, db = emp(K_in, N_out), emp(N_out)
-            call("rs_gemm", 1, 0, K_in, N_out, B, 1.0, ptr(a_in), a_in.stride(0), ptr(delta), delta.stride(0), 0.0,
-                 ptr(dW), N_out, None, 0, *gw, st)
-            call("rs_col_sum", ptr(delta), delta.stride(0), B, N_out, ptr(db), st)
-            grads.append((L, dW, db))
-            relu_below = li > 0 and layers[li - 1].activation == "relu"
-            prev = emp(B, K_in)
-            call("rs_gemm", 0, 1, B, K_in, N_out, 1.0, ptr(delta), delta.stride(0), ptr(L.kernel), N_out, 0.0,
-                 ptr(prev), K_in, ptr(a_in) if relu_below else None, a_in.stride(0), *gw, st)
-            delta = prev
+        grads, delta = _dnn_backward(layers, acts, g_dnn.view(B, 1), gw, emp, st)
         dx = delta  # [B, d]: the DNN's gradient w.r.t. x; the FM's is added next
         call("rs_fm_x_grad", ptr(x), d, ptr(s), ptr(fm.w1), ptr(fm.v), B, d, kfm, ptr(g_fm), ptr(dx), d, st)
         dw1, dv, dw0 = emp(d), emp(d, kfm), emp(1)
         call("rs_fm_param_grads", ptr(x), d, ptr(s), ptr(fm.v), B, d, kfm, ptr(g_fm), ptr(dw1), ptr(dv), ptr(dw0), st)
         # updates (every gradient above used the pre-step weights)
-        for L, dW, db in grads:
-            call("rs_sgd_update", ptr(L.kernel), ptr(dW), dW.numel(), float(lr), 0.0, st)
-            call("rs_sgd_update", ptr(L.bias), ptr(db), db.numel(), float(lr), 0.0, st)
+        _dnn_apply(grads, lr, st)
         call("rs_sgd_update", ptr(fm.w1), ptr(dw1), d, float(lr), float(fm.reg_w), st)
         call("rs_sgd_update", ptr(fm.v), ptr(dv), d * kfm, float(lr), float(fm.reg_b), st)
         call("rs_sgd_update", ptr(fm.w0), ptr(dw0), 1, float(lr), 0.0, st)
-        n = B * e.n_fields
-        ws_n = _lib.lib().rs_embedding_sgd_workspace_size(n)
-        ws = self.__dict__.get("_emb_ws")
-        if ws is None or ws.numel() < ws_n:
-            ws = self.__dict__["_emb_ws"] = torch.empty(ws_n, dtype=torch.uint8, device=dev)
-        call("rs_embedding_sgd", ptr(e.table), e.total_rows, e.k, ptr(ids), _lib.id_kind(ids), ids.stride(0),
-             ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, B, ptr(dx) + 4 * self.nd, d, float(lr), ptr(ws),
-             None, st)
+        _embedding_sgd(self, ids, dx, d, lr, st)
         self._weights_changed()  # packed operand images of the old weights are stale
         return loss
 
     def _gemm_ws(self, nbytes):
-        ws = self.__dict__.get("_gemm_wsbuf")
-        if ws is None or ws.numel() < max(nbytes, 1):
-            ws = self.__dict__["_gemm_wsbuf"] = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self._dev)
-        return ws
+        return _gemm_ws(self, nbytes)
 
     def _fused_rows(self):
         """Tower input permutation for the fused kernel: its LDS tile holds
@@ -332,6 +360,81 @@ class DCN(KerasModule):
         if check_ids:
             self._err.check("DCN")
         return out
+
+    def _invalidate(self):
+        self._fused_key = None
+
+    def train_step(self, inputs, labels, lr=0.01, return_loss=False, check_ids=True):
+        """One step of compile_fit on DCN (model/dcn.py:24-34, utils/compile_fit.py:
+        9-15): SGD(lr), binary cross-entropy on sigmoid(Dense1([CrossLayer(x) |
+        DNNLayer(x)])), CrossLayer's l2(reg_w) / l2(reg_b) regularisers
+        (layer/interaction.py:57-73), every weight updated in place from the
+        pre-step gradients.  The CrossNet runs as rs_cross_train_fwd (keeps
+        x_1..x_L and x_l . w_l) and rs_cross_train_bwd (delta_l recursion);
+        dw_l = x_l^T s_l and the Dense grads through rs_gemm, db_l / Dense
+        biases through rs_col_sum, the looked-up rows by rs_embedding_sgd.
+        DNNLayer's Dropout is the identity (rate 0): its masks are random
+        draws TF does not expose, so no dropout parity exists to test."""
+        dense, ids = _split_criteo(inputs, self.nd, self._dev)
+        labels = _to_device_f32(labels, self._dev).reshape(-1)
+        e, cl, dnn, out = self.embed_layer, self.cross_layer, self.dense_layer, self.output_layer
+        _check_train_tower("DCN", dnn)
+        B, d, dev, st = ids.shape[0], self.d, self._dev, _lib.stream()
+        od, Lc = dnn.output_layer.units, cl.layer_num
+        dz_n = d + od
+        emp = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=dev)
+        layers = list(dnn.hidden_layer) + [dnn.output_layer]
+        gws = _gemm_ws(self, max(_lib.lib().rs_gemm_workspace_size(K, N, B)
+                                 for K, N in [L.kernel.shape for L in layers] + [(d, 1), (dz_n, 1)]))
+        gw = (ptr(gws), gws.numel())
+        # forward, keeping what the backward needs
+        x = e.gather(ids, dense, check_ids=check_ids)
+        zc = emp(B, dz_n)  # [cross_out | dnn_out], the output Dense's input
+        W = torch.stack([w.reshape(-1) for w in cl.cross_weight]).contiguous() if Lc else None
+        Bc = torch.stack([b.reshape(-1) for b in cl.cross_bias]).contiguous() if Lc else None
+        xs, gl = (emp(Lc, B, d), emp(Lc, B)) if Lc else (None, None)
+        if Lc:
+            call("rs_cross_train_fwd", ptr(x), d, d, Lc, ptr(W), ptr(Bc), B, ptr(xs), ptr(gl), ptr(zc), dz_n, st)
+        else:
+            zc[:, :d].copy_(x)
+        acts = [x]
+        for layer in dnn.hidden_layer:
+            acts.append(layer(acts[-1]))
+        dnn.output_layer(acts[-1], out=zc[:, d:])
+        logit = emp(B)
+        call("rs_dense_fwd", ptr(zc), dz_n, ptr(out.kernel), ptr(out.bias), None, 0, ptr(logit), 1, B, dz_n, 1, st)
+        g, g0 = emp(B), emp(B)
+        loss = emp(B) if return_loss else None
+        call("rs_head_grad", ptr(logit), ptr(logit), ptr(labels), B, 1.0, 0.0, ptr(g), ptr(g0), ptr(loss), st)
+        # output Dense: dWo = zc^T g, dbo = sum g, dzc = g Wo^T
+        dWo, dbo, dzc = emp(dz_n, 1), emp(1), emp(B, dz_n)
+        call("rs_gemm", 1, 0, dz_n, 1, B, 1.0, ptr(zc), dz_n, ptr(g), 1, 0.0, ptr(dWo), 1, None, 0, *gw, st)
+        call("rs_col_sum", ptr(g), 1, B, 1, ptr(dbo), st)
+        call("rs_gemm", 0, 1, B, dz_n, 1, 1.0, ptr(g), 1, ptr(out.kernel), 1, 0.0, ptr(dzc), dz_n, None, 0, *gw, st)
+        # DNN backward from dzc[:, d:], then the CrossNet's from dzc[:, :d]
+        grads, dx = _dnn_backward(layers, acts, dzc[:, d:], gw, emp, st)
+        if Lc:
+            deltas, sl = emp(Lc, B, d), emp(Lc, B)
+        else:
+            deltas = sl = None
+        call("rs_cross_train_bwd", ptr(x), d, d, Lc, ptr(W), B, ptr(gl), ptr(dzc), dz_n, ptr(deltas), ptr(sl),
+             ptr(dx), d, st)
+        dWc, dBc = emp(max(Lc, 1), d), emp(max(Lc, 1), d)
+        for l in range(Lc):
+            xl = x if l == 0 else xs[l - 1]
+            call("rs_gemm", 1, 0, d, 1, B, 1.0, ptr(xl), d, ptr(sl[l]), 1, 0.0, ptr(dWc[l]), 1, None, 0, *gw, st)
+            call("rs_col_sum", ptr(deltas[l]), d, B, d, ptr(dBc[l]), st)
+        # updates
+        _dnn_apply(grads, lr, st)
+        call("rs_sgd_update", ptr(out.kernel), ptr(dWo), dz_n, float(lr), 0.0, st)
+        call("rs_sgd_update", ptr(out.bias), ptr(dbo), 1, float(lr), 0.0, st)
+        for l in range(Lc):
+            call("rs_sgd_update", ptr(cl.cross_weight[l]), ptr(dWc[l]), d, float(lr), float(cl.reg_w), st)
+            call("rs_sgd_update", ptr(cl.cross_bias[l]), ptr(dBc[l]), d, float(lr), float(cl.reg_b), st)
+        _embedding_sgd(self, ids, dx, d, lr, st)
+        self.__dict__["_keep"] = (W, Bc)  # stream-ordered lifetime of the stacked operands
+        self._weights_changed()
+        return loss
 
     # ---- one-launch forward (rs_dcn_fwd)
     def _fused_layers(self):

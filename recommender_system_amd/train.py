@@ -6,23 +6,24 @@ binary cross-entropy, ``epochs`` passes.  The data is the compact form of the
 reference's X (dataset.criteo_compact / an RSCB file): dense [N, nd], label
 codes [N, F], labels [N], per-field vocab.  Each batch is one
 ``model.train_step``: ``FM`` (rs_fm_train_step; the one-hot X of
-model/fm.py) or ``DeepFM`` (model/deepFM.py; dense + label-encoded X).
+model/fm.py), ``DeepFM`` (model/deepFM.py) or ``DCN`` (model/dcn.py) — the
+last two on dense + label-encoded X.
 """
 from __future__ import annotations
 
 import numpy as np
 import torch
 
-from .models import FM, DeepFM
+from .models import DCN, FM, DeepFM
 
 
 def compile_fit(model, dense, ids, labels, field_vocab=None, batch_size=32, epochs=10, sgd=0.01, device=None):
-    """Train ``model`` (models.FM or models.DeepFM) in place; returns the
+    """Train ``model`` (models.FM, models.DeepFM or models.DCN) in place; returns the
     per-epoch mean cross-entropy (before each step, without the l2 terms).
     ``field_vocab`` (feat_onehot_dim per field) is needed for FM's one-hot
-    layout; DeepFM reads it from its EmbedLayer."""
-    if not isinstance(model, (FM, DeepFM)):
-        raise NotImplementedError("compile_fit: FM and DeepFM have a training step in this build")
+    layout; DeepFM / DCN read it from their EmbedLayer."""
+    if not isinstance(model, (FM, DeepFM, DCN)):
+        raise NotImplementedError("compile_fit: FM, DeepFM and DCN have a training step in this build")
     dev = torch.device(device) if device is not None else model._dev
     dense = torch.as_tensor(np.asarray(dense, np.float32), device=dev)
     ids = torch.as_tensor(np.asarray(ids), device=dev)

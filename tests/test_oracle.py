@@ -212,3 +212,50 @@ def test_deepfm_train_step_gradient_matches_finite_differences():
         check(p["dnn_hidden"][li][1], new["dnn_hidden"][li][1], (1,))
     check(p["dnn_out"][0], new["dnn_out"][0], (2, 0))
     check(p["dnn_out"][1], new["dnn_out"][1], (0,))
+
+
+def test_dcn_train_step_gradient_matches_finite_differences():
+    """oracle.dcn_train_step's hand backprop (CrossNet delta recursion, DNN,
+    output Dense, embedding scatter-add) == central differences of
+    compile_fit's DCN objective with CrossLayer's l2 terms."""
+    rng = np.random.default_rng(13)
+    nd, k, L, od = 2, 3, 3, 2
+    vocab = [3, 2]
+    tables = [rng.normal(size=(v_, k)) * 0.5 for v_ in vocab]
+    d = nd + len(vocab) * k
+    p = {"tables": tables,
+         "cross_w": [rng.normal(size=(d, 1)) * 0.3 for _ in range(L)],
+         "cross_b": [rng.normal(size=(d, 1)) * 0.3 for _ in range(L)],
+         "dnn_hidden": [(rng.normal(size=(d, 5)), rng.normal(size=5) * 0.1)],
+         "dnn_out": (rng.normal(size=(5, od)), rng.normal(size=od) * 0.1),
+         "out_kernel": rng.normal(size=(d + od, 1)) * 0.3, "out_bias": np.array([0.05])}
+    dense = rng.random((4, nd))
+    ids = np.array([[0, 1], [2, 1], [0, 0], [1, 1]])
+    t = np.array([1.0, 0.0, 1.0, 0.0])
+    lr, rw, rb = 1.0, 1e-2, 3e-2
+    new, _ = O.dcn_train_step(dense, ids, t, p, lr, rw, rb, nd=nd)
+    eps = 1e-6
+
+    def check(arr, new_arr, idx):
+        keep = arr[idx]
+        arr[idx] = keep + eps
+        lp = O.dcn_loss(dense, ids, t, p, rw, rb, nd=nd)
+        arr[idx] = keep - eps
+        lm = O.dcn_loss(dense, ids, t, p, rw, rb, nd=nd)
+        arr[idx] = keep
+        assert abs((lp - lm) / (2 * eps) - (arr[idx] - new_arr[idx]) / lr) < 1e-6, idx
+
+    for idx in [(0, 0), (0, 2), (2, 1), (1, 0)]:
+        check(p["tables"][0], new["tables"][0], idx)
+    check(p["tables"][1], new["tables"][1], (1, 2))
+    for l in range(L):
+        for idx in [(0, 0), (4, 0), (7, 0)]:
+            check(p["cross_w"][l], new["cross_w"][l], idx)
+            check(p["cross_b"][l], new["cross_b"][l], idx)
+    check(p["dnn_hidden"][0][0], new["dnn_hidden"][0][0], (3, 2))
+    check(p["dnn_hidden"][0][1], new["dnn_hidden"][0][1], (1,))
+    check(p["dnn_out"][0], new["dnn_out"][0], (2, 1))
+    check(p["dnn_out"][1], new["dnn_out"][1], (0,))
+    for idx in [(0, 0), (5, 0), (9, 0)]:
+        check(p["out_kernel"], new["out_kernel"], idx)
+    check(p["out_bias"], new["out_bias"], (0,))

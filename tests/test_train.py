@@ -165,3 +165,89 @@ def test_compile_fit_deepfm_on_bundled_sample(gpu):
     m2 = rs.DeepFM(cols, 10, 1e-4, 1e-4, [64, 32], 1, "relu", seed=4)
     hist = compile_fit(m2, dense[:960], ids[:960], label[:960], batch_size=32, epochs=4, sgd=0.05)
     assert hist[-1] < hist[0]
+
+
+def _dcn_params(m):
+    from tests.helpers import dnn_params, tables_of
+    hid, out = dnn_params(m.dense_layer)
+    return {"tables": tables_of(m.embed_layer),
+            "cross_w": [w.detach().cpu().numpy() for w in m.cross_layer.cross_weight],
+            "cross_b": [b.detach().cpu().numpy() for b in m.cross_layer.cross_bias],
+            "dnn_hidden": hid, "dnn_out": out,
+            "out_kernel": m.output_layer.kernel.detach().cpu().numpy(),
+            "out_bias": m.output_layer.bias.detach().cpu().numpy()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,k,hidden,od,L,vmax,id_dtype", [(32, 8, [64, 32], 4, 3, 5, np.int32),
+                                                           (300, 16, [24], 1, 2, 50, np.int64),
+                                                           (7, 4, [], 2, 0, 3, np.int32)])
+def test_dcn_train_steps_match_oracle(gpu, B, k, hidden, od, L, vmax, id_dtype):
+    """DCN.train_step (rs_cross_train_fwd / _bwd, output Dense and DNN through
+    rs_gemm / rs_col_sum, CrossLayer l2, SGD, row-sparse embedding update) ==
+    the oracle's hand backprop (pinned by finite differences) over 3 steps;
+    the fused forward then runs on the trained weights."""
+    import recommender_system_amd as rs
+    from tests.helpers import criteo_columns
+    rng = np.random.default_rng(B + k + L)
+    vocab = rng.integers(1, vmax, 26)
+    m = rs.DCN(criteo_columns(vocab, embed_dim=k), hidden, od, "relu", layer_num=L, reg_w=1e-3, reg_b=2e-3,
+               embed_dim=k, seed=3)
+    with torch.no_grad():
+        m.embed_layer.table.mul_(10.0)
+        for l in m.dense_layer._layers():
+            l.bias.uniform_(-0.1, 0.1)
+        m.output_layer.bias.uniform_(-0.1, 0.1)
+    p = _dcn_params(m)
+    lr = 0.5
+    for step in range(3):
+        dense = rng.random((B, 13)).astype(np.float32)
+        ids = np.stack([rng.integers(0, v_, B) for v_ in vocab], 1).astype(id_dtype)
+        t = rng.integers(0, 2, B).astype(np.float32)
+        loss = m.train_step((dense, ids), t, lr=lr, return_loss=True)
+        p, ce = O.dcn_train_step(dense, ids, t, p, lr, 1e-3, 2e-3)
+        got = _dcn_params(m)
+        assert_scaled_close(loss, ce, what=f"step {step} loss")
+        for c in range(26):
+            assert_scaled_close(got["tables"][c], p["tables"][c], what=f"step {step} table {c}")
+        for l in range(L):
+            assert_scaled_close(got["cross_w"][l], p["cross_w"][l], what=f"step {step} w{l}")
+            assert_scaled_close(got["cross_b"][l], p["cross_b"][l], what=f"step {step} b{l}")
+        for li, ((W, b), (Wr, br)) in enumerate(zip(got["dnn_hidden"], p["dnn_hidden"])):
+            assert_scaled_close(W, Wr, what=f"step {step} W{li}")
+            assert_scaled_close(b, br, what=f"step {step} b{li}")
+        assert_scaled_close(got["dnn_out"][0], p["dnn_out"][0], what=f"step {step} dnn W_out")
+        assert_scaled_close(got["out_kernel"], p["out_kernel"], what=f"step {step} out kernel")
+        assert_scaled_close(got["out_bias"], p["out_bias"], what=f"step {step} out bias")
+    y = m((dense, ids))
+    assert_scaled_close(y, O.dcn(None, dict(p, act="relu"), inputs=(dense, ids))[0], what="forward after training")
+
+
+@pytest.mark.gpu
+def test_compile_fit_dcn_on_bundled_sample(gpu):
+    """compile_fit on DCN (model/dcn.py's __main__ flow, layer_num 3) over the
+    reference's bundled Criteo sample: the first 5 SGD steps equal the
+    oracle's, and the loss falls epoch over epoch."""
+    import os
+
+    import recommender_system_amd as rs
+    from recommender_system_amd.dataset import criteo_compact, features_dict
+    from recommender_system_amd.train import compile_fit
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "criteo_train_1w.txt.gz")
+    dense, ids, label, _ = criteo_compact(path)
+    cols = features_dict(path)
+    m = rs.DCN(cols, [64, 32], 1, "relu", 3, seed=5)
+    p = _dcn_params(m)
+    N = 160
+    compile_fit(m, dense[:N], ids[:N], label[:N], batch_size=32, epochs=1, sgd=0.01)
+    d32 = dense[:N].astype(np.float32)
+    for r0 in range(0, N, 32):
+        p, _ = O.dcn_train_step(d32[r0:r0 + 32], ids[r0:r0 + 32], label[r0:r0 + 32], p, 0.01, 1e-4, 1e-4)
+    got = _dcn_params(m)
+    for l in range(3):
+        assert_scaled_close(got["cross_w"][l], p["cross_w"][l], what=f"DCN compile_fit w{l}")
+    for c in (0, 7, 25):
+        assert_scaled_close(got["tables"][c], p["tables"][c], what=f"DCN compile_fit table {c}")
+    m2 = rs.DCN(cols, [64, 32], 1, "relu", 3, seed=5)
+    hist = compile_fit(m2, dense[:960], ids[:960], label[:960], batch_size=32, epochs=4, sgd=0.05)
+    assert hist[-1] < hist[0]
