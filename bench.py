@@ -437,6 +437,14 @@ def bench_sharded(args, world, rank, vocabs, dense_pool):
     fl = sh.ops.flags(sh._bufs(B))
     dist.all_reduce(fl, op=dist.ReduceOp.MAX)
     bufs = sh._bufs(B)
+    # data-parallel training step on the sharded table (sharded.py train_step)
+    labels = (torch.rand(npool, B, generator=g, device=dev) < 0.25).to(torch.float32)
+
+    def train(i):
+        j = i % npool
+        sh.train_step(dense_pool[j], ids_pool[j], labels[j], lr=0.01, check=False)
+
+    tdt, tstep_ms, ttiming = run(train)
     S, P = sh.slot_stride, sh.partial_width
     res = {"exchange": {
         "protocol": "owner-side FM partials, pipelined: ONE RCCL all-to-all of [row ids of t | FM partials of "
@@ -453,7 +461,12 @@ def bench_sharded(args, world, rank, vocabs, dense_pool):
                           "timing": rtiming, "slots_per_peer": bufs["cap"],
                           "row_bytes_per_rank_each_way": world * bufs["cap"] * k * 4,
                           "overflow_during_timing": bool(fl[1].item()),
-                          "note": "fixed-capacity row exchange (forward_slots): rows back to the requester"}}}
+                          "note": "fixed-capacity row exchange (forward_slots): rows back to the requester"}},
+           "sharded_train_step": {"samples_per_s": world * args.steps * B / tdt, "ms_per_step": tdt / args.steps * 1e3,
+                          "timing": ttiming,
+                          "note": "ShardedEmbeddingFM.train_step: partial-protocol forward (2 all-to-alls) + "
+                                  "combine_grad, all-gather of [s | g] records, owner row grads + row-sparse SGD "
+                                  "of the shard, all-reduce of the FM parameter grads, SGD + l2"}}
     res["value"] = world * args.steps * B / dt
     res["ms_per_step"] = dt / args.steps * 1e3
     alg = B * 1824 + 18880
@@ -930,7 +943,7 @@ def main():
                        "ids": "int32 uniform per field", "parallelism": f"dp{world}" + ("+rowshard" if world > 1 or args.sharded else "")},
             "roofline": res["roofline"], "cpu_baseline": res["cpu_baseline"],
         }
-        for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "exchange"):
+        for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "exchange", "sharded_train_step"):
             if key in res:
                 line[key] = res[key]
         print(json.dumps(line), flush=True)

@@ -417,6 +417,13 @@ int rs_fm_param_grads(const float* x, int64_t ldx, const float* s,
                       const float* v, int64_t batch, int d, int kfm,
                       const float* g, float* dw1, float* dv, float* dw0,
                       rs_stream_t stream);
+/* rs_fm_param_grads with s rows lds floats apart and g ldg floats apart
+ * (the sharded backward's interleaved [s | g] records); dw0 NULL = skip.   */
+int rs_fm_param_grads_strided(const float* x, int64_t ldx, const float* s,
+                              int64_t lds, const float* g, int64_t ldg,
+                              const float* v, int64_t batch, int d, int kfm,
+                              float* dw1, float* dv, float* dw0,
+                              rs_stream_t stream);
 /* CrossNet training (layer/interaction.py:75-83, DCN.train_step):
  * rs_cross_train_fwd: x_{l+1} = x0 (x_l . w_l) + b_l + x_l for l < L;
  *  W, b [L, d] (row l = w_l, b_l); keeps xs [L, B, d] (x_1 .. x_L) and
@@ -536,6 +543,37 @@ int rs_shard_fm_combine(const float* partials, int64_t partial_stride,
                         int n_fields, int k, const float* prepared,
                         const float* w0, int kfm, float* logit,
                         rs_stream_t stream);
+
+/* Sharded FM training (sharded.py ShardedEmbeddingFM.train_step;
+ * utils/compile_fit.py:9-15 on the FM logit, data parallel over the ranks):
+ *  rs_shard_fm_combine_grad: rs_shard_fm_combine that also writes, per
+ *   sample, the record gs[b] = [s_0 .. s_{kfm-1} | g] (gs_stride floats
+ *   apart; s = x @ v over the whole sample, g = (sigmoid(logit) - label) *
+ *   grad_scale, grad_scale = 1 / global batch) and the BCE loss (optional).
+ *  rs_shard_owner_fm_grad: owner side of the backward.  recv = the forward's
+ *   received row-id records (n_pairs of rec_stride words, requester-major),
+ *   gs = every requester's [s | g] records in the same pair order (an
+ *   all-gather).  For the owned fields field_lo .. +n_owned: rows_ws [n_pairs,
+ *   n_owned*k] = the rows (absent -> 0); drows [n_pairs, n_owned*k] =
+ *   dL/drow = g (w1_e + v_e . s - x_e |v_e|^2); dw1 [n_owned*k] and dv
+ *   [n_owned*k, kfm] = this owner's part of the FM parameter gradients of
+ *   those columns (fixed-order trees; summed over owners by an all-reduce).
+ *   w1 / v are the WHOLE model's [d, 1] / [d, kfm].  The row update is then
+ *   rs_embedding_sgd on recv (ids = local rows, -1 skipped) and drows.     */
+int rs_shard_fm_combine_grad(const float* partials, int64_t partial_stride,
+                             int world, int64_t batch, const float* dense,
+                             int64_t dense_stride, int nd, int n_fields, int k,
+                             const float* prepared, const float* w0, int kfm,
+                             const float* labels, float grad_scale,
+                             float* logit, float* gs, int64_t gs_stride,
+                             float* loss, rs_stream_t stream);
+int rs_shard_owner_fm_grad(const int32_t* recv, int64_t rec_stride,
+                           int field_lo, int n_owned, const float* shard,
+                           int64_t shard_rows, int nd, int k, const float* w1,
+                           const float* v, int kfm, const float* gs,
+                           int64_t gs_stride, int64_t n_pairs, float* rows_ws,
+                           float* drows, float* dw1, float* dv,
+                           rs_stream_t stream);
 
 /* One launch per pipelined step (sharded.py pipe_step), run after the
  * step's all-to-all: the owner part of batch t on recv's row-id words

@@ -641,3 +641,42 @@ def dcn_loss(dense, ids, t, p, reg_w, reg_b, nd=13, dt=np.float64):
     ce = np.maximum(logit, 0) - logit * t + np.log1p(np.exp(-np.abs(logit)))
     return np.mean(ce) + reg_w * sum(np.sum(np.asarray(w, dt) ** 2) for w in p["cross_w"]) + \
         reg_b * sum(np.sum(np.asarray(b, dt) ** 2) for b in p["cross_b"])
+
+
+def embed_fm_train_step(dense, ids, t, p, lr, l2_w, l2_v, nd=13, dt=np.float64):
+    """One SGD step of compile_fit (utils/compile_fit.py:9-15) on
+    sigmoid(FMLayer([dense | EmbedLayer(ids)])) — DeepFM's FM half
+    (model/deepFM.py:23-31 without the DNN), the objective the row-sharded
+    trainer (sharded.py train_step) optimises over its global batch:
+    g = (sigmoid(fm) - t)/B; dx = g (w1 + v s - x |v|^2); dw1 = x^T g,
+    dv = x^T (g s) - (x^2)^T g * v (+ 2 l2 terms), dw0 = sum g; rows by
+    scatter-add.  p: {"tables", "w0", "w1", "v"}.  Returns (new p, losses)."""
+    dense = np.asarray(dense, dt)
+    ids = cast_ids(ids)
+    t = np.asarray(t, dt)
+    tables = [np.array(tb, dt) for tb in p["tables"]]
+    k = tables[0].shape[1]
+    x = np.concatenate([dense, embed_layer(ids, tables, dt)], axis=1)
+    w0, w1, v = (np.array(p[n], dt) for n in ("w0", "w1", "v"))
+    z = fm_layer(x, w0, w1, v, dt)[:, 0]
+    loss = np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z)))
+    g = (sigmoid(z) - t) / x.shape[0]
+    s = x @ v
+    dx = g[:, None] * (w1[:, 0][None, :] + s @ v.T - x * np.sum(v * v, axis=1)[None, :])
+    dw1 = x.T @ g[:, None]
+    dv = x.T @ (g[:, None] * s) - ((x * x).T @ g)[:, None] * v
+    out = {"w0": w0 - lr * g.sum(keepdims=True), "w1": w1 - lr * (dw1 + 2 * l2_w * w1),
+           "v": v - lr * (dv + 2 * l2_v * v)}
+    for c, tb in enumerate(tables):
+        np.add.at(tb, ids[:, c], -lr * dx[:, nd + c * k: nd + (c + 1) * k])
+    out["tables"] = tables
+    return out, loss
+
+
+def embed_fm_loss(dense, ids, t, p, l2_w, l2_v, nd=13, dt=np.float64):
+    """Objective of embed_fm_train_step: mean BCE + l2_w |w1|^2 + l2_v |v|^2."""
+    x = np.concatenate([np.asarray(dense, dt), embed_layer(ids, p["tables"], dt)], axis=1)
+    z = fm_layer(x, p["w0"], p["w1"], p["v"], dt)[:, 0]
+    t = np.asarray(t, dt)
+    ce = np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z)))
+    return np.mean(ce) + l2_w * np.sum(np.asarray(p["w1"], dt) ** 2) + l2_v * np.sum(np.asarray(p["v"], dt) ** 2)

@@ -77,6 +77,9 @@ SIGNATURES = {
     "rs_head_grad": (I, [P, P, P, L, F, F, P, P, P, P]),
     "rs_fm_x_grad": (I, [P, L, P, P, P, L, I, I, P, P, L, P]),
     "rs_fm_param_grads": (I, [P, L, P, P, L, I, I, P, P, P, P, P]),
+    "rs_fm_param_grads_strided": (I, [P, L, P, L, P, L, P, L, I, I, P, P, P, P]),
+    "rs_shard_fm_combine_grad": (I, [P, L, I, L, P, L, I, I, I, P, P, I, P, F, P, P, L, P, P]),
+    "rs_shard_owner_fm_grad": (I, [P, L, I, I, P, L, I, I, P, P, I, P, L, L, P, P, P, P, P]),
     "rs_cross_train_fwd": (I, [P, L, I, I, P, P, L, P, P, P, L, P]),
     "rs_cross_train_bwd": (I, [P, L, I, I, P, L, P, P, L, P, P, P, L, P]),
     "rs_embedding_sgd_workspace_size": (L, [L]),

@@ -143,13 +143,16 @@ __global__ __launch_bounds__(256) void head_grad_kernel(const float* __restrict_
   if (loss) loss[b] = fmaxf(z, 0.f) - z * t[b] + log1pf(expf(-fabsf(z)));
 }
 
-// FM gradient w.r.t. x, accumulated: dx[b,i] += g_b (w1_i + sum_f v_if s_bf
-// - x_bi sum_f v_if^2); one thread per (b, i).
+// FM gradient w.r.t. x: dx[b,i] (+)= g_b (w1_i + sum_f v_if s_bf - x_bi
+// sum_f v_if^2); one thread per (b, i).  s rows lds apart, g ldg apart
+// (the sharded backward reads both out of interleaved [s | g] records);
+// ACC: accumulate into dx, else store.
+template <bool ACC>
 __global__ __launch_bounds__(256) void fm_x_grad_kernel(const float* __restrict__ x, int64_t ldx,
-                                                        const float* __restrict__ s, const float* __restrict__ w1,
-                                                        const float* __restrict__ v, int64_t B, int d, int kfm,
-                                                        const float* __restrict__ g, float* __restrict__ dx,
-                                                        int64_t lddx) {
+                                                        const float* __restrict__ s, int64_t lds,
+                                                        const float* __restrict__ w1, const float* __restrict__ v,
+                                                        int64_t B, int d, int kfm, const float* __restrict__ g,
+                                                        int64_t ldg, float* __restrict__ dx, int64_t lddx) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= B * d) return;
   const int64_t b = idx / d;
@@ -157,34 +160,37 @@ __global__ __launch_bounds__(256) void fm_x_grad_kernel(const float* __restrict_
   float vs = 0.f, vv = 0.f;
   for (int f = 0; f < kfm; ++f) {
     const float vf = v[(int64_t)i * kfm + f];
-    vs = fmaf(vf, s[b * kfm + f], vs);
+    vs = fmaf(vf, s[b * lds + f], vs);
     vv = fmaf(vf, vf, vv);
   }
-  dx[b * lddx + i] += g[b] * ((w1[i] + vs) - x[b * ldx + i] * vv);
+  const float r = g[b * ldg] * ((w1[i] + vs) - x[b * ldx + i] * vv);
+  if (ACC) dx[b * lddx + i] += r;
+  else dx[b * lddx + i] = r;
 }
 
 // FM parameter gradients (without the l2 terms): one block per feature i,
 // fixed-shape trees over the batch:
 //   dw1_i = sum_b g_b x_bi,  dv_if = sum_b g_b x_bi s_bf - (sum_b g_b x_bi^2) v_if;
-// block d computes dw0 = sum_b g_b.
+// block d computes dw0 = sum_b g_b (when dw0 is given).
 __global__ __launch_bounds__(256) void fm_param_grad_kernel(const float* __restrict__ x, int64_t ldx,
-                                                            const float* __restrict__ s,
+                                                            const float* __restrict__ s, int64_t lds,
                                                             const float* __restrict__ v, int64_t B, int d, int kfm,
-                                                            const float* __restrict__ g, float* __restrict__ dw1,
-                                                            float* __restrict__ dv, float* __restrict__ dw0) {
+                                                            const float* __restrict__ g, int64_t ldg,
+                                                            float* __restrict__ dw1, float* __restrict__ dv,
+                                                            float* __restrict__ dw0) {
   __shared__ float red[34][256];
   const int i = blockIdx.x;
   const int NQ = kfm + 2;  // [x s_0 .. x s_{kfm-1} | x | x^2] weighted by g
   float acc[34];
   for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
   for (int64_t b = threadIdx.x; b < B; b += 256) {
-    const float gb = g[b];
+    const float gb = g[b * ldg];
     if (i == d) {
       acc[0] += gb;
       continue;
     }
     const float xg = gb * x[b * ldx + i];
-    for (int f = 0; f < kfm; ++f) acc[f] = fmaf(xg, s[b * kfm + f], acc[f]);
+    for (int f = 0; f < kfm; ++f) acc[f] = fmaf(xg, s[b * lds + f], acc[f]);
     acc[kfm] += xg;
     acc[kfm + 1] = fmaf(xg, x[b * ldx + i], acc[kfm + 1]);
   }
@@ -204,6 +210,21 @@ __global__ __launch_bounds__(256) void fm_param_grad_kernel(const float* __restr
     dv[(int64_t)i * kfm + f] = red[f][0] - red[kfm + 1][0] * v[(int64_t)i * kfm + f];
   }
   if (threadIdx.x == 0) dw1[i] = red[kfm][0];
+}
+
+// Sharded FM backward, owner side: x rows of the owned slots of every
+// (requester, sample) record, [n_pairs][n_owned * k] (absent slot -> 0).
+__global__ __launch_bounds__(256) void owner_rows_kernel(const int32_t* __restrict__ recv, int64_t rec, int n_owned,
+                                                         const float* __restrict__ shard, int64_t shard_rows, int k,
+                                                         int64_t n_pairs, float* __restrict__ xo) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t w = (int64_t)n_owned * k;
+  if (idx >= n_pairs * w) return;
+  const int64_t p = idx / w;
+  const int e = (int)(idx - p * w);
+  const int u = e / k;
+  const int64_t r = recv[p * rec + u];
+  xo[idx] = (r >= 0 && r < shard_rows) ? shard[r * k + (e - u * k)] : 0.f;
 }
 
 // ------------------------------------------- row-sparse SGD of the tables
@@ -431,8 +452,8 @@ extern "C" int rs_fm_x_grad(const float* x, int64_t ldx, const float* s, const f
   if (batch == 0) return RS_OK;
   RS_REQUIRE(x && s && w1 && v && g && dx && batch > 0 && d > 0 && kfm >= 1 && ldx >= d && lddx >= d,
              "rs_fm_x_grad: bad arguments");
-  fm_x_grad_kernel<<<(unsigned)((batch * d + 255) / 256), 256, 0, as_stream(stream)>>>(x, ldx, s, w1, v, batch, d,
-                                                                                       kfm, g, dx, lddx);
+  fm_x_grad_kernel<true><<<(unsigned)((batch * d + 255) / 256), 256, 0, as_stream(stream)>>>(
+      x, ldx, s, kfm, w1, v, batch, d, kfm, g, 1, dx, lddx);
   return launch_status("rs_fm_x_grad");
 }
 
@@ -440,9 +461,42 @@ extern "C" int rs_fm_param_grads(const float* x, int64_t ldx, const float* s, co
                                  int kfm, const float* g, float* dw1, float* dv, float* dw0, rs_stream_t stream) {
   RS_REQUIRE(x && s && v && g && dw1 && dv && dw0 && batch >= 0 && d > 0 && kfm >= 1 && kfm <= 32 && ldx >= d,
              "rs_fm_param_grads: bad arguments (kfm <= 32)");
-  fm_param_grad_kernel<<<(unsigned)(d + 1), 256, 0, as_stream(stream)>>>(x, ldx, s, v, batch, d, kfm, g, dw1, dv,
-                                                                          dw0);
+  fm_param_grad_kernel<<<(unsigned)(d + 1), 256, 0, as_stream(stream)>>>(x, ldx, s, kfm, v, batch, d, kfm, g, 1,
+                                                                          dw1, dv, dw0);
   return launch_status("rs_fm_param_grads");
+}
+
+extern "C" int rs_fm_param_grads_strided(const float* x, int64_t ldx, const float* s, int64_t lds, const float* g,
+                                         int64_t ldg, const float* v, int64_t batch, int d, int kfm, float* dw1,
+                                         float* dv, float* dw0, rs_stream_t stream) {
+  if (d == 0 && !dw0) return RS_OK;
+  RS_REQUIRE((x || d == 0) && s && v && g && dw1 && dv && batch >= 0 && d >= 0 && kfm >= 1 && kfm <= 32 &&
+                 ldx >= d && lds >= kfm && ldg >= 1,
+             "rs_fm_param_grads_strided: bad arguments (kfm <= 32)");
+  fm_param_grad_kernel<<<(unsigned)(d + (dw0 ? 1 : 0)), 256, 0, as_stream(stream)>>>(x, ldx, s, lds, v, batch, d, kfm,
+                                                                                     g, ldg, dw1, dv, dw0);
+  return launch_status("rs_fm_param_grads_strided");
+}
+
+extern "C" int rs_shard_owner_fm_grad(const int32_t* recv, int64_t rec_stride, int field_lo, int n_owned,
+                                      const float* shard, int64_t shard_rows, int nd, int k, const float* w1,
+                                      const float* v, int kfm, const float* gs, int64_t gs_stride, int64_t n_pairs,
+                                      float* rows_ws, float* drows, float* dw1, float* dv, rs_stream_t stream) {
+  if (n_pairs == 0 || n_owned == 0) return RS_OK;
+  RS_REQUIRE(recv && shard && w1 && v && gs && rows_ws && drows && dw1 && dv, "rs_shard_owner_fm_grad: null pointer");
+  RS_REQUIRE(n_pairs > 0 && n_owned > 0 && rec_stride >= n_owned && field_lo >= 0 && nd >= 0 && k >= 1 &&
+                 kfm >= 1 && kfm <= 32 && gs_stride >= kfm + 1 && shard_rows >= 0,
+             "rs_shard_owner_fm_grad: bad shape (kfm <= 32)");
+  hipStream_t st = as_stream(stream);
+  const int w = n_owned * k;
+  const int64_t col = nd + (int64_t)field_lo * k;  // first FM feature of the owned fields
+  owner_rows_kernel<<<(unsigned)((n_pairs * w + 255) / 256), 256, 0, st>>>(recv, rec_stride, n_owned, shard,
+                                                                             shard_rows, k, n_pairs, rows_ws);
+  fm_x_grad_kernel<false><<<(unsigned)((n_pairs * w + 255) / 256), 256, 0, st>>>(
+      rows_ws, w, gs, gs_stride, w1 + col, v + col * kfm, n_pairs, w, kfm, gs + kfm, gs_stride, drows, w);
+  fm_param_grad_kernel<<<(unsigned)w, 256, 0, st>>>(rows_ws, w, gs, gs_stride, v + col * kfm, n_pairs, w, kfm,
+                                                    gs + kfm, gs_stride, dw1, dv, nullptr);
+  return launch_status("rs_shard_owner_fm_grad");
 }
 
 static int64_t emb_sort_bytes(int64_t n) {

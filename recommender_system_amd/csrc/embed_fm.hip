@@ -517,6 +517,13 @@ struct CombineArgs {
   const float* w0;
   int kfm;
   float* logit;
+  // training (rs_shard_fm_combine_grad): [s_0..s_{kfm-1} | g] records gst
+  // floats apart, g = (sigmoid(logit) - label) * gscale; per-sample BCE
+  const float* labels;
+  float gscale;
+  float* gs;
+  int64_t gst;
+  float* loss;
 };
 
 // 16 lanes per sample (lane = partial column, strided by 16), DPP row sums;
@@ -536,14 +543,24 @@ __device__ __forceinline__ void fm_combine_part(const CombineArgs& c, int blk, i
         if (col <= c.kfm) acc = fmaf(x, rec[(col >> 4) * 64 + (e & 3) * 16 + (col & 15)], acc);
         else acc = fmaf(x * x, rec[c.NT * 64 + (e & 3)], acc);
       }
-      if (col < c.kfm) t = fmaf(acc, acc, t);
-      else if (col == c.kfm) lin = acc;
+      if (col < c.kfm) {
+        t = fmaf(acc, acc, t);
+        if (c.gs) c.gs[b * c.gst + col] = acc;
+      } else if (col == c.kfm) lin = acc;
       else q = acc;
     }
     t = row16_sum(t);
     lin = row16_sum(lin);
     q = row16_sum(q);
-    if (cl == 0) c.logit[b] = (lin + c.w0[0]) + 0.5f * (t - q);
+    if (cl == 0) {
+      const float z = (lin + c.w0[0]) + 0.5f * (t - q);
+      c.logit[b] = z;
+      if (c.gs) {
+        const float y = c.labels[b];
+        c.gs[b * c.gst + c.kfm] = (sigmoidf_(z) - y) * c.gscale;
+        if (c.loss) c.loss[b] = fmaxf(z, 0.f) - z * y + log1pf(expf(-fabsf(z)));
+      }
+    }
   }
 }
 
@@ -1073,6 +1090,27 @@ extern "C" int rs_shard_fm_combine(const float* partials, int64_t partial_stride
                     w0, kfm, logit};
   launch_pipe(a, p, g, as_stream(stream));
   return launch_status("rs_shard_fm_combine");
+}
+
+extern "C" int rs_shard_fm_combine_grad(const float* partials, int64_t partial_stride, int world, int64_t batch,
+                                        const float* dense, int64_t dense_stride, int nd, int n_fields, int k,
+                                        const float* prepared, const float* w0, int kfm, const float* labels,
+                                        float grad_scale, float* logit, float* gs, int64_t gs_stride, float* loss,
+                                        rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(batch > 0 && world >= 1 && nd >= 0 && n_fields >= 0 && kfm >= 1 && gs_stride >= kfm + 1,
+             "rs_shard_fm_combine_grad: bad shape");
+  RS_REQUIRE(partials && prepared && w0 && logit && labels && gs && (nd == 0 || dense),
+             "rs_shard_fm_combine_grad: null pointer");
+  RS_PIPE_GEOM("rs_shard_fm_combine_grad");
+  RS_REQUIRE(partial_stride >= pw, "rs_shard_fm_combine_grad: partial_stride < rs_fm_partial_width");
+  EmbedFmArgs a{};
+  PipeArgs p{};
+  p.combine_blocks = 1;
+  p.c = CombineArgs{partials, partial_stride, world, batch, dense, dense_stride, nd, prepared, g.dense_rec, g.NT,
+                    w0, kfm, logit, labels, grad_scale, gs, gs_stride, loss};
+  launch_pipe(a, p, g, as_stream(stream));
+  return launch_status("rs_shard_fm_combine_grad");
 }
 
 extern "C" int rs_shard_fm_pipe(const int32_t* recv, int field_lo, int n_owned, const float* shard,

@@ -157,6 +157,43 @@ class HipShardOps:
              ptr(sh.owner_fields), sh.slot_stride, ptr(send), sh.world, B, sh.nd, sh.F, sh.k, ptr(sh.prepared),
              ptr(sh.w0), sh.kfm, ptr(self.err), _lib.stream())
 
+    # -- training (ShardedEmbeddingFM.train_step)
+    def combine_grad(self, sh, partials, dense, labels, scale, logit, gs, loss=None):
+        B = dense.shape[0]
+        call("rs_shard_fm_combine_grad", ptr(partials), sh.partial_width, sh.world, B, ptr(dense), dense.stride(0),
+             dense.shape[1], sh.F, sh.k, ptr(sh.prepared), ptr(sh.w0), sh.kfm, ptr(labels), float(scale), ptr(logit),
+             ptr(gs), gs.stride(0), ptr(loss), _lib.stream())
+
+    def dense_grads(self, sh, dense, gs, grad):
+        """The requester's FM parameter gradients: dense columns + dw0."""
+        d, kfm, nd = sh.d, sh.kfm, sh.nd
+        call("rs_fm_param_grads_strided", ptr(dense) if nd else None, dense.stride(0), ptr(gs), gs.stride(0),
+             ptr(gs) + 4 * kfm, gs.stride(0), ptr(sh.v), dense.shape[0], nd, kfm, ptr(grad), ptr(grad) + 4 * d,
+             ptr(grad) + 4 * d * (1 + kfm), _lib.stream())
+
+    def owner_grads(self, sh, recv, gs_all, grad, lr, bufs):
+        """Owner side: dL/drow of every owned lookup, this owner's part of the
+        FM parameter gradients over its columns, and the row SGD."""
+        lo, n_own = sh.owner_field_ranges[sh.rank]
+        if n_own == 0:
+            return
+        n_pairs = gs_all.shape[0]
+        d, kfm, k, S = sh.d, sh.kfm, sh.k, sh.slot_stride
+        col = sh.nd + lo * k
+        call("rs_shard_owner_fm_grad", ptr(recv), S, lo, n_own, ptr(sh.table_shard), sh.table_shard.shape[0], sh.nd,
+             k, ptr(sh.w1), ptr(sh.v), kfm, ptr(gs_all), gs_all.stride(0), n_pairs, ptr(bufs["xo"]),
+             ptr(bufs["drows"]), ptr(grad) + 4 * col, ptr(grad) + 4 * (d + col * kfm), _lib.stream())
+        call("rs_embedding_sgd", ptr(sh.table_shard), sh.table_shard.shape[0], k, ptr(recv), _lib.ID_I32, S,
+             ptr(bufs["zoff"]), ptr(bufs["svocab"]), n_own, n_pairs, ptr(bufs["drows"]), n_own * k, float(lr),
+             ptr(bufs["ws"]), None, _lib.stream())
+
+    def apply(self, sh, grad, lr, reg_w, reg_v):
+        d, kfm, st = sh.d, sh.kfm, _lib.stream()
+        call("rs_sgd_update", ptr(sh.w1), ptr(grad), d, float(lr), float(reg_w), st)
+        call("rs_sgd_update", ptr(sh.v), ptr(grad) + 4 * d, d * kfm, float(lr), float(reg_v), st)
+        call("rs_sgd_update", ptr(sh.w0), ptr(grad) + 4 * d * (1 + kfm), 1, float(lr), 0.0, st)
+        sh.prepare()
+
     def bad_flag(self):
         """[out-of-range id seen] (device tensor; resets)."""
         v = self.err.clamp(max=1)
@@ -225,7 +262,8 @@ class ShardedEmbeddingFM:
 
     def prepare(self):
         n = _lib.lib().rs_fm_prepared_size(self.nd, self.F, self.k, self.kfm)
-        self.prepared = torch.empty(n, dtype=torch.float32, device=self.device)
+        if self.prepared is None or self.prepared.numel() != n:
+            self.prepared = torch.empty(n, dtype=torch.float32, device=self.device)
         call("rs_fm_prepare", ptr(self.w1), ptr(self.v), self.nd, self.F, self.k, self.kfm, ptr(self.prepared),
              _lib.stream())
 
@@ -274,6 +312,84 @@ class ShardedEmbeddingFM:
             if bool(f.item()):
                 raise IndexError("sharded lookup: embedding id out of range")
         return logit
+
+    # -- training: compile_fit's SGD on the FM logit, data parallel
+    @property
+    def d(self):
+        return self.nd + self.F * self.k
+
+    def _tbufs(self, B):
+        tb = getattr(self, "_train_bufs", None)
+        if tb is None or tb["B"] != B:
+            W, dev, kfm, k = self.world, self.device, self.kfm, self.k
+            lo, n_own = self.owner_field_ranges[self.rank]
+            n_pairs = W * B
+            tb = {"B": B,
+                  "gs": torch.empty(B, kfm + 1, dtype=torch.float32, device=dev),
+                  "gs_all": torch.empty(n_pairs, kfm + 1, dtype=torch.float32, device=dev),
+                  "grad": torch.empty(self.d * (kfm + 1) + 1, dtype=torch.float32, device=dev),
+                  "logit": torch.empty(B, 1, dtype=torch.float32, device=dev),
+                  "xo": torch.empty(n_pairs, max(n_own, 1) * k, dtype=torch.float32, device=dev),
+                  "drows": torch.empty(n_pairs, max(n_own, 1) * k, dtype=torch.float32, device=dev),
+                  "zoff": torch.zeros(max(n_own, 1), dtype=torch.int64, device=dev),
+                  "svocab": torch.full((max(n_own, 1),), self.table_shard.shape[0], dtype=torch.int64, device=dev),
+                  "ws": torch.empty(max(_lib.lib().rs_embedding_sgd_workspace_size(n_pairs * max(n_own, 1))
+                                        if isinstance(self.ops, HipShardOps) else 1, 1),
+                                    dtype=torch.uint8, device=dev)}
+            self._train_bufs = tb
+        return tb
+
+    def train_step(self, dense, ids, labels, lr=0.01, reg_w=1e-4, reg_v=1e-4, return_loss=False, check=True):
+        """One SGD step of compile_fit (utils/compile_fit.py:9-15: SGD(lr),
+        binary cross-entropy on sigmoid(FM logit), FMLayer's l2(reg_w) / l2(reg_v)
+        on w1 / v — layer/interaction.py:94-104) over the GLOBAL batch (every
+        rank's B samples; g scaled by 1 / (world * B)), as data-parallel
+        training with the table row-sharded:
+          forward  (the partial protocol, ``forward``) + rs_shard_fm_combine_grad
+                   -> logit and each sample's [s | g] record
+          all_gather([s | g])        -> every requester's records at every owner (RCCL)
+          rs_fm_param_grads_strided  -> dense columns' dw1 / dv, dw0 (requester)
+          rs_shard_owner_fm_grad     -> dL/drow of my owned lookups + my part of
+                                        dw1 / dv over my fields' columns
+          rs_embedding_sgd           -> row-sparse SGD of my shard (duplicates
+                                        summed in global lookup order)
+          all_reduce(dw1, dv, dw0)   -> replicated FM parameters stay identical (RCCL)
+          rs_sgd_update x3, rs_fm_prepare
+        Every gradient comes from the pre-step weights.  Returns the per-sample
+        losses of the local batch (before the step) if ``return_loss``."""
+        B = ids.shape[0]
+        W = self.world
+        pb, tb = self._pbufs(B), self._tbufs(B)
+        exchange = W > 1 or self._force_exchange
+        send = self.ops.field_route(self, ids, pb["send"])
+        recv = send
+        if exchange:
+            recv = pb["recv"]
+            dist.all_to_all_single(recv, send, group=self.group)
+        part = self.ops.owner_partials(self, recv, W * B, pb["pout"])
+        if exchange:
+            dist.all_to_all_single(pb["pin"], part, group=self.group)
+            part = pb["pin"]
+        loss = torch.empty(B, dtype=torch.float32, device=self.device) if return_loss else None
+        self.ops.combine_grad(self, part, dense, labels, 1.0 / (W * B), tb["logit"], tb["gs"], loss)
+        gs_all = tb["gs"]
+        if exchange:
+            gs_all = tb["gs_all"]
+            dist.all_gather_into_tensor(gs_all, tb["gs"], group=self.group)
+        grad = tb["grad"]
+        grad.zero_()
+        self.ops.dense_grads(self, dense, tb["gs"], grad)
+        self.ops.owner_grads(self, recv, gs_all, grad, lr, tb)
+        if W > 1:
+            dist.all_reduce(grad, group=self.group)
+        self.ops.apply(self, grad, lr, reg_w, reg_v)
+        if check:
+            f = self.ops.bad_flag()
+            if W > 1:
+                dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
+            if bool(f.item()):
+                raise IndexError("sharded lookup: embedding id out of range")
+        return loss
 
     # -- the pipelined partial protocol: one all-to-all per batch
     def _sbufs(self, B):

@@ -259,3 +259,37 @@ def test_dcn_train_step_gradient_matches_finite_differences():
     for idx in [(0, 0), (5, 0), (9, 0)]:
         check(p["out_kernel"], new["out_kernel"], idx)
     check(p["out_bias"], new["out_bias"], (0,))
+
+
+def test_embed_fm_train_step_gradient_matches_finite_differences():
+    """oracle.embed_fm_train_step (the sharded trainer's objective) == central
+    differences of its loss, for rows (one repeated), w0, w1, v."""
+    rng = np.random.default_rng(14)
+    nd, k, kfm = 2, 3, 2
+    tables = [rng.normal(size=(v_, k)) * 0.5 for v_ in (3, 2)]
+    d = nd + 2 * k
+    p = {"tables": tables, "w0": np.array([0.1]), "w1": rng.normal(size=(d, 1)), "v": rng.normal(size=(d, kfm))}
+    dense = rng.random((4, nd))
+    ids = np.array([[0, 1], [2, 1], [0, 0], [1, 1]])
+    t = np.array([1.0, 0.0, 1.0, 0.0])
+    lr, l2w, l2v = 1.0, 1e-2, 3e-2
+    new, _ = O.embed_fm_train_step(dense, ids, t, p, lr, l2w, l2v, nd=nd)
+    eps = 1e-6
+
+    def check(arr, new_arr, idx):
+        keep = arr[idx]
+        arr[idx] = keep + eps
+        lp = O.embed_fm_loss(dense, ids, t, p, l2w, l2v, nd=nd)
+        arr[idx] = keep - eps
+        lm = O.embed_fm_loss(dense, ids, t, p, l2w, l2v, nd=nd)
+        arr[idx] = keep
+        assert abs((lp - lm) / (2 * eps) - (arr[idx] - new_arr[idx]) / lr) < 1e-6, idx
+
+    for idx in [(0, 0), (0, 2), (2, 1)]:
+        check(p["tables"][0], new["tables"][0], idx)
+    check(p["tables"][1], new["tables"][1], (1, 2))
+    check(p["w0"], new["w0"], (0,))
+    for idx in [(0, 0), (5, 0)]:
+        check(p["w1"], new["w1"], idx)
+    for idx in [(1, 1), (6, 0)]:
+        check(p["v"], new["v"], idx)

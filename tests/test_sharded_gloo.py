@@ -139,6 +139,62 @@ class CpuOps:
         if nxt is not None:
             self.field_route(sh, nxt[1], send, rec=R)
 
+    # training (fp64 inside)
+    def combine_grad(self, sh, partials, dense, labels, scale, logit, gs, loss=None):
+        B, nd, kfm, P = dense.shape[0], sh.nd, sh.kfm, sh.partial_width
+        p = partials.numpy().reshape(sh.world, B, P).astype(np.float64).sum(0)
+        d = dense.numpy().astype(np.float64)
+        v, w1 = sh.v.numpy().astype(np.float64), sh.w1.numpy().astype(np.float64)[:, 0]
+        S = p[:, :kfm] + d @ v[:nd]
+        z = p[:, kfm] + d @ w1[:nd] + float(sh.w0[0]) + 0.5 * ((S ** 2).sum(1) - p[:, kfm + 1] -
+                                                                (d * d) @ (v[:nd] ** 2).sum(1))
+        t = labels.numpy().astype(np.float64)
+        logit.copy_(torch.as_tensor(z.reshape(B, 1), dtype=torch.float32))
+        gs[:, :kfm] = torch.as_tensor(S, dtype=torch.float32)
+        gs[:, kfm] = torch.as_tensor((1 / (1 + np.exp(-z)) - t) * scale, dtype=torch.float32)
+        if loss is not None:
+            loss.copy_(torch.as_tensor(np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z))), dtype=torch.float32))
+
+    def dense_grads(self, sh, dense, gs, grad):
+        nd, kfm, d = sh.nd, sh.kfm, sh.d
+        x = dense.numpy().astype(np.float64)
+        s, g = gs[:, :kfm].numpy().astype(np.float64), gs[:, kfm].numpy().astype(np.float64)
+        v = sh.v.numpy().astype(np.float64)
+        grad[:nd] = torch.as_tensor(x.T @ g, dtype=torch.float32)
+        dv = x.T @ (g[:, None] * s) - ((x * x).T @ g)[:, None] * v[:nd]
+        grad[d:d + nd * kfm] = torch.as_tensor(dv.reshape(-1), dtype=torch.float32)
+        grad[d * (1 + kfm)] = float(g.sum())
+
+    def owner_grads(self, sh, recv, gs_all, grad, lr, bufs=None):
+        lo, n = sh.owner_field_ranges[sh.rank]
+        if n == 0:
+            return
+        k, kfm, d, S = sh.k, sh.kfm, sh.d, sh.slot_stride
+        r = recv.numpy().reshape(-1, S)[:, :n].astype(np.int64)
+        T = sh.table_shard.numpy().astype(np.float64)
+        s, g = gs_all[:, :kfm].numpy().astype(np.float64), gs_all[:, kfm].numpy().astype(np.float64)
+        v, w1 = sh.v.numpy().astype(np.float64), sh.w1.numpy().astype(np.float64)[:, 0]
+        upd = np.zeros_like(T)
+        for j in range(n):
+            e = sh.nd + (lo + j) * k + np.arange(k)
+            loc = r[:, j]
+            x = np.zeros((r.shape[0], k))
+            x[loc >= 0] = T[loc[loc >= 0]]
+            ve = v[e]
+            dx = g[:, None] * (w1[e][None, :] + s @ ve.T - x * (ve * ve).sum(1)[None, :])
+            np.add.at(upd, loc[loc >= 0], dx[loc >= 0])
+            grad[e] = torch.as_tensor(x.T @ g, dtype=torch.float32)
+            dv = x.T @ (g[:, None] * s) - ((x * x).T @ g)[:, None] * ve
+            grad[d + e[0] * kfm: d + (e[-1] + 1) * kfm] = torch.as_tensor(dv.reshape(-1), dtype=torch.float32)
+        sh.table_shard.copy_(torch.as_tensor(T - lr * upd, dtype=torch.float32))
+
+    def apply(self, sh, grad, lr, reg_w, reg_v):
+        d, kfm = sh.d, sh.kfm
+        with torch.no_grad():
+            sh.w1 -= lr * (grad[:d].reshape(d, 1) + 2 * reg_w * sh.w1)
+            sh.v -= lr * (grad[d:d * (1 + kfm)].reshape(d, kfm) + 2 * reg_v * sh.v)
+            sh.w0 -= lr * grad[d * (1 + kfm):]
+
     def bad_flag(self):
         return torch.zeros(1, dtype=torch.int32)
 
@@ -199,6 +255,65 @@ def _worker(rank, world, port, vocabs, k, B, q):
         q.put((rank, ok_rows and ok_part, float(np.max(np.abs(fm_sh - fm_ref))), sh.row_range))
     finally:
         dist.destroy_process_group()
+
+
+def _train_worker(rank, world, port, vocabs, k, B, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from recommender_system_amd.sharded import ShardedEmbeddingFM
+        nd, kfm = 3, 4
+        sh = ShardedEmbeddingFM(vocabs, k, nd=nd, kfm=kfm, device="cpu", seed=7, ops=CpuOps())
+        with torch.no_grad():
+            sh.table_shard.mul_(20.0)  # O(1) activations: a visible update
+        shards = [None] * world
+        dist.all_gather_object(shards, sh.table_shard.numpy().copy())
+        full = np.concatenate(shards).astype(np.float64)
+        offs = sh.offsets.numpy()
+        p = {"tables": [full[o:o + v] for o, v in zip(offs, vocabs)], "w0": sh.w0.numpy().copy(),
+             "w1": sh.w1.numpy().copy(), "v": sh.v.numpy().copy()}
+        ok = True
+        for step in range(2):
+            rngs = [np.random.default_rng(1000 * step + r) for r in range(world)]
+            batch = [(rg.random((B, nd)).astype(np.float32),
+                      np.stack([rg.integers(0, v, B) for v in vocabs], 1).astype(np.int32),
+                      rg.integers(0, 2, B).astype(np.float32)) for rg in rngs]
+            dense, ids, t = batch[rank]
+            loss = sh.train_step(torch.as_tensor(dense), torch.as_tensor(ids), torch.as_tensor(t), lr=0.5,
+                                 reg_w=1e-3, reg_v=2e-3, return_loss=True)
+            gd, gi, gt = (np.concatenate([b_[j] for b_ in batch]) for j in range(3))
+            p, ce = O.embed_fm_train_step(gd, gi, gt, p, 0.5, 1e-3, 2e-3, nd=nd)
+            ok = ok and np.allclose(loss.numpy(), ce[rank * B:(rank + 1) * B], rtol=1e-5, atol=1e-6)
+            dist.all_gather_object(shards, sh.table_shard.numpy().copy())
+            got = np.concatenate(shards)
+            want = np.concatenate(p["tables"])
+            ok = ok and np.allclose(got, want, rtol=1e-5, atol=1e-6)
+            for name in ("w0", "w1", "v"):
+                ok = ok and np.allclose(getattr(sh, name).numpy(), p[name], rtol=1e-5, atol=1e-6)
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_train_step_gloo(world):
+    """ShardedEmbeddingFM.train_step over gloo (world 2, 3): forward partials,
+    the [s | g] all-gather, owner row gradients + row SGD, the parameter
+    all-reduce — every rank's shard and the replicated w0 / w1 / v equal the
+    oracle's SGD step on the concatenated global batch, over 2 steps."""
+    vocabs = [50, 7, 300, 1, 120]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_train_worker, args=(r, world, port, vocabs, 4, 17, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok in res:
+        assert ok, f"rank {rank}: sharded training step differs from the oracle"
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -425,4 +540,73 @@ def test_gpu_pipe_kernel_simulated_world(gpu, world):
             g, f = outs[r][t].cpu().numpy(), ref.cpu().numpy()
             rms = float(np.sqrt(np.mean(f ** 2)))
             assert np.all(np.abs(g - f) <= 1e-5 * np.maximum(np.abs(f), rms)), (r, t)
+        sh.ops.check()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,k,kfm", [(1, 16, 10), (3, 16, 10), (8, 16, 10), (5, 4, 3)])
+def test_gpu_sharded_train_step_simulated_world(gpu, world, k, kfm):
+    """The sharded training step's HIP kernels (rs_shard_fm_combine_grad,
+    rs_fm_param_grads_strided, rs_shard_owner_fm_grad, rs_embedding_sgd on the
+    received records, rs_sgd_update) at world 1 (ShardedEmbeddingFM.train_step
+    itself) and simulated worlds 3 / 5 / 8 in one process (all-to-all = block
+    transpose, all-gather = concatenation, all-reduce = sum in rank order),
+    2 steps: every rank's shard and the replicated parameters equal the fp64
+    oracle's SGD step on the concatenated global batch."""
+    from tests.helpers import assert_scaled_close
+    from recommender_system_amd.sharded import ShardedEmbeddingFM
+    rng = np.random.default_rng(world * 31 + k)
+    vocabs = [int(v) for v in rng.integers(1, 60, 26)]
+    vocabs[7] = 900  # one field straddles several owners; many repeated rows elsewhere
+    B, nd = 129, 13
+    shs = [ShardedEmbeddingFM(vocabs, k, nd, kfm, device=gpu, seed=11, table_init=False, world=world, rank=r)
+           for r in range(world)]
+    full = torch.empty(shs[0].total_rows, k, device=gpu).uniform_(-1.0, 1.0)
+    for sh in shs:
+        lo, hi = sh.row_range
+        sh.table_shard = full[lo:hi].contiguous()
+    offs = shs[0].offsets.cpu().numpy()
+    T = full.cpu().numpy().astype(np.float64)
+    p = {"tables": [T[o:o + v] for o, v in zip(offs, vocabs)], "w0": shs[0].w0.cpu().numpy(),
+         "w1": shs[0].w1.cpu().numpy(), "v": shs[0].v.cpu().numpy()}
+    lr, rw, rv = 0.5, 1e-3, 2e-3
+    for step in range(2):
+        dense = [torch.rand(B, nd, device=gpu) for _ in range(world)]
+        ids = [torch.as_tensor(np.stack([rng.integers(0, v, B) for v in vocabs], 1), dtype=torch.int32, device=gpu)
+               for _ in range(world)]
+        lab = [torch.as_tensor(rng.integers(0, 2, B), dtype=torch.float32, device=gpu) for _ in range(world)]
+        if world == 1:
+            losses = [shs[0].train_step(dense[0], ids[0], lab[0], lr=lr, reg_w=rw, reg_v=rv, return_loss=True)]
+        else:
+            S, P = shs[0].slot_stride, shs[0].partial_width
+            pbs = [sh._pbufs(B) for sh in shs]
+            tbs = [sh._tbufs(B) for sh in shs]
+            sends = [sh.ops.field_route(sh, ids[r], pbs[r]["send"]) for r, sh in enumerate(shs)]
+            recvs = [torch.cat([sends[r].view(world, B * S)[o] for r in range(world)]) for o in range(world)]
+            pouts = [sh.ops.owner_partials(sh, recvs[o], world * B, pbs[o]["pout"]) for o, sh in enumerate(shs)]
+            pins = [torch.cat([pouts[o].view(world, B * P)[r] for o in range(world)]) for r in range(world)]
+            losses = []
+            for r, sh in enumerate(shs):
+                losses.append(torch.empty(B, device=gpu))
+                sh.ops.combine_grad(sh, pins[r], dense[r], lab[r], 1.0 / (world * B), tbs[r]["logit"], tbs[r]["gs"],
+                                    losses[-1])
+            gs_all = torch.cat([tb["gs"] for tb in tbs])
+            for r, sh in enumerate(shs):
+                tbs[r]["grad"].zero_()
+                sh.ops.dense_grads(sh, dense[r], tbs[r]["gs"], tbs[r]["grad"])
+                sh.ops.owner_grads(sh, recvs[r], gs_all, tbs[r]["grad"], lr, tbs[r])
+            total = tbs[0]["grad"].clone()
+            for tb in tbs[1:]:
+                total += tb["grad"]
+            for sh in shs:
+                sh.ops.apply(sh, total, lr, rw, rv)
+        cat = lambda xs: np.concatenate([x.cpu().numpy() for x in xs])
+        p, ce = O.embed_fm_train_step(cat(dense), cat(ids), cat(lab), p, lr, rw, rv, nd=nd)
+        assert_scaled_close(cat(losses), ce, what=f"step {step} loss")
+        got = np.concatenate([sh.table_shard.cpu().numpy() for sh in shs])
+        assert_scaled_close(got, np.concatenate(p["tables"]), what=f"step {step} table")
+        for sh in shs:
+            for name in ("w0", "w1", "v"):
+                assert_scaled_close(getattr(sh, name), p[name], what=f"step {step} {name}")
+    for sh in shs:
         sh.ops.check()
