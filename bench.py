@@ -43,6 +43,7 @@ sys.path.insert(0, ROOT)
 PEAK_HBM = 8.0e12
 PEAK_F32 = 157.3e12
 SEED = 20261015
+LANES = 2  # sharded stream: batches in flight on separate HIP streams (sharded.PipeLanes)
 
 
 def _dist_setup(args):
@@ -80,9 +81,13 @@ def _max_over_ranks(x, world):
     return float(t.item())
 
 
-def _timed(fn, steps, warmup, world, events=True):
+def _timed(fn, steps, warmup, world, events=True, begin=None, end=None):
     """Run warmup, then exactly `steps` timed steps between barrier+sync on
-    both sides; returns (seconds, [per-step event ms])."""
+    both sides; returns (seconds, [per-step event ms]).  begin/end bracket
+    multi-stream steps (their per-step events are then not kept)."""
+    if begin is not None:
+        begin()
+        events = False
     for i in range(warmup):
         fn(i)
     torch.cuda.synchronize()
@@ -99,6 +104,8 @@ def _timed(fn, steps, warmup, world, events=True):
             evs.append((s, e))
         else:
             fn(warmup + i)
+    if end is not None:
+        end()
     torch.cuda.synchronize()
     _barrier(world)
     torch.cuda.synchronize()
@@ -107,30 +114,41 @@ def _timed(fn, steps, warmup, world, events=True):
     return _max_over_ranks(dt, world), ms
 
 
-def _capture(fn, first, count):
-    """HIP graph of `count` consecutive steps fn(first) .. fn(first+count-1)."""
+def _capture(fn, first, count, begin=None, end=None):
+    """HIP graph of `count` consecutive steps fn(first) .. fn(first+count-1);
+    begin/end (optional) fork side streams off the capture stream and join
+    them back (multi-stream steps, e.g. sharded.PipeLanes)."""
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         with torch.cuda.graph(g, stream=s):
+            if begin is not None:
+                begin()
             for i in range(count):
                 fn(first + i)
+            if end is not None:
+                end()
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     return g
 
 
-def _timed_graph(fn, steps, warmup, world, chunk=64):
+def _timed_graph(fn, steps, warmup, world, chunk=64, begin=None, end=None):
     """Exactly `steps` steps replayed from HIP graphs of `chunk` steps (plus
     one tail graph), timed between barrier+sync; also returns the event time
     per graph launch-slot (kernel + inter-kernel boundary)."""
-    for i in range(warmup):
-        fn(i)
+    if warmup:
+        if begin is not None:
+            begin()
+        for i in range(warmup):
+            fn(i)
+        if end is not None:
+            end()
     torch.cuda.synchronize()
     full, tail = divmod(steps, chunk)
-    g_full = _capture(fn, 0, chunk) if full else None
-    g_tail = _capture(fn, 0, tail) if tail else None
+    g_full = _capture(fn, 0, chunk, begin, end) if full else None
+    g_tail = _capture(fn, 0, tail, begin, end) if tail else None
     for g in (g_full, g_tail):
         if g is not None:
             g.replay()
@@ -356,14 +374,14 @@ def bench_hotpath(args, world, rank):
     return result
 
 
-def _graph_capturable(fn, first):
-    """Capture (never replay) one step in a HIP graph on every rank, then agree
-    collectively: the RCCL all-to-alls are graph-captured only if every rank
-    captured cleanly, otherwise every rank times the eager step."""
+def _graph_capturable(fn, first, begin=None, end=None, count=1):
+    """Capture (never replay) `count` steps in a HIP graph on every rank, then
+    agree collectively: the RCCL all-to-alls are graph-captured only if every
+    rank captured cleanly, otherwise every rank times the eager step."""
     import torch.distributed as dist
     ok, why = 1, None
     try:
-        _capture(fn, first, 1)
+        _capture(fn, first, count, begin, end)
     except Exception as e:  # noqa: BLE001 - any capture failure selects the eager path
         ok, why = 0, f"{type(e).__name__}: {e}"[:200]
     torch.cuda.synchronize()
@@ -379,7 +397,9 @@ def bench_sharded(args, world, rank, vocabs, dense_pool):
     all-to-all carrying [row ids of t | FM partials of t-1], then ONE launch
     (rs_shard_fm_pipe) doing combine of t-1 | owner FM partials of t over its
     field range | field route of t+1 (steady state: every step does one
-    batch's full work).  Also timed: the same
+    batch's full work), run as LANES independent batch streams on their own
+    HIP streams (sharded.PipeLanes) so one lane's launch overlaps the next
+    lane's all-to-all.  Also timed: the one-lane stream, the same
     protocol unpipelined (``forward``: two all-to-alls per batch) and the
     fixed-capacity ROW exchange (``forward_slots``), which returns every
     lookup's 64-B row to the requester.  Steps are replayed from HIP graphs
@@ -387,7 +407,7 @@ def bench_sharded(args, world, rank, vocabs, dense_pool):
     otherwise.  With --sharded at world 1 the all-to-alls still run (RCCL
     self-exchange): the N=1 point of the same curve."""
     import torch.distributed as dist
-    from recommender_system_amd.sharded import ShardedEmbeddingFM
+    from recommender_system_amd.sharded import PipeLanes, ShardedEmbeddingFM
     B, F, k, nd = args.batch, len(vocabs), 16, 13
     dev = torch.device("cuda")
     sh = ShardedEmbeddingFM(vocabs, k, nd, 10, device=dev, seed=SEED)
@@ -404,6 +424,16 @@ def bench_sharded(args, world, rank, vocabs, dense_pool):
         j, jp, jn = i % npool, (i - 1) % npool, (i + 1) % npool
         sh.pipe_step(prev=(dense_pool[jp], outs[(i - 1) % 2]), cur=ids_pool[j], nxt=(dense_pool[jn], ids_pool[jn]))
 
+    L = LANES
+    lanes = PipeLanes(sh, L)
+    louts = [torch.empty(B, 1, device=dev) for _ in range(2 * L)]
+
+    def laned(i):
+        # batch i on lane i % L; its lane's previous batch is i - L, next i + L
+        j, jp, jn = i % npool, (i - L) % npool, (i + L) % npool
+        lanes.step(i % L, prev=(dense_pool[jp], louts[(i - L) % (2 * L)]), cur=ids_pool[j],
+                   nxt=(dense_pool[jn], ids_pool[jn]))
+
     def per_batch(fwd):
         def step(i):
             # fixed-size exchange, no host sync inside the step
@@ -411,22 +441,31 @@ def bench_sharded(args, world, rank, vocabs, dense_pool):
             fwd(dense_pool[j], ids_pool[j], check=False, out=out)
         return step
 
-    def run(step):
+    def run(step, begin=None, end=None):
+        if begin is not None:
+            begin()
         for i in range(args.warmup):
             step(i)
+        if end is not None:
+            end()
         torch.cuda.synchronize()
         _barrier(world)
-        graphed, why = _graph_capturable(step, args.warmup)
+        graphed, why = _graph_capturable(step, 0, begin, end, count=2 * L if begin is not None else 1)
         if graphed:
-            dt, slot_ms = _timed_graph(step, args.steps, 0, world, chunk=16)
+            dt, slot_ms = _timed_graph(step, args.steps, 0, world, chunk=16, begin=begin, end=end)
             step_ms = _max_over_ranks(slot_ms, world)
         else:
-            dt, ms = _timed(step, args.steps, 0, world)
-            step_ms = _max_over_ranks(float(np.mean(ms)), world)
+            dt, ms = _timed(step, args.steps, 0, world, begin=begin, end=end)
+            step_ms = _max_over_ranks(float(np.mean(ms)) if ms else dt / args.steps * 1e3, world)
         return dt, step_ms, ("HIP graph replay (RCCL captured)" if graphed else f"eager launches ({why})")
 
-    sh.pipe_route(ids_pool[0])  # prologue: batch 0's row ids
-    dt, step_ms, timing = run(pipelined)
+    lanes.begin()
+    for l in range(L):  # prologue: each lane's first batch's row ids
+        lanes.route(l, ids_pool[l % npool])
+    lanes.end()
+    dt, step_ms, timing = run(laned, lanes.begin, lanes.end)
+    sh.pipe_route(ids_pool[0])  # prologue of the one-lane stream: batch 0's row ids
+    odt, ostep_ms, otiming = run(pipelined)
     udt, ustep_ms, utiming = run(per_batch(sh.forward))
     f = sh.ops.bad_flag()  # any bad id during the timed steps?
     dist.all_reduce(f, op=dist.ReduceOp.MAX)
@@ -447,12 +486,17 @@ def bench_sharded(args, world, rank, vocabs, dense_pool):
     tdt, tstep_ms, ttiming = run(train)
     S, P = sh.slot_stride, sh.partial_width
     res = {"exchange": {
-        "protocol": "owner-side FM partials, pipelined: ONE RCCL all-to-all of [row ids of t | FM partials of "
-                    "t-1] records + ONE launch (combine t-1 | owner FM partials of t over its field range | field "
-                    "route of t+1) per batch; fixed sizes, no host sync",
+        "protocol": f"owner-side FM partials, pipelined: ONE RCCL all-to-all of [row ids of t | FM partials of "
+                    f"t-1] records + ONE launch (combine t-1 | owner FM partials of t over its field range | field "
+                    f"route of t+1) per batch; fixed sizes, no host sync; {L} lanes (sharded.PipeLanes: batch i on "
+                    f"lane i % {L}, own HIP stream and records, all-to-alls chained in batch order) so a lane's "
+                    f"launch overlaps the next lane's all-to-all",
         "timing": timing, "lookups_per_rank": B * F, "rows_per_rank": sh.rows_per_rank,
         "owner_field_ranges": sh.owner_field_ranges,
         "bytes_per_rank_each_way": world * B * (S + P) * 4,
+        "one_lane": {"samples_per_s": world * args.steps * B / odt, "ms_per_step": odt / args.steps * 1e3,
+                     "timing": otiming, "note": "the same pipelined stream on one HIP stream (all-to-all and "
+                                                "launch serialised)"},
         "unpipelined": {"samples_per_s": world * args.steps * B / udt, "ms_per_step": udt / args.steps * 1e3,
                         "timing": utiming, "id_bytes_per_rank_each_way": world * B * S * 4,
                         "partial_bytes_per_rank_each_way": world * B * P * 4,
@@ -472,7 +516,7 @@ def bench_sharded(args, world, rank, vocabs, dense_pool):
     alg = B * 1824 + 18880
     res["roofline"] = {"bound": "hbm", "achieved": alg / (step_ms * 1e-3) / 1e9, "peak": PEAK_HBM / 1e9,
                        "unit": "GB/s", "frac": alg / (step_ms * 1e-3) / PEAK_HBM, "traffic": None,
-                       "kernel": "sharded step (RCCL all-to-all + rs_shard_fm_pipe)",
+                       "kernel": f"sharded step (RCCL all-to-all + rs_shard_fm_pipe, {L} lanes overlapped)",
                        "kernel_ms_avg": step_ms}
     res["cpu_baseline"] = None
     return res
