@@ -19,9 +19,13 @@ namespace rs {
 // ------------------------------------------------------------------ GEMM
 // C[M,N] = alpha * op(A)[M,K] op(B)[K,N] + beta * C, row-major, optionally
 // masked: C[m,n] *= (mask[m,n] > 0) (ReLU backward: a = relu(z) > 0 <=> z > 0).
-// 64x64 tiles, 256 threads, 4x4 outputs per thread, K in steps of 16 through
-// LDS; each output's K sum runs in one fixed order.
+// 64x64 tiles, 256 threads = four waves in 2x2, each a 32x32 tile of
+// v_mfma_f32_32x32x2_f32 (lane l: A row / B column l&31, k-slot l>>5; C:
+// column l&31, rows (r&3) + 8(r>>2) + 4(l>>5)); K in steps of 16 through LDS.
+// The f32 MFMA is a k-ordered fmaf chain, so each output's K sum runs in one
+// fixed order (deterministic, the same order as a scalar k loop).
 constexpr int GT = 64, GK = 16;
+typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 // Split-K (part != nullptr): block z of gridDim.z covers K range
 // [z*kslice, (z+1)*kslice) and stores its raw partial tile to part[z][M][N];
@@ -34,13 +38,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(int ta, int tb, int M, int N,
                                                    float* __restrict__ part) {
   __shared__ float As[GK][GT + 4];
   __shared__ float Bs[GK][GT + 4];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1, li = lane & 31, lk = lane >> 5;
   const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
-  float acc[4][4];
+  floatx16 acc;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   const int kb = part ? blockIdx.z * kslice : 0;
   const int ke = part ? min(K, kb + kslice) : K;
   for (int k0 = kb; k0 < ke; k0 += GK) {
@@ -58,36 +61,25 @@ __global__ __launch_bounds__(256) void gemm_kernel(int ta, int tb, int M, int N,
     }
     __syncthreads();
 #pragma unroll
-    for (int kk = 0; kk < GK; ++kk) {
-      float a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty * 4 + i];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx * 4 + j];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
-    }
+    for (int ks = 0; ks < GK / 2; ++ks)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[2 * ks + lk][wm * 32 + li], Bs[2 * ks + lk][wn * 32 + li], acc,
+                                                 0, 0, 0);
     __syncthreads();
   }
+  const int n = n0 + wn * 32 + li;
+  if (n >= N) return;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + ty * 4 + i;
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
     if (m >= M) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + tx * 4 + j;
-      if (n >= N) continue;
-      if (part) {
-        part[((int64_t)blockIdx.z * M + m) * N + n] = acc[i][j];
-        continue;
-      }
-      float v = alpha * acc[i][j];
-      if (beta != 0.f) v += beta * C[(int64_t)m * ldc + n];
-      if (mask && !(mask[(int64_t)m * ldm + n] > 0.f)) v = 0.f;
-      C[(int64_t)m * ldc + n] = v;
+    if (part) {
+      part[((int64_t)blockIdx.z * M + m) * N + n] = acc[r];
+      continue;
     }
+    float v = alpha * acc[r];
+    if (beta != 0.f) v += beta * C[(int64_t)m * ldc + n];
+    if (mask && !(mask[(int64_t)m * ldm + n] > 0.f)) v = 0.f;
+    C[(int64_t)m * ldc + n] = v;
   }
 }
 

@@ -251,3 +251,32 @@ def test_compile_fit_dcn_on_bundled_sample(gpu):
     m2 = rs.DCN(cols, [64, 32], 1, "relu", 3, seed=5)
     hist = compile_fit(m2, dense[:960], ids[:960], label[:960], batch_size=32, epochs=4, sgd=0.05)
     assert hist[-1] < hist[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ta,tb", [(0, 0), (1, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(4096, 256, 429), (429, 256, 4096), (37, 1, 70), (64, 65, 16), (3, 5, 0)])
+def test_rs_gemm_mfma_matches_torch(gpu, ta, tb, M, N, K):
+    """rs_gemm (v_mfma_f32_32x32x2_f32 tiles, split-K through the workspace
+    when K is long) == a torch fp64 GEMM of the same fp32 operands, with
+    alpha / beta / the ReLU-mask epilogue; bitwise run to run."""
+    from recommender_system_amd import _lib
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N * 3 + K + ta * 2 + tb)
+    A = torch.randn(*((K, M) if ta else (M, K)), generator=g).to(gpu)
+    B = torch.randn(*((N, K) if tb else (K, N)), generator=g).to(gpu)
+    C0 = torch.randn(M, N, generator=g).to(gpu)
+    mask = (torch.rand(M, N, generator=g) > 0.3).float().to(gpu)
+    ws = torch.empty(max(int(_lib.lib().rs_gemm_workspace_size(M, N, K)), 1), dtype=torch.uint8, device=gpu)
+    st = _lib.stream()
+    outs = []
+    for _ in range(2):
+        C = C0.clone()
+        _lib.call("rs_gemm", ta, tb, M, N, K, 0.5, A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), 2.0,
+                  C.data_ptr(), N, mask.data_ptr(), N, ws.data_ptr(), ws.numel(), st)
+        outs.append(C.cpu())
+    opA = (A.T if ta else A).double().cpu()
+    opB = (B.T if tb else B).double().cpu()
+    ref = (0.5 * (opA @ opB) + 2.0 * C0.double().cpu()) * mask.double().cpu()
+    scale = float(opA.abs().sum(1).max() * opB.abs().max()) if K else 1.0
+    assert float((outs[0].double() - ref).abs().max()) <= 2e-6 * max(scale, 1.0)
+    assert torch.equal(outs[0], outs[1])
