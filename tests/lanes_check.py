@@ -34,7 +34,7 @@ def check(exchange):
     sh._force_exchange = exchange
     rng = np.random.default_rng(1)
     B, n = 260, 7
-    batches = [(torch.rand(B, 13, device=dev),
+    batches = [(torch.as_tensor(rng.random((B, 13)), dtype=torch.float32, device=dev),
                 torch.as_tensor(np.stack([rng.integers(0, v, B) for v in vocabs], 1), dtype=torch.int32,
                                 device=dev)) for _ in range(n)]
     ref = [o.cpu().numpy() for o in sh.forward_stream(batches)]
