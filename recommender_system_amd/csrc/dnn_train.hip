@@ -47,17 +47,20 @@ __global__ __launch_bounds__(256) void gemm_kernel(int ta, int tb, int M, int N,
   const int kb = part ? blockIdx.z * kslice : 0;
   const int ke = part ? min(K, kb + kslice) : K;
   for (int k0 = kb; k0 < ke; k0 += GK) {
-    // stage op(A)[m0:m0+64, k0:k0+16] as As[k][m] and op(B)[k0:k0+16, n0:n0+64] as Bs[k][n]
+    // stage op(A)[m0:m0+64, k0:k0+16] as As[k][m] and op(B)[k0:k0+16, n0:n0+64] as Bs[k][n];
+    // consecutive threads walk each operand's contiguous memory dimension
+    // (k for a row-major A / transposed B, m or n otherwise): coalesced loads
     for (int e = threadIdx.x; e < GK * GT; e += 256) {
-      const int kk = e / GT, mm = e % GT;
-      const int m = m0 + mm, k = k0 + kk;
+      const int ka = ta ? e / GT : e % GK, ma = ta ? e % GT : e / GK;
+      const int m = m0 + ma, k = k0 + ka;
       float av = 0.f;
       if (m < M && k < ke) av = ta ? A[(int64_t)k * lda + m] : A[(int64_t)m * lda + k];
-      As[kk][mm] = av;
-      const int n = n0 + mm;
+      As[ka][ma] = av;
+      const int kb2 = tb ? e % GK : e / GT, nb = tb ? e / GK : e % GT;
+      const int n = n0 + nb, k2 = k0 + kb2;
       float bv = 0.f;
-      if (n < N && k < ke) bv = tb ? B[(int64_t)n * ldb + k] : B[(int64_t)k * ldb + n];
-      Bs[kk][mm] = bv;
+      if (n < N && k2 < ke) bv = tb ? B[(int64_t)n * ldb + k2] : B[(int64_t)k2 * ldb + n];
+      Bs[kb2][nb] = bv;
     }
     __syncthreads();
 #pragma unroll
