@@ -171,11 +171,21 @@ extern "C" void* rs_cb_open(const char* path) {
   f->size = (size_t)st.st_size;
   memcpy(&f->h, f->base, sizeof(Header));
   const Header& h = f->h;
+  // section extents in checked arithmetic: a crafted header must not wrap a
+  // product past the bounds checks (rs_cb_read copies straight from the map)
+  auto sect_end = [](uint64_t off, uint64_t rows, uint64_t cols, uint64_t width, uint64_t* end) {
+    uint64_t n = 0;
+    return !__builtin_mul_overflow(rows, cols, &n) && !__builtin_mul_overflow(n, width, &n) &&
+           !__builtin_add_overflow(off, n, end);
+  };
+  uint64_t end_dense = 0, end_ids = 0, end_labels = 0;
+  const bool aligned = h.off_dense % kHeader == 0 && h.off_ids % kHeader == 0 && h.off_labels % kHeader == 0;
   const bool ok = memcmp(h.magic, kMagic, 8) == 0 && h.version == 1 && (h.id_bytes == 4 || h.id_bytes == 8) &&
-                  h.n_sparse <= (uint32_t)kMaxSparse && h.file_size <= f->size &&
-                  h.off_dense + h.n_rows * h.n_dense * 4 <= h.off_ids &&
-                  h.off_ids + h.n_rows * h.n_sparse * h.id_bytes <= h.off_labels &&
-                  h.off_labels + h.n_rows * 4 <= h.file_size;
+                  h.n_sparse <= (uint32_t)kMaxSparse && h.file_size <= f->size && aligned &&
+                  h.off_dense >= (uint64_t)kHeader &&
+                  sect_end(h.off_dense, h.n_rows, h.n_dense, 4, &end_dense) && end_dense <= h.off_ids &&
+                  sect_end(h.off_ids, h.n_rows, h.n_sparse, h.id_bytes, &end_ids) && end_ids <= h.off_labels &&
+                  sect_end(h.off_labels, h.n_rows, 1, 4, &end_labels) && end_labels <= h.file_size;
   if (!ok) {
     rs_cb_close(f);
     rs::set_error("rs_cb_open: %s: bad RSCB header", path);

@@ -374,9 +374,12 @@ using namespace rs;
 static int g_sp_mode = 0;
 extern "C" void rs_diag_shard_set_mode(int m) { g_sp_mode = m; }
 
-// workspace = [hist (int32 per 256-lookup block and owner) | status (u64 per
-// 1024-lookup block and owner) share one region][256 B control words]
-static int64_t sh_ctrl_offset(int64_t n_lookups, int world) {
+// workspace = [256 B control word (fixed offset: it must survive calls with a
+// different n or world, and the exact protocol's hist) | hist (int32 per
+// 256-lookup block and owner) and status (u64 per 1024-lookup block and owner)
+// share one region]
+constexpr int64_t SH_CTRL_BYTES = 256;
+static int64_t sh_region_bytes(int64_t n_lookups, int world) {
   const int64_t hist = (n_lookups + SH_CHUNK - 1) / SH_CHUNK * world * 4;
   const int64_t stat = (n_lookups + SP_PER - 1) / SP_PER * world * 8;
   return (((hist > stat ? hist : stat) + 255) / 256) * 256;
@@ -384,7 +387,7 @@ static int64_t sh_ctrl_offset(int64_t n_lookups, int world) {
 
 extern "C" int64_t rs_shard_workspace_size(int64_t n_lookups, int world) {
   if (n_lookups < 0 || world < 1 || world > SH_MAXW) return -1;
-  return sh_ctrl_offset(n_lookups, world) + 256;
+  return SH_CTRL_BYTES + sh_region_bytes(n_lookups, world);
 }
 
 extern "C" int rs_shard_bucketize(const void* ids, int id_kind, int64_t id_stride, const int64_t* field_offsets,
@@ -401,7 +404,7 @@ extern "C" int rs_shard_bucketize(const void* ids, int id_kind, int64_t id_strid
   ShardArgs a{ids, id_kind, id_stride, field_offsets, field_vocab, n_fields, batch * n_fields, rows_per_rank, world,
               err_flag, 1.0 / (double)rows_per_rank};
   const int nb = (int)((a.n + SH_CHUNK - 1) / SH_CHUNK);
-  int32_t* hist = static_cast<int32_t*>(workspace);
+  int32_t* hist = reinterpret_cast<int32_t*>(static_cast<uint8_t*>(workspace) + SH_CTRL_BYTES);
   if (a.n == 0) {
     (void)hipMemsetAsync(counts, 0, world * sizeof(int32_t), st);
     return launch_status("rs_shard_bucketize");
@@ -428,7 +431,7 @@ extern "C" int rs_shard_slot_bucketize(const void* ids, int id_kind, int64_t id_
   ShardArgs a{ids, id_kind, id_stride, field_offsets, field_vocab, n_fields, batch * n_fields, rows_per_rank, world,
               err_flag, 1.0 / (double)rows_per_rank};
   const int nb = (int)((a.n + SH_CHUNK - 1) / SH_CHUNK);
-  int32_t* hist = static_cast<int32_t*>(workspace);
+  int32_t* hist = reinterpret_cast<int32_t*>(static_cast<uint8_t*>(workspace) + SH_CTRL_BYTES);
   if (a.n == 0) {
     (void)hipMemsetAsync(counts, 0, world * sizeof(int32_t), st);
     return launch_status("rs_shard_slot_bucketize");
@@ -436,8 +439,8 @@ extern "C" int rs_shard_slot_bucketize(const void* ids, int id_kind, int64_t id_
   (void)hist;
   const int nbp = (int)((a.n + SP_PER - 1) / SP_PER);
   uint8_t* ws = static_cast<uint8_t*>(workspace);
-  shard_slot_onepass<<<nbp, SP_THREADS, 0, st>>>(a, reinterpret_cast<uint64_t*>(ws),
-                                                 reinterpret_cast<uint64_t*>(ws + sh_ctrl_offset(a.n, world)), nbp,
+  shard_slot_onepass<<<nbp, SP_THREADS, 0, st>>>(a, reinterpret_cast<uint64_t*>(ws + SH_CTRL_BYTES),
+                                                 reinterpret_cast<uint64_t*>(ws), nbp,
                                                  counts, slot_of, send_slots, cap, overflow_flag, g_sp_mode);
   return launch_status("rs_shard_slot_bucketize");
 }

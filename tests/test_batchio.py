@@ -68,6 +68,18 @@ def test_rejects_bad_ids_and_files(tmp_path):
     empty = write_criteo(tmp_path / "empty.rscb", dense[:0], ids[:0], labels[:0], vocab)
     with RSCBFile(empty) as f:
         assert f.n_rows == 0
+    # crafted headers: n_rows whose section sizes wrap uint64, a misaligned
+    # section offset, a dense section overlapping the header page
+    ids[2, 7] = 9
+    good = write_criteo(tmp_path / "good.rscb", dense, ids, labels, vocab)
+    raw = bytearray(open(good, "rb").read())
+    import struct
+    for field_off, value in [(24, (1 << 64) // (13 * 4) + 1), (32, 4096 + 4), (32, 0)]:
+        b = bytearray(raw)
+        struct.pack_into("<Q", b, field_off, value)  # 24: n_rows, 32: off_dense
+        (tmp_path / "crafted").write_bytes(bytes(b))
+        with pytest.raises(OSError, match="bad RSCB header"):
+            RSCBFile(tmp_path / "crafted")
 
 
 def test_bundled_sample_matches_reference_preprocessing(tmp_path):
