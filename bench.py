@@ -8,10 +8,14 @@ Default (N=1) workload — the configuration the metric is quoted on:
   pre-generated batches rotated per step, inputs resident in HBM.  One step =
   one rs_embed_fm_fwd launch over one batch.
 
-  N>1 (driver: torch.distributed.run, one rank per GPU): the same table
-  row-sharded over the ranks (recommender_system_amd/sharded.py, RCCL
-  all-to-all of row ids and rows), 4096 local samples per rank (weak
-  scaling).  value = N*4096 / max-over-ranks step time.
+  N>1 (driver: torch.distributed.run, one rank per GPU) and --sharded at
+  N=1: BASELINE config 5 — the full DeepFM forward with ONE 1e8-row table
+  (26 x 3,846,154 x 16 fp32) row-sharded over the ranks
+  (recommender_system_amd/sharded.py ShardedDeepFM: RCCL all-to-all of row
+  ids and of rows, then the fused DeepFM kernel from the exchange buffer),
+  4096 local samples per rank (weak scaling).  value = N*4096 /
+  max-over-ranks step time.  The headline hot path sharded the same way
+  (26 x 1e7 table, FM partial protocol) is nested as `fm_hotpath_sharded`.
 
 Also measured (nested in the JSON line, not `value`):
   * `roofline`: the fused gather+FM kernel's algorithmic bytes per launch
@@ -370,7 +374,12 @@ def bench_hotpath(args, world, rank):
         else:
             result["cpu_baseline"] = None
     else:
-        result.update(bench_sharded(args, world, rank, vocabs, dense_pool))
+        res, V5 = bench_sharded_deepfm(args, world, rank)
+        result.update(res)
+        result["vocab_per_field"] = V5
+        if not args.deepfm_only:
+            result["fm_hotpath_sharded"] = bench_sharded_fm(args, world, rank, vocabs, dense_pool)
+        result["cpu_baseline"] = None
     return result
 
 
@@ -390,9 +399,10 @@ def _graph_capturable(fn, first, begin=None, end=None, count=1):
     return bool(t.item()), why
 
 
-def bench_sharded(args, world, rank, vocabs, dense_pool):
-    """BASELINE config 5 shape: the table row-sharded over the ranks, each rank
-    B local samples (weak scaling).  Timed protocol (the value): owner-side FM
+def bench_sharded_fm(args, world, rank, vocabs, dense_pool):
+    """The headline hot path (embedding lookup + FM logit, 26 x 1e7 x 16) with
+    the table row-sharded over the ranks, each rank B local samples (weak
+    scaling); nested in the N>1 line as `fm_hotpath_sharded`.  Timed protocol: owner-side FM
     partials, pipelined (sharded.py ``pipe_step``): per batch t, ONE RCCL
     all-to-all carrying [row ids of t | FM partials of t-1], then ONE launch
     (rs_shard_fm_pipe) doing combine of t-1 | owner FM partials of t over its
@@ -520,6 +530,79 @@ def bench_sharded(args, world, rank, vocabs, dense_pool):
                        "kernel_ms_avg": step_ms}
     res["cpu_baseline"] = None
     return res
+
+
+def bench_sharded_deepfm(args, world, rank):
+    """BASELINE config 5 (the N>1 value, and --sharded at N=1): DeepFM forward
+    with ONE 1e8-row table (26 fields x 3,846,154 rows x 16 fp32 = 6.4 GB)
+    row-sharded over the ranks, B = 4096 local samples per rank (weak
+    scaling), DNN 429-256-128-64-1, FM k 10.  One step = ShardedDeepFM.forward
+    on one batch: rs_shard_row_route -> RCCL all-to-all of row ids ->
+    rs_gather_rows (owner) -> RCCL all-to-all of rows -> rs_deepfm_fwd from
+    the exchange buffer (gather + FM + DNN tower + sigmoid, one launch).  The
+    all-to-alls run at world 1 too (RCCL self-exchange).  Replayed from HIP
+    graphs when RCCL capture works on every rank (collective decision)."""
+    import torch.distributed as dist
+    from recommender_system_amd.sharded import ShardedDeepFM
+    B, F, k, nd, kfm = args.batch, 26, 16, 13, 10
+    V = 3846154  # 26 x 3,846,154 = 1.0e8 rows
+    vocabs = [V] * F
+    dev = torch.device("cuda")
+    cols = [[{"feat": f"I{i + 1}"} for i in range(nd)],
+            [{"feat": f"C{i + 1}", "feat_onehot_dim": V, "embed_dim": k} for i in range(F)]]
+    model = ShardedDeepFM(cols, kfm, 1e-4, 1e-4, [256, 128, 64], 1, "relu", embed_dim=k, device=dev, seed=SEED)
+    model.emb._force_exchange = True
+    g = torch.Generator(device=dev)
+    g.manual_seed(SEED + 101 + rank)
+    npool = 16
+    ids_pool = torch.randint(0, V, (npool, B, F), generator=g, device=dev, dtype=torch.int32)
+    dense_pool = torch.rand(npool, B, nd, generator=g, device=dev)
+    out = torch.empty(B, 1, device=dev)
+
+    def step(i):
+        j = i % npool
+        model.forward((dense_pool[j], ids_pool[j]), check=False, out=out)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    _barrier(world)
+    graphed, why = _graph_capturable(step, 0)
+    if graphed:
+        dt, slot_ms = _timed_graph(step, args.steps, 0, world, chunk=16)
+        timing = "HIP graph replay (RCCL captured)"
+    else:
+        dt, _ = _timed(step, args.steps, 0, world, events=False)
+        timing = f"eager launches ({why})"
+    f = model.ops.bad_flag()
+    dist.all_reduce(f, op=dist.ReduceOp.MAX)
+    if bool(f.item()):
+        raise RuntimeError("sharded DeepFM bench: bad ids during timing")
+    # the fused DeepFM kernel alone, from the exchange buffer of the last step
+    rb = model._rbufs(B)
+
+    def finish(i):
+        model.finish(dense_pool[i % npool], rb["got"], rb, out)
+
+    fdt, fslot_ms = _timed_graph(finish, args.steps, 2, world, chunk=16)
+    fin_ms = _max_over_ranks(fslot_ms, world)
+    flops = B * 2 * (429 * 256 + 256 * 128 + 128 * 64 + 64)
+    ms = dt / args.steps * 1e3
+    S = model.emb.slot_stride
+    res = {"value": world * args.steps * B / dt, "ms_per_step": ms,
+           "roofline": {"bound": "mfma", "achieved": flops / (fin_ms * 1e-3) / 1e12, "peak": PEAK_F32 / 1e12,
+                        "unit": "TFLOP/s", "frac": flops / (fin_ms * 1e-3) / PEAK_F32, "traffic": None,
+                        "kernel": "deepfm_fused (rs_deepfm_fwd from the row-exchange buffer)",
+                        "kernel_ms": fin_ms, "dnn_flop_per_launch": flops,
+                        "kernel_ms_source": "HIP events around graph-replayed launches of the fused kernel alone"},
+           "exchange": {"protocol": "field-range row records: rs_shard_row_route, RCCL all-to-all of row ids, "
+                                    "owner rs_gather_rows, RCCL all-to-all of rows, rs_deepfm_fwd with ids = slot_of",
+                        "timing": timing, "rows_per_rank": model.emb.rows_per_rank,
+                        "owner_field_ranges": model.emb.owner_field_ranges, "slots_per_sample_per_owner": S,
+                        "id_bytes_per_rank_each_way": world * B * S * 4,
+                        "row_bytes_per_rank_each_way": world * B * S * k * 4,
+                        "exchange_ms_per_step": ms - fin_ms}}
+    return res, V
 
 
 def _line(metric, value, unit, args, world, ms_per_step, config, roofline, extra=None, dtype="f32", hib=True):
@@ -959,6 +1042,8 @@ def main():
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--deepfm-only", dest="deepfm_only", action="store_true",
+                    help="sharded: skip the secondary FM hot-path protocols")
     ap.add_argument("--sharded", action="store_true",
                     help="time the row-sharded exchange path even at world 1 (N=1 point of the sharded curve)")
     args = ap.parse_args()
@@ -981,13 +1066,18 @@ def main():
             "value": res["value"], "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": res["ms_per_step"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "deepfm_embed_fm_hotpath" if world == 1 and not args.sharded else "deepfm_embed_fm_rowsharded",
-                       "global_batch": args.batch * world, "batch_per_gpu": args.batch, "sparse_fields": 26,
-                       "vocab_per_field": int(args.vocab), "embed_dim": 16, "fm_k": 10, "dense_features": 13,
-                       "ids": "int32 uniform per field", "parallelism": f"dp{world}" + ("+rowshard" if world > 1 or args.sharded else "")},
+            "config": ({"workload": "deepfm_embed_fm_hotpath", "global_batch": args.batch, "batch_per_gpu": args.batch,
+                        "sparse_fields": 26, "vocab_per_field": int(args.vocab), "embed_dim": 16, "fm_k": 10,
+                        "dense_features": 13, "ids": "int32 uniform per field", "parallelism": "dp1"}
+                       if world == 1 and not args.sharded else
+                       {"workload": "deepfm_forward_rowsharded_1e8 (BASELINE config 5)",
+                        "global_batch": args.batch * world, "batch_per_gpu": args.batch, "sparse_fields": 26,
+                        "vocab_per_field": res["vocab_per_field"], "table_rows": 26 * res["vocab_per_field"],
+                        "embed_dim": 16, "fm_k": 10, "dnn": [256, 128, 64, 1], "dense_features": 13,
+                        "ids": "int32 uniform per field", "parallelism": f"dp{world}+rowshard{world}"}),
             "roofline": res["roofline"], "cpu_baseline": res["cpu_baseline"],
         }
-        for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "exchange", "sharded_train_step"):
+        for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "exchange", "fm_hotpath_sharded"):
             if key in res:
                 line[key] = res[key]
         print(json.dumps(line), flush=True)

@@ -531,6 +531,24 @@ int rs_shard_field_route(const void* ids, int id_kind, int64_t id_stride,
                          const int32_t* owner_fields, int slot_stride,
                          int64_t rec_stride, int32_t* send, int* err_flag,
                          rs_stream_t stream);
+/* Row protocol on the same field-range records (ShardedDeepFM, config 5: the
+ * DNN needs every row at the requester, so rows come back instead of FM
+ * partials; EmbedLayer.call, layer/core.py:273-280, sharded):
+ *  rs_shard_row_route: rs_shard_field_route with rec_stride = slot_stride,
+ *   plus slot_of[b*n_fields + c] = the record word (o*batch + b)*slot_stride
+ *   + j of lookup (b, c) (o = its owner, j = c - field_lo(o)), or -1 for an
+ *   out-of-range id (*err_flag set).  The owner answers the received words
+ *   with rs_gather_rows (-1 -> zero row) into [world*batch*slot_stride, k];
+ *   after the row all-to-all, lookup (b, c)'s row is got[slot_of[b*F + c]],
+ *   so rs_deepfm_fwd(ids = slot_of, offsets 0, vocab world*batch*slot_stride,
+ *   table = got) runs the whole DeepFM forward straight from the exchange
+ *   buffer.  Fixed sizes, no scan, no capacity, no overflow.                 */
+int rs_shard_row_route(const void* ids, int id_kind, int64_t id_stride,
+                       const int64_t* field_offsets, const int64_t* field_vocab,
+                       int n_fields, int64_t batch, int64_t rows_per_rank,
+                       int world, const int32_t* owner_fields, int slot_stride,
+                       int32_t* send, int32_t* slot_of, int* err_flag,
+                       rs_stream_t stream);
 int rs_shard_owner_fm(const int32_t* local_rows, int64_t rec_stride,
                       int field_lo, int n_owned, const float* shard,
                       int64_t shard_rows, int nd, int n_fields, int k,

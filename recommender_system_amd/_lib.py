@@ -90,6 +90,7 @@ SIGNATURES = {
     "rs_attention_pool_fwd": (I, [P, L, I, I, L, P, P]),
     "rs_ffm_fwd": (I, [P, I, L, P, L, I, P, P, P, P, P, I, I, I, P, L, P, P]),
     "rs_shard_field_route": (I, [P, I, L, P, P, I, L, L, I, P, I, L, P, P, P]),
+    "rs_shard_row_route": (I, [P, I, L, P, P, I, L, L, I, P, I, P, P, P, P]),
     "rs_shard_owner_fm": (I, [P, L, I, I, P, L, I, I, I, P, I, P, L, L, P, P]),
     "rs_shard_fm_combine": (I, [P, L, I, L, P, L, I, I, I, P, P, I, P, P]),
     "rs_shard_fm_pipe": (I, [P, I, I, P, L, P, L, P, P, I, L, P, P, L, P, I, P, I, L, I, I, I, P, P, I, P, P]),

@@ -464,6 +464,27 @@ extern "C" int rs_shard_field_route(const void* ids, int id_kind, int64_t id_str
   return launch_status("rs_shard_field_route");
 }
 
+extern "C" int rs_shard_row_route(const void* ids, int id_kind, int64_t id_stride, const int64_t* field_offsets,
+                                  const int64_t* field_vocab, int n_fields, int64_t batch, int64_t rows_per_rank,
+                                  int world, const int32_t* owner_fields, int slot_stride, int32_t* send,
+                                  int32_t* slot_of, int* err_flag, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
+  RS_REQUIRE(ids && field_offsets && field_vocab && owner_fields && send && slot_of,
+             "rs_shard_row_route: null pointer");
+  RS_REQUIRE(world >= 1 && world <= SH_MAXW && rows_per_rank >= 1 && n_fields >= 1 && batch > 0 &&
+                 slot_stride >= 1 && slot_stride <= n_fields,
+             "rs_shard_row_route: bad shape (1 <= world <= %d, 1 <= slot_stride <= n_fields)", SH_MAXW);
+  RS_REQUIRE((int64_t)world * batch * slot_stride < ((int64_t)1 << 31) && rows_per_rank < ((int64_t)1 << 31) &&
+                 batch * n_fields < ((int64_t)1 << 31),
+             "rs_shard_row_route: too many slots / shard rows must fit int32");
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_shard_row_route: bad id_kind");
+  const int64_t total = (int64_t)world * batch * slot_stride;
+  RouteArgs a{ids, id_kind, id_stride, field_offsets, field_vocab, rows_per_rank, owner_fields, slot_stride,
+              (int)batch, slot_stride, send, err_flag, total, slot_of, n_fields};
+  shard_field_route<<<sh_grid(total), 256, 0, as_stream(stream)>>>(a);
+  return launch_status("rs_shard_row_route");
+}
+
 extern "C" int rs_gather_rows(const float* table, int64_t n_rows, int k, const int32_t* rows, int64_t n, float* out,
                               int* err_flag, rs_stream_t stream) {
   if (n == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)

@@ -29,6 +29,10 @@ struct RouteArgs {
   int32_t* send;
   int* err;
   int64_t total;       // world * batch * stride (< 2^31)
+  // row protocol (rs_shard_row_route) only, else null: slot_of[b*n_fields+c]
+  // = the record word of lookup (b, c) = its row's index in the owner's reply
+  int32_t* slot_of;
+  int n_fields;
 };
 
 template <int NTH>
@@ -61,6 +65,9 @@ __device__ __forceinline__ void field_route_part(const RouteArgs& a, int blk, in
         const int64_t local = a.offs[c] + id - (int64_t)o * a.rpr;
         if (local >= 0 && local < a.rpr) out = (int32_t)local;
       }
+      // exactly one owner holds a valid lookup; a bad id is -1 (every owner
+      // of its field writes the same value)
+      if (a.slot_of != nullptr && (out >= 0 || !ok)) a.slot_of[(int64_t)b * a.n_fields + c] = out >= 0 ? idx : -1;
     }
     a.send[(int64_t)ob * a.rec_stride + j] = out;
   }

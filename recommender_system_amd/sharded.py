@@ -32,6 +32,7 @@ exchange protocol is testable with world_size>1 on CPU (tests/test_sharded_gloo.
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
 
 import torch
@@ -193,6 +194,23 @@ class HipShardOps:
         call("rs_sgd_update", ptr(sh.v), ptr(grad) + 4 * d, d * kfm, float(lr), float(reg_v), st)
         call("rs_sgd_update", ptr(sh.w0), ptr(grad) + 4 * d * (1 + kfm), 1, float(lr), 0.0, st)
         sh.prepare()
+
+    # -- row protocol of ShardedDeepFM (rs_shard_row_route / rs_gather_rows / rs_deepfm_fwd)
+    def row_route(self, sh, ids, send, slot_of):
+        B, F = ids.shape
+        call("rs_shard_row_route", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(sh.offsets), ptr(sh.vocab), F,
+             B, sh.rows_per_rank, sh.world, ptr(sh.owner_fields), sh.slot_stride, ptr(send), ptr(slot_of),
+             ptr(self.err), _lib.stream())
+        return send, slot_of
+
+    def deepfm_rows(self, model, got, rb, dense, out):
+        """DeepFM forward with lookup (b, c)'s row at got[slot_of[b, c]]."""
+        return _hip_deepfm(self, model, rb["slot_of"], got, rb["zoff"], rb["nslots"], dense, out)
+
+    def deepfm_table(self, model, ids, dense, out):
+        """World 1: the DeepFM forward on the (whole-table) shard itself."""
+        sh = model.emb
+        return _hip_deepfm(self, model, ids, sh.table_shard, sh.offsets, sh.vocab, dense, out)
 
     def bad_flag(self):
         """[out-of-range id seen] (device tensor; resets)."""
@@ -630,3 +648,170 @@ class PipeLanes:
     def end(self):
         for s in self.streams:
             self.hub.wait_stream(s)
+
+
+class ShardedDeepFM:
+    """DeepFM (model/deepFM.py:15-31) with its embedding table row-sharded over
+    a process group: BASELINE config 5.  ``forward(inputs) -> [B,1]``
+    (post-sigmoid) on every rank for its local batch, where inputs is the
+    reference's packed ``X[B, nd+F]`` or ``(dense[B,nd], ids[B,F])``.
+
+    The DNN branch (``self.dnn(x)`` at model/deepFM.py:28-30) needs every
+    row of x at the requester, so rows come back (EmbedLayer semantics,
+    layer/core.py:273-280), over the same field-range records as the FM's
+    partial protocol:
+      1. rs_shard_row_route -> [world][B][S] local rows (-1 = not yours) and
+                               slot_of[b*F + c] = where lookup (b, c)'s row
+                               will land in the reply
+      2. all_to_all(row ids)   (RCCL)
+      3. rs_gather_rows       -> the owner serves [world*B*S, k] rows
+      4. all_to_all(rows)      (RCCL)
+      5. rs_deepfm_fwd        -> gather (from the exchange buffer, ids =
+                               slot_of) + FM + DNN tower + sigmoid head, ONE
+                               launch
+    Fixed, host-known message sizes (no scan, no capacity, no overflow case),
+    no host sync unless ``check``.  World 1 without a forced exchange runs
+    step 5 on the table itself.  Dense parameters (FM w0 / w1 / v, the DNN)
+    are replicated: every rank builds them from the same seed.  The local
+    steps are pluggable (``ops``) so the protocol is testable over gloo on
+    CPU (tests/test_sharded_gloo.py)."""
+
+    def __init__(self, feature_columns, k, w_reg, v_reg, hidden_units, output_dim, activation, embed_dim=8,
+                 group=None, device=None, seed=0, ops=None, table_init=True, world=None, rank=None):
+        from .layers import DNNLayer
+        dense_cols, sparse_cols = feature_columns
+        self.nd = len(dense_cols)
+        vocabs = [int(f["feat_onehot_dim"]) for f in sparse_cols]
+        self.reg_w, self.reg_v = float(w_reg), float(v_reg)
+        self.emb = ShardedEmbeddingFM(vocabs, embed_dim, self.nd, k, group=group, device=device, seed=seed, ops=ops,
+                                      table_init=table_init, world=world, rank=rank)
+        sh = self.emb
+        self.device, self.group, self.ops = sh.device, group, sh.ops
+        self.world, self.rank, self.F, self.k, self.kfm = sh.world, sh.rank, sh.F, sh.k, sh.kfm
+        self.dnn = DNNLayer(hidden_units, output_dim, activation, device=self.device, seed=seed * 7919 + 11)
+        self.dnn.build(sh.d)
+        self._in_rows = None
+        # world 1: run the row protocol anyway (route, serve, finish; the
+        # exchange is the identity) instead of the direct table path
+        self.force_rows = False
+
+    # -- parameters (replicated; Keras names of FMLayer + DNNLayer)
+    @property
+    def table_shard(self):
+        return self.emb.table_shard
+
+    def keras_weights(self):
+        w = {"w0": self.emb.w0, "w1": self.emb.w1, "v": self.emb.v}
+        w.update({f"dnn/{n}": p for n, p in self.dnn.keras_weights().items()})
+        return w
+
+    def fused_rows(self):
+        """Tower input permutation: the fused kernel's LDS tile holds
+        [emb F*k | dense nd], Keras rows are [dense nd | emb F*k]."""
+        if self._in_rows is None:
+            fk = self.F * self.k
+            kp = (fk + self.nd + 15) // 16 * 16
+            rows = torch.full((kp,), -1, dtype=torch.int32)
+            rows[:fk] = torch.arange(fk, dtype=torch.int32) + self.nd
+            rows[fk:fk + self.nd] = torch.arange(self.nd, dtype=torch.int32)
+            self._in_rows = rows.to(self.device)
+        return self._in_rows
+
+    # -- the row exchange, step by step (forward = route, exchange, serve, exchange, finish)
+    def _rbufs(self, B):
+        rb = getattr(self, "_row_bufs", None)
+        if rb is None or rb["B"] != B:
+            W, S, dev, F = self.world, self.emb.slot_stride, self.device, self.F
+            n = W * B * S
+            rb = {"B": B, "n": n,
+                  "send": torch.empty(n, dtype=torch.int32, device=dev),
+                  "recv": torch.empty(n, dtype=torch.int32, device=dev),
+                  "slot_of": torch.empty(B, F, dtype=torch.int32, device=dev),
+                  "reply": torch.empty(n, self.k, dtype=torch.float32, device=dev),
+                  "got": torch.empty(n, self.k, dtype=torch.float32, device=dev),
+                  "zoff": torch.zeros(F, dtype=torch.int64, device=dev),
+                  "nslots": torch.full((F,), n, dtype=torch.int64, device=dev)}
+            self._row_bufs = rb
+        return rb
+
+    def route(self, ids, rb):
+        """Step 1: the row-id records to every owner and slot_of."""
+        return self.ops.row_route(self.emb, ids, rb["send"], rb["slot_of"])
+
+    def serve(self, recv, reply):
+        """Step 3 (owner): rows of the received record words (-1 -> zero row)."""
+        return self.ops.gather_rows_into(self.emb.table_shard, recv, reply)
+
+    def finish(self, dense, got, rb, out):
+        """Step 5: the DeepFM forward from the exchange buffer."""
+        return self.ops.deepfm_rows(self, got, rb, dense, out)
+
+    def forward(self, inputs, check=True, out=None):
+        from .models import _split_criteo
+        sh = self.emb
+        if isinstance(inputs, (tuple, list)) and not isinstance(self.ops, HipShardOps):
+            dense, ids = inputs  # CPU test double: host tensors as given
+        else:
+            dense, ids = _split_criteo(inputs, self.nd, self.device)
+        B = ids.shape[0]
+        if out is None:
+            out = torch.empty(B, 1, dtype=torch.float32, device=self.device)
+        if not sh.exchanges and not self.force_rows and isinstance(self.ops, HipShardOps):
+            self.ops.deepfm_table(self, ids, dense, out)  # world 1: the shard is the whole table
+        else:
+            rb = self._rbufs(B)
+            self.route(ids, rb)
+            recv = rb["send"]
+            if sh.exchanges:
+                recv = rb["recv"]
+                dist.all_to_all_single(recv, rb["send"], group=self.group)
+            reply = got = self.serve(recv, rb["reply"])
+            if sh.exchanges:
+                got = rb["got"]
+                dist.all_to_all_single(got, reply, group=self.group)
+            self.finish(dense, got, rb, out)
+        if check:
+            f = self.ops.bad_flag()
+            if self.world > 1:
+                dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
+            if bool(f.item()):
+                raise IndexError("sharded DeepFM: embedding id out of range")
+        return out
+
+    __call__ = forward
+
+
+def _deepfm_tower_args(model):
+    dims = model.dnn._dims()
+    n = len(dims) - 1
+    acts = [_lib.ACT[l.activation] for l in model.dnn._layers()]
+    return n, (C.c_int * (n + 1))(*dims), (C.c_int * n)(*acts)
+
+
+def _deepfm_fused_ok(model):
+    if not model.dnn.tower_ok() or model.dnn.output_layer.units != 1:
+        return False
+    n, dims, _ = _deepfm_tower_args(model)
+    return bool(_lib.lib().rs_deepfm_fused_ok(model.nd, model.F, model.k, model.kfm, n, dims))
+
+
+def _hip_deepfm(ops, model, ids, table, offs, vocab, dense, out):
+    """rs_deepfm_fwd (one launch) or, for shapes it does not take, the fused
+    gather+FM kernel emitting x + the tower / per-layer DNN."""
+    sh = model.emb
+    if _deepfm_fused_ok(model):
+        n, dims, acts = _deepfm_tower_args(model)
+        mlp = model.dnn.prepared(model.fused_rows())
+        call("rs_deepfm_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), model.nd,
+             ptr(table), ptr(offs), ptr(vocab), model.F, model.k, ptr(sh.prepared), ptr(sh.w0), model.kfm, n, dims,
+             acts, ptr(mlp), 0.5, 0.5, ptr(out), None, ids.shape[0], ptr(ops.err), _lib.stream())
+        return out
+    from .layers import sigmoid_combine
+    B = ids.shape[0]
+    x = torch.empty(B, sh.d, dtype=torch.float32, device=model.device)
+    fm = torch.empty(B, 1, dtype=torch.float32, device=model.device)
+    call("rs_embed_fm_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), model.nd,
+         ptr(table), ptr(offs), ptr(vocab), model.F, model.k, ptr(sh.prepared), ptr(sh.w0), model.kfm, ptr(fm),
+         ptr(x), B, ptr(ops.err), _lib.stream())
+    out.copy_(sigmoid_combine(fm, model.dnn(x), 0.5, 0.5))
+    return out
