@@ -47,7 +47,6 @@ sys.path.insert(0, ROOT)
 PEAK_HBM = 8.0e12
 PEAK_F32 = 157.3e12
 SEED = 20261015
-LANES = 2  # sharded stream: batches in flight on separate HIP streams (sharded.PipeLanes)
 
 
 def _dist_setup(args):
@@ -121,7 +120,7 @@ def _timed(fn, steps, warmup, world, events=True, begin=None, end=None):
 def _capture(fn, first, count, begin=None, end=None):
     """HIP graph of `count` consecutive steps fn(first) .. fn(first+count-1);
     begin/end (optional) fork side streams off the capture stream and join
-    them back (multi-stream steps, e.g. sharded.PipeLanes)."""
+    them back (multi-stream steps)."""
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -402,25 +401,21 @@ def _graph_capturable(fn, first, begin=None, end=None, count=1):
 def bench_sharded_fm(args, world, rank, vocabs, dense_pool):
     """The headline hot path (embedding lookup + FM logit, 26 x 1e7 x 16) with
     the table row-sharded over the ranks, each rank B local samples (weak
-    scaling); nested in the N>1 line as `fm_hotpath_sharded`.  Timed protocol: owner-side FM
-    partials, pipelined (sharded.py ``pipe_step``): per batch t, ONE RCCL
-    all-to-all carrying [row ids of t | FM partials of t-1], then ONE launch
-    (rs_shard_fm_pipe) doing combine of t-1 | owner FM partials of t over its
-    field range | field route of t+1 (steady state: every step does one
-    batch's full work), run as LANES independent batch streams on their own
-    HIP streams (sharded.PipeLanes) so one lane's launch overlaps the next
-    lane's all-to-all.  Also timed: the one-lane stream, the same
-    protocol unpipelined (``forward``: two all-to-alls per batch) and the
-    fixed-capacity ROW exchange (``forward_slots``), which returns every
-    lookup's 64-B row to the requester.  Steps are replayed from HIP graphs
-    when RCCL capture works on every rank (decided collectively), eager
-    otherwise.  With --sharded at world 1 the all-to-alls still run (RCCL
-    self-exchange): the N=1 point of the same curve."""
+    scaling); nested in the N>1 line as `fm_hotpath_sharded`.  Timed protocol:
+    owner-side FM partials, pipelined (sharded.py ``pipe_step``): per batch t,
+    ONE RCCL all-to-all carrying [row ids of t | FM partials of t-1], then ONE
+    launch (rs_shard_fm_pipe) doing combine of t-1 | owner FM partials of t
+    over its field range | field route of t+1.  Also timed: the same protocol
+    unpipelined (``forward``: two all-to-alls per batch), the fixed-capacity
+    ROW exchange (``forward_slots``, every lookup's 64-B row back to the
+    requester) and the data-parallel training step.  Steps are replayed from
+    HIP graphs when RCCL capture works on every rank (decided collectively),
+    eager otherwise; the all-to-alls run at world 1 too (RCCL self-exchange)."""
     import torch.distributed as dist
-    from recommender_system_amd.sharded import PipeLanes, ShardedEmbeddingFM
-    B, F, k, nd = args.batch, len(vocabs), 16, 13
+    from recommender_system_amd.sharded import ShardedEmbeddingFM
+    B, F, k = args.batch, len(vocabs), 16
     dev = torch.device("cuda")
-    sh = ShardedEmbeddingFM(vocabs, k, nd, 10, device=dev, seed=SEED)
+    sh = ShardedEmbeddingFM(vocabs, k, 13, 10, device=dev, seed=SEED)
     sh._force_exchange = True
     g = torch.Generator(device=dev)
     g.manual_seed(SEED + rank)
@@ -434,16 +429,6 @@ def bench_sharded_fm(args, world, rank, vocabs, dense_pool):
         j, jp, jn = i % npool, (i - 1) % npool, (i + 1) % npool
         sh.pipe_step(prev=(dense_pool[jp], outs[(i - 1) % 2]), cur=ids_pool[j], nxt=(dense_pool[jn], ids_pool[jn]))
 
-    L = LANES
-    lanes = PipeLanes(sh, L)
-    louts = [torch.empty(B, 1, device=dev) for _ in range(2 * L)]
-
-    def laned(i):
-        # batch i on lane i % L; its lane's previous batch is i - L, next i + L
-        j, jp, jn = i % npool, (i - L) % npool, (i + L) % npool
-        lanes.step(i % L, prev=(dense_pool[jp], louts[(i - L) % (2 * L)]), cur=ids_pool[j],
-                   nxt=(dense_pool[jn], ids_pool[jn]))
-
     def per_batch(fwd):
         def step(i):
             # fixed-size exchange, no host sync inside the step
@@ -451,31 +436,22 @@ def bench_sharded_fm(args, world, rank, vocabs, dense_pool):
             fwd(dense_pool[j], ids_pool[j], check=False, out=out)
         return step
 
-    def run(step, begin=None, end=None):
-        if begin is not None:
-            begin()
+    def run(step):
         for i in range(args.warmup):
             step(i)
-        if end is not None:
-            end()
         torch.cuda.synchronize()
         _barrier(world)
-        graphed, why = _graph_capturable(step, 0, begin, end, count=2 * L if begin is not None else 1)
+        graphed, why = _graph_capturable(step, 0)
         if graphed:
-            dt, slot_ms = _timed_graph(step, args.steps, 0, world, chunk=16, begin=begin, end=end)
+            dt, slot_ms = _timed_graph(step, args.steps, 0, world, chunk=16)
             step_ms = _max_over_ranks(slot_ms, world)
         else:
-            dt, ms = _timed(step, args.steps, 0, world, begin=begin, end=end)
+            dt, ms = _timed(step, args.steps, 0, world)
             step_ms = _max_over_ranks(float(np.mean(ms)) if ms else dt / args.steps * 1e3, world)
         return dt, step_ms, ("HIP graph replay (RCCL captured)" if graphed else f"eager launches ({why})")
 
-    lanes.begin()
-    for l in range(L):  # prologue: each lane's first batch's row ids
-        lanes.route(l, ids_pool[l % npool])
-    lanes.end()
-    dt, step_ms, timing = run(laned, lanes.begin, lanes.end)
-    sh.pipe_route(ids_pool[0])  # prologue of the one-lane stream: batch 0's row ids
-    odt, ostep_ms, otiming = run(pipelined)
+    sh.pipe_route(ids_pool[0])  # prologue of the stream: batch 0's row ids
+    dt, step_ms, timing = run(pipelined)
     udt, ustep_ms, utiming = run(per_batch(sh.forward))
     f = sh.ops.bad_flag()  # any bad id during the timed steps?
     dist.all_reduce(f, op=dist.ReduceOp.MAX)
@@ -495,18 +471,15 @@ def bench_sharded_fm(args, world, rank, vocabs, dense_pool):
 
     tdt, tstep_ms, ttiming = run(train)
     S, P = sh.slot_stride, sh.partial_width
-    res = {"exchange": {
-        "protocol": f"owner-side FM partials, pipelined: ONE RCCL all-to-all of [row ids of t | FM partials of "
-                    f"t-1] records + ONE launch (combine t-1 | owner FM partials of t over its field range | field "
-                    f"route of t+1) per batch; fixed sizes, no host sync; {L} lanes (sharded.PipeLanes: batch i on "
-                    f"lane i % {L}, own HIP stream and records, all-to-alls chained in batch order) so a lane's "
-                    f"launch overlaps the next lane's all-to-all",
+    alg = B * 1824 + 18880
+    return {
+        "samples_per_s": world * args.steps * B / dt, "ms_per_step": dt / args.steps * 1e3,
+        "protocol": "owner-side FM partials, pipelined: ONE RCCL all-to-all of [row ids of t | FM partials of t-1] "
+                    "records + ONE launch (combine t-1 | owner FM partials of t over its field range | field route "
+                    "of t+1) per batch; fixed sizes, no host sync",
         "timing": timing, "lookups_per_rank": B * F, "rows_per_rank": sh.rows_per_rank,
-        "owner_field_ranges": sh.owner_field_ranges,
-        "bytes_per_rank_each_way": world * B * (S + P) * 4,
-        "one_lane": {"samples_per_s": world * args.steps * B / odt, "ms_per_step": odt / args.steps * 1e3,
-                     "timing": otiming, "note": "the same pipelined stream on one HIP stream (all-to-all and "
-                                                "launch serialised)"},
+        "owner_field_ranges": sh.owner_field_ranges, "bytes_per_rank_each_way": world * B * (S + P) * 4,
+        "hbm_frac_vs_unsharded_bytes": alg / (step_ms * 1e-3) / PEAK_HBM,
         "unpipelined": {"samples_per_s": world * args.steps * B / udt, "ms_per_step": udt / args.steps * 1e3,
                         "timing": utiming, "id_bytes_per_rank_each_way": world * B * S * 4,
                         "partial_bytes_per_rank_each_way": world * B * P * 4,
@@ -515,21 +488,12 @@ def bench_sharded_fm(args, world, rank, vocabs, dense_pool):
                           "timing": rtiming, "slots_per_peer": bufs["cap"],
                           "row_bytes_per_rank_each_way": world * bufs["cap"] * k * 4,
                           "overflow_during_timing": bool(fl[1].item()),
-                          "note": "fixed-capacity row exchange (forward_slots): rows back to the requester"}},
-           "sharded_train_step": {"samples_per_s": world * args.steps * B / tdt, "ms_per_step": tdt / args.steps * 1e3,
-                          "timing": ttiming,
-                          "note": "ShardedEmbeddingFM.train_step: partial-protocol forward (2 all-to-alls) + "
-                                  "combine_grad, all-gather of [s | g] records, owner row grads + row-sparse SGD "
-                                  "of the shard, all-reduce of the FM parameter grads, SGD + l2"}}
-    res["value"] = world * args.steps * B / dt
-    res["ms_per_step"] = dt / args.steps * 1e3
-    alg = B * 1824 + 18880
-    res["roofline"] = {"bound": "hbm", "achieved": alg / (step_ms * 1e-3) / 1e9, "peak": PEAK_HBM / 1e9,
-                       "unit": "GB/s", "frac": alg / (step_ms * 1e-3) / PEAK_HBM, "traffic": None,
-                       "kernel": f"sharded step (RCCL all-to-all + rs_shard_fm_pipe, {L} lanes overlapped)",
-                       "kernel_ms_avg": step_ms}
-    res["cpu_baseline"] = None
-    return res
+                          "note": "fixed-capacity row exchange (forward_slots): rows back to the requester"},
+        "train_step": {"samples_per_s": world * args.steps * B / tdt, "ms_per_step": tdt / args.steps * 1e3,
+                       "timing": ttiming,
+                       "note": "ShardedEmbeddingFM.train_step: partial-protocol forward (2 all-to-alls) + "
+                               "combine_grad, all-gather of [s | g] records, owner row grads + row-sparse SGD "
+                               "of the shard, all-reduce of the FM parameter grads, SGD + l2"}}
 
 
 def bench_sharded_deepfm(args, world, rank):
@@ -1031,7 +995,23 @@ def _pmc_traffic():
         return None
 
 
+_RESULT_OUT = None
+
+
+def _emit(line):
+    """The one JSON result line, on the process's original stdout (everything
+    else — e.g. RCCL's version banner, which it prints to stdout at
+    communicator init — goes to stderr, so stdout holds exactly that line)."""
+    out = _RESULT_OUT if _RESULT_OUT is not None else sys.stdout
+    out.write(json.dumps(line) + "\n")
+    out.flush()
+
+
 def main():
+    global _RESULT_OUT
+    sys.stdout.flush()
+    _RESULT_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -1053,7 +1033,7 @@ def main():
     if args.config in other:
         line = other[args.config](args, world, rank)
         if rank == 0:
-            print(json.dumps(line), flush=True)
+            _emit(line)
         return
     if args.config == "deepfm1e6":
         args.vocab = 1e6
@@ -1080,7 +1060,7 @@ def main():
         for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "exchange", "fm_hotpath_sharded"):
             if key in res:
                 line[key] = res[key]
-        print(json.dumps(line), flush=True)
+        _emit(line)
     if _dist_on():
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -410,25 +410,21 @@ class ShardedEmbeddingFM:
         return loss
 
     # -- the pipelined partial protocol: one all-to-all per batch
-    def _sbufs(self, B, lane=0):
-        """Send/recv records of one pipeline lane (each lane is an independent
-        batch stream with its own buffers)."""
-        lanes = getattr(self, "_stream_bufs", None)
-        if lanes is None:
-            lanes = self._stream_bufs = {}
-        sb = lanes.get(lane)
+    def _sbufs(self, B):
+        """Send/recv records of the pipelined stream."""
+        sb = getattr(self, "_stream_bufs", None)
         if sb is None or sb["B"] != B:
             R = self.slot_stride + self.partial_width
             n = self.world * B * R
             sb = {"B": B, "R": R,
                   "send": torch.zeros(n, dtype=torch.int32, device=self.device),
                   "recv": torch.zeros(n, dtype=torch.int32, device=self.device)}
-            lanes[lane] = sb
+            self._stream_bufs = sb
         return sb
 
-    def pipe_route(self, ids, lane=0):
+    def pipe_route(self, ids):
         """Prologue of a stream: the first batch's row-id words."""
-        sb = self._sbufs(ids.shape[0], lane)
+        sb = self._sbufs(ids.shape[0])
         self.ops.field_route(self, ids, sb["send"], rec=sb["R"])
 
     @property
@@ -437,7 +433,7 @@ class ShardedEmbeddingFM:
         bench forces the RCCL self-exchange)."""
         return self.world > 1 or self._force_exchange
 
-    def pipe_step(self, prev=None, cur=None, nxt=None, lane=0):
+    def pipe_step(self, prev=None, cur=None, nxt=None):
         """One step of the pipelined partial protocol, for batch t = cur:
           all_to_all                  -> ONE collective: [row ids of t | partials of t-1]
           rs_shard_fm_pipe (1 launch) -> combine(t-1) into prev's out
@@ -447,7 +443,7 @@ class ShardedEmbeddingFM:
         routed by the previous step or pipe_route), nxt = (dense, ids) of
         batch t+1; any may be None."""
         B = next(x for x in (cur, prev and prev[0], nxt and nxt[1]) if x is not None).shape[0]
-        sb = self._sbufs(B, lane)
+        sb = self._sbufs(B)
         if self.exchanges:
             dist.all_to_all_single(sb["recv"], sb["send"], group=self.group)
             self.ops.pipe(self, sb["recv"], sb["send"], prev=prev, cur=cur, nxt=nxt)
@@ -457,42 +453,21 @@ class ShardedEmbeddingFM:
             self.ops.pipe(self, sb["send"], sb["recv"], prev=prev, cur=cur, nxt=nxt)
             sb["send"], sb["recv"] = sb["recv"], sb["send"]
 
-    def forward_stream(self, batches, check=True, lanes=1):
+    def forward_stream(self, batches, check=True):
         """FM logits of a sequence of local batches [(dense, ids), ...] with the
         pipelined partial protocol: batch t's row-id message and batch t-1's
         partials share one all-to-all and one launch, so a stream of n batches
-        costs n + 1 collectives and n + 2 launches (vs 2n and 3n).  With
-        ``lanes`` > 1 batch i goes to lane i % lanes (``PipeLanes``: each lane
-        its own HIP stream and records, the all-to-alls chained in batch
-        order) so one lane's launch overlaps the next lane's all-to-all.
-        Every rank must pass the same number of batches.  Returns
-        [logit [B,1] per batch]."""
+        costs n + 1 collectives and n + 2 launches (vs 2n and 3n).  Every rank
+        must pass the same number of batches.  Returns [logit [B,1] per batch]."""
         n = len(batches)
         outs = [torch.empty(ids.shape[0], 1, dtype=torch.float32, device=self.device) for _, ids in batches]
-        L = max(1, int(lanes))
-        pl = PipeLanes(self, L) if L > 1 else None
-        if pl is not None:
-            pl.begin()
-        per_lane = [list(range(l, n, L)) for l in range(L)]  # batch indices of each lane
-        for l in range(min(L, n)):
-            if pl is not None:
-                pl.route(l, batches[l][1])
-            else:
-                self.pipe_route(batches[0][1])
-        for u in range((n + L - 1) // L + 1):  # lane-local step u, lanes in batch order
-            for l in range(L):
-                idx = per_lane[l]
-                if u > len(idx) or not idx:
-                    continue
-                prev = (batches[idx[u - 1]][0], outs[idx[u - 1]]) if u > 0 else None
-                cur = batches[idx[u]][1] if u < len(idx) else None
-                nxt = batches[idx[u + 1]] if u + 1 < len(idx) else None
-                if pl is not None:
-                    pl.step(l, prev, cur, nxt)
-                else:
-                    self.pipe_step(prev, cur, nxt)
-        if pl is not None:
-            pl.end()
+        if n:
+            self.pipe_route(batches[0][1])
+        for t in range(n + 1):
+            prev = (batches[t - 1][0], outs[t - 1]) if t > 0 else None
+            cur = batches[t][1] if t < n else None
+            nxt = batches[t + 1] if t + 1 < n else None
+            self.pipe_step(prev, cur, nxt)
         if check:
             f = self.ops.bad_flag()
             if self.world > 1:
@@ -593,61 +568,6 @@ class ShardedEmbeddingFM:
         return logit
 
     __call__ = forward
-
-
-class PipeLanes:
-    """Overlapped pipelined partial protocol: ``n`` independent batch streams
-    ("lanes"), each with its own send/recv records (``_sbufs(lane=l)``) and
-    its own HIP stream for the ``rs_shard_fm_pipe`` launches.  Every
-    all-to-all is issued on ONE stream, the hub (the stream current at
-    ``begin``), in the order the caller issues the steps — batch order, the
-    same on every rank — so the collectives are serialised on the
-    communicator exactly as in the one-lane stream, while lane l's launch runs
-    beside the next lane's all-to-all: per step the GPU pays ~max(all-to-all,
-    launch) instead of their sum.
-
-    Dependencies form a star (hub <-> lanes): before batch t's all-to-all the
-    hub waits for its lane's previous launch (which wrote the send records);
-    the lane waits for the all-to-all before its launch.  (Lane-to-lane event
-    waits, or collectives issued on the lanes, crash hipStreamEndCapture on
-    this ROCm: scripts/diag_lanes_capture.py.)
-
-    Usage: ``begin()``, ``route(l, ids)`` for each lane's first batch,
-    ``step(l, prev, cur, nxt)`` in batch order, ``end()`` (the hub joins every
-    lane).  begin/end bracket a HIP graph capture the same way."""
-
-    def __init__(self, sh, n=2):
-        self.sh, self.n = sh, int(n)
-        self.streams = [torch.cuda.Stream(device=sh.device) for _ in range(self.n)]
-        self.hub = None
-
-    def begin(self):
-        self.hub = torch.cuda.current_stream(self.sh.device)
-        for s in self.streams:
-            s.wait_stream(self.hub)
-
-    def route(self, lane, ids):
-        with torch.cuda.stream(self.streams[lane]):
-            self.sh.pipe_route(ids, lane=lane)
-
-    def step(self, lane, prev=None, cur=None, nxt=None):
-        sh, s = self.sh, self.streams[lane]
-        if not sh.exchanges:
-            with torch.cuda.stream(s):
-                sh.pipe_step(prev, cur, nxt, lane=lane)
-            return
-        B = next(x for x in (cur, prev and prev[0], nxt and nxt[1]) if x is not None).shape[0]
-        sb = sh._sbufs(B, lane)
-        self.hub.wait_stream(s)  # the lane's previous launch wrote its send records
-        with torch.cuda.stream(self.hub):
-            dist.all_to_all_single(sb["recv"], sb["send"], group=sh.group)
-        s.wait_stream(self.hub)
-        with torch.cuda.stream(s):
-            sh.ops.pipe(sh, sb["recv"], sb["send"], prev=prev, cur=cur, nxt=nxt)
-
-    def end(self):
-        for s in self.streams:
-            self.hub.wait_stream(s)
 
 
 class ShardedDeepFM:

@@ -508,25 +508,6 @@ def test_gpu_sharded_single_rank_equals_fused(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("exchange", [False, True])
-def test_gpu_pipe_lanes_equal_forward(gpu, exchange):
-    """PipeLanes (2 / 3 lanes, eager and HIP-graph replayed) == the one-lane
-    stream, bit for bit (tests/lanes_check.py).  exchange=True runs the RCCL
-    self-exchange of a 1-rank nccl group in a child process (its own time
-    limit; it exits without tearing RCCL down)."""
-    if not exchange:
-        from lanes_check import check
-        check(False)
-        return
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    r = subprocess.run([sys.executable, os.path.join(here, "lanes_check.py"), "exchange"], capture_output=True,
-                       text=True, timeout=100)
-    assert r.returncode == 0 and "LANES OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("world,k,kfm", [(8, 16, 10), (3, 16, 10), (2, 8, 20), (5, 4, 3)])
 def test_gpu_partial_protocol_simulated_world(gpu, world, k, kfm, fused):
@@ -885,3 +866,17 @@ def test_gpu_sharded_deepfm_world1(gpu):
         m.force_rows = force
         with pytest.raises(IndexError):
             m.forward((dense, bad))
+
+
+@pytest.mark.gpu
+def test_gpu_rccl_self_exchange(gpu):
+    """The sharded paths with their RCCL all-to-alls forced on (a 1-rank nccl
+    group, eager and HIP-graph captured) equal the same paths without the
+    exchange, bit for bit (tests/rccl_selfcheck.py, in a child process with
+    its own time limit)."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "rccl_selfcheck.py")], capture_output=True, text=True,
+                       timeout=100)
+    assert r.returncode == 0 and "RCCL OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
