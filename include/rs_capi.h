@@ -224,6 +224,24 @@ int rs_din_attention_dice_fwd(const float* query, const float* keys,
                               const float* b_out, float* out, int64_t batch,
                               rs_stream_t stream);
 
+/* Attention.call 'prelu' at any depth (layer/interaction.py:355-406 with
+ * len(hidden_units) = n_layers, any H, k <= 64 or larger): e = [q, key_t,
+ * q-key_t, q*key_t] per (b, t) row, Dense(hidden[l], PReLU()) with alpha
+ * [T, hidden[l]] as fp32 MFMA GEMMs over the B*T rows, Dense(1), masked
+ * softmax, weighted sum of the values.  W[l] (in, out) Keras orientation,
+ * b[l] [hidden[l]], alpha[l] [T, hidden[l]] (device pointers in host
+ * arrays).  workspace: rs_din_attention_gen_workspace_size bytes (device).   */
+int64_t rs_din_attention_gen_workspace_size(int64_t batch, int T, int k,
+                                            int n_layers, const int* hidden);
+int rs_din_attention_gen_fwd(const float* query, const float* keys,
+                             const float* values, const float* mask, int T,
+                             int k, int n_layers, const int* hidden,
+                             const float* const* W, const float* const* b,
+                             const float* const* alpha, const float* w_out,
+                             const float* b_out, float* out, int64_t batch,
+                             void* workspace, int64_t workspace_bytes,
+                             rs_stream_t stream);
+
 /* DIN attention straight from behaviour ids (model/din.py:56-80 + Attention
  * 'prelu', layer/interaction.py:355-406): key = value = table[hist[b,t]],
  * query = table[cand[b]], mask = hist != 0.  Two launches: scores (MFMA, the
@@ -294,6 +312,15 @@ int rs_deepfm_fwd(const void* ids, int id_kind, int64_t id_stride,
                   const float* mlp_prepared, float c0, float c1, float* out,
                   float* fm_logit, int64_t batch, int* err_flag,
                   rs_stream_t stream);
+
+/* Dense + PReLU whose alpha is [alpha_rows, N], row m using alpha row
+ * m % alpha_rows: Keras Dense(N, activation=PReLU()) on a 3-D input
+ * [B, alpha_rows, K] flattened to [B*alpha_rows, K] (PReLU's alpha has shape
+ * input_shape[1:] = (T, N)).                                                */
+int rs_dense_prelu_rows_fwd(const float* x, int64_t x_stride, const float* W,
+                            const float* bias, const float* alpha,
+                            int alpha_rows, float* y, int64_t y_stride,
+                            int64_t M, int K, int N, rs_stream_t stream);
 
 /* Per-column affine + activation, in place allowed: y = act(x*scale + shift).
  * Used for BatchNormalization at inference (model/din.py:89).               */

@@ -339,13 +339,19 @@ def pnn_inner(X, p, nd=13, dt=np.float64, inputs=None):
 
 
 def din(inputs, p, dense_feats, sparse_feats, behavior_feats, dt=np.float64,
-        att_act="prelu"):
+        att_act="prelu", dnn_act="prelu"):
     """DIN.call (model/din.py:56-95).
 
+    behavior_feats in sparse-column order (the reference builds history_seq
+    and embed_seq_layers by iterating sparse_feature_columns, :44-46,73-78);
+    inputs['movie_id'] is [B, n_behaviour] (candidate_item[:, i], :79).
     p: 'sparse_tables' {feat: table} for non-behaviour sparse feats,
        'seq_tables' {feat: table} for behaviour feats, 'att' attention params,
-       'bn' (gamma, beta, mean, var, eps), 'dnn' [(kernel, bias, alpha)],
-       'out' (kernel, bias)."""
+       'bn' (gamma, beta, mean, var, eps), 'dnn' [(kernel, bias, act_params)]
+       with act_params = alpha [units] for dnn_act 'prelu' (Dense(unit,
+       activation=PReLU()), :51) or (alpha, mean, var, eps) for 'dice'
+       (Dense(unit, activation=Dice()), layer/interaction.py:410-425 at
+       inference), 'out' (kernel, bias)."""
     dense_in = np.concatenate([cast_inputs(inputs[f], dt).reshape(-1, 1) for f in dense_feats], -1)
     other_sparse = [f for f in sparse_feats if f not in behavior_feats]
     sp = np.concatenate([np.asarray(inputs[f]).reshape(-1, 1) for f in other_sparse], -1)
@@ -353,7 +359,7 @@ def din(inputs, p, dense_feats, sparse_feats, behavior_feats, dt=np.float64,
                             for i, f in enumerate(other_sparse)], -1)
     other = np.concatenate([other, dense_in], -1)
     hist = np.stack([np.asarray(inputs[f]) for f in behavior_feats], -1)  # [B,T,nb]
-    cand = np.asarray(inputs["movie_id"]).reshape(-1, 1)
+    cand = np.asarray(inputs["movie_id"]).reshape(hist.shape[0], -1)
     seq = np.concatenate([embedding_lookup(np.asarray(p["seq_tables"][f], dt), hist[:, :, i])
                           for i, f in enumerate(behavior_feats)], -1)
     item = np.concatenate([embedding_lookup(np.asarray(p["seq_tables"][f], dt), cand[:, i])
@@ -363,8 +369,14 @@ def din(inputs, p, dense_feats, sparse_feats, behavior_feats, dt=np.float64,
     emb = np.concatenate([att, item, other], -1)
     g, bt, mu, var, eps = p["bn"]
     emb = batchnorm_inference(emb, mu, var, g, bt, eps, dt=dt)
-    for kern, bias, alpha in p["dnn"]:
-        emb = dense(emb, kern, bias, "prelu", alpha, dt=dt)
+    for kern, bias, ap in p["dnn"]:
+        if dnn_act == "prelu":
+            emb = dense(emb, kern, bias, "prelu", ap, dt=dt)
+        elif dnn_act == "dice":
+            alpha, dmu, dvar, deps = ap
+            emb = dice(dense(emb, kern, bias, None, dt=dt), alpha, dmu, dvar, deps, dt=dt)
+        else:
+            raise ValueError(dnn_act)
     return sigmoid(dense(emb, p["out"][0], p["out"][1], dt=dt)), att
 
 

@@ -278,6 +278,67 @@ __global__ __launch_bounds__(ATT_WAVES * 64) void din_attention_dice(DiceArgs a)
   }
 }
 
+// Generic-depth 'prelu' path (any len(hidden_units), any H, k <= 64): the
+// activation-unit input e = [q, key_t, q-key_t, q*key_t] is formed once per
+// (b, t) row, every Dense(h, PReLU()) runs as an fp32 MFMA GEMM over the B*T
+// rows (rs_dense_prelu_rows_fwd: alpha [T, h] indexed by row mod T), the
+// Dense(1) score as the small-N GEMM, then the masked softmax + weighted sum.
+__global__ void att_concat_kernel(const float* __restrict__ q, const float* __restrict__ keys, int T, int k,
+                                  int64_t n, float* __restrict__ e) {
+  // n = B*T*k elements (b, t, j)
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t bt = i / k;
+    const int j = (int)(i - bt * k);
+    const int64_t b = bt / T;
+    const float qv = q[b * k + j], kv = keys[i];
+    float* row = e + bt * 4 * k;
+    row[j] = qv;
+    row[k + j] = kv;
+    row[2 * k + j] = qv - kv;
+    row[3 * k + j] = qv * kv;
+  }
+}
+
+__global__ __launch_bounds__(ATT_WAVES * 64) void att_masked_pool(const float* __restrict__ scores,
+                                                                  const float* __restrict__ mask,
+                                                                  const float* __restrict__ values, int T, int k,
+                                                                  float* __restrict__ out, int64_t batch) {
+  __shared__ float sbuf[ATT_WAVES][ATT_TMAX];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float* sc = sbuf[w];
+  for (int64_t b = (int64_t)blockIdx.x * ATT_WAVES + w; b < batch; b += (int64_t)gridDim.x * ATT_WAVES) {
+    for (int t = lane; t < T; t += 64) {
+      const float sv = scores[b * T + t];
+      sc[t] = mask[b * T + t] == 0.f ? -4294967296.0f : sv;
+    }
+    if (k <= 64) {
+      softmax_weighted_sum(sc, T, k, values, b, out, lane);
+      continue;
+    }
+    wave_lds_sync();
+    float mx = -INFINITY;
+    for (int t = lane; t < T; t += 64) mx = fmaxf(mx, sc[t]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    float sum = 0.f;
+    for (int t = lane; t < T; t += 64) {
+      const float ev = expf(sc[t] - mx);
+      sc[t] = ev;
+      sum += ev;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    wave_lds_sync();
+    const float* vb = values + b * (int64_t)T * k;
+    for (int j = lane; j < k; j += 64) {
+      float acc = 0.f;
+      for (int t = 0; t < T; ++t) acc = fmaf(sc[t] / sum, vb[(int64_t)t * k + j], acc);
+      out[b * k + j] = acc;
+    }
+    wave_lds_sync();
+  }
+}
+
 static unsigned att_grid(int64_t batch) {
   int64_t g = (batch + ATT_WAVES - 1) / ATT_WAVES;
   if (g > 4096) g = 4096;
@@ -340,4 +401,67 @@ extern "C" int rs_din_attention_dice_fwd(const float* query, const float* keys, 
              batch};
   din_attention_dice<<<att_grid(batch), ATT_WAVES * 64, 0, as_stream(stream)>>>(a);
   return launch_status("rs_din_attention_dice_fwd");
+}
+
+static int64_t att_gen_max_width(int k, int n_layers, const int* hidden) {
+  int64_t mx = 1;
+  for (int l = 0; l < n_layers; ++l) mx = hidden[l] > mx ? hidden[l] : mx;
+  (void)k;
+  return mx;
+}
+
+extern "C" int64_t rs_din_attention_gen_workspace_size(int64_t batch, int T, int k, int n_layers,
+                                                       const int* hidden) {
+  if (batch < 0 || T < 1 || k < 1 || n_layers < 0 || (n_layers > 0 && !hidden)) return -1;
+  for (int l = 0; l < n_layers; ++l)
+    if (hidden[l] < 1) return -1;
+  const int64_t rows = batch * T;
+  const int64_t h = att_gen_max_width(k, n_layers, hidden);
+  // e [rows, 4k] | ping / pong [rows, h] | scores [rows], each 256-B aligned
+  auto al = [](int64_t floats) { return (floats * 4 + 255) / 256 * 256; };
+  return al(rows * 4 * k) + 2 * al(rows * h) + al(rows);
+}
+
+extern "C" int rs_din_attention_gen_fwd(const float* query, const float* keys, const float* values,
+                                        const float* mask, int T, int k, int n_layers, const int* hidden,
+                                        const float* const* W, const float* const* b, const float* const* alpha,
+                                        const float* w_out, const float* b_out, float* out, int64_t batch,
+                                        void* workspace, int64_t workspace_bytes, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
+  RS_REQUIRE(query && keys && values && mask && w_out && b_out && out && workspace,
+             "rs_din_attention_gen_fwd: null pointer");
+  RS_REQUIRE(T >= 1 && T <= ATT_TMAX && k >= 1 && n_layers >= 0 && batch > 0,
+             "rs_din_attention_gen_fwd: bad shape (1 <= T <= %d)", ATT_TMAX);
+  RS_REQUIRE(n_layers == 0 || (hidden && W && b && alpha), "rs_din_attention_gen_fwd: null layer arrays");
+  for (int l = 0; l < n_layers; ++l)
+    RS_REQUIRE(hidden[l] >= 1 && W[l] && b[l] && alpha[l], "rs_din_attention_gen_fwd: bad layer %d", l);
+  const int64_t need = rs_din_attention_gen_workspace_size(batch, T, k, n_layers, hidden);
+  RS_REQUIRE(workspace_bytes >= need, "rs_din_attention_gen_fwd: workspace needs %lld bytes", (long long)need);
+  hipStream_t st = as_stream(stream);
+  const int64_t rows = batch * T;
+  const int64_t h = att_gen_max_width(k, n_layers, hidden);
+  auto al = [](int64_t floats) { return (floats * 4 + 255) / 256 * 256; };
+  uint8_t* ws = static_cast<uint8_t*>(workspace);
+  float* e = reinterpret_cast<float*>(ws);
+  float* buf[2] = {reinterpret_cast<float*>(ws + al(rows * 4 * k)),
+                   reinterpret_cast<float*>(ws + al(rows * 4 * k) + al(rows * h))};
+  float* scores = reinterpret_cast<float*>(ws + al(rows * 4 * k) + 2 * al(rows * h));
+  const int64_t n = rows * k;
+  int64_t g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  att_concat_kernel<<<(unsigned)g, 256, 0, st>>>(query, keys, T, k, n, e);
+  if (hipPeekAtLastError() != hipSuccess) return launch_status("rs_din_attention_gen_fwd");
+  const float* in = e;
+  int kin = 4 * k;
+  for (int l = 0; l < n_layers; ++l) {
+    const int rc = rs_dense_prelu_rows_fwd(in, kin, W[l], b[l], alpha[l], T, buf[l & 1], hidden[l], rows, kin,
+                                           hidden[l], stream);
+    if (rc != RS_OK) return rc;
+    in = buf[l & 1];
+    kin = hidden[l];
+  }
+  const int rc = rs_dense_fwd(in, kin, w_out, b_out, nullptr, RS_ACT_NONE, scores, 1, rows, kin, 1, stream);
+  if (rc != RS_OK) return rc;
+  att_masked_pool<<<att_grid(batch), ATT_WAVES * 64, 0, st>>>(scores, mask, values, T, k, out, batch);
+  return launch_status("rs_din_attention_gen_fwd");
 }

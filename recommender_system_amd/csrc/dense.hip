@@ -29,7 +29,14 @@ struct DenseArgs {
   int64_t ys;
   int64_t M;
   int K, N;
+  int arows;  // PReLU alpha rows: 1 = alpha[n]; > 1 = alpha[(m % arows) * N + n]
 };
+
+// PReLU slope of output (m, n): per column, or per (row mod arows, column) —
+// Keras PReLU() on a 3-D input [B, T, N] flattened to [B*T, N] has alpha [T, N]
+__device__ __forceinline__ float prelu_alpha(const DenseArgs& a, int64_t m, int n, float col_alpha) {
+  return a.arows > 1 ? a.alpha[(m % a.arows) * a.N + n] : col_alpha;
+}
 
 __device__ __forceinline__ float apply_act(float v, int act, float alpha) {
   switch (act) {
@@ -96,11 +103,12 @@ __global__ __launch_bounds__(256) void dense_mfma(DenseArgs a) {
   const int n = n0 + wn * 32 + li;
   if (n < a.N) {
     const float bz = a.bias ? a.bias[n] : 0.f;
-    const float al = (a.act == RS_ACT_PRELU && a.alpha) ? a.alpha[n] : 0.f;
+    const bool pre = a.act == RS_ACT_PRELU && a.alpha;
+    const float al = (pre && a.arows <= 1) ? a.alpha[n] : 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int64_t m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-      if (m < a.M) a.y[m * a.ys + n] = apply_act(acc[r] + bz, a.act, al);
+      if (m < a.M) a.y[m * a.ys + n] = apply_act(acc[r] + bz, a.act, pre ? prelu_alpha(a, m, n, al) : 0.f);
     }
   }
 }
@@ -119,7 +127,7 @@ __global__ __launch_bounds__(256) void dense_small_n(DenseArgs a) {
       for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o);
       if (lane == 0) {
         const float bz = a.bias ? a.bias[n] : 0.f;
-        const float al = (a.act == RS_ACT_PRELU && a.alpha) ? a.alpha[n] : 0.f;
+        const float al = (a.act == RS_ACT_PRELU && a.alpha) ? prelu_alpha(a, m, n, a.alpha[n]) : 0.f;
         a.y[m * a.ys + n] = apply_act(p + bz, a.act, al);
       }
     }
@@ -157,6 +165,18 @@ static unsigned ew_grid(int64_t n) {
 
 using namespace rs;
 
+static int dense_launch(const DenseArgs& a, hipStream_t st, const char* what) {
+  if (a.N <= 4) {
+    int64_t g = (a.M * 64 + 255) / 256;
+    if (g > 4096) g = 4096;
+    dense_small_n<<<(unsigned)g, 256, 0, st>>>(a);
+  } else {
+    dim3 grid((a.N + GBN - 1) / GBN, (unsigned)((a.M + GBM - 1) / GBM));
+    dense_mfma<<<grid, 256, 0, st>>>(a);
+  }
+  return launch_status(what);
+}
+
 extern "C" int rs_dense_fwd(const float* x, int64_t x_stride, const float* W, const float* bias, const float* alpha,
                             int act, float* y, int64_t y_stride, int64_t M, int K, int N, rs_stream_t stream) {
   if (M == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
@@ -165,18 +185,20 @@ extern "C" int rs_dense_fwd(const float* x, int64_t x_stride, const float* W, co
   RS_REQUIRE(act >= RS_ACT_NONE && act <= RS_ACT_SIGMOID, "rs_dense_fwd: bad activation");
   RS_REQUIRE(act != RS_ACT_PRELU || alpha, "rs_dense_fwd: PReLU needs alpha");
   RS_REQUIRE((M + GBM - 1) / GBM < 65536, "rs_dense_fwd: M too large for one launch");
-  if (M == 0) return RS_OK;
-  DenseArgs a{x, x_stride, W, bias, alpha, act, y, y_stride, M, K, N};
-  hipStream_t st = as_stream(stream);
-  if (N <= 4) {
-    int64_t g = (M * 64 + 255) / 256;
-    if (g > 4096) g = 4096;
-    dense_small_n<<<(unsigned)g, 256, 0, st>>>(a);
-  } else {
-    dim3 grid((N + GBN - 1) / GBN, (unsigned)((M + GBM - 1) / GBM));
-    dense_mfma<<<grid, 256, 0, st>>>(a);
-  }
-  return launch_status("rs_dense_fwd");
+  DenseArgs a{x, x_stride, W, bias, alpha, act, y, y_stride, M, K, N, 1};
+  return dense_launch(a, as_stream(stream), "rs_dense_fwd");
+}
+
+extern "C" int rs_dense_prelu_rows_fwd(const float* x, int64_t x_stride, const float* W, const float* bias,
+                                       const float* alpha, int alpha_rows, float* y, int64_t y_stride, int64_t M,
+                                       int K, int N, rs_stream_t stream) {
+  if (M == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
+  RS_REQUIRE(x && W && y && alpha, "rs_dense_prelu_rows_fwd: null pointer");
+  RS_REQUIRE(M >= 0 && K >= 1 && N >= 1 && x_stride >= K && y_stride >= N && alpha_rows >= 1,
+             "rs_dense_prelu_rows_fwd: bad shape");
+  RS_REQUIRE((M + GBM - 1) / GBM < 65536, "rs_dense_prelu_rows_fwd: M too large for one launch");
+  DenseArgs a{x, x_stride, W, bias, alpha, RS_ACT_PRELU, y, y_stride, M, K, N, alpha_rows};
+  return dense_launch(a, as_stream(stream), "rs_dense_prelu_rows_fwd");
 }
 
 extern "C" int rs_affine_act(const float* x, int64_t x_stride, const float* scale, const float* shift,

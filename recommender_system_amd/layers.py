@@ -670,9 +670,6 @@ class Attention(KerasModule):
         self.T = T
         n = 4 * k
         if self.activation == "prelu":
-            if len(self.hidden_units) != 2:
-                raise NotImplementedError("Attention(prelu): the fused kernel implements the reference's "
-                                          "two hidden layers (hidden_units of length 2)")
             for h in self.hidden_units:
                 self.kernels.append(nn.Parameter(_glorot_uniform(n, h, self._gen, self._dev), requires_grad=False))
                 self.biases.append(nn.Parameter(torch.zeros(h, device=self._dev), requires_grad=False))
@@ -686,10 +683,17 @@ class Attention(KerasModule):
         self.out_kernel = nn.Parameter(_glorot_uniform(n, 1, self._gen, self._dev), requires_grad=False)
         self.out_bias = nn.Parameter(torch.zeros(1, device=self._dev), requires_grad=False)
 
+    def fused_ok(self, k):
+        """The one-launch MFMA kernel (rs_din_attention_fwd) takes the shape:
+        the reference's two hidden layers, H <= 128, k in {4, 8, 16, 32}.
+        Other depths / sizes run the generic path (rs_din_attention_gen_fwd)."""
+        return (self.activation == "prelu" and len(self.hidden_units) == 2 and k in (4, 8, 16, 32)
+                and max(self.hidden_units) <= 128)
+
     def ids_ok(self, k):
         """The id-driven fused path (rs_din_attention_ids_fwd) supports it."""
-        return (self.activation == "prelu" and self.out_kernel is not None and k in (4, 8, 16)
-                and self.hidden_units[0] <= 128 and self.hidden_units[1] <= 64)
+        return (self.activation == "prelu" and self.out_kernel is not None and len(self.hidden_units) == 2
+                and k in (4, 8, 16) and self.hidden_units[0] <= 128 and self.hidden_units[1] <= 64)
 
     def prepared_ids(self, k):
         params = list(self.kernels) + list(self.biases) + list(self.alphas) + [self.out_kernel, self.out_bias]
@@ -754,6 +758,7 @@ class Attention(KerasModule):
         key = _to_device_f32(key, self._dev)
         value = key if value is None else _to_device_f32(value, self._dev)
         mask = _to_device_f32(mask, self._dev)
+        q, key, value, mask = (t.contiguous() for t in (q, key, value, mask))  # the kernels take dense rows
         B, T, k = key.shape
         if self.out_kernel is None:
             self.build(T, k)
@@ -762,7 +767,19 @@ class Attention(KerasModule):
         if out is None:
             out = torch.empty(B, k, dtype=torch.float32, device=self._dev)
         s = _stream()
-        if self.activation == "prelu":
+        if self.activation == "prelu" and not self.fused_ok(k):
+            n = len(self.hidden_units)
+            hid = (C.c_int * max(n, 1))(*self.hidden_units)
+            wsz = _lib.lib().rs_din_attention_gen_workspace_size(B, T, k, n, hid)
+            if wsz < 0:
+                _lib.check(-1, "rs_din_attention_gen_workspace_size")
+            ws = self.__dict__.get("_gen_ws")
+            if ws is None or ws.numel() < wsz:
+                ws = self.__dict__["_gen_ws"] = torch.empty(wsz, dtype=torch.uint8, device=self._dev)
+            pa = lambda ts: (C.c_void_p * max(n, 1))(*[ptr(t) for t in ts])
+            call("rs_din_attention_gen_fwd", ptr(q), ptr(key), ptr(value), ptr(mask), T, k, n, hid, pa(self.kernels), pa(self.biases), pa(self.alphas),
+                 ptr(self.out_kernel), ptr(self.out_bias), ptr(out), B, ptr(ws), ws.numel(), s)
+        elif self.activation == "prelu":
             h1, h2 = self.hidden_units
             call("rs_din_attention_fwd", ptr(q), ptr(key), ptr(value), ptr(mask), T, k, ptr(self.kernels[0]),
                  ptr(self.biases[0]), ptr(self.alphas[0]), h1, ptr(self.kernels[1]), ptr(self.biases[1]),

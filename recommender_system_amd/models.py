@@ -580,7 +580,11 @@ class DIN(TowerMixin, KerasModule):
     """DIN — model/din.py:15-95.  ``forward(inputs)`` takes the reference's
     dict: each dense / non-behaviour sparse feature [B,1] (or [B]), each
     behaviour feature [B,T] (0 = padding), and the candidate under the
-    hard-coded key 'movie_id' (model/din.py:74)."""
+    hard-coded key 'movie_id' (model/din.py:74) as [B, n_behaviour]: column i
+    is the candidate's id for behaviour feature i (e.g. item id and category
+    id, :73,77-79).  Behaviour features are taken in sparse-column order; their
+    embeddings are concatenated along k and the mask comes from the first
+    (:80)."""
 
     def __init__(self, feature_columns, behavior_feature_list, att_hidden_units=(80, 40),
                  dnn_hidden_units=(256, 128, 64), att_attention="prelu", dnn_activation="prelu", dnn_dropout=0.0,
@@ -590,8 +594,8 @@ class DIN(TowerMixin, KerasModule):
         self.behavior_feature_list = list(behavior_feature_list)
         self.other_sparse = [f for f in self.sparse_feature_columns if f["feat"] not in self.behavior_feature_list]
         self.seq_feats = [f for f in self.sparse_feature_columns if f["feat"] in self.behavior_feature_list]
-        if len(self.seq_feats) != 1:
-            raise NotImplementedError("DIN: exactly one behaviour feature (the reference's use) is supported")
+        if not self.seq_feats:
+            raise ValueError("DIN: behavior_feature_list names no sparse feature column")
         self.other_sparse_num = len(self.other_sparse)
         self.dense_num = len(self.dense_feature_columns)
         self.behavior_num = len(self.behavior_feature_list)
@@ -609,32 +613,48 @@ class DIN(TowerMixin, KerasModule):
         self.out_layer = Dense(1, activation="sigmoid", device=dev, seed=_subseed(self._gen))
         self._err = _ErrFlag(self._dev)
 
+    def _behaviour_embed(self, ids_cols, rows, check_ids):
+        """[rows, K] = concat_i embed_seq_layers[i](ids_cols[i]) along k."""
+        K = sum(l.k for l in self.embed_seq_layers)
+        out = torch.empty(rows, K, dtype=torch.float32, device=self._dev)
+        col = 0
+        for ids, layer in zip(ids_cols, self.embed_seq_layers):
+            layer.gather(ids, out=out[:, col:col + layer.k], check_ids=check_ids)
+            col += layer.k
+        return out
+
     def forward(self, inputs, check_ids=True):
         dev = self._dev
-        seq_layer = self.embed_seq_layers[0]
-        k = seq_layer.k
-        hist = _ids_tensor(inputs[self.seq_feats[0]["feat"]], dev)
-        B, T = hist.shape
-        cand = _ids_tensor(inputs["movie_id"], dev).reshape(B, 1)
-        item_embed = seq_layer.gather(cand, check_ids=check_ids)
+        nb = len(self.seq_feats)
+        hists = [_ids_tensor(inputs[f["feat"]], dev) for f in self.seq_feats]
+        B, T = hists[0].shape
+        if any(h.shape != (B, T) for h in hists):
+            raise ValueError("DIN: every behaviour feature must be [B, T]")
+        cand = _ids_tensor(inputs["movie_id"], dev).reshape(B, -1)
+        if cand.shape[1] != nb:
+            raise ValueError(f"DIN: inputs['movie_id'] needs one candidate id per behaviour feature ({nb})")
+        K = sum(l.k for l in self.embed_seq_layers)
+        item_embed = self._behaviour_embed([cand[:, i:i + 1] for i in range(nb)], B, check_ids)
         if self.att_layer.out_kernel is None:
-            self.att_layer.build(T, k)
-        if self.att_layer.ids_ok(k):
+            self.att_layer.build(T, K)
+        if nb == 1 and self.att_layer.ids_ok(K):
             # keys/values read through the ids from the (L2-resident) table
-            att_emb = self.att_layer.forward_ids(seq_layer.table, int(seq_layer.vocab_sizes[0]), hist, cand,
+            seq_layer = self.embed_seq_layers[0]
+            att_emb = self.att_layer.forward_ids(seq_layer.table, int(seq_layer.vocab_sizes[0]), hists[0], cand,
                                                  err=self._err.t)
             if check_ids:
                 self._err.check("DIN")
         else:
-            seq_embed = seq_layer.gather(hist.reshape(B * T, 1), check_ids=check_ids).reshape(B, T, k)
-            mask = (hist != 0).to(torch.float32)
+            seq_embed = self._behaviour_embed([h.reshape(B * T, 1) for h in hists], B * T, check_ids)
+            seq_embed = seq_embed.view(B, T, K)
+            mask = (hists[0] != 0).to(torch.float32)  # model/din.py:80: the first behaviour feature
             att_emb = self.att_layer([item_embed, seq_embed, seq_embed, mask])
         other_k = sum(l.k for l in self.embed_sparse_layers)
-        width = 2 * k + other_k + self.dense_num
+        width = 2 * K + other_k + self.dense_num
         emb = torch.empty(B, width, dtype=torch.float32, device=dev)
-        emb[:, :k] = att_emb
-        emb[:, k:2 * k] = item_embed
-        col = 2 * k
+        emb[:, :K] = att_emb
+        emb[:, K:2 * K] = item_embed
+        col = 2 * K
         for f, layer in zip(self.other_sparse, self.embed_sparse_layers):
             ids = _ids_tensor(inputs[f["feat"]], dev).reshape(B, 1)
             layer.gather(ids, out=emb[:, col:col + layer.k], check_ids=check_ids)

@@ -1,0 +1,175 @@
+"""DIN model end to end (a15: model/din.py:15-95) against the oracle's
+O.din, which restates DIN.call op for op (Keras Embedding / Attention / BN at
+inference / PReLU or Dice Dense / sigmoid).
+
+GPU: the config-4 shape (Amazon-Electronics-shaped: B 2048, T 100, k 8,
+behaviour vocab 63,001, 1 dense + a user-id sparse feature of 192,404 ids),
+padded histories and a fully padded row, non-trivial BatchNormalization
+moving statistics, random PReLU / Dice parameters; dnn_activation 'prelu' and
+'dice'; two behaviour features (item + category ids concatenated along k,
+model/din.py:73,77-79); attention depths other than the reference's two
+hidden layers.  Post-sigmoid outputs at 1e-5 relative."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ctr_oracle as O
+from tests.helpers import assert_rel_close
+
+C = lambda t: t.detach().cpu().numpy()
+
+
+def din_columns(n_behaviour, k, item_vocab=63001, cate_vocab=801, user_vocab=192404):
+    dense = [{"feat": "price"}]
+    sparse = [{"feat": "user_id", "feat_onehot_dim": user_vocab, "embed_dim": k},
+              {"feat": "movie_seq", "feat_onehot_dim": item_vocab, "embed_dim": k}]
+    if n_behaviour > 1:
+        sparse.append({"feat": "cate_seq", "feat_onehot_dim": cate_vocab, "embed_dim": k})
+    behaviour = [f["feat"] for f in sparse[1:]]
+    return [dense, sparse], behaviour
+
+
+def din_inputs(rng, cols, behaviour, B, T):
+    dense, sparse = cols
+    lens = rng.integers(1, T + 1, size=B)
+    lens[0] = 0  # fully padded history -> uniform average of the padding rows
+    lens[1] = T
+    valid = np.arange(T)[None, :] < lens[:, None]
+    inputs = {}
+    for f in sparse:
+        V = f["feat_onehot_dim"]
+        if f["feat"] in behaviour:
+            inputs[f["feat"]] = np.where(valid, rng.integers(1, V, size=(B, T)), 0).astype(np.int64)
+        else:
+            inputs[f["feat"]] = rng.integers(0, V, size=(B, 1)).astype(np.int64)
+    for f in dense:
+        inputs[f["feat"]] = rng.random((B, 1)).astype(np.float32)
+    vocab = {f["feat"]: f["feat_onehot_dim"] for f in sparse}
+    cand = np.stack([rng.integers(0, vocab[b], size=B) for b in behaviour], 1)
+    cand[2] = [vocab[b] - 1 for b in behaviour]  # last row of each behaviour table
+    inputs["movie_id"] = cand.astype(np.int64)
+    return inputs
+
+
+def randomize(model, rng):
+    """Non-trivial values for every parameter the reference initialises to a
+    constant (PReLU / Dice alphas, BN statistics, biases)."""
+    u = lambda t, lo, hi: t.copy_(torch.as_tensor(rng.uniform(lo, hi, size=tuple(t.shape)), dtype=torch.float32))
+    with torch.no_grad():
+        for L in model.embed_seq_layers:
+            L.table.mul_(10.0)  # O(0.5) embeddings: the attention scores spread
+        att = model.att_layer
+        for a in att.alphas:
+            u(a, -0.5, 0.5)
+        for b in att.biases:
+            u(b, -0.1, 0.1)
+        for d in att.dice:
+            u(d.alphas, -0.5, 0.5)
+            u(d.moving_mean, -0.1, 0.1)
+            u(d.moving_variance, 0.5, 1.5)
+        bn = model.bn_layer
+        u(bn.gamma, 0.5, 1.5)
+        u(bn.beta, -0.1, 0.1)
+        u(bn.moving_mean, -0.05, 0.05)
+        u(bn.moving_variance, 0.5, 2.0)
+        for L in list(model.dense_layer) + [model.out_layer]:
+            u(L.bias, -0.1, 0.1)
+            if L.alpha is not None:
+                u(L.alpha, -0.5, 0.5)
+            if L.dice is not None:
+                u(L.dice.alphas, -0.5, 0.5)
+                u(L.dice.moving_mean, -0.2, 0.2)
+                u(L.dice.moving_variance, 0.5, 1.5)
+    model._weights_changed()
+
+
+def din_params(model):
+    att = model.att_layer
+    p_att = {"out": (C(att.out_kernel), C(att.out_bias))}
+    if att.activation == "prelu":
+        p_att["prelu"] = [(C(att.kernels[i]), C(att.biases[i]), C(att.alphas[i])) for i in range(len(att.kernels))]
+    else:
+        p_att["dice"] = [(C(d.alphas), C(d.moving_mean), C(d.moving_variance), d.epsilon) for d in att.dice]
+    dnn = []
+    for L in model.dense_layer:
+        ap = C(L.alpha) if L.activation == "prelu" else (C(L.dice.alphas), C(L.dice.moving_mean),
+                                                          C(L.dice.moving_variance), L.dice.epsilon)
+        dnn.append((C(L.kernel), C(L.bias), ap))
+    bn = model.bn_layer
+    return {"sparse_tables": {f["feat"]: L.field_table(0).cpu().numpy()
+                              for f, L in zip(model.other_sparse, model.embed_sparse_layers)},
+            "seq_tables": {f["feat"]: L.field_table(0).cpu().numpy()
+                           for f, L in zip(model.seq_feats, model.embed_seq_layers)},
+            "att": p_att, "bn": (C(bn.gamma), C(bn.beta), C(bn.moving_mean), C(bn.moving_variance), bn.epsilon),
+            "dnn": dnn, "out": (C(model.out_layer.kernel), C(model.out_layer.bias))}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dnn_act,att_act,att_hidden,nb,k,B,T", [
+    ("prelu", "prelu", (80, 40), 1, 8, 2048, 100),     # config 4, the reference's defaults (id-driven attention)
+    ("dice", "prelu", (80, 40), 1, 8, 2048, 100),      # config 4, dnn_activation='dice'
+    ("prelu", "prelu", (80, 40), 2, 8, 512, 100),      # item + category behaviour (K = 16, fused attention)
+    ("dice", "dice", (80, 40), 2, 8, 300, 30),         # att_attention='dice' on two behaviour features
+    ("prelu", "prelu", (64,), 1, 8, 256, 100),         # one attention hidden layer (generic path)
+    ("prelu", "prelu", (80, 40, 20), 2, 4, 256, 50),   # three hidden layers (generic path), K = 8
+    ("prelu", "prelu", (200, 40), 1, 8, 128, 20),      # H > 128 (generic path)
+])
+def test_din_model(gpu, dnn_act, att_act, att_hidden, nb, k, B, T):
+    from recommender_system_amd import DIN
+    rng = np.random.default_rng(B + T + nb * 7 + len(att_hidden))
+    cols, behaviour = din_columns(nb, k)
+    model = DIN(cols, behaviour, att_hidden_units=att_hidden, att_attention=att_act, dnn_activation=dnn_act,
+                seed=11)
+    inputs = din_inputs(rng, cols, behaviour, B, T)
+    model(inputs)  # builds the lazily-shaped layers (Keras build on first call)
+    randomize(model, rng)
+    y = model(inputs)
+    sparse = [f["feat"] for f in cols[1]]
+    ref, att = O.din(inputs, din_params(model), [f["feat"] for f in cols[0]], sparse,
+                     [f for f in sparse if f in behaviour], att_act=att_act, dnn_act=dnn_act)
+    assert_rel_close(y, ref, what=f"DIN {dnn_act}/{att_act} {att_hidden} nb={nb}")
+    # the fully padded row attends uniformly; its output is still finite
+    assert np.isfinite(y.cpu().numpy()).all()
+
+
+@pytest.mark.gpu
+def test_din_model_bad_ids(gpu):
+    """An out-of-range behaviour / candidate id raises IndexError (Keras
+    Embedding's InvalidArgumentError on CPU)."""
+    from recommender_system_amd import DIN
+    rng = np.random.default_rng(5)
+    cols, behaviour = din_columns(2, 8)
+    model = DIN(cols, behaviour, seed=1)
+    inputs = din_inputs(rng, cols, behaviour, 64, 20)
+    model(inputs)
+    for key, val in (("cate_seq", 801), ("movie_id", 63001)):
+        bad = {k_: v.copy() for k_, v in inputs.items()}
+        if key == "movie_id":
+            bad[key][3, 0] = val
+        else:
+            bad[key][3, 0] = val
+        with pytest.raises(IndexError):
+            model(bad)
+
+
+def test_oracle_din_two_behaviours_is_concat():
+    """CPU: O.din with two behaviour features equals the attention over the
+    k-concatenated embeddings with the mask of the first feature."""
+    rng = np.random.default_rng(3)
+    B, T, k = 6, 7, 4
+    cols, behaviour = din_columns(2, k, item_vocab=50, cate_vocab=9, user_vocab=11)
+    inputs = din_inputs(rng, cols, behaviour, B, T)
+    tabs = {f["feat"]: rng.standard_normal((f["feat_onehot_dim"], k)) for f in cols[1]}
+    att = {"prelu": [(rng.standard_normal((8 * k, 5)), rng.standard_normal(5), rng.standard_normal((T, 5)))],
+           "out": (rng.standard_normal((5, 1)), rng.standard_normal(1))}
+    width = 2 * 2 * k + k + 1
+    p = {"sparse_tables": {"user_id": tabs["user_id"]}, "seq_tables": {b: tabs[b] for b in behaviour}, "att": att,
+         "bn": (np.ones(width), np.zeros(width), np.zeros(width), np.ones(width), 1e-3),
+         "dnn": [(rng.standard_normal((width, 3)), np.zeros(3), np.zeros(3))],
+         "out": (rng.standard_normal((3, 1)), np.zeros(1))}
+    _, a = O.din(inputs, p, ["price"], ["user_id"] + behaviour, behaviour)
+    seq = np.concatenate([tabs[b][inputs[b]] for b in behaviour], -1)
+    item = np.concatenate([tabs[b][inputs["movie_id"][:, i]] for i, b in enumerate(behaviour)], -1)
+    mask = (inputs[behaviour[0]] != 0).astype(np.float64)
+    np.testing.assert_allclose(a, O.attention(item, seq, seq, mask, att), rtol=1e-12)
+    np.testing.assert_allclose(a[0], seq[0].mean(0), rtol=1e-12)  # fully padded row: uniform average
