@@ -569,6 +569,40 @@ def bench_sharded_deepfm(args, world, rank):
     return res, V
 
 
+def _cpu_leg(args, rank, B, run_batch, n_pool, what, gpu_batch0=None, max_batches=64, kind_scale="scaled"):
+    """`cpu_baseline` of a config line: the oracle's numpy fp32 op-for-op
+    restatement of that config's step (the reference's TF graph; TF is not
+    installed) on host copies of the same batches, a bounded sample of about
+    --cpu-budget seconds on rank 0.  gpu_batch0(): the GPU step's output for
+    batch 0, compared with the CPU's (max |a-b| / max(|b|, rms(b)))."""
+    if not args.cpu_baseline or rank != 0:
+        return None
+    n, first, t0 = 0, None, time.perf_counter()
+    while n < max_batches and (time.perf_counter() - t0) < args.cpu_budget:
+        y = run_batch(n % n_pool)
+        if first is None:
+            first = np.asarray(y, np.float64)
+        n += 1
+    dt = time.perf_counter() - t0
+    res = {"value": n * B / dt, "unit": "samples/s", "cores": _cpu_threads(), "kind": "port",
+           "sample": f"{n} batches x {B} samples of this config's step ({what}); numpy fp32 oracle = the "
+                     f"reference TF graph restated (TF not installed); host copies of the same tables and batches"}
+    if gpu_batch0 is not None and first is not None:
+        g = np.asarray(gpu_batch0(), np.float64).reshape(first.shape)
+        rms = float(np.sqrt(np.mean(first ** 2))) or 1.0
+        res["max_scaled_diff_vs_gpu"] = float(np.max(np.abs(g - first) / np.maximum(np.abs(first), rms)))
+    return res
+
+
+def _host_tables(embed_layer):
+    t = embed_layer.table.detach().cpu().numpy()
+    return [t[o:o + v] for o, v in zip(embed_layer.row_offsets, embed_layer.vocab_sizes)]
+
+
+def _host_pool(ids_pool, dense_pool, n=8):
+    return ids_pool[:n].cpu().numpy(), dense_pool[:n].cpu().numpy()
+
+
 def _line(metric, value, unit, args, world, ms_per_step, config, roofline, extra=None, dtype="f32", hib=True):
     out = {"metric": metric, "value": value, "unit": unit, "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": hib, "scaling": "weak",
@@ -627,6 +661,23 @@ def bench_dcn(args, world, rank):
         model((dense_pool[j], ids_pool[j]), check_ids=False)
 
     dt2, _ = _timed_graph(full, n2, args.warmup, world, chunk=16)
+    cpu = None
+    if args.cpu_baseline and rank == 0:
+        from oracle import ctr_oracle as O
+        tables = _host_tables(model.embed_layer)
+        ws = [w.detach().cpu().numpy() for w in model.cross_layer.cross_weight]
+        bs = [b.detach().cpu().numpy() for b in model.cross_layer.cross_bias]
+        ids_h, dense_h = _host_pool(ids_pool, dense_pool)
+
+        def cpu_step(j):
+            x0 = np.concatenate([dense_h[j], O.embed_layer(ids_h[j], tables, np.float32)], 1)
+            return O.cross_layer(x0, ws, bs, np.float32)
+
+        def gpu0():
+            step(0)
+            return y.cpu().numpy()
+
+        cpu = _cpu_leg(args, rank, B, cpu_step, 8, "EmbedLayer + concat + CrossLayer depth 3 -> x_L", gpu0)
     return _line("DCN CrossNet forward samples/sec @ batch 4096, 26 sparse x 1e6 vocab, dim 16, depth 3",
                  args.steps * B / dt, "samples/s", args, world, kern_ms,
                  {"workload": "dcn_embed+crossnet_depth3_fused", "global_batch": B, "d": d, "layer_num": 3,
@@ -639,7 +690,8 @@ def bench_dcn(args, world, rank):
                  {"two_launch_gather_then_cross": {"samples_per_s": args.steps * B / dt_two,
                                                    "cross_mfma_kernel_ms": cross_ms,
                                                    "cross_mfma_hbm_frac": (B * 2 * d * 4) / (cross_ms * 1e-3) / PEAK_HBM},
-                  "dcn_forward": {"samples_per_s": n2 * B / dt2, "ms_per_step": dt2 / n2 * 1e3}})
+                  "dcn_forward": {"samples_per_s": n2 * B / dt2, "ms_per_step": dt2 / n2 * 1e3},
+                  "cpu_baseline": cpu})
 
 
 def bench_din(args, world, rank):
@@ -703,6 +755,27 @@ def bench_din(args, world, rank):
         model(pool[i % 8], check_ids=False)
 
     dt2, _ = _timed_graph(full, n2, args.warmup, world, chunk=8)
+    cpu = None
+    if args.cpu_baseline and rank == 0:
+        from oracle import ctr_oracle as O
+        table_h = table.detach().cpu().numpy()
+        c_ = lambda t: t.detach().cpu().numpy()
+        params = {"prelu": [(c_(att.kernels[i]), c_(att.biases[i]), c_(att.alphas[i])) for i in range(2)],
+                  "out": (c_(att.out_kernel), c_(att.out_bias))}
+        hist_h = [p["movies_seq"].cpu().numpy() for p in pool]
+        cand_h = [p["movie_id"].cpu().numpy()[:, 0] for p in pool]
+
+        def cpu_step(j):
+            key = table_h[hist_h[j]]
+            return O.attention(table_h[cand_h[j]], key, key, (hist_h[j] != 0).astype(np.float32), params, "prelu",
+                               dt=np.float32)
+
+        def gpu0():
+            step(0)
+            return out.cpu().numpy()
+
+        cpu = _cpu_leg(args, rank, B, cpu_step, 8, "Attention 'prelu' (80, 40) on table[hist], table[cand], mask "
+                                                  "= hist != 0", gpu0)
     return _line("DIN forward samples/sec @ batch 2048, behaviour seq len 100 (attention unit)",
                  args.steps * B / dt, "samples/s", args, world, att_ms,
                  {"workload": "din_attention_unit_from_ids", "global_batch": B, "seq_len": T, "embed_dim": k,
@@ -718,7 +791,8 @@ def bench_din(args, world, rank):
                                              "ms_per_step": dt_old / args.steps * 1e3},
                   "din_forward": {"samples_per_s": n2 * B / dt2, "ms_per_step": dt2 / n2 * 1e3,
                                   "note": "graph-replayed full DIN.call (id checks off): gathers, attention "
-                                          "from ids, BN, PReLU MLP + sigmoid head"}})
+                                          "from ids, BN, PReLU MLP + sigmoid head"},
+                  "cpu_baseline": cpu})
 
 
 def bench_pnn(args, world, rank):
@@ -751,6 +825,20 @@ def bench_pnn(args, world, rank):
     n2 = max(10, args.steps // 5)
     dtb, slotb = _timed_graph(step_both, n2, args.warmup, world)
     dtf, _ = _timed_graph(full, n2, args.warmup, world, chunk=16)
+    cpu = None
+    if args.cpu_baseline and rank == 0:
+        from oracle import ctr_oracle as O
+        tables = _host_tables(model.embed_layer)
+        ids_h, dense_h = _host_pool(ids_pool, dense_pool)
+
+        def cpu_step(j):
+            flat = O.embed_layer(ids_h[j], tables, np.float32)
+            return np.concatenate([flat, O.inner_product_layer(flat.reshape(B, F, k), np.float32)], 1)
+
+        def gpu0():
+            return model.product_inputs((dense_pool[0], ids_pool[0]), check_ids=False).cpu().numpy()
+
+        cpu = _cpu_leg(args, rank, B, cpu_step, 8, "EmbedLayer (3-D) + InnerProductLayer -> [flat | inner]", gpu0)
     return _line("PNN inner-product input samples/sec @ batch 4096, 26 sparse x 1e6 vocab, dim 16",
                  args.steps * B / dt, "samples/s", args, world, dt / args.steps * 1e3,
                  {"workload": "pnn_embed_inner_fused", "global_batch": B, "vocab_per_field": V, "parallelism": "dp1"},
@@ -761,7 +849,8 @@ def bench_pnn(args, world, rank):
                                 "outer_mfma_tflops": B * P * k * k * 2 / (slotb * 1e-3) / 1e12,
                                 "note": "[flat | inner | outer] in one launch (rs_embed_product_fwd)"},
                   "pnn_inner_forward": {"samples_per_s": n2 * B / dtf, "ms_per_step": dtf / n2 * 1e3,
-                                        "note": "product inputs + DNN tower (rs_mlp_fwd, K = 741)"}})
+                                        "note": "product inputs + DNN tower (rs_mlp_fwd, K = 741)"},
+                  "cpu_baseline": cpu})
 
 
 def _rank3_setup(args, k, nd=13):
@@ -800,10 +889,25 @@ def bench_nfm(args, world, rank):
     n2 = max(10, args.steps // 5)
     dtf, _ = _timed_graph(full, n2, args.warmup, world, chunk=16)
     alg = B * (F * 4 + F * k * 4 + 13 * 4 + (13 + k) * 4)
+    cpu = None
+    if args.cpu_baseline and rank == 0:
+        from oracle import ctr_oracle as O
+        tables = _host_tables(m.emb_layers)
+        ids_h, dense_h = _host_pool(ids_pool, dense_pool)
+
+        def cpu_step(j):
+            flat = O.embed_layer(ids_h[j], tables, np.float32)
+            return np.concatenate([dense_h[j], O.bi_interaction(flat.reshape(B, F, k), np.float32)], 1)
+
+        def gpu0():
+            return m.bi_interaction_input((dense_pool[0], ids_pool[0]), check_ids=False).cpu().numpy()
+
+        cpu = _cpu_leg(args, rank, B, cpu_step, 8, "EmbedLayer (3-D) + Bi-Interaction -> [dense | pooled]", gpu0)
     return _hbm_line("NFM bi-interaction input samples/sec @ batch 4096, 26 sparse x 1e6 vocab, dim 16", args,
                      world, B, dt, slot, alg, "nfm_embed_bi_interaction_fused", V, "pair_pool_kernel (sum)",
                      {"nfm_forward": {"samples_per_s": n2 * B / dtf, "ms_per_step": dtf / n2 * 1e3,
-                                      "note": "bi-interaction launch + BN + DNN 29-256-128-64-1 + Dense(1) tower"}})
+                                      "note": "bi-interaction launch + BN + DNN 29-256-128-64-1 + Dense(1) tower"},
+                      "cpu_baseline": cpu})
 
 
 def bench_afm(args, world, rank):
@@ -825,10 +929,33 @@ def bench_afm(args, world, rank):
     dt, slot = _timed_graph(step, args.steps, args.warmup, world)
     dtm, slotm = _timed_graph(step_max, args.steps, args.warmup, world)
     alg = B * (F * 4 + F * k * 4 + 4)
+    cpu = None
+    if args.cpu_baseline and rank == 0:
+        from oracle import ctr_oracle as O
+        L = m.afm_layer
+        c_ = lambda t: t.detach().cpu().numpy()
+        m((dense_pool[0], ids_pool[0]), check_ids=False)  # attention weights are built on the first call
+        a = L.attention_layer
+        p = {"tables": _host_tables(L.embed_layer), "out_kernel": c_(L.output_layer.kernel),
+             "out_bias": c_(L.output_layer.bias)}
+        if a.attention_w is not None:
+            p.update({"att_w_kernel": c_(a.attention_w.kernel), "att_w_bias": c_(a.attention_w.bias),
+                      "att_h_kernel": c_(a.attention_h.kernel), "att_h_bias": c_(a.attention_h.bias)})
+        ids_h, dense_h = _host_pool(ids_pool, dense_pool)
+
+        def cpu_step(j):
+            return O.afm(None, p, "att", dt=np.float32, inputs=(dense_h[j], ids_h[j]))[0]
+
+        def gpu0():
+            return m((dense_pool[0], ids_pool[0]), check_ids=False).cpu().numpy()
+
+        cpu = _cpu_leg(args, rank, B, cpu_step, 8, "AFM.call 'att': Embedding per field, InteractionLayer [B, 325, "
+                                                  "k], AttentionLayer, Dense(1), two sigmoids", gpu0)
     return _hbm_line("AFM forward samples/sec @ batch 4096, 26 sparse x 1e6 vocab, dim 16", args, world, B, dt,
                      slot, alg, "afm_att_fused", V, "pair_pool_kernel (att == sum)",
                      {"mode_max": {"samples_per_s": args.steps * B / dtm, "kernel_ms": slotm,
-                                   "note": "max over the 325 pair products per dim, in registers"}})
+                                   "note": "max over the 325 pair products per dim, in registers"},
+                      "cpu_baseline": cpu})
 
 
 def bench_ffm(args, world, rank):
@@ -845,9 +972,37 @@ def bench_ffm(args, world, rank):
     dt, slot = _timed_graph(step, args.steps, args.warmup, world)
     NF = 13 + F
     alg = B * (F * 4 + 13 * 4 + F * NF * k * 4 + F * 4 + 4)
+    cpu = None
+    if args.cpu_baseline and rank == 0:
+        from oracle import ctr_oracle as O
+        L = m.ffm
+        ids_h, dense_h = _host_pool(ids_pool, dense_pool)
+        # the touched rows of w / v only (the 32 GB field-aware table is not
+        # copied to the host): per field, the rows of the pool's ids, ids remapped
+        offs = np.concatenate([[0], np.cumsum(L.onehot_dims)[:-1]]).astype(np.int64)
+        nd_ = L.nd
+        cw, cv, rid, cdims = [L.w[:nd_].cpu().numpy()], [L.v[:nd_].cpu().numpy()], np.empty_like(ids_h), []
+        for c in range(F):
+            u, inv = np.unique(ids_h[:, :, c], return_inverse=True)
+            rows = torch.as_tensor(nd_ + offs[c] + u, device=L.w.device)
+            cw.append(L.w[rows].cpu().numpy())
+            cv.append(L.v[rows].cpu().numpy())
+            rid[:, :, c] = inv.reshape(ids_h.shape[:2])
+            cdims.append(u.size)
+        cw, cv, w0 = np.concatenate(cw), np.concatenate(cv), L.w0.cpu().numpy()
+
+        def cpu_step(j):
+            return O.sigmoid(O.ffm_layer_gather(dense_h[j], rid[j], cdims, w0, cw, cv, np.float32))
+
+        def gpu0():
+            return m((dense_pool[0], ids_pool[0])).cpu().numpy()
+
+        cpu = _cpu_leg(args, rank, B, cpu_step, 8, "FFM.call: FFMLayer as row gathers of w / v (the one-hot x "
+                                                  "never formed) + sigmoid; host copy holds the touched rows only",
+                       gpu0)
     return _hbm_line("FFM forward samples/sec @ batch 4096, 26 sparse x 1e6 vocab, k 8", args, world, B, dt, slot,
                      alg, "ffm_fused", V, "ffm_kernel",
-                     {"table_GB": (13 + F * V) * NF * k * 4 / 1e9})
+                     {"table_GB": (13 + F * V) * NF * k * 4 / 1e9, "cpu_baseline": cpu})
 
 
 def bench_io(args, world, rank):

@@ -471,6 +471,26 @@ def ffm_layer(dense_in, sparse, onehot_dims, w0, w, v, dt=np.float64):
     return linear + inter
 
 
+def ffm_layer_gather(dense_in, sparse, onehot_dims, w0, w, v, dt=np.float64):
+    """ffm_layer without the one-hot matrix (for vocabularies too large to
+    materialise, e.g. the bench's 26 x 1e6 CPU baseline): x has exactly one 1
+    per field at column nd + offset_c + id_c, so x@w and tensordot(x, v) are
+    row gathers (pinned == ffm_layer by tests/test_interactions.py);
+    out-of-range ids contribute a zero row like tf.one_hot."""
+    dense_in = np.asarray(dense_in, dt)
+    ids = cast_ids(sparse)
+    nd = dense_in.shape[1]
+    w, v = np.asarray(w), np.asarray(v)
+    offs = np.concatenate([[0], np.cumsum(onehot_dims)[:-1]]).astype(np.int64)
+    ok = (ids >= 0) & (ids < np.asarray(onehot_dims)[None, :])
+    rows = np.where(ok, nd + offs[None, :] + ids, 0)
+    okf = ok.astype(dt)
+    Fm = np.einsum("bi,ifk->bfk", dense_in, v[:nd].astype(dt)) + np.einsum("bc,bcfk->bfk", okf, v[rows].astype(dt))
+    lin = np.asarray(w0, dt) + dense_in @ w[:nd].astype(dt) + (okf * w[rows, 0].astype(dt)).sum(1, keepdims=True)
+    inter = dt(0.5) * ((Fm.sum(1) ** 2).sum(1) - (Fm ** 2).sum((1, 2)))
+    return lin + inter[:, None]
+
+
 def ffm(X, p, onehot_dims, nd=13, dt=np.float64, inputs=None):
     """FFM.call (model/ffm.py:20-22): sigmoid(FFMLayer(inputs))."""
     dense_in, sparse = inputs if inputs is not None else _split_dense_sparse(X, nd, dt)

@@ -53,10 +53,12 @@ def test_ffm_closed_form_and_gather():
     lin = w0 + dense @ w[:nd] + w[rows, 0].sum(1, keepdims=True)
     inter = 0.5 * ((Fm.sum(1) ** 2).sum(1) - (Fm ** 2).sum((1, 2)))
     np.testing.assert_allclose(ref, lin + inter[:, None], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(O.ffm_layer_gather(dense, ids, dims, w0, w, v), ref, rtol=1e-12, atol=1e-12)
     # tf.one_hot: an out-of-range id contributes a zero row, no error
     bad = ids.copy()
     bad[0, 1] = 99
-    O.ffm_layer(dense, bad, dims, w0, w, v)
+    np.testing.assert_allclose(O.ffm_layer_gather(dense, bad, dims, w0, w, v), O.ffm_layer(dense, bad, dims, w0, w, v),
+                               rtol=1e-12, atol=1e-12)
 
 
 # ------------------------------------------------------------------- GPU
