@@ -164,7 +164,7 @@ struct EmbedFmArgs {
   do {                                                                                       \
     __builtin_amdgcn_sched_barrier(0);                                                       \
     if (a.dbg && lane == 0)                                                                  \
-      a.dbg[((int64_t)blockIdx.x * NW + w) * 8 + (i)] = __builtin_amdgcn_s_memrealtime();   \
+      a.dbg[((int64_t)blockIdx.x * NW + w) * 12 + (i)] = __builtin_amdgcn_s_memrealtime();  \
     __builtin_amdgcn_sched_barrier(0);                                                       \
   } while (0)
 #define RS_USE(x) asm volatile("" ::"v"(x))
@@ -279,7 +279,12 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     for (int t = threadIdx.x; t < 16 * a.F; t += NW * 64) {
       const int ss = t / a.F, c = t - ss * a.F;
       const int64_t bb = b0 + ss < a.batch ? b0 + ss : a.batch - 1;
-      lid[ss][c] = I::load(a.ids, bb * a.id_stride + c);
+      const auto idv = I::load(a.ids, bb * a.id_stride + c);
+#ifdef RS_DIAG_STAMPS
+      RS_USE(idv);
+      RS_STAMP(8);
+#endif
+      lid[ss][c] = idv;
     }
     if constexpr (!OWNER) {
       for (int t = threadIdx.x; t < 2 * a.F; t += NW * 64) {
@@ -290,6 +295,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   }
   if (a.F == 0 || coop) load_dense();
   if (coop) __syncthreads();
+  RS_STAMP(9);
 
   // ---- fields c = cg + j*NW + w; slots past F re-read field F-1 and add 0
   for (int cg = 0; cg < a.F; cg += NW * MAXC) {
