@@ -922,11 +922,15 @@ template <int MODE>
 __global__ __launch_bounds__(256) void diag_gather_sum(const float* __restrict__ table,
                                                       const int64_t* __restrict__ rows, int64_t n, float* out) {
   float acc = 0.f;
-  const int q = threadIdx.x & 3;
-  const int64_t quad = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  // MODE 5: nontemporal with the MFMA A-operand lane layout of embed_fm_mfma
+  // (lane l reads chunk l>>4 of row l&15: the 4 lanes of a row are 16 apart)
+  const int lane = threadIdx.x & 63;
+  const int q = MODE == 5 ? lane >> 4 : threadIdx.x & 3;
+  const int64_t quad = MODE == 5 ? (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 16 + (lane & 15)
+                                 : ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
   const int64_t nquads = ((int64_t)gridDim.x * blockDim.x) >> 2;
   for (int64_t i = quad; i < n; i += nquads) {
-    const floatx4 v = probe_load<MODE>(table + rows[i] * 16 + 4 * q);
+    const floatx4 v = probe_load<MODE == 5 ? 1 : MODE>(table + rows[i] * 16 + 4 * q);
     acc += v[0] + v[1] + v[2] + v[3];
   }
   if (acc == 12345.678f) out[blockIdx.x] = acc;  // keep the loads live, never true
@@ -939,9 +943,65 @@ extern "C" int rs_diag_gather_sum(const float* table, const int64_t* rows, int64
     case 1: diag_gather_sum<1><<<grid, 256, 0, st>>>(table, rows, n, out); break;
     case 2: diag_gather_sum<2><<<grid, 256, 0, st>>>(table, rows, n, out); break;
     case 3: diag_gather_sum<3><<<grid, 256, 0, st>>>(table, rows, n, out); break;
+    case 5: diag_gather_sum<5><<<grid, 256, 0, st>>>(table, rows, n, out); break;
     default: diag_gather_sum<4><<<grid, 256, 0, st>>>(table, rows, n, out); break;
   }
   return launch_status("rs_diag_gather_sum");
+}
+
+// Cache-policy probe: U unrolled 16-B loads per lane in flight (4 lanes per
+// 64-B row), issued by inline asm with the given policy bits and waited for
+// together; POL 0 plain, 1 nt, 2 sc1, 3 sc0 sc1, 4 sc0 sc1 nt, 5 sc1 nt, 6 sc0,
+// 7 sc0 nt.
+#define RS_PROBE_ASM(bits) asm volatile("global_load_dwordx4 %0, %1, off " bits : "=v"(v[u]) : "v"(p[u]) : "memory")
+template <int POL>
+__global__ __launch_bounds__(256) void diag_policy_sum(const float* __restrict__ table, const int64_t* __restrict__ rows,
+                                                       int64_t n, float* out) {
+  constexpr int U = 4;
+  float acc = 0.f;
+  const int q = threadIdx.x & 3;
+  const int64_t quad = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  const int64_t nquads = ((int64_t)gridDim.x * blockDim.x) >> 2;
+  for (int64_t i0 = quad; i0 < n; i0 += U * nquads) {
+    const float* p[U];
+    floatx4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * nquads < n ? i0 + u * nquads : i0;
+      p[u] = table + rows[i] * 16 + 4 * q;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (POL == 0) RS_PROBE_ASM("");
+      else if constexpr (POL == 1) RS_PROBE_ASM("nt");
+      else if constexpr (POL == 2) RS_PROBE_ASM("sc1");
+      else if constexpr (POL == 3) RS_PROBE_ASM("sc0 sc1");
+      else if constexpr (POL == 4) RS_PROBE_ASM("sc0 sc1 nt");
+      else if constexpr (POL == 5) RS_PROBE_ASM("sc1 nt");
+      else if constexpr (POL == 6) RS_PROBE_ASM("sc0");
+      else RS_PROBE_ASM("sc0 nt");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u][0] + v[u][1] + v[u][2] + v[u][3];
+  }
+  if (acc == 12345.678f) out[blockIdx.x] = acc;  // keep the loads live, never true
+}
+extern "C" int rs_diag_policy_sum(const float* table, const int64_t* rows, int64_t n, int grid, float* out, int pol,
+                                  rs_stream_t stream) {
+  hipStream_t st = as_stream(stream);
+  switch (pol) {
+    case 0: diag_policy_sum<0><<<grid, 256, 0, st>>>(table, rows, n, out); break;
+    case 1: diag_policy_sum<1><<<grid, 256, 0, st>>>(table, rows, n, out); break;
+    case 2: diag_policy_sum<2><<<grid, 256, 0, st>>>(table, rows, n, out); break;
+    case 3: diag_policy_sum<3><<<grid, 256, 0, st>>>(table, rows, n, out); break;
+    case 4: diag_policy_sum<4><<<grid, 256, 0, st>>>(table, rows, n, out); break;
+    case 5: diag_policy_sum<5><<<grid, 256, 0, st>>>(table, rows, n, out); break;
+    case 6: diag_policy_sum<6><<<grid, 256, 0, st>>>(table, rows, n, out); break;
+    default: diag_policy_sum<7><<<grid, 256, 0, st>>>(table, rows, n, out); break;
+  }
+  return launch_status("rs_diag_policy_sum");
 }
 
 extern "C" int rs_diag_embed_fm_fwd(const void* ids, int id_kind, int64_t id_stride, const float* dense,

@@ -48,8 +48,13 @@ def run_one(ablate):
         lib.rs_diag_gather_sum(table.data_ptr(), r.data_ptr(), r.numel(), 1024, out.data_ptr(), 1,
                                torch.cuda.current_stream().cuda_stream)
 
+    def probe_mfma_layout(i):
+        r = rows[i % 64]
+        lib.rs_diag_gather_sum(table.data_ptr(), r.data_ptr(), r.numel(), 1024, out.data_ptr(), 5,
+                               torch.cuda.current_stream().cuda_stream)
+
     res = {}
-    for name, fn in (("embed_fm", fm), ("probe_gather", probe)):
+    for name, fn in (("embed_fm", fm), ("probe_gather", probe), ("probe_mfma_layout", probe_mfma_layout)):
         for i in range(8):
             fn(i)
         torch.cuda.synchronize()
@@ -77,7 +82,7 @@ if __name__ == "__main__":
     if len(sys.argv) > 1:
         run_one(int(sys.argv[1]))
     else:
-        runs = [(a, None) for a in (0, 8)] + [(0, "13"), (8, "13"), (0, "8")]
+        runs = [(a, None) for a in (0, 4, 7)]
         for ab, nw in runs:
             env = dict(os.environ, RS_ABLATE=str(ab))
             if nw:
