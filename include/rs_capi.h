@@ -437,6 +437,13 @@ int rs_sgd_update(float* w, const float* grad, int64_t n, float lr, float l2,
 int rs_head_grad(const float* fm, const float* dnn, const float* labels,
                  int64_t batch, float c_fm, float c_dnn, float* g_fm,
                  float* g_dnn, float* loss, rs_stream_t stream);
+/* rs_head_grad with g = scale (sigmoid(z) - t) (scale > 0): the sharded
+ * DeepFM step's local batch is a 1/world share of the global batch mean,
+ * scale = 1 / (world * batch).                                             */
+int rs_head_grad_scaled(const float* fm, const float* dnn, const float* labels,
+                        int64_t batch, float c_fm, float c_dnn, float scale,
+                        float* g_fm, float* g_dnn, float* loss,
+                        rs_stream_t stream);
 int rs_fm_x_grad(const float* x, int64_t ldx, const float* s, const float* w1,
                  const float* v, int64_t batch, int d, int kfm, const float* g,
                  float* dx, int64_t lddx, rs_stream_t stream);
@@ -570,6 +577,15 @@ int rs_shard_field_route(const void* ids, int id_kind, int64_t id_stride,
  *   so rs_deepfm_fwd(ids = slot_of, offsets 0, vocab world*batch*slot_stride,
  *   table = got) runs the whole DeepFM forward straight from the exchange
  *   buffer.  Fixed sizes, no scan, no capacity, no overflow.                 */
+/* Sharded DeepFM backward (ShardedDeepFM.train_step): rs_scatter_rows
+ * writes lookup j = b*n_fields + c's gradient row src[b*src_stride + c*k ..]
+ * into dst[slot_of[j]] (slot_of < 0 skipped) — the row-exchange layout, so
+ * the reverse all-to-all returns every owner the dL/drow of the rows it
+ * served, aligned with its received row ids (rs_embedding_sgd on those ids
+ * then sums duplicates in record order).                                   */
+int rs_scatter_rows(const float* src, int64_t src_stride, int n_fields, int k,
+                    const int32_t* slot_of, int64_t batch, float* dst,
+                    rs_stream_t stream);
 int rs_shard_row_route(const void* ids, int id_kind, int64_t id_stride,
                        const int64_t* field_offsets, const int64_t* field_vocab,
                        int n_fields, int64_t batch, int64_t rows_per_rank,

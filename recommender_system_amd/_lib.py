@@ -78,6 +78,8 @@ SIGNATURES = {
     "rs_col_sum": (I, [P, L, L, L, P, P]),
     "rs_sgd_update": (I, [P, P, L, F, F, P]),
     "rs_head_grad": (I, [P, P, P, L, F, F, P, P, P, P]),
+    "rs_head_grad_scaled": (I, [P, P, P, L, F, F, F, P, P, P, P]),
+    "rs_scatter_rows": (I, [P, L, I, I, P, L, P, P]),
     "rs_fm_x_grad": (I, [P, L, P, P, P, L, I, I, P, P, L, P]),
     "rs_fm_param_grads": (I, [P, L, P, P, L, I, I, P, P, P, P, P]),
     "rs_fm_param_grads_strided": (I, [P, L, P, L, P, L, P, L, I, I, P, P, P, P]),

@@ -127,12 +127,13 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ w, const f
 // g_fm = c_fm*g, g_dnn = c_dnn*g (dL/dfm, dL/ddnn) and the BCE loss.
 __global__ __launch_bounds__(256) void head_grad_kernel(const float* __restrict__ fm, const float* __restrict__ dnn,
                                                         const float* __restrict__ t, int64_t B, float c_fm,
-                                                        float c_dnn, float* __restrict__ g_fm,
+                                                        float c_dnn, float scale, float* __restrict__ g_fm,
                                                         float* __restrict__ g_dnn, float* __restrict__ loss) {
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (b >= B) return;
   const float z = c_fm * fm[b] + c_dnn * dnn[b];
-  const float g = (sigmoidf_(z) - t[b]) / (float)B;
+  // scale = 0: the batch mean 1/B (rs_head_grad)
+  const float g = scale == 0.f ? (sigmoidf_(z) - t[b]) / (float)B : scale * (sigmoidf_(z) - t[b]);
   g_fm[b] = c_fm * g;
   g_dnn[b] = c_dnn * g;
   if (loss) loss[b] = fmaxf(z, 0.f) - z * t[b] + log1pf(expf(-fabsf(z)));
@@ -244,26 +245,27 @@ __global__ __launch_bounds__(256) void emb_keys_kernel(const void* ids, int64_t 
 // Sorted lookups: the first position of each row's segment sums the
 // segment's gradient rows (grad row of lookup j = b*F + c at
 // grad[b*ldg + c*k]) in lookup order and applies table[r] -= lr * G.
+// One thread per (position, column): the k columns of a segment are summed
+// by k adjacent lanes (a hot row's duplicates cost one pass, not k), each
+// in the same fixed lookup order, so the result stays bitwise reproducible.
 __global__ __launch_bounds__(256) void emb_apply_kernel(const uint32_t* __restrict__ key,
                                                         const uint32_t* __restrict__ val, int64_t n, int F, int k,
                                                         const float* __restrict__ grad, int64_t ldg, float lr,
                                                         float* __restrict__ table) {
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t p = t / k;
+  const int f = (int)(t - p * k);
   if (p >= n) return;
   const uint32_t r = key[p];
   if (r == 0xffffffffu || (p > 0 && key[p - 1] == r)) return;
-  int64_t e = p + 1;
-  while (e < n && key[e] == r) ++e;
-  for (int f = 0; f < k; ++f) {
-    float acc = 0.f;
-    for (int64_t q = p; q < e; ++q) {
-      const int64_t j = val[q];
-      const int64_t b = j / F;
-      const int c = (int)(j - b * F);
-      acc += grad[b * ldg + (int64_t)c * k + f];
-    }
-    table[(int64_t)r * k + f] -= lr * acc;
+  float acc = 0.f;
+  for (int64_t q = p; q < n && key[q] == r; ++q) {
+    const int64_t j = val[q];
+    const int64_t b = j / F;
+    const int c = (int)(j - b * F);
+    acc += grad[b * ldg + (int64_t)c * k + f];
   }
+  table[(int64_t)r * k + f] -= lr * acc;
 }
 
 // ------------------------------------------------------ CrossNet training
@@ -437,8 +439,18 @@ extern "C" int rs_head_grad(const float* fm, const float* dnn, const float* labe
   if (batch == 0) return RS_OK;
   RS_REQUIRE(fm && dnn && labels && g_fm && g_dnn && batch > 0, "rs_head_grad: bad arguments");
   head_grad_kernel<<<(unsigned)((batch + 255) / 256), 256, 0, as_stream(stream)>>>(fm, dnn, labels, batch, c_fm,
-                                                                                   c_dnn, g_fm, g_dnn, loss);
+                                                                                   c_dnn, 0.f, g_fm, g_dnn, loss);
   return launch_status("rs_head_grad");
+}
+
+extern "C" int rs_head_grad_scaled(const float* fm, const float* dnn, const float* labels, int64_t batch, float c_fm,
+                                   float c_dnn, float scale, float* g_fm, float* g_dnn, float* loss,
+                                   rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(fm && dnn && labels && g_fm && g_dnn && batch > 0 && scale > 0.f, "rs_head_grad_scaled: bad arguments");
+  head_grad_kernel<<<(unsigned)((batch + 255) / 256), 256, 0, as_stream(stream)>>>(fm, dnn, labels, batch, c_fm,
+                                                                                   c_dnn, scale, g_fm, g_dnn, loss);
+  return launch_status("rs_head_grad_scaled");
 }
 
 extern "C" int rs_fm_x_grad(const float* x, int64_t ldx, const float* s, const float* w1, const float* v,
@@ -539,8 +551,8 @@ extern "C" int rs_embedding_sgd(float* table, int64_t n_rows, int k, const void*
     set_error("rs_embedding_sgd: radix sort failed: %s", hipGetErrorString(e));
     return RS_ERR_HIP;
   }
-  emb_apply_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(key_out, val_out, n, n_fields, k, grad, grad_stride,
-                                                               lr, table);
+  emb_apply_kernel<<<(unsigned)((n * k + 255) / 256), 256, 0, st>>>(key_out, val_out, n, n_fields, k, grad,
+                                                                   grad_stride, lr, table);
   return launch_status("rs_embedding_sgd");
 }
 

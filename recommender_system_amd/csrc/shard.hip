@@ -513,3 +513,35 @@ extern "C" int rs_unpermute_rows(const float* src, const int32_t* perm, int k, i
     unpermute_rows_kernel<1><<<sh_grid(n * k), 256, 0, st>>>(src, perm, k, n, dst);
   return launch_status("rs_unpermute_rows");
 }
+
+// ------------------------------------- row-gradient scatter (sharded backward)
+// dst[slot_of[j]] = src[b*src_stride + c*k : +k] for lookup j = b*n_fields + c
+// (slot_of < 0: skipped).  The sharded DeepFM backward writes each lookup's
+// dL/drow into its slot of the row-exchange layout, so the reverse
+// all-to-all hands every owner the gradients aligned with the row ids it
+// served.  One thread per (lookup, column).
+namespace rs {
+__global__ __launch_bounds__(256) void scatter_rows_kernel(const float* __restrict__ src, int64_t src_stride,
+                                                           int n_fields, int k, const int32_t* __restrict__ slot_of,
+                                                           int64_t n, float* __restrict__ dst) {
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n * k; t += (int64_t)gridDim.x * 256) {
+    const int64_t j = t / k;
+    const int f = (int)(t - j * k);
+    const int64_t slot = slot_of[j];
+    if (slot < 0) continue;
+    const int64_t b = j / n_fields;
+    const int c = (int)(j - b * n_fields);
+    dst[slot * k + f] = src[b * src_stride + (int64_t)c * k + f];
+  }
+}
+}  // namespace rs
+
+extern "C" int rs_scatter_rows(const float* src, int64_t src_stride, int n_fields, int k, const int32_t* slot_of,
+                               int64_t batch, float* dst, rs_stream_t stream) {
+  if (batch == 0 || n_fields == 0) return RS_OK;
+  RS_REQUIRE(src && slot_of && dst && k >= 1 && batch > 0 && n_fields > 0 && src_stride >= (int64_t)n_fields * k,
+             "rs_scatter_rows: bad arguments");
+  const int64_t n = batch * n_fields;
+  scatter_rows_kernel<<<sh_grid(n * k), 256, 0, as_stream(stream)>>>(src, src_stride, n_fields, k, slot_of, n, dst);
+  return launch_status("rs_scatter_rows");
+}

@@ -184,26 +184,26 @@ __global__ __launch_bounds__(256) void fm_train_decay(FmTrainArgs a) {
 }
 
 // Sorted lookups: the first position of each row's segment sums the
-// segment's contributions in lookup order and applies them; then the dense
-// rows and w0.
+// segment's contributions in lookup order and applies them (one thread per
+// (position, column): a hot row's k+1 columns are summed by adjacent lanes,
+// each in the same fixed order, so the step stays bitwise reproducible);
+// then the dense rows and w0.
 __global__ __launch_bounds__(256) void fm_train_apply(FmTrainArgs a) {
   const int64_t n = a.batch * a.F;
   const int K1 = a.k + 1;
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (p < n) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t < n * K1) {
+    const int64_t p = t / K1;
+    const int f = (int)(t - p * K1);
     const uint32_t r = a.key_out[p];
     if (p == 0 || a.key_out[p - 1] != r) {
-      int64_t e = p + 1;
-      while (e < n && a.key_out[e] == r) ++e;
-      for (int f = 0; f < K1; ++f) {
-        float acc = 0.f;
-        for (int64_t q = p; q < e; ++q) acc += a.contrib[(int64_t)a.val_out[q] * K1 + f];
-        if (f < a.k) a.v[(int64_t)r * a.k + f] -= a.lr * acc;
-        else a.w1[r] -= a.lr * acc;
-      }
+      float acc = 0.f;
+      for (int64_t q = p; q < n && a.key_out[q] == r; ++q) acc += a.contrib[(int64_t)a.val_out[q] * K1 + f];
+      if (f < a.k) a.v[(int64_t)r * a.k + f] -= a.lr * acc;
+      else a.w1[r] -= a.lr * acc;
     }
-  } else if (p < n + a.nd * K1 + 1) {
-    const int idx = (int)(p - n);
+  } else if (t < n * K1 + a.nd * K1 + 1) {
+    const int idx = (int)(t - n * K1);
     const float gsum = a.gdense[idx];
     if (idx == a.nd * K1) {
       a.w0[0] -= a.lr * gsum;
@@ -300,7 +300,7 @@ extern "C" int rs_fm_train_step(const void* ids, int id_kind, int64_t id_stride,
   }
   const int64_t dn = n_rows * (int64_t)(k + 1);
   fm_train_decay<<<(unsigned)std::min<int64_t>((dn / 4 + 255) / 256 + 1, 8192), 256, 0, st>>>(a);
-  const int64_t ap = n + nd * (k + 1) + 1;
+  const int64_t ap = (n + nd) * (k + 1) + 1;
   fm_train_apply<<<(unsigned)((ap + 255) / 256), 256, 0, st>>>(a);
   return launch_status("rs_fm_train_step");
 }

@@ -58,17 +58,18 @@ def _subseed(gen):
     return int(torch.randint(0, 2 ** 31, (1,), generator=gen))
 
 
-def _dnn_backward(layers, acts, delta, gw, emp, st):
+def _dnn_backward(layers, acts, delta, gw, emp, st, outs=None):
     """Backward through Dense layers (relu or linear hidden activations):
     delta = dL/d(pre-activation) of the top layer; returns the (layer, dW, db)
     gradients and dL/d(acts[0]).  dW = a_in^T delta (split-K rs_gemm), db =
-    column sums, delta_below = (delta W^T) [a_in > 0] (mask epilogue)."""
+    column sums, delta_below = (delta W^T) [a_in > 0] (mask epilogue).
+    outs: optional [(dW, db)] per layer to write into (contiguous views)."""
     B = acts[0].shape[0]
     grads = []
     for li in reversed(range(len(layers))):
         L, a_in = layers[li], acts[li]
         K_in, N_out = L.kernel.shape
-        dW, db = emp(K_in, N_out), emp(N_out)
+        dW, db = outs[li] if outs is not None else (emp(K_in, N_out), emp(N_out))
         call("rs_gemm", 1, 0, K_in, N_out, B, 1.0, ptr(a_in), a_in.stride(0), ptr(delta), delta.stride(0), 0.0,
              ptr(dW), N_out, None, 0, *gw, st)
         call("rs_col_sum", ptr(delta), delta.stride(0), B, N_out, ptr(db), st)

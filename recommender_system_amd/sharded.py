@@ -212,6 +212,71 @@ class HipShardOps:
         sh = model.emb
         return _hip_deepfm(self, model, ids, sh.table_shard, sh.offsets, sh.vocab, dense, out)
 
+    # -- training of ShardedDeepFM (row protocol + reverse row exchange)
+    def deepfm_grads(self, model, got, rb, dense, labels, scale, tb, loss):
+        """This rank's share of the DeepFM step: x = [dense | rows from the
+        exchange buffer] (rs_embed_gather with ids = slot_of), forward with
+        saved activations (rs_dense_fwd, rs_fm_fwd, s = x@v on rs_gemm),
+        g = scale (sigmoid(z) - t) (rs_head_grad_scaled, scale = 1/(world B)),
+        the DNN backward (split-K rs_gemm, rs_col_sum) and the FM gradients
+        (rs_fm_x_grad, rs_fm_param_grads) into the views of tb's flat
+        gradient; returns dL/dx [B, d]."""
+        from .models import _dnn_backward
+        sh, st = model.emb, _lib.stream()
+        B, d, kfm = dense.shape[0], sh.d, sh.kfm
+        x = tb["x"]
+        call("rs_embed_gather", ptr(rb["slot_of"]), _lib.ID_I32, model.F, ptr(dense), dense.stride(0), model.nd,
+             ptr(got), ptr(rb["zoff"]), ptr(rb["nslots"]), model.F, model.k, ptr(x), d, B, ptr(self.err), st)
+        dnn = model.dnn
+        layers = list(dnn.hidden_layer) + [dnn.output_layer]
+        acts = [x]
+        for layer in dnn.hidden_layer:
+            acts.append(layer(acts[-1]))
+        dnn_out = dnn.output_layer(acts[-1])
+        fm_out = tb["fm"]
+        call("rs_fm_fwd", ptr(x), d, d, ptr(sh.prepared), ptr(sh.w0), kfm, ptr(fm_out), B, st)
+        gw = (ptr(tb["gemm_ws"]), tb["gemm_ws"].numel())
+        s = tb["s"]
+        call("rs_gemm", 0, 0, B, kfm, d, 1.0, ptr(x), d, ptr(sh.v), kfm, 0.0, ptr(s), kfm, None, 0, *gw, st)
+        g_fm, g_dnn = tb["g_fm"], tb["g_dnn"]
+        call("rs_head_grad_scaled", ptr(fm_out), ptr(dnn_out), ptr(labels), B, 0.5, 0.5, float(scale), ptr(g_fm),
+             ptr(g_dnn), ptr(loss), st)
+        emp = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=self.device)
+        _, dx = _dnn_backward(layers, acts, g_dnn.view(B, 1), gw, emp, st, outs=tb["dnn_views"])
+        call("rs_fm_x_grad", ptr(x), d, ptr(s), ptr(sh.w1), ptr(sh.v), B, d, kfm, ptr(g_fm), ptr(dx), d, st)
+        call("rs_fm_param_grads", ptr(x), d, ptr(s), ptr(sh.v), B, d, kfm, ptr(g_fm), ptr(tb["dw1"]), ptr(tb["dv"]),
+             ptr(tb["dw0"]), st)
+        return dx
+
+    def scatter_row_grads(self, model, dx, rb):
+        """dL/drow of every lookup into its slot of the row-exchange layout."""
+        call("rs_scatter_rows", ptr(dx) + 4 * model.nd, dx.stride(0), model.F, model.k, ptr(rb["slot_of"]),
+             dx.shape[0], ptr(rb["gsend"]), _lib.stream())
+        return rb["gsend"]
+
+    def owner_row_sgd(self, model, recv, grecv, lr, tb):
+        """Owner: row-sparse SGD of the shard from the received row ids and
+        their gradients (-1 words skipped; duplicates summed in record order:
+        requester-major, sample-major, field order — the same on every rank)."""
+        sh = model.emb
+        n_pairs = recv.numel() // sh.slot_stride
+        call("rs_embedding_sgd", ptr(sh.table_shard), sh.table_shard.shape[0], sh.k, ptr(recv), _lib.ID_I32,
+             sh.slot_stride, ptr(tb["zoff"]), ptr(tb["svocab"]), sh.slot_stride, n_pairs, ptr(grecv),
+             sh.slot_stride * sh.k, float(lr), ptr(tb["emb_ws"]), None, _lib.stream())
+
+    def deepfm_apply(self, model, tb, lr):
+        """SGD of the replicated parameters from the (all-reduced) flat
+        gradient: l2(w_reg) on w1, l2(v_reg) on v (FMLayer), none elsewhere."""
+        sh, st = model.emb, _lib.stream()
+        for (L, _), (dW, db) in zip(tb["layers"], tb["dnn_views"]):
+            call("rs_sgd_update", ptr(L.kernel), ptr(dW), dW.numel(), float(lr), 0.0, st)
+            call("rs_sgd_update", ptr(L.bias), ptr(db), db.numel(), float(lr), 0.0, st)
+        call("rs_sgd_update", ptr(sh.w1), ptr(tb["dw1"]), sh.d, float(lr), float(model.reg_w), st)
+        call("rs_sgd_update", ptr(sh.v), ptr(tb["dv"]), sh.d * sh.kfm, float(lr), float(model.reg_v), st)
+        call("rs_sgd_update", ptr(sh.w0), ptr(tb["dw0"]), 1, float(lr), 0.0, st)
+        sh.prepare()
+        model.dnn._weights_changed()
+
     def bad_flag(self):
         """[out-of-range id seen] (device tensor; resets)."""
         v = self.err.clamp(max=1)
@@ -649,6 +714,9 @@ class ShardedDeepFM:
                   "slot_of": torch.empty(B, F, dtype=torch.int32, device=dev),
                   "reply": torch.empty(n, self.k, dtype=torch.float32, device=dev),
                   "got": torch.empty(n, self.k, dtype=torch.float32, device=dev),
+                  # reverse exchange of the training step: dL/drow per slot
+                  "gsend": torch.zeros(n, self.k, dtype=torch.float32, device=dev),
+                  "grecv": torch.zeros(n, self.k, dtype=torch.float32, device=dev),
                   "zoff": torch.zeros(F, dtype=torch.int64, device=dev),
                   "nslots": torch.full((F,), n, dtype=torch.int64, device=dev)}
             self._row_bufs = rb
@@ -665,6 +733,98 @@ class ShardedDeepFM:
     def finish(self, dense, got, rb, out):
         """Step 5: the DeepFM forward from the exchange buffer."""
         return self.ops.deepfm_rows(self, got, rb, dense, out)
+
+    # -- training: compile_fit's SGD step, data parallel, table row-sharded
+    def _tbufs(self, B):
+        tb = getattr(self, "_train_bufs", None)
+        if tb is None or tb["B"] != B:
+            sh, dev = self.emb, self.device
+            W, S, k, d, kfm = self.world, sh.slot_stride, self.k, sh.d, sh.kfm
+            layers = [(L, L.kernel.shape) for L in list(self.dnn.hidden_layer) + [self.dnn.output_layer]]
+            sizes = [K * N + N for _, (K, N) in layers] + [d, d * kfm, 1]
+            flat = torch.zeros(sum(sizes), dtype=torch.float32, device=dev)
+            views, o = [], 0
+            for _, (K, N) in layers:
+                views.append((flat[o:o + K * N].view(K, N), flat[o + K * N:o + K * N + N]))
+                o += K * N + N
+            dw1, dv, dw0 = flat[o:o + d], flat[o + d:o + d + d * kfm].view(d, kfm), flat[o + d + d * kfm:]
+            n_look = W * B * S
+            tb = {"B": B, "flat": flat, "layers": layers, "dnn_views": views, "dw1": dw1, "dv": dv, "dw0": dw0,
+                  "x": torch.empty(B, d, dtype=torch.float32, device=dev),
+                  "fm": torch.empty(B, 1, dtype=torch.float32, device=dev),
+                  "s": torch.empty(B, kfm, dtype=torch.float32, device=dev),
+                  "g_fm": torch.empty(B, dtype=torch.float32, device=dev),
+                  "g_dnn": torch.empty(B, dtype=torch.float32, device=dev),
+                  "zoff": torch.zeros(S, dtype=torch.int64, device=dev),
+                  "svocab": torch.full((S,), max(sh.table_shard.shape[0], 1), dtype=torch.int64, device=dev)}
+            if isinstance(self.ops, HipShardOps):
+                lib = _lib.lib()
+                gmax = max(lib.rs_gemm_workspace_size(K, N, B) for _, (K, N) in layers)
+                gmax = max(gmax, lib.rs_gemm_workspace_size(B, kfm, d))
+                tb["gemm_ws"] = torch.empty(max(gmax, 1), dtype=torch.uint8, device=dev)
+                tb["emb_ws"] = torch.empty(max(lib.rs_embedding_sgd_workspace_size(n_look), 1), dtype=torch.uint8,
+                                           device=dev)
+            self._train_bufs = tb
+        return tb
+
+    def train_step(self, inputs, labels, lr=0.01, return_loss=False, check=True):
+        """One SGD step of compile_fit (utils/compile_fit.py:9-15: SGD(lr),
+        binary cross-entropy on sigmoid(0.5 (FM + DNN)), FMLayer's l2
+        regularisers; model/deepFM.py:23-31) over the GLOBAL batch — every
+        rank's B samples, g scaled by 1/(world B) — as data-parallel training
+        with the table row-sharded:
+          forward exchange (rs_shard_row_route, all_to_all ids, owner
+            rs_gather_rows, all_to_all rows)      -> every lookup's row here
+          deepfm_grads  -> x, local forward + backward: this rank's share of
+                           the DNN / FM gradients (flat buffer) and dL/dx
+          rs_scatter_rows -> dL/drow into the row-exchange slot layout
+          all_to_all(row gradients)  (RCCL; the reverse of the row exchange)
+          owner: rs_embedding_sgd of the shard on the ids it served
+          all_reduce(flat gradient)  (RCCL) -> rs_sgd_update of the replicas
+        Every gradient comes from the pre-step weights; every rank's update of
+        the replicated parameters is identical.  Returns the per-sample losses
+        of the local batch (before the step) if ``return_loss``."""
+        from .models import _split_criteo
+        from .layers import _to_device_f32
+        sh = self.emb
+        if self.dnn.output_layer.units != 1 or any(l.activation not in (None, "linear", "relu")
+                                                   for l in self.dnn.hidden_layer):
+            raise NotImplementedError("ShardedDeepFM.train_step: output_dim 1, 'relu' / linear hidden layers")
+        if isinstance(inputs, (tuple, list)) and not isinstance(self.ops, HipShardOps):
+            dense, ids = inputs
+            labels = torch.as_tensor(labels, dtype=torch.float32).reshape(-1)
+        else:
+            dense, ids = _split_criteo(inputs, self.nd, self.device)
+            labels = _to_device_f32(labels, self.device).reshape(-1)
+        B, W = ids.shape[0], self.world
+        rb, tb = self._rbufs(B), self._tbufs(B)
+        self.route(ids, rb)
+        recv = rb["send"]
+        if sh.exchanges:
+            recv = rb["recv"]
+            dist.all_to_all_single(recv, rb["send"], group=self.group)
+        reply = got = self.serve(recv, rb["reply"])
+        if sh.exchanges:
+            got = rb["got"]
+            dist.all_to_all_single(got, reply, group=self.group)
+        loss = torch.empty(B, dtype=torch.float32, device=self.device) if return_loss else None
+        dx = self.ops.deepfm_grads(self, got, rb, dense, labels, 1.0 / (W * B), tb, loss)
+        gsend = self.ops.scatter_row_grads(self, dx, rb)
+        grecv = gsend
+        if sh.exchanges:
+            grecv = rb["grecv"]
+            dist.all_to_all_single(grecv, gsend, group=self.group)
+        self.ops.owner_row_sgd(self, recv, grecv, lr, tb)
+        if W > 1:
+            dist.all_reduce(tb["flat"], group=self.group)
+        self.ops.deepfm_apply(self, tb, lr)
+        if check:
+            f = self.ops.bad_flag()
+            if W > 1:
+                dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
+            if bool(f.item()):
+                raise IndexError("sharded DeepFM: embedding id out of range")
+        return loss
 
     def forward(self, inputs, check=True, out=None):
         from .models import _split_criteo

@@ -110,6 +110,64 @@ class CpuOps:
         out.copy_(torch.as_tensor(O.sigmoid(0.5 * (fm + dnn)), dtype=torch.float32))
         return out
 
+    # training of ShardedDeepFM (fp64 inside, fp32 buffers like the device path)
+    def deepfm_grads(self, model, got, rb, dense, labels, scale, tb, loss):
+        so = rb["slot_of"].numpy().astype(np.int64)
+        B = so.shape[0]
+        x = np.concatenate([np.asarray(dense, np.float64), got.numpy().astype(np.float64)[so].reshape(B, -1)], 1)
+        c = lambda t: t.detach().numpy().astype(np.float64)
+        sh = model.emb
+        layers = [(c(l.kernel), c(l.bias)) for l in model.dnn.hidden_layer]
+        layers.append((c(model.dnn.output_layer.kernel), c(model.dnn.output_layer.bias)))
+        acts = [x]
+        for W_, b_ in layers[:-1]:
+            acts.append(np.maximum(acts[-1] @ W_ + b_, 0.0))
+        dnn = (acts[-1] @ layers[-1][0] + layers[-1][1])[:, 0]
+        w0, w1, v = c(sh.w0), c(sh.w1), c(sh.v)
+        z = 0.5 * (O.fm_layer(x, w0, w1, v)[:, 0] + dnn)
+        t = labels.numpy().astype(np.float64)
+        if loss is not None:
+            loss.copy_(torch.as_tensor(np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z)))))
+        gf = 0.5 * scale * (O.sigmoid(z) - t)
+        delta = gf[:, None]
+        for li in reversed(range(len(layers))):
+            dW, db = tb["dnn_views"][li]
+            dW.copy_(torch.as_tensor(acts[li].T @ delta))
+            db.copy_(torch.as_tensor(delta.sum(0)))
+            prev = delta @ layers[li][0].T
+            delta = prev * (acts[li] > 0) if li > 0 else prev
+        s = x @ v
+        dx = delta + gf[:, None] * (w1[:, 0][None, :] + s @ v.T - x * np.sum(v * v, 1)[None, :])
+        tb["dw1"].copy_(torch.as_tensor((x.T @ gf[:, None])[:, 0]))
+        tb["dv"].copy_(torch.as_tensor(x.T @ (gf[:, None] * s) - ((x * x).T @ gf)[:, None] * v))
+        tb["dw0"].copy_(torch.as_tensor([gf.sum()]))
+        return torch.as_tensor(dx)
+
+    def scatter_row_grads(self, model, dx, rb):
+        so = rb["slot_of"].numpy().reshape(-1).astype(np.int64)
+        rows = dx.numpy()[:, model.nd:].reshape(-1, model.k)
+        g = rb["gsend"].numpy()
+        g[so[so >= 0]] = rows[so >= 0]
+        return rb["gsend"]
+
+    def owner_row_sgd(self, model, recv, grecv, lr, tb):
+        ids = recv.numpy().astype(np.int64)
+        gr = grecv.numpy().astype(np.float64)
+        t = model.emb.table_shard.numpy()
+        acc = np.zeros(t.shape, np.float64)
+        np.add.at(acc, ids[ids >= 0], gr[ids >= 0])
+        t[:] = (t.astype(np.float64) - lr * acc).astype(np.float32)
+
+    def deepfm_apply(self, model, tb, lr):
+        sh = model.emb
+        with torch.no_grad():
+            for (L, _), (dW, db) in zip(tb["layers"], tb["dnn_views"]):
+                L.kernel -= lr * dW
+                L.bias -= lr * db
+            sh.w1 -= lr * (tb["dw1"].view(-1, 1) + 2 * model.reg_w * sh.w1)
+            sh.v -= lr * (tb["dv"] + 2 * model.reg_v * sh.v)
+            sh.w0 -= lr * tb["dw0"]
+
     # partial protocol (fp64 inside, fp32 buffers like the device path)
     @staticmethod
     def _f32(t):
@@ -327,8 +385,9 @@ def _train_worker(rank, world, port, vocabs, k, B, q):
 
 
 def _deepfm_params(model, full):
-    """Oracle parameters of a ShardedDeepFM given the assembled full table."""
-    c = lambda t: t.detach().cpu().numpy()
+    """Oracle parameters of a ShardedDeepFM given the assembled full table
+    (copies: the model's tensors change in place when it trains)."""
+    c = lambda t: t.detach().cpu().numpy().copy()
     sh = model.emb
     offs = sh.offsets.cpu().numpy()
     return {"tables": [full[o:o + v] for o, v in zip(offs, sh.vocab_sizes)], "w0": c(sh.w0), "w1": c(sh.w1),
@@ -374,6 +433,68 @@ def _deepfm_worker(rank, world, port, vocabs, k, B, q):
         q.put((rank, bool(ok), m.emb.owner_field_ranges))
     finally:
         dist.destroy_process_group()
+
+
+def _deepfm_train_worker(rank, world, port, vocabs, k, B, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from recommender_system_amd.sharded import ShardedDeepFM
+        nd, lr = 5, 0.5
+        m = ShardedDeepFM(_deepfm_columns(vocabs, nd, k), 6, 1e-3, 2e-3, [32, 16], 1, "relu", embed_dim=k,
+                          device="cpu", seed=3, ops=CpuOps())
+        with torch.no_grad():
+            m.table_shard.mul_(20.0)  # O(1) embeddings: visible row updates
+        shards = [None] * world
+        dist.all_gather_object(shards, m.table_shard.numpy().copy())
+        p = _deepfm_params(m, np.concatenate(shards).astype(np.float64))
+        ok = True
+        for step in range(2):
+            rngs = [np.random.default_rng(500 * step + r) for r in range(world)]
+            batch = [(rg.random((B, nd)).astype(np.float32),
+                      np.stack([rg.integers(0, v, B) for v in vocabs], 1).astype(np.int32),
+                      rg.integers(0, 2, B).astype(np.float32)) for rg in rngs]
+            for b_ in batch:
+                b_[1][:3, 1] = 0  # repeated rows inside and across ranks
+            dense, ids, t = batch[rank]
+            loss = m.train_step((torch.as_tensor(dense), torch.as_tensor(ids)), torch.as_tensor(t), lr=lr,
+                                return_loss=True)
+            gd, gi, gt = (np.concatenate([b_[j] for b_ in batch]) for j in range(3))
+            p, ce = O.deepfm_train_step(gd, gi, gt, p, lr, 1e-3, 2e-3, nd=nd)
+            ok = ok and np.allclose(loss.numpy(), ce[rank * B:(rank + 1) * B], rtol=1e-5, atol=1e-6)
+            dist.all_gather_object(shards, m.table_shard.numpy().copy())
+            ok = ok and np.allclose(np.concatenate(shards), np.concatenate(p["tables"]), rtol=1e-5, atol=1e-6)
+            mine = _deepfm_params(m, np.concatenate(shards))
+            for n in ("w0", "w1", "v"):
+                ok = ok and np.allclose(mine[n], p[n], rtol=1e-5, atol=1e-6)
+            for (W1, b1), (W2, b2) in zip(mine["dnn_hidden"] + [mine["dnn_out"]], p["dnn_hidden"] + [p["dnn_out"]]):
+                ok = ok and np.allclose(W1, W2, rtol=1e-5, atol=1e-6) and np.allclose(b1, b2, rtol=1e-5, atol=1e-6)
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_deepfm_train_step_gloo(world):
+    """ShardedDeepFM.train_step over gloo (world 2, 3): forward row exchange,
+    each rank's local DeepFM backward scaled to the global batch, the REVERSE
+    all-to-all of dL/drow to the owners (row-sparse SGD of each shard,
+    duplicates across ranks summed), the all-reduce of the flat replicated
+    gradient — every shard, w0 / w1 / v and every DNN layer equal
+    O.deepfm_train_step on the concatenated global batch, over 2 steps."""
+    vocabs = [50, 7, 300, 1, 120, 33]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_deepfm_train_worker, args=(r, world, port, vocabs, 4, 19, q)) for r in range(world)]
+    for p_ in procs:
+        p_.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p_ in procs:
+        p_.join(timeout=60)
+        assert p_.exitcode == 0
+    for rank, ok in res:
+        assert ok, f"rank {rank}: sharded DeepFM training step differs from the oracle"
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -880,3 +1001,100 @@ def test_gpu_rccl_self_exchange(gpu):
     r = subprocess.run([sys.executable, os.path.join(here, "rccl_selfcheck.py")], capture_output=True, text=True,
                        timeout=100)
     assert r.returncode == 0 and "RCCL OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+
+
+def _simulated_deepfm_train(models, batches, labels, lr):
+    """One ShardedDeepFM.train_step of every rank of a simulated world on one
+    GPU, step by step: the forward row exchange (block transposes), every
+    rank's deepfm_grads + rs_scatter_rows, the reverse all-to-all of the row
+    gradients (block transpose), every owner's row SGD, the all-reduce of the
+    flat replicated gradient (sum in rank order), every rank's SGD."""
+    W = len(models)
+    B = batches[0][1].shape[0]
+    k = models[0].k
+    rbs = [m._rbufs(B) for m in models]
+    tbs = [m._tbufs(B) for m in models]
+    for m, rb, (_, ids) in zip(models, rbs, batches):
+        m.route(ids, rb)
+    for o in range(W):
+        rbs[o]["recv"].view(W, -1).copy_(torch.stack([rbs[r]["send"].view(W, -1)[o] for r in range(W)]))
+    for m, rb in zip(models, rbs):
+        m.serve(rb["recv"], rb["reply"])
+    for r in range(W):
+        rbs[r]["got"].view(W, -1, k).copy_(torch.stack([rbs[o]["reply"].view(W, -1, k)[r] for o in range(W)]))
+    losses = []
+    for m, rb, tb, (dense, _), t in zip(models, rbs, tbs, batches, labels):
+        losses.append(torch.empty(B, device=dense.device))
+        dx = m.ops.deepfm_grads(m, rb["got"], rb, dense, t, 1.0 / (W * B), tb, losses[-1])
+        m.ops.scatter_row_grads(m, dx, rb)
+    for o in range(W):
+        rbs[o]["grecv"].view(W, -1, k).copy_(torch.stack([rbs[r]["gsend"].view(W, -1, k)[o] for r in range(W)]))
+    for m, rb, tb in zip(models, rbs, tbs):
+        m.ops.owner_row_sgd(m, rb["recv"], rb["grecv"], lr, tb)
+    total = tbs[0]["flat"].clone()
+    for tb in tbs[1:]:
+        total += tb["flat"]
+    for m, tb in zip(models, tbs):
+        tb["flat"].copy_(total)
+        m.ops.deepfm_apply(m, tb, lr)
+    return losses
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,B,k", [(1, 300, 16), (2, 200, 16), (3, 129, 8), (8, 128, 16)])
+def test_gpu_sharded_deepfm_train_simulated_world(gpu, world, B, k):
+    """ShardedDeepFM.train_step's HIP path (rs_embed_gather from the exchange
+    buffer, rs_dense_fwd / rs_fm_fwd with saved activations,
+    rs_head_grad_scaled, the rs_gemm DNN backward, rs_fm_x_grad /
+    rs_fm_param_grads, rs_scatter_rows into the slot layout, the reverse
+    all-to-all, the owners' rs_embedding_sgd on the ids they served, the
+    flat-gradient all-reduce, rs_sgd_update) at world 1 (train_step itself)
+    and simulated worlds 2 / 3 / 8, 2 steps with rows repeated within and
+    across ranks: every shard, w0 / w1 / v and every DNN layer equal
+    O.deepfm_train_step on the concatenated global batch."""
+    from recommender_system_amd.sharded import ShardedDeepFM
+    from tests.helpers import assert_scaled_close
+    rng = np.random.default_rng(world * 13 + k)
+    vocabs = [int(v) for v in rng.integers(1, 400, 26)]
+    vocabs[5] = 3000  # straddles owners
+    nd, kfm, lr, rw, rv = 13, 10, 0.5, 1e-3, 2e-3
+    cols = _deepfm_columns(vocabs, nd, k)
+    models = [ShardedDeepFM(cols, kfm, rw, rv, [64, 32], 1, "relu", embed_dim=k, device=gpu, seed=9,
+                            world=world, rank=r) for r in range(world)]
+    for m in models:
+        with torch.no_grad():
+            m.table_shard.mul_(10.0)  # O(1) embeddings: visible row updates
+            for l in m.dnn._layers():
+                l.bias.fill_(0.05)
+    p = _deepfm_params(models[0], np.concatenate([m.table_shard.cpu().numpy() for m in models]).astype(np.float64))
+    for step in range(2):
+        batches, labels = [], []
+        for r in range(world):
+            ids = np.stack([rng.integers(0, v, B) for v in vocabs], 1).astype(np.int32)
+            ids[:4, 2] = 0  # repeated rows within and across ranks
+            batches.append((torch.as_tensor(rng.random((B, nd)), dtype=torch.float32, device=gpu),
+                            torch.as_tensor(ids, device=gpu)))
+            labels.append(torch.as_tensor(rng.integers(0, 2, B), dtype=torch.float32, device=gpu))
+        if world == 1:
+            losses = [models[0].train_step(batches[0], labels[0], lr=lr, return_loss=True)]
+        else:
+            losses = _simulated_deepfm_train(models, batches, labels, lr)
+        cat = lambda xs: np.concatenate([x.cpu().numpy() for x in xs])
+        p, ce = O.deepfm_train_step(cat([b_[0] for b_ in batches]), cat([b_[1] for b_ in batches]), cat(labels), p,
+                                    lr, rw, rv, nd=nd)
+        assert_scaled_close(cat(losses), ce, what=f"step {step} loss")
+        full = np.concatenate([m.table_shard.cpu().numpy() for m in models])
+        assert_scaled_close(full, np.concatenate(p["tables"]), what=f"step {step} tables")
+        for r, m in enumerate(models):
+            mine = _deepfm_params(m, full)
+            for name in ("w1", "v"):
+                assert_scaled_close(mine[name], p[name], what=f"step {step} rank {r} {name}")
+            for li, ((W_, b_), (Wr, br)) in enumerate(zip(mine["dnn_hidden"] + [mine["dnn_out"]],
+                                                        p["dnn_hidden"] + [p["dnn_out"]])):
+                assert_scaled_close(W_, Wr, what=f"step {step} rank {r} W{li}")
+                assert_scaled_close(b_, br, what=f"step {step} rank {r} b{li}")
+            # w0 moves by -lr * sum_b g_b (|g_b| <= 1/(world B)): fp32 error ~ lr, not |w0|
+            w0, r0 = float(mine["w0"].reshape(-1)[0]), float(np.asarray(p["w0"]).reshape(-1)[0])
+            assert abs(w0 - r0) <= 1e-5 * max(abs(r0), lr * (step + 1)), (step, w0, r0)
+    for m in models:
+        assert int(m.ops.err.item()) == 0
