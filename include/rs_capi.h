@@ -577,6 +577,33 @@ int rs_shard_field_route(const void* ids, int id_kind, int64_t id_stride,
  *   so rs_deepfm_fwd(ids = slot_of, offsets 0, vocab world*batch*slot_stride,
  *   table = got) runs the whole DeepFM forward straight from the exchange
  *   buffer.  Fixed sizes, no scan, no capacity, no overflow.                 */
+/* Row-id deduplication before the sharded row exchange (ShardedDeepFM with
+ * dedup): the rank sends each owner only the DISTINCT rows it needs, in a
+ * fixed-capacity message of `cap` words per owner (send[world*cap]: distinct
+ * local row u of owner o at word o*cap + u, in row order; unused words -1,
+ * served as zero rows by rs_gather_rows).  slot_of[b*n_fields + c] = o*cap +
+ * u, the reply row of lookup (b, c) after the row all-to-all (rs_deepfm_fwd
+ * with ids = slot_of, vocab world*cap, reads the exchange buffer unchanged);
+ * -1 for a bad id (*err_flag) or a distinct row past `cap` (*overflow_flag:
+ * the caller redoes the step without dedup).  One stable radix sort of
+ * (global row, lookup) + a scan of the segment heads; deterministic.
+ * rs_shard_dedup_grad (backward, same workspace, after the route of the same
+ * step): dst[slot] = sum of the gradient rows grad[b*grad_stride + c*k ..]
+ * of every lookup of that distinct row, in lookup order — one gradient row
+ * per distinct row travels back to its owner.  Workspace:
+ * rs_shard_dedup_workspace_size(batch*n_fields, world) bytes.              */
+int64_t rs_shard_dedup_workspace_size(int64_t n_lookups, int world);
+int rs_shard_dedup_route(const void* ids, int id_kind, int64_t id_stride,
+                         const int64_t* field_offsets,
+                         const int64_t* field_vocab, int n_fields,
+                         int64_t batch, int64_t rows_per_rank, int world,
+                         int64_t cap, int32_t* send, int32_t* slot_of,
+                         void* workspace, int* err_flag, int* overflow_flag,
+                         rs_stream_t stream);
+int rs_shard_dedup_grad(const float* grad, int64_t grad_stride, int n_fields,
+                        int k, int64_t batch, int world, const int32_t* slot_of,
+                        const void* workspace, float* dst, rs_stream_t stream);
+
 /* Sharded DeepFM backward (ShardedDeepFM.train_step): rs_scatter_rows
  * writes lookup j = b*n_fields + c's gradient row src[b*src_stride + c*k ..]
  * into dst[slot_of[j]] (slot_of < 0 skipped) — the row-exchange layout, so

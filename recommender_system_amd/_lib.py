@@ -80,6 +80,9 @@ SIGNATURES = {
     "rs_head_grad": (I, [P, P, P, L, F, F, P, P, P, P]),
     "rs_head_grad_scaled": (I, [P, P, P, L, F, F, F, P, P, P, P]),
     "rs_scatter_rows": (I, [P, L, I, I, P, L, P, P]),
+    "rs_shard_dedup_workspace_size": (L, [L, I]),
+    "rs_shard_dedup_route": (I, [P, I, L, P, P, I, L, L, I, L, P, P, P, P, P, P]),
+    "rs_shard_dedup_grad": (I, [P, L, I, I, L, I, P, P, P, P]),
     "rs_fm_x_grad": (I, [P, L, P, P, P, L, I, I, P, P, L, P]),
     "rs_fm_param_grads": (I, [P, L, P, P, L, I, I, P, P, P, P, P]),
     "rs_fm_param_grads_strided": (I, [P, L, P, L, P, L, P, L, I, I, P, P, P, P]),

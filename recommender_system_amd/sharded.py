@@ -248,21 +248,43 @@ class HipShardOps:
              ptr(tb["dw0"]), st)
         return dx
 
+    def dedup_route(self, sh, ids, rb):
+        """Distinct rows per owner (rs_shard_dedup_route): send words, slot_of."""
+        B, F = ids.shape
+        call("rs_shard_dedup_route", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(sh.offsets), ptr(sh.vocab), F,
+             B, sh.rows_per_rank, sh.world, rb["cap"], ptr(rb["send"]), ptr(rb["slot_of"]), ptr(rb["ws"]),
+             ptr(self.err), ptr(rb["overflow"]), _lib.stream())
+        return rb["send"], rb["slot_of"]
+
+    def dedup_grads(self, model, dx, rb):
+        """One gradient row per distinct row: the sum over its lookups."""
+        B = dx.shape[0]
+        call("rs_shard_dedup_grad", ptr(dx) + 4 * model.nd, dx.stride(0), model.F, model.k, B, model.world,
+             ptr(rb["slot_of"]), ptr(rb["ws"]), ptr(rb["gsend"]), _lib.stream())
+        return rb["gsend"]
+
+    def overflow_flag(self, rb):
+        """[distinct rows past the capacity seen] (device tensor; resets)."""
+        v = rb["overflow"].clamp(max=1)
+        rb["overflow"].zero_()
+        return v
+
     def scatter_row_grads(self, model, dx, rb):
         """dL/drow of every lookup into its slot of the row-exchange layout."""
         call("rs_scatter_rows", ptr(dx) + 4 * model.nd, dx.stride(0), model.F, model.k, ptr(rb["slot_of"]),
              dx.shape[0], ptr(rb["gsend"]), _lib.stream())
         return rb["gsend"]
 
-    def owner_row_sgd(self, model, recv, grecv, lr, tb):
+    def owner_row_sgd(self, model, recv, grecv, lr, tb, rec):
         """Owner: row-sparse SGD of the shard from the received row ids and
-        their gradients (-1 words skipped; duplicates summed in record order:
-        requester-major, sample-major, field order — the same on every rank)."""
+        their gradients, records of `rec` words (-1 words skipped; duplicates
+        summed in record order: requester-major, then word order — the same
+        on every rank)."""
         sh = model.emb
-        n_pairs = recv.numel() // sh.slot_stride
-        call("rs_embedding_sgd", ptr(sh.table_shard), sh.table_shard.shape[0], sh.k, ptr(recv), _lib.ID_I32,
-             sh.slot_stride, ptr(tb["zoff"]), ptr(tb["svocab"]), sh.slot_stride, n_pairs, ptr(grecv),
-             sh.slot_stride * sh.k, float(lr), ptr(tb["emb_ws"]), None, _lib.stream())
+        n_pairs = recv.numel() // rec
+        call("rs_embedding_sgd", ptr(sh.table_shard), sh.table_shard.shape[0], sh.k, ptr(recv), _lib.ID_I32, rec,
+             ptr(tb["zoff"]), ptr(tb["svocab"]), rec, n_pairs, ptr(grecv), rec * sh.k, float(lr), ptr(tb["emb_ws"]),
+             None, _lib.stream())
 
     def deepfm_apply(self, model, tb, lr):
         """SGD of the replicated parameters from the (all-reduced) flat
@@ -662,8 +684,16 @@ class ShardedDeepFM:
     CPU (tests/test_sharded_gloo.py)."""
 
     def __init__(self, feature_columns, k, w_reg, v_reg, hidden_units, output_dim, activation, embed_dim=8,
-                 group=None, device=None, seed=0, ops=None, table_init=True, world=None, rank=None):
+                 group=None, device=None, seed=0, ops=None, table_init=True, world=None, rank=None, dedup=None):
+        """dedup: None (field-range records) or the capacity fraction f in
+        (0, 1] of the deduplicated exchange: each owner receives at most
+        cap = f * B * slot_stride distinct rows per rank and step (rounded up
+        to 64); f = 1 can never overflow, f < 1 moves fewer bytes when ids
+        repeat (an overflow redoes the step without dedup when ``check``)."""
         from .layers import DNNLayer
+        if dedup is not None and not (0.0 < float(dedup) <= 1.0):
+            raise ValueError("dedup: a capacity fraction in (0, 1]")
+        self.dedup = None if dedup is None else float(dedup)
         dense_cols, sparse_cols = feature_columns
         self.nd = len(dense_cols)
         vocabs = [int(f["feat_onehot_dim"]) for f in sparse_cols]
@@ -703,12 +733,22 @@ class ShardedDeepFM:
         return self._in_rows
 
     # -- the row exchange, step by step (forward = route, exchange, serve, exchange, finish)
-    def _rbufs(self, B):
-        rb = getattr(self, "_row_bufs", None)
+    def _dedup_cap(self, B):
+        full = B * self.emb.slot_stride
+        return min((full + 63) // 64 * 64, max(64, (int(math.ceil(self.dedup * full)) + 63) // 64 * 64))
+
+    def _rbufs(self, B, dedup=None):
+        """Row-exchange buffers: field-range records (rec = slot_stride words
+        per sample and owner) or, with dedup, cap distinct-row words per owner."""
+        dedup = self.dedup is not None if dedup is None else dedup
+        name = "_dedup_bufs" if dedup else "_row_bufs"
+        rb = getattr(self, name, None)
         if rb is None or rb["B"] != B:
             W, S, dev, F = self.world, self.emb.slot_stride, self.device, self.F
-            n = W * B * S
-            rb = {"B": B, "n": n,
+            cap = self._dedup_cap(B) if dedup else B * S
+            n = W * cap
+            rb = {"B": B, "n": n, "dedup": dedup, "cap": cap, "rec": 1 if dedup else S,
+                  "overflow": torch.zeros(1, dtype=torch.int32, device=dev),
                   "send": torch.empty(n, dtype=torch.int32, device=dev),
                   "recv": torch.empty(n, dtype=torch.int32, device=dev),
                   "slot_of": torch.empty(B, F, dtype=torch.int32, device=dev),
@@ -719,12 +759,33 @@ class ShardedDeepFM:
                   "grecv": torch.zeros(n, self.k, dtype=torch.float32, device=dev),
                   "zoff": torch.zeros(F, dtype=torch.int64, device=dev),
                   "nslots": torch.full((F,), n, dtype=torch.int64, device=dev)}
-            self._row_bufs = rb
+            if dedup and isinstance(self.ops, HipShardOps):
+                rb["ws"] = torch.empty(max(_lib.lib().rs_shard_dedup_workspace_size(B * F, W), 1),
+                                       dtype=torch.uint8, device=dev)
+            setattr(self, name, rb)
         return rb
 
     def route(self, ids, rb):
-        """Step 1: the row-id records to every owner and slot_of."""
+        """Step 1: the row-id records (or distinct rows) to every owner and slot_of."""
+        if rb["dedup"]:
+            return self.ops.dedup_route(self.emb, ids, rb)
         return self.ops.row_route(self.emb, ids, rb["send"], rb["slot_of"])
+
+    def _routed(self, ids, check):
+        """Route the batch; with dedup and ``check``, a capacity overflow on
+        any rank (collective decision: one host sync) reroutes it through the
+        field-range records, so the step stays exact."""
+        B = ids.shape[0]
+        rb = self._rbufs(B)
+        self.route(ids, rb)
+        if rb["dedup"] and check:
+            f = self.ops.overflow_flag(rb)
+            if self.world > 1:
+                dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
+            if bool(f.item()):
+                rb = self._rbufs(B, dedup=False)
+                self.route(ids, rb)
+        return rb
 
     def serve(self, recv, reply):
         """Step 3 (owner): rows of the received record words (-1 -> zero row)."""
@@ -748,7 +809,7 @@ class ShardedDeepFM:
                 views.append((flat[o:o + K * N].view(K, N), flat[o + K * N:o + K * N + N]))
                 o += K * N + N
             dw1, dv, dw0 = flat[o:o + d], flat[o + d:o + d + d * kfm].view(d, kfm), flat[o + d + d * kfm:]
-            n_look = W * B * S
+            n_look = W * ((B * S + 63) // 64 * 64)  # either exchange layout
             tb = {"B": B, "flat": flat, "layers": layers, "dnn_views": views, "dw1": dw1, "dv": dv, "dw0": dw0,
                   "x": torch.empty(B, d, dtype=torch.float32, device=dev),
                   "fm": torch.empty(B, 1, dtype=torch.float32, device=dev),
@@ -797,8 +858,8 @@ class ShardedDeepFM:
             dense, ids = _split_criteo(inputs, self.nd, self.device)
             labels = _to_device_f32(labels, self.device).reshape(-1)
         B, W = ids.shape[0], self.world
-        rb, tb = self._rbufs(B), self._tbufs(B)
-        self.route(ids, rb)
+        tb = self._tbufs(B)
+        rb = self._routed(ids, check)
         recv = rb["send"]
         if sh.exchanges:
             recv = rb["recv"]
@@ -809,12 +870,15 @@ class ShardedDeepFM:
             dist.all_to_all_single(got, reply, group=self.group)
         loss = torch.empty(B, dtype=torch.float32, device=self.device) if return_loss else None
         dx = self.ops.deepfm_grads(self, got, rb, dense, labels, 1.0 / (W * B), tb, loss)
-        gsend = self.ops.scatter_row_grads(self, dx, rb)
+        if rb["dedup"]:
+            gsend = self.ops.dedup_grads(self, dx, rb)  # one row per distinct row
+        else:
+            gsend = self.ops.scatter_row_grads(self, dx, rb)
         grecv = gsend
         if sh.exchanges:
             grecv = rb["grecv"]
             dist.all_to_all_single(grecv, gsend, group=self.group)
-        self.ops.owner_row_sgd(self, recv, grecv, lr, tb)
+        self.ops.owner_row_sgd(self, recv, grecv, lr, tb, rb["rec"])
         if W > 1:
             dist.all_reduce(tb["flat"], group=self.group)
         self.ops.deepfm_apply(self, tb, lr)
@@ -839,8 +903,7 @@ class ShardedDeepFM:
         if not sh.exchanges and not self.force_rows and isinstance(self.ops, HipShardOps):
             self.ops.deepfm_table(self, ids, dense, out)  # world 1: the shard is the whole table
         else:
-            rb = self._rbufs(B)
-            self.route(ids, rb)
+            rb = self._routed(ids, check)
             recv = rb["send"]
             if sh.exchanges:
                 recv = rb["recv"]
