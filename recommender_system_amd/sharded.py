@@ -234,7 +234,9 @@ class HipShardOps:
             acts.append(layer(acts[-1]))
         dnn_out = dnn.output_layer(acts[-1])
         fm_out = tb["fm"]
-        call("rs_fm_fwd", ptr(x), d, d, ptr(sh.prepared), ptr(sh.w0), kfm, ptr(fm_out), B, st)
+        # FMLayer on the dense x: its own packed image (nd = d, no fields)
+        call("rs_fm_prepare", ptr(sh.w1), ptr(sh.v), d, 0, 0, kfm, ptr(tb["fm_prep"]), st)
+        call("rs_fm_fwd", ptr(x), d, d, ptr(tb["fm_prep"]), ptr(sh.w0), kfm, ptr(fm_out), B, st)
         gw = (ptr(tb["gemm_ws"]), tb["gemm_ws"].numel())
         s = tb["s"]
         call("rs_gemm", 0, 0, B, kfm, d, 1.0, ptr(x), d, ptr(sh.v), kfm, 0.0, ptr(s), kfm, None, 0, *gw, st)
@@ -823,6 +825,7 @@ class ShardedDeepFM:
                 gmax = max(lib.rs_gemm_workspace_size(K, N, B) for _, (K, N) in layers)
                 gmax = max(gmax, lib.rs_gemm_workspace_size(B, kfm, d))
                 tb["gemm_ws"] = torch.empty(max(gmax, 1), dtype=torch.uint8, device=dev)
+                tb["fm_prep"] = torch.empty(lib.rs_fm_prepared_size(d, 0, 0, kfm), dtype=torch.float32, device=dev)
                 tb["emb_ws"] = torch.empty(max(lib.rs_embedding_sgd_workspace_size(n_look), 1), dtype=torch.uint8,
                                            device=dev)
             self._train_bufs = tb

@@ -1065,6 +1065,8 @@ def _simulated_deepfm_train(models, batches, labels, lr):
     tbs = [m._tbufs(B) for m in models]
     for m, rb, (_, ids) in zip(models, rbs, batches):
         m.route(ids, rb)
+        if rb["dedup"]:  # this helper has no fallback: the capacity must hold
+            assert not bool(m.ops.overflow_flag(rb).item())
     for o in range(W):
         rbs[o]["recv"].view(W, -1).copy_(torch.stack([rbs[r]["send"].view(W, -1)[o] for r in range(W)]))
     for m, rb in zip(models, rbs):
@@ -1094,7 +1096,7 @@ def _simulated_deepfm_train(models, batches, labels, lr):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,B,k,dedup", [(1, 300, 16, None), (2, 200, 16, None), (3, 129, 8, None),
-                                             (8, 128, 16, None), (1, 300, 16, 1.0), (3, 129, 8, 0.5),
+                                             (8, 128, 16, None), (1, 300, 16, 1.0), (3, 129, 8, 1.0),
                                              (8, 128, 16, 1.0)])
 def test_gpu_sharded_deepfm_train_simulated_world(gpu, world, B, k, dedup):
     """ShardedDeepFM.train_step's HIP path (rs_embed_gather from the exchange
