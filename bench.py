@@ -550,6 +550,41 @@ def bench_sharded_deepfm(args, world, rank):
 
     fdt, fslot_ms = _timed_graph(finish, args.steps, 2, world, chunk=16)
     fin_ms = _max_over_ranks(fslot_ms, world)
+    # secondary: the deduplicated exchange on Zipf(1.2) ids (hot rows repeat:
+    # each owner receives every distinct row once per rank) and the training
+    # step (forward exchange, local backward, reverse all-to-all of dL/drow,
+    # owner row SGD, all-reduce of the replicated gradient)
+    zrng = np.random.default_rng(SEED + 17 + rank)
+    zipf_pool = torch.as_tensor(np.minimum(zrng.zipf(1.2, size=(npool, B, F)) - 1, V - 1).astype(np.int32),
+                                device=dev)
+    dmodel = ShardedDeepFM(cols, kfm, 1e-4, 1e-4, [256, 128, 64], 1, "relu", embed_dim=k, device=dev, seed=SEED,
+                           dedup=0.5, table_init=False)
+    dmodel.emb._force_exchange = True
+    dmodel.emb.table_shard = model.emb.table_shard  # same shard (no second 1e8-row allocation)
+    over = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def step_zipf(m):
+        def st(i):
+            j = i % npool
+            m.forward((dense_pool[j], zipf_pool[j]), check=False, out=out)
+        return st
+
+    zdt, _ = _timed(step_zipf(model), max(10, args.steps // 2), 2, world, events=False)
+    ddt, _ = _timed(step_zipf(dmodel), max(10, args.steps // 2), 2, world, events=False)
+    over += dmodel.ops.overflow_flag(dmodel._rbufs(B))
+    dist.all_reduce(over, op=dist.ReduceOp.MAX)
+    nz = max(10, args.steps // 2)
+    distinct = float(np.mean([sum(len(np.unique((model.emb.offsets[None, :].cpu().numpy() +
+                                                 zipf_pool[j].cpu().numpy().astype(np.int64))[:, c]))
+                                  for c in range(F)) for j in range(2)])) / (B * F)
+    labels = (torch.rand(npool, B, generator=g, device=dev) < 0.25).to(torch.float32)
+
+    def train(i):
+        j = i % npool
+        model.train_step((dense_pool[j], ids_pool[j]), labels[j], lr=0.01, check=False)
+
+    nt = max(10, args.steps // 4)
+    tdt, _ = _timed(train, nt, 2, world, events=False)
     flops = B * 2 * (429 * 256 + 256 * 128 + 128 * 64 + 64)
     ms = dt / args.steps * 1e3
     S = model.emb.slot_stride
@@ -565,7 +600,21 @@ def bench_sharded_deepfm(args, world, rank):
                         "owner_field_ranges": model.emb.owner_field_ranges, "slots_per_sample_per_owner": S,
                         "id_bytes_per_rank_each_way": world * B * S * 4,
                         "row_bytes_per_rank_each_way": world * B * S * k * 4,
-                        "exchange_ms_per_step": ms - fin_ms}}
+                        "exchange_ms_per_step": ms - fin_ms},
+           "zipf_ids": {"distinct_lookup_fraction": distinct,
+                        "field_range_records": {"samples_per_s": world * nz * B / zdt, "ms_per_step": zdt / nz * 1e3,
+                                                "row_bytes_per_rank_each_way": world * B * S * k * 4},
+                        "dedup": {"samples_per_s": world * nz * B / ddt, "ms_per_step": ddt / nz * 1e3,
+                                  "capacity_fraction": 0.5, "overflow_seen": bool(over.item()),
+                                  "row_bytes_per_rank_each_way": dmodel._rbufs(B)["n"] * k * 4},
+                        "timing": "eager launches (the dedup route's radix sort is not graph-captured here)",
+                        "note": "Zipf(1.2) ids per field, clipped to the vocab; dedup = rs_shard_dedup_route: "
+                                "each owner receives each distinct row once per rank"},
+           "train_step": {"samples_per_s": world * nt * B / tdt, "ms_per_step": tdt / nt * 1e3,
+                          "timing": "eager launches",
+                          "note": "ShardedDeepFM.train_step: row exchange, local DeepFM backward (rs_gemm), "
+                                  "rs_scatter_rows + reverse all-to-all of dL/drow, owner rs_embedding_sgd, "
+                                  "all-reduce of the flat replicated gradient, SGD"}}
     return res, V
 
 
@@ -1097,6 +1146,21 @@ def bench_fm_train(args, world, rank):
     k = 16
     m, step = setup(B, V, k)
     dt, slot = _timed_graph(step, args.steps, args.warmup, world, chunk=16)
+    # the same step on Zipf(1.05) ids: hot rows repeat thousands of times per
+    # batch, so the sparse update's segment sums (one lane per column, fixed
+    # order) carry long segments
+    zrng = np.random.default_rng(SEED + 5)
+    zpool = torch.as_tensor(np.minimum(zrng.zipf(1.05, size=(16, B, F)) - 1, V - 1).astype(np.int32), device=dev)
+    zd = torch.rand(16, B, nd, device=dev)
+    zl = (torch.rand(16, B, device=dev) < 0.25).to(torch.float32)
+    zo = torch.as_tensor(np.arange(F, dtype=np.int64) * V, device=dev)
+    zv = torch.full((F,), V, dtype=torch.int64, device=dev)
+
+    def step_z(i):
+        m.train_step(zd[i % 16], zpool[i % 16], zl[i % 16], zo, zv, lr=0.01, check_ids=False)
+
+    dtz, _ = _timed_graph(step_z, args.steps, args.warmup, world, chunk=16)
+    zmax = int(max(np.bincount(zpool[j, :, c].cpu().numpy()).max() for j in range(2) for c in range(F)))
     n_rows = nd + F * V
     decay = 2 * n_rows * (k + 1) * 4
     ach = decay / (slot * 1e-3)
@@ -1130,7 +1194,10 @@ def bench_fm_train(args, world, rank):
                   "frac": ach / PEAK_HBM, "traffic": None,
                   "kernel": "whole step; bytes = the l2 decay pass (read+write of w1 and v)", "kernel_ms": slot,
                   "decay_bytes_per_step": decay},
-                 {"deepfm_train": {"samples_per_s": n_d * B / dtd, "ms_per_step": dtd / n_d * 1e3,
+                 {"zipf_ids": {"samples_per_s": args.steps * B / dtz, "ms_per_step": dtz / args.steps * 1e3,
+                               "max_lookups_of_one_row": zmax,
+                               "note": "Zipf(1.05) ids per field (clipped to the vocab)"},
+                  "deepfm_train": {"samples_per_s": n_d * B / dtd, "ms_per_step": dtd / n_d * 1e3,
                                    "note": "DeepFM.train_step: gather, DNN 429-256-128-64-1 fwd/bwd (rs_dense_fwd, "
                                            "rs_gemm), FM grads, SGD + l2, row-sparse embedding SGD"},
                   "dcn_train": {"samples_per_s": n_d * B / dtc, "ms_per_step": dtc / n_d * 1e3,
@@ -1212,7 +1279,7 @@ def main():
                         "ids": "int32 uniform per field", "parallelism": f"dp{world}+rowshard{world}"}),
             "roofline": res["roofline"], "cpu_baseline": res["cpu_baseline"],
         }
-        for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "exchange", "fm_hotpath_sharded"):
+        for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "exchange", "train_step", "fm_hotpath_sharded"):
             if key in res:
                 line[key] = res[key]
         _emit(line)

@@ -246,8 +246,8 @@ __global__ __launch_bounds__(256) void emb_keys_kernel(const void* ids, int64_t 
 // segment's gradient rows (grad row of lookup j = b*F + c at
 // grad[b*ldg + c*k]) in lookup order and applies table[r] -= lr * G.
 // One thread per (position, column): the k columns of a segment are summed
-// by k adjacent lanes (a hot row's duplicates cost one pass, not k), each
-// in the same fixed lookup order, so the result stays bitwise reproducible.
+// by k adjacent lanes (a hot row's duplicates cost one pass, not k), each in
+// the same fixed order (seg_sum8), so the result stays bitwise reproducible.
 __global__ __launch_bounds__(256) void emb_apply_kernel(const uint32_t* __restrict__ key,
                                                         const uint32_t* __restrict__ val, int64_t n, int F, int k,
                                                         const float* __restrict__ grad, int64_t ldg, float lr,
@@ -258,13 +258,12 @@ __global__ __launch_bounds__(256) void emb_apply_kernel(const uint32_t* __restri
   if (p >= n) return;
   const uint32_t r = key[p];
   if (r == 0xffffffffu || (p > 0 && key[p - 1] == r)) return;
-  float acc = 0.f;
-  for (int64_t q = p; q < n && key[q] == r; ++q) {
+  const float acc = seg_sum8(p, seg_end(key, p, n, r), [&](int64_t q) {
     const int64_t j = val[q];
     const int64_t b = j / F;
     const int c = (int)(j - b * F);
-    acc += grad[b * ldg + (int64_t)c * k + f];
-  }
+    return grad[b * ldg + (int64_t)c * k + f];
+  });
   table[(int64_t)r * k + f] -= lr * acc;
 }
 

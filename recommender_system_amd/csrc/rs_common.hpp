@@ -137,6 +137,33 @@ struct Chunk {
 
 // Sum over the 16 lanes of a DPP row (lanes 16r..16r+15); every lane of the
 // row receives the total.  Four row_ror steps, VALU only.
+// Sorted-segment helpers for the deterministic scatter-adds (embedding SGD,
+// FM training, dedup gradients): the end of key r's segment starting at p
+// (binary search: keys are sorted), and the segment's sum of get(q) with 8
+// independent partial sums (q mod 8 in segment order) combined in a fixed
+// tree — a hot row's thousands of duplicates keep 8 loads in flight instead
+// of one, and the result is the same on every run.
+__device__ __forceinline__ int64_t seg_end(const uint32_t* __restrict__ key, int64_t p, int64_t n, uint32_t r) {
+  int64_t lo = p + 1, hi = n;  // first q > p with key[q] != r
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (key[mid] == r) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+template <class G>
+__device__ __forceinline__ float seg_sum8(int64_t p, int64_t e, G get) {
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int64_t q = p;
+  for (; q + 8 <= e; q += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += get(q + u);
+  }
+  for (int u = 0; q < e; ++q, ++u) a[u] += get(q);
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
 __device__ __forceinline__ float row16_sum(float x) {
   x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xF, 0xF, false));
   x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x124, 0xF, 0xF, false));

@@ -139,14 +139,12 @@ __global__ __launch_bounds__(256) void dedup_grad_sum(const uint32_t* __restrict
   if (r == 0xffffffffu || (p > 0 && key[p - 1] == r)) return;
   const int32_t slot = slot_of[val[p]];
   if (slot < 0) return;
-  float acc = 0.f;
-  for (int64_t q = p; q < n && key[q] == r; ++q) {
+  dst[(int64_t)slot * k + f] = seg_sum8(p, seg_end(key, p, n, r), [&](int64_t q) {
     const int64_t j = val[q];
     const int64_t b = j / F;
     const int c = (int)(j - b * F);
-    acc += grad[b * ldg + (int64_t)c * k + f];
-  }
-  dst[(int64_t)slot * k + f] = acc;
+    return grad[b * ldg + (int64_t)c * k + f];
+  });
 }
 
 }  // namespace rs

@@ -197,8 +197,8 @@ __global__ __launch_bounds__(256) void fm_train_apply(FmTrainArgs a) {
     const int f = (int)(t - p * K1);
     const uint32_t r = a.key_out[p];
     if (p == 0 || a.key_out[p - 1] != r) {
-      float acc = 0.f;
-      for (int64_t q = p; q < n && a.key_out[q] == r; ++q) acc += a.contrib[(int64_t)a.val_out[q] * K1 + f];
+      const float acc = seg_sum8(p, seg_end(a.key_out, p, n, r),
+                                 [&](int64_t q) { return a.contrib[(int64_t)a.val_out[q] * K1 + f]; });
       if (f < a.k) a.v[(int64_t)r * a.k + f] -= a.lr * acc;
       else a.w1[r] -= a.lr * acc;
     }
