@@ -581,7 +581,7 @@ def bench_sharded_deepfm(args, world, rank):
 
     def train(i):
         j = i % npool
-        model.train_step((dense_pool[j], ids_pool[j]), labels[j], lr=0.01, check=False)
+        model.train_step((dense_pool[j], ids_pool[j]), labels[j], lr=0.01, check=False, dropout=False)
 
     nt = max(10, args.steps // 4)
     tdt, _ = _timed(train, nt, 2, world, events=False)
@@ -1174,7 +1174,7 @@ def bench_fm_train(args, world, rank):
     lab = (torch.rand(16, B, device=dev) < 0.25).to(torch.float32)
 
     def step_dfm(i):
-        dfm.train_step((dense_pool[i % 16], ids_pool[i % 16]), lab[i % 16], lr=0.01, check_ids=False)
+        dfm.train_step((dense_pool[i % 16], ids_pool[i % 16]), lab[i % 16], lr=0.01, check_ids=False, dropout=False)
 
     n_d = max(10, args.steps // 5)
     dtd, _ = _timed_graph(step_dfm, n_d, args.warmup, world, chunk=16)
@@ -1183,7 +1183,7 @@ def bench_fm_train(args, world, rank):
     dcn = rs.DCN(cols, [256, 128, 64], 1, "relu", 3, embed_dim=16, seed=SEED, device=dev)
 
     def step_dcn(i):
-        dcn.train_step((dense_pool[i % 16], ids_pool[i % 16]), lab[i % 16], lr=0.01, check_ids=False)
+        dcn.train_step((dense_pool[i % 16], ids_pool[i % 16]), lab[i % 16], lr=0.01, check_ids=False, dropout=False)
 
     dtc, _ = _timed_graph(step_dcn, n_d, args.warmup, world, chunk=16)
     return _line("FM training samples/sec @ batch 4096, 26 x 1e6 one-hot columns, k 16 (SGD + l2, compile_fit)",

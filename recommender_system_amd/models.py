@@ -108,6 +108,24 @@ def _check_train_tower(name, dnn):
         raise NotImplementedError(f"{name}.train_step: 'relu' or linear hidden layers only")
 
 
+_DROPOUT_WARNED = set()
+
+
+def _dropout_notice(name, dnn, dropout):
+    """The training steps run DNNLayer's Dropout (layer/interaction.py:44) as
+    the identity: its masks are TF's own random draws, so no parity with the
+    reference's fit exists to test.  A layer with rate > 0 trained this way
+    optimises the no-dropout objective: say so once, unless the caller
+    passed dropout=False to acknowledge it."""
+    if dropout is False or not getattr(dnn, "dropout", 0):
+        return
+    if name not in _DROPOUT_WARNED:
+        _DROPOUT_WARNED.add(name)
+        import warnings
+        warnings.warn(f"{name}.train_step: DNNLayer dropout={dnn.dropout} is applied as the identity (no dropout "
+                      f"masks); pass dropout=False to silence", RuntimeWarning, stacklevel=3)
+
+
 def _gemm_ws(model, nbytes):
     ws = model.__dict__.get("_gemm_wsbuf")
     if ws is None or ws.numel() < max(nbytes, 1):
@@ -216,7 +234,7 @@ class DeepFM(KerasModule):
             self._err.check("DeepFM")
         return logit
 
-    def train_step(self, inputs, labels, lr=0.01, return_loss=False, check_ids=True):
+    def train_step(self, inputs, labels, lr=0.01, return_loss=False, check_ids=True, dropout=None):
         """One step of compile_fit (utils/compile_fit.py:9-15: SGD(lr),
         binary cross-entropy on sigmoid(0.5 (FM + DNN)), FMLayer's l2
         regularisers) on a batch, every weight updated in place: the DNN's
@@ -233,6 +251,7 @@ class DeepFM(KerasModule):
         if dnn.output_layer.units != 1:
             raise NotImplementedError("DeepFM.train_step: output_dim 1 only")
         _check_train_tower("DeepFM", dnn)
+        _dropout_notice("DeepFM", dnn, dropout)
         B, dev, st = ids.shape[0], self._dev, _lib.stream()
         d, kfm = self.nd + e.n_fields * e.k, fm.k
         emp = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=dev)
@@ -365,7 +384,7 @@ class DCN(KerasModule):
     def _invalidate(self):
         self._fused_key = None
 
-    def train_step(self, inputs, labels, lr=0.01, return_loss=False, check_ids=True):
+    def train_step(self, inputs, labels, lr=0.01, return_loss=False, check_ids=True, dropout=None):
         """One step of compile_fit on DCN (model/dcn.py:24-34, utils/compile_fit.py:
         9-15): SGD(lr), binary cross-entropy on sigmoid(Dense1([CrossLayer(x) |
         DNNLayer(x)])), CrossLayer's l2(reg_w) / l2(reg_b) regularisers
@@ -379,6 +398,7 @@ class DCN(KerasModule):
         dense, ids = _split_criteo(inputs, self.nd, self._dev)
         labels = _to_device_f32(labels, self._dev).reshape(-1)
         e, cl, dnn, out = self.embed_layer, self.cross_layer, self.dense_layer, self.output_layer
+        _dropout_notice("DCN", dnn, dropout)
         _check_train_tower("DCN", dnn)
         B, d, dev, st = ids.shape[0], self.d, self._dev, _lib.stream()
         od, Lc = dnn.output_layer.units, cl.layer_num

@@ -831,7 +831,7 @@ class ShardedDeepFM:
             self._train_bufs = tb
         return tb
 
-    def train_step(self, inputs, labels, lr=0.01, return_loss=False, check=True):
+    def train_step(self, inputs, labels, lr=0.01, return_loss=False, check=True, dropout=None):
         """One SGD step of compile_fit (utils/compile_fit.py:9-15: SGD(lr),
         binary cross-entropy on sigmoid(0.5 (FM + DNN)), FMLayer's l2
         regularisers; model/deepFM.py:23-31) over the GLOBAL batch — every
@@ -848,9 +848,10 @@ class ShardedDeepFM:
         Every gradient comes from the pre-step weights; every rank's update of
         the replicated parameters is identical.  Returns the per-sample losses
         of the local batch (before the step) if ``return_loss``."""
-        from .models import _split_criteo
+        from .models import _split_criteo, _dropout_notice
         from .layers import _to_device_f32
         sh = self.emb
+        _dropout_notice("ShardedDeepFM", self.dnn, dropout)
         if self.dnn.output_layer.units != 1 or any(l.activation not in (None, "linear", "relu")
                                                    for l in self.dnn.hidden_layer):
             raise NotImplementedError("ShardedDeepFM.train_step: output_dim 1, 'relu' / linear hidden layers")

@@ -280,3 +280,30 @@ def test_rs_gemm_mfma_matches_torch(gpu, ta, tb, M, N, K):
     scale = float(opA.abs().sum(1).max() * opB.abs().max()) if K else 1.0
     assert float((outs[0].double() - ref).abs().max()) <= 2e-6 * max(scale, 1.0)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.gpu
+def test_train_step_dropout_notice(gpu):
+    """DNNLayer's Dropout is the identity in the training steps: a model with
+    rate > 0 gets one RuntimeWarning saying so; dropout=False acknowledges it
+    (no warning); rate 0 never warns."""
+    import warnings
+    import recommender_system_amd as rs
+    from recommender_system_amd import models as M
+    from tests.helpers import criteo_columns
+    rng = np.random.default_rng(0)
+    vocab = [5] * 26
+    B = 8
+    dense = rng.random((B, 13)).astype(np.float32)
+    ids = np.stack([rng.integers(0, 5, B) for _ in vocab], 1)
+    t = rng.integers(0, 2, B).astype(np.float32)
+    m = rs.DeepFM(criteo_columns(vocab, embed_dim=8), 4, 1e-4, 1e-4, [16], 1, "relu", embed_dim=8, seed=1)
+    m.dnn.dropout = 0.2
+    M._DROPOUT_WARNED.discard("DeepFM")
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        m.train_step((dense, ids), t, lr=0.01, dropout=False)
+        assert not [x for x in w if issubclass(x.category, RuntimeWarning)]
+        m.train_step((dense, ids), t, lr=0.01)
+        m.train_step((dense, ids), t, lr=0.01)
+        assert len([x for x in w if "dropout" in str(x.message)]) == 1
