@@ -313,7 +313,7 @@ __global__ __launch_bounds__(16 * 64) void dcn_fused(CrossArgs a, EmbedCrossArgs
   const int F = e.F, RS = t.rs, d = a.d;
 
   // tower weights and biases first (independent of the ids)
-  floatx4 ring[4];
+  floatx4 ring[MLP_R];
   mlp_first_fill<NW>(t, ring);
   float* par = tsm + 32 * RS + NW * 256;
   for (int i = tid; i < t.ptot; i += NW * 64) par[i] = t.prep[t.wtot + i];

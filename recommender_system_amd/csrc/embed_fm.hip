@@ -232,7 +232,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   // zero padding do not depend on the ids; issue them first
   extern __shared__ float tsm[];
   __shared__ float fmlog[TW ? 16 : 1];
-  floatx4 ring[TW ? 4 : 1];
+  floatx4 ring[TW ? MLP_R : 1];
   const int xrs = TW ? tw->rs : 0;
   if constexpr (TW) {
     mlp_first_fill<NW>(*tw, ring);

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(NW * 64) void mlp_tower(MlpArgs a) {
   // layer-0 weights first (independent of everything), then the input tile
   // (one row per wave, coalesced; rows past M re-read row M-1 and are never
   // stored) and the bias/alpha block into LDS
-  floatx4 ring[4];
+  floatx4 ring[MLP_R];
   mlp_first_fill<NW>(a, ring);
   for (int r = w; r < 16; r += NW) {
     const int64_t m = m0 + r < a.M ? m0 + r : a.M - 1;

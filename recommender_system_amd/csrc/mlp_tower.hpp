@@ -106,13 +106,17 @@ __device__ __forceinline__ MlpItem mlp_item(int item, int T, int G, int S) {
 // the ring D deep, refilling the slot it just consumed with group g + D, so
 // every MFMA's weights were requested D groups (4D MFMAs) earlier.  D | (g1-g0)
 // keeps it branch-free; refills past g1 are clamped in-bounds re-reads.
-__device__ __forceinline__ void mlp_ring_fill(floatx4 (&ring)[4], const floatx4* bp, int g0, int g1) {
+#ifndef MLP_RING
+#define MLP_RING 4
+#endif
+constexpr int MLP_R = MLP_RING;  // B-fragment ring slots (the deepest D)
+__device__ __forceinline__ void mlp_ring_fill(floatx4 (&ring)[MLP_R], const floatx4* bp, int g0, int g1) {
 #pragma unroll
-  for (int u = 0; u < 4; ++u) ring[u] = bp[(int64_t)min(g0 + u, g1 - 1) * 64];
+  for (int u = 0; u < MLP_R; ++u) ring[u] = bp[(int64_t)min(g0 + u, g1 - 1) * 64];
 }
 
 template <int D>
-__device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[4], const float* __restrict__ ap,
+__device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[MLP_R], const float* __restrict__ ap,
                                           const floatx4* __restrict__ bp, int g0, int g1, floatx4& acc) {
   // A fragments are read one group ahead so the LDS latency hides behind
   // the previous group's MFMAs
@@ -134,9 +138,14 @@ __device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[4], const float* __res
   }
 }
 
-__device__ __forceinline__ void mlp_mac(floatx4 (&ring)[4], const float* ap, const floatx4* bp, int g0, int g1,
+__device__ __forceinline__ void mlp_mac(floatx4 (&ring)[MLP_R], const float* ap, const floatx4* bp, int g0, int g1,
                                         floatx4& acc) {
   const int n = g1 - g0;  // wave-uniform
+  if constexpr (MLP_R >= 9) {
+    if (n % 9 == 0) return mlp_mac_d<9>(ring, ap, bp, g0, g1, acc);
+    if (n % 8 == 0) return mlp_mac_d<8>(ring, ap, bp, g0, g1, acc);
+    if (n % 6 == 0) return mlp_mac_d<6>(ring, ap, bp, g0, g1, acc);
+  }
   // (a 4-deep ring gets a full vmcnt(0) at its loop head from the compiler)
   if (n % 3 == 0) mlp_mac_d<3>(ring, ap, bp, g0, g1, acc);
   else if (n % 2 == 0) mlp_mac_d<2>(ring, ap, bp, g0, g1, acc);
@@ -147,7 +156,7 @@ __device__ __forceinline__ void mlp_mac(floatx4 (&ring)[4], const float* ap, con
 // yet taken) and whose layer-0 ring was filled by the caller.  smem layout:
 // buf0 [16][rs] | buf1 [16][rs] | red [NW][256] | par [ptot] (loaded here).
 template <int NW>
-__device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, int64_t m0, floatx4 (&ring)[4],
+__device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, int64_t m0, floatx4 (&ring)[MLP_R],
                                                const float* extra_lds = nullptr) {
   const int RS = a.rs;
   float* red = smem + 32 * RS;
@@ -232,7 +241,7 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
 
 // Layer-0 ring fill for the wave's first item (issue before anything else).
 template <int NW>
-__device__ __forceinline__ void mlp_first_fill(const MlpArgs& a, floatx4 (&ring)[4]) {
+__device__ __forceinline__ void mlp_first_fill(const MlpArgs& a, floatx4 (&ring)[MLP_R]) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int T = a.Np[0] >> 4, G = a.Kp[0] >> 4;
