@@ -437,6 +437,23 @@ int rs_sgd_update(float* w, const float* grad, int64_t n, float lr, float l2,
 int rs_head_grad(const float* fm, const float* dnn, const float* labels,
                  int64_t batch, float c_fm, float c_dnn, float* g_fm,
                  float* g_dnn, float* loss, rs_stream_t stream);
+/* PNN training (the reference's GradientTape loop, model/pnn.py:74-85):
+ * rs_bce_prob_grad: tf.reduce_mean(losses.binary_crossentropy(y[B],
+ *  pre[B,1])) on the DNN LOGIT as Keras computes it — pre clipped to
+ *  [1e-7, 1-1e-7], labels broadcast against the [B,1] output (per sample i
+ *  the mean over j of BCE(y_j, pre_i)): loss[i] = -(ybar log(q_i+eps) +
+ *  (1-ybar) log(1-q_i+eps)), g[i] = dL/dpre_i (0 outside the clip range).
+ * rs_inner_product_bwd: InnerProductLayer backward (layer/interaction.py:
+ *  170-183): demb[b,i,:] = dflat[b,i,:] + sum_{j!=i} dinner[b,p(i,j)]
+ *  emb[b,j,:] (p = the row-major pair index); 2 <= n_fields <= 64, k <= 64. */
+int rs_bce_prob_grad(const float* pred, int64_t pred_stride,
+                     const float* labels, int64_t batch, float* g, float* loss,
+                     rs_stream_t stream);
+int rs_inner_product_bwd(const float* emb, int64_t emb_stride,
+                         const float* dinner, int64_t dinner_stride,
+                         const float* dflat, int64_t dflat_stride, int n_fields,
+                         int k, int64_t batch, float* demb, int64_t demb_stride,
+                         rs_stream_t stream);
 /* rs_head_grad with g = scale (sigmoid(z) - t) (scale > 0): the sharded
  * DeepFM step's local batch is a 1/world share of the global batch mean,
  * scale = 1 / (world * batch).                                             */

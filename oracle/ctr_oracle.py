@@ -587,6 +587,85 @@ def deepfm_train_step(dense, ids, t, p, lr, l2_w, l2_v, nd=13, act="relu", dt=np
     return out, loss
 
 
+KERAS_EPS = 1e-7  # keras.backend.epsilon()
+
+
+def pnn_bce(pre, t, dt=np.float64):
+    """model/pnn.py:79: tf.reduce_mean(losses.binary_crossentropy(y_train,
+    pre)) with y_train [B] and pre = the DNN LOGIT [B, 1] (no sigmoid).
+    Keras' probability form clips pre to [eps, 1-eps] and adds eps inside the
+    logs; the [B] labels broadcast against [B, 1] to [B, B] before the mean
+    over the last axis, so sample i's loss is the mean over j of
+    BCE(y_j, pre_i) = -(ybar log(q_i + eps) + (1 - ybar) log(1 - q_i + eps)).
+    Returns (mean loss, per-sample losses)."""
+    pre = np.asarray(pre, dt).reshape(-1)
+    t = np.asarray(t, dt).reshape(-1)
+    q = np.clip(pre, KERAS_EPS, 1 - KERAS_EPS)
+    per = -(t[None, :] * np.log(q[:, None] + KERAS_EPS) + (1 - t[None, :]) * np.log(1 - q[:, None] + KERAS_EPS))
+    per = per.mean(axis=1)
+    return per.mean(), per
+
+
+def pnn_train_step(ids, t, p, lr, act="relu", dt=np.float64):
+    """One step of the reference's PNN loop (model/pnn.py:74-81: GradientTape,
+    SGD(lr) over model.variables) for mode 'inner', backpropagated by hand:
+    dL/dpre_i = (-ybar/(q_i+eps) + (1-ybar)/(1-q_i+eps))/B inside the clip
+    range, 0 outside (tf.clip_by_value); the DNN by the chain rule (Dropout is
+    the identity: the loop calls model(X) without training=True); the inner
+    products p_ij = e_i . e_j give de_i += dL/dp_ij e_j; embedding rows by
+    scatter-add.  No regularisers (DNNLayer's Dense layers have none).
+    Returns (new p, per-sample losses before the step)."""
+    ids = cast_ids(ids)
+    t = np.asarray(t, dt).reshape(-1)
+    tables = [np.array(tb, dt) for tb in p["tables"]]
+    k = tables[0].shape[1]
+    F = len(tables)
+    flat = embed_layer(ids, tables, dt)
+    e = flat.reshape(flat.shape[0], F, k)
+    x = np.concatenate([flat, inner_product_layer(e, dt=dt)], axis=1)
+    layers = [(np.array(W, dt), np.array(b, dt)) for W, b in p["dnn_hidden"]] + \
+             [(np.array(p["dnn_out"][0], dt), np.array(p["dnn_out"][1], dt))]
+    acts = [x]
+    for W, b in layers[:-1]:
+        acts.append(activation(acts[-1] @ W + b, act))
+    pre = (acts[-1] @ layers[-1][0] + layers[-1][1])[:, 0]
+    _, loss = pnn_bce(pre, t, dt)
+    B = x.shape[0]
+    ybar = t.mean()
+    q = np.clip(pre, KERAS_EPS, 1 - KERAS_EPS)
+    inside = (pre >= KERAS_EPS) & (pre <= 1 - KERAS_EPS)
+    g = np.where(inside, (-ybar / (q + KERAS_EPS) + (1 - ybar) / (1 - q + KERAS_EPS)) / B, 0.0)
+    delta = g[:, None]
+    new_layers = [None] * len(layers)
+    for li in reversed(range(len(layers))):
+        W, b = layers[li]
+        dW, db = acts[li].T @ delta, delta.sum(0)
+        prev = delta @ W.T
+        if li > 0 and act == "relu":
+            prev = prev * (acts[li] > 0)
+        new_layers[li] = (W - lr * dW, b - lr * db)
+        delta = prev
+    de = delta[:, :F * k].reshape(B, F, k).copy()
+    row, col = pair_indices(F)
+    dpi = delta[:, F * k:]
+    for pi, (i, j) in enumerate(zip(row, col)):
+        de[:, i, :] += dpi[:, pi:pi + 1] * e[:, j, :]
+        de[:, j, :] += dpi[:, pi:pi + 1] * e[:, i, :]
+    for c, tb in enumerate(tables):
+        np.add.at(tb, ids[:, c], -lr * de[:, c, :])
+    return {"tables": tables, "dnn_hidden": new_layers[:-1], "dnn_out": new_layers[-1]}, loss
+
+
+def pnn_loss(ids, t, p, act="relu", dt=np.float64):
+    """The PNN loop's objective (pnn_bce of the inner-mode forward)."""
+    flat = embed_layer(cast_ids(ids), p["tables"], dt)
+    k = np.asarray(p["tables"][0]).shape[1]
+    e = flat.reshape(flat.shape[0], -1, k)
+    x = np.concatenate([flat, inner_product_layer(e, dt=dt)], axis=1)
+    pre = dnn_layer(x, p["dnn_hidden"], p["dnn_out"], act, dt)
+    return pnn_bce(pre, t, dt)[0]
+
+
 def deepfm_loss(dense, ids, t, p, l2_w, l2_v, nd=13, dt=np.float64):
     """compile_fit's objective on DeepFM: mean BCE(t, sigmoid(0.5(fm+dnn)))
     + l2_w |w1|^2 + l2_v |v|^2."""

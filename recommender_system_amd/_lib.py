@@ -79,6 +79,8 @@ SIGNATURES = {
     "rs_sgd_update": (I, [P, P, L, F, F, P]),
     "rs_head_grad": (I, [P, P, P, L, F, F, P, P, P, P]),
     "rs_head_grad_scaled": (I, [P, P, P, L, F, F, F, P, P, P, P]),
+    "rs_bce_prob_grad": (I, [P, L, P, L, P, P, P]),
+    "rs_inner_product_bwd": (I, [P, L, P, L, P, L, I, I, L, P, L, P]),
     "rs_scatter_rows": (I, [P, L, I, I, P, L, P, P]),
     "rs_shard_dedup_workspace_size": (L, [L, I]),
     "rs_shard_dedup_route": (I, [P, I, L, P, P, I, L, L, I, L, P, P, P, P, P, P]),

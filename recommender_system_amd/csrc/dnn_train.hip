@@ -139,6 +139,72 @@ __global__ __launch_bounds__(256) void head_grad_kernel(const float* __restrict_
   if (loss) loss[b] = fmaxf(z, 0.f) - z * t[b] + log1pf(expf(-fabsf(z)));
 }
 
+// PNN's training loss (model/pnn.py:79): tf.reduce_mean(
+// losses.binary_crossentropy(y[B], pre[B,1])) on the DNN's LOGIT (no
+// sigmoid), i.e. Keras' probability form: pre clipped to [eps, 1-eps], eps =
+// 1e-7, and the label vector broadcast against the [B,1] output, so per
+// sample i the loss is the mean over j of BCE(y_j, pre_i):
+//   loss_i = -(ybar log(q_i + eps) + (1 - ybar) log(1 - q_i + eps)),
+//   q_i = clip(pre_i), ybar = mean_j y_j,
+//   dL/dpre_i = (-ybar/(q_i + eps) + (1 - ybar)/(1 - q_i + eps)) / B inside
+//   the clip range, 0 outside (tf.clip_by_value's gradient).
+// One workgroup: ybar by a fixed-order tree, then every sample.
+__global__ __launch_bounds__(1024) void bce_prob_grad_kernel(const float* __restrict__ pre, int64_t ldp,
+                                                             const float* __restrict__ t, int64_t B,
+                                                             float* __restrict__ g, float* __restrict__ loss) {
+  __shared__ float red[1024];
+  float acc = 0.f;
+  for (int64_t b = threadIdx.x; b < B; b += 1024) acc += t[b];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 512; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  const float ybar = red[0] / (float)B;
+  const float eps = 1e-7f;
+  for (int64_t b = threadIdx.x; b < B; b += 1024) {
+    const float p = pre[b * ldp];
+    const float q = fminf(fmaxf(p, eps), 1.f - eps);
+    const bool inside = p >= eps && p <= 1.f - eps;
+    g[b] = inside ? (-ybar / (q + eps) + (1.f - ybar) / (1.f - q + eps)) / (float)B : 0.f;
+    if (loss) loss[b] = -(ybar * logf(q + eps) + (1.f - ybar) * logf(1.f - q + eps));
+  }
+}
+
+// InnerProductLayer backward (layer/interaction.py:170-183, pairs i < j in
+// row-major order p(i,j) = i(2F-i-1)/2 + j-i-1): with the DNN's gradient
+// w.r.t. its input [flat | inner], de[b,i,:] = dflat[b,i,:] + sum_{j != i}
+// dinner[b, p(i,j)] e[b,j,:].  One wave per sample; the sample's rows and
+// pair gradients staged in LDS; the j sum in fixed order.
+constexpr int IPB_MAXF = 64, IPB_MAXK = 64;
+__global__ __launch_bounds__(256) void inner_product_bwd_kernel(const float* __restrict__ e, int64_t lde,
+                                                                const float* __restrict__ dinner, int64_t ldi,
+                                                                const float* __restrict__ dflat, int64_t ldf, int F,
+                                                                int k, int64_t B, float* __restrict__ de,
+                                                                int64_t ldo) {
+  __shared__ float se[4][IPB_MAXF * IPB_MAXK];
+  __shared__ float sp[4][IPB_MAXF * (IPB_MAXF - 1) / 2];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + w;
+  if (b >= B) return;  // wave-uniform; no block barrier below
+  const int n = F * k, P = F * (F - 1) / 2;
+  for (int t = lane; t < n; t += 64) se[w][t] = e[b * lde + t];
+  for (int t = lane; t < P; t += 64) sp[w][t] = dinner[b * ldi + t];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  for (int t = lane; t < n; t += 64) {
+    const int i = t / k, f = t - i * k;
+    float acc = dflat[b * ldf + t];
+    for (int j = 0; j < F; ++j) {
+      if (j == i) continue;
+      const int lo = i < j ? i : j, hi = i < j ? j : i;
+      acc = fmaf(sp[w][lo * (2 * F - lo - 1) / 2 + hi - lo - 1], se[w][j * k + f], acc);
+    }
+    de[b * ldo + t] = acc;
+  }
+}
+
 // FM gradient w.r.t. x: dx[b,i] (+)= g_b (w1_i + sum_f v_if s_bf - x_bi
 // sum_f v_if^2); one thread per (b, i).  s rows lds apart, g ldg apart
 // (the sharded backward reads both out of interleaved [s | g] records);
@@ -431,6 +497,29 @@ extern "C" int rs_sgd_update(float* w, const float* grad, int64_t n, float lr, f
   RS_REQUIRE(w && grad && n > 0, "rs_sgd_update: bad arguments");
   sgd_kernel<<<(unsigned)std::min<int64_t>((n + 255) / 256, 8192), 256, 0, as_stream(stream)>>>(w, grad, n, lr, l2);
   return launch_status("rs_sgd_update");
+}
+
+extern "C" int rs_bce_prob_grad(const float* pred, int64_t pred_stride, const float* labels, int64_t batch, float* g,
+                                float* loss, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(pred && labels && g && batch > 0 && pred_stride >= 1, "rs_bce_prob_grad: bad arguments");
+  bce_prob_grad_kernel<<<1, 1024, 0, as_stream(stream)>>>(pred, pred_stride, labels, batch, g, loss);
+  return launch_status("rs_bce_prob_grad");
+}
+
+extern "C" int rs_inner_product_bwd(const float* emb, int64_t emb_stride, const float* dinner, int64_t dinner_stride,
+                                    const float* dflat, int64_t dflat_stride, int n_fields, int k, int64_t batch,
+                                    float* demb, int64_t demb_stride, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(emb && dinner && dflat && demb && batch > 0 && n_fields >= 2 && n_fields <= IPB_MAXF && k >= 1 &&
+                 k <= IPB_MAXK && n_fields * k <= 4096 && emb_stride >= n_fields * k &&
+                 dflat_stride >= n_fields * k && demb_stride >= n_fields * k &&
+                 dinner_stride >= n_fields * (n_fields - 1) / 2,
+             "rs_inner_product_bwd: bad arguments (2 <= n_fields <= %d, k <= %d, n_fields*k <= 4096)", IPB_MAXF,
+             IPB_MAXK);
+  inner_product_bwd_kernel<<<(unsigned)((batch + 3) / 4), 256, 0, as_stream(stream)>>>(
+      emb, emb_stride, dinner, dinner_stride, dflat, dflat_stride, n_fields, k, batch, demb, demb_stride);
+  return launch_status("rs_inner_product_bwd");
 }
 
 extern "C" int rs_head_grad(const float* fm, const float* dnn, const float* labels, int64_t batch, float c_fm,

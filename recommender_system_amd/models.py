@@ -596,6 +596,56 @@ class PNN(KerasModule):
     def forward(self, inputs, check_ids=True):
         return self.dnn_layer(self.product_inputs(inputs, check_ids))
 
+    def train_step(self, inputs, labels, lr=0.01, return_loss=False, check_ids=True):
+        """One step of the reference's own PNN loop (model/pnn.py:74-81:
+        GradientTape, SGD(lr) over model.variables, loss
+        tf.reduce_mean(losses.binary_crossentropy(y_train, pre)) on the DNN
+        LOGIT — Keras' clipped probability form with the labels broadcast
+        against the [B, 1] output, rs_bce_prob_grad), mode 'inner':
+          [flat | inner] in one launch (rs_embed_inner_fwd), DNN forward with
+          saved activations (rs_dense_fwd), the DNN backward (split-K rs_gemm,
+          rs_col_sum), rs_inner_product_bwd (dflat + sum_j dinner_ij e_j),
+          SGD of the DNN and row-sparse rs_embedding_sgd of the tables.
+        The loop calls model(X) without training=True, so Dropout is the
+        identity there too.  Returns the per-sample losses (before the step)
+        if ``return_loss``."""
+        if self.mode != "inner":
+            raise NotImplementedError("PNN.train_step: mode 'inner' (outer-product backward not built)")
+        dnn = self.dnn_layer
+        if dnn.output_layer.units != 1:
+            raise NotImplementedError("PNN.train_step: output_dim 1 only")
+        _check_train_tower("PNN", dnn)
+        _, ids = _split_criteo(inputs, self.nd, self._dev)
+        labels = _to_device_f32(labels, self._dev).reshape(-1)
+        e = self.embed_layer
+        B, F, k, st = ids.shape[0], e.n_fields, e.k, _lib.stream()
+        emp = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=self._dev)
+        x = self.product_inputs(inputs, check_ids)  # [B, F*k + P]: [flat | inner]
+        layers = list(dnn.hidden_layer) + [dnn.output_layer]
+        acts = [x]
+        for layer in dnn.hidden_layer:
+            acts.append(layer(acts[-1]))
+        pre = dnn.output_layer(acts[-1])
+        g = emp(B)
+        loss = emp(B) if return_loss else None
+        call("rs_bce_prob_grad", ptr(pre), pre.stride(0), ptr(labels), B, ptr(g), ptr(loss), st)
+        gws = _gemm_ws(self, max(_lib.lib().rs_gemm_workspace_size(L.kernel.shape[0], L.kernel.shape[1], B)
+                                 for L in layers))
+        grads, delta = _dnn_backward(layers, acts, g.view(B, 1), (ptr(gws), gws.numel()), emp, st)
+        w = self.width
+        de = emp(B, F * k)
+        call("rs_inner_product_bwd", ptr(x), w, ptr(delta) + 4 * F * k, w, ptr(delta), w, F, k, B, ptr(de), F * k,
+             st)
+        _dnn_apply(grads, lr, st)
+        ws_n = _lib.lib().rs_embedding_sgd_workspace_size(B * F)
+        ws = self.__dict__.get("_emb_ws")
+        if ws is None or ws.numel() < ws_n:
+            ws = self.__dict__["_emb_ws"] = torch.empty(ws_n, dtype=torch.uint8, device=self._dev)
+        call("rs_embedding_sgd", ptr(e.table), e.total_rows, k, ptr(ids), _lib.id_kind(ids), ids.stride(0),
+             ptr(e.field_offsets), ptr(e.field_vocab), F, B, ptr(de), F * k, float(lr), ptr(ws), None, st)
+        self._weights_changed()
+        return loss
+
 
 class DIN(TowerMixin, KerasModule):
     """DIN — model/din.py:15-95.  ``forward(inputs)`` takes the reference's

@@ -293,3 +293,62 @@ def test_embed_fm_train_step_gradient_matches_finite_differences():
         check(p["w1"], new["w1"], idx)
     for idx in [(1, 1), (6, 0)]:
         check(p["v"], new["v"], idx)
+
+
+def test_pnn_bce_is_the_keras_broadcast_form():
+    """O.pnn_bce == Keras' binary_crossentropy on a [B] label vector against a
+    [B, 1] logit output, written out: clip to [eps, 1-eps], eps inside the
+    logs, the [B, B] broadcast, mean over the last axis, then the batch mean
+    (model/pnn.py:79)."""
+    rng = np.random.default_rng(3)
+    pre = np.concatenate([rng.random(5), [-0.3, 1.7]])  # two outside the clip range
+    t = np.array([1, 0, 1, 1, 0, 0, 1], np.float64)
+    eps = 1e-7
+    q = np.clip(pre, eps, 1 - eps)
+    want = np.array([[-(t[j] * np.log(q[i] + eps) + (1 - t[j]) * np.log(1 - q[i] + eps)) for j in range(7)]
+                     for i in range(7)]).mean(axis=1)
+    mean, per = O.pnn_bce(pre[:, None], t)
+    np.testing.assert_allclose(per, want, rtol=1e-13)
+    assert abs(mean - want.mean()) < 1e-13
+
+
+def test_pnn_train_step_gradient_matches_finite_differences():
+    """oracle.pnn_train_step's hand backprop (the Keras-broadcast BCE on the
+    logit, the DNN, the inner products' e_i . e_j backward, embedding
+    scatter-add) == central differences of the PNN loop's objective, for
+    embedding rows (one repeated), every DNN layer's weights and biases; the
+    outputs sit inside the clip range."""
+    rng = np.random.default_rng(21)
+    k = 3
+    vocab = [3, 2, 4]
+    tables = [rng.normal(size=(v_, k)) * 0.5 for v_ in vocab]
+    F = len(vocab)
+    w = F * k + F * (F - 1) // 2
+    p = {"tables": tables,
+         "dnn_hidden": [(rng.normal(size=(w, 5)) * 0.3, rng.normal(size=5) * 0.1),
+                        (rng.normal(size=(5, 3)) * 0.3, rng.normal(size=3) * 0.1)],
+         "dnn_out": (rng.normal(size=(3, 1)) * 0.1, np.array([0.5]))}
+    ids = np.array([[0, 1, 3], [2, 1, 0], [0, 0, 3], [1, 1, 2]])
+    t = np.array([1.0, 0.0, 1.0, 0.0])
+    lr = 1.0
+    new, loss = O.pnn_train_step(ids, t, p, lr)
+    assert loss.shape == (4,)
+    eps = 1e-6
+
+    def check(arr, new_arr, idx):
+        keep = arr[idx]
+        arr[idx] = keep + eps
+        lp = O.pnn_loss(ids, t, p)
+        arr[idx] = keep - eps
+        lm = O.pnn_loss(ids, t, p)
+        arr[idx] = keep
+        assert abs((lp - lm) / (2 * eps) - (arr[idx] - new_arr[idx]) / lr) < 1e-6, idx
+
+    for c, idx in [(0, (0, 0)), (0, (2, 1)), (1, (1, 2)), (2, (3, 0)), (2, (0, 1))]:
+        check(p["tables"][c], new["tables"][c], idx)
+    for li in range(2):
+        for idx in [(0, 0), (2, 1)]:
+            check(p["dnn_hidden"][li][0], new["dnn_hidden"][li][0], idx)
+        check(p["dnn_hidden"][li][1], new["dnn_hidden"][li][1], (1,))
+    check(p["dnn_out"][0], new["dnn_out"][0], (2, 0))
+    check(p["dnn_out"][1], new["dnn_out"][1], (0,))
