@@ -109,6 +109,9 @@ __device__ __forceinline__ MlpItem mlp_item(int item, int T, int G, int S) {
 #ifndef MLP_RING
 #define MLP_RING 4
 #endif
+#ifndef MLP_ACC2
+#define MLP_ACC2 0
+#endif
 constexpr int MLP_R = MLP_RING;  // B-fragment ring slots (the deepest D)
 __device__ __forceinline__ void mlp_ring_fill(floatx4 (&ring)[MLP_R], const floatx4* bp, int g0, int g1) {
 #pragma unroll
@@ -121,14 +124,26 @@ __device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[MLP_R], const float* _
   // A fragments are read one group ahead so the LDS latency hides behind
   // the previous group's MFMAs
   floatx4 an = *reinterpret_cast<const floatx4*>(ap + 16 * g0);
+#if MLP_ACC2
+  // two accumulation chains (k-steps 0,2 / 1,3 of every group): half the
+  // dependent-MFMA latency per wave; summed once at the end
+  floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
+#endif
   for (int g = g0; g < g1; g += D) {
 #pragma unroll
     for (int u = 0; u < D; ++u) {
       const floatx4 av = an;
       an = *reinterpret_cast<const floatx4*>(ap + 16 * min(g + u + 1, g1 - 1));
       __builtin_amdgcn_sched_barrier(0);
+#if MLP_ACC2
+      acc = mfma16x16x4(av[0], ring[u][0], acc);
+      acc1 = mfma16x16x4(av[1], ring[u][1], acc1);
+      acc = mfma16x16x4(av[2], ring[u][2], acc);
+      acc1 = mfma16x16x4(av[3], ring[u][3], acc1);
+#else
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc = mfma16x16x4(av[j], ring[u][j], acc);
+#endif
       // refill the slot in place right after its MFMAs and pin it there: left
       // alone the scheduler sinks every refill to the end of the iteration
       // (or copies in-flight registers), which drains the ring each pass
@@ -136,6 +151,12 @@ __device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[MLP_R], const float* _
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+#if MLP_ACC2
+  acc[0] += acc1[0];
+  acc[1] += acc1[1];
+  acc[2] += acc1[2];
+  acc[3] += acc1[3];
+#endif
 }
 
 __device__ __forceinline__ void mlp_mac(floatx4 (&ring)[MLP_R], const float* ap, const floatx4* bp, int g0, int g1,
