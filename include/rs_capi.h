@@ -454,6 +454,61 @@ int rs_inner_product_bwd(const float* emb, int64_t emb_stride,
                          const float* dflat, int64_t dflat_stride, int n_fields,
                          int k, int64_t batch, float* demb, int64_t demb_stride,
                          rs_stream_t stream);
+/* DIN training (compile_fit on model/din.py:56-95, training=True; the host
+ * layer DIN.train_step composes these with rs_dense_fwd / rs_gemm /
+ * rs_col_sum / rs_sgd_update / rs_embedding_sgd):
+ * rs_din_att_concat: out[b*T+t] = [q_b, s_bt, q_b - s_bt, q_b * s_bt]
+ *  (the attention unit input, layer/interaction.py:381-391); item [B,K],
+ *  seq [B*T,K], out [B*T,4K] dense rows.
+ * rs_din_att_concat_bwd: from d = dL/dout: dq[b] += sum_t (d0 + d2 + s d3)
+ *  (row stride dq_stride), dseq[b*T+t] += d1 - d2 + q d3.
+ * rs_prelu_rows_fwd / _bwd: Keras PReLU on rows, y = max(z,0) +
+ *  alpha[(r mod period), c] min(z,0) (the attention's [T,h] alphas: period
+ *  T; a Dense layer's [N]: period 1); bwd writes dz = dy (z>0 ? 1 : alpha)
+ *  and dalpha[p,c] = sum_{r = p mod period} dy min(z,0) (fixed order).
+ * rs_masked_softmax_pool: s = score, or -2^32+1 where hist[b,0..T) == 0
+ *  (the first behaviour feature, model/din.py:80); a = softmax_T(s) [B,T];
+ *  out[b] = sum_t a_t seq[b*T+t] (:396-404).  T <= 512.
+ * rs_masked_softmax_pool_bwd: from datt: ds[b,t] = live ? a_t (da_t -
+ *  sum_s a_s da_s) : 0 with da_t = datt . seq_t; dseq[b*T+t] = a_t datt
+ *  (stored, not accumulated).
+ * rs_bn_train_fwd: BatchNormalization in training mode — per column the
+ *  batch mean and biased variance into mean / var, y = (x - mean)
+ *  rsqrt(var + eps) gamma + beta, and (when non-NULL) moving = momentum
+ *  moving + (1 - momentum) batch stat.
+ * rs_bn_train_bwd: dgamma = sum dy xhat, dbeta = sum dy, dx = gamma
+ *  rsqrt(var+eps) (dy - dbeta/B - xhat dgamma/B).                          */
+int rs_din_att_concat(const float* item, const float* seq, int64_t batch,
+                      int T, int K, float* out, rs_stream_t stream);
+int rs_din_att_concat_bwd(const float* d, const float* item, const float* seq,
+                          int64_t batch, int T, int K, float* dq,
+                          int64_t dq_stride, float* dseq, rs_stream_t stream);
+int rs_prelu_rows_fwd(const float* z, int64_t M, int N, const float* alpha,
+                      int period, float* y, rs_stream_t stream);
+int rs_prelu_rows_bwd(const float* z, const float* dy, int64_t M, int N,
+                      const float* alpha, int period, float* dz,
+                      float* dalpha, rs_stream_t stream);
+int rs_masked_softmax_pool(const float* score, const void* hist,
+                           int hist_kind, int64_t hist_stride,
+                           const float* seq, int64_t batch, int T, int K,
+                           float* a, float* out, int64_t out_stride,
+                           rs_stream_t stream);
+int rs_masked_softmax_pool_bwd(const float* a, const void* hist,
+                               int hist_kind, int64_t hist_stride,
+                               const float* seq, const float* datt,
+                               int64_t datt_stride, int64_t batch, int T,
+                               int K, float* ds, float* dseq,
+                               rs_stream_t stream);
+int rs_bn_train_fwd(const float* x, int64_t x_stride, int64_t batch, int D,
+                    const float* gamma, const float* beta, float eps,
+                    float momentum, float* moving_mean, float* moving_var,
+                    float* mean, float* var, float* y, int64_t y_stride,
+                    rs_stream_t stream);
+int rs_bn_train_bwd(const float* x, int64_t x_stride, int64_t batch, int D,
+                    const float* mean, const float* var, const float* gamma,
+                    float eps, const float* dy, int64_t dy_stride, float* dx,
+                    int64_t dx_stride, float* dgamma, float* dbeta,
+                    rs_stream_t stream);
 /* rs_head_grad with g = scale (sigmoid(z) - t) (scale > 0): the sharded
  * DeepFM step's local batch is a 1/world share of the global batch mean,
  * scale = 1 / (world * batch).                                             */

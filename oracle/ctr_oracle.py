@@ -666,6 +666,145 @@ def pnn_loss(ids, t, p, act="relu", dt=np.float64):
     return pnn_bce(pre, t, dt)[0]
 
 
+def _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt):
+    """DIN.call (model/din.py:56-95) with training=True (Keras fit): the
+    BatchNormalization normalises with the batch's own mean and (biased)
+    variance; att 'prelu' and dnn 'prelu' (the reference defaults).  Returns
+    every intermediate the hand backward needs."""
+    c = {}
+    dense_in = np.concatenate([cast_inputs(inputs[f], dt).reshape(-1, 1) for f in dense_feats], -1) \
+        if dense_feats else None
+    other_sparse = [f for f in sparse_feats if f not in behavior_feats]
+    c["other_ids"] = [np.asarray(inputs[f]).reshape(-1) for f in other_sparse]
+    parts = [embedding_lookup(np.asarray(p["sparse_tables"][f], dt), i) for f, i in zip(other_sparse, c["other_ids"])]
+    if dense_in is not None:
+        parts.append(dense_in)
+    other = np.concatenate(parts, -1) if parts else None
+    hist = np.stack([np.asarray(inputs[f]) for f in behavior_feats], -1)  # [B,T,nb]
+    cand = np.asarray(inputs["movie_id"]).reshape(hist.shape[0], -1)
+    c["hist"], c["cand"] = hist, cand
+    seq = np.concatenate([embedding_lookup(np.asarray(p["seq_tables"][f], dt), hist[:, :, i])
+                          for i, f in enumerate(behavior_feats)], -1)
+    item = np.concatenate([embedding_lookup(np.asarray(p["seq_tables"][f], dt), cand[:, i])
+                           for i, f in enumerate(behavior_feats)], -1)
+    mask = hist[:, :, 0] != 0
+    B, T, K = seq.shape
+    q = np.tile(item[:, None, :], (1, T, 1))
+    h = np.concatenate([q, seq, q - seq, q * seq], -1)
+    att_pre, att_in = [], [h]
+    for W, b, a in p["att"]["prelu"]:
+        z = np.tensordot(att_in[-1], np.asarray(W, dt), axes=[[2], [0]]) + np.asarray(b, dt)
+        att_pre.append(z)
+        att_in.append(prelu(z, np.asarray(a, dt)))
+    score = (np.tensordot(att_in[-1], np.asarray(p["att"]["out"][0], dt), axes=[[2], [0]])
+             + np.asarray(p["att"]["out"][1], dt))[..., 0]
+    score = np.where(mask, score, dt(np.float32(MASK_FILL)))
+    e = np.exp(score - score.max(-1, keepdims=True))
+    a = e / e.sum(-1, keepdims=True)
+    att = np.einsum("bt,btk->bk", a, seq)
+    x = np.concatenate([att, item] + ([other] if other is not None else []), -1)
+    g, bt, mu, var, eps = p["bn"]
+    bmu, bvar = x.mean(0), x.var(0)
+    xhat = (x - bmu) / np.sqrt(bvar + eps)
+    y = xhat * np.asarray(g, dt) + np.asarray(bt, dt)
+    pre, acts = [], [y]
+    for W, b, al in p["dnn"]:
+        z = acts[-1] @ np.asarray(W, dt) + np.asarray(b, dt)
+        pre.append(z)
+        acts.append(prelu(z, np.asarray(al, dt)))
+    logit = (acts[-1] @ np.asarray(p["out"][0], dt) + np.asarray(p["out"][1], dt))[:, 0]
+    c.update(seq=seq, item=item, mask=mask, q=q, att_pre=att_pre, att_in=att_in, a=a, x=x, bmu=bmu, bvar=bvar,
+             xhat=xhat, pre=pre, acts=acts, logit=logit, B=B, T=T, K=K, nd=0 if dense_in is None else
+             dense_in.shape[1], other_sparse=other_sparse)
+    return c
+
+
+def din_loss(inputs, t, p, dense_feats, sparse_feats, behavior_feats, dt=np.float64):
+    """compile_fit's objective on DIN (training-mode forward): mean BCE."""
+    z = _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt)["logit"]
+    t = np.asarray(t, dt).reshape(-1)
+    return np.mean(np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z))))
+
+
+def din_train_step(inputs, t, p, dense_feats, sparse_feats, behavior_feats, lr, momentum=0.99, dt=np.float64):
+    """One SGD step of compile_fit on DIN (utils/compile_fit.py:9-15; model/
+    din.py:56-95, att 'prelu', dnn 'prelu'), backpropagated by hand:
+    BCE on the sigmoid's logit (g = (sigmoid(z) - t)/B); Dense + PReLU layers
+    (dalpha = sum dy min(0, z), the attention's alpha [T, h] summed over the
+    batch); BatchNormalization in training mode (batch mean / biased variance,
+    dx = gamma/sigma (dy - mean dy - xhat mean(dy xhat))) and its moving
+    averages (momentum 0.99, biased batch variance); the masked softmax pool
+    (ds_t = a_t (dv.seq_t - sum_s a_s dv.seq_s)); the [q, k, q-k, q*k] concat
+    (dq sums over T); embedding rows by scatter-add.  No regularisers.
+    Returns (new p, per-sample losses before the step)."""
+    c = _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt)
+    B, T, K = c["B"], c["T"], c["K"]
+    t = np.asarray(t, dt).reshape(-1)
+    z = c["logit"]
+    loss = np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z)))
+    g = (sigmoid(z) - t) / B
+    new = {"sparse_tables": {f: np.array(v, dt) for f, v in p["sparse_tables"].items()},
+           "seq_tables": {f: np.array(v, dt) for f, v in p["seq_tables"].items()}}
+    Wo, bo = (np.asarray(v, dt) for v in p["out"])
+    new["out"] = (Wo - lr * (c["acts"][-1].T @ g[:, None]), bo - lr * g.sum(keepdims=True))
+    dh = g[:, None] @ Wo.T
+    new_dnn = [None] * len(p["dnn"])
+    for li in reversed(range(len(p["dnn"]))):
+        W, b, al = (np.asarray(v, dt) for v in p["dnn"][li])
+        zl = c["pre"][li]
+        dz = dh * np.where(zl > 0, 1.0, al)
+        dal = (dh * np.minimum(zl, 0)).sum(0)
+        new_dnn[li] = (W - lr * (c["acts"][li].T @ dz), b - lr * dz.sum(0), al - lr * dal)
+        dh = dz @ W.T
+    new["dnn"] = new_dnn
+    gam, bet, mu, var, eps = p["bn"]
+    gam, bet = np.asarray(gam, dt), np.asarray(bet, dt)
+    xhat = c["xhat"]
+    dgam, dbet = (dh * xhat).sum(0), dh.sum(0)
+    inv = 1.0 / np.sqrt(c["bvar"] + eps)
+    dx = gam * inv * (dh - dh.mean(0) - xhat * (dh * xhat).mean(0))
+    new["bn"] = (gam - lr * dgam, bet - lr * dbet, momentum * np.asarray(mu, dt) + (1 - momentum) * c["bmu"],
+                 momentum * np.asarray(var, dt) + (1 - momentum) * c["bvar"], eps)
+    datt, ditem, doth = dx[:, :K], dx[:, K:2 * K], dx[:, 2 * K:]
+    seq, a, mask = c["seq"], c["a"], c["mask"]
+    da = np.einsum("bk,btk->bt", datt, seq)
+    dseq = a[:, :, None] * datt[:, None, :]
+    ds = a * (da - (a * da).sum(-1, keepdims=True))
+    ds = np.where(mask, ds, 0.0)
+    Wso, bso = (np.asarray(v, dt) for v in p["att"]["out"])
+    hl = c["att_in"][-1]
+    new_att_out = (Wso - lr * np.tensordot(hl, ds, axes=[[0, 1], [0, 1]])[:, None], bso - lr * np.array([ds.sum()]))
+    dh3 = ds[:, :, None] * Wso[:, 0][None, None, :]
+    new_prelu = [None] * len(p["att"]["prelu"])
+    for li in reversed(range(len(p["att"]["prelu"]))):
+        W, b, al = (np.asarray(v, dt) for v in p["att"]["prelu"][li])
+        zl = c["att_pre"][li]
+        dz = dh3 * np.where(zl > 0, 1.0, al)
+        dal = (dh3 * np.minimum(zl, 0)).sum(0)
+        new_prelu[li] = (W - lr * np.tensordot(c["att_in"][li], dz, axes=[[0, 1], [0, 1]]), b - lr * dz.sum((0, 1)),
+                         al - lr * dal)
+        dh3 = np.tensordot(dz, W.T, axes=[[2], [0]])
+    new["att"] = {"prelu": new_prelu, "out": new_att_out}
+    d0, d1, d2, d3 = (dh3[..., i * K:(i + 1) * K] for i in range(4))
+    q = c["q"]
+    dq = (d0 + d2 + seq * d3).sum(1)
+    dseq = dseq + d1 - d2 + q * d3
+    ditem = ditem + dq
+    col = 0
+    for i, f in enumerate(behavior_feats):
+        k = np.asarray(p["seq_tables"][f]).shape[1]
+        tb = new["seq_tables"][f]
+        np.add.at(tb, c["hist"][:, :, i].reshape(-1), -lr * dseq[:, :, col:col + k].reshape(-1, k))
+        np.add.at(tb, c["cand"][:, i], -lr * ditem[:, col:col + k])
+        col += k
+    col = 0
+    for f, ids in zip(c["other_sparse"], c["other_ids"]):
+        k = np.asarray(p["sparse_tables"][f]).shape[1]
+        np.add.at(new["sparse_tables"][f], ids, -lr * doth[:, col:col + k])
+        col += k
+    return new, loss
+
+
 def deepfm_loss(dense, ids, t, p, l2_w, l2_v, nd=13, dt=np.float64):
     """compile_fit's objective on DeepFM: mean BCE(t, sigmoid(0.5(fm+dnn)))
     + l2_w |w1|^2 + l2_v |v|^2."""

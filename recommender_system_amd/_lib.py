@@ -81,6 +81,14 @@ SIGNATURES = {
     "rs_head_grad_scaled": (I, [P, P, P, L, F, F, F, P, P, P, P]),
     "rs_bce_prob_grad": (I, [P, L, P, L, P, P, P]),
     "rs_inner_product_bwd": (I, [P, L, P, L, P, L, I, I, L, P, L, P]),
+    "rs_din_att_concat": (I, [P, P, L, I, I, P, P]),
+    "rs_din_att_concat_bwd": (I, [P, P, P, L, I, I, P, L, P, P]),
+    "rs_prelu_rows_fwd": (I, [P, L, I, P, I, P, P]),
+    "rs_prelu_rows_bwd": (I, [P, P, L, I, P, I, P, P, P]),
+    "rs_masked_softmax_pool": (I, [P, P, I, L, P, L, I, I, P, P, L, P]),
+    "rs_masked_softmax_pool_bwd": (I, [P, P, I, L, P, P, L, L, I, I, P, P, P]),
+    "rs_bn_train_fwd": (I, [P, L, L, I, P, P, F, F, P, P, P, P, P, L, P]),
+    "rs_bn_train_bwd": (I, [P, L, L, I, P, P, P, F, P, L, P, L, P, P, P]),
     "rs_scatter_rows": (I, [P, L, I, I, P, L, P, P]),
     "rs_shard_dedup_workspace_size": (L, [L, I]),
     "rs_shard_dedup_route": (I, [P, I, L, P, P, I, L, L, I, L, P, P, P, P, P, P]),

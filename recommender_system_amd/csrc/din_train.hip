@@ -1,0 +1,395 @@
+// din_train.hip — DIN training kernels (compile_fit on DIN: utils/compile_fit.py:9-15,
+// model/din.py:56-95 with training=True).
+//
+// DIN.train_step composes these with rs_dense_fwd / rs_gemm / rs_col_sum /
+// rs_sgd_update / rs_embedding_sgd:
+//   rs_din_att_concat[_bwd]   the attention unit's input [q, k, q-k, q*k]
+//                             (layer/interaction.py:381-391) and its backward
+//   rs_prelu_rows_fwd / _bwd  Keras PReLU with alpha[(row mod period), col]
+//                             (the attention's [T, h] alphas: period T; the
+//                             DNN's [units]: period 1); dalpha by a fixed-
+//                             order sum over the rows of each alpha
+//   rs_masked_softmax_pool[_bwd]  score masking (-2^32+1 where the first
+//                             behaviour id is 0), softmax over T, the weighted
+//                             sum of the values (:396-404) and its backward
+//   rs_bn_train_stats / _apply / _bwd  BatchNormalization in training mode
+//                             (batch mean / biased variance, eps; moving
+//                             averages with momentum) and its backward
+// Every reduction runs in a fixed order: the step is bitwise reproducible.
+#include "rs_common.hpp"
+
+namespace rs {
+
+__global__ __launch_bounds__(256) void din_concat_kernel(const float* __restrict__ item, const float* __restrict__ seq,
+                                                         int64_t B, int T, int K, float* __restrict__ out) {
+  const int64_t n = B * T * (int64_t)K;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / K;  // row b*T + t
+    const int c = (int)(i - r * K);
+    const float q = item[(r / T) * K + c], s = seq[i];
+    float* o = out + r * 4 * K;
+    o[c] = q;
+    o[K + c] = s;
+    o[2 * K + c] = q - s;
+    o[3 * K + c] = q * s;
+  }
+}
+
+// dq[b,c] (+)= sum_t (d0 + d2 + s d3); dseq[r,c] += d1 - d2 + q d3
+__global__ __launch_bounds__(256) void din_concat_bwd_kernel(const float* __restrict__ d, const float* __restrict__ item,
+                                                             const float* __restrict__ seq, int64_t B, int T, int K,
+                                                             float* __restrict__ dq, int64_t lddq,
+                                                             float* __restrict__ dseq) {
+  const int64_t n = B * (int64_t)K;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t b = i / K;
+    const int c = (int)(i - b * K);
+    const float q = item[i];
+    float acc = 0.f;
+    for (int t = 0; t < T; ++t) {
+      const int64_t r = b * T + t;
+      const float* dr = d + r * 4 * K;
+      const float s = seq[r * K + c];
+      acc += dr[c] + dr[2 * K + c] + s * dr[3 * K + c];
+      dseq[r * K + c] += dr[K + c] - dr[2 * K + c] + q * dr[3 * K + c];
+    }
+    dq[b * lddq + c] += acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void prelu_rows_fwd_kernel(const float* __restrict__ z, int64_t M, int N,
+                                                             const float* __restrict__ alpha, int period,
+                                                             float* __restrict__ y) {
+  const int64_t n = M * (int64_t)N;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / N;
+    const int c = (int)(i - r * N);
+    const float v = z[i];
+    y[i] = fmaxf(v, 0.f) + alpha[(r % period) * N + c] * fminf(v, 0.f);
+  }
+}
+
+// dz = dy * (z > 0 ? 1 : alpha)
+__global__ __launch_bounds__(256) void prelu_rows_dz_kernel(const float* __restrict__ z, const float* __restrict__ dy,
+                                                            int64_t M, int N, const float* __restrict__ alpha,
+                                                            int period, float* __restrict__ dz) {
+  const int64_t n = M * (int64_t)N;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / N;
+    const int c = (int)(i - r * N);
+    const float v = z[i];
+    dz[i] = dy[i] * (v > 0.f ? 1.f : alpha[(r % period) * N + c]);
+  }
+}
+
+// dalpha[p, c] = sum over rows r = p, p + period, ... of dy * min(z, 0): one
+// block per alpha, 256 lanes striding the rows, a fixed tree at the end
+__global__ __launch_bounds__(256) void prelu_rows_dalpha_kernel(const float* __restrict__ z,
+                                                                const float* __restrict__ dy, int64_t M, int N,
+                                                                int period, float* __restrict__ dalpha) {
+  __shared__ float red[256];
+  const int64_t a = blockIdx.x;  // alpha index p*N + c
+  const int p = (int)(a / N), c = (int)(a - (int64_t)p * N);
+  float acc = 0.f;
+  for (int64_t r = p + (int64_t)threadIdx.x * period; r < M; r += (int64_t)256 * period) {
+    const int64_t i = r * N + c;
+    acc += dy[i] * fminf(z[i], 0.f);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dalpha[a] = red[0];
+}
+
+// one wave per sample: score masking, softmax over T (T <= 64 * 8), pool
+constexpr int SP_MAXT = 512;
+template <int KIND>
+__global__ __launch_bounds__(256) void masked_softmax_pool_kernel(const float* __restrict__ score, const void* hist,
+                                                                  int64_t hist_stride, const float* __restrict__ seq,
+                                                                  int64_t B, int T, int K, float* __restrict__ a,
+                                                                  float* __restrict__ out, int64_t ldo) {
+  typedef Ids<KIND> I;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  constexpr int NT = SP_MAXT / 64;
+  float s[NT];
+  float m = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int t = lane + 64 * j;
+    s[j] = -INFINITY;
+    if (t < T) {
+      const bool live = I::load(hist, b * hist_stride + t) != (typename I::raw_t)0;
+      s[j] = live ? score[b * T + t] : -4294967296.0f;  // -2**32+1 in fp32
+      m = fmaxf(m, s[j]);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    s[j] = (lane + 64 * j < T) ? expf(s[j] - m) : 0.f;
+    sum += s[j];
+  }
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  const float inv = 1.f / sum;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int t = lane + 64 * j;
+    if (t < T) a[b * T + t] = s[j] * inv;
+  }
+  // pool: lanes own columns; a_t is broadcast from lane t % 64 (t ascending)
+  for (int c0 = 0; c0 < K; c0 += 64) {
+    const int c = c0 + lane;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      if (64 * j >= T) break;
+      const float w = s[j] * inv;
+      const int tn = min(64, T - 64 * j);
+      for (int l = 0; l < tn; ++l) {
+        const float wl = __shfl(w, l);
+        if (c < K) acc += wl * seq[(b * T + 64 * j + l) * K + c];
+      }
+    }
+    if (c < K) out[b * ldo + c] = acc;
+  }
+}
+
+// backward: da_t = datt . seq_t; ds_t = live ? a_t (da_t - sum_s a_s da_s) : 0;
+// dseq_t = a_t datt (stored, not accumulated)
+template <int KIND>
+__global__ __launch_bounds__(256) void masked_softmax_pool_bwd_kernel(const float* __restrict__ a, const void* hist,
+                                                                      int64_t hist_stride,
+                                                                      const float* __restrict__ seq,
+                                                                      const float* __restrict__ datt, int64_t ldd,
+                                                                      int64_t B, int T, int K,
+                                                                      float* __restrict__ ds,
+                                                                      float* __restrict__ dseq) {
+  typedef Ids<KIND> I;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  constexpr int NT = SP_MAXT / 64;
+  float da[NT];
+  float dot = 0.f;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int t = lane + 64 * j;
+    da[j] = 0.f;
+    if (t < T) {
+      float acc = 0.f;
+      for (int c = 0; c < K; ++c) acc += datt[b * ldd + c] * seq[(b * T + t) * K + c];
+      da[j] = acc;
+      dot += a[b * T + t] * acc;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o);
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int t = lane + 64 * j;
+    if (t < T) {
+      const bool live = I::load(hist, b * hist_stride + t) != (typename I::raw_t)0;
+      const float at = a[b * T + t];
+      ds[b * T + t] = live ? at * (da[j] - dot) : 0.f;
+      for (int c = 0; c < K; ++c) dseq[(b * T + t) * K + c] = at * datt[b * ldd + c];
+    }
+  }
+}
+
+// BatchNormalization, training mode: one block per column
+__global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__ x, int64_t ldx, int64_t B,
+                                                       float momentum, float* __restrict__ mean,
+                                                       float* __restrict__ var, float* __restrict__ mov_mean,
+                                                       float* __restrict__ mov_var) {
+  __shared__ float red[256];
+  const int c = blockIdx.x;
+  float acc = 0.f;
+  for (int64_t b = threadIdx.x; b < B; b += 256) acc += x[b * ldx + c];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  const float mu = red[0] / (float)B;
+  __syncthreads();
+  acc = 0.f;
+  for (int64_t b = threadIdx.x; b < B; b += 256) {
+    const float d = x[b * ldx + c] - mu;
+    acc += d * d;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float v = red[0] / (float)B;  // biased (tf.nn.moments)
+    mean[c] = mu;
+    var[c] = v;
+    if (mov_mean) mov_mean[c] = momentum * mov_mean[c] + (1.f - momentum) * mu;
+    if (mov_var) mov_var[c] = momentum * mov_var[c] + (1.f - momentum) * v;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ x, int64_t ldx, int64_t B, int D,
+                                                       const float* __restrict__ mean, const float* __restrict__ var,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, float eps,
+                                                       float* __restrict__ y, int64_t ldy) {
+  const int64_t n = B * (int64_t)D;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t b = i / D;
+    const int c = (int)(i - b * D);
+    y[b * ldy + c] = (x[b * ldx + c] - mean[c]) * rsqrtf(var[c] + eps) * gamma[c] + beta[c];
+  }
+}
+
+// per column: dbeta = sum dy, dgamma = sum dy xhat; dx = gamma/sigma (dy -
+// dbeta/B - xhat dgamma/B)
+__global__ __launch_bounds__(256) void bn_bwd_kernel(const float* __restrict__ x, int64_t ldx, int64_t B,
+                                                     const float* __restrict__ mean, const float* __restrict__ var,
+                                                     const float* __restrict__ gamma, float eps,
+                                                     const float* __restrict__ dy, int64_t ldy,
+                                                     float* __restrict__ dx, int64_t lddx,
+                                                     float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float r1[256], r2[256];
+  const int c = blockIdx.x;
+  const float mu = mean[c], is = rsqrtf(var[c] + eps);
+  float s1 = 0.f, s2 = 0.f;
+  for (int64_t b = threadIdx.x; b < B; b += 256) {
+    const float g = dy[b * ldy + c];
+    s1 += g;
+    s2 += g * (x[b * ldx + c] - mu) * is;
+  }
+  r1[threadIdx.x] = s1;
+  r2[threadIdx.x] = s2;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      r1[threadIdx.x] += r1[threadIdx.x + s];
+      r2[threadIdx.x] += r2[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  const float db = r1[0], dg = r2[0];
+  if (threadIdx.x == 0) {
+    dgamma[c] = dg;
+    dbeta[c] = db;
+  }
+  const float k = gamma[c] * is, inB = 1.f / (float)B;
+  for (int64_t b = threadIdx.x; b < B; b += 256) {
+    const float xh = (x[b * ldx + c] - mu) * is;
+    dx[b * lddx + c] = k * (dy[b * ldy + c] - db * inB - xh * dg * inB);
+  }
+}
+
+static unsigned dt_grid(int64_t n) {
+  int64_t g = (n + 255) / 256;
+  return (unsigned)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" int rs_din_att_concat(const float* item, const float* seq, int64_t batch, int T, int K, float* out,
+                                 rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(item && seq && out && batch > 0 && T >= 1 && K >= 1, "rs_din_att_concat: bad arguments");
+  din_concat_kernel<<<dt_grid(batch * T * (int64_t)K), 256, 0, as_stream(stream)>>>(item, seq, batch, T, K, out);
+  return launch_status("rs_din_att_concat");
+}
+
+extern "C" int rs_din_att_concat_bwd(const float* d, const float* item, const float* seq, int64_t batch, int T, int K,
+                                     float* dq, int64_t dq_stride, float* dseq, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(d && item && seq && dq && dseq && batch > 0 && T >= 1 && K >= 1 && dq_stride >= K,
+             "rs_din_att_concat_bwd: bad arguments");
+  din_concat_bwd_kernel<<<dt_grid(batch * (int64_t)K), 256, 0, as_stream(stream)>>>(d, item, seq, batch, T, K, dq,
+                                                                                   dq_stride, dseq);
+  return launch_status("rs_din_att_concat_bwd");
+}
+
+extern "C" int rs_prelu_rows_fwd(const float* z, int64_t M, int N, const float* alpha, int period, float* y,
+                                 rs_stream_t stream) {
+  if (M == 0) return RS_OK;
+  RS_REQUIRE(z && alpha && y && M > 0 && N >= 1 && period >= 1, "rs_prelu_rows_fwd: bad arguments");
+  prelu_rows_fwd_kernel<<<dt_grid(M * (int64_t)N), 256, 0, as_stream(stream)>>>(z, M, N, alpha, period, y);
+  return launch_status("rs_prelu_rows_fwd");
+}
+
+extern "C" int rs_prelu_rows_bwd(const float* z, const float* dy, int64_t M, int N, const float* alpha, int period,
+                                 float* dz, float* dalpha, rs_stream_t stream) {
+  if (M == 0) return RS_OK;
+  RS_REQUIRE(z && dy && alpha && dz && dalpha && M > 0 && N >= 1 && period >= 1 && dz != dy,
+             "rs_prelu_rows_bwd: bad arguments");
+  hipStream_t st = as_stream(stream);
+  prelu_rows_dalpha_kernel<<<(unsigned)((int64_t)period * N), 256, 0, st>>>(z, dy, M, N, period, dalpha);
+  prelu_rows_dz_kernel<<<dt_grid(M * (int64_t)N), 256, 0, st>>>(z, dy, M, N, alpha, period, dz);
+  return launch_status("rs_prelu_rows_bwd");
+}
+
+extern "C" int rs_masked_softmax_pool(const float* score, const void* hist, int hist_kind, int64_t hist_stride,
+                                      const float* seq, int64_t batch, int T, int K, float* a, float* out,
+                                      int64_t out_stride, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(score && hist && seq && a && out && batch > 0 && T >= 1 && T <= SP_MAXT && K >= 1 && out_stride >= K &&
+                 hist_kind >= RS_ID_I32 && hist_kind <= RS_ID_F32,
+             "rs_masked_softmax_pool: bad arguments (T <= %d)", SP_MAXT);
+  const unsigned g = (unsigned)((batch + 3) / 4);
+  hipStream_t st = as_stream(stream);
+  with_id_kind(hist_kind, [&](auto kc) {
+    masked_softmax_pool_kernel<decltype(kc)::value>
+        <<<g, 256, 0, st>>>(score, hist, hist_stride, seq, batch, T, K, a, out, out_stride);
+  });
+  return launch_status("rs_masked_softmax_pool");
+}
+
+extern "C" int rs_masked_softmax_pool_bwd(const float* a, const void* hist, int hist_kind, int64_t hist_stride,
+                                          const float* seq, const float* datt, int64_t datt_stride, int64_t batch,
+                                          int T, int K, float* ds, float* dseq, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(a && hist && seq && datt && ds && dseq && batch > 0 && T >= 1 && T <= SP_MAXT && K >= 1 &&
+                 datt_stride >= K && hist_kind >= RS_ID_I32 && hist_kind <= RS_ID_F32,
+             "rs_masked_softmax_pool_bwd: bad arguments (T <= %d)", SP_MAXT);
+  const unsigned g = (unsigned)((batch + 3) / 4);
+  hipStream_t st = as_stream(stream);
+  with_id_kind(hist_kind, [&](auto kc) {
+    masked_softmax_pool_bwd_kernel<decltype(kc)::value>
+        <<<g, 256, 0, st>>>(a, hist, hist_stride, seq, datt, datt_stride, batch, T, K, ds, dseq);
+  });
+  return launch_status("rs_masked_softmax_pool_bwd");
+}
+
+extern "C" int rs_bn_train_fwd(const float* x, int64_t x_stride, int64_t batch, int D, const float* gamma,
+                               const float* beta, float eps, float momentum, float* moving_mean,
+                               float* moving_var, float* mean, float* var, float* y, int64_t y_stride,
+                               rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(x && gamma && beta && mean && var && y && batch > 0 && D >= 1 && x_stride >= D && y_stride >= D,
+             "rs_bn_train_fwd: bad arguments");
+  hipStream_t st = as_stream(stream);
+  bn_stats_kernel<<<(unsigned)D, 256, 0, st>>>(x, x_stride, batch, momentum, mean, var, moving_mean, moving_var);
+  bn_apply_kernel<<<dt_grid(batch * (int64_t)D), 256, 0, st>>>(x, x_stride, batch, D, mean, var, gamma, beta, eps, y,
+                                                               y_stride);
+  return launch_status("rs_bn_train_fwd");
+}
+
+extern "C" int rs_bn_train_bwd(const float* x, int64_t x_stride, int64_t batch, int D, const float* mean,
+                               const float* var, const float* gamma, float eps, const float* dy, int64_t dy_stride,
+                               float* dx, int64_t dx_stride, float* dgamma, float* dbeta, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(x && mean && var && gamma && dy && dx && dgamma && dbeta && batch > 0 && D >= 1 && x_stride >= D &&
+                 dy_stride >= D && dx_stride >= D && dx != dy,
+             "rs_bn_train_bwd: bad arguments");
+  bn_bwd_kernel<<<(unsigned)D, 256, 0, as_stream(stream)>>>(x, x_stride, batch, mean, var, gamma, eps, dy, dy_stride,
+                                                            dx, dx_stride, dgamma, dbeta);
+  return launch_status("rs_bn_train_bwd");
+}

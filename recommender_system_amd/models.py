@@ -743,6 +743,175 @@ class DIN(TowerMixin, KerasModule):
     def _layers(self):
         return list(self.dense_layer) + [self.out_layer]
 
+    def train_step(self, inputs, labels, lr=0.01, return_loss=False, check_ids=True, dropout=None):
+        """One step of compile_fit on DIN (utils/compile_fit.py:9-15: Keras
+        fit, SGD(lr), binary_crossentropy on the sigmoid output — Keras takes
+        the sigmoid's logit) with DIN.call in training mode (model/din.py:
+        56-95): BatchNormalization normalises with the batch's own mean and
+        biased variance and moves its averages (momentum 0.99).  att_attention
+        and dnn_activation 'prelu' (the reference defaults).
+          forward: behaviour / candidate rows (rs_embed_gather), the
+          attention input [q, k, q-k, q*k] (rs_din_att_concat), each
+          attention Dense (rs_dense_fwd) + PReLU over [T, h] alphas
+          (rs_prelu_rows_fwd, kept pre-activations), the score Dense, masked
+          softmax + pool (rs_masked_softmax_pool), rs_bn_train_fwd, the PReLU
+          DNN and the output logit;
+          backward: rs_head_grad, per Dense layer split-K rs_gemm / rs_col_sum
+          / rs_prelu_rows_bwd, rs_bn_train_bwd, rs_masked_softmax_pool_bwd,
+          rs_din_att_concat_bwd; then rs_sgd_update of every dense parameter
+          and row-sparse rs_embedding_sgd of the behaviour tables (history
+          rows, then candidates) and the other sparse tables.
+        Dropout (after the DNN, :93) runs as the identity (see
+        _dropout_notice).  Returns per-sample losses (before the step) if
+        ``return_loss``."""
+        att, bn = self.att_layer, self.bn_layer
+        if att.activation != "prelu" or any(L.activation != "prelu" for L in self.dense_layer):
+            raise NotImplementedError("DIN.train_step: att_attention 'prelu' and dnn_activation 'prelu' only")
+        _dropout_notice("DIN", self, dropout)
+        dev, st = self._dev, _lib.stream()
+        nb = len(self.seq_feats)
+        hists = [_ids_tensor(inputs[f["feat"]], dev) for f in self.seq_feats]
+        B, T = hists[0].shape
+        if any(h.shape != (B, T) for h in hists):
+            raise ValueError("DIN: every behaviour feature must be [B, T]")
+        cand = _ids_tensor(inputs["movie_id"], dev).reshape(B, -1)
+        if cand.shape[1] != nb:
+            raise ValueError(f"DIN: inputs['movie_id'] needs one candidate id per behaviour feature ({nb})")
+        if self.out_layer.kernel is None:
+            self.forward(inputs, check_ids)  # Keras build on the first call
+        if T != att.T:
+            raise ValueError(f"Attention built for T={att.T} (PReLU alpha is [T,h]); got T={T}")
+        labels = _to_device_f32(labels, dev).reshape(-1)
+        emp = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=dev)
+        K = sum(l.k for l in self.embed_seq_layers)
+        M = B * T
+        width = 2 * K + sum(l.k for l in self.embed_sparse_layers) + self.dense_num
+        shapes = [(W.shape[0], W.shape[1], M) for W in att.kernels] + [(att.out_kernel.shape[0], 1, M)]
+        shapes += [(L.kernel.shape[0], L.kernel.shape[1], B) for L in self._layers()]
+        gws = _gemm_ws(self, max(max(_lib.lib().rs_gemm_workspace_size(kin, n, m),
+                                     _lib.lib().rs_gemm_workspace_size(m, kin, n)) for kin, n, m in shapes))
+        gw = (ptr(gws), gws.numel())
+
+        # ---- forward, keeping what the backward needs
+        hist_ids = [h.reshape(M, 1) for h in hists]
+        cand_ids = [cand[:, i:i + 1] for i in range(nb)]
+        item = self._behaviour_embed(cand_ids, B, check_ids)
+        seq = self._behaviour_embed(hist_ids, M, check_ids)
+        x = emp(B, width)
+        h0 = emp(M, 4 * K)
+        call("rs_din_att_concat", ptr(item), ptr(seq), B, T, K, ptr(h0), st)
+        att_in, att_pre = [h0], []
+        for W, b, al in zip(att.kernels, att.biases, att.alphas):
+            n = W.shape[1]
+            z, y = emp(M, n), emp(M, n)
+            call("rs_dense_fwd", ptr(att_in[-1]), att_in[-1].stride(0), ptr(W), ptr(b), None, _lib.ACT[None],
+                 ptr(z), n, M, W.shape[0], n, st)
+            call("rs_prelu_rows_fwd", ptr(z), M, n, ptr(al), T, ptr(y), st)
+            att_pre.append(z)
+            att_in.append(y)
+        score = emp(M)
+        hl = att_in[-1]
+        call("rs_dense_fwd", ptr(hl), hl.stride(0), ptr(att.out_kernel), ptr(att.out_bias), None, _lib.ACT[None],
+             ptr(score), 1, M, hl.shape[1], 1, st)
+        a = emp(B, T)
+        h_first = hists[0]
+        call("rs_masked_softmax_pool", ptr(score), ptr(h_first), _lib.id_kind(h_first), h_first.stride(0), ptr(seq),
+             B, T, K, ptr(a), ptr(x), width, st)
+        x[:, K:2 * K].copy_(item)
+        col = 2 * K
+        other_ids = []
+        for f, layer in zip(self.other_sparse, self.embed_sparse_layers):
+            ids = _ids_tensor(inputs[f["feat"]], dev).reshape(B, 1)
+            other_ids.append(ids)
+            layer.gather(ids, out=x[:, col:col + layer.k], check_ids=check_ids)
+            col += layer.k
+        for f in self.dense_feature_columns:
+            x[:, col:col + 1] = _to_device_f32(inputs[f["feat"]], dev).reshape(B, 1)
+            col += 1
+        mean, var, y0 = emp(width), emp(width), emp(B, width)
+        call("rs_bn_train_fwd", ptr(x), width, B, width, ptr(bn.gamma), ptr(bn.beta), bn.epsilon, 0.99,
+             ptr(bn.moving_mean), ptr(bn.moving_variance), ptr(mean), ptr(var), ptr(y0), width, st)
+        acts, pre = [y0], []
+        for L in self.dense_layer:
+            z, y = emp(B, L.units), emp(B, L.units)
+            call("rs_dense_fwd", ptr(acts[-1]), acts[-1].stride(0), ptr(L.kernel), ptr(L.bias), None,
+                 _lib.ACT[None], ptr(z), L.units, B, L.kernel.shape[0], L.units, st)
+            call("rs_prelu_rows_fwd", ptr(z), B, L.units, ptr(L.alpha), 1, ptr(y), st)
+            pre.append(z)
+            acts.append(y)
+        out = self.out_layer
+        logit = emp(B)
+        call("rs_dense_fwd", ptr(acts[-1]), acts[-1].stride(0), ptr(out.kernel), ptr(out.bias), None,
+             _lib.ACT[None], ptr(logit), 1, B, out.kernel.shape[0], 1, st)
+        g, g0 = emp(B), emp(B)
+        loss = emp(B) if return_loss else None
+        call("rs_head_grad", ptr(logit), ptr(logit), ptr(labels), B, 1.0, 0.0, ptr(g), ptr(g0), ptr(loss), st)
+
+        # ---- backward (every gradient before any update)
+        updates = []
+
+        def dense_back(W, bias, a_in, dz, m):
+            kin, n = W.shape
+            dW, db, din = emp(kin, n), emp(n), emp(m, kin)
+            call("rs_gemm", 1, 0, kin, n, m, 1.0, ptr(a_in), a_in.stride(0), ptr(dz), dz.stride(0), 0.0, ptr(dW), n,
+                 None, 0, *gw, st)
+            call("rs_col_sum", ptr(dz), dz.stride(0), m, n, ptr(db), st)
+            call("rs_gemm", 0, 1, m, kin, n, 1.0, ptr(dz), dz.stride(0), ptr(W), n, 0.0, ptr(din), kin, None, 0,
+                 *gw, st)
+            updates.extend([(W, dW), (bias, db)])
+            return din
+
+        def prelu_back(z, dy, alpha, period, m):
+            n = z.shape[1]
+            dz, dal = emp(m, n), emp(alpha.numel())
+            call("rs_prelu_rows_bwd", ptr(z), ptr(dy), m, n, ptr(alpha), period, ptr(dz), ptr(dal), st)
+            updates.append((alpha, dal))
+            return dz
+
+        dh = dense_back(out.kernel, out.bias, acts[-1], g.view(B, 1), B)
+        for li in reversed(range(len(self.dense_layer))):
+            L = self.dense_layer[li]
+            dh = dense_back(L.kernel, L.bias, acts[li], prelu_back(pre[li], dh, L.alpha, 1, B), B)
+        dx, dgam, dbet = emp(B, width), emp(width), emp(width)
+        call("rs_bn_train_bwd", ptr(x), width, B, width, ptr(mean), ptr(var), ptr(bn.gamma), bn.epsilon, ptr(dh),
+             dh.stride(0), ptr(dx), width, ptr(dgam), ptr(dbet), st)
+        updates.extend([(bn.gamma, dgam), (bn.beta, dbet)])
+        ds, dseq = emp(M), emp(M, K)
+        call("rs_masked_softmax_pool_bwd", ptr(a), ptr(h_first), _lib.id_kind(h_first), h_first.stride(0), ptr(seq),
+             ptr(dx), width, B, T, K, ptr(ds), ptr(dseq), st)
+        dh3 = dense_back(att.out_kernel, att.out_bias, hl, ds.view(M, 1), M)
+        for li in reversed(range(len(att.kernels))):
+            dz = prelu_back(att_pre[li], dh3, att.alphas[li], T, M)
+            dh3 = dense_back(att.kernels[li], att.biases[li], att_in[li], dz, M)
+        call("rs_din_att_concat_bwd", ptr(dh3), ptr(item), ptr(seq), B, T, K, ptr(dx) + 4 * K, width, ptr(dseq), st)
+
+        # ---- SGD
+        for w, gr in updates:
+            call("rs_sgd_update", ptr(w), ptr(gr), gr.numel(), float(lr), 0.0, st)
+        ws_n = _lib.lib().rs_embedding_sgd_workspace_size(M)
+        ws = self.__dict__.get("_emb_ws")
+        if ws is None or ws.numel() < ws_n:
+            ws = self.__dict__["_emb_ws"] = torch.empty(ws_n, dtype=torch.uint8, device=dev)
+
+        def emb_sgd(layer, ids, grad_ptr, ldg, rows):
+            call("rs_embedding_sgd", ptr(layer.table), layer.total_rows, layer.k, ptr(ids), _lib.id_kind(ids),
+                 ids.stride(0), ptr(layer.field_offsets), ptr(layer.field_vocab), 1, rows, grad_ptr, ldg, float(lr),
+                 ptr(ws), None, st)
+
+        col = 0
+        for i, layer in enumerate(self.embed_seq_layers):
+            emb_sgd(layer, hist_ids[i], ptr(dseq) + 4 * col, K, M)
+            emb_sgd(layer, cand_ids[i], ptr(dx) + 4 * (K + col), width, B)
+            col += layer.k
+        col = 2 * K
+        for layer, ids in zip(self.embed_sparse_layers, other_ids):
+            emb_sgd(layer, ids, ptr(dx) + 4 * col, width, B)
+            col += layer.k
+        self._weights_changed()
+        for L in list(self.embed_seq_layers) + list(self.embed_sparse_layers):
+            L._weights_changed()
+        return loss
+
 
 # ------------------------------------ other CTR models (SURVEY §8(f) rank 3)
 class NFM(TowerMixin, KerasModule):

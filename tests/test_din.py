@@ -14,7 +14,7 @@ import pytest
 import torch
 
 from oracle import ctr_oracle as O
-from tests.helpers import assert_rel_close
+from tests.helpers import assert_rel_close, assert_scaled_close
 
 C = lambda t: t.detach().cpu().numpy()
 
@@ -173,3 +173,82 @@ def test_oracle_din_two_behaviours_is_concat():
     mask = (inputs[behaviour[0]] != 0).astype(np.float64)
     np.testing.assert_allclose(a, O.attention(item, seq, seq, mask, att), rtol=1e-12)
     np.testing.assert_allclose(a[0], seq[0].mean(0), rtol=1e-12)  # fully padded row: uniform average
+
+
+def _din_train_params(model):
+    p = din_params(model)
+    return {"sparse_tables": {f: v.copy() for f, v in p["sparse_tables"].items()},
+            "seq_tables": {f: v.copy() for f, v in p["seq_tables"].items()},
+            "att": {"prelu": [tuple(x.copy() for x in l) for l in p["att"]["prelu"]],
+                    "out": tuple(x.copy() for x in p["att"]["out"])},
+            "bn": tuple(x.copy() if isinstance(x, np.ndarray) else x for x in p["bn"]),
+            "dnn": [tuple(x.copy() for x in l) for l in p["dnn"]], "out": tuple(x.copy() for x in p["out"])}
+
+
+def _flat_params(p):
+    out = {f"sparse/{f}": v for f, v in p["sparse_tables"].items()}
+    out.update({f"seq/{f}": v for f, v in p["seq_tables"].items()})
+    for i, l in enumerate(p["att"]["prelu"]):
+        out.update({f"att{i}/W": l[0], f"att{i}/b": l[1], f"att{i}/alpha": l[2]})
+    out.update({"att_out/W": p["att"]["out"][0], "att_out/b": p["att"]["out"][1]})
+    out.update({f"bn/{n}": v for n, v in zip(("gamma", "beta", "mean", "var"), p["bn"][:4])})
+    for i, l in enumerate(p["dnn"]):
+        out.update({f"dnn{i}/W": l[0], f"dnn{i}/b": l[1], f"dnn{i}/alpha": l[2]})
+    out.update({"out/W": p["out"][0], "out/b": p["out"][1]})
+    return out
+
+
+def _assert_update_close(got, ref, before, rtol=2e-3, what=""):
+    """(got - before) vs (ref - before) at rtol of the update's scale, plus
+    the fp32 storage quantum of the parameter (4 ulp of |before|): an update
+    far below a parameter's ulp is only as exact as fp32 can hold it.  1e-8
+    absolute floor: the attention's output bias has an exactly-zero gradient
+    (softmax is shift invariant), 1e-19 in the fp64 oracle."""
+    got, ref, before = (np.asarray(v, np.float64) for v in (got, ref, before))
+    dg, dr = got - before, ref - before
+    rms = float(np.sqrt(np.mean(dr ** 2)))
+    bound = rtol * np.maximum(np.abs(dr), rms) + 4 * np.finfo(np.float32).eps * np.abs(before) + 1e-8
+    bad = ~(np.abs(dg - dr) <= bound)
+    assert not bad.any(), f"{what}: {int(bad.sum())}/{bad.size} outside tolerance"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("att_hidden,dnn_hidden,nb,k,B,T", [
+    ((80, 40), (256, 128, 64), 1, 8, 256, 20),   # the reference defaults
+    ((80, 40), (64, 32), 2, 8, 192, 30),         # item + category behaviour features (K = 16)
+    ((32,), (16,), 2, 4, 64, 7),                 # one attention layer, small ragged T
+])
+def test_din_train_steps_match_oracle(gpu, att_hidden, dnn_hidden, nb, k, B, T):
+    """DIN.train_step (compile_fit on DIN in training mode: batch-statistics
+    BatchNormalization with moving averages, PReLU attention over [T, h]
+    alphas, masked softmax pool, PReLU DNN, SGD + row-sparse embedding SGD)
+    == oracle.din_train_step (pinned by finite differences) over 3 steps with
+    small vocabularies (repeated rows, candidates inside the histories), a
+    fully padded history row and non-trivial parameters.  Parameters and the
+    per-step updates are compared at 2e-3 of their scale."""
+    from recommender_system_amd import DIN
+    rng = np.random.default_rng(B + T + nb)
+    cols, behaviour = din_columns(nb, k, item_vocab=40, cate_vocab=9, user_vocab=17)
+    model = DIN(cols, behaviour, att_hidden_units=att_hidden, dnn_hidden_units=dnn_hidden, seed=3)
+    inputs = din_inputs(rng, cols, behaviour, B, T)
+    model(inputs)
+    randomize(model, rng)
+    dense_f = [f["feat"] for f in cols[0]]
+    sparse_f = [f["feat"] for f in cols[1]]
+    beh = [f for f in sparse_f if f in behaviour]
+    p = _din_train_params(model)
+    lr = 0.2
+    for step in range(3):
+        inputs = din_inputs(rng, cols, behaviour, B, T)
+        t = rng.integers(0, 2, B).astype(np.float32)
+        before = _flat_params(_din_train_params(model))
+        loss = model.train_step(inputs, t, lr=lr, return_loss=True)
+        p, ce = O.din_train_step(inputs, t, p, dense_f, sparse_f, beh, lr)
+        got = _flat_params(_din_train_params(model))
+        ref = _flat_params(p)
+        assert_scaled_close(loss, ce, rtol=1e-4, what=f"step {step} loss")
+        for name in ref:
+            _assert_update_close(got[name], ref[name], before[name], what=f"step {step} update {name}")
+        p = _din_train_params(model)  # next step from the same fp32 point
+    y = model(inputs)
+    assert np.isfinite(y.cpu().numpy()).all()

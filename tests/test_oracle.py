@@ -352,3 +352,83 @@ def test_pnn_train_step_gradient_matches_finite_differences():
         check(p["dnn_hidden"][li][1], new["dnn_hidden"][li][1], (1,))
     check(p["dnn_out"][0], new["dnn_out"][0], (2, 0))
     check(p["dnn_out"][1], new["dnn_out"][1], (0,))
+
+
+def _din_small(rng, nb=2, kb=2, ko=3, T=4, B=6, att=(5, 3), dnn=(6, 4)):
+    beh = [f"b{i}" for i in range(nb)]
+    sparse = ["u"] + beh
+    dense = ["d0", "d1"]
+    vb, vo = 7, 5
+    K = nb * kb
+    p = {"sparse_tables": {"u": rng.normal(size=(vo, ko))},
+         "seq_tables": {f: rng.normal(size=(vb, kb)) for f in beh}}
+    n, pr = 4 * K, []
+    for h in att:
+        pr.append((rng.normal(size=(n, h)) * 0.5, rng.normal(size=h) * 0.1, rng.normal(size=(T, h)) * 0.3))
+        n = h
+    p["att"] = {"prelu": pr, "out": (rng.normal(size=(n, 1)), np.array([0.1]))}
+    D = 2 * K + ko + len(dense)
+    p["bn"] = (1.0 + 0.1 * rng.normal(size=D), 0.1 * rng.normal(size=D), np.zeros(D), np.ones(D), 1e-3)
+    n, dl = D, []
+    for u in dnn:
+        dl.append((rng.normal(size=(n, u)) * 0.4, rng.normal(size=u) * 0.1, rng.normal(size=u) * 0.2))
+        n = u
+    p["dnn"] = dl
+    p["out"] = (rng.normal(size=(n, 1)) * 0.5, np.array([0.05]))
+    hist = rng.integers(0, vb, size=(B, T, nb))
+    hist[1, 2:, 0] = 0  # padded tail
+    hist[3, :, 0] = 0   # fully masked row
+    inputs = {"d0": rng.random((B, 1)), "d1": rng.random((B, 1)), "u": rng.integers(0, vo, (B, 1)),
+              "movie_id": rng.integers(1, vb, (B, nb))}
+    for i, f in enumerate(beh):
+        inputs[f] = hist[:, :, i]
+    t = (rng.random(B) < 0.5).astype(np.float64)
+    return inputs, t, p, dense, sparse, beh
+
+
+def test_din_train_step_gradient_matches_finite_differences():
+    """oracle.din_train_step's hand backprop (training-mode BatchNormalization,
+    Dense + PReLU layers incl. the attention's [T, h] alphas, the masked
+    softmax pool with a padded and a fully masked row, the [q, k, q-k, q*k]
+    concat, two behaviour features concatenated along k, embedding
+    scatter-add) == central differences of compile_fit's DIN objective."""
+    rng = np.random.default_rng(7)
+    inputs, t, p, dense, sparse, beh = _din_small(rng)
+    lr = 1.0
+    new, loss = O.din_train_step(inputs, t, p, dense, sparse, beh, lr)
+    assert loss.shape == (6,)
+    eps = 1e-6
+
+    def check(get, idx, get_new):
+        arr = get(p)
+        keep = arr[idx]
+        arr[idx] = keep + eps
+        lp = O.din_loss(inputs, t, p, dense, sparse, beh)
+        arr[idx] = keep - eps
+        lm = O.din_loss(inputs, t, p, dense, sparse, beh)
+        arr[idx] = keep
+        fd = (lp - lm) / (2 * eps)
+        got = (arr[idx] - get_new(new)[idx]) / lr
+        assert abs(fd - got) < 1e-6 * max(1.0, abs(fd)), (idx, fd, got)
+
+    for f in beh:
+        for idx in [(0, 0), (2, 1), (4, 0), (5, 1)]:
+            check(lambda q, f=f: q["seq_tables"][f], idx, lambda q, f=f: q["seq_tables"][f])
+    for idx in [(1, 2), (3, 0)]:
+        check(lambda q: q["sparse_tables"]["u"], idx, lambda q: q["sparse_tables"]["u"])
+    for li in range(2):
+        for j, idx in [(0, (1, 1)), (0, (4, 0)), (1, (2,)), (2, (1, 2)), (2, (3, 0))]:
+            check(lambda q, li=li, j=j: q["att"]["prelu"][li][j], idx, lambda q, li=li, j=j: q["att"]["prelu"][li][j])
+    check(lambda q: q["att"]["out"][0], (1, 0), lambda q: q["att"]["out"][0])
+    check(lambda q: q["att"]["out"][1], (0,), lambda q: q["att"]["out"][1])
+    for j, idx in [(0, (2,)), (0, (9,)), (1, (4,))]:
+        check(lambda q, j=j: q["bn"][j], idx, lambda q, j=j: q["bn"][j])
+    for li in range(2):
+        for j, idx in [(0, (0, 1)), (1, (2,)), (2, (1,))]:
+            check(lambda q, li=li, j=j: q["dnn"][li][j], idx, lambda q, li=li, j=j: q["dnn"][li][j])
+    check(lambda q: q["out"][0], (2, 0), lambda q: q["out"][0])
+    check(lambda q: q["out"][1], (0,), lambda q: q["out"][1])
+    # moving statistics: momentum 0.99 toward the batch mean / biased variance
+    c = O._din_train_forward(inputs, p, dense, sparse, beh, np.float64)
+    np.testing.assert_allclose(new["bn"][2], 0.01 * c["bmu"], rtol=1e-12)
+    np.testing.assert_allclose(new["bn"][3], 0.99 + 0.01 * c["bvar"], rtol=1e-12)
