@@ -470,6 +470,18 @@ def bench_sharded_fm(args, world, rank, vocabs, dense_pool):
         sh.train_step(dense_pool[j], ids_pool[j], labels[j], lr=0.01, check=False)
 
     tdt, tstep_ms, ttiming = run(train)
+    local = None
+    if world == 1:
+        # the same pipelined step without the RCCL self-exchange (what a world-1
+        # job runs: sharded.py skips the all-to-alls unless forced)
+        sh._force_exchange = False
+        sh.pipe_route(ids_pool[0])
+        ldt, lstep_ms, ltiming = run(pipelined)
+        sh._force_exchange = True
+        local = {"samples_per_s": args.steps * B / ldt, "ms_per_step": ldt / args.steps * 1e3,
+                 "slot_ms": lstep_ms, "timing": ltiming,
+                 "note": "world 1 without the self-exchange: rs_shard_fm_pipe alone per batch (the records "
+                         "alternate between two buffers); the RCCL lines above are the comparison"}
     S, P = sh.slot_stride, sh.partial_width
     alg = B * 1824 + 18880
     return {
@@ -493,7 +505,8 @@ def bench_sharded_fm(args, world, rank, vocabs, dense_pool):
                        "timing": ttiming,
                        "note": "ShardedEmbeddingFM.train_step: partial-protocol forward (2 all-to-alls) + "
                                "combine_grad, all-gather of [s | g] records, owner row grads + row-sparse SGD "
-                               "of the shard, all-reduce of the FM parameter grads, SGD + l2"}}
+                               "of the shard, all-reduce of the FM parameter grads, SGD + l2"},
+        "world1_no_exchange": local}
 
 
 def bench_sharded_deepfm(args, world, rank):
@@ -585,6 +598,17 @@ def bench_sharded_deepfm(args, world, rank):
 
     nt = max(10, args.steps // 4)
     tdt, _ = _timed(train, nt, 2, world, events=False)
+    local = None
+    if world == 1:
+        # what a world-1 job runs: no self-exchange, the fused DeepFM straight
+        # from the (whole-table) shard
+        model.emb._force_exchange = False
+        ldt, lslot_ms = _timed_graph(step, args.steps, 2, world, chunk=16)
+        model.emb._force_exchange = True
+        local = {"samples_per_s": args.steps * B / ldt, "ms_per_step": ldt / args.steps * 1e3, "slot_ms": lslot_ms,
+                 "timing": "HIP graph replay",
+                 "note": "world 1 without the RCCL self-exchange (ShardedDeepFM.forward -> rs_deepfm_fwd on the "
+                         "shard); the exchange line above is the comparison"}
     flops = B * 2 * (429 * 256 + 256 * 128 + 128 * 64 + 64)
     ms = dt / args.steps * 1e3
     S = model.emb.slot_stride
@@ -614,7 +638,8 @@ def bench_sharded_deepfm(args, world, rank):
                           "timing": "eager launches",
                           "note": "ShardedDeepFM.train_step: row exchange, local DeepFM backward (rs_gemm), "
                                   "rs_scatter_rows + reverse all-to-all of dL/drow, owner rs_embedding_sgd, "
-                                  "all-reduce of the flat replicated gradient, SGD"}}
+                                  "all-reduce of the flat replicated gradient, SGD"},
+           "world1_no_exchange": local}
     return res, V
 
 
@@ -825,6 +850,15 @@ def bench_din(args, world, rank):
 
         cpu = _cpu_leg(args, rank, B, cpu_step, 8, "Attention 'prelu' (80, 40) on table[hist], table[cand], mask "
                                                   "= hist != 0", gpu0)
+    # compile_fit's training step on DIN (DIN.train_step; after the forward
+    # timings and the CPU leg: it moves the weights)
+    labels = (torch.rand(8, B, generator=g, device=dev) < 0.25).to(torch.float32)
+
+    def train(i):
+        model.train_step(pool[i % 8], labels[i % 8], lr=0.01, check_ids=False)
+
+    nt = max(10, args.steps // 10)
+    tdt, _ = _timed(train, nt, 2, world, events=False)
     return _line("DIN forward samples/sec @ batch 2048, behaviour seq len 100 (attention unit)",
                  args.steps * B / dt, "samples/s", args, world, att_ms,
                  {"workload": "din_attention_unit_from_ids", "global_batch": B, "seq_len": T, "embed_dim": k,
@@ -841,6 +875,11 @@ def bench_din(args, world, rank):
                   "din_forward": {"samples_per_s": n2 * B / dt2, "ms_per_step": dt2 / n2 * 1e3,
                                   "note": "graph-replayed full DIN.call (id checks off): gathers, attention "
                                           "from ids, BN, PReLU MLP + sigmoid head"},
+                  "train_step": {"samples_per_s": nt * B / tdt, "ms_per_step": tdt / nt * 1e3,
+                                 "timing": "eager launches",
+                                 "note": "DIN.train_step: gathers, attention Dense+PReLU layers over [B*T] rows, "
+                                         "masked softmax pool, training-mode BN, PReLU DNN, full backward, SGD + "
+                                         "row-sparse embedding SGD"},
                   "cpu_baseline": cpu})
 
 
@@ -888,6 +927,16 @@ def bench_pnn(args, world, rank):
             return model.product_inputs((dense_pool[0], ids_pool[0]), check_ids=False).cpu().numpy()
 
         cpu = _cpu_leg(args, rank, B, cpu_step, 8, "EmbedLayer (3-D) + InnerProductLayer -> [flat | inner]", gpu0)
+    # the reference's PNN training loop (PNN.train_step, mode 'inner'; moves the weights)
+    gl = torch.Generator(device=dev)
+    gl.manual_seed(SEED + 5)
+    labels = (torch.rand(16, B, generator=gl, device=dev) < 0.25).to(torch.float32)
+
+    def train(i):
+        model.train_step((dense_pool[i % 64], ids_pool[i % 64]), labels[i % 16], lr=0.01, check_ids=False)
+
+    nt = max(10, args.steps // 10)
+    tdt, _ = _timed(train, nt, 2, world, events=False)
     return _line("PNN inner-product input samples/sec @ batch 4096, 26 sparse x 1e6 vocab, dim 16",
                  args.steps * B / dt, "samples/s", args, world, dt / args.steps * 1e3,
                  {"workload": "pnn_embed_inner_fused", "global_batch": B, "vocab_per_field": V, "parallelism": "dp1"},
@@ -899,6 +948,11 @@ def bench_pnn(args, world, rank):
                                 "note": "[flat | inner | outer] in one launch (rs_embed_product_fwd)"},
                   "pnn_inner_forward": {"samples_per_s": n2 * B / dtf, "ms_per_step": dtf / n2 * 1e3,
                                         "note": "product inputs + DNN tower (rs_mlp_fwd, K = 741)"},
+                  "train_step": {"samples_per_s": nt * B / tdt, "ms_per_step": tdt / nt * 1e3,
+                                 "timing": "eager launches",
+                                 "note": "PNN.train_step (mode 'inner', model/pnn.py:74-81): [flat | inner], DNN "
+                                         "fwd/bwd, Keras-broadcast BCE on the logit, inner-product backward, SGD + "
+                                         "row-sparse embedding SGD"},
                   "cpu_baseline": cpu})
 
 
@@ -1279,7 +1333,8 @@ def main():
                         "ids": "int32 uniform per field", "parallelism": f"dp{world}+rowshard{world}"}),
             "roofline": res["roofline"], "cpu_baseline": res["cpu_baseline"],
         }
-        for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "exchange", "train_step", "fm_hotpath_sharded"):
+        for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "exchange", "train_step", "fm_hotpath_sharded",
+                    "world1_no_exchange"):
             if key in res:
                 line[key] = res[key]
         _emit(line)
