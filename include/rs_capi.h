@@ -432,6 +432,13 @@ int rs_gemm(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
             rs_stream_t stream);
 int rs_col_sum(const float* A, int64_t lda, int64_t M, int64_t N, float* out,
                rs_stream_t stream);
+/* rs_col_sum over many rows: slices of 256 rows summed into a workspace of
+ * rs_col_sum_workspace_size(M, N) bytes, then the slices in order
+ * (deterministic); without room (or one slice) it is rs_col_sum.           */
+int64_t rs_col_sum_workspace_size(int64_t M, int64_t N);
+int rs_col_sum_split(const float* A, int64_t lda, int64_t M, int64_t N,
+                     float* out, void* workspace, int64_t workspace_bytes,
+                     rs_stream_t stream);
 int rs_sgd_update(float* w, const float* grad, int64_t n, float lr, float l2,
                   rs_stream_t stream);
 int rs_head_grad(const float* fm, const float* dnn, const float* labels,
@@ -465,7 +472,9 @@ int rs_inner_product_bwd(const float* emb, int64_t emb_stride,
  * rs_prelu_rows_fwd / _bwd: Keras PReLU on rows, y = max(z,0) +
  *  alpha[(r mod period), c] min(z,0) (the attention's [T,h] alphas: period
  *  T; a Dense layer's [N]: period 1); bwd writes dz = dy (z>0 ? 1 : alpha)
- *  and dalpha[p,c] = sum_{r = p mod period} dy min(z,0) (fixed order).
+ *  and dalpha[p,c] = sum_{r = p mod period} dy min(z,0) (the split column
+ *  sums below; M a multiple of period); workspace:
+ *  rs_prelu_rows_bwd_workspace_size(M, N, period) bytes.
  * rs_masked_softmax_pool: s = score, or -2^32+1 where hist[b,0..T) == 0
  *  (the first behaviour feature, model/din.py:80); a = softmax_T(s) [B,T];
  *  out[b] = sum_t a_t seq[b*T+t] (:396-404).  T <= 512.
@@ -485,9 +494,11 @@ int rs_din_att_concat_bwd(const float* d, const float* item, const float* seq,
                           int64_t dq_stride, float* dseq, rs_stream_t stream);
 int rs_prelu_rows_fwd(const float* z, int64_t M, int N, const float* alpha,
                       int period, float* y, rs_stream_t stream);
+int64_t rs_prelu_rows_bwd_workspace_size(int64_t M, int N, int period);
 int rs_prelu_rows_bwd(const float* z, const float* dy, int64_t M, int N,
                       const float* alpha, int period, float* dz,
-                      float* dalpha, rs_stream_t stream);
+                      float* dalpha, void* workspace, int64_t workspace_bytes,
+                      rs_stream_t stream);
 int rs_masked_softmax_pool(const float* score, const void* hist,
                            int hist_kind, int64_t hist_stride,
                            const float* seq, int64_t batch, int T, int K,

@@ -84,7 +84,10 @@ SIGNATURES = {
     "rs_din_att_concat": (I, [P, P, L, I, I, P, P]),
     "rs_din_att_concat_bwd": (I, [P, P, P, L, I, I, P, L, P, P]),
     "rs_prelu_rows_fwd": (I, [P, L, I, P, I, P, P]),
-    "rs_prelu_rows_bwd": (I, [P, P, L, I, P, I, P, P, P]),
+    "rs_prelu_rows_bwd_workspace_size": (L, [L, I, I]),
+    "rs_prelu_rows_bwd": (I, [P, P, L, I, P, I, P, P, P, L, P]),
+    "rs_col_sum_workspace_size": (L, [L, L]),
+    "rs_col_sum_split": (I, [P, L, L, L, P, P, L, P]),
     "rs_masked_softmax_pool": (I, [P, P, I, L, P, L, I, I, P, P, L, P]),
     "rs_masked_softmax_pool_bwd": (I, [P, P, I, L, P, P, L, L, I, I, P, P, P]),
     "rs_bn_train_fwd": (I, [P, L, L, I, P, P, F, F, P, P, P, P, P, L, P]),

@@ -57,6 +57,36 @@ __global__ __launch_bounds__(256) void din_concat_bwd_kernel(const float* __rest
   }
 }
 
+// The same with one block per sample when K divides 256: the B*T*K updates
+// of dseq coalesced, dq[c] from the 256/K lanes of column c combined in lane
+// order through LDS (T*K loads in flight per block instead of T per thread)
+__global__ __launch_bounds__(256) void din_concat_bwd_block_kernel(const float* __restrict__ d,
+                                                                   const float* __restrict__ item,
+                                                                   const float* __restrict__ seq, int T, int K,
+                                                                   float* __restrict__ dq, int64_t lddq,
+                                                                   float* __restrict__ dseq) {
+  __shared__ float red[256];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x, c = tid % K, step = 256 / K;
+  const float q = item[b * K + c];
+  float acc = 0.f;
+  for (int t = tid / K; t < T; t += step) {
+    const int64_t r = b * T + t;
+    const float* dr = d + r * 4 * K;
+    const float d0 = dr[c], d1 = dr[K + c], d2 = dr[2 * K + c], d3 = dr[3 * K + c];
+    const float sv = seq[r * K + c];
+    acc += d0 + d2 + sv * d3;
+    dseq[r * K + c] += d1 - d2 + q * d3;
+  }
+  red[tid] = acc;
+  __syncthreads();
+  if (tid < K) {
+    float v = 0.f;
+    for (int j = tid; j < 256; j += K) v += red[j];
+    dq[b * lddq + c] += v;
+  }
+}
+
 __global__ __launch_bounds__(256) void prelu_rows_fwd_kernel(const float* __restrict__ z, int64_t M, int N,
                                                              const float* __restrict__ alpha, int period,
                                                              float* __restrict__ y) {
@@ -69,39 +99,20 @@ __global__ __launch_bounds__(256) void prelu_rows_fwd_kernel(const float* __rest
   }
 }
 
-// dz = dy * (z > 0 ? 1 : alpha)
-__global__ __launch_bounds__(256) void prelu_rows_dz_kernel(const float* __restrict__ z, const float* __restrict__ dy,
-                                                            int64_t M, int N, const float* __restrict__ alpha,
-                                                            int period, float* __restrict__ dz) {
+// PReLU backward elementwise part: dz = dy (z > 0 ? 1 : alpha[row mod period]),
+// prod = dy min(z, 0) (dalpha = column sums of prod viewed as [M/period, period*N])
+__global__ __launch_bounds__(256) void prelu_rows_bwd_kernel(const float* __restrict__ z, const float* __restrict__ dy,
+                                                             int64_t M, int N, const float* __restrict__ alpha,
+                                                             int period, float* __restrict__ dz,
+                                                             float* __restrict__ prod) {
   const int64_t n = M * (int64_t)N;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int64_t r = i / N;
     const int c = (int)(i - r * N);
-    const float v = z[i];
-    dz[i] = dy[i] * (v > 0.f ? 1.f : alpha[(r % period) * N + c]);
+    const float v = z[i], g = dy[i];
+    dz[i] = g * (v > 0.f ? 1.f : alpha[(r % period) * N + c]);
+    prod[i] = g * fminf(v, 0.f);
   }
-}
-
-// dalpha[p, c] = sum over rows r = p, p + period, ... of dy * min(z, 0): one
-// block per alpha, 256 lanes striding the rows, a fixed tree at the end
-__global__ __launch_bounds__(256) void prelu_rows_dalpha_kernel(const float* __restrict__ z,
-                                                                const float* __restrict__ dy, int64_t M, int N,
-                                                                int period, float* __restrict__ dalpha) {
-  __shared__ float red[256];
-  const int64_t a = blockIdx.x;  // alpha index p*N + c
-  const int p = (int)(a / N), c = (int)(a - (int64_t)p * N);
-  float acc = 0.f;
-  for (int64_t r = p + (int64_t)threadIdx.x * period; r < M; r += (int64_t)256 * period) {
-    const int64_t i = r * N + c;
-    acc += dy[i] * fminf(z[i], 0.f);
-  }
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) dalpha[a] = red[0];
 }
 
 // one wave per sample: score masking, softmax over T (T <= 64 * 8), pool
@@ -141,6 +152,26 @@ __global__ __launch_bounds__(256) void masked_softmax_pool_kernel(const float* _
   for (int j = 0; j < NT; ++j) {
     const int t = lane + 64 * j;
     if (t < T) a[b * T + t] = s[j] * inv;
+  }
+  if (K < 64 && 64 % K == 0) {
+    // pool with G = 64/K row groups: lane (g, c) sums rows t = g (mod G) of
+    // column c (a_t fetched from lane t % 64), then a butterfly over the
+    // groups (fixed order): the wave reads 64 contiguous floats per step
+    const int G = 64 / K, g = lane / K, c = lane - g * K;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      if (64 * j >= T) break;
+      const float w = s[j] * inv;
+      for (int l0 = 0; l0 < 64 && 64 * j + l0 < T; l0 += G) {
+        const int t = 64 * j + l0 + g;
+        const float wl = __shfl(w, (l0 + g) & 63);
+        if (t < T) acc += wl * seq[(b * T + t) * K + c];
+      }
+    }
+    for (int o = K; o < 64; o <<= 1) acc += __shfl_xor(acc, o);
+    if (g == 0) out[b * ldo + c] = acc;
+    return;
   }
   // pool: lanes own columns; a_t is broadcast from lane t % 64 (t ascending)
   for (int c0 = 0; c0 < K; c0 += 64) {
@@ -312,8 +343,12 @@ extern "C" int rs_din_att_concat_bwd(const float* d, const float* item, const fl
   if (batch == 0) return RS_OK;
   RS_REQUIRE(d && item && seq && dq && dseq && batch > 0 && T >= 1 && K >= 1 && dq_stride >= K,
              "rs_din_att_concat_bwd: bad arguments");
-  din_concat_bwd_kernel<<<dt_grid(batch * (int64_t)K), 256, 0, as_stream(stream)>>>(d, item, seq, batch, T, K, dq,
-                                                                                   dq_stride, dseq);
+  if (K <= 256 && 256 % K == 0)
+    din_concat_bwd_block_kernel<<<(unsigned)batch, 256, 0, as_stream(stream)>>>(d, item, seq, T, K, dq, dq_stride,
+                                                                                 dseq);
+  else
+    din_concat_bwd_kernel<<<dt_grid(batch * (int64_t)K), 256, 0, as_stream(stream)>>>(d, item, seq, batch, T, K, dq,
+                                                                                     dq_stride, dseq);
   return launch_status("rs_din_att_concat_bwd");
 }
 
@@ -325,15 +360,28 @@ extern "C" int rs_prelu_rows_fwd(const float* z, int64_t M, int N, const float* 
   return launch_status("rs_prelu_rows_fwd");
 }
 
+extern "C" int64_t rs_prelu_rows_bwd_workspace_size(int64_t M, int N, int period) {
+  if (M < 0 || N < 1 || period < 1) return -1;
+  return (M * N * 4 + 255) / 256 * 256 + rs_col_sum_workspace_size(M / period, (int64_t)period * N);
+}
+
 extern "C" int rs_prelu_rows_bwd(const float* z, const float* dy, int64_t M, int N, const float* alpha, int period,
-                                 float* dz, float* dalpha, rs_stream_t stream) {
+                                 float* dz, float* dalpha, void* workspace, int64_t workspace_bytes,
+                                 rs_stream_t stream) {
   if (M == 0) return RS_OK;
-  RS_REQUIRE(z && dy && alpha && dz && dalpha && M > 0 && N >= 1 && period >= 1 && dz != dy,
-             "rs_prelu_rows_bwd: bad arguments");
+  RS_REQUIRE(z && dy && alpha && dz && dalpha && workspace && M > 0 && N >= 1 && period >= 1 && M % period == 0 &&
+                 dz != dy,
+             "rs_prelu_rows_bwd: bad arguments (rows a multiple of period)");
+  RS_REQUIRE(workspace_bytes >= rs_prelu_rows_bwd_workspace_size(M, N, period),
+             "rs_prelu_rows_bwd: workspace too small");
   hipStream_t st = as_stream(stream);
-  prelu_rows_dalpha_kernel<<<(unsigned)((int64_t)period * N), 256, 0, st>>>(z, dy, M, N, period, dalpha);
-  prelu_rows_dz_kernel<<<dt_grid(M * (int64_t)N), 256, 0, st>>>(z, dy, M, N, alpha, period, dz);
-  return launch_status("rs_prelu_rows_bwd");
+  uint8_t* ws = static_cast<uint8_t*>(workspace);
+  float* prod = reinterpret_cast<float*>(ws);
+  const int64_t pb = (M * N * 4 + 255) / 256 * 256;
+  prelu_rows_bwd_kernel<<<dt_grid(M * (int64_t)N), 256, 0, st>>>(z, dy, M, N, alpha, period, dz, prod);
+  // dalpha[p, c] = column (p*N + c) sum of prod viewed as [M/period, period*N]
+  const int64_t W = (int64_t)period * N;
+  return rs_col_sum_split(prod, W, M / period, W, dalpha, ws + pb, workspace_bytes - pb, stream);
 }
 
 extern "C" int rs_masked_softmax_pool(const float* score, const void* hist, int hist_kind, int64_t hist_stride,

@@ -25,11 +25,17 @@ namespace rs {
 // The f32 MFMA is a k-ordered fmaf chain, so each output's K sum runs in one
 // fixed order (deterministic, the same order as a scalar k loop).
 constexpr int GT = 64, GK = 16;
+// Split-K launches (the weight gradients: a tall K = batch or batch*T, few
+// output tiles) stage 64 k-rows per round trip instead of 16: each slice is a
+// chain of dependent load -> MFMA steps, so 4x the bytes per step is 4x fewer
+// steps.
+constexpr int GK_SPLIT = 64;
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 // Split-K (part != nullptr): block z of gridDim.z covers K range
 // [z*kslice, (z+1)*kslice) and stores its raw partial tile to part[z][M][N];
 // gemm_reduce sums the slices in z order (deterministic).
+template <int GK>
 __global__ __launch_bounds__(256) void gemm_kernel(int ta, int tb, int M, int N, int K, float alpha,
                                                    const float* __restrict__ A, int64_t lda,
                                                    const float* __restrict__ B, int64_t ldb, float beta,
@@ -46,23 +52,44 @@ __global__ __launch_bounds__(256) void gemm_kernel(int ta, int tb, int M, int N,
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   const int kb = part ? blockIdx.z * kslice : 0;
   const int ke = part ? min(K, kb + kslice) : K;
-  for (int k0 = kb; k0 < ke; k0 += GK) {
-    // stage op(A)[m0:m0+64, k0:k0+16] as As[k][m] and op(B)[k0:k0+16, n0:n0+64] as Bs[k][n];
-    // consecutive threads walk each operand's contiguous memory dimension
-    // (k for a row-major A / transposed B, m or n otherwise): coalesced loads
-    for (int e = threadIdx.x; e < GK * GT; e += 256) {
+  // stage op(A)[m0:m0+64, k0:k0+GK] as As[k][m] and op(B)[k0:k0+GK, n0:n0+64]
+  // as Bs[k][n]; consecutive threads walk each operand's contiguous memory
+  // dimension (k for a row-major A / transposed B, m or n otherwise).  Every
+  // load is unconditional (an out-of-range element reads a clamped address in
+  // the tile's own lines and is zeroed by a select: a load under a branch
+  // merged with a default makes the compiler wait for it before the next one,
+  // and a common dummy address would be a chip-wide L2 hot spot), and the next
+  // stage's loads are in flight while this stage's MFMAs run.
+  constexpr int NE = GK * GT / 256;
+  float av[NE], bv[NE];
+  auto load_stage = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int e = threadIdx.x + 256 * i;
       const int ka = ta ? e / GT : e % GK, ma = ta ? e % GT : e / GK;
       const int m = m0 + ma, k = k0 + ka;
-      float av = 0.f;
-      if (m < M && k < ke) av = ta ? A[(int64_t)k * lda + m] : A[(int64_t)m * lda + k];
-      As[ka][ma] = av;
+      const bool oka = m < M && k < ke;
+      const int mc = min(m, M - 1), kc = min(k, ke - 1);  // clamped into the tile's own lines
+      const float x = A[ta ? (int64_t)kc * lda + mc : (int64_t)mc * lda + kc];
+      av[i] = oka ? x : 0.f;
       const int kb2 = tb ? e % GK : e / GT, nb = tb ? e / GK : e % GT;
       const int n = n0 + nb, k2 = k0 + kb2;
-      float bv = 0.f;
-      if (n < N && k2 < ke) bv = tb ? B[(int64_t)n * ldb + k2] : B[(int64_t)k2 * ldb + n];
-      Bs[kb2][nb] = bv;
+      const bool okb = n < N && k2 < ke;
+      const int nc = min(n, N - 1), kc2 = min(k2, ke - 1);
+      const float y = B[tb ? (int64_t)nc * ldb + kc2 : (int64_t)kc2 * ldb + nc];
+      bv[i] = okb ? y : 0.f;
+    }
+  };
+  if (kb < ke) load_stage(kb);
+  for (int k0 = kb; k0 < ke; k0 += GK) {
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      As[ta ? e / GT : e % GK][ta ? e % GT : e / GK] = av[i];
+      Bs[tb ? e % GK : e / GT][tb ? e / GK : e % GT] = bv[i];
     }
     __syncthreads();
+    if (k0 + GK < ke) load_stage(k0 + GK);
 #pragma unroll
     for (int ks = 0; ks < GK / 2; ++ks)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[2 * ks + lk][wm * 32 + li], Bs[2 * ks + lk][wn * 32 + li], acc,
@@ -92,8 +119,35 @@ __global__ __launch_bounds__(256) void gemm_reduce(int M, int N, int S, float al
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (int64_t)M * N) return;
   const int m = (int)(idx / N), n = (int)(idx - (int64_t)m * N);
-  float acc = 0.f;
-  for (int z = 0; z < S; ++z) acc += part[(int64_t)z * M * N + idx];
+  const int64_t MN = (int64_t)M * N;
+  const float acc = seg_sum8(0, S, [&](int64_t z) { return part[z * MN + idx]; });
+  float v = alpha * acc;
+  if (beta != 0.f) v += beta * C[(int64_t)m * ldc + n];
+  if (mask && !(mask[(int64_t)m * ldm + n] > 0.f)) v = 0.f;
+  C[(int64_t)m * ldc + n] = v;
+}
+
+// The same reduction with one wave per output when the slices are many
+// (S >= 64): lane l sums slices l, l+64, ... (8 partial sums), then a fixed
+// butterfly over the lanes; the epilogue as gemm_reduce
+__device__ __forceinline__ float wave_sum_fixed(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void gemm_reduce_wave(int M, int N, int S, float alpha,
+                                                        const float* __restrict__ part, float beta,
+                                                        float* __restrict__ C, int64_t ldc,
+                                                        const float* __restrict__ mask, int64_t ldm) {
+  const int64_t idx = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (idx >= (int64_t)M * N) return;
+  const int64_t MN = (int64_t)M * N;
+  const int ns = S > lane ? (S - lane + 63) / 64 : 0;  // slices lane, lane+64, ...
+  const float acc = wave_sum_fixed(seg_sum8(0, ns, [&](int64_t i) { return part[(lane + 64 * i) * MN + idx]; }));
+  if (lane) return;
+  const int m = (int)(idx / N), n = (int)(idx - (int64_t)m * N);
   float v = alpha * acc;
   if (beta != 0.f) v += beta * C[(int64_t)m * ldc + n];
   if (mask && !(mask[(int64_t)m * ldm + n] > 0.f)) v = 0.f;
@@ -114,6 +168,43 @@ __global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ 
     __syncthreads();
   }
   if (threadIdx.x == 0) out[n] = red[0];
+}
+
+// Split column sums (rs_col_sum_split): slice s of CS_R rows -> part[s][n]
+// (64 columns x 4 row lanes per block, the lanes combined in order), then
+// out[n] = the slices in order (seg_sum8).  Deterministic for a given shape.
+constexpr int CS_R = 256;
+__global__ __launch_bounds__(256) void col_sum_part_kernel(const float* __restrict__ A, int64_t lda, int64_t M, int N,
+                                                           float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + c;
+  const int64_t m0 = (int64_t)blockIdx.y * CS_R;
+  const int64_t m1 = m0 + CS_R < M ? m0 + CS_R : M;
+  float acc = 0.f;
+  if (n < N)
+    for (int64_t m = m0 + rl; m < m1; m += 4) acc += A[m * lda + n];
+  red[rl][c] = acc;
+  __syncthreads();
+  if (rl == 0 && n < N) part[(int64_t)blockIdx.y * N + n] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+}
+
+__global__ __launch_bounds__(256) void col_sum_fin_kernel(const float* __restrict__ part, int S, int N,
+                                                          float* __restrict__ out) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  out[n] = seg_sum8(0, S, [&](int64_t s) { return part[s * N + n]; });
+}
+
+// one wave per column when the slices are many (S >= 64; as gemm_reduce_wave)
+__global__ __launch_bounds__(256) void col_sum_fin_wave(const float* __restrict__ part, int S, int N,
+                                                        float* __restrict__ out) {
+  const int64_t n = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (n >= N) return;
+  const int ns = S > lane ? (S - lane + 63) / 64 : 0;
+  const float v = wave_sum_fixed(seg_sum8(0, ns, [&](int64_t i) { return part[(lane + 64 * i) * (int64_t)N + n]; }));
+  if (lane == 0) out[n] = v;
 }
 
 // w -= lr * (g + 2 l2 w)
@@ -308,15 +399,65 @@ __global__ __launch_bounds__(256) void emb_keys_kernel(const void* ids, int64_t 
   val[j] = (uint32_t)j;
 }
 
-// Sorted lookups: the first position of each row's segment sums the
-// segment's gradient rows (grad row of lookup j = b*F + c at
-// grad[b*ldg + c*k]) in lookup order and applies table[r] -= lr * G.
-// One thread per (position, column): the k columns of a segment are summed
-// by k adjacent lanes (a hot row's duplicates cost one pass, not k), each in
-// the same fixed order (seg_sum8), so the result stays bitwise reproducible.
-__global__ __launch_bounds__(256) void emb_apply_kernel(const uint32_t* __restrict__ key,
+// Sorted lookups -> table[r] -= lr * (sum of the segment's gradient rows);
+// grad row of lookup j = b*F + c at grad[b*ldg + c*k].  One thread per
+// (position, column): the k columns of a segment are summed by k adjacent
+// lanes.  A segment is cut into PIECES at the fixed chunk boundaries
+// (multiples of C sorted positions); each piece is summed in position order
+// by one lane (seg_sum8) and a segment's pieces are added in chunk order, so
+// the result is bitwise reproducible and a hot row with 10^5 duplicates costs
+// C/8 + (#chunks)/8 dependent steps instead of 10^5/8.
+//   emb_piece_kernel: a segment inside one chunk is applied at once; a piece
+//     of a segment that crosses a chunk boundary goes to part_last[chunk]
+//     (the segment's head piece) or part_first[chunk] (a piece starting at the
+//     chunk's first position);
+//   emb_cross_kernel: the head lane of each crossing segment adds its head
+//     piece and the following chunks' first pieces and applies.
+__device__ __forceinline__ int64_t seg_end_in(const uint32_t* __restrict__ key, int64_t p, int64_t hi, uint32_t r) {
+  int64_t lo = p + 1;  // first q in (p, hi) with key[q] != r, else hi
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (key[mid] == r) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void emb_piece_kernel(const uint32_t* __restrict__ key,
                                                         const uint32_t* __restrict__ val, int64_t n, int F, int k,
                                                         const float* __restrict__ grad, int64_t ldg, float lr,
+                                                        int64_t C, float* __restrict__ part_first,
+                                                        float* __restrict__ part_last, float* __restrict__ table) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t p = t / k;
+  const int f = (int)(t - p * k);
+  if (p >= n) return;
+  const uint32_t r = key[p];
+  if (r == 0xffffffffu) return;
+  const bool seg_head = p == 0 || key[p - 1] != r;
+  const int64_t c = p / C;
+  if (!seg_head && p != c * C) return;
+  const int64_t cend = (c + 1) * C < n ? (c + 1) * C : n;
+  const int64_t e = seg_end_in(key, p, cend, r);
+  const float s = seg_sum8(p, e, [&](int64_t q) {
+    const int64_t j = val[q];
+    const int64_t b = j / F;
+    const int cc = (int)(j - b * F);
+    return grad[b * ldg + (int64_t)cc * k + f];
+  });
+  const bool crosses_out = e == cend && cend < n && key[cend] == r;
+  if (seg_head && !crosses_out) {
+    table[(int64_t)r * k + f] -= lr * s;
+  } else if (seg_head) {
+    part_last[c * k + f] = s;
+  } else {
+    part_first[c * k + f] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void emb_cross_kernel(const uint32_t* __restrict__ key, int64_t n, int k,
+                                                        float lr, int64_t C, const float* __restrict__ part_first,
+                                                        const float* __restrict__ part_last,
                                                         float* __restrict__ table) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t p = t / k;
@@ -324,13 +465,13 @@ __global__ __launch_bounds__(256) void emb_apply_kernel(const uint32_t* __restri
   if (p >= n) return;
   const uint32_t r = key[p];
   if (r == 0xffffffffu || (p > 0 && key[p - 1] == r)) return;
-  const float acc = seg_sum8(p, seg_end(key, p, n, r), [&](int64_t q) {
-    const int64_t j = val[q];
-    const int64_t b = j / F;
-    const int c = (int)(j - b * F);
-    return grad[b * ldg + (int64_t)c * k + f];
-  });
-  table[(int64_t)r * k + f] -= lr * acc;
+  const int64_t c0 = p / C;
+  const int64_t cend = (c0 + 1) * C;
+  if (cend >= n || key[cend] != r) return;  // ends inside its chunk (keys are sorted)
+  const int64_t e = seg_end(key, cend, n, r);
+  const int64_t c1 = (e - 1) / C;
+  const float rest = seg_sum8(c0 + 1, c1 + 1, [&](int64_t c) { return part_first[c * k + f]; });
+  table[(int64_t)r * k + f] -= lr * (part_last[c0 * k + f] + rest);
 }
 
 // ------------------------------------------------------ CrossNet training
@@ -448,12 +589,13 @@ __global__ __launch_bounds__(256) void cross_train_bwd(const float* __restrict__
 using namespace rs;
 
 // K slices for a launch of few output tiles (the weight gradients x^T delta:
-// M x N small, K = batch): aim for ~512 workgroups, slices of >= 64.
+// M x N small, K = batch): aim for ~1024 workgroups (4 per CU: each slice is
+// a latency-bound chain of stages), slices of >= 64.
 static int gemm_splits(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ((M + GT - 1) / GT) * ((N + GT - 1) / GT);
-  int64_t s = 512 / (tiles > 0 ? tiles : 1);
+  int64_t s = 1024 / (tiles > 0 ? tiles : 1);
   s = std::min<int64_t>(s, K / 64);
-  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 256));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 1024));
 }
 
 extern "C" int64_t rs_gemm_workspace_size(int64_t M, int64_t N, int64_t K) {
@@ -475,11 +617,19 @@ extern "C" int rs_gemm(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K
   int S = gemm_splits(M, N, K);
   if (S > 1 && (!workspace || workspace_bytes < (int64_t)S * M * N * 4)) S = 1;  // no room: one pass over K
   dim3 grid((unsigned)((N + GT - 1) / GT), (unsigned)((M + GT - 1) / GT), (unsigned)S);
-  const int kslice = (int)((K + S - 1) / S + GK - 1) / GK * GK;
+  const int gk = S > 1 ? GK_SPLIT : GK;
+  const int kslice = (int)((K + S - 1) / S + gk - 1) / gk * gk;
   float* part = S > 1 ? static_cast<float*>(workspace) : nullptr;
-  gemm_kernel<<<grid, 256, 0, st>>>(trans_a, trans_b, (int)M, (int)N, (int)K, alpha, A, lda, B, ldb, beta, C, ldc,
-                                    mask, ldm, kslice, part);
   if (part)
+    gemm_kernel<GK_SPLIT><<<grid, 256, 0, st>>>(trans_a, trans_b, (int)M, (int)N, (int)K, alpha, A, lda, B, ldb, beta,
+                                                C, ldc, mask, ldm, kslice, part);
+  else
+    gemm_kernel<GK><<<grid, 256, 0, st>>>(trans_a, trans_b, (int)M, (int)N, (int)K, alpha, A, lda, B, ldb, beta, C,
+                                          ldc, mask, ldm, kslice, part);
+  if (part && S >= 64 && M * N <= (1 << 20))
+    gemm_reduce_wave<<<(unsigned)((M * N + 3) / 4), 256, 0, st>>>((int)M, (int)N, S, alpha, part, beta, C, ldc, mask,
+                                                                 ldm);
+  else if (part)
     gemm_reduce<<<(unsigned)((M * N + 255) / 256), 256, 0, st>>>((int)M, (int)N, S, alpha, part, beta, C, ldc, mask,
                                                                  ldm);
   return launch_status("rs_gemm");
@@ -490,6 +640,38 @@ extern "C" int rs_col_sum(const float* A, int64_t lda, int64_t M, int64_t N, flo
   RS_REQUIRE(A && out && M >= 0 && N > 0 && M < (1ll << 31) && lda >= N, "rs_col_sum: bad arguments");
   col_sum_kernel<<<(unsigned)N, 256, 0, as_stream(stream)>>>(A, lda, (int)M, (int)N, out);
   return launch_status("rs_col_sum");
+}
+
+static int64_t col_sum_slices(int64_t M) { return (M + CS_R - 1) / CS_R; }
+
+extern "C" int64_t rs_col_sum_workspace_size(int64_t M, int64_t N) {
+  if (M < 0 || N < 0) return -1;
+  const int64_t S = col_sum_slices(M);
+  return S > 1 ? S * N * 4 : 0;
+}
+
+static void col_sum_launch(const float* A, int64_t lda, int64_t M, int64_t N, float* out, void* ws, int64_t ws_bytes,
+                           hipStream_t st) {
+  const int64_t S = col_sum_slices(M);
+  if (S <= 1 || !ws || ws_bytes < S * N * 4 || S > (1 << 20)) {
+    col_sum_kernel<<<(unsigned)N, 256, 0, st>>>(A, lda, (int)M, (int)N, out);
+    return;
+  }
+  float* part = static_cast<float*>(ws);
+  col_sum_part_kernel<<<dim3((unsigned)((N + 63) / 64), (unsigned)S), 256, 0, st>>>(A, lda, M, (int)N, part);
+  if (S >= 64 && N <= (1 << 20))
+    col_sum_fin_wave<<<(unsigned)((N + 3) / 4), 256, 0, st>>>(part, (int)S, (int)N, out);
+  else
+    col_sum_fin_kernel<<<(unsigned)((N + 255) / 256), 256, 0, st>>>(part, (int)S, (int)N, out);
+}
+
+extern "C" int rs_col_sum_split(const float* A, int64_t lda, int64_t M, int64_t N, float* out, void* workspace,
+                                int64_t workspace_bytes, rs_stream_t stream) {
+  if (N == 0) return RS_OK;
+  RS_REQUIRE(A && out && M >= 0 && N > 0 && M < (1ll << 31) && N < (1ll << 30) && lda >= N,
+             "rs_col_sum_split: bad arguments");
+  col_sum_launch(A, lda, M, N, out, workspace, workspace_bytes, as_stream(stream));
+  return launch_status("rs_col_sum_split");
 }
 
 extern "C" int rs_sgd_update(float* w, const float* grad, int64_t n, float lr, float l2, rs_stream_t stream) {
@@ -601,9 +783,17 @@ static int64_t emb_sort_bytes(int64_t n) {
   return (int64_t)sb;
 }
 
+// chunk of sorted positions per piece: >= 4k so the crossing-segment
+// partials (2 k floats per chunk, only when n > C) fit in n floats
+static int64_t emb_chunk(int k) {
+  int64_t C = 256;
+  while (C < 4 * (int64_t)k) C <<= 1;
+  return C;
+}
+
 extern "C" int64_t rs_embedding_sgd_workspace_size(int64_t n_lookups) {
   if (n_lookups < 0) return -1;
-  return 4 * ((n_lookups * 4 + 255) / 256 * 256) + (emb_sort_bytes(n_lookups) + 255) / 256 * 256;
+  return 5 * ((n_lookups * 4 + 255) / 256 * 256) + (emb_sort_bytes(n_lookups) + 255) / 256 * 256;
 }
 
 extern "C" int rs_embedding_sgd(float* table, int64_t n_rows, int k, const void* ids, int id_kind, int64_t id_stride,
@@ -633,14 +823,20 @@ extern "C" int rs_embedding_sgd(float* table, int64_t n_rows, int k, const void*
   int bits = 1;
   while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)n_rows) ++bits;
   size_t sb = (size_t)emb_sort_bytes(n);
-  const hipError_t e = hipcub::DeviceRadixSort::SortPairs(ws + 4 * slab, sb, key_in, key_out, val_in, val_out, (int)n,
+  const hipError_t e = hipcub::DeviceRadixSort::SortPairs(ws + 5 * slab, sb, key_in, key_out, val_in, val_out, (int)n,
                                                           0, bits, st);
   if (e != hipSuccess) {
     set_error("rs_embedding_sgd: radix sort failed: %s", hipGetErrorString(e));
     return RS_ERR_HIP;
   }
-  emb_apply_kernel<<<(unsigned)((n * k + 255) / 256), 256, 0, st>>>(key_out, val_out, n, n_fields, k, grad,
-                                                                   grad_stride, lr, table);
+  const int64_t C = emb_chunk(k);
+  const int64_t nchunk = (n + C - 1) / C;
+  float* part_first = reinterpret_cast<float*>(ws + 4 * slab);
+  float* part_last = part_first + nchunk * k;
+  const unsigned g = (unsigned)((n * k + 255) / 256);
+  emb_piece_kernel<<<g, 256, 0, st>>>(key_out, val_out, n, n_fields, k, grad, grad_stride, lr, C, part_first,
+                                      part_last, table);
+  if (nchunk > 1) emb_cross_kernel<<<g, 256, 0, st>>>(key_out, n, k, lr, C, part_first, part_last, table);
   return launch_status("rs_embedding_sgd");
 }
 

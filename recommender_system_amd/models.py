@@ -788,8 +788,14 @@ class DIN(TowerMixin, KerasModule):
         width = 2 * K + sum(l.k for l in self.embed_sparse_layers) + self.dense_num
         shapes = [(W.shape[0], W.shape[1], M) for W in att.kernels] + [(att.out_kernel.shape[0], 1, M)]
         shapes += [(L.kernel.shape[0], L.kernel.shape[1], B) for L in self._layers()]
-        gws = _gemm_ws(self, max(max(_lib.lib().rs_gemm_workspace_size(kin, n, m),
-                                     _lib.lib().rs_gemm_workspace_size(m, kin, n)) for kin, n, m in shapes))
+        lb = _lib.lib()
+        # one scratch buffer for every stream-ordered call below (gemm split-K
+        # slices, column-sum slices, the PReLU backward's products)
+        need = [max(lb.rs_gemm_workspace_size(kin, n, m), lb.rs_gemm_workspace_size(m, kin, n),
+                    lb.rs_col_sum_workspace_size(m, n)) for kin, n, m in shapes]
+        need += [lb.rs_prelu_rows_bwd_workspace_size(M, W.shape[1], T) for W in att.kernels]
+        need += [lb.rs_prelu_rows_bwd_workspace_size(B, L.units, 1) for L in self.dense_layer]
+        gws = _gemm_ws(self, max(need))
         gw = (ptr(gws), gws.numel())
 
         # ---- forward, keeping what the backward needs
@@ -855,7 +861,7 @@ class DIN(TowerMixin, KerasModule):
             dW, db, din = emp(kin, n), emp(n), emp(m, kin)
             call("rs_gemm", 1, 0, kin, n, m, 1.0, ptr(a_in), a_in.stride(0), ptr(dz), dz.stride(0), 0.0, ptr(dW), n,
                  None, 0, *gw, st)
-            call("rs_col_sum", ptr(dz), dz.stride(0), m, n, ptr(db), st)
+            call("rs_col_sum_split", ptr(dz), dz.stride(0), m, n, ptr(db), *gw, st)
             call("rs_gemm", 0, 1, m, kin, n, 1.0, ptr(dz), dz.stride(0), ptr(W), n, 0.0, ptr(din), kin, None, 0,
                  *gw, st)
             updates.extend([(W, dW), (bias, db)])
@@ -864,7 +870,7 @@ class DIN(TowerMixin, KerasModule):
         def prelu_back(z, dy, alpha, period, m):
             n = z.shape[1]
             dz, dal = emp(m, n), emp(alpha.numel())
-            call("rs_prelu_rows_bwd", ptr(z), ptr(dy), m, n, ptr(alpha), period, ptr(dz), ptr(dal), st)
+            call("rs_prelu_rows_bwd", ptr(z), ptr(dy), m, n, ptr(alpha), period, ptr(dz), ptr(dal), *gw, st)
             updates.append((alpha, dal))
             return dz
 
