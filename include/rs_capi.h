@@ -672,9 +672,11 @@ int rs_shard_field_route(const void* ids, int id_kind, int64_t id_stride,
  * (global row, lookup) + a scan of the segment heads; deterministic.
  * rs_shard_dedup_grad (backward, same workspace, after the route of the same
  * step): dst[slot] = sum of the gradient rows grad[b*grad_stride + c*k ..]
- * of every lookup of that distinct row, in lookup order — one gradient row
- * per distinct row travels back to its owner.  Workspace:
- * rs_shard_dedup_workspace_size(batch*n_fields, world) bytes.              */
+ * of every lookup of that distinct row, in lookup order (in fixed chunk
+ * pieces, so hot rows stay parallel; it overwrites the route's scratch slabs,
+ * not its sorted keys) — one gradient row per distinct row travels back to
+ * its owner.  Workspace: rs_shard_dedup_workspace_size(batch*n_fields,
+ * world) bytes.                                                            */
 int64_t rs_shard_dedup_workspace_size(int64_t n_lookups, int world);
 int rs_shard_dedup_route(const void* ids, int id_kind, int64_t id_stride,
                          const int64_t* field_offsets,
@@ -685,7 +687,7 @@ int rs_shard_dedup_route(const void* ids, int id_kind, int64_t id_stride,
                          rs_stream_t stream);
 int rs_shard_dedup_grad(const float* grad, int64_t grad_stride, int n_fields,
                         int k, int64_t batch, int world, const int32_t* slot_of,
-                        const void* workspace, float* dst, rs_stream_t stream);
+                        void* workspace, float* dst, rs_stream_t stream);
 
 /* Sharded DeepFM backward (ShardedDeepFM.train_step): rs_scatter_rows
  * writes lookup j = b*n_fields + c's gradient row src[b*src_stride + c*k ..]

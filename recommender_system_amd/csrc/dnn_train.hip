@@ -402,27 +402,9 @@ __global__ __launch_bounds__(256) void emb_keys_kernel(const void* ids, int64_t 
 // Sorted lookups -> table[r] -= lr * (sum of the segment's gradient rows);
 // grad row of lookup j = b*F + c at grad[b*ldg + c*k].  One thread per
 // (position, column): the k columns of a segment are summed by k adjacent
-// lanes.  A segment is cut into PIECES at the fixed chunk boundaries
-// (multiples of C sorted positions); each piece is summed in position order
-// by one lane (seg_sum8) and a segment's pieces are added in chunk order, so
-// the result is bitwise reproducible and a hot row with 10^5 duplicates costs
-// C/8 + (#chunks)/8 dependent steps instead of 10^5/8.
-//   emb_piece_kernel: a segment inside one chunk is applied at once; a piece
-//     of a segment that crosses a chunk boundary goes to part_last[chunk]
-//     (the segment's head piece) or part_first[chunk] (a piece starting at the
-//     chunk's first position);
-//   emb_cross_kernel: the head lane of each crossing segment adds its head
-//     piece and the following chunks' first pieces and applies.
-__device__ __forceinline__ int64_t seg_end_in(const uint32_t* __restrict__ key, int64_t p, int64_t hi, uint32_t r) {
-  int64_t lo = p + 1;  // first q in (p, hi) with key[q] != r, else hi
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (key[mid] == r) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
+// lanes, in chunk pieces (seg_piece / seg_cross, rs_common.hpp), so a hot row
+// (the DIN padding id: 10^5 lookups per batch) stays parallel and the result
+// bitwise reproducible.
 __global__ __launch_bounds__(256) void emb_piece_kernel(const uint32_t* __restrict__ key,
                                                         const uint32_t* __restrict__ val, int64_t n, int F, int k,
                                                         const float* __restrict__ grad, int64_t ldg, float lr,
@@ -432,27 +414,15 @@ __global__ __launch_bounds__(256) void emb_piece_kernel(const uint32_t* __restri
   const int64_t p = t / k;
   const int f = (int)(t - p * k);
   if (p >= n) return;
-  const uint32_t r = key[p];
-  if (r == 0xffffffffu) return;
-  const bool seg_head = p == 0 || key[p - 1] != r;
-  const int64_t c = p / C;
-  if (!seg_head && p != c * C) return;
-  const int64_t cend = (c + 1) * C < n ? (c + 1) * C : n;
-  const int64_t e = seg_end_in(key, p, cend, r);
-  const float s = seg_sum8(p, e, [&](int64_t q) {
-    const int64_t j = val[q];
-    const int64_t b = j / F;
-    const int cc = (int)(j - b * F);
-    return grad[b * ldg + (int64_t)cc * k + f];
-  });
-  const bool crosses_out = e == cend && cend < n && key[cend] == r;
-  if (seg_head && !crosses_out) {
+  uint32_t r;
+  float s;
+  if (seg_piece(key, n, C, p, k, f, [&](int64_t q) {
+        const int64_t j = val[q];
+        const int64_t b = j / F;
+        const int cc = (int)(j - b * F);
+        return grad[b * ldg + (int64_t)cc * k + f];
+      }, part_first, part_last, r, s))
     table[(int64_t)r * k + f] -= lr * s;
-  } else if (seg_head) {
-    part_last[c * k + f] = s;
-  } else {
-    part_first[c * k + f] = s;
-  }
 }
 
 __global__ __launch_bounds__(256) void emb_cross_kernel(const uint32_t* __restrict__ key, int64_t n, int k,
@@ -463,15 +433,9 @@ __global__ __launch_bounds__(256) void emb_cross_kernel(const uint32_t* __restri
   const int64_t p = t / k;
   const int f = (int)(t - p * k);
   if (p >= n) return;
-  const uint32_t r = key[p];
-  if (r == 0xffffffffu || (p > 0 && key[p - 1] == r)) return;
-  const int64_t c0 = p / C;
-  const int64_t cend = (c0 + 1) * C;
-  if (cend >= n || key[cend] != r) return;  // ends inside its chunk (keys are sorted)
-  const int64_t e = seg_end(key, cend, n, r);
-  const int64_t c1 = (e - 1) / C;
-  const float rest = seg_sum8(c0 + 1, c1 + 1, [&](int64_t c) { return part_first[c * k + f]; });
-  table[(int64_t)r * k + f] -= lr * (part_last[c0 * k + f] + rest);
+  uint32_t r;
+  float s;
+  if (seg_cross(key, n, C, p, k, f, part_first, part_last, r, s)) table[(int64_t)r * k + f] -= lr * s;
 }
 
 // ------------------------------------------------------ CrossNet training
@@ -783,14 +747,6 @@ static int64_t emb_sort_bytes(int64_t n) {
   return (int64_t)sb;
 }
 
-// chunk of sorted positions per piece: >= 4k so the crossing-segment
-// partials (2 k floats per chunk, only when n > C) fit in n floats
-static int64_t emb_chunk(int k) {
-  int64_t C = 256;
-  while (C < 4 * (int64_t)k) C <<= 1;
-  return C;
-}
-
 extern "C" int64_t rs_embedding_sgd_workspace_size(int64_t n_lookups) {
   if (n_lookups < 0) return -1;
   return 5 * ((n_lookups * 4 + 255) / 256 * 256) + (emb_sort_bytes(n_lookups) + 255) / 256 * 256;
@@ -829,7 +785,7 @@ extern "C" int rs_embedding_sgd(float* table, int64_t n_rows, int k, const void*
     set_error("rs_embedding_sgd: radix sort failed: %s", hipGetErrorString(e));
     return RS_ERR_HIP;
   }
-  const int64_t C = emb_chunk(k);
+  const int64_t C = seg_chunk(k);
   const int64_t nchunk = (n + C - 1) / C;
   float* part_first = reinterpret_cast<float*>(ws + 4 * slab);
   float* part_last = part_first + nchunk * k;

@@ -164,6 +164,66 @@ __device__ __forceinline__ float seg_sum8(int64_t p, int64_t e, G get) {
   return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
+// Chunked segment sums over sorted keys (row-sparse SGD with hot rows): a
+// segment is cut into PIECES at the fixed chunk boundaries (multiples of C
+// sorted positions); each piece is summed in position order (seg_sum8) and a
+// segment's pieces are added in chunk order, so the sum is bitwise
+// reproducible and a row with 10^5 duplicates costs C/8 + (#chunks)/8
+// dependent steps instead of 10^5/8.  One lane per (position p, column f) of
+// W columns; key 0xffffffff = skip.
+//  seg_piece: true (with r and the whole sum) when p heads a segment inside
+//   one chunk; a piece of a crossing segment goes to part_last[chunk] (its
+//   head piece) or part_first[chunk] (the piece starting at the chunk start);
+//  seg_cross (after every seg_piece): true (with r and the sum) when p heads a
+//   crossing segment.
+__device__ __forceinline__ int64_t seg_end_in(const uint32_t* __restrict__ key, int64_t p, int64_t hi, uint32_t r) {
+  int64_t lo = p + 1;  // first q in (p, hi) with key[q] != r, else hi
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (key[mid] == r) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+template <class G>
+__device__ __forceinline__ bool seg_piece(const uint32_t* __restrict__ key, int64_t n, int64_t C, int64_t p, int W,
+                                          int f, G get, float* __restrict__ part_first,
+                                          float* __restrict__ part_last, uint32_t& r, float& sum) {
+  r = key[p];
+  if (r == 0xffffffffu) return false;
+  const bool head = p == 0 || key[p - 1] != r;
+  const int64_t c = p / C;
+  if (!head && p != c * C) return false;
+  const int64_t cend = (c + 1) * C < n ? (c + 1) * C : n;
+  const int64_t e = seg_end_in(key, p, cend, r);
+  const float s = seg_sum8(p, e, get);
+  const bool crosses = e == cend && cend < n && key[cend] == r;
+  if (head && !crosses) {
+    sum = s;
+    return true;
+  }
+  (head ? part_last : part_first)[c * W + f] = s;
+  return false;
+}
+__device__ __forceinline__ bool seg_cross(const uint32_t* __restrict__ key, int64_t n, int64_t C, int64_t p, int W,
+                                          int f, const float* __restrict__ part_first,
+                                          const float* __restrict__ part_last, uint32_t& r, float& sum) {
+  r = key[p];
+  if (r == 0xffffffffu || (p > 0 && key[p - 1] == r)) return false;
+  const int64_t c0 = p / C, cend = (c0 + 1) * C;
+  if (cend >= n || key[cend] != r) return false;  // ends inside its chunk (keys are sorted)
+  const int64_t c1 = (seg_end(key, cend, n, r) - 1) / C;
+  sum = part_last[c0 * W + f] + seg_sum8(c0 + 1, c1 + 1, [&](int64_t c) { return part_first[c * W + f]; });
+  return true;
+}
+// chunk length for W columns: >= 4W so the partials (2W floats per chunk,
+// only when n > C) fit in n floats
+inline int64_t seg_chunk(int W) {
+  int64_t C = 256;
+  while (C < 4 * (int64_t)W) C <<= 1;
+  return C;
+}
+
 __device__ __forceinline__ float row16_sum(float x) {
   x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xF, 0xF, false));
   x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x124, 0xF, 0xF, false));

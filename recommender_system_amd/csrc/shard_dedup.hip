@@ -125,26 +125,47 @@ __global__ __launch_bounds__(256) void dedup_scatter(const uint32_t* __restrict_
   if (head[p]) send[o * cap + u] = (int32_t)((int64_t)r - (int64_t)o * rpr);
 }
 
-// one thread per (sorted position, column): a segment head sums its row's
-// gradient over the segment (lookup order) into dst[slot]
-__global__ __launch_bounds__(256) void dedup_grad_sum(const uint32_t* __restrict__ key,
-                                                      const int32_t* __restrict__ val, int64_t n, int F, int k,
-                                                      const float* __restrict__ grad, int64_t ldg,
-                                                      const int32_t* __restrict__ slot_of, float* __restrict__ dst) {
+// one thread per (sorted position, column): each row's gradient summed over
+// its segment (lookup order) into dst[slot of the segment head], in chunk
+// pieces (seg_piece / seg_cross, rs_common.hpp) so a Zipf-hot row stays
+// parallel; the pieces' partials reuse the route's head / scan slabs
+__global__ __launch_bounds__(256) void dedup_grad_piece(const uint32_t* __restrict__ key,
+                                                        const int32_t* __restrict__ val, int64_t n, int F, int k,
+                                                        const float* __restrict__ grad, int64_t ldg,
+                                                        const int32_t* __restrict__ slot_of, int64_t C,
+                                                        float* __restrict__ part_first, float* __restrict__ part_last,
+                                                        float* __restrict__ dst) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t p = t / k;
   const int f = (int)(t - p * k);
   if (p >= n) return;
-  const uint32_t r = key[p];
-  if (r == 0xffffffffu || (p > 0 && key[p - 1] == r)) return;
+  uint32_t r;
+  float s;
+  if (!seg_piece(key, n, C, p, k, f, [&](int64_t q) {
+        const int64_t j = val[q];
+        const int64_t b = j / F;
+        const int c = (int)(j - b * F);
+        return grad[b * ldg + (int64_t)c * k + f];
+      }, part_first, part_last, r, s))
+    return;
   const int32_t slot = slot_of[val[p]];
-  if (slot < 0) return;
-  dst[(int64_t)slot * k + f] = seg_sum8(p, seg_end(key, p, n, r), [&](int64_t q) {
-    const int64_t j = val[q];
-    const int64_t b = j / F;
-    const int c = (int)(j - b * F);
-    return grad[b * ldg + (int64_t)c * k + f];
-  });
+  if (slot >= 0) dst[(int64_t)slot * k + f] = s;
+}
+
+__global__ __launch_bounds__(256) void dedup_grad_cross(const uint32_t* __restrict__ key,
+                                                        const int32_t* __restrict__ val, int64_t n, int k,
+                                                        const int32_t* __restrict__ slot_of, int64_t C,
+                                                        const float* __restrict__ part_first,
+                                                        const float* __restrict__ part_last, float* __restrict__ dst) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t p = t / k;
+  const int f = (int)(t - p * k);
+  if (p >= n) return;
+  uint32_t r;
+  float s;
+  if (!seg_cross(key, n, C, p, k, f, part_first, part_last, r, s)) return;
+  const int32_t slot = slot_of[val[p]];
+  if (slot >= 0) dst[(int64_t)slot * k + f] = s;
 }
 
 }  // namespace rs
@@ -211,16 +232,26 @@ extern "C" int rs_shard_dedup_route(const void* ids, int id_kind, int64_t id_str
 }
 
 extern "C" int rs_shard_dedup_grad(const float* grad, int64_t grad_stride, int n_fields, int k, int64_t batch,
-                                   int world, const int32_t* slot_of, const void* workspace, float* dst,
+                                   int world, const int32_t* slot_of, void* workspace, float* dst,
                                    rs_stream_t stream) {
   const int64_t n = batch * n_fields;
   if (n == 0) return RS_OK;
   RS_REQUIRE(grad && slot_of && workspace && dst && k >= 1 && world >= 1 && grad_stride >= (int64_t)n_fields * k,
              "rs_shard_dedup_grad: bad arguments");
   const DedupWs w = dedup_ws(n, world);
-  const uint8_t* ws = static_cast<const uint8_t*>(workspace);
-  dedup_grad_sum<<<(unsigned)((n * k + 255) / 256), 256, 0, as_stream(stream)>>>(
-      reinterpret_cast<const uint32_t*>(ws + w.key_out), reinterpret_cast<const int32_t*>(ws + w.val_out), n,
-      n_fields, k, grad, grad_stride, slot_of, dst);
+  uint8_t* ws = static_cast<uint8_t*>(workspace);
+  const uint32_t* key = reinterpret_cast<const uint32_t*>(ws + w.key_out);
+  const int32_t* val = reinterpret_cast<const int32_t*>(ws + w.val_out);
+  // piece partials (2 k floats per chunk, <= n floats when n > C) in the
+  // route's head + scan slabs (2n floats), which the route no longer needs
+  const int64_t C = seg_chunk(k);
+  const int64_t nch = (n + C - 1) / C;
+  float* part_first = reinterpret_cast<float*>(ws + w.head);
+  float* part_last = part_first + nch * k;
+  hipStream_t st = as_stream(stream);
+  const unsigned g = (unsigned)((n * k + 255) / 256);
+  dedup_grad_piece<<<g, 256, 0, st>>>(key, val, n, n_fields, k, grad, grad_stride, slot_of, C, part_first, part_last,
+                                      dst);
+  if (nch > 1) dedup_grad_cross<<<g, 256, 0, st>>>(key, val, n, k, slot_of, C, part_first, part_last, dst);
   return launch_status("rs_shard_dedup_grad");
 }

@@ -23,8 +23,8 @@
 // The decay touches every row (as Keras' dense regulariser gradient does);
 // G is non-zero only on the nd dense rows and the rows the batch looked up.
 // Sparse rows: per-lookup contributions are sorted by row (hipCUB radix sort,
-// stable) and each row's contributions are summed in lookup order by one
-// thread, so the result is bitwise reproducible.
+// stable) and each row's contributions are summed in lookup order, in chunk
+// pieces added in chunk order, so the result is bitwise reproducible.
 #include <hipcub/hipcub.hpp>
 
 #include "rs_common.hpp"
@@ -56,6 +56,8 @@ struct FmTrainArgs {
   uint32_t* val_in;
   uint32_t* val_out;
   float* gdense;  // [nd, k+1] + 1 (w0)
+  float* part;    // chunk-piece partials of crossing row segments (2 * nchunk * (k+1))
+  int64_t chunk;
   float* loss;    // [B] (optional)
   int* err;
 };
@@ -183,11 +185,16 @@ __global__ __launch_bounds__(256) void fm_train_decay(FmTrainArgs a) {
   }
 }
 
-// Sorted lookups: the first position of each row's segment sums the
-// segment's contributions in lookup order and applies them (one thread per
-// (position, column): a hot row's k+1 columns are summed by adjacent lanes,
-// each in the same fixed order, so the step stays bitwise reproducible);
+// Sorted lookups: each row's contributions summed in lookup order in chunk
+// pieces (seg_piece / seg_cross, rs_common.hpp: one lane per (position,
+// column), a hot row's k+1 columns by adjacent lanes, pieces added in chunk
+// order — bitwise reproducible, and a Zipf-hot row no longer serialises);
 // then the dense rows and w0.
+__device__ __forceinline__ void fm_apply_row(const FmTrainArgs& a, uint32_t r, int f, float acc) {
+  if (f < a.k) a.v[(int64_t)r * a.k + f] -= a.lr * acc;
+  else a.w1[r] -= a.lr * acc;
+}
+
 __global__ __launch_bounds__(256) void fm_train_apply(FmTrainArgs a) {
   const int64_t n = a.batch * a.F;
   const int K1 = a.k + 1;
@@ -195,13 +202,13 @@ __global__ __launch_bounds__(256) void fm_train_apply(FmTrainArgs a) {
   if (t < n * K1) {
     const int64_t p = t / K1;
     const int f = (int)(t - p * K1);
-    const uint32_t r = a.key_out[p];
-    if (p == 0 || a.key_out[p - 1] != r) {
-      const float acc = seg_sum8(p, seg_end(a.key_out, p, n, r),
-                                 [&](int64_t q) { return a.contrib[(int64_t)a.val_out[q] * K1 + f]; });
-      if (f < a.k) a.v[(int64_t)r * a.k + f] -= a.lr * acc;
-      else a.w1[r] -= a.lr * acc;
-    }
+    const int64_t nch = (n + a.chunk - 1) / a.chunk;
+    uint32_t r;
+    float acc;
+    if (seg_piece(a.key_out, n, a.chunk, p, K1, f,
+                  [&](int64_t q) { return a.contrib[(int64_t)a.val_out[q] * K1 + f]; }, a.part,
+                  a.part + nch * K1, r, acc))
+      fm_apply_row(a, r, f, acc);
   } else if (t < n * K1 + a.nd * K1 + 1) {
     const int idx = (int)(t - n * K1);
     const float gsum = a.gdense[idx];
@@ -215,9 +222,22 @@ __global__ __launch_bounds__(256) void fm_train_apply(FmTrainArgs a) {
   }
 }
 
+__global__ __launch_bounds__(256) void fm_train_apply_cross(FmTrainArgs a) {
+  const int64_t n = a.batch * a.F;
+  const int K1 = a.k + 1;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n * K1) return;
+  const int64_t p = t / K1;
+  const int f = (int)(t - p * K1);
+  const int64_t nch = (n + a.chunk - 1) / a.chunk;
+  uint32_t r;
+  float acc;
+  if (seg_cross(a.key_out, n, a.chunk, p, K1, f, a.part, a.part + nch * K1, r, acc)) fm_apply_row(a, r, f, acc);
+}
+
 // workspace layout (all 256-B aligned)
 struct TrainWs {
-  int64_t g, s, contrib, key_in, key_out, val_in, val_out, gdense, sort, total;
+  int64_t g, s, contrib, key_in, key_out, val_in, val_out, gdense, part, sort, total;
   size_t sort_bytes;
 };
 
@@ -239,6 +259,7 @@ static TrainWs train_ws(int64_t batch, int n_fields, int k, int nd) {
   w.val_in = o; o = al256(o + n * 4);
   w.val_out = o; o = al256(o + n * 4);
   w.gdense = o; o = al256(o + ((int64_t)nd * (k + 1) + 1) * 4);
+  w.part = o; o = al256(o + n * 4);  // <= n floats (seg_chunk(k + 1))
   w.sort = o; o = al256(o + (int64_t)sb);
   w.total = o;
   return w;
@@ -274,8 +295,8 @@ extern "C" int rs_fm_train_step(const void* ids, int id_kind, int64_t id_stride,
                 reinterpret_cast<float*>(ws + w.g), reinterpret_cast<float*>(ws + w.s),
                 reinterpret_cast<float*>(ws + w.contrib), reinterpret_cast<uint32_t*>(ws + w.key_in),
                 reinterpret_cast<uint32_t*>(ws + w.key_out), reinterpret_cast<uint32_t*>(ws + w.val_in),
-                reinterpret_cast<uint32_t*>(ws + w.val_out), reinterpret_cast<float*>(ws + w.gdense), loss,
-                err_flag};
+                reinterpret_cast<uint32_t*>(ws + w.val_out), reinterpret_cast<float*>(ws + w.gdense),
+                reinterpret_cast<float*>(ws + w.part), seg_chunk(k + 1), loss, err_flag};
   hipStream_t st = as_stream(stream);
   const int64_t n = batch * n_fields;
   with_id_kind(id_kind, [&](auto K) {
@@ -302,5 +323,6 @@ extern "C" int rs_fm_train_step(const void* ids, int id_kind, int64_t id_stride,
   fm_train_decay<<<(unsigned)std::min<int64_t>((dn / 4 + 255) / 256 + 1, 8192), 256, 0, st>>>(a);
   const int64_t ap = (n + nd) * (k + 1) + 1;
   fm_train_apply<<<(unsigned)((ap + 255) / 256), 256, 0, st>>>(a);
+  if (n > a.chunk) fm_train_apply_cross<<<(unsigned)((n * (k + 1) + 255) / 256), 256, 0, st>>>(a);
   return launch_status("rs_fm_train_step");
 }
