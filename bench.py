@@ -757,7 +757,7 @@ def bench_dcn(args, world, rank):
                  {"workload": "dcn_embed+crossnet_depth3_fused", "global_batch": B, "d": d, "layer_num": 3,
                   "vocab_per_field": V, "parallelism": "dp1"},
                  {"bound": "hbm", "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                  "frac": ach / PEAK_HBM, "traffic": None, "kernel": "embed_cross", "kernel_ms": kern_ms,
+                  "frac": ach / PEAK_HBM, "traffic": _pmc_cfg("dcn"), "kernel": "embed_cross", "kernel_ms": kern_ms,
                   "kernel_ms_source": "graph-replayed slot time per launch",
                   "algorithmic_bytes_per_launch": alg, "mfma_useful_flop_per_launch": useful,
                   "mfma_issued_flop_per_launch": issued, "mfma_useful_fraction_by_construction": useful / issued},
@@ -864,7 +864,7 @@ def bench_din(args, world, rank):
                  {"workload": "din_attention_unit_from_ids", "global_batch": B, "seq_len": T, "embed_dim": k,
                   "att_hidden": [80, 40], "behaviour_vocab": 63001, "parallelism": "dp1"},
                  {"bound": "mfma", "achieved": ach / 1e12, "peak": PEAK_F32 / 1e12, "unit": "TFLOP/s",
-                  "frac": ach / PEAK_F32, "traffic": None, "kernel": "din_scores (+din_pool)", "kernel_ms": att_ms,
+                  "frac": ach / PEAK_F32, "traffic": _pmc_cfg("din"), "kernel": "din_scores (+din_pool)", "kernel_ms": att_ms,
                   "kernel_ms_source": "graph-replayed step (both launches) / steps",
                   "useful_flop_per_launch": flop,
                   "useful_flop_note": "reference formulation T*2*(4k*80+80*40+40); the kernel regroups layer 1 "
@@ -941,7 +941,7 @@ def bench_pnn(args, world, rank):
                  args.steps * B / dt, "samples/s", args, world, dt / args.steps * 1e3,
                  {"workload": "pnn_embed_inner_fused", "global_batch": B, "vocab_per_field": V, "parallelism": "dp1"},
                  {"bound": "hbm", "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                  "frac": ach / PEAK_HBM, "traffic": None, "kernel": "inner_fast", "kernel_ms": slot,
+                  "frac": ach / PEAK_HBM, "traffic": _pmc_cfg("pnn"), "kernel": "inner_fast", "kernel_ms": slot,
                   "algorithmic_bytes_per_launch": alg},
                  {"mode_both": {"samples_per_s": n2 * B / dtb, "kernel_ms": slotb,
                                 "outer_mfma_tflops": B * P * k * k * 2 / (slotb * 1e-3) / 1e12,
@@ -965,13 +965,17 @@ def _rank3_setup(args, k, nd=13):
     return B, F, V, cols, ids_pool, dense_pool
 
 
+_PMC_OF_WORKLOAD = {"nfm_embed_bi_interaction_fused": "nfm", "afm_att_fused": "afm", "ffm_fused": "ffm"}
+
+
 def _hbm_line(metric, args, world, B, dt, slot, alg, workload, V, kernel, extra=None):
     ach = alg / (slot * 1e-3)
+    cfg = _PMC_OF_WORKLOAD.get(workload)
     return _line(metric, args.steps * B / dt, "samples/s", args, world, dt / args.steps * 1e3,
                  {"workload": workload, "global_batch": B, "vocab_per_field": V, "parallelism": "dp1"},
                  {"bound": "hbm", "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                  "frac": ach / PEAK_HBM, "traffic": None, "kernel": kernel, "kernel_ms": slot,
-                  "algorithmic_bytes_per_launch": alg}, extra)
+                  "frac": ach / PEAK_HBM, "traffic": _pmc_cfg(cfg) if cfg else None, "kernel": kernel,
+                  "kernel_ms": slot, "algorithmic_bytes_per_launch": alg}, extra)
 
 
 def bench_nfm(args, world, rank):
@@ -1007,7 +1011,7 @@ def bench_nfm(args, world, rank):
 
         cpu = _cpu_leg(args, rank, B, cpu_step, 8, "EmbedLayer (3-D) + Bi-Interaction -> [dense | pooled]", gpu0)
     return _hbm_line("NFM bi-interaction input samples/sec @ batch 4096, 26 sparse x 1e6 vocab, dim 16", args,
-                     world, B, dt, slot, alg, "nfm_embed_bi_interaction_fused", V, "pair_pool_kernel (sum)",
+                     world, B, dt, slot, alg, "nfm_embed_bi_interaction_fused", V, "pair_pool_ksplit (sum)",
                      {"nfm_forward": {"samples_per_s": n2 * B / dtf, "ms_per_step": dtf / n2 * 1e3,
                                       "note": "bi-interaction launch + BN + DNN 29-256-128-64-1 + Dense(1) tower"},
                       "cpu_baseline": cpu})
@@ -1055,7 +1059,7 @@ def bench_afm(args, world, rank):
         cpu = _cpu_leg(args, rank, B, cpu_step, 8, "AFM.call 'att': Embedding per field, InteractionLayer [B, 325, "
                                                   "k], AttentionLayer, Dense(1), two sigmoids", gpu0)
     return _hbm_line("AFM forward samples/sec @ batch 4096, 26 sparse x 1e6 vocab, dim 16", args, world, B, dt,
-                     slot, alg, "afm_att_fused", V, "pair_pool_kernel (att == sum)",
+                     slot, alg, "afm_att_fused", V, "pair_pool_ksplit (att == sum)",
                      {"mode_max": {"samples_per_s": args.steps * B / dtm, "kernel_ms": slotm,
                                    "note": "max over the 325 pair products per dim, in registers"},
                       "cpu_baseline": cpu})
@@ -1104,7 +1108,7 @@ def bench_ffm(args, world, rank):
                                                   "never formed) + sigmoid; host copy holds the touched rows only",
                        gpu0)
     return _hbm_line("FFM forward samples/sec @ batch 4096, 26 sparse x 1e6 vocab, k 8", args, world, B, dt, slot,
-                     alg, "ffm_fused", V, "ffm_kernel",
+                     alg, "ffm_fused", V, "ffm4_kernel",
                      {"table_GB": (13 + F * V) * NF * k * 4 / 1e9, "cpu_baseline": cpu})
 
 
@@ -1260,6 +1264,16 @@ def bench_fm_train(args, world, rank):
                   "reference_scale": {"steps_per_s": args.steps / dts, "ms_per_step": dts / args.steps * 1e3,
                                       "note": "batch 32, 26 x 1,677 + 13 = 43,615 columns, k 8 (compile_fit's "
                                               "defaults on the bundled sample's width)"}})
+
+
+def _pmc_cfg(cfg):
+    """PMC HBM bytes per launch of a config line's dominant kernel
+    (profiles/pmc_configs.json, scripts/gpu_pmc_configs.sh), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_configs.json")) as f:
+            return json.load(f)[cfg]["hbm_bytes_per_launch"]
+    except Exception:
+        return None
 
 
 def _pmc_traffic():
