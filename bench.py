@@ -54,11 +54,19 @@ def _dist_setup(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 or args.sharded:
-        torch.cuda.set_device(local)
+        # RS_BENCH_BACKEND=gloo RS_BENCH_ONE_DEVICE=1: rehearsal of the N > 1
+        # code path with every rank on device 0 (one-GPU box; gloo stages the
+        # collectives through the host, so steps run eager) — never a result
+        one_dev = os.environ.get("RS_BENCH_ONE_DEVICE") == "1"
+        backend = os.environ.get("RS_BENCH_BACKEND", "nccl")
+        torch.cuda.set_device(0 if one_dev else local)
         import torch.distributed as dist
         for key, val in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29533"), ("RANK", "0"), ("WORLD_SIZE", "1")):
             os.environ.setdefault(key, val)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", 0 if one_dev else local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return world, rank
@@ -387,6 +395,8 @@ def _graph_capturable(fn, first, begin=None, end=None, count=1):
     agree collectively: the RCCL all-to-alls are graph-captured only if every
     rank captured cleanly, otherwise every rank times the eager step."""
     import torch.distributed as dist
+    if dist.get_backend() != "nccl":  # the gloo rehearsal: host-staged collectives cannot be captured
+        return False, "gloo rehearsal (collectives staged through the host)"
     ok, why = 1, None
     try:
         _capture(fn, first, count, begin, end)
