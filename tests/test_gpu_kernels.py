@@ -647,3 +647,26 @@ def test_full_size_table_addressing(gpu):
     zz = x_emb.reshape(B, F, k)
     pref = np.concatenate([x_emb, O.inner_product_layer(zz), O.outer_product_layer(zz, p.outer_product_layer.W.cpu().numpy())], 1)
     assert_scaled_close(xin, pref, what="PNN both @16.6 GB")
+
+
+def test_headline_shape_full_size(gpu):
+    """The headline configuration itself (BASELINE metric: batch 4096, 26 x
+    1e7 x 16 fp32 table = 16.6 GB, uniform int32 ids over the full range):
+    rs_embed_fm_fwd (the benched kernel, DeepFM.fm_logit) and the fused DeepFM
+    forward against the fp64 oracle on the rows the batch touches."""
+    from recommender_system_amd import DeepFM
+    from tests.helpers import criteo_columns, dnn_params
+    V, F, k, B = 10_000_000, 26, 16, 4096
+    rng = np.random.default_rng(4096)
+    ids = rng.integers(0, V, size=(B, F)).astype(np.int32)
+    ids[0] = V - 1
+    dense = rng.random((B, 13)).astype(np.float32)
+    m = DeepFM(criteo_columns([V] * F, embed_dim=k), 10, 1e-4, 1e-4, [256, 128, 64], 1, "relu", embed_dim=k, seed=5)
+    e = m.embed_layer
+    rows = torch.as_tensor((e.field_offsets.cpu().numpy()[None, :] + ids).reshape(-1), device="cuda")
+    x = np.concatenate([dense, e.table[rows].cpu().numpy().reshape(B, F * k)], 1)
+    fm = O.fm_layer(x, m.fm.w0.cpu().numpy(), m.fm.w1.cpu().numpy(), m.fm.v.cpu().numpy())
+    assert_scaled_close(m.fm_logit((dense, ids)), fm, what="FM logit, headline shape")
+    hidden, out = dnn_params(m.dnn)
+    ref = 1.0 / (1.0 + np.exp(-(0.5 * (fm + O.dnn_layer(x, hidden, out)))))
+    assert_rel_close(m((dense, ids)), ref, what="DeepFM fused, headline shape")
