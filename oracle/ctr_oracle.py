@@ -606,14 +606,28 @@ def pnn_bce(pre, t, dt=np.float64):
     return per.mean(), per
 
 
-def pnn_train_step(ids, t, p, lr, act="relu", dt=np.float64):
+def _pnn_x(e, flat, p, mode, dt):
+    parts = [flat]
+    if mode in ("inner", "both"):
+        parts.append(inner_product_layer(e, dt=dt))
+    if mode in ("outer", "both"):
+        parts.append(outer_product_layer(e, p["outer_W"], dt=dt))
+    return np.concatenate(parts, axis=1)
+
+
+def pnn_train_step(ids, t, p, lr, act="relu", dt=np.float64, mode="inner"):
     """One step of the reference's PNN loop (model/pnn.py:74-81: GradientTape,
-    SGD(lr) over model.variables) for mode 'inner', backpropagated by hand:
+    SGD(lr) over model.variables) for mode 'inner' / 'outer' / 'both' (the
+    loop's own example runs 'both', :61), backpropagated by hand:
     dL/dpre_i = (-ybar/(q_i+eps) + (1-ybar)/(1-q_i+eps))/B inside the clip
     range, 0 outside (tf.clip_by_value); the DNN by the chain rule (Dropout is
     the identity: the loop calls model(X) without training=True); the inner
-    products p_ij = e_i . e_j give de_i += dL/dp_ij e_j; embedding rows by
-    scatter-add.  No regularisers (DNNLayer's Dense layers have none).
+    products p_ij = e_i . e_j give de_i += dL/dp_ij e_j; the outer products
+    o_p = e_j^T W_p e_i (W_p[a][c] = W[a,p,c], i = row(p), j = col(p),
+    layer/interaction.py:200-215) give de_i += g_p W_p^T e_j, de_j += g_p W_p e_i
+    and dW[a,p,c] = sum_b g_bp e_j[a] e_i[c]; embedding rows by scatter-add.
+    No regularisers: the loop's loss is the BCE alone (OuterProductLayer's
+    l2(1e-4) sits in model.losses, which the loop never adds).
     Returns (new p, per-sample losses before the step)."""
     ids = cast_ids(ids)
     t = np.asarray(t, dt).reshape(-1)
@@ -622,7 +636,7 @@ def pnn_train_step(ids, t, p, lr, act="relu", dt=np.float64):
     F = len(tables)
     flat = embed_layer(ids, tables, dt)
     e = flat.reshape(flat.shape[0], F, k)
-    x = np.concatenate([flat, inner_product_layer(e, dt=dt)], axis=1)
+    x = _pnn_x(e, flat, p, mode, dt)
     layers = [(np.array(W, dt), np.array(b, dt)) for W, b in p["dnn_hidden"]] + \
              [(np.array(p["dnn_out"][0], dt), np.array(p["dnn_out"][1], dt))]
     acts = [x]
@@ -647,21 +661,38 @@ def pnn_train_step(ids, t, p, lr, act="relu", dt=np.float64):
         delta = prev
     de = delta[:, :F * k].reshape(B, F, k).copy()
     row, col = pair_indices(F)
-    dpi = delta[:, F * k:]
-    for pi, (i, j) in enumerate(zip(row, col)):
-        de[:, i, :] += dpi[:, pi:pi + 1] * e[:, j, :]
-        de[:, j, :] += dpi[:, pi:pi + 1] * e[:, i, :]
+    P = len(row)
+    off = F * k
+    new = {}
+    if mode in ("inner", "both"):
+        dpi = delta[:, off:off + P]
+        off += P
+        for pi, (i, j) in enumerate(zip(row, col)):
+            de[:, i, :] += dpi[:, pi:pi + 1] * e[:, j, :]
+            de[:, j, :] += dpi[:, pi:pi + 1] * e[:, i, :]
+    if mode in ("outer", "both"):
+        W = np.array(p["outer_W"], dt)  # [k, P, k]
+        dpo = delta[:, off:off + P]
+        dW = np.zeros_like(W)
+        for pi, (i, j) in enumerate(zip(row, col)):
+            Wp = W[:, pi, :]                                      # [a, c]
+            g = dpo[:, pi:pi + 1]
+            de[:, i, :] += g * (e[:, j, :] @ Wp)                  # sum_a e_j[a] W[a,c]
+            de[:, j, :] += g * (e[:, i, :] @ Wp.T)                # sum_c W[a,c] e_i[c]
+            dW[:, pi, :] = (g * e[:, j, :]).T @ e[:, i, :]        # sum_b g e_j[a] e_i[c]
+        new["outer_W"] = W - lr * dW
     for c, tb in enumerate(tables):
         np.add.at(tb, ids[:, c], -lr * de[:, c, :])
-    return {"tables": tables, "dnn_hidden": new_layers[:-1], "dnn_out": new_layers[-1]}, loss
+    new.update({"tables": tables, "dnn_hidden": new_layers[:-1], "dnn_out": new_layers[-1]})
+    return new, loss
 
 
-def pnn_loss(ids, t, p, act="relu", dt=np.float64):
-    """The PNN loop's objective (pnn_bce of the inner-mode forward)."""
+def pnn_loss(ids, t, p, act="relu", dt=np.float64, mode="inner"):
+    """The PNN loop's objective (pnn_bce of the forward in ``mode``)."""
     flat = embed_layer(cast_ids(ids), p["tables"], dt)
     k = np.asarray(p["tables"][0]).shape[1]
     e = flat.reshape(flat.shape[0], -1, k)
-    x = np.concatenate([flat, inner_product_layer(e, dt=dt)], axis=1)
+    x = _pnn_x(e, flat, p, mode, dt)
     pre = dnn_layer(x, p["dnn_hidden"], p["dnn_out"], act, dt)
     return pnn_bce(pre, t, dt)[0]
 

@@ -432,3 +432,41 @@ def test_din_train_step_gradient_matches_finite_differences():
     c = O._din_train_forward(inputs, p, dense, sparse, beh, np.float64)
     np.testing.assert_allclose(new["bn"][2], 0.01 * c["bmu"], rtol=1e-12)
     np.testing.assert_allclose(new["bn"][3], 0.99 + 0.01 * c["bvar"], rtol=1e-12)
+
+
+@pytest.mark.parametrize("mode", ["outer", "both"])
+def test_pnn_train_step_outer_gradient_matches_finite_differences(mode):
+    """The same for modes 'outer' / 'both' (the reference loop's own example,
+    model/pnn.py:61): the OuterProductLayer weight W [k, P, k] and the rows
+    feeding the outer products o_p = e_j^T W_p e_i, against central
+    differences of the loop's objective."""
+    rng = np.random.default_rng(22)
+    k = 3
+    vocab = [3, 2, 4]
+    F = len(vocab)
+    P = F * (F - 1) // 2
+    tables = [rng.normal(size=(v_, k)) * 0.5 for v_ in vocab]
+    w = F * k + (2 if mode == "both" else 1) * P
+    p = {"tables": tables, "outer_W": rng.normal(size=(k, P, k)) * 0.4,
+         "dnn_hidden": [(rng.normal(size=(w, 5)) * 0.3, rng.normal(size=5) * 0.1)],
+         "dnn_out": (rng.normal(size=(5, 1)) * 0.1, np.array([0.5]))}
+    ids = np.array([[0, 1, 3], [2, 1, 0], [0, 0, 3], [1, 1, 2]])
+    t = np.array([1.0, 0.0, 1.0, 0.0])
+    lr = 1.0
+    new, _ = O.pnn_train_step(ids, t, p, lr, mode=mode)
+    eps = 1e-6
+
+    def check(arr, new_arr, idx):
+        keep = arr[idx]
+        arr[idx] = keep + eps
+        lp = O.pnn_loss(ids, t, p, mode=mode)
+        arr[idx] = keep - eps
+        lm = O.pnn_loss(ids, t, p, mode=mode)
+        arr[idx] = keep
+        assert abs((lp - lm) / (2 * eps) - (arr[idx] - new_arr[idx]) / lr) < 1e-6, idx
+
+    for idx in [(0, 0, 0), (2, 1, 1), (1, 2, 0), (0, 2, 2)]:
+        check(p["outer_W"], new["outer_W"], idx)
+    for c, idx in [(0, (0, 0)), (0, (2, 1)), (1, (1, 2)), (2, (3, 0))]:
+        check(p["tables"][c], new["tables"][c], idx)
+    check(p["dnn_hidden"][0][0], new["dnn_hidden"][0][0], (w - 1, 2))
