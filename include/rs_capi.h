@@ -461,6 +461,20 @@ int rs_inner_product_bwd(const float* emb, int64_t emb_stride,
                          const float* dflat, int64_t dflat_stride, int n_fields,
                          int k, int64_t batch, float* demb, int64_t demb_stride,
                          rs_stream_t stream);
+/* OuterProductLayer backward (layer/interaction.py:200-215, PNN modes
+ * 'outer' / 'both'): o_p = e_j^T W_p e_i, W_p[a][c] = W[a,p,c], W [k, P, k].
+ * rs_outer_product_bwd ADDS to demb[b, f*k ..]: sum_{j>f} g_p e_j W_p +
+ *  sum_{i<f} g_p e_i W_p^T (g = dout[b, p], pairs in order).
+ * rs_outer_product_w_grad: dW[a,p,c] = sum_b g_bp e_j[b,a] e_i[b,c].
+ * 2 <= n_fields <= 64, 1 <= k <= 16; fp32 MFMA, deterministic.              */
+int rs_outer_product_bwd(const float* emb, int64_t emb_stride,
+                         const float* dout, int64_t dout_stride, const float* W,
+                         int n_fields, int k, int64_t batch, float* demb,
+                         int64_t demb_stride, rs_stream_t stream);
+int rs_outer_product_w_grad(const float* emb, int64_t emb_stride,
+                            const float* dout, int64_t dout_stride,
+                            int n_fields, int k, int64_t batch, float* dW,
+                            rs_stream_t stream);
 /* DIN training (compile_fit on model/din.py:56-95, training=True; the host
  * layer DIN.train_step composes these with rs_dense_fwd / rs_gemm /
  * rs_col_sum / rs_sgd_update / rs_embedding_sgd):

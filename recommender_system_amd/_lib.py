@@ -81,6 +81,8 @@ SIGNATURES = {
     "rs_head_grad_scaled": (I, [P, P, P, L, F, F, F, P, P, P, P]),
     "rs_bce_prob_grad": (I, [P, L, P, L, P, P, P]),
     "rs_inner_product_bwd": (I, [P, L, P, L, P, L, I, I, L, P, L, P]),
+    "rs_outer_product_bwd": (I, [P, L, P, L, P, I, I, L, P, L, P]),
+    "rs_outer_product_w_grad": (I, [P, L, P, L, I, I, L, P, P]),
     "rs_din_att_concat": (I, [P, P, L, I, I, P, P]),
     "rs_din_att_concat_bwd": (I, [P, P, P, L, I, I, P, L, P, P]),
     "rs_prelu_rows_fwd": (I, [P, L, I, P, I, P, P]),

@@ -380,6 +380,102 @@ __global__ __launch_bounds__(256) void owner_rows_kernel(const int32_t* __restri
   xo[idx] = (r >= 0 && r < shard_rows) ? shard[r * k + (e - u * k)] : 0.f;
 }
 
+// ------------------------------------------ OuterProductLayer backward
+// layer/interaction.py:200-215: o_p = e_j^T W_p e_i with W_p[a][c] = W[a,p,c]
+// (W [k, P, k]), i = row(p) < j = col(p).  With g = dL/do:
+//   de_f += sum_{j>f} g_p (e_j W_p) + sum_{i<f} g_p (e_i W_p^T)    (outer_bwd)
+//   dW[a,p,c] = sum_b g_bp e_j[b,a] e_i[b,c]                       (outer_w_grad)
+// Both on v_mfma_f32_16x16x4f32 (k <= 16 padded to 16 columns): the scaling by
+// g rides in the A fragment, so every field's contributions accumulate in one
+// MFMA chain in pair order (deterministic).
+__device__ __forceinline__ int pair_of(int i, int j, int F) { return i * (2 * F - i - 1) / 2 + j - i - 1; }
+
+// one workgroup per 16-sample tile: the tile's [16][F*k] embeddings in LDS;
+// wave w owns fields f = w, w + NW, ... and adds its MFMA tile into demb
+__global__ __launch_bounds__(1024) void outer_bwd_kernel(const float* __restrict__ emb, int64_t lde,
+                                                         const float* __restrict__ dout, int64_t ldd,
+                                                         const float* __restrict__ W, int F, int k, int64_t B,
+                                                         float* __restrict__ demb, int64_t lddm) {
+  extern __shared__ float se[];
+  const int Fk = F * k, LS = Fk + 1, P = F * (F - 1) / 2;
+  const int64_t b0 = (int64_t)blockIdx.x * 16;
+  for (int e = threadIdx.x; e < 16 * Fk; e += 1024) {
+    const int r = e / Fk, c = e - r * Fk;
+    const int64_t b = b0 + r < B ? b0 + r : B - 1;
+    se[r * LS + c] = emb[b * lde + c];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int s = lane & 15, kk = lane >> 4;
+  const int64_t bs = b0 + s < B ? b0 + s : B - 1;
+  const bool vs = b0 + s < B;
+  for (int f = w; f < F; f += 16) {
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int o = 0; o < F; ++o) {
+      if (o == f) continue;
+      const int p = o > f ? pair_of(f, o, F) : pair_of(o, f, F);
+      const float gx = dout[bs * ldd + p];
+      const float g = vs ? gx : 0.f;
+      const float* eo = se + s * LS + o * k;
+      for (int k0 = 0; k0 < k; k0 += 4) {
+        const int kr = k0 + kk;
+        const float av = kr < k ? g * eo[kr] : 0.f;
+        // B[kr][col]: W[kr, p, col] (e_o W_p, o = j > f) or W[col, p, kr] (e_o W_p^T, o = i < f)
+        const int ac = s < k ? s : 0, ak = kr < k ? kr : 0;
+        const float wx = o > f ? W[((int64_t)ak * P + p) * k + ac] : W[((int64_t)ac * P + p) * k + ak];
+        const float bv = (s < k && kr < k) ? wx : 0.f;
+        acc = mfma16x16x4(av, bv, acc);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t b = b0 + 4 * kk + r;
+      if (b < B && s < k) demb[b * lddm + (int64_t)f * k + s] += acc[r];
+    }
+  }
+}
+
+// one workgroup per pair: 4 waves stride the batch 4 samples per MFMA, the
+// 4 partial tiles added in wave order
+__global__ __launch_bounds__(256) void outer_w_grad_kernel(const float* __restrict__ emb, int64_t lde,
+                                                           const float* __restrict__ dout, int64_t ldd, int F, int k,
+                                                           int64_t B, float* __restrict__ dW) {
+  __shared__ floatx4 red[4][64];
+  const int p = blockIdx.x, P = F * (F - 1) / 2;
+  int i = 0, rem = p;
+  while (rem >= F - 1 - i) {
+    rem -= F - 1 - i;
+    ++i;
+  }
+  const int j = i + 1 + rem;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int s = lane & 15, kk = lane >> 4;
+  const int sc = s < k ? s : 0;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t bb = 4 * w; bb < B; bb += 16) {
+    const int64_t b = bb + kk;
+    const int64_t bc = b < B ? b : B - 1;  // clamped: the loads stay unconditional
+    const float g = dout[bc * ldd + p];
+    const float ej = emb[bc * lde + (int64_t)j * k + sc];
+    const float ei = emb[bc * lde + (int64_t)i * k + sc];
+    const bool ok = b < B && s < k;
+    // A[row a = s][kdim = kk] = g_b e_j[b][a];  B[kdim = kk][col c = s] = e_i[b][c]
+    acc = mfma16x16x4(ok ? g * ej : 0.f, ok ? ei : 0.f, acc);
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0) {
+    floatx4 t = red[0][lane];
+#pragma unroll
+    for (int u = 1; u < 4; ++u) t += red[u][lane];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int a = 4 * kk + r;
+      if (a < k && s < k) dW[((int64_t)a * P + p) * k + s] = t[r];
+    }
+  }
+}
+
 // ------------------------------------------- row-sparse SGD of the tables
 template <int KIND>
 __global__ __launch_bounds__(256) void emb_keys_kernel(const void* ids, int64_t id_stride,
@@ -651,6 +747,31 @@ extern "C" int rs_bce_prob_grad(const float* pred, int64_t pred_stride, const fl
   RS_REQUIRE(pred && labels && g && batch > 0 && pred_stride >= 1, "rs_bce_prob_grad: bad arguments");
   bce_prob_grad_kernel<<<1, 1024, 0, as_stream(stream)>>>(pred, pred_stride, labels, batch, g, loss);
   return launch_status("rs_bce_prob_grad");
+}
+
+extern "C" int rs_outer_product_bwd(const float* emb, int64_t emb_stride, const float* dout, int64_t dout_stride,
+                                    const float* W, int n_fields, int k, int64_t batch, float* demb,
+                                    int64_t demb_stride, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(emb && dout && W && demb && batch > 0 && n_fields >= 2 && n_fields <= 64 && k >= 1 && k <= 16 &&
+                 emb_stride >= n_fields * k && demb_stride >= n_fields * k &&
+                 dout_stride >= n_fields * (n_fields - 1) / 2,
+             "rs_outer_product_bwd: bad arguments (2 <= n_fields <= 64, 1 <= k <= 16)");
+  const size_t lds = (size_t)16 * (n_fields * k + 1) * sizeof(float);
+  outer_bwd_kernel<<<(unsigned)((batch + 15) / 16), 1024, lds, as_stream(stream)>>>(
+      emb, emb_stride, dout, dout_stride, W, n_fields, k, batch, demb, demb_stride);
+  return launch_status("rs_outer_product_bwd");
+}
+
+extern "C" int rs_outer_product_w_grad(const float* emb, int64_t emb_stride, const float* dout, int64_t dout_stride,
+                                       int n_fields, int k, int64_t batch, float* dW, rs_stream_t stream) {
+  RS_REQUIRE(emb && dout && dW && batch >= 0 && n_fields >= 2 && n_fields <= 64 && k >= 1 && k <= 16 &&
+                 emb_stride >= n_fields * k && dout_stride >= n_fields * (n_fields - 1) / 2,
+             "rs_outer_product_w_grad: bad arguments (2 <= n_fields <= 64, 1 <= k <= 16)");
+  if (batch == 0) return RS_OK;  // (dW untouched: callers size the step on a non-empty batch)
+  outer_w_grad_kernel<<<(unsigned)(n_fields * (n_fields - 1) / 2), 256, 0, as_stream(stream)>>>(
+      emb, emb_stride, dout, dout_stride, n_fields, k, batch, dW);
+  return launch_status("rs_outer_product_w_grad");
 }
 
 extern "C" int rs_inner_product_bwd(const float* emb, int64_t emb_stride, const float* dinner, int64_t dinner_stride,

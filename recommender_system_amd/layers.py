@@ -364,6 +364,9 @@ class OuterProductLayer(KerasModule):
         with torch.no_grad():
             self.W.copy_(torch.as_tensor(weights["W"], dtype=torch.float32).reshape(self.W.shape))
 
+    def _invalidate(self):
+        self._prep_key = None  # W moved through a raw pointer (training): repack
+
     def prepared(self):
         """W packed into per-lane MFMA fragments (rs_outer_prepare), cached."""
         key = (self.W._version, self.W.data_ptr())
@@ -694,6 +697,9 @@ class Attention(KerasModule):
         """The id-driven fused path (rs_din_attention_ids_fwd) supports it."""
         return (self.activation == "prelu" and self.out_kernel is not None and len(self.hidden_units) == 2
                 and k in (4, 8, 16) and self.hidden_units[0] <= 128 and self.hidden_units[1] <= 64)
+
+    def _invalidate(self):
+        self._ids_key = None  # weights moved through raw pointers (training): repack
 
     def prepared_ids(self, k):
         params = list(self.kernels) + list(self.biases) + list(self.alphas) + [self.out_kernel, self.out_bias]

@@ -601,16 +601,19 @@ class PNN(KerasModule):
         GradientTape, SGD(lr) over model.variables, loss
         tf.reduce_mean(losses.binary_crossentropy(y_train, pre)) on the DNN
         LOGIT — Keras' clipped probability form with the labels broadcast
-        against the [B, 1] output, rs_bce_prob_grad), mode 'inner':
-          [flat | inner] in one launch (rs_embed_inner_fwd), DNN forward with
-          saved activations (rs_dense_fwd), the DNN backward (split-K rs_gemm,
-          rs_col_sum), rs_inner_product_bwd (dflat + sum_j dinner_ij e_j),
-          SGD of the DNN and row-sparse rs_embedding_sgd of the tables.
-        The loop calls model(X) without training=True, so Dropout is the
-        identity there too.  Returns the per-sample losses (before the step)
-        if ``return_loss``."""
-        if self.mode != "inner":
-            raise NotImplementedError("PNN.train_step: mode 'inner' (outer-product backward not built)")
+        against the [B, 1] output, rs_bce_prob_grad), modes 'inner' /
+        'outer' / 'both' (the loop's own example runs 'both', :61):
+          [flat | inner | outer] in one launch (rs_embed_inner_fwd /
+          rs_embed_product_fwd), DNN forward with saved activations
+          (rs_dense_fwd), the DNN backward (split-K rs_gemm, rs_col_sum),
+          rs_inner_product_bwd (dflat + sum_j dinner_ij e_j),
+          rs_outer_product_bwd (+ sum g_p e_j W_p / e_i W_p^T) and
+          rs_outer_product_w_grad (dW), then SGD of the DNN and of W and
+          row-sparse rs_embedding_sgd of the tables.  The loop's loss has no
+          regulariser (OuterProductLayer's l2 sits in model.losses, never
+          added there).  The loop calls model(X) without training=True, so
+          Dropout is the identity there too.  Returns the per-sample losses
+          (before the step) if ``return_loss``."""
         dnn = self.dnn_layer
         if dnn.output_layer.units != 1:
             raise NotImplementedError("PNN.train_step: output_dim 1 only")
@@ -633,10 +636,23 @@ class PNN(KerasModule):
                                  for L in layers))
         grads, delta = _dnn_backward(layers, acts, g.view(B, 1), (ptr(gws), gws.numel()), emp, st)
         w = self.width
+        P = F * (F - 1) // 2
         de = emp(B, F * k)
-        call("rs_inner_product_bwd", ptr(x), w, ptr(delta) + 4 * F * k, w, ptr(delta), w, F, k, B, ptr(de), F * k,
-             st)
+        if self.mode in ("inner", "both"):
+            call("rs_inner_product_bwd", ptr(x), w, ptr(delta) + 4 * F * k, w, ptr(delta), w, F, k, B, ptr(de),
+                 F * k, st)
+        else:
+            de.copy_(delta[:, :F * k])
+        dW = None
+        if self.mode in ("outer", "both"):
+            op = self.outer_product_layer
+            o0 = F * k + (P if self.mode == "both" else 0)  # the outer block's first column
+            dW = emp(*op.W.shape)
+            call("rs_outer_product_bwd", ptr(x), w, ptr(delta) + 4 * o0, w, ptr(op.W), F, k, B, ptr(de), F * k, st)
+            call("rs_outer_product_w_grad", ptr(x), w, ptr(delta) + 4 * o0, w, F, k, B, ptr(dW), st)
         _dnn_apply(grads, lr, st)
+        if dW is not None:
+            call("rs_sgd_update", ptr(self.outer_product_layer.W), ptr(dW), dW.numel(), float(lr), 0.0, st)
         ws_n = _lib.lib().rs_embedding_sgd_workspace_size(B * F)
         ws = self.__dict__.get("_emb_ws")
         if ws is None or ws.numel() < ws_n:

@@ -314,26 +314,34 @@ def test_train_step_dropout_notice(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,k,hidden", [(32, 8, [64, 32]), (300, 16, [256, 128, 64])])
-def test_pnn_train_steps_match_oracle(gpu, B, k, hidden):
-    """PNN.train_step (mode 'inner': the reference's GradientTape loop, its
-    Keras-broadcast BCE on the logit, DNN backward, inner-product backward,
-    SGD, row-sparse embedding SGD) == oracle.pnn_train_step (pinned by finite
-    differences) over 3 steps with repeated rows; the forward then runs on the
-    trained weights."""
+@pytest.mark.parametrize("B,k,hidden,mode", [(32, 8, [64, 32], "inner"), (300, 16, [256, 128, 64], "inner"),
+                                             (64, 8, [64, 32], "outer"), (300, 16, [256, 128, 64], "both")])
+def test_pnn_train_steps_match_oracle(gpu, B, k, hidden, mode):
+    """PNN.train_step (the reference's GradientTape loop, its Keras-broadcast
+    BCE on the logit, DNN backward, inner- and outer-product backward
+    (rs_outer_product_bwd / _w_grad), SGD of the DNN and of W, row-sparse
+    embedding SGD) == oracle.pnn_train_step (pinned by finite differences)
+    over 3 steps with repeated rows, modes 'inner' / 'outer' / 'both'; the
+    forward then runs on the trained weights."""
     import recommender_system_amd as rs
     from tests.helpers import criteo_columns, dnn_params, tables_of
-    rng = np.random.default_rng(B + k)
+    rng = np.random.default_rng(B + k + (0 if mode == "inner" else len(mode)))
     vocab = rng.integers(1, 300, 26)
-    m = rs.PNN(criteo_columns(vocab, embed_dim=k), "inner", hidden, 1, "relu", embed_dim=k, seed=4)
+    m = rs.PNN(criteo_columns(vocab, embed_dim=k), mode, hidden, 1, "relu", embed_dim=k, seed=4)
+    outer = mode in ("outer", "both")
     with torch.no_grad():
         m.embed_layer.table.mul_(8.0)  # O(1) products: visible row updates
         m.dnn_layer.output_layer.bias.fill_(0.5)  # logits inside the clip range
         m.dnn_layer.output_layer.kernel.mul_(0.1)
+        if outer:
+            m.outer_product_layer.W.mul_(4.0)
 
     def params():
         hid, out = dnn_params(m.dnn_layer)
-        return {"tables": tables_of(m.embed_layer), "dnn_hidden": hid, "dnn_out": out}
+        q = {"tables": tables_of(m.embed_layer), "dnn_hidden": hid, "dnn_out": out}
+        if outer:
+            q["outer_W"] = m.outer_product_layer.W.cpu().numpy().astype(np.float64)
+        return q
 
     p = params()
     lr = 0.5
@@ -343,7 +351,7 @@ def test_pnn_train_steps_match_oracle(gpu, B, k, hidden):
         ids[:5, 4] = 0  # repeated rows
         t = rng.integers(0, 2, B).astype(np.float32)
         loss = m.train_step((dense, ids), t, lr=lr, return_loss=True)
-        p, ce = O.pnn_train_step(ids, t, p, lr)
+        p, ce = O.pnn_train_step(ids, t, p, lr, mode=mode)
         got = params()
         assert_scaled_close(loss, ce, what=f"step {step} loss")
         for c in range(26):
@@ -353,8 +361,11 @@ def test_pnn_train_steps_match_oracle(gpu, B, k, hidden):
             assert_scaled_close(b, br, what=f"step {step} b{li}")
         assert_scaled_close(got["dnn_out"][0], p["dnn_out"][0], what=f"step {step} W_out")
         assert_scaled_close(got["dnn_out"][1], p["dnn_out"][1], what=f"step {step} b_out")
+        if outer:
+            assert_scaled_close(got["outer_W"], p["outer_W"], what=f"step {step} outer W")
     y = m((dense, ids))
-    assert_scaled_close(y, O.pnn(None, {**p, "act": "relu"}, inputs=(dense, ids))[0], what="forward after training")
+    assert_scaled_close(y, O.pnn(None, {**p, "act": "relu"}, mode=mode, inputs=(dense, ids))[0],
+                        what="forward after training")
 
 
 @pytest.mark.gpu
