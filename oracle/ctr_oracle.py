@@ -697,11 +697,38 @@ def pnn_loss(ids, t, p, act="relu", dt=np.float64, mode="inner"):
     return pnn_bce(pre, t, dt)[0]
 
 
-def _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt):
+def _dice_train(z, alpha, eps, dt):
+    """Dice.call in training (layer/interaction.py:416-425 under fit): its
+    BatchNormalization(center=False, scale=False) normalises with the batch's
+    mean and biased variance over every axis but the last."""
+    axes = tuple(range(z.ndim - 1))
+    mu, var = z.mean(axes), z.var(axes)
+    zh = (z - mu) / np.sqrt(var + eps)
+    pz = 1.0 / (1.0 + np.exp(-zh))
+    a = np.asarray(alpha, dt)
+    return a * (1.0 - pz) * z + pz * z, (mu, var, zh, pz)
+
+
+def _dice_train_bwd(dy, z, alpha, eps, saved):
+    """dL/dz and dL/dalpha of _dice_train: y = alpha (1-p) z + p z, p =
+    sigmoid(zhat); through zhat the batch-norm backward without gamma."""
+    mu, var, zh, pz = saved
+    axes = tuple(range(z.ndim - 1))
+    a = np.asarray(alpha, dy.dtype)
+    dalpha = (dy * (1.0 - pz) * z).sum(axes)
+    dx = dy * (a * (1.0 - pz) + pz)
+    dzh = dy * (1.0 - a) * z * pz * (1.0 - pz)
+    dx = dx + (dzh - dzh.mean(axes) - zh * (dzh * zh).mean(axes)) / np.sqrt(var + eps)
+    return dx, dalpha
+
+
+def _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt, att_act="prelu", dnn_act="prelu"):
     """DIN.call (model/din.py:56-95) with training=True (Keras fit): the
     BatchNormalization normalises with the batch's own mean and (biased)
-    variance; att 'prelu' and dnn 'prelu' (the reference defaults).  Returns
-    every intermediate the hand backward needs."""
+    variance, and so do the Dice layers' BatchNormalizations (the fit's
+    training flag reaches every nested layer call).  att / dnn activation
+    'prelu' (the reference defaults) or 'dice'.  Returns every intermediate
+    the hand backward needs."""
     c = {}
     dense_in = np.concatenate([cast_inputs(inputs[f], dt).reshape(-1, 1) for f in dense_feats], -1) \
         if dense_feats else None
@@ -723,10 +750,16 @@ def _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt)
     q = np.tile(item[:, None, :], (1, T, 1))
     h = np.concatenate([q, seq, q - seq, q * seq], -1)
     att_pre, att_in = [], [h]
-    for W, b, a in p["att"]["prelu"]:
-        z = np.tensordot(att_in[-1], np.asarray(W, dt), axes=[[2], [0]]) + np.asarray(b, dt)
-        att_pre.append(z)
-        att_in.append(prelu(z, np.asarray(a, dt)))
+    if att_act == "prelu":
+        for W, b, a in p["att"]["prelu"]:
+            z = np.tensordot(att_in[-1], np.asarray(W, dt), axes=[[2], [0]]) + np.asarray(b, dt)
+            att_pre.append(z)
+            att_in.append(prelu(z, np.asarray(a, dt)))
+    else:  # 'dice': len(hidden_units) Dice layers on the 4k-wide concat, no Dense (:363-364)
+        for alpha, _, _, eps in p["att"]["dice"]:
+            y, saved = _dice_train(att_in[-1], alpha, eps, dt)
+            att_pre.append(saved)
+            att_in.append(y)
     score = (np.tensordot(att_in[-1], np.asarray(p["att"]["out"][0], dt), axes=[[2], [0]])
              + np.asarray(p["att"]["out"][1], dt))[..., 0]
     score = np.where(mask, score, dt(np.float32(MASK_FILL)))
@@ -738,26 +771,33 @@ def _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt)
     bmu, bvar = x.mean(0), x.var(0)
     xhat = (x - bmu) / np.sqrt(bvar + eps)
     y = xhat * np.asarray(g, dt) + np.asarray(bt, dt)
-    pre, acts = [], [y]
+    pre, acts, dsaved = [], [y], []
     for W, b, al in p["dnn"]:
         z = acts[-1] @ np.asarray(W, dt) + np.asarray(b, dt)
         pre.append(z)
-        acts.append(prelu(z, np.asarray(al, dt)))
+        if dnn_act == "prelu":
+            acts.append(prelu(z, np.asarray(al, dt)))
+        else:
+            yz, saved = _dice_train(z, al[0], al[3], dt)
+            dsaved.append(saved)
+            acts.append(yz)
     logit = (acts[-1] @ np.asarray(p["out"][0], dt) + np.asarray(p["out"][1], dt))[:, 0]
     c.update(seq=seq, item=item, mask=mask, q=q, att_pre=att_pre, att_in=att_in, a=a, x=x, bmu=bmu, bvar=bvar,
-             xhat=xhat, pre=pre, acts=acts, logit=logit, B=B, T=T, K=K, nd=0 if dense_in is None else
+             xhat=xhat, pre=pre, acts=acts, dsaved=dsaved, logit=logit, B=B, T=T, K=K, nd=0 if dense_in is None else
              dense_in.shape[1], other_sparse=other_sparse)
     return c
 
 
-def din_loss(inputs, t, p, dense_feats, sparse_feats, behavior_feats, dt=np.float64):
+def din_loss(inputs, t, p, dense_feats, sparse_feats, behavior_feats, dt=np.float64, att_act="prelu",
+             dnn_act="prelu"):
     """compile_fit's objective on DIN (training-mode forward): mean BCE."""
-    z = _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt)["logit"]
+    z = _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt, att_act, dnn_act)["logit"]
     t = np.asarray(t, dt).reshape(-1)
     return np.mean(np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z))))
 
 
-def din_train_step(inputs, t, p, dense_feats, sparse_feats, behavior_feats, lr, momentum=0.99, dt=np.float64):
+def din_train_step(inputs, t, p, dense_feats, sparse_feats, behavior_feats, lr, momentum=0.99, dt=np.float64,
+                   att_act="prelu", dnn_act="prelu"):
     """One SGD step of compile_fit on DIN (utils/compile_fit.py:9-15; model/
     din.py:56-95, att 'prelu', dnn 'prelu'), backpropagated by hand:
     BCE on the sigmoid's logit (g = (sigmoid(z) - t)/B); Dense + PReLU layers
@@ -767,8 +807,10 @@ def din_train_step(inputs, t, p, dense_feats, sparse_feats, behavior_feats, lr, 
     averages (momentum 0.99, biased batch variance); the masked softmax pool
     (ds_t = a_t (dv.seq_t - sum_s a_s dv.seq_s)); the [q, k, q-k, q*k] concat
     (dq sums over T); embedding rows by scatter-add.  No regularisers.
-    Returns (new p, per-sample losses before the step)."""
-    c = _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt)
+    Dice (att / dnn 'dice'): training-mode batch statistics in the forward,
+    the batch-norm backward inside its gradient, its moving averages moved
+    like the BN's.  Returns (new p, per-sample losses before the step)."""
+    c = _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt, att_act, dnn_act)
     B, T, K = c["B"], c["T"], c["K"]
     t = np.asarray(t, dt).reshape(-1)
     z = c["logit"]
@@ -781,11 +823,20 @@ def din_train_step(inputs, t, p, dense_feats, sparse_feats, behavior_feats, lr, 
     dh = g[:, None] @ Wo.T
     new_dnn = [None] * len(p["dnn"])
     for li in reversed(range(len(p["dnn"]))):
-        W, b, al = (np.asarray(v, dt) for v in p["dnn"][li])
+        W, b = (np.asarray(v, dt) for v in p["dnn"][li][:2])
         zl = c["pre"][li]
-        dz = dh * np.where(zl > 0, 1.0, al)
-        dal = (dh * np.minimum(zl, 0)).sum(0)
-        new_dnn[li] = (W - lr * (c["acts"][li].T @ dz), b - lr * dz.sum(0), al - lr * dal)
+        if dnn_act == "prelu":
+            al = np.asarray(p["dnn"][li][2], dt)
+            dz = dh * np.where(zl > 0, 1.0, al)
+            dal = (dh * np.minimum(zl, 0)).sum(0)
+            ap_new = al - lr * dal
+        else:
+            al, dmu, dvar, deps = p["dnn"][li][2]
+            dz, dal = _dice_train_bwd(dh, zl, al, deps, c["dsaved"][li])
+            bmu_l, bvar_l = c["dsaved"][li][:2]
+            ap_new = (np.asarray(al, dt) - lr * dal, momentum * np.asarray(dmu, dt) + (1 - momentum) * bmu_l,
+                      momentum * np.asarray(dvar, dt) + (1 - momentum) * bvar_l, deps)
+        new_dnn[li] = (W - lr * (c["acts"][li].T @ dz), b - lr * dz.sum(0), ap_new)
         dh = dz @ W.T
     new["dnn"] = new_dnn
     gam, bet, mu, var, eps = p["bn"]
@@ -806,16 +857,26 @@ def din_train_step(inputs, t, p, dense_feats, sparse_feats, behavior_feats, lr, 
     hl = c["att_in"][-1]
     new_att_out = (Wso - lr * np.tensordot(hl, ds, axes=[[0, 1], [0, 1]])[:, None], bso - lr * np.array([ds.sum()]))
     dh3 = ds[:, :, None] * Wso[:, 0][None, None, :]
-    new_prelu = [None] * len(p["att"]["prelu"])
-    for li in reversed(range(len(p["att"]["prelu"]))):
-        W, b, al = (np.asarray(v, dt) for v in p["att"]["prelu"][li])
-        zl = c["att_pre"][li]
-        dz = dh3 * np.where(zl > 0, 1.0, al)
-        dal = (dh3 * np.minimum(zl, 0)).sum(0)
-        new_prelu[li] = (W - lr * np.tensordot(c["att_in"][li], dz, axes=[[0, 1], [0, 1]]), b - lr * dz.sum((0, 1)),
-                         al - lr * dal)
-        dh3 = np.tensordot(dz, W.T, axes=[[2], [0]])
-    new["att"] = {"prelu": new_prelu, "out": new_att_out}
+    if att_act == "prelu":
+        new_prelu = [None] * len(p["att"]["prelu"])
+        for li in reversed(range(len(p["att"]["prelu"]))):
+            W, b, al = (np.asarray(v, dt) for v in p["att"]["prelu"][li])
+            zl = c["att_pre"][li]
+            dz = dh3 * np.where(zl > 0, 1.0, al)
+            dal = (dh3 * np.minimum(zl, 0)).sum(0)
+            new_prelu[li] = (W - lr * np.tensordot(c["att_in"][li], dz, axes=[[0, 1], [0, 1]]),
+                             b - lr * dz.sum((0, 1)), al - lr * dal)
+            dh3 = np.tensordot(dz, W.T, axes=[[2], [0]])
+        new["att"] = {"prelu": new_prelu, "out": new_att_out}
+    else:
+        new_dice = [None] * len(p["att"]["dice"])
+        for li in reversed(range(len(p["att"]["dice"]))):
+            al, dmu, dvar, deps = p["att"]["dice"][li]
+            saved = c["att_pre"][li]
+            dh3, dal = _dice_train_bwd(dh3, c["att_in"][li], al, deps, saved)
+            new_dice[li] = (np.asarray(al, dt) - lr * dal, momentum * np.asarray(dmu, dt) + (1 - momentum) * saved[0],
+                            momentum * np.asarray(dvar, dt) + (1 - momentum) * saved[1], deps)
+        new["att"] = {"dice": new_dice, "out": new_att_out}
     d0, d1, d2, d3 = (dh3[..., i * K:(i + 1) * K] for i in range(4))
     q = c["q"]
     dq = (d0 + d2 + seq * d3).sum(1)

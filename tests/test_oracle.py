@@ -470,3 +470,56 @@ def test_pnn_train_step_outer_gradient_matches_finite_differences(mode):
     for c, idx in [(0, (0, 0)), (0, (2, 1)), (1, (1, 2)), (2, (3, 0))]:
         check(p["tables"][c], new["tables"][c], idx)
     check(p["dnn_hidden"][0][0], new["dnn_hidden"][0][0], (w - 1, 2))
+
+
+@pytest.mark.parametrize("att_act,dnn_act", [("dice", "prelu"), ("prelu", "dice"), ("dice", "dice")])
+def test_din_train_step_dice_gradient_matches_finite_differences(att_act, dnn_act):
+    """The same with Dice (layer/interaction.py:410-425) in the attention
+    (len(hidden) Dice layers on the 4k-wide concat, no Dense) and / or the DNN
+    (Dense(unit, activation=Dice())): training-mode batch statistics inside
+    Dice, its BatchNormalization backward, the alphas; the Dice moving
+    averages move toward the batch mean / biased variance."""
+    rng = np.random.default_rng(8)
+    inputs, t, p, dense, sparse, beh = _din_small(rng)
+    K = 4
+    if att_act == "dice":
+        p["att"] = {"dice": [(rng.normal(size=4 * K) * 0.3, np.zeros(4 * K), np.ones(4 * K), 1e-9) for _ in range(2)],
+                    "out": (rng.normal(size=(4 * K, 1)), np.array([0.1]))}
+    if dnn_act == "dice":
+        p["dnn"] = [(W, b, (rng.normal(size=b.shape[0]) * 0.3, np.zeros(b.shape[0]), np.ones(b.shape[0]), 1e-9))
+                    for W, b, _ in p["dnn"]]
+    lr = 1.0
+    kw = dict(att_act=att_act, dnn_act=dnn_act)
+    new, _ = O.din_train_step(inputs, t, p, dense, sparse, beh, lr, **kw)
+    eps = 1e-6
+
+    def check(get, idx, get_new):
+        arr = get(p)
+        keep = arr[idx]
+        arr[idx] = keep + eps
+        lp = O.din_loss(inputs, t, p, dense, sparse, beh, **kw)
+        arr[idx] = keep - eps
+        lm = O.din_loss(inputs, t, p, dense, sparse, beh, **kw)
+        arr[idx] = keep
+        fd = (lp - lm) / (2 * eps)
+        got = (arr[idx] - get_new(new)[idx]) / lr
+        assert abs(fd - got) < 1e-5 * max(1.0, abs(fd)), (idx, fd, got)
+
+    for f in beh:
+        for idx in [(0, 0), (2, 1), (5, 1)]:
+            check(lambda q, f=f: q["seq_tables"][f], idx, lambda q, f=f: q["seq_tables"][f])
+    check(lambda q: q["sparse_tables"]["u"], (1, 2), lambda q: q["sparse_tables"]["u"])
+    if att_act == "dice":
+        for li in range(2):
+            for idx in [(1,), (9,), (14,)]:
+                check(lambda q, li=li: q["att"]["dice"][li][0], idx, lambda q, li=li: q["att"]["dice"][li][0])
+        saved = O._din_train_forward(inputs, p, dense, sparse, beh, np.float64, **kw)["att_pre"][0]
+        np.testing.assert_allclose(new["att"]["dice"][0][1], 0.01 * saved[0], rtol=1e-12)
+    check(lambda q: q["att"]["out"][0], (1, 0), lambda q: q["att"]["out"][0])
+    for li in range(2):
+        check(lambda q, li=li: q["dnn"][li][0], (0, 1), lambda q, li=li: q["dnn"][li][0])
+        check(lambda q, li=li: q["dnn"][li][1], (2,), lambda q, li=li: q["dnn"][li][1])
+        if dnn_act == "dice":
+            check(lambda q, li=li: q["dnn"][li][2][0], (1,), lambda q, li=li: q["dnn"][li][2][0])
+    for j, idx in [(0, (2,)), (1, (4,))]:
+        check(lambda q, j=j: q["bn"][j], idx, lambda q, j=j: q["bn"][j])
