@@ -534,6 +534,26 @@ int rs_bn_train_bwd(const float* x, int64_t x_stride, int64_t batch, int D,
                     float eps, const float* dy, int64_t dy_stride, float* dx,
                     int64_t dx_stride, float* dgamma, float* dbeta,
                     rs_stream_t stream);
+/* Dice in training (layer/interaction.py:416-425 under fit, DIN with
+ * att_attention / dnn_activation 'dice'), x [M, N] dense rows (the
+ * attention's [B, T, 4k] as [B*T, 4k]): its BatchNormalization(center=False,
+ * scale=False) with the batch's per-column mean and biased variance (into
+ * mean / var, moving averages moved with momentum when non-NULL);
+ * y = alpha (1 - p) x + p x, p = sigmoid((x - mean) rsqrt(var + eps)).
+ * rs_dice_train_bwd: dx = dy (alpha (1-p) + p) + the batch-norm backward of
+ * dL/dxhat = dy (1 - alpha) x p (1 - p); dalpha = sum dy (1 - p) x.
+ * Workspace: rs_dice_train_workspace_size(M, N) bytes.  Deterministic.     */
+int64_t rs_dice_train_workspace_size(int64_t M, int N);
+int rs_dice_train_fwd(const float* x, int64_t M, int N, const float* alpha,
+                      float eps, float momentum, float* moving_mean,
+                      float* moving_var, float* mean, float* var, float* y,
+                      void* workspace, int64_t workspace_bytes,
+                      rs_stream_t stream);
+int rs_dice_train_bwd(const float* x, int64_t M, int N, const float* alpha,
+                      const float* mean, const float* var, float eps,
+                      const float* dy, float* dx, float* dalpha,
+                      void* workspace, int64_t workspace_bytes,
+                      rs_stream_t stream);
 /* rs_head_grad with g = scale (sigmoid(z) - t) (scale > 0): the sharded
  * DeepFM step's local batch is a 1/world share of the global batch mean,
  * scale = 1 / (world * batch).                                             */

@@ -93,6 +93,9 @@ SIGNATURES = {
     "rs_masked_softmax_pool": (I, [P, P, I, L, P, L, I, I, P, P, L, P]),
     "rs_masked_softmax_pool_bwd": (I, [P, P, I, L, P, P, L, L, I, I, P, P, P]),
     "rs_bn_train_fwd": (I, [P, L, L, I, P, P, F, F, P, P, P, P, P, L, P]),
+    "rs_dice_train_workspace_size": (L, [L, I]),
+    "rs_dice_train_fwd": (I, [P, L, I, P, F, F, P, P, P, P, P, P, L, P]),
+    "rs_dice_train_bwd": (I, [P, L, I, P, P, P, F, P, P, P, P, L, P]),
     "rs_bn_train_bwd": (I, [P, L, L, I, P, P, P, F, P, L, P, L, P, P, P]),
     "rs_scatter_rows": (I, [P, L, I, I, P, L, P, P]),
     "rs_shard_dedup_workspace_size": (L, [L, I]),

@@ -321,6 +321,88 @@ __global__ __launch_bounds__(256) void bn_bwd_kernel(const float* __restrict__ x
   }
 }
 
+// ---- Dice in training (layer/interaction.py:416-425 under fit): its
+// BatchNormalization(center=False, scale=False) uses the batch's mean and
+// biased variance per column (every row of [M, N]); y = alpha (1-p) x + p x,
+// p = sigmoid(xhat).  Column statistics through the split column sums
+// (rs_col_sum_split: fixed slice order), the rest elementwise.
+__global__ __launch_bounds__(256) void dice_sq_kernel(const float* __restrict__ x, int64_t M, int N,
+                                                      const float* __restrict__ sum, float* __restrict__ sq) {
+  const int64_t n = M * (int64_t)N;
+  const float inv = 1.f / (float)M;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % N);
+    const float d = x[i] - sum[c] * inv;
+    sq[i] = d * d;
+  }
+}
+
+// sums -> mean / var (biased); moving averages with momentum
+__global__ __launch_bounds__(256) void dice_stats_kernel(int64_t M, int N, float momentum, float* __restrict__ mean,
+                                                         float* __restrict__ var, float* __restrict__ mov_mean,
+                                                         float* __restrict__ mov_var) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= N) return;
+  const float mu = mean[c] / (float)M, v = var[c] / (float)M;
+  mean[c] = mu;
+  var[c] = v;
+  if (mov_mean) mov_mean[c] = momentum * mov_mean[c] + (1.f - momentum) * mu;
+  if (mov_var) mov_var[c] = momentum * mov_var[c] + (1.f - momentum) * v;
+}
+
+__global__ __launch_bounds__(256) void dice_apply_kernel(const float* __restrict__ x, int64_t M, int N,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ var, float eps,
+                                                         const float* __restrict__ alpha, float* __restrict__ y) {
+  const int64_t n = M * (int64_t)N;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % N);
+    const float v = x[i];
+    const float pz = 1.f / (1.f + expf(-(v - mean[c]) * rsqrtf(var[c] + eps)));
+    y[i] = alpha[c] * (1.f - pz) * v + pz * v;
+  }
+}
+
+// backward, elementwise part: dx = dy (alpha (1-p) + p); dxh = dy (1-alpha) x
+// p (1-p) (dL/dxhat); dxh * xhat; prod = dy (1-p) x (dalpha = its column sums)
+__global__ __launch_bounds__(256) void dice_bwd_elem_kernel(const float* __restrict__ x, int64_t M, int N,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ var, float eps,
+                                                            const float* __restrict__ alpha,
+                                                            const float* __restrict__ dy, float* __restrict__ dx,
+                                                            float* __restrict__ dxh, float* __restrict__ dxhx,
+                                                            float* __restrict__ prod) {
+  const int64_t n = M * (int64_t)N;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % N);
+    const float v = x[i], g = dy[i], a = alpha[c];
+    const float xh = (v - mean[c]) * rsqrtf(var[c] + eps);
+    const float pz = 1.f / (1.f + expf(-xh));
+    dx[i] = g * (a * (1.f - pz) + pz);
+    const float d = g * (1.f - a) * v * pz * (1.f - pz);
+    dxh[i] = d;
+    dxhx[i] = d * xh;
+    prod[i] = g * (1.f - pz) * v;
+  }
+}
+
+// dx += (dxh - S1/M - xhat S2/M) rsqrt(var + eps)   (batch-norm backward, no gamma)
+__global__ __launch_bounds__(256) void dice_bwd_fin_kernel(const float* __restrict__ x, int64_t M, int N,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ var, float eps,
+                                                           const float* __restrict__ dxh,
+                                                           const float* __restrict__ s1,
+                                                           const float* __restrict__ s2, float* __restrict__ dx) {
+  const int64_t n = M * (int64_t)N;
+  const float inv = 1.f / (float)M;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % N);
+    const float is = rsqrtf(var[c] + eps);
+    const float xh = (x[i] - mean[c]) * is;
+    dx[i] += (dxh[i] - s1[c] * inv - xh * s2[c] * inv) * is;
+  }
+}
+
 static unsigned dt_grid(int64_t n) {
   int64_t g = (n + 255) / 256;
   return (unsigned)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
@@ -440,4 +522,60 @@ extern "C" int rs_bn_train_bwd(const float* x, int64_t x_stride, int64_t batch, 
   bn_bwd_kernel<<<(unsigned)D, 256, 0, as_stream(stream)>>>(x, x_stride, batch, mean, var, gamma, eps, dy, dy_stride,
                                                             dx, dx_stride, dgamma, dbeta);
   return launch_status("rs_bn_train_bwd");
+}
+
+static int64_t dt_al(int64_t b) { return (b + 255) / 256 * 256; }
+
+extern "C" int64_t rs_dice_train_workspace_size(int64_t M, int N) {
+  if (M < 0 || N < 1) return -1;
+  return 3 * dt_al(M * N * 4) + 2 * dt_al((int64_t)N * 4) + dt_al(rs_col_sum_workspace_size(M, N));
+}
+
+extern "C" int rs_dice_train_fwd(const float* x, int64_t M, int N, const float* alpha, float eps, float momentum,
+                                 float* moving_mean, float* moving_var, float* mean, float* var, float* y,
+                                 void* workspace, int64_t workspace_bytes, rs_stream_t stream) {
+  if (M == 0) return RS_OK;
+  RS_REQUIRE(x && alpha && mean && var && y && workspace && M > 0 && N >= 1 && mean != var,
+             "rs_dice_train_fwd: bad arguments");
+  RS_REQUIRE(workspace_bytes >= rs_dice_train_workspace_size(M, N), "rs_dice_train_fwd: workspace too small");
+  hipStream_t st = as_stream(stream);
+  uint8_t* ws = static_cast<uint8_t*>(workspace);
+  float* sq = reinterpret_cast<float*>(ws);
+  uint8_t* cws = ws + 3 * dt_al(M * N * 4) + 2 * dt_al((int64_t)N * 4);
+  const int64_t cb = rs_col_sum_workspace_size(M, N);
+  int rc = rs_col_sum_split(x, N, M, N, mean, cws, cb, stream);  // column sums
+  if (rc != RS_OK) return rc;
+  dice_sq_kernel<<<dt_grid(M * (int64_t)N), 256, 0, st>>>(x, M, N, mean, sq);
+  rc = rs_col_sum_split(sq, N, M, N, var, cws, cb, stream);
+  if (rc != RS_OK) return rc;
+  dice_stats_kernel<<<(unsigned)((N + 255) / 256), 256, 0, st>>>(M, N, momentum, mean, var, moving_mean, moving_var);
+  dice_apply_kernel<<<dt_grid(M * (int64_t)N), 256, 0, st>>>(x, M, N, mean, var, eps, alpha, y);
+  return launch_status("rs_dice_train_fwd");
+}
+
+extern "C" int rs_dice_train_bwd(const float* x, int64_t M, int N, const float* alpha, const float* mean,
+                                 const float* var, float eps, const float* dy, float* dx, float* dalpha,
+                                 void* workspace, int64_t workspace_bytes, rs_stream_t stream) {
+  if (M == 0) return RS_OK;
+  RS_REQUIRE(x && alpha && mean && var && dy && dx && dalpha && workspace && M > 0 && N >= 1 && dx != dy,
+             "rs_dice_train_bwd: bad arguments");
+  RS_REQUIRE(workspace_bytes >= rs_dice_train_workspace_size(M, N), "rs_dice_train_bwd: workspace too small");
+  hipStream_t st = as_stream(stream);
+  uint8_t* ws = static_cast<uint8_t*>(workspace);
+  const int64_t slab = dt_al(M * N * 4);
+  float* dxh = reinterpret_cast<float*>(ws);
+  float* dxhx = reinterpret_cast<float*>(ws + slab);
+  float* prod = reinterpret_cast<float*>(ws + 2 * slab);
+  float* s1 = reinterpret_cast<float*>(ws + 3 * slab);
+  float* s2 = reinterpret_cast<float*>(ws + 3 * slab + dt_al((int64_t)N * 4));
+  uint8_t* cws = ws + 3 * slab + 2 * dt_al((int64_t)N * 4);
+  const int64_t cb = rs_col_sum_workspace_size(M, N);
+  dice_bwd_elem_kernel<<<dt_grid(M * (int64_t)N), 256, 0, st>>>(x, M, N, mean, var, eps, alpha, dy, dx, dxh, dxhx,
+                                                                prod);
+  int rc = rs_col_sum_split(dxh, N, M, N, s1, cws, cb, stream);
+  if (rc == RS_OK) rc = rs_col_sum_split(dxhx, N, M, N, s2, cws, cb, stream);
+  if (rc == RS_OK) rc = rs_col_sum_split(prod, N, M, N, dalpha, cws, cb, stream);
+  if (rc != RS_OK) return rc;
+  dice_bwd_fin_kernel<<<dt_grid(M * (int64_t)N), 256, 0, st>>>(x, M, N, mean, var, eps, dxh, s1, s2, dx);
+  return launch_status("rs_dice_train_bwd");
 }

@@ -187,8 +187,11 @@ struct EmbedFmArgs {
 // TW: fused DeepFM — x goes to an LDS tile ([emb F*k | dense nd | 0-pad],
 // row stride tw->rs) instead of x_out, and the DNN tower of mlp_tower.hpp runs
 // on it, closed by sigmoid(c0*dnn + c1*fm) (model/deepFM.py:24-30).
-template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0>
+// TS: samples per workgroup (16 = one MFMA row tile; 8 = the tile's rows
+// 8..15 repeat rows 0..7, two workgroups per CU at batch 4096)
+template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, int TS = 16>
 __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArgs* tw, const int tile) {
+  static_assert(TS == 16 || (TS == 8 && !TW && KIND != 4), "8-sample tiles: plain FM kernel only");
   // MC > 0: field slots per wave and pass (owner kernels with few fields)
   constexpr int MAXC0 = MC > 0 ? MC : 128 / (NW * KV);
   constexpr int MAXC = MAXC0 < 1 ? 1 : (MAXC0 > 8 ? 8 : MAXC0);
@@ -201,11 +204,12 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int s = lane & 15;   // A: sample row of the tile; B/C: column
   const int kk = lane >> 4;  // k-slot
-  const int64_t bt = (int64_t)tile * 16 + s;
-  const bool valid = bt < a.batch;
-  // Padded lanes of the last tile recompute the last sample: an MFMA output
-  // row depends only on its own A row, so they never touch valid outputs.
-  const int64_t b = valid ? bt : a.batch - 1;
+  const int64_t bt = (int64_t)tile * TS + (s % TS);
+  const bool valid = s < TS && bt < a.batch;
+  // Padded lanes of the last tile recompute the last sample (and with TS = 8
+  // rows 8..15 repeat rows 0..7): an MFMA output row depends only on its own
+  // A row, so they never touch valid outputs.
+  const int64_t b = bt < a.batch ? bt : a.batch - 1;
   const int d = a.nd + a.F * a.k;
 
   floatx4 acc[NT];
@@ -275,8 +279,8 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   const bool coop = (KIND != 3) && a.F <= FMAX;
 #endif
   if (coop) {
-    const int64_t b0 = (int64_t)tile * 16;
-    for (int t = threadIdx.x; t < 16 * a.F; t += NW * 64) {
+    const int64_t b0 = (int64_t)tile * TS;
+    for (int t = threadIdx.x; t < TS * a.F; t += NW * 64) {
       const int ss = t / a.F, c = t - ss * a.F;
       const int64_t bb = b0 + ss < a.batch ? b0 + ss : a.batch - 1;
       const auto idv = I::load(a.ids, bb * a.id_stride + c);
@@ -317,11 +321,11 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
         if (OWNER) {
           offc[j] = 0;
           vocc[j] = a.owner_rows;
-          rid[j] = coop ? lid[s][cj[j]] : I::load(a.ids, b * a.id_stride + cj[j]);
+          rid[j] = coop ? lid[s % TS][cj[j]] : I::load(a.ids, b * a.id_stride + cj[j]);
         } else if (coop) {
           offc[j] = lmeta[0][cj[j]];
           vocc[j] = lmeta[1][cj[j]];
-          rid[j] = lid[s][cj[j]];
+          rid[j] = lid[s % TS][cj[j]];
         } else {
           const int cv = min(cg + j * NW + wv, a.F - 1);
           offc[j] = a.offs[cv];
@@ -479,7 +483,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       t += __shfl_xor(t, 16);
       lin += __shfl_xor(lin, 16);
     }
-    const int64_t bb = (int64_t)tile * 16 + smp;
+    const int64_t bb = (int64_t)tile * TS + smp;
     if constexpr (OWNER) {
       // partial record: column sums as they stand, the q term row-summed
       float q = col < NW ? qs[col][smp] : 0.f;
@@ -494,7 +498,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       return;
     }
     const float fm = (lin + a.w0[0]) + 0.5f * t;
-    if (col == 0 && bb < a.batch && a.logit) a.logit[bb] = fm;
+    if (col == 0 && smp < TS && bb < a.batch && a.logit) a.logit[bb] = fm;
     if constexpr (TW) {
       if (col == 0) fmlog[smp] = fm;
     }
@@ -503,9 +507,9 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   if constexpr (TW) mlp_tower_tile<NW>(*tw, tsm, (int64_t)tile * 16, ring, fmlog);
 }
 
-template <int KV, int NT, int NW, int KIND, int MC>
+template <int KV, int NT, int NW, int KIND, int MC, int TS = 16>
 __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
-  embed_fm_body<KV, NT, NW, KIND, false, MC>(a, nullptr, blockIdx.x);
+  embed_fm_body<KV, NT, NW, KIND, false, MC, TS>(a, nullptr, blockIdx.x);
 }
 
 // ---- sharded FM, partial protocol: combine (requester side) as a block part
@@ -785,9 +789,13 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st) {
   // (16 + 10), 6.05 us per launch against 6.54 with both in one pass (2 slots
   // per wave) — the second pass's row requests queue behind a shorter first
   // wave of 256 rows per CU.  More than 32 fields: 2 slots per pass.
-  const int grid = (int)((a.batch + 15) / 16);
-  if (a.F <= 32) embed_fm_mfma<KV, NT, 16, KIND, 1><<<grid, 16 * 64, 0, st>>>(a);
-  else embed_fm_mfma<KV, NT, 16, KIND, 0><<<grid, 16 * 64, 0, st>>>(a);
+#ifndef RS_EMBED_TS
+#define RS_EMBED_TS 16
+#endif
+  constexpr int TS = RS_EMBED_TS;
+  const int grid = (int)((a.batch + TS - 1) / TS);
+  if (a.F <= 32) embed_fm_mfma<KV, NT, 16, KIND, 1, TS><<<grid, 16 * 64, 0, st>>>(a);
+  else embed_fm_mfma<KV, NT, 16, KIND, 0, TS><<<grid, 16 * 64, 0, st>>>(a);
 }
 
 template <int KIND>

@@ -764,8 +764,9 @@ class DIN(TowerMixin, KerasModule):
         fit, SGD(lr), binary_crossentropy on the sigmoid output — Keras takes
         the sigmoid's logit) with DIN.call in training mode (model/din.py:
         56-95): BatchNormalization normalises with the batch's own mean and
-        biased variance and moves its averages (momentum 0.99).  att_attention
-        and dnn_activation 'prelu' (the reference defaults).
+        biased variance and moves its averages (momentum 0.99), and so do
+        the Dice layers' BatchNormalizations (att_attention / dnn_activation
+        'prelu' — the reference defaults — or 'dice': rs_dice_train_fwd/_bwd).
           forward: behaviour / candidate rows (rs_embed_gather), the
           attention input [q, k, q-k, q*k] (rs_din_att_concat), each
           attention Dense (rs_dense_fwd) + PReLU over [T, h] alphas
@@ -781,8 +782,6 @@ class DIN(TowerMixin, KerasModule):
         _dropout_notice).  Returns per-sample losses (before the step) if
         ``return_loss``."""
         att, bn = self.att_layer, self.bn_layer
-        if att.activation != "prelu" or any(L.activation != "prelu" for L in self.dense_layer):
-            raise NotImplementedError("DIN.train_step: att_attention 'prelu' and dnn_activation 'prelu' only")
         _dropout_notice("DIN", self, dropout)
         dev, st = self._dev, _lib.stream()
         nb = len(self.seq_feats)
@@ -811,6 +810,8 @@ class DIN(TowerMixin, KerasModule):
                     lb.rs_col_sum_workspace_size(m, n)) for kin, n, m in shapes]
         need += [lb.rs_prelu_rows_bwd_workspace_size(M, W.shape[1], T) for W in att.kernels]
         need += [lb.rs_prelu_rows_bwd_workspace_size(B, L.units, 1) for L in self.dense_layer]
+        need += [lb.rs_dice_train_workspace_size(M, 4 * K)] if att.activation == "dice" else []
+        need += [lb.rs_dice_train_workspace_size(B, L.units) for L in self.dense_layer if L.activation == "dice"]
         gws = _gemm_ws(self, max(need))
         gw = (ptr(gws), gws.numel())
 
@@ -823,6 +824,14 @@ class DIN(TowerMixin, KerasModule):
         h0 = emp(M, 4 * K)
         call("rs_din_att_concat", ptr(item), ptr(seq), B, T, K, ptr(h0), st)
         att_in, att_pre = [h0], []
+
+        def dice_fwd(d, x, m, n):
+            # Dice under fit: batch statistics (kept for the backward), moving averages moved
+            mu, vr, y = emp(n), emp(n), emp(m, n)
+            call("rs_dice_train_fwd", ptr(x), m, n, ptr(d.alphas), d.epsilon, 0.99, ptr(d.moving_mean),
+                 ptr(d.moving_variance), ptr(mu), ptr(vr), ptr(y), *gw, st)
+            return (mu, vr), y
+
         for W, b, al in zip(att.kernels, att.biases, att.alphas):
             n = W.shape[1]
             z, y = emp(M, n), emp(M, n)
@@ -830,6 +839,10 @@ class DIN(TowerMixin, KerasModule):
                  ptr(z), n, M, W.shape[0], n, st)
             call("rs_prelu_rows_fwd", ptr(z), M, n, ptr(al), T, ptr(y), st)
             att_pre.append(z)
+            att_in.append(y)
+        for d in att.dice:  # att_attention 'dice': Dice layers on the 4k-wide concat, no Dense
+            saved, y = dice_fwd(d, att_in[-1], M, 4 * K)
+            att_pre.append(saved)
             att_in.append(y)
         score = emp(M)
         hl = att_in[-1]
@@ -853,12 +866,17 @@ class DIN(TowerMixin, KerasModule):
         mean, var, y0 = emp(width), emp(width), emp(B, width)
         call("rs_bn_train_fwd", ptr(x), width, B, width, ptr(bn.gamma), ptr(bn.beta), bn.epsilon, 0.99,
              ptr(bn.moving_mean), ptr(bn.moving_variance), ptr(mean), ptr(var), ptr(y0), width, st)
-        acts, pre = [y0], []
+        acts, pre, dsaved = [y0], [], []
         for L in self.dense_layer:
             z, y = emp(B, L.units), emp(B, L.units)
             call("rs_dense_fwd", ptr(acts[-1]), acts[-1].stride(0), ptr(L.kernel), ptr(L.bias), None,
                  _lib.ACT[None], ptr(z), L.units, B, L.kernel.shape[0], L.units, st)
-            call("rs_prelu_rows_fwd", ptr(z), B, L.units, ptr(L.alpha), 1, ptr(y), st)
+            if L.activation == "dice":
+                saved, y = dice_fwd(L.dice, z, B, L.units)
+                dsaved.append(saved)
+            else:
+                call("rs_prelu_rows_fwd", ptr(z), B, L.units, ptr(L.alpha), 1, ptr(y), st)
+                dsaved.append(None)
             pre.append(z)
             acts.append(y)
         out = self.out_layer
@@ -890,10 +908,21 @@ class DIN(TowerMixin, KerasModule):
             updates.append((alpha, dal))
             return dz
 
+        def dice_back(d, x, saved, dy, m, n):
+            dx, dal = emp(m, n), emp(n)
+            call("rs_dice_train_bwd", ptr(x), m, n, ptr(d.alphas), ptr(saved[0]), ptr(saved[1]), d.epsilon, ptr(dy),
+                 ptr(dx), ptr(dal), *gw, st)
+            updates.append((d.alphas, dal))
+            return dx
+
         dh = dense_back(out.kernel, out.bias, acts[-1], g.view(B, 1), B)
         for li in reversed(range(len(self.dense_layer))):
             L = self.dense_layer[li]
-            dh = dense_back(L.kernel, L.bias, acts[li], prelu_back(pre[li], dh, L.alpha, 1, B), B)
+            if L.activation == "dice":
+                dz = dice_back(L.dice, pre[li], dsaved[li], dh, B, L.units)
+            else:
+                dz = prelu_back(pre[li], dh, L.alpha, 1, B)
+            dh = dense_back(L.kernel, L.bias, acts[li], dz, B)
         dx, dgam, dbet = emp(B, width), emp(width), emp(width)
         call("rs_bn_train_bwd", ptr(x), width, B, width, ptr(mean), ptr(var), ptr(bn.gamma), bn.epsilon, ptr(dh),
              dh.stride(0), ptr(dx), width, ptr(dgam), ptr(dbet), st)
@@ -905,6 +934,8 @@ class DIN(TowerMixin, KerasModule):
         for li in reversed(range(len(att.kernels))):
             dz = prelu_back(att_pre[li], dh3, att.alphas[li], T, M)
             dh3 = dense_back(att.kernels[li], att.biases[li], att_in[li], dz, M)
+        for li in reversed(range(len(att.dice))):
+            dh3 = dice_back(att.dice[li], att_in[li], att_pre[li], dh3, M, 4 * K)
         call("rs_din_att_concat_bwd", ptr(dh3), ptr(item), ptr(seq), B, T, K, ptr(dx) + 4 * K, width, ptr(dseq), st)
 
         # ---- SGD

@@ -175,25 +175,38 @@ def test_oracle_din_two_behaviours_is_concat():
     np.testing.assert_allclose(a[0], seq[0].mean(0), rtol=1e-12)  # fully padded row: uniform average
 
 
+def _cp(x):
+    if isinstance(x, np.ndarray):
+        return x.copy()
+    if isinstance(x, tuple):
+        return tuple(_cp(y) for y in x)
+    return x
+
+
 def _din_train_params(model):
     p = din_params(model)
+    att = {k_: [_cp(l) for l in v] for k_, v in p["att"].items() if k_ != "out"}
+    att["out"] = _cp(p["att"]["out"])
     return {"sparse_tables": {f: v.copy() for f, v in p["sparse_tables"].items()},
             "seq_tables": {f: v.copy() for f, v in p["seq_tables"].items()},
-            "att": {"prelu": [tuple(x.copy() for x in l) for l in p["att"]["prelu"]],
-                    "out": tuple(x.copy() for x in p["att"]["out"])},
-            "bn": tuple(x.copy() if isinstance(x, np.ndarray) else x for x in p["bn"]),
-            "dnn": [tuple(x.copy() for x in l) for l in p["dnn"]], "out": tuple(x.copy() for x in p["out"])}
+            "att": att, "bn": _cp(p["bn"]), "dnn": [_cp(l) for l in p["dnn"]], "out": _cp(p["out"])}
 
 
 def _flat_params(p):
     out = {f"sparse/{f}": v for f, v in p["sparse_tables"].items()}
     out.update({f"seq/{f}": v for f, v in p["seq_tables"].items()})
-    for i, l in enumerate(p["att"]["prelu"]):
+    for i, l in enumerate(p["att"].get("prelu", [])):
         out.update({f"att{i}/W": l[0], f"att{i}/b": l[1], f"att{i}/alpha": l[2]})
+    for i, l in enumerate(p["att"].get("dice", [])):
+        out.update({f"att_dice{i}/alpha": l[0], f"att_dice{i}/mean": l[1], f"att_dice{i}/var": l[2]})
     out.update({"att_out/W": p["att"]["out"][0], "att_out/b": p["att"]["out"][1]})
     out.update({f"bn/{n}": v for n, v in zip(("gamma", "beta", "mean", "var"), p["bn"][:4])})
     for i, l in enumerate(p["dnn"]):
-        out.update({f"dnn{i}/W": l[0], f"dnn{i}/b": l[1], f"dnn{i}/alpha": l[2]})
+        out.update({f"dnn{i}/W": l[0], f"dnn{i}/b": l[1]})
+        if isinstance(l[2], tuple):  # Dice: alpha, moving mean, moving var
+            out.update({f"dnn{i}/alpha": l[2][0], f"dnn{i}/mean": l[2][1], f"dnn{i}/var": l[2][2]})
+        else:
+            out[f"dnn{i}/alpha"] = l[2]
     out.update({"out/W": p["out"][0], "out/b": p["out"][1]})
     return out
 
@@ -213,12 +226,14 @@ def _assert_update_close(got, ref, before, rtol=2e-3, what=""):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("att_hidden,dnn_hidden,nb,k,B,T", [
-    ((80, 40), (256, 128, 64), 1, 8, 256, 20),   # the reference defaults
-    ((80, 40), (64, 32), 2, 8, 192, 30),         # item + category behaviour features (K = 16)
-    ((32,), (16,), 2, 4, 64, 7),                 # one attention layer, small ragged T
+@pytest.mark.parametrize("att_hidden,dnn_hidden,nb,k,B,T,att_act,dnn_act", [
+    ((80, 40), (256, 128, 64), 1, 8, 256, 20, "prelu", "prelu"),   # the reference defaults
+    ((80, 40), (64, 32), 2, 8, 192, 30, "prelu", "prelu"),         # item + category behaviour features (K = 16)
+    ((32,), (16,), 2, 4, 64, 7, "prelu", "prelu"),                 # one attention layer, small ragged T
+    ((80, 40), (64, 32), 1, 8, 256, 20, "prelu", "dice"),          # dnn_activation='dice'
+    ((80, 40), (64, 32), 2, 8, 128, 30, "dice", "dice"),           # att_attention='dice' too
 ])
-def test_din_train_steps_match_oracle(gpu, att_hidden, dnn_hidden, nb, k, B, T):
+def test_din_train_steps_match_oracle(gpu, att_hidden, dnn_hidden, nb, k, B, T, att_act, dnn_act):
     """DIN.train_step (compile_fit on DIN in training mode: batch-statistics
     BatchNormalization with moving averages, PReLU attention over [T, h]
     alphas, masked softmax pool, PReLU DNN, SGD + row-sparse embedding SGD)
@@ -229,7 +244,8 @@ def test_din_train_steps_match_oracle(gpu, att_hidden, dnn_hidden, nb, k, B, T):
     from recommender_system_amd import DIN
     rng = np.random.default_rng(B + T + nb)
     cols, behaviour = din_columns(nb, k, item_vocab=40, cate_vocab=9, user_vocab=17)
-    model = DIN(cols, behaviour, att_hidden_units=att_hidden, dnn_hidden_units=dnn_hidden, seed=3)
+    model = DIN(cols, behaviour, att_hidden_units=att_hidden, dnn_hidden_units=dnn_hidden, att_attention=att_act,
+                dnn_activation=dnn_act, seed=3)
     inputs = din_inputs(rng, cols, behaviour, B, T)
     model(inputs)
     randomize(model, rng)
@@ -243,7 +259,7 @@ def test_din_train_steps_match_oracle(gpu, att_hidden, dnn_hidden, nb, k, B, T):
         t = rng.integers(0, 2, B).astype(np.float32)
         before = _flat_params(_din_train_params(model))
         loss = model.train_step(inputs, t, lr=lr, return_loss=True)
-        p, ce = O.din_train_step(inputs, t, p, dense_f, sparse_f, beh, lr)
+        p, ce = O.din_train_step(inputs, t, p, dense_f, sparse_f, beh, lr, att_act=att_act, dnn_act=dnn_act)
         got = _flat_params(_din_train_params(model))
         ref = _flat_params(p)
         assert_scaled_close(loss, ce, rtol=1e-4, what=f"step {step} loss")
@@ -252,5 +268,5 @@ def test_din_train_steps_match_oracle(gpu, att_hidden, dnn_hidden, nb, k, B, T):
         p = _din_train_params(model)  # next step from the same fp32 point
     # the inference forward on the trained weights (packed attention images
     # rebuilt after the raw-pointer updates; BN on the moved averages)
-    ref, _ = O.din(inputs, din_params(model), dense_f, sparse_f, beh)
+    ref, _ = O.din(inputs, din_params(model), dense_f, sparse_f, beh, att_act=att_act, dnn_act=dnn_act)
     assert_rel_close(model(inputs), ref, what="forward after training")
