@@ -321,37 +321,45 @@ __global__ __launch_bounds__(256) void fm_x_grad_kernel(const float* __restrict_
   else dx[b * lddx + i] = r;
 }
 
-// FM parameter gradients (without the l2 terms): one block per feature i,
-// fixed-shape trees over the batch:
+// FM parameter gradients (without the l2 terms), kfm <= KF: one block per
+// feature i (block d: dw0 = sum_b g_b), fixed-shape trees over the batch,
 //   dw1_i = sum_b g_b x_bi,  dv_if = sum_b g_b x_bi s_bf - (sum_b g_b x_bi^2) v_if;
-// block d computes dw0 = sum_b g_b (when dw0 is given).
-__global__ __launch_bounds__(256) void fm_param_grad_kernel(const float* __restrict__ x, int64_t ldx,
-                                                            const float* __restrict__ s, int64_t lds,
-                                                            const float* __restrict__ v, int64_t B, int d, int kfm,
-                                                            const float* __restrict__ g, int64_t ldg,
-                                                            float* __restrict__ dw1, float* __restrict__ dv,
-                                                            float* __restrict__ dw0) {
-  __shared__ float red[34][256];
+// KF is a compile-time bound so the KF + 2 partial sums stay in registers
+template <int KF>
+__global__ __launch_bounds__(256) void fm_param_grad_col(const float* __restrict__ x, int64_t ldx,
+                                                         const float* __restrict__ s, int64_t lds,
+                                                         const float* __restrict__ v, int64_t B, int d, int kfm,
+                                                         const float* __restrict__ g, int64_t ldg,
+                                                         float* __restrict__ dw1, float* __restrict__ dv,
+                                                         float* __restrict__ dw0) {
+  __shared__ float red[KF + 2][256];
   const int i = blockIdx.x;
-  const int NQ = kfm + 2;  // [x s_0 .. x s_{kfm-1} | x | x^2] weighted by g
-  float acc[34];
-  for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
-  for (int64_t b = threadIdx.x; b < B; b += 256) {
-    const float gb = g[b * ldg];
-    if (i == d) {
-      acc[0] += gb;
-      continue;
+  float acc[KF + 2];
+#pragma unroll
+  for (int q = 0; q < KF + 2; ++q) acc[q] = 0.f;
+  if (i == d) {
+    for (int64_t b = threadIdx.x; b < B; b += 256) acc[0] += g[b * ldg];
+  } else {
+    for (int64_t b = threadIdx.x; b < B; b += 256) {
+      const float xv = x[b * ldx + i];
+      const float xg = g[b * ldg] * xv;
+#pragma unroll
+      for (int f = 0; f < KF; ++f) {
+        const float sv = s[b * lds + (f < kfm ? f : 0)];
+        acc[f] = fmaf(xg, f < kfm ? sv : 0.f, acc[f]);
+      }
+      acc[KF] += xg;
+      acc[KF + 1] = fmaf(xg, xv, acc[KF + 1]);
     }
-    const float xg = gb * x[b * ldx + i];
-    for (int f = 0; f < kfm; ++f) acc[f] = fmaf(xg, s[b * lds + f], acc[f]);
-    acc[kfm] += xg;
-    acc[kfm + 1] = fmaf(xg, x[b * ldx + i], acc[kfm + 1]);
   }
-  for (int q = 0; q < NQ; ++q) red[q][threadIdx.x] = acc[q];
+#pragma unroll
+  for (int q = 0; q < KF + 2; ++q) red[q][threadIdx.x] = acc[q];
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o)
-      for (int q = 0; q < NQ; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + o];
+    if ((int)threadIdx.x < o) {
+#pragma unroll
+      for (int q = 0; q < KF + 2; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + o];
+    }
     __syncthreads();
   }
   if (i == d) {
@@ -360,10 +368,22 @@ __global__ __launch_bounds__(256) void fm_param_grad_kernel(const float* __restr
   }
   if ((int)threadIdx.x < kfm) {
     const int f = threadIdx.x;
-    dv[(int64_t)i * kfm + f] = red[f][0] - red[kfm + 1][0] * v[(int64_t)i * kfm + f];
+    dv[(int64_t)i * kfm + f] = red[f][0] - red[KF + 1][0] * v[(int64_t)i * kfm + f];
   }
-  if (threadIdx.x == 0) dw1[i] = red[kfm][0];
+  if (threadIdx.x == 0) dw1[i] = red[KF][0];
 }
+
+static void launch_fm_param_grads(const float* x, int64_t ldx, const float* s, int64_t lds, const float* v,
+                                  int64_t B, int d, int kfm, const float* g, int64_t ldg, float* dw1, float* dv,
+                                  float* dw0, hipStream_t st) {
+  const unsigned grid = (unsigned)(d + (dw0 ? 1 : 0));
+  if (grid == 0) return;
+  if (kfm <= 16)
+    fm_param_grad_col<16><<<grid, 256, 0, st>>>(x, ldx, s, lds, v, B, d, kfm, g, ldg, dw1, dv, dw0);
+  else
+    fm_param_grad_col<32><<<grid, 256, 0, st>>>(x, ldx, s, lds, v, B, d, kfm, g, ldg, dw1, dv, dw0);
+}
+
 
 // Sharded FM backward, owner side: x rows of the owned slots of every
 // (requester, sample) record, [n_pairs][n_owned * k] (absent slot -> 0).
@@ -823,8 +843,7 @@ extern "C" int rs_fm_param_grads(const float* x, int64_t ldx, const float* s, co
                                  int kfm, const float* g, float* dw1, float* dv, float* dw0, rs_stream_t stream) {
   RS_REQUIRE(x && s && v && g && dw1 && dv && dw0 && batch >= 0 && d > 0 && kfm >= 1 && kfm <= 32 && ldx >= d,
              "rs_fm_param_grads: bad arguments (kfm <= 32)");
-  fm_param_grad_kernel<<<(unsigned)(d + 1), 256, 0, as_stream(stream)>>>(x, ldx, s, kfm, v, batch, d, kfm, g, 1,
-                                                                          dw1, dv, dw0);
+  launch_fm_param_grads(x, ldx, s, kfm, v, batch, d, kfm, g, 1, dw1, dv, dw0, as_stream(stream));
   return launch_status("rs_fm_param_grads");
 }
 
@@ -835,8 +854,7 @@ extern "C" int rs_fm_param_grads_strided(const float* x, int64_t ldx, const floa
   RS_REQUIRE((x || d == 0) && s && v && g && dw1 && dv && batch >= 0 && d >= 0 && kfm >= 1 && kfm <= 32 &&
                  ldx >= d && lds >= kfm && ldg >= 1,
              "rs_fm_param_grads_strided: bad arguments (kfm <= 32)");
-  fm_param_grad_kernel<<<(unsigned)(d + (dw0 ? 1 : 0)), 256, 0, as_stream(stream)>>>(x, ldx, s, lds, v, batch, d, kfm,
-                                                                                     g, ldg, dw1, dv, dw0);
+  launch_fm_param_grads(x, ldx, s, lds, v, batch, d, kfm, g, ldg, dw1, dv, dw0, as_stream(stream));
   return launch_status("rs_fm_param_grads_strided");
 }
 
@@ -856,8 +874,8 @@ extern "C" int rs_shard_owner_fm_grad(const int32_t* recv, int64_t rec_stride, i
                                                                              shard_rows, k, n_pairs, rows_ws);
   fm_x_grad_kernel<false><<<(unsigned)((n_pairs * w + 255) / 256), 256, 0, st>>>(
       rows_ws, w, gs, gs_stride, w1 + col, v + col * kfm, n_pairs, w, kfm, gs + kfm, gs_stride, drows, w);
-  fm_param_grad_kernel<<<(unsigned)w, 256, 0, st>>>(rows_ws, w, gs, gs_stride, v + col * kfm, n_pairs, w, kfm,
-                                                    gs + kfm, gs_stride, dw1, dv, nullptr);
+  launch_fm_param_grads(rows_ws, w, gs, gs_stride, v + col * kfm, n_pairs, w, kfm, gs + kfm, gs_stride, dw1, dv,
+                        nullptr, st);
   return launch_status("rs_shard_owner_fm_grad");
 }
 
