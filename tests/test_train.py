@@ -406,3 +406,94 @@ def test_embedding_sgd_hot_rows(gpu, k, B):
     err = np.abs((outs[0] - table0) - delta_ref)
     scale = np.maximum(np.abs(delta_ref), np.sqrt(np.mean(delta_ref ** 2)))
     assert (err <= 1e-4 * scale + 4 * np.finfo(np.float32).eps * np.abs(table0)).all(), float((err / scale).max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N", [(1, 1), (255, 63), (256, 64), (257, 65), (5000, 300), (204800, 40)])
+def test_col_sum_split_matches_numpy(gpu, M, N):
+    """rs_col_sum_split (256-row slices in a workspace, then the slices in
+    order; one-wave-per-column finish for many slices) == the fp64 column sums,
+    on a strided A, bitwise reproducible run to run."""
+    from recommender_system_amd import _lib
+    rng = np.random.default_rng(M + N)
+    A = torch.as_tensor(rng.standard_normal((M, N + 3)).astype(np.float32), device=gpu)
+    ws = torch.empty(max(int(_lib.lib().rs_col_sum_workspace_size(M, N)), 1), dtype=torch.uint8, device=gpu)
+    outs = []
+    for _ in range(2):
+        out = torch.empty(N, device=gpu)
+        _lib.call("rs_col_sum_split", A.data_ptr(), A.stride(0), M, N, out.data_ptr(), ws.data_ptr(), ws.numel(),
+                  _lib.stream())
+        outs.append(out.cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
+    ref = A.cpu().numpy().astype(np.float64)[:, :N].sum(0)
+    scale = np.sqrt(M) * 4 + 1
+    assert np.abs(outs[0] - ref).max() <= 1e-6 * scale, float(np.abs(outs[0] - ref).max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N", [(1, 5), (300, 16), (20000, 64)])
+def test_dice_train_fwd_bwd_match_oracle(gpu, M, N):
+    """rs_dice_train_fwd / _bwd (Dice under fit: batch statistics, the
+    batch-norm backward, dalpha, moving averages) == the oracle's
+    _dice_train / _dice_train_bwd in fp64."""
+    from recommender_system_amd import _lib
+    rng = np.random.default_rng(M * 7 + N)
+    x = rng.standard_normal((M, N)) * 1.5 + 0.3
+    alpha = rng.uniform(-0.5, 0.5, N)
+    dy = rng.standard_normal((M, N))
+    mm, mv = rng.uniform(-0.1, 0.1, N), rng.uniform(0.5, 1.5, N)
+    eps = 1e-9
+    t = lambda a: torch.as_tensor(np.asarray(a, np.float32), device=gpu).contiguous()
+    xd, ad, dyd, mmd, mvd = t(x), t(alpha), t(dy), t(mm), t(mv)
+    mean, var, y = torch.empty(N, device=gpu), torch.empty(N, device=gpu), torch.empty(M, N, device=gpu)
+    dx, dal = torch.empty(M, N, device=gpu), torch.empty(N, device=gpu)
+    ws = torch.empty(int(_lib.lib().rs_dice_train_workspace_size(M, N)), dtype=torch.uint8, device=gpu)
+    _lib.call("rs_dice_train_fwd", xd.data_ptr(), M, N, ad.data_ptr(), eps, 0.99, mmd.data_ptr(), mvd.data_ptr(),
+              mean.data_ptr(), var.data_ptr(), y.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream())
+    _lib.call("rs_dice_train_bwd", xd.data_ptr(), M, N, ad.data_ptr(), mean.data_ptr(), var.data_ptr(), eps,
+              dyd.data_ptr(), dx.data_ptr(), dal.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream())
+    x32 = x.astype(np.float32).astype(np.float64)
+    yr, saved = O._dice_train(x32, alpha.astype(np.float32), eps, np.float64)
+    dxr, dalr = O._dice_train_bwd(dy.astype(np.float32).astype(np.float64), x32, alpha.astype(np.float32), eps, saved)
+    assert_scaled_close(y, yr, what="dice y")
+    assert_scaled_close(mean, saved[0], what="batch mean")
+    assert_scaled_close(var, saved[1], what="batch var")
+    if M > 1:  # one row: var 0, xhat 0 — dx is the direct term alone
+        assert_scaled_close(dx, dxr, rtol=1e-4, what="dice dx")
+    assert_scaled_close(dal, dalr, rtol=1e-4, what="dice dalpha")
+    assert_scaled_close(mmd, 0.99 * mm.astype(np.float32) + 0.01 * saved[0], what="moving mean")
+    assert_scaled_close(mvd, 0.99 * mv.astype(np.float32) + 0.01 * saved[1], what="moving var")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,F,k", [(1, 2, 4), (17, 3, 8), (100, 26, 16), (33, 5, 5)])
+def test_outer_product_bwd_matches_oracle(gpu, B, F, k):
+    """rs_outer_product_bwd (adds sum_p g_p e_j W_p / e_i W_p^T into demb) and
+    rs_outer_product_w_grad (dW) == the oracle's OuterProductLayer backward,
+    partial 16-sample tiles and k not a multiple of 4 included."""
+    from recommender_system_amd import _lib
+    rng = np.random.default_rng(B + F + k)
+    P = F * (F - 1) // 2
+    e = rng.standard_normal((B, F, k))
+    W = rng.standard_normal((k, P, k)) * 0.3
+    g = rng.standard_normal((B, P))
+    base = rng.standard_normal((B, F * k))
+    t = lambda a: torch.as_tensor(np.asarray(a, np.float32), device=gpu).contiguous()
+    ed, Wd, gd = t(e.reshape(B, F * k)), t(W), t(g)
+    demb = t(base)
+    dW = torch.empty(k, P, k, device=gpu)
+    _lib.call("rs_outer_product_bwd", ed.data_ptr(), F * k, gd.data_ptr(), P, Wd.data_ptr(), F, k, B,
+              demb.data_ptr(), F * k, _lib.stream())
+    _lib.call("rs_outer_product_w_grad", ed.data_ptr(), F * k, gd.data_ptr(), P, F, k, B, dW.data_ptr(),
+              _lib.stream())
+    e32, W32, g32 = (a.astype(np.float32).astype(np.float64) for a in (e, W, g))
+    row, col = O.pair_indices(F)
+    de = base.astype(np.float32).astype(np.float64).reshape(B, F, k).copy()
+    dWr = np.zeros_like(W32)
+    for p_, (i, j) in enumerate(zip(row, col)):
+        Wp = W32[:, p_, :]
+        de[:, i, :] += g32[:, p_:p_ + 1] * (e32[:, j, :] @ Wp)
+        de[:, j, :] += g32[:, p_:p_ + 1] * (e32[:, i, :] @ Wp.T)
+        dWr[:, p_, :] = (g32[:, p_:p_ + 1] * e32[:, j, :]).T @ e32[:, i, :]
+    assert_scaled_close(demb, de.reshape(B, F * k), what="demb")
+    assert_scaled_close(dW, dWr, what="dW")
