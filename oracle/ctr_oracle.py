@@ -897,6 +897,81 @@ def din_train_step(inputs, t, p, dense_feats, sparse_feats, behavior_feats, lr, 
     return new, loss
 
 
+def _nfm_train_forward(dense, ids, p, dt):
+    tables = [np.asarray(tb, dt) for tb in p["tables"]]
+    k = tables[0].shape[1]
+    flat = embed_layer(cast_ids(ids), tables, dt)
+    e = flat.reshape(flat.shape[0], -1, k)
+    x = np.concatenate([np.asarray(dense, dt), bi_interaction(e, dt)], axis=-1)
+    g_, b_, _, _, eps = p["bn"]
+    mu, var = x.mean(0), x.var(0)
+    xhat = (x - mu) / np.sqrt(var + eps)
+    acts = [xhat * np.asarray(g_, dt) + np.asarray(b_, dt)]
+    for W, b in p["dnn_hidden"]:
+        acts.append(activation(acts[-1] @ np.asarray(W, dt) + np.asarray(b, dt), p.get("act", "relu")))
+    acts.append(acts[-1] @ np.asarray(p["dnn_out"][0], dt) + np.asarray(p["dnn_out"][1], dt))
+    logit = (acts[-1] @ np.asarray(p["out"][0], dt) + np.asarray(p["out"][1], dt))[:, 0]
+    return dict(e=e, x=x, mu=mu, var=var, xhat=xhat, acts=acts, logit=logit)
+
+
+def nfm_loss(dense, ids, t, p, dt=np.float64):
+    """compile_fit's objective on NFM (training-mode BatchNormalization)."""
+    z = _nfm_train_forward(dense, ids, p, dt)["logit"]
+    t = np.asarray(t, dt).reshape(-1)
+    return np.mean(np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z))))
+
+
+def nfm_train_step(dense, ids, t, p, lr, momentum=0.99, dt=np.float64):
+    """One SGD step of compile_fit on NFM (utils/compile_fit.py:9-15;
+    model/nfm.py:22-33 with 3-D embeddings, training=True): BCE on the
+    sigmoid's logit; output Dense(1) and the DNNLayer (relu hidden, linear
+    output) by the chain rule; BatchNormalization in training mode (batch
+    mean / biased variance, moving averages with momentum); the
+    Bi-Interaction 0.5((sum_f e_f)^2 - sum_f e_f^2) gives de_f = dbi (S - e_f),
+    S = sum_f e_f; embedding rows by scatter-add.  No regularisers.
+    p: tables, bn (gamma, beta, mean, var, eps), dnn_hidden [(W, b)],
+    dnn_out (W, b), out (W, b).  Returns (new p, per-sample losses)."""
+    ids = cast_ids(ids)
+    c = _nfm_train_forward(dense, ids, p, dt)
+    t = np.asarray(t, dt).reshape(-1)
+    z = c["logit"]
+    B = z.shape[0]
+    loss = np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z)))
+    g = (sigmoid(z) - t) / B
+    layers = [(np.asarray(W, dt), np.asarray(b, dt)) for W, b in p["dnn_hidden"]]
+    layers += [(np.asarray(p["dnn_out"][0], dt), np.asarray(p["dnn_out"][1], dt)),
+               (np.asarray(p["out"][0], dt), np.asarray(p["out"][1], dt))]
+    acts = c["acts"]
+    nh = len(p["dnn_hidden"])
+    delta = g[:, None]
+    new_layers = [None] * len(layers)
+    for li in reversed(range(len(layers))):
+        W, b = layers[li]
+        new_layers[li] = (W - lr * (acts[li].T @ delta), b - lr * delta.sum(0))
+        prev = delta @ W.T
+        if 0 < li <= nh and p.get("act", "relu") == "relu":  # acts[li] = relu output of hidden layer li-1
+            prev = prev * (acts[li] > 0)
+        delta = prev
+    gam, bet, mu0, var0, eps = p["bn"]
+    gam, bet = np.asarray(gam, dt), np.asarray(bet, dt)
+    xhat = c["xhat"]
+    dgam, dbet = (delta * xhat).sum(0), delta.sum(0)
+    dx = gam / np.sqrt(c["var"] + eps) * (delta - delta.mean(0) - xhat * (delta * xhat).mean(0))
+    nd = np.asarray(dense).shape[1]
+    dbi = dx[:, nd:]
+    e = c["e"]
+    de = dbi[:, None, :] * (e.sum(1, keepdims=True) - e)
+    tables = [np.array(tb, dt) for tb in p["tables"]]
+    for f, tb in enumerate(tables):
+        np.add.at(tb, ids[:, f], -lr * de[:, f, :])
+    new = {"tables": tables, "dnn_hidden": new_layers[:nh], "dnn_out": new_layers[nh], "out": new_layers[nh + 1],
+           "bn": (gam - lr * dgam, bet - lr * dbet, momentum * np.asarray(mu0, dt) + (1 - momentum) * c["mu"],
+                  momentum * np.asarray(var0, dt) + (1 - momentum) * c["var"], eps)}
+    if "act" in p:
+        new["act"] = p["act"]
+    return new, loss
+
+
 def deepfm_loss(dense, ids, t, p, l2_w, l2_v, nd=13, dt=np.float64):
     """compile_fit's objective on DeepFM: mean BCE(t, sigmoid(0.5(fm+dnn)))
     + l2_w |w1|^2 + l2_v |v|^2."""

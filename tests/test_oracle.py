@@ -523,3 +523,40 @@ def test_din_train_step_dice_gradient_matches_finite_differences(att_act, dnn_ac
             check(lambda q, li=li: q["dnn"][li][2][0], (1,), lambda q, li=li: q["dnn"][li][2][0])
     for j, idx in [(0, (2,)), (1, (4,))]:
         check(lambda q, j=j: q["bn"][j], idx, lambda q, j=j: q["bn"][j])
+
+
+def test_nfm_train_step_gradient_matches_finite_differences():
+    """oracle.nfm_train_step (compile_fit on NFM: training-mode BN, the
+    Bi-Interaction backward de_f = dbi (S - e_f), relu DNNLayer + linear
+    output + Dense(1), embedding scatter-add) == central differences."""
+    rng = np.random.default_rng(31)
+    k, vocab, nd = 3, [3, 2, 4], 2
+    tables = [rng.normal(size=(v_, k)) * 0.7 for v_ in vocab]
+    D = nd + k
+    p = {"tables": tables, "bn": (1 + 0.1 * rng.normal(size=D), 0.1 * rng.normal(size=D), np.zeros(D), np.ones(D), 1e-3),
+         "dnn_hidden": [(rng.normal(size=(D, 5)) * 0.5, rng.normal(size=5) * 0.1)],
+         "dnn_out": (rng.normal(size=(5, 2)) * 0.5, rng.normal(size=2) * 0.1),
+         "out": (rng.normal(size=(2, 1)), np.array([0.1]))}
+    ids = np.array([[0, 1, 3], [2, 1, 0], [0, 0, 3], [1, 1, 2], [2, 0, 1]])
+    dense = rng.random((5, nd))
+    t = np.array([1.0, 0.0, 1.0, 0.0, 1.0])
+    new, _ = O.nfm_train_step(dense, ids, t, p, 1.0)
+    eps = 1e-6
+
+    def check(arr, new_arr, idx):
+        keep = arr[idx]
+        arr[idx] = keep + eps
+        lp = O.nfm_loss(dense, ids, t, p)
+        arr[idx] = keep - eps
+        lm = O.nfm_loss(dense, ids, t, p)
+        arr[idx] = keep
+        assert abs((lp - lm) / (2 * eps) - (arr[idx] - new_arr[idx])) < 1e-6, idx
+
+    for c, idx in [(0, (0, 0)), (0, (2, 1)), (1, (1, 2)), (2, (3, 0))]:
+        check(p["tables"][c], new["tables"][c], idx)
+    check(p["dnn_hidden"][0][0], new["dnn_hidden"][0][0], (3, 2))
+    check(p["dnn_out"][0], new["dnn_out"][0], (1, 1))
+    check(p["out"][0], new["out"][0], (0, 0))
+    check(p["out"][1], new["out"][1], (0,))
+    for j, idx in [(0, (2,)), (1, (4,))]:
+        check(p["bn"][j], new["bn"][j], idx)
