@@ -461,6 +461,12 @@ int rs_inner_product_bwd(const float* emb, int64_t emb_stride,
                          const float* dflat, int64_t dflat_stride, int n_fields,
                          int k, int64_t batch, float* demb, int64_t demb_stride,
                          rs_stream_t stream);
+/* NFM Bi-Interaction backward (model/nfm.py:28, 3-D embeddings; NFM
+ * training): demb[b, f*k + c] = dbi[b, c] (S_bc - e_bfc), S = sum_f e_f.      */
+int rs_bi_interaction_bwd(const float* emb, int64_t emb_stride,
+                          const float* dbi, int64_t dbi_stride, int n_fields,
+                          int k, int64_t batch, float* demb,
+                          int64_t demb_stride, rs_stream_t stream);
 /* OuterProductLayer backward (layer/interaction.py:200-215, PNN modes
  * 'outer' / 'both'): o_p = e_j^T W_p e_i, W_p[a][c] = W[a,p,c], W [k, P, k].
  * rs_outer_product_bwd ADDS to demb[b, f*k ..]: sum_{j>f} g_p e_j W_p +

@@ -82,6 +82,7 @@ SIGNATURES = {
     "rs_bce_prob_grad": (I, [P, L, P, L, P, P, P]),
     "rs_inner_product_bwd": (I, [P, L, P, L, P, L, I, I, L, P, L, P]),
     "rs_outer_product_bwd": (I, [P, L, P, L, P, I, I, L, P, L, P]),
+    "rs_bi_interaction_bwd": (I, [P, L, P, L, I, I, L, P, L, P]),
     "rs_outer_product_w_grad": (I, [P, L, P, L, I, I, L, P, P]),
     "rs_din_att_concat": (I, [P, P, L, I, I, P, P]),
     "rs_din_att_concat_bwd": (I, [P, P, P, L, I, I, P, L, P, P]),

@@ -496,6 +496,25 @@ __global__ __launch_bounds__(256) void outer_w_grad_kernel(const float* __restri
   }
 }
 
+// ------------------------------------------- NFM Bi-Interaction backward
+// model/nfm.py:28 on [B, F, k]: bi_c = 0.5((sum_f e_fc)^2 - sum_f e_fc^2) ->
+// de_fc = dbi_c (S_c - e_fc), S_c = sum_f e_fc (fields summed in order).
+// One thread per (sample, column).
+__global__ __launch_bounds__(256) void bi_interaction_bwd_kernel(const float* __restrict__ emb, int64_t lde,
+                                                                 const float* __restrict__ dbi, int64_t ldd, int F,
+                                                                 int k, int64_t B, float* __restrict__ demb,
+                                                                 int64_t lddm) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= B * k) return;
+  const int64_t b = t / k;
+  const int c = (int)(t - b * k);
+  const float* e = emb + b * lde + c;
+  float S = 0.f;
+  for (int f = 0; f < F; ++f) S += e[(int64_t)f * k];
+  const float g = dbi[b * ldd + c];
+  for (int f = 0; f < F; ++f) demb[b * lddm + (int64_t)f * k + c] = g * (S - e[(int64_t)f * k]);
+}
+
 // ------------------------------------------- row-sparse SGD of the tables
 template <int KIND>
 __global__ __launch_bounds__(256) void emb_keys_kernel(const void* ids, int64_t id_stride,
@@ -792,6 +811,18 @@ extern "C" int rs_outer_product_w_grad(const float* emb, int64_t emb_stride, con
   outer_w_grad_kernel<<<(unsigned)(n_fields * (n_fields - 1) / 2), 256, 0, as_stream(stream)>>>(
       emb, emb_stride, dout, dout_stride, n_fields, k, batch, dW);
   return launch_status("rs_outer_product_w_grad");
+}
+
+extern "C" int rs_bi_interaction_bwd(const float* emb, int64_t emb_stride, const float* dbi, int64_t dbi_stride,
+                                     int n_fields, int k, int64_t batch, float* demb, int64_t demb_stride,
+                                     rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(emb && dbi && demb && batch > 0 && n_fields >= 1 && k >= 1 && emb_stride >= (int64_t)n_fields * k &&
+                 dbi_stride >= k && demb_stride >= (int64_t)n_fields * k,
+             "rs_bi_interaction_bwd: bad arguments");
+  bi_interaction_bwd_kernel<<<(unsigned)((batch * k + 255) / 256), 256, 0, as_stream(stream)>>>(
+      emb, emb_stride, dbi, dbi_stride, n_fields, k, batch, demb, demb_stride);
+  return launch_status("rs_bi_interaction_bwd");
 }
 
 extern "C" int rs_inner_product_bwd(const float* emb, int64_t emb_stride, const float* dinner, int64_t dinner_stride,

@@ -1015,6 +1015,62 @@ class NFM(TowerMixin, KerasModule):
             return self.tower(x)  # DNNLayer + Dense(1, sigmoid) in one launch
         return self.output_layer(self.dnn_layers(x))
 
+    def train_step(self, inputs, labels, lr=0.01, return_loss=False, check_ids=True, dropout=None):
+        """One step of compile_fit on NFM (utils/compile_fit.py:9-15; the
+        reference's NFM demo trains this way, model/nfm.py:47) with
+        NFM.call in training mode:
+          [dense | Bi-Interaction] (rs_embed_pair_pool_fwd) and the rows
+          (rs_embed_gather), rs_bn_train_fwd (batch statistics, moving
+          averages), the DNNLayer + output Dense with saved activations
+          (rs_dense_fwd, logit), rs_head_grad, the DNN backward (rs_gemm /
+          rs_col_sum), rs_bn_train_bwd, rs_bi_interaction_bwd (de_f = dbi
+          (S - e_f)), SGD of the dense parameters and row-sparse
+          rs_embedding_sgd.  Dropout as the identity (_dropout_notice).
+        Returns per-sample losses (before the step) if ``return_loss``."""
+        dnn = self.dnn_layers
+        _dropout_notice("NFM", dnn, dropout)
+        _check_train_tower("NFM", dnn)
+        dense, ids = _split_criteo(inputs, self.nd, self._dev)
+        labels = _to_device_f32(labels, self._dev).reshape(-1)
+        e, bn, out = self.emb_layers, self.bn_layer, self.output_layer
+        B, F, k, st, dev = ids.shape[0], e.n_fields, e.k, _lib.stream(), self._dev
+        emp = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=dev)
+        x = self.bi_interaction_input(inputs, check_ids)  # [B, nd + k]
+        rows = e.gather(ids, check_ids=False)             # [B, F*k] (ids checked above)
+        D = self.nd + k
+        mean, var, y0 = emp(D), emp(D), emp(B, D)
+        call("rs_bn_train_fwd", ptr(x), D, B, D, ptr(bn.gamma), ptr(bn.beta), bn.epsilon, 0.99, ptr(bn.moving_mean),
+             ptr(bn.moving_variance), ptr(mean), ptr(var), ptr(y0), D, st)
+        layers = self._layers()
+        acts = [y0]
+        for L in layers[:-1]:
+            acts.append(L(acts[-1]))
+        logit = emp(B)
+        call("rs_dense_fwd", ptr(acts[-1]), acts[-1].stride(0), ptr(out.kernel), ptr(out.bias), None,
+             _lib.ACT[None], ptr(logit), 1, B, out.kernel.shape[0], 1, st)
+        g, g0 = emp(B), emp(B)
+        loss = emp(B) if return_loss else None
+        call("rs_head_grad", ptr(logit), ptr(logit), ptr(labels), B, 1.0, 0.0, ptr(g), ptr(g0), ptr(loss), st)
+        gws = _gemm_ws(self, max(_lib.lib().rs_gemm_workspace_size(L.kernel.shape[0], L.kernel.shape[1], B)
+                                 for L in layers))
+        grads, delta = _dnn_backward(layers, acts, g.view(B, 1), (ptr(gws), gws.numel()), emp, st)
+        dx, dgam, dbet = emp(B, D), emp(D), emp(D)
+        call("rs_bn_train_bwd", ptr(x), D, B, D, ptr(mean), ptr(var), ptr(bn.gamma), bn.epsilon, ptr(delta),
+             delta.stride(0), ptr(dx), D, ptr(dgam), ptr(dbet), st)
+        de = emp(B, F * k)
+        call("rs_bi_interaction_bwd", ptr(rows), F * k, ptr(dx) + 4 * self.nd, D, F, k, B, ptr(de), F * k, st)
+        _dnn_apply(grads, lr, st)
+        call("rs_sgd_update", ptr(bn.gamma), ptr(dgam), D, float(lr), 0.0, st)
+        call("rs_sgd_update", ptr(bn.beta), ptr(dbet), D, float(lr), 0.0, st)
+        ws_n = _lib.lib().rs_embedding_sgd_workspace_size(B * F)
+        ws = self.__dict__.get("_emb_ws")
+        if ws is None or ws.numel() < ws_n:
+            ws = self.__dict__["_emb_ws"] = torch.empty(ws_n, dtype=torch.uint8, device=dev)
+        call("rs_embedding_sgd", ptr(e.table), e.total_rows, k, ptr(ids), _lib.id_kind(ids), ids.stride(0),
+             ptr(e.field_offsets), ptr(e.field_vocab), F, B, ptr(de), F * k, float(lr), ptr(ws), None, st)
+        self._weights_changed()
+        return loss
+
 
 class AFM(KerasModule):
     """AFM(feature_columns, mode) — model/afm.py:11-19: sigmoid(AFMLayer(x)),

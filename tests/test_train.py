@@ -497,3 +497,54 @@ def test_outer_product_bwd_matches_oracle(gpu, B, F, k):
         dWr[:, p_, :] = (g32[:, p_:p_ + 1] * e32[:, j, :]).T @ e32[:, i, :]
     assert_scaled_close(demb, de.reshape(B, F * k), what="demb")
     assert_scaled_close(dW, dWr, what="dW")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,k,hidden", [(64, 8, [32, 16]), (300, 16, [256, 128, 64])])
+def test_nfm_train_steps_match_oracle(gpu, B, k, hidden):
+    """NFM.train_step (compile_fit on NFM: training-mode BatchNormalization,
+    the DNNLayer + output Dense backward, the Bi-Interaction backward,
+    row-sparse embedding SGD) == oracle.nfm_train_step (pinned by finite
+    differences) over 3 steps with repeated rows; the inference forward then
+    runs on the trained weights and the moved BN averages."""
+    import recommender_system_amd as rs
+    from tests.helpers import criteo_columns, dnn_params, tables_of
+    rng = np.random.default_rng(B + k + 5)
+    vocab = rng.integers(1, 200, 26)
+    m = rs.NFM(criteo_columns(vocab, embed_dim=k), hidden, 1, embed_dim=k, seed=6)
+    with torch.no_grad():
+        m.emb_layers.table.mul_(4.0)
+
+    def params():
+        hid, dout = dnn_params(m.dnn_layers)
+        bn = m.bn_layer
+        c = lambda t: t.detach().cpu().numpy().astype(np.float64)
+        return {"tables": tables_of(m.emb_layers), "dnn_hidden": hid, "dnn_out": dout,
+                "out": (c(m.output_layer.kernel), c(m.output_layer.bias)),
+                "bn": (c(bn.gamma), c(bn.beta), c(bn.moving_mean), c(bn.moving_variance), bn.epsilon)}
+
+    p = params()
+    lr = 0.2
+    for step in range(3):
+        dense = rng.random((B, 13)).astype(np.float32)
+        ids = np.stack([rng.integers(0, v_, B) for v_ in vocab], 1).astype(np.int32)
+        ids[:7, 3] = 0  # repeated rows
+        t = rng.integers(0, 2, B).astype(np.float32)
+        loss = m.train_step((dense, ids), t, lr=lr, return_loss=True)
+        p, ce = O.nfm_train_step(dense, ids, t, p, lr)
+        got = params()
+        assert_scaled_close(loss, ce, what=f"step {step} loss")
+        for c_ in range(26):
+            assert_scaled_close(got["tables"][c_], p["tables"][c_], what=f"step {step} table {c_}")
+        for li, ((W, b), (Wr, br)) in enumerate(zip(got["dnn_hidden"], p["dnn_hidden"])):
+            assert_scaled_close(W, Wr, what=f"step {step} W{li}")
+            assert_scaled_close(b, br, what=f"step {step} b{li}")
+        for name in ("dnn_out", "out"):
+            assert_scaled_close(got[name][0], p[name][0], what=f"step {step} {name} W")
+            assert_scaled_close(got[name][1], p[name][1], what=f"step {step} {name} b")
+        for j, nm in enumerate(("gamma", "beta", "moving_mean", "moving_variance")):
+            assert_scaled_close(got["bn"][j], p["bn"][j], what=f"step {step} bn {nm}")
+    pin = {"tables": p["tables"], "bn_mean": p["bn"][2], "bn_var": p["bn"][3], "bn_gamma": p["bn"][0],
+           "bn_beta": p["bn"][1], "dnn_hidden": p["dnn_hidden"], "dnn_out": p["dnn_out"], "out_kernel": p["out"][0],
+           "out_bias": p["out"][1]}
+    assert_scaled_close(m((dense, ids)), O.nfm(None, pin, inputs=(dense, ids))[0], what="forward after training")
