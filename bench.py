@@ -1117,9 +1117,27 @@ def bench_ffm(args, world, rank):
         cpu = _cpu_leg(args, rank, B, cpu_step, 8, "FFM.call: FFMLayer as row gathers of w / v (the one-hot x "
                                                   "never formed) + sigmoid; host copy holds the touched rows only",
                        gpu0)
+    # compile_fit's step on FFM (FFM.train_step; after the forward timings and
+    # the CPU leg: it moves the weights).  Keras' l2 on every row of v makes
+    # the step a read + write of the whole table.
+    gl = torch.Generator(device="cuda")
+    gl.manual_seed(SEED + 9)
+    labels = (torch.rand(16, B, generator=gl, device="cuda") < 0.25).to(torch.float32)
+
+    def train(i):
+        m.train_step((dense_pool[i % 64], ids_pool[i % 64]), labels[i % 16], lr=0.01)
+
+    nt = max(5, args.steps // 20)
+    tdt, _ = _timed(train, nt, 1, world, events=False)
+    vbytes = (13 + F * V) * NF * k * 4
     return _hbm_line("FFM forward samples/sec @ batch 4096, 26 sparse x 1e6 vocab, k 8", args, world, B, dt, slot,
                      alg, "ffm_fused", V, "ffm4_kernel",
-                     {"table_GB": (13 + F * V) * NF * k * 4 / 1e9, "cpu_baseline": cpu})
+                     {"table_GB": (13 + F * V) * NF * k * 4 / 1e9, "cpu_baseline": cpu,
+                      "train_step": {"samples_per_s": nt * B / tdt, "ms_per_step": tdt / nt * 1e3,
+                                     "l2_decay_hbm_frac": 2 * vbytes / (tdt / nt) / PEAK_HBM,
+                                     "timing": "eager launches",
+                                     "note": "FFM.train_step: rs_ffm_train_fwd, dense-row rs_gemm, l2 decay of every "
+                                             "row of w and v (2 x table bytes), row-sparse SGD of the looked-up rows"}})
 
 
 def bench_io(args, world, rank):

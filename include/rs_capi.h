@@ -598,6 +598,33 @@ int rs_cross_train_bwd(const float* x0, int64_t ldx, int d, int n_layers,
                        const float* dxl, int64_t lddxl, float* deltas,
                        float* s, float* dx, int64_t lddx,
                        rs_stream_t stream);
+/* rs_embedding_sgd with the gradient row of lookup (b, c) at grad[b *
+ * grad_stride + c * grad_field_stride] (k for one row per lookup; 0 for one
+ * row per sample shared by all its fields — the FFM step).                 */
+int rs_embedding_sgd_strided(float* table, int64_t n_rows, int k,
+                             const void* ids, int id_kind, int64_t id_stride,
+                             const int64_t* field_offsets,
+                             const int64_t* field_vocab, int n_fields,
+                             int64_t batch, const float* grad,
+                             int64_t grad_stride, int64_t grad_field_stride,
+                             float lr, void* workspace, int* err_flag,
+                             rs_stream_t stream);
+/* FFM training (compile_fit on FFM, model/ffm.py:20-22; FFM.train_step
+ * composes it with rs_gemm / rs_col_sum / rs_sgd_update / rs_l2_decay /
+ * rs_embedding_sgd_strided): rs_ffm_train_fwd computes, per sample, Fm[f,c]
+ * = sum_i x_i v[i,f,c] (v [feature_num, nd+F, k]; the nd dense rows and row
+ * nd + field_offsets[c] + id of each field, an out-of-range id being
+ * tf.one_hot's zero row), z = w0 + x.w + 0.5(|sum_f Fm_f|^2 - sum_f |Fm_f|^2),
+ * g[b] = (sigmoid(z) - t)/B, loss[b] (optional) and G[b, f*k + c] =
+ * g (T_c - Fm[f,c]), T = sum_f Fm_f.  (nd + F) * k <= 4096, k <= 64.
+ * rs_l2_decay: w -= lr * 2 l2 w over n floats (Keras l2 on every row).      */
+int rs_ffm_train_fwd(const void* ids, int id_kind, int64_t id_stride,
+                     const float* dense, int64_t dense_stride, int nd,
+                     const float* v, const float* w, const float* w0,
+                     const int64_t* field_offsets, const int64_t* field_vocab,
+                     int n_fields, int k, const float* labels, int64_t batch,
+                     float* G, float* g, float* loss, rs_stream_t stream);
+int rs_l2_decay(float* w, int64_t n, float lr, float l2, rs_stream_t stream);
 int64_t rs_embedding_sgd_workspace_size(int64_t n_lookups);
 int rs_embedding_sgd(float* table, int64_t n_rows, int k, const void* ids,
                      int id_kind, int64_t id_stride,

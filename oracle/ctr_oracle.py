@@ -539,6 +539,36 @@ def fm_train_step(x, t, w0, w1, v, lr, l2_w, l2_v, dt=np.float64):
     return w0 - lr * g_w0, w1 - lr * g_w1, v - lr * g_v, ce
 
 
+def ffm_loss(dense, ids, t, w0, w, v, onehot_dims, l2_w, l2_v, dt=np.float64):
+    """compile_fit's objective on FFM (model/ffm.py:20-22): mean BCE of
+    sigmoid(FFMLayer) plus FFMLayer's l2(w_reg) on w and l2(v_reg) on v
+    (layer/interaction.py:131-139; Keras fit adds model.losses)."""
+    z = ffm_layer(dense, ids, onehot_dims, w0, w, v, dt)[:, 0]
+    t = np.asarray(t, dt).reshape(-1)
+    bce = np.mean(np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z))))
+    return bce + l2_w * np.sum(np.asarray(w, dt) ** 2) + l2_v * np.sum(np.asarray(v, dt) ** 2)
+
+
+def ffm_train_step(dense, ids, t, w0, w, v, onehot_dims, lr, l2_w, l2_v, dt=np.float64):
+    """One SGD step of ffm_loss in closed form: with x the one-hot input,
+    Fm_f = sum_i x_i v[i, f] and inter = 0.5 (|sum_f Fm_f|^2 - sum_f |Fm_f|^2),
+    g = (sigmoid(z) - t)/B and G_b[f] = g_b (T_b - Fm_bf), T = sum_f Fm_f:
+    dw0 = sum g, dw = x^T g + 2 l2_w w, dv[i, f] = sum_b x_bi G_b[f] + 2 l2_v v.
+    Returns ((w0, w, v) after the step, per-sample BCE losses before it)."""
+    x = onehot_matrix(dense, ids, onehot_dims, dt)
+    w0, w, v = (np.asarray(a, dt) for a in (w0, w, v))
+    Fm = np.tensordot(x, v, axes=1)                          # [B, NF, k]
+    T = Fm.sum(1, keepdims=True)
+    z = (w0 + x @ w)[:, 0] + 0.5 * ((T[:, 0] ** 2).sum(1) - (Fm ** 2).sum((1, 2)))
+    t = np.asarray(t, dt).reshape(-1)
+    loss = np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z)))
+    g = (sigmoid(z) - t) / z.shape[0]
+    G = g[:, None, None] * (T - Fm)
+    dv = np.tensordot(x, G, axes=[[0], [0]]) + 2 * l2_v * v
+    dw = x.T @ g[:, None] + 2 * l2_w * w
+    return (w0 - lr * g.sum(keepdims=True)[:1], w - lr * dw, v - lr * dv), loss
+
+
 def deepfm_train_step(dense, ids, t, p, lr, l2_w, l2_v, nd=13, act="relu", dt=np.float64):
     """One SGD step of compile_fit on DeepFM (model/deepFM.py:23-31,
     utils/compile_fit.py:9-15), backpropagated by hand: z = 0.5 (fm + dnn),

@@ -111,6 +111,9 @@ SIGNATURES = {
     "rs_cross_train_bwd": (I, [P, L, I, I, P, L, P, P, L, P, P, P, L, P]),
     "rs_embedding_sgd_workspace_size": (L, [L]),
     "rs_embedding_sgd": (I, [P, L, I, P, I, L, P, P, I, L, P, L, F, P, P, P]),
+    "rs_embedding_sgd_strided": (I, [P, L, I, P, I, L, P, P, I, L, P, L, L, F, P, P, P]),
+    "rs_ffm_train_fwd": (I, [P, I, L, P, L, I, P, P, P, P, P, I, I, P, L, P, P, P, P]),
+    "rs_l2_decay": (I, [P, L, F, F, P]),
     "rs_fm_partial_width": (I, [I]),
     "rs_embed_pair_pool_fwd": (I, [P, I, L, P, P, P, I, I, I, P, L, I, P, L, I, P, P, I, P, L, P, P]),
     "rs_pair_products_fwd": (I, [P, L, I, I, L, P, P]),

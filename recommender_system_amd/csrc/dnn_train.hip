@@ -540,10 +540,12 @@ __global__ __launch_bounds__(256) void emb_keys_kernel(const void* ids, int64_t 
 // lanes, in chunk pieces (seg_piece / seg_cross, rs_common.hpp), so a hot row
 // (the DIN padding id: 10^5 lookups per batch) stays parallel and the result
 // bitwise reproducible.
+// (grad row of lookup (b, c) at grad[b*ldg + c*gfs]: gfs = k for one row per
+// lookup, 0 for one row per sample shared by its fields — FFM)
 __global__ __launch_bounds__(256) void emb_piece_kernel(const uint32_t* __restrict__ key,
                                                         const uint32_t* __restrict__ val, int64_t n, int F, int k,
-                                                        const float* __restrict__ grad, int64_t ldg, float lr,
-                                                        int64_t C, float* __restrict__ part_first,
+                                                        const float* __restrict__ grad, int64_t ldg, int64_t gfs,
+                                                        float lr, int64_t C, float* __restrict__ part_first,
                                                         float* __restrict__ part_last, float* __restrict__ table) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t p = t / k;
@@ -555,7 +557,7 @@ __global__ __launch_bounds__(256) void emb_piece_kernel(const uint32_t* __restri
         const int64_t j = val[q];
         const int64_t b = j / F;
         const int cc = (int)(j - b * F);
-        return grad[b * ldg + (int64_t)cc * k + f];
+        return grad[b * ldg + (int64_t)cc * gfs + f];
       }, part_first, part_last, r, s))
     table[(int64_t)r * k + f] -= lr * s;
 }
@@ -922,14 +924,15 @@ extern "C" int64_t rs_embedding_sgd_workspace_size(int64_t n_lookups) {
   return 5 * ((n_lookups * 4 + 255) / 256 * 256) + (emb_sort_bytes(n_lookups) + 255) / 256 * 256;
 }
 
-extern "C" int rs_embedding_sgd(float* table, int64_t n_rows, int k, const void* ids, int id_kind, int64_t id_stride,
-                                const int64_t* field_offsets, const int64_t* field_vocab, int n_fields,
-                                int64_t batch, const float* grad, int64_t grad_stride, float lr, void* workspace,
-                                int* err_flag, rs_stream_t stream) {
+extern "C" int rs_embedding_sgd_strided(float* table, int64_t n_rows, int k, const void* ids, int id_kind,
+                                        int64_t id_stride, const int64_t* field_offsets, const int64_t* field_vocab,
+                                        int n_fields, int64_t batch, const float* grad, int64_t grad_stride,
+                                        int64_t grad_field_stride, float lr, void* workspace, int* err_flag,
+                                        rs_stream_t stream) {
   const int64_t n = batch * n_fields;
   if (n == 0) return RS_OK;
   RS_REQUIRE(table && ids && field_offsets && field_vocab && grad && workspace && k >= 1 && batch > 0 &&
-                 grad_stride >= (int64_t)n_fields * k,
+                 grad_field_stride >= 0 && grad_stride >= (int64_t)(n_fields - 1) * grad_field_stride + k,
              "rs_embedding_sgd: bad arguments");
   RS_REQUIRE(n_rows < 0xffffffffll && n < (1ll << 31), "rs_embedding_sgd: rows must fit uint32, lookups int32");
   RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_embedding_sgd: bad id_kind");
@@ -960,10 +963,22 @@ extern "C" int rs_embedding_sgd(float* table, int64_t n_rows, int k, const void*
   float* part_first = reinterpret_cast<float*>(ws + 4 * slab);
   float* part_last = part_first + nchunk * k;
   const unsigned g = (unsigned)((n * k + 255) / 256);
-  emb_piece_kernel<<<g, 256, 0, st>>>(key_out, val_out, n, n_fields, k, grad, grad_stride, lr, C, part_first,
-                                      part_last, table);
+  emb_piece_kernel<<<g, 256, 0, st>>>(key_out, val_out, n, n_fields, k, grad, grad_stride, grad_field_stride, lr, C,
+                                      part_first, part_last, table);
   if (nchunk > 1) emb_cross_kernel<<<g, 256, 0, st>>>(key_out, n, k, lr, C, part_first, part_last, table);
   return launch_status("rs_embedding_sgd");
+}
+
+extern "C" int rs_embedding_sgd(float* table, int64_t n_rows, int k, const void* ids, int id_kind, int64_t id_stride,
+                                const int64_t* field_offsets, const int64_t* field_vocab, int n_fields,
+                                int64_t batch, const float* grad, int64_t grad_stride, float lr, void* workspace,
+                                int* err_flag, rs_stream_t stream) {
+  if (grad_stride < (int64_t)n_fields * k) {
+    set_error("rs_embedding_sgd: bad arguments");
+    return RS_ERR_ARG;
+  }
+  return rs_embedding_sgd_strided(table, n_rows, k, ids, id_kind, id_stride, field_offsets, field_vocab, n_fields,
+                                  batch, grad, grad_stride, k, lr, workspace, err_flag, stream);
 }
 
 extern "C" int rs_cross_train_fwd(const float* x0, int64_t ldx, int d, int n_layers, const float* W, const float* b,

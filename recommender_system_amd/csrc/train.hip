@@ -235,6 +235,105 @@ __global__ __launch_bounds__(256) void fm_train_apply_cross(FmTrainArgs a) {
   if (seg_cross(a.key_out, n, a.chunk, p, K1, f, a.part, a.part + nch * K1, r, acc)) fm_apply_row(a, r, f, acc);
 }
 
+// ---- FFM training (compile_fit on FFM, model/ffm.py:20-22 over FFMLayer,
+// layer/interaction.py:134-163).  One wave per sample: Fm[f, c] = sum_i x_i
+// v[i, f, c] over the nd dense rows and the F looked-up rows (an out-of-range
+// id is tf.one_hot's zero row), T_c = sum_f Fm[f, c], z = w0 + x.w +
+// 0.5 (sum_c T_c^2 - sum Fm^2); g = (sigmoid(z) - t)/B and the per-sample
+// gradient row G[f, c] = g (T_c - Fm[f, c]) (shared by the sample's looked-up
+// rows: dv[row] += G; dense rows: dv[i] += x_i G).  Fixed orders throughout.
+constexpr int FFMT_MAXE = 4096;  // NF * k
+template <int KIND>
+__global__ __launch_bounds__(256) void ffm_train_fwd_kernel(const void* ids, int64_t id_stride,
+                                                            const float* __restrict__ dense, int64_t ds, int nd,
+                                                            const float* __restrict__ v, const float* __restrict__ w,
+                                                            const float* __restrict__ w0,
+                                                            const int64_t* __restrict__ offs,
+                                                            const int64_t* __restrict__ vocab, int F, int k,
+                                                            const float* __restrict__ labels, int64_t B,
+                                                            float* __restrict__ G, float* __restrict__ g,
+                                                            float* __restrict__ loss) {
+  typedef Ids<KIND> I;
+  __shared__ float sfm[4][FFMT_MAXE];
+  __shared__ float st[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wv;
+  if (b >= B) return;  // wave-uniform
+  const int NF = nd + F, E = NF * k;
+  float* fm = sfm[wv];
+  float q = 0.f;  // sum Fm^2 (this lane's elements)
+  for (int e = lane; e < E; e += 64) {
+    float a = 0.f;
+    for (int i = 0; i < nd; ++i) a = fmaf(dense[b * ds + i], v[(int64_t)i * E + e], a);
+    for (int c = 0; c < F; ++c) {
+      int64_t id;
+      const bool ok = I::decode(I::load(ids, b * id_stride + c), vocab[c], id);
+      const int64_t row = nd + offs[c] + (ok ? id : 0);
+      const float x = v[row * E + e];
+      a += ok ? x : 0.f;
+    }
+    fm[e] = a;
+    q = fmaf(a, a, q);
+  }
+  // linear part: lanes over the dense features and the fields
+  float lin = 0.f;
+  for (int i = lane; i < nd + F; i += 64) {
+    if (i < nd) {
+      lin = fmaf(dense[b * ds + i], w[i], lin);
+    } else {
+      const int c = i - nd;
+      int64_t id;
+      const bool ok = I::decode(I::load(ids, b * id_stride + c), vocab[c], id);
+      const float x = w[nd + offs[c] + (ok ? id : 0)];
+      lin += ok ? x : 0.f;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  float tt = 0.f;  // T_c^2 for c = lane
+  if (lane < k) {
+    float T = 0.f;
+    for (int f = 0; f < NF; ++f) T += fm[f * k + lane];
+    st[wv][lane] = T;
+    tt = T * T;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    q += __shfl_xor(q, o);
+    lin += __shfl_xor(lin, o);
+    tt += __shfl_xor(tt, o);
+  }
+  const float z = (w0[0] + lin) + 0.5f * (tt - q);
+  const float t = labels[b];
+  const float gb = (1.f / (1.f + expf(-z)) - t) / (float)B;
+  if (lane == 0) {
+    g[b] = gb;
+    if (loss) loss[b] = fmaxf(z, 0.f) - z * t + log1pf(expf(-fabsf(z)));
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  for (int e = lane; e < E; e += 64) G[b * E + e] = gb * (st[wv][e % k] - fm[e]);
+}
+
+// Keras l2(l) regulariser's gradient on every row: w -= lr * 2 l w
+__global__ __launch_bounds__(256) void l2_decay_kernel(float* __restrict__ w, int64_t n, float f) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int64_t done = 0;
+  if ((n & 3) == 0 && ((uintptr_t)w & 15) == 0) {
+    floatx4* w4 = reinterpret_cast<floatx4*>(w);
+    for (int64_t q = t0; q < n / 4; q += stride) {
+      floatx4 x = __builtin_nontemporal_load(w4 + q);
+      x -= f * x;
+      __builtin_nontemporal_store(x, w4 + q);
+    }
+    done = n;
+  }
+  for (int64_t i = done + t0; i < n; i += stride) w[i] -= f * w[i];
+}
+
 // workspace layout (all 256-B aligned)
 struct TrainWs {
   int64_t g, s, contrib, key_in, key_out, val_in, val_out, gdense, part, sort, total;
@@ -325,4 +424,31 @@ extern "C" int rs_fm_train_step(const void* ids, int id_kind, int64_t id_stride,
   fm_train_apply<<<(unsigned)((ap + 255) / 256), 256, 0, st>>>(a);
   if (n > a.chunk) fm_train_apply_cross<<<(unsigned)((n * (k + 1) + 255) / 256), 256, 0, st>>>(a);
   return launch_status("rs_fm_train_step");
+}
+
+extern "C" int rs_ffm_train_fwd(const void* ids, int id_kind, int64_t id_stride, const float* dense,
+                                int64_t dense_stride, int nd, const float* v, const float* w, const float* w0,
+                                const int64_t* field_offsets, const int64_t* field_vocab, int n_fields, int k,
+                                const float* labels, int64_t batch, float* G, float* g, float* loss,
+                                rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(v && w && w0 && labels && G && g && batch > 0 && nd >= 0 && n_fields >= 1 && k >= 1 && k <= 64 &&
+                 (int64_t)(nd + n_fields) * k <= FFMT_MAXE && (nd == 0 || dense) && ids && field_offsets &&
+                 field_vocab && id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32,
+             "rs_ffm_train_fwd: bad arguments (k <= 64, (nd + n_fields) * k <= %d)", FFMT_MAXE);
+  hipStream_t st = as_stream(stream);
+  with_id_kind(id_kind, [&](auto K) {
+    ffm_train_fwd_kernel<decltype(K)::value><<<(unsigned)((batch + 3) / 4), 256, 0, st>>>(
+        ids, id_stride, dense, dense_stride, nd, v, w, w0, field_offsets, field_vocab, n_fields, k, labels, batch, G,
+        g, loss);
+  });
+  return launch_status("rs_ffm_train_fwd");
+}
+
+extern "C" int rs_l2_decay(float* w, int64_t n, float lr, float l2, rs_stream_t stream) {
+  if (n == 0 || l2 == 0.f) return RS_OK;
+  RS_REQUIRE(w && n > 0, "rs_l2_decay: bad arguments");
+  l2_decay_kernel<<<(unsigned)std::min<int64_t>((n / 4 + 255) / 256 + 1, 8192), 256, 0, as_stream(stream)>>>(
+      w, n, lr * 2.f * l2);
+  return launch_status("rs_l2_decay");
 }

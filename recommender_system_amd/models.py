@@ -1096,3 +1096,60 @@ class FFM(KerasModule):
 
     def forward(self, inputs):
         return self.ffm.logits(inputs, n_sigmoid=1)
+
+    def train_step(self, inputs, labels, lr=0.01, return_loss=False):
+        """One step of compile_fit on FFM (utils/compile_fit.py:9-15; the
+        reference's FFM demo trains this way, model/ffm.py:36): BCE on
+        sigmoid(FFMLayer) plus FFMLayer's l2(w_reg) / l2(v_reg) regularisers on
+        every row of w / v (layer/interaction.py:131-139), plain SGD:
+          rs_ffm_train_fwd (per sample: Fm, z, g and the shared gradient row
+          G = g (T - Fm)), rs_gemm / rs_col_sum (the dense rows' and w0's
+          gradients), rs_l2_decay (every row of w and v), rs_sgd_update (dense
+          rows, w0) and rs_embedding_sgd_strided (each looked-up row of v
+          gets its sample's G, of w its g; duplicates summed in lookup order).
+        Out-of-range ids train nothing (tf.one_hot's zero row).  Every
+        gradient comes from the pre-step weights.  Returns per-sample losses
+        (before the step) if ``return_loss``."""
+        L = self.ffm
+        if isinstance(inputs, (tuple, list)):
+            dense, ids = _to_device_f32(inputs[0], self._dev), _ids_tensor(inputs[1], self._dev)
+        else:
+            X = _to_device_f32(inputs, self._dev)
+            dense, ids = X[:, :L.nd], X[:, L.nd:]
+        labels = _to_device_f32(labels, self._dev).reshape(-1)
+        B, F, k, nd, st, dev = ids.shape[0], len(L.onehot_dims), L.k, L.nd, _lib.stream(), self._dev
+        E = L.field_num * k
+        emp = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=dev)
+        G, g = emp(B, E), emp(B)
+        loss = emp(B) if return_loss else None
+        call("rs_ffm_train_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), nd,
+             ptr(L.v), ptr(L.w), ptr(L.w0), ptr(L.field_offsets), ptr(L.field_vocab), F, k, ptr(labels), B, ptr(G),
+             ptr(g), ptr(loss), st)
+        gws = _gemm_ws(self, max(_lib.lib().rs_gemm_workspace_size(nd, E, B), _lib.lib().rs_gemm_workspace_size(nd, 1, B)))
+        gw = (ptr(gws), gws.numel())
+        dvd, dwd, dw0 = emp(max(nd, 1), E), emp(max(nd, 1)), emp(1)
+        if nd:
+            call("rs_gemm", 1, 0, nd, E, B, 1.0, ptr(dense), dense.stride(0), ptr(G), E, 0.0, ptr(dvd), E, None, 0,
+                 *gw, st)
+            call("rs_gemm", 1, 0, nd, 1, B, 1.0, ptr(dense), dense.stride(0), ptr(g), 1, 0.0, ptr(dwd), 1, None, 0,
+                 *gw, st)
+        call("rs_col_sum", ptr(g), 1, B, 1, ptr(dw0), st)
+        # l2 on every row (old weights), then the data gradients
+        call("rs_l2_decay", ptr(L.v), L.v.numel(), float(lr), float(L.v_reg), st)
+        call("rs_l2_decay", ptr(L.w), L.w.numel(), float(lr), float(L.w_reg), st)
+        if nd:
+            call("rs_sgd_update", ptr(L.v), ptr(dvd), nd * E, float(lr), 0.0, st)
+            call("rs_sgd_update", ptr(L.w), ptr(dwd), nd, float(lr), 0.0, st)
+        call("rs_sgd_update", ptr(L.w0), ptr(dw0), 1, float(lr), 0.0, st)
+        n_sparse = L.feature_num - nd
+        ws_n = _lib.lib().rs_embedding_sgd_workspace_size(B * F)
+        ws = self.__dict__.get("_emb_ws")
+        if ws is None or ws.numel() < ws_n:
+            ws = self.__dict__["_emb_ws"] = torch.empty(ws_n, dtype=torch.uint8, device=dev)
+        call("rs_embedding_sgd_strided", ptr(L.v) + 4 * nd * E, n_sparse, E, ptr(ids), _lib.id_kind(ids),
+             ids.stride(0), ptr(L.field_offsets), ptr(L.field_vocab), F, B, ptr(G), E, 0, float(lr), ptr(ws), None,
+             st)
+        call("rs_embedding_sgd_strided", ptr(L.w) + 4 * nd, n_sparse, 1, ptr(ids), _lib.id_kind(ids), ids.stride(0),
+             ptr(L.field_offsets), ptr(L.field_vocab), F, B, ptr(g), 1, 0, float(lr), ptr(ws), None, st)
+        self._weights_changed()
+        return loss

@@ -560,3 +560,36 @@ def test_nfm_train_step_gradient_matches_finite_differences():
     check(p["out"][1], new["out"][1], (0,))
     for j, idx in [(0, (2,)), (1, (4,))]:
         check(p["bn"][j], new["bn"][j], idx)
+
+
+def test_ffm_train_step_gradient_matches_finite_differences():
+    """oracle.ffm_train_step (compile_fit on FFM: BCE + l2(w_reg) on w + l2(v_reg)
+    on v, the field-aware interaction's G = g (T - Fm)) == central differences
+    of ffm_loss, on dense rows, looked-up rows (one repeated) and w0."""
+    rng = np.random.default_rng(41)
+    dims, nd, k = [3, 2, 4], 2, 3
+    NF, nfeat = nd + len(dims), nd + sum(dims)
+    w0 = np.array([0.1])
+    w = rng.normal(size=(nfeat, 1)) * 0.3
+    v = rng.normal(size=(nfeat, NF, k)) * 0.3
+    dense = rng.random((5, nd))
+    ids = np.array([[0, 1, 3], [2, 1, 0], [0, 0, 3], [1, 1, 2], [2, 0, 1]])
+    t = np.array([1.0, 0.0, 1.0, 0.0, 1.0])
+    l2w, l2v = 1e-2, 2e-2
+    (nw0, nw, nv), _ = O.ffm_train_step(dense, ids, t, w0, w, v, dims, 1.0, l2w, l2v)
+    eps = 1e-6
+
+    def check(arr, new_arr, idx):
+        keep = arr[idx]
+        arr[idx] = keep + eps
+        lp = O.ffm_loss(dense, ids, t, w0, w, v, dims, l2w, l2v)
+        arr[idx] = keep - eps
+        lm = O.ffm_loss(dense, ids, t, w0, w, v, dims, l2w, l2v)
+        arr[idx] = keep
+        assert abs((lp - lm) / (2 * eps) - (arr[idx] - new_arr[idx])) < 1e-6, idx
+
+    check(w0, nw0, (0,))
+    for idx in [(0, 0), (2, 0), (nd + 3, 0), (nfeat - 1, 0)]:
+        check(w, nw, idx)
+    for idx in [(1, 0, 2), (nd + 0, 3, 1), (nd + 3, 1, 0), (nfeat - 1, 4, 2), (nd + 2, 0, 0)]:
+        check(v, nv, idx)

@@ -548,3 +548,35 @@ def test_nfm_train_steps_match_oracle(gpu, B, k, hidden):
            "bn_beta": p["bn"][1], "dnn_hidden": p["dnn_hidden"], "dnn_out": p["dnn_out"], "out_kernel": p["out"][0],
            "out_bias": p["out"][1]}
     assert_scaled_close(m((dense, ids)), O.nfm(None, pin, inputs=(dense, ids))[0], what="forward after training")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,k,vmax", [(64, 4, 9), (300, 8, 40)])
+def test_ffm_train_steps_match_oracle(gpu, B, k, vmax):
+    """FFM.train_step (compile_fit on FFM: BCE + l2 on every row of w and v,
+    the per-sample shared gradient row G = g (T - Fm) scattered into the
+    looked-up rows, dense rows through rs_gemm) == oracle.ffm_train_step
+    (pinned by finite differences; one-hot formulation) over 3 steps with
+    repeated rows; the forward then runs on the trained weights."""
+    import recommender_system_amd as rs
+    from tests.helpers import criteo_columns
+    rng = np.random.default_rng(B + k)
+    vocab = rng.integers(1, vmax, 26)
+    m = rs.FFM(criteo_columns(vocab), k, w_reg=1e-3, v_reg=2e-3, seed=7)
+    L = m.ffm
+    c = lambda t: t.detach().cpu().numpy().astype(np.float64)
+    w0, w, v = c(L.w0), c(L.w), c(L.v)
+    lr = 0.5
+    for step in range(3):
+        dense = rng.random((B, 13)).astype(np.float32)
+        ids = np.stack([rng.integers(0, v_, B) for v_ in vocab], 1).astype(np.int32)
+        ids[:9, 2] = 0  # repeated rows
+        t = rng.integers(0, 2, B).astype(np.float32)
+        loss = m.train_step((dense, ids), t, lr=lr, return_loss=True)
+        (w0, w, v), ce = O.ffm_train_step(dense, ids, t, w0, w, v, list(vocab), lr, 1e-3, 2e-3)
+        assert_scaled_close(loss, ce, what=f"step {step} loss")
+        assert_scaled_close(L.w0, w0, rtol=1e-4, what=f"step {step} w0")
+        assert_scaled_close(L.w, w, what=f"step {step} w")
+        assert_scaled_close(L.v, v, what=f"step {step} v")
+    y = m((dense, ids))
+    assert_scaled_close(y, O.sigmoid(O.ffm_layer(dense, ids, list(vocab), w0, w, v)), what="forward after training")
