@@ -973,10 +973,8 @@ extern "C" int rs_embedding_sgd(float* table, int64_t n_rows, int k, const void*
                                 const int64_t* field_offsets, const int64_t* field_vocab, int n_fields,
                                 int64_t batch, const float* grad, int64_t grad_stride, float lr, void* workspace,
                                 int* err_flag, rs_stream_t stream) {
-  if (grad_stride < (int64_t)n_fields * k) {
-    set_error("rs_embedding_sgd: bad arguments");
-    return RS_ERR_ARG;
-  }
+  if (batch * n_fields == 0) return RS_OK;
+  RS_REQUIRE(grad_stride >= (int64_t)n_fields * k, "rs_embedding_sgd: bad arguments");
   return rs_embedding_sgd_strided(table, n_rows, k, ids, id_kind, id_stride, field_offsets, field_vocab, n_fields,
                                   batch, grad, grad_stride, k, lr, workspace, err_flag, stream);
 }
