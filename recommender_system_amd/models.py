@@ -28,9 +28,10 @@ sets the embedding width: the reference ignores feat['embed_dim'] and always
 uses k=8 (layer/core.py:268-271), so 8 is the drop-in behaviour.
 
 PNN runs with 3-D embeddings [B,F,k] (documented deviation: the reference's
-rank-2 EmbedLayer makes PNN.call raise at model/pnn.py:38).  Modes 'outer' /
-'both' and use_fgcnn=True are outside this build's hot path and raise
-NotImplementedError; an unknown mode raises the reference's ValueError.
+rank-2 EmbedLayer makes PNN.call raise at model/pnn.py:38).  Modes 'inner',
+'outer' and 'both' are built (forward and training); use_fgcnn=True is
+outside this build's hot path and raises NotImplementedError; an unknown mode
+raises the reference's ValueError.
 """
 from __future__ import annotations
 
