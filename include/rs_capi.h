@@ -260,8 +260,8 @@ int rs_din_attention_ids_fwd(const void* hist, int id_kind, int64_t hist_stride,
                              const void* cand, int64_t cand_stride, int T,
                              int k, const float* table, int64_t vocab, int H1,
                              int H2, const float* prepared, float* scores,
-                             float* out, int64_t batch, int* err_flag,
-                             rs_stream_t stream);
+                             float* out, int64_t out_stride, int64_t batch,
+                             int* err_flag, rs_stream_t stream);
 
 /* --------------------------------------------------- dense tower (a7, a15)
  * Keras Dense: y = act(x @ W + bias), W:[K,N] (Keras (in,out) orientation),

@@ -128,7 +128,8 @@ struct DinArgs {
   DinGeom g;
   int64_t spc;    // samples per workgroup (din_scores)
   float* scores;  // [B, T] workspace
-  float* out;     // [B, k]
+  float* out;     // [B, k], rows ldo floats apart
+  int64_t ldo;
   int64_t batch;
   int* err;
   unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_din_set_dbg)
@@ -387,7 +388,7 @@ __global__ __launch_bounds__(256) void din_pool(DinArgs a) {
   for (; t < T; t += ntg) acc[0] = fmaf(es[w][t], a.table[(int64_t)rs_[w][t] * k + j], acc[0]);
   float v = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   for (int o = k; o < 64; o <<= 1) v += __shfl_xor(v, o);
-  if (lane < k) a.out[b * k + lane] = v / sum;
+  if (lane < k) a.out[b * a.ldo + lane] = v / sum;
 }
 
 template <int KS, int HT1M, int HT2M, int KIND, bool EXACT>
@@ -439,7 +440,7 @@ extern "C" int rs_din_prepare(const float* W1, const float* b1, const float* alp
 extern "C" int rs_din_attention_ids_fwd(const void* hist, int id_kind, int64_t hist_stride, const void* cand,
                                         int64_t cand_stride, int T, int k, const float* table, int64_t vocab,
                                         int H1, int H2, const float* prepared, float* scores, float* out,
-                                        int64_t batch, int* err_flag, rs_stream_t stream) {
+                                        int64_t out_stride, int64_t batch, int* err_flag, rs_stream_t stream) {
   if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(rs_din_prepared_size(T, k, H1, H2) > 0,
              "rs_din_attention_ids_fwd: need k in {4,8,16}, H1 <= 128, H2 <= 64");
@@ -448,9 +449,10 @@ extern "C" int rs_din_attention_ids_fwd(const void* hist, int id_kind, int64_t h
   RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32 && vocab >= 1 && batch >= 0 && hist_stride >= T,
              "rs_din_attention_ids_fwd: bad ids / shape");
   RS_REQUIRE((uintptr_t)table % 16 == 0, "rs_din_attention_ids_fwd: table must be 16-B aligned");
+  RS_REQUIRE(out_stride >= k, "rs_din_attention_ids_fwd: out_stride < k");
   if (batch == 0) return RS_OK;
   DinArgs a{hist, hist_stride, cand, cand_stride, table, vocab, prepared, din_geom(T, k, H1, H2),
-            0, scores, out, batch, err_flag, g_din_dbg};
+            0, scores, out, out_stride, batch, err_flag, g_din_dbg};
   hipStream_t st = as_stream(stream);
   with_id_kind(id_kind, [&](auto K) {
     constexpr int KIND = decltype(K)::value;

@@ -632,11 +632,24 @@ class BatchNormalization(KerasModule):
             for name, p in self.keras_weights().items():
                 p.copy_(torch.as_tensor(weights[name], dtype=torch.float32).reshape(-1))
 
+    def _invalidate(self):
+        self._aff_key = None  # statistics / affine moved through raw pointers (training)
+
+    def affine(self):
+        """(inv, shift) = (gamma rsqrt(var + eps), beta - mean inv), cached per
+        parameter version (inference calls launch no elementwise kernels)."""
+        ps = (self.gamma, self.beta, self.moving_mean, self.moving_variance)
+        key = tuple((q._version, q.data_ptr()) for q in ps)
+        if getattr(self, "_aff_key", None) != key:
+            inv = torch.rsqrt(self.moving_variance + self.epsilon) * self.gamma
+            self._aff = (inv, self.beta - self.moving_mean * inv)
+            self._aff_key = key
+        return self._aff
+
     def forward(self, x, out=None):
         if self.gamma is None:
             self.build(x.shape[-1])
-        inv = torch.rsqrt(self.moving_variance + self.epsilon) * self.gamma
-        shift = self.beta - self.moving_mean * inv
+        inv, shift = self.affine()
         M, N = x.shape
         if out is None:
             out = torch.empty_like(x)
@@ -733,8 +746,8 @@ class Attention(KerasModule):
             raise ValueError("forward_ids: scores workspace needs B*T elements")
         h1, h2 = self.hidden_units
         call("rs_din_attention_ids_fwd", ptr(hist), _lib.id_kind(hist), hist.stride(0), ptr(cand),
-             cand.stride(0), T, k, ptr(table), vocab, h1, h2, ptr(self.prepared_ids(k)), ptr(scores), ptr(out), B,
-             ptr(err), _stream())
+             cand.stride(0), T, k, ptr(table), vocab, h1, h2, ptr(self.prepared_ids(k)), ptr(scores), ptr(out),
+             out.stride(0), B, ptr(err), _stream())
         return out
 
     def keras_weights(self):

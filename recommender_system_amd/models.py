@@ -722,26 +722,28 @@ class DIN(TowerMixin, KerasModule):
         if cand.shape[1] != nb:
             raise ValueError(f"DIN: inputs['movie_id'] needs one candidate id per behaviour feature ({nb})")
         K = sum(l.k for l in self.embed_seq_layers)
-        item_embed = self._behaviour_embed([cand[:, i:i + 1] for i in range(nb)], B, check_ids)
+        other_k = sum(l.k for l in self.embed_sparse_layers)
+        width = 2 * K + other_k + self.dense_num
+        emb = torch.empty(B, width, dtype=torch.float32, device=dev)
         if self.att_layer.out_kernel is None:
             self.att_layer.build(T, K)
         if nb == 1 and self.att_layer.ids_ok(K):
-            # keys/values read through the ids from the (L2-resident) table
+            # keys/values read through the ids from the (L2-resident) table; the
+            # candidate rows go straight into emb (the attention reads the ids)
             seq_layer = self.embed_seq_layers[0]
-            att_emb = self.att_layer.forward_ids(seq_layer.table, int(seq_layer.vocab_sizes[0]), hists[0], cand,
-                                                 err=self._err.t)
+            seq_layer.gather(cand, out=emb[:, K:2 * K], check_ids=check_ids)
+            self.att_layer.forward_ids(seq_layer.table, int(seq_layer.vocab_sizes[0]), hists[0], cand,
+                                       err=self._err.t, out=emb[:, :K])  # pooled rows straight into emb
             if check_ids:
                 self._err.check("DIN")
         else:
+            item_embed = self._behaviour_embed([cand[:, i:i + 1] for i in range(nb)], B, check_ids)
             seq_embed = self._behaviour_embed([h.reshape(B * T, 1) for h in hists], B * T, check_ids)
             seq_embed = seq_embed.view(B, T, K)
             mask = (hists[0] != 0).to(torch.float32)  # model/din.py:80: the first behaviour feature
             att_emb = self.att_layer([item_embed, seq_embed, seq_embed, mask])
-        other_k = sum(l.k for l in self.embed_sparse_layers)
-        width = 2 * K + other_k + self.dense_num
-        emb = torch.empty(B, width, dtype=torch.float32, device=dev)
-        emb[:, :K] = att_emb
-        emb[:, K:2 * K] = item_embed
+            emb[:, K:2 * K] = item_embed
+            emb[:, :K] = att_emb
         col = 2 * K
         for f, layer in zip(self.other_sparse, self.embed_sparse_layers):
             ids = _ids_tensor(inputs[f["feat"]], dev).reshape(B, 1)
