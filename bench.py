@@ -868,7 +868,7 @@ def bench_din(args, world, rank):
         model.train_step(pool[i % 8], labels[i % 8], lr=0.01, check_ids=False)
 
     nt = max(10, args.steps // 10)
-    tdt, _ = _timed(train, nt, 2, world, events=False)
+    tdt, ttiming = _train_timed(train, nt, world)
     return _line("DIN forward samples/sec @ batch 2048, behaviour seq len 100 (attention unit)",
                  args.steps * B / dt, "samples/s", args, world, att_ms,
                  {"workload": "din_attention_unit_from_ids", "global_batch": B, "seq_len": T, "embed_dim": k,
@@ -886,7 +886,7 @@ def bench_din(args, world, rank):
                                   "note": "graph-replayed full DIN.call (id checks off): gathers, attention "
                                           "from ids, BN, PReLU MLP + sigmoid head"},
                   "train_step": {"samples_per_s": nt * B / tdt, "ms_per_step": tdt / nt * 1e3,
-                                 "timing": "eager launches",
+                                 "timing": ttiming,
                                  "note": "DIN.train_step: gathers, attention Dense+PReLU layers over [B*T] rows, "
                                          "masked softmax pool, training-mode BN, PReLU DNN, full backward, SGD + "
                                          "row-sparse embedding SGD"},
@@ -946,7 +946,7 @@ def bench_pnn(args, world, rank):
         model.train_step((dense_pool[i % 64], ids_pool[i % 64]), labels[i % 16], lr=0.01, check_ids=False)
 
     nt = max(10, args.steps // 10)
-    tdt, _ = _timed(train, nt, 2, world, events=False)
+    tdt, ttiming = _train_timed(train, nt, world)
     return _line("PNN inner-product input samples/sec @ batch 4096, 26 sparse x 1e6 vocab, dim 16",
                  args.steps * B / dt, "samples/s", args, world, dt / args.steps * 1e3,
                  {"workload": "pnn_embed_inner_fused", "global_batch": B, "vocab_per_field": V, "parallelism": "dp1"},
@@ -959,7 +959,7 @@ def bench_pnn(args, world, rank):
                   "pnn_inner_forward": {"samples_per_s": n2 * B / dtf, "ms_per_step": dtf / n2 * 1e3,
                                         "note": "product inputs + DNN tower (rs_mlp_fwd, K = 741)"},
                   "train_step": {"samples_per_s": nt * B / tdt, "ms_per_step": tdt / nt * 1e3,
-                                 "timing": "eager launches",
+                                 "timing": ttiming,
                                  "note": "PNN.train_step (mode 'inner', model/pnn.py:74-81): [flat | inner], DNN "
                                          "fwd/bwd, Keras-broadcast BCE on the logit, inner-product backward, SGD + "
                                          "row-sparse embedding SGD"},
@@ -1128,14 +1128,14 @@ def bench_ffm(args, world, rank):
         m.train_step((dense_pool[i % 64], ids_pool[i % 64]), labels[i % 16], lr=0.01)
 
     nt = max(5, args.steps // 20)
-    tdt, _ = _timed(train, nt, 1, world, events=False)
+    tdt, ttiming = _train_timed(train, nt, world)
     vbytes = (13 + F * V) * NF * k * 4
     return _hbm_line("FFM forward samples/sec @ batch 4096, 26 sparse x 1e6 vocab, k 8", args, world, B, dt, slot,
                      alg, "ffm_fused", V, "ffm4_kernel",
                      {"table_GB": (13 + F * V) * NF * k * 4 / 1e9, "cpu_baseline": cpu,
                       "train_step": {"samples_per_s": nt * B / tdt, "ms_per_step": tdt / nt * 1e3,
                                      "l2_decay_hbm_frac": 2 * vbytes / (tdt / nt) / PEAK_HBM,
-                                     "timing": "eager launches",
+                                     "timing": ttiming,
                                      "note": "FFM.train_step: rs_ffm_train_fwd, dense-row rs_gemm, l2 decay of every "
                                              "row of w and v (2 x table bytes), row-sparse SGD of the looked-up rows"}})
 
@@ -1292,6 +1292,19 @@ def bench_fm_train(args, world, rank):
                   "reference_scale": {"steps_per_s": args.steps / dts, "ms_per_step": dts / args.steps * 1e3,
                                       "note": "batch 32, 26 x 1,677 + 13 = 43,615 columns, k 8 (compile_fit's "
                                               "defaults on the bundled sample's width)"}})
+
+
+def _train_timed(fn, n, world):
+    """A single-GPU training step timed from HIP graphs of its launches when
+    it captures (every launch is stream-ordered, no host sync inside), else
+    eager; returns (seconds, timing label)."""
+    try:
+        dt, _ = _timed_graph(fn, n, 2, world, chunk=min(n, 8))
+        return dt, "HIP graph replay"
+    except Exception as e:  # noqa: BLE001 - a step that does not capture is timed eagerly
+        torch.cuda.synchronize()
+        dt, _ = _timed(fn, n, 2, world, events=False)
+        return dt, f"eager launches ({type(e).__name__})"
 
 
 def _pmc_cfg(cfg):
