@@ -248,8 +248,9 @@ int rs_din_attention_gen_fwd(const float* query, const float* keys,
  * tile's PReLU alphas and W2 staged once per workgroup, layer 1 regrouped per
  * sample as q(Wq+Wd) + key(Wk-Wd+diag(q)Wp)) then the masked softmax pool.
  * prepared: rs_din_prepare (k in {4,8,16}, H1 <= 128, H2 <= 64); scores: a
- * caller-owned [B, T] fp32 workspace; out [B, k].  T <= 1024.  OOR ids set
- * *err_flag.                                                               */
+ * caller-owned [B, T] fp32 workspace; out [B, k] with rows out_stride
+ * floats apart (>= k: DIN.call writes straight into its concat).  T <= 1024.
+ * OOR ids set *err_flag.                                                   */
 int64_t rs_din_prepared_size(int T, int k, int H1, int H2);
 int rs_din_prepare(const float* W1, const float* b1, const float* alpha1,
                    int H1, const float* W2, const float* b2,
