@@ -442,6 +442,13 @@ int rs_col_sum_split(const float* A, int64_t lda, int64_t M, int64_t N,
                      rs_stream_t stream);
 int rs_sgd_update(float* w, const float* grad, int64_t n, float lr, float l2,
                   rs_stream_t stream);
+/* rs_sgd_update over `count` tensors (host arrays of device pointers, sizes
+ * and per-tensor l2) in one launch per 32 tensors: the optimizer step of a
+ * model's dense parameters (Keras' SGD.apply_gradients over the variable
+ * list, utils/compile_fit.py:11 / model/pnn.py:81), same arithmetic.       */
+int rs_sgd_update_multi(int count, float* const* w, const float* const* grad,
+                        const int64_t* n, const float* l2, float lr,
+                        rs_stream_t stream);
 int rs_head_grad(const float* fm, const float* dnn, const float* labels,
                  int64_t batch, float c_fm, float c_dnn, float* g_fm,
                  float* g_dnn, float* loss, rs_stream_t stream);
@@ -520,6 +527,35 @@ int rs_prelu_rows_bwd(const float* z, const float* dy, int64_t M, int N,
                       const float* alpha, int period, float* dz,
                       float* dalpha, void* workspace, int64_t workspace_bytes,
                       rs_stream_t stream);
+/* rs_din_att_prelu_bwd: the whole backward of the PReLU attention unit
+ * with two hidden layers (layer/interaction.py:366-395; default (80, 40)) in
+ * one launch + a fixed-order partial sum: from h0 [B*T, K0] (the concat
+ * [q, k, q-k, q*k]), the pre-activations z1 [B*T, h1], z2 [B*T, h2], ds
+ * [B*T] (dL/dscore), the kernels W1 [K0, h1], W2 [h1, h2], the PReLU alphas
+ * [T, h1] / [T, h2] and the score kernel wo [h2], writes dh0 [B*T, K0] and
+ * dW1, db1, dalpha1, dW2, db2, dalpha2, dwo [h2], dbo [1].  Shapes with T,
+ * K0, h1, h2 <= 128, multiples of 4, whose sample fits in LDS:
+ * rs_din_att_prelu_bwd_workspace_size returns -1 for the others.           */
+/* rs_din_att_prelu_fwd: the unit's forward under fit for the same shapes:
+ * z1 = h0 W1 + b1, z2 = prelu(z1; alpha1) W2 + b2 (kept for the backward),
+ * score = prelu(z2; alpha2) wo + bo [B*T], one launch.                      */
+int rs_din_att_prelu_fwd(const float* h0, const float* W1, const float* b1,
+                         const float* alpha1, const float* W2,
+                         const float* b2, const float* alpha2,
+                         const float* wo, const float* bo, int64_t batch,
+                         int T, int K0, int h1, int h2, float* z1, float* z2,
+                         float* score, rs_stream_t stream);
+int64_t rs_din_att_prelu_bwd_workspace_size(int64_t batch, int T, int K0,
+                                            int h1, int h2);
+int rs_din_att_prelu_bwd(const float* h0, const float* z1, const float* z2,
+                         const float* ds, const float* W1, const float* W2,
+                         const float* alpha1, const float* alpha2,
+                         const float* wo, int64_t batch, int T, int K0, int h1,
+                         int h2, float* dh0, float* dW1, float* db1,
+                         float* dalpha1, float* dW2, float* db2,
+                         float* dalpha2, float* dwo, float* dbo,
+                         void* workspace, int64_t workspace_bytes,
+                         rs_stream_t stream);
 int rs_masked_softmax_pool(const float* score, const void* hist,
                            int hist_kind, int64_t hist_stride,
                            const float* seq, int64_t batch, int T, int K,

@@ -77,6 +77,7 @@ SIGNATURES = {
     "rs_gemm": (I, [I, I, L, L, L, F, P, L, P, L, F, P, L, P, L, P, L, P]),
     "rs_col_sum": (I, [P, L, L, L, P, P]),
     "rs_sgd_update": (I, [P, P, L, F, F, P]),
+    "rs_sgd_update_multi": (I, [I, P, P, P, P, F, P]),
     "rs_head_grad": (I, [P, P, P, L, F, F, P, P, P, P]),
     "rs_head_grad_scaled": (I, [P, P, P, L, F, F, F, P, P, P, P]),
     "rs_bce_prob_grad": (I, [P, L, P, L, P, P, P]),
@@ -89,6 +90,9 @@ SIGNATURES = {
     "rs_prelu_rows_fwd": (I, [P, L, I, P, I, P, P]),
     "rs_prelu_rows_bwd_workspace_size": (L, [L, I, I]),
     "rs_prelu_rows_bwd": (I, [P, P, L, I, P, I, P, P, P, L, P]),
+    "rs_din_att_prelu_fwd": (I, [P, P, P, P, P, P, P, P, P, L, I, I, I, I, P, P, P, P]),
+    "rs_din_att_prelu_bwd_workspace_size": (L, [L, I, I, I, I]),
+    "rs_din_att_prelu_bwd": (I, [P, P, P, P, P, P, P, P, P, L, I, I, I, I, P, P, P, P, P, P, P, P, P, P, L, P]),
     "rs_col_sum_workspace_size": (L, [L, L]),
     "rs_col_sum_split": (I, [P, L, L, L, P, P, L, P]),
     "rs_masked_softmax_pool": (I, [P, P, I, L, P, L, I, I, P, P, L, P]),
@@ -178,6 +182,19 @@ def ptr(t) -> int | None:
     if not t.is_cuda:
         raise RSError("librs_hip kernels need device (HIP) tensors; got a CPU tensor")
     return t.data_ptr()
+
+
+def sgd_update_multi(updates, lr, st) -> None:
+    """One rs_sgd_update_multi launch for [(w, grad, n, l2)] (w / grad device
+    tensors or raw pointers; n elements; l2 the Keras l2 factor)."""
+    if not updates:
+        return
+    cnt = len(updates)
+    ws = (C.c_void_p * cnt)(*[u[0] if isinstance(u[0], int) else ptr(u[0]) for u in updates])
+    gs = (C.c_void_p * cnt)(*[u[1] if isinstance(u[1], int) else ptr(u[1]) for u in updates])
+    ns = (C.c_int64 * cnt)(*[int(u[2]) for u in updates])
+    l2 = (C.c_float * cnt)(*[float(u[3]) for u in updates])
+    call("rs_sgd_update_multi", cnt, ws, gs, ns, l2, float(lr), st)
 
 
 def stream(device=None) -> int:

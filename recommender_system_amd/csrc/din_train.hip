@@ -408,6 +408,566 @@ static unsigned dt_grid(int64_t n) {
   return (unsigned)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
 }
 
+// ---------------------------------------------------------------------------
+// Fused backward of the PReLU attention unit (layer/interaction.py:366-395 with
+// two hidden Dense+PReLU layers, the reference default (80, 40)): from the
+// saved h0 = [q, k, q-k, q*k] [B*T, K0], the pre-activations z1 [B*T, h1], z2
+// [B*T, h2] and dL/dscore ds [B*T]:
+//   dy2 = ds wo^T, dz2 = dy2 prelu'(z2), dy1 = dz2 W2^T, dz1 = dy1 prelu'(z1),
+//   dh0 = dz1 W1^T, and the parameter gradients dW1 = h0^T dz1, dW2 =
+//   y1^T dz2, dwo = y2^T ds, biases = column sums, dalpha[t] = sum over the
+//   batch of dy min(z, 0).
+// One workgroup (8 waves) per sample at a time: the sample's T rows (padded
+// to Rp = 16 * ceil(T/16)) sit in LDS; the four products run on MFMA
+// 16x16x4 f32 tiles; the weight gradients stay in MFMA accumulators across
+// the workgroup's samples, the layer-2 elementwise sums in registers of the
+// thread that owns each element, so every sum runs in a fixed order.  The
+// next sample's h0 / z1 / z2 / ds are loaded into registers (float4, every
+// load issued at once) while the current one runs its products.  The
+// per-workgroup partials are then summed in workgroup order (fin kernel).
+constexpr int AB_NW = 8;  // waves per workgroup
+struct AttBwdArgs {
+  const float *h0, *z1, *z2, *ds, *W1, *W2, *al1, *al2, *wo;
+  int64_t B;
+  int T, K0, h1, h2, Rp, K0p, h1p, h2p;
+  int sW1, sW2, sH0, sY1, sZ2;                 // LDS row strides (odd; z1 / dz1 use sY1)
+  int oW1, oW2, oH0, oY1, oZ1, oZ2, oDS, oWo;  // LDS offsets (floats)
+  int lds_floats;
+  int64_t P;                                   // partial floats per workgroup
+  int64_t pW1, pW2, pA1, pA2, pB1, pB2, pWo, pBo;  // partial layout
+  float* dh0;
+  float* part;
+};
+
+__device__ __forceinline__ floatx4 ab_ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
+
+// c += sum over k < n (n % 16 == 0) of the 16x16x4 MFMA steps whose operands
+// are pa[k * sa] / pb[k * sb] (k = 0, 4, 8, ...): the next 4 steps' LDS reads
+// are issued before the current 4 MFMAs (the last group re-reads in bounds)
+__device__ __forceinline__ floatx4 ab_mfma_loop(const float* pa, int sa, const float* pb, int sb, int n, floatx4 c) {
+  float a0[4], b0[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    a0[u] = pa[4 * u * sa];
+    b0[u] = pb[4 * u * sb];
+  }
+  for (int k = 0; k < n; k += 16) {
+    const int kn = min(k + 16, n - 16);
+    float a1[4], b1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a1[u] = pa[(kn + 4 * u) * sa];
+      b1[u] = pb[(kn + 4 * u) * sb];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) c = mfma16x16x4(a0[u], b0[u], c);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a0[u] = a1[u];
+      b0[u] = b1[u];
+    }
+  }
+  return c;
+}
+
+// SA / SB / SC: tile slots per wave (ceil(tiles / AB_NW)) of the dy1, dW2
+// and dW1 products; V0 / V1 / V2: float4 vectors per thread of a sample's
+// h0 / z1 / z2 block
+template <int SA, int SB, int SC, int V0, int V1, int V2>
+__global__ __launch_bounds__(512) void din_att_bwd_kernel(const AttBwdArgs a) {
+  extern __shared__ float sm[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, lg = lane >> 4;
+  const int T = a.T, K0 = a.K0, h1 = a.h1, h2 = a.h2;
+  const int n0 = T * K0, n1 = T * h1, n2 = T * h2;
+  float *sW1 = sm + a.oW1, *sW2 = sm + a.oW2, *sH0 = sm + a.oH0, *sY1 = sm + a.oY1, *sZ1 = sm + a.oZ1;
+  float *sZ2 = sm + a.oZ2, *sWo = sm + a.oWo;
+  // zero every region once (pads stay zero: nothing writes them except as 0)
+  for (int e = tid; e < a.lds_floats; e += 512) sm[e] = 0.f;
+  __syncthreads();
+  for (int e = tid; e < K0 * h1; e += 512) {
+    const int k = e / h1;
+    sW1[k * a.sW1 + (e - k * h1)] = a.W1[e];
+  }
+  for (int e = tid; e < h1 * h2; e += 512) {
+    const int i = e / h2;
+    sW2[i * a.sW2 + (e - i * h2)] = a.W2[e];
+  }
+  for (int j = tid; j < h2; j += 512) sWo[j] = a.wo[j];
+  const int RT = a.Rp >> 4, IT = a.h1p >> 4, JT = a.h2p >> 4, KT = a.K0p >> 4;
+  const int Ta = RT * IT, Tb = IT * JT, Tc = KT * IT, Td = RT * KT;
+  floatx4 accB[SB], accC[SC], accA[SA];
+  float s1[SA];
+#pragma unroll
+  for (int s = 0; s < SB; ++s) accB[s] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < SC; ++s) accC[s] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < SA; ++s) {
+    accA[s] = floatx4{0.f, 0.f, 0.f, 0.f};
+    s1[s] = 0.f;
+  }
+  // the alphas of this lane's dy1 tile elements (the same for every sample)
+  float al[SA][4];
+#pragma unroll
+  for (int s = 0; s < SA; ++s) {
+    const int rt = (w + s * AB_NW) / IT, i = min((w + s * AB_NW - rt * IT) * 16 + l16, h1 - 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) al[s][r] = a.al1[min(rt * 16 + 4 * lg + r, T - 1) * h1 + i];
+  }
+  // this thread's elements (4 consecutive floats of one row, fixed for every
+  // sample): their alphas / score weights and the layer-2 sums
+  floatx4 al1v[V1], al2v[V2], sA2[V2], sSW[V2], sS2[V2];
+  const floatx4 zero4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < V1; ++i) {
+    const int e = 4 * (tid + 512 * i);
+    al1v[i] = e < n1 ? ab_ld4(a.al1 + e) : zero4;
+  }
+#pragma unroll
+  for (int i = 0; i < V2; ++i) {
+    const int e = 4 * (tid + 512 * i);
+    al2v[i] = e < n2 ? ab_ld4(a.al2 + e) : zero4;
+    sA2[i] = sSW[i] = sS2[i] = zero4;
+  }
+  float dbo = 0.f;  // sum of ds over the rows whose (t, 0) element this thread owns
+  // every load above has landed before the loop: inside it only the
+  // prefetches below are outstanding (vmcnt counts in order)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+
+  // the next sample's inputs, every load unconditional at a clamped address
+  floatx4 ph0[V0], pz1[V1], pz2[V2];
+  float pds[V2];
+  auto prefetch = [&](int64_t b) {
+    const int64_t r0 = b * T;
+#pragma unroll
+    for (int i = 0; i < V0; ++i) ph0[i] = ab_ld4(a.h0 + r0 * K0 + min(4 * (tid + 512 * i), n0 - 4));
+#pragma unroll
+    for (int i = 0; i < V1; ++i) pz1[i] = ab_ld4(a.z1 + r0 * h1 + min(4 * (tid + 512 * i), n1 - 4));
+#pragma unroll
+    for (int i = 0; i < V2; ++i) {
+      const int e = min(4 * (tid + 512 * i), n2 - 4);
+      pz2[i] = ab_ld4(a.z2 + r0 * h2 + e);
+      pds[i] = a.ds[r0 + e / h2];
+    }
+  };
+  if ((int64_t)blockIdx.x < a.B) prefetch(blockIdx.x);
+
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    __syncthreads();  // the previous sample's readers are done
+    const int64_t r0 = b * T;
+    // stage h0, z1, y1 = prelu(z1); layer 2 + the score Dense elementwise
+#pragma unroll
+    for (int i = 0; i < V0; ++i) {
+      const int e = 4 * (tid + 512 * i);
+      if (e < n0) {
+        const int t = e / K0;
+        float* d = sH0 + t * a.sH0 + (e - t * K0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = ph0[i][q];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < V1; ++i) {
+      const int e = 4 * (tid + 512 * i);
+      if (e < n1) {
+        const int t = e / h1, o = t * a.sY1 + (e - t * h1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float z = pz1[i][q];
+          sZ1[o + q] = z;
+          sY1[o + q] = fmaxf(z, 0.f) + al1v[i][q] * fminf(z, 0.f);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < V2; ++i) {
+      const int e = 4 * (tid + 512 * i);
+      if (e < n2) {
+        const int t = e / h2, o = t * a.sZ2 + (e - t * h2);
+        const float dsv = pds[i];
+        const floatx4 wv = ab_ld4(sWo + (e - t * h2));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float z = pz2[i][q], al = al2v[i][q];
+          const float dy = dsv * wv[q], mn = fminf(z, 0.f);
+          const float dz = z > 0.f ? dy : dy * al;
+          sA2[i][q] += dy * mn;
+          sSW[i][q] += (fmaxf(z, 0.f) + al * mn) * dsv;
+          sS2[i][q] += dz;
+          sZ2[o + q] = dz;
+        }
+        if (e - t * h2 == 0) dbo += dsv;
+      }
+    }
+    // the next sample's loads fly during this sample's products
+    if (b + gridDim.x < a.B) prefetch(b + gridDim.x);
+    __syncthreads();
+    // dW2 += y1^T dz2   (tile (it, jt); k runs over the sample's rows)
+#pragma unroll
+    for (int s = 0; s < SB; ++s) {
+      const int q = w + s * AB_NW;
+      if (q < Tb) {
+        const int it = q / JT, jt = q - it * JT;
+        const float* pa = sY1 + lg * a.sY1 + it * 16 + l16;
+        const float* pb = sZ2 + lg * a.sZ2 + jt * 16 + l16;
+        accB[s] = ab_mfma_loop(pa, a.sY1, pb, a.sZ2, a.Rp, accB[s]);
+      }
+    }
+    // dy1 = dz2 W2^T -> dz1 (in z1's place: each element read and rewritten
+    // by its own lane), dalpha1, db1
+#pragma unroll
+    for (int s = 0; s < SA; ++s) {
+      const int q = w + s * AB_NW;
+      if (q < Ta) {
+        const int rt = q / IT, it = q - rt * IT;
+        const float* pa = sZ2 + (rt * 16 + l16) * a.sZ2 + lg;
+        const float* pb = sW2 + (it * 16 + l16) * a.sW2 + lg;
+        const floatx4 c = ab_mfma_loop(pa, 1, pb, 1, a.h2p, floatx4{0.f, 0.f, 0.f, 0.f});
+        const int i = it * 16 + l16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int t = rt * 16 + 4 * lg + r;
+          float* zp = sZ1 + t * a.sY1 + i;
+          float dz = 0.f;
+          if (t < T && i < h1) {
+            const float z = *zp, dy = c[r];
+            dz = z > 0.f ? dy : dy * al[s][r];
+            accA[s][r] += dy * fminf(z, 0.f);
+            s1[s] += dz;
+          }
+          *zp = dz;
+        }
+      }
+    }
+    __syncthreads();
+    // dW1 += h0^T dz1
+#pragma unroll
+    for (int s = 0; s < SC; ++s) {
+      const int q = w + s * AB_NW;
+      if (q < Tc) {
+        const int kt = q / IT, it = q - kt * IT;
+        const float* pa = sH0 + lg * a.sH0 + kt * 16 + l16;
+        const float* pb = sZ1 + lg * a.sY1 + it * 16 + l16;
+        accC[s] = ab_mfma_loop(pa, a.sH0, pb, a.sY1, a.Rp, accC[s]);
+      }
+    }
+    // dh0 = dz1 W1^T
+    for (int q = w; q < Td; q += AB_NW) {
+      const int rt = q / KT, kt = q - rt * KT;
+      const float* pa = sZ1 + (rt * 16 + l16) * a.sY1 + lg;
+      const float* pb = sW1 + (kt * 16 + l16) * a.sW1 + lg;
+      const floatx4 c = ab_mfma_loop(pa, 1, pb, 1, a.h1p, floatx4{0.f, 0.f, 0.f, 0.f});
+      const int col = kt * 16 + l16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = rt * 16 + 4 * lg + r;
+        if (t < T && col < K0) a.dh0[(r0 + t) * K0 + col] = c[r];
+      }
+    }
+  }
+
+  // this workgroup's partial sums
+  __syncthreads();
+  float* part = a.part + blockIdx.x * a.P;
+  float* sS1 = sY1;  // [Ta][64] per-lane column sums of dz1
+#pragma unroll
+  for (int s = 0; s < SB; ++s) {
+    const int q = w + s * AB_NW;
+    if (q < Tb) {
+      const int it = q / JT, jt = q - it * JT, j = jt * 16 + l16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = it * 16 + 4 * lg + r;
+        if (i < h1 && j < h2) part[a.pW2 + i * h2 + j] = accB[s][r];
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < SC; ++s) {
+    const int q = w + s * AB_NW;
+    if (q < Tc) {
+      const int kt = q / IT, it = q - kt * IT, i = it * 16 + l16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = kt * 16 + 4 * lg + r;
+        if (c < K0 && i < h1) part[a.pW1 + c * h1 + i] = accC[s][r];
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < SA; ++s) {
+    const int q = w + s * AB_NW;
+    if (q < Ta) {
+      const int rt = q / IT, it = q - rt * IT, i = it * 16 + l16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = rt * 16 + 4 * lg + r;
+        if (t < T && i < h1) part[a.pA1 + t * h1 + i] = accA[s][r];
+      }
+      sS1[q * 64 + lane] = s1[s];
+    }
+  }
+  float* sT = sZ2;  // [T][h2] staging of the per-element layer-2 sums
+#pragma unroll
+  for (int i = 0; i < V2; ++i) {
+    const int e = 4 * (tid + 512 * i);
+    if (e < n2)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        part[a.pA2 + e + q] = sA2[i][q];
+        sT[e + q] = sSW[i][q];
+      }
+  }
+  __syncthreads();
+  for (int i = tid; i < h1; i += 512) {
+    const int it = i >> 4;
+    float v = 0.f;
+    for (int rt = 0; rt < RT; ++rt)
+      for (int g = 0; g < 4; ++g) v += sS1[(rt * IT + it) * 64 + g * 16 + (i & 15)];
+    part[a.pB1 + i] = v;
+  }
+  for (int j = tid; j < h2; j += 512) {
+    float v = 0.f;
+    for (int t = 0; t < T; ++t) v += sT[t * h2 + j];
+    part[a.pWo + j] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < V2; ++i) {
+    const int e = 4 * (tid + 512 * i);
+    if (e < n2)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sT[e + q] = sS2[i][q];
+  }
+  __syncthreads();
+  for (int j = tid; j < h2; j += 512) {
+    float v = 0.f;
+    for (int t = 0; t < T; ++t) v += sT[t * h2 + j];
+    part[a.pB2 + j] = v;
+  }
+  __syncthreads();
+  sm[tid] = dbo;  // (every region is free by now; LDS holds >= 512 floats)
+  __syncthreads();
+  if (tid == 0) {
+    float v = 0.f;
+    for (int t = 0; t < 512; ++t) v += sm[t];
+    part[a.pBo] = v;
+  }
+}
+
+// Forward of the same unit under fit: z1 = h0 W1 + b1, y1 = prelu(z1),
+// z2 = y1 W2 + b2, y2 = prelu(z2), score = y2 wo + bo, keeping z1 / z2 for
+// the backward.  Same layout as din_att_bwd_kernel: one sample's rows in LDS
+// at a time, the next sample's h0 in registers, MFMA 16x16x4 f32 tiles.
+struct AttFwdArgs {
+  const float *h0, *W1, *b1, *al1, *W2, *b2, *al2, *wo, *bo;
+  int64_t B;
+  int T, K0, h1, h2, Rp, K0p, h1p, h2p;
+  int sW1, sW2, sH0, sY1, sP;
+  int oW1, oW2, oH0, oY1, oP;
+  int lds_floats;
+  float *z1, *z2, *score;
+};
+
+template <int SA, int SB, int V0>
+__global__ __launch_bounds__(512) void din_att_fwd_kernel(const AttFwdArgs a) {
+  extern __shared__ float sm[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, lg = lane >> 4;
+  const int T = a.T, K0 = a.K0, h1 = a.h1, h2 = a.h2, n0 = T * K0;
+  float *sW1 = sm + a.oW1, *sW2 = sm + a.oW2, *sH0 = sm + a.oH0, *sY1 = sm + a.oY1, *sP = sm + a.oP;
+  for (int e = tid; e < a.lds_floats; e += 512) sm[e] = 0.f;
+  __syncthreads();
+  for (int e = tid; e < K0 * h1; e += 512) {
+    const int k = e / h1;
+    sW1[k * a.sW1 + (e - k * h1)] = a.W1[e];
+  }
+  for (int e = tid; e < h1 * h2; e += 512) {
+    const int i = e / h2;
+    sW2[i * a.sW2 + (e - i * h2)] = a.W2[e];
+  }
+  const int RT = a.Rp >> 4, IT = a.h1p >> 4, JT = a.h2p >> 4;
+  const int Ta = RT * IT, Tb = RT * JT;
+  // per-lane constants of this wave's tiles (the same for every sample)
+  float al1[SA][4], b1[SA], al2[SB][4], b2[SB], wo[SB];
+#pragma unroll
+  for (int s = 0; s < SA; ++s) {
+    const int q = w + s * AB_NW, rt = q / IT, i = min((q - rt * IT) * 16 + l16, h1 - 1);
+    b1[s] = a.b1[i];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) al1[s][r] = a.al1[min(rt * 16 + 4 * lg + r, T - 1) * h1 + i];
+  }
+#pragma unroll
+  for (int s = 0; s < SB; ++s) {
+    const int q = w + s * AB_NW, rt = q / JT, j = min((q - rt * JT) * 16 + l16, h2 - 1);
+    b2[s] = a.b2[j];
+    wo[s] = a.wo[j];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) al2[s][r] = a.al2[min(rt * 16 + 4 * lg + r, T - 1) * h2 + j];
+  }
+  const float bo = a.bo[0];
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): only the prefetches are outstanding in the loop
+
+  floatx4 ph0[V0];
+  auto prefetch = [&](int64_t b) {
+#pragma unroll
+    for (int i = 0; i < V0; ++i) ph0[i] = ab_ld4(a.h0 + b * n0 + min(4 * (tid + 512 * i), n0 - 4));
+  };
+  if ((int64_t)blockIdx.x < a.B) prefetch(blockIdx.x);
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    __syncthreads();
+    const int64_t r0 = b * T;
+#pragma unroll
+    for (int i = 0; i < V0; ++i) {
+      const int e = 4 * (tid + 512 * i);
+      if (e < n0) {
+        const int t = e / K0;
+        float* d = sH0 + t * a.sH0 + (e - t * K0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = ph0[i][q];
+      }
+    }
+    if (b + gridDim.x < a.B) prefetch(b + gridDim.x);
+    __syncthreads();
+    // z1 = h0 W1 + b1 -> HBM; y1 = prelu(z1) -> LDS
+#pragma unroll
+    for (int s = 0; s < SA; ++s) {
+      const int q = w + s * AB_NW;
+      if (q < Ta) {
+        const int rt = q / IT, it = q - rt * IT;
+        const floatx4 c = ab_mfma_loop(sH0 + (rt * 16 + l16) * a.sH0 + lg, 1, sW1 + lg * a.sW1 + it * 16 + l16, a.sW1,
+                                       a.K0p, floatx4{0.f, 0.f, 0.f, 0.f});
+        const int i = it * 16 + l16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int t = rt * 16 + 4 * lg + r;
+          float y = 0.f;
+          if (t < T && i < h1) {
+            const float z = c[r] + b1[s];
+            a.z1[(r0 + t) * h1 + i] = z;
+            y = fmaxf(z, 0.f) + al1[s][r] * fminf(z, 0.f);
+          }
+          sY1[t * a.sY1 + i] = y;
+        }
+      }
+    }
+    __syncthreads();
+    // z2 = y1 W2 + b2 -> HBM; y2 wo -> LDS (summed per row below)
+#pragma unroll
+    for (int s = 0; s < SB; ++s) {
+      const int q = w + s * AB_NW;
+      if (q < Tb) {
+        const int rt = q / JT, jt = q - rt * JT;
+        const floatx4 c = ab_mfma_loop(sY1 + (rt * 16 + l16) * a.sY1 + lg, 1, sW2 + lg * a.sW2 + jt * 16 + l16, a.sW2,
+                                       a.h1p, floatx4{0.f, 0.f, 0.f, 0.f});
+        const int j = jt * 16 + l16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int t = rt * 16 + 4 * lg + r;
+          float v = 0.f;
+          if (t < T && j < h2) {
+            const float z = c[r] + b2[s];
+            a.z2[(r0 + t) * h2 + j] = z;
+            v = (fmaxf(z, 0.f) + al2[s][r] * fminf(z, 0.f)) * wo[s];
+          }
+          sP[t * a.sP + j] = v;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < T) {
+      float v = 0.f;
+      for (int j = 0; j < h2; ++j) v += sP[tid * a.sP + j];
+      a.score[r0 + tid] = v + bo;
+    }
+  }
+}
+
+struct AttBwdOut {
+  float *dW1, *db1, *dal1, *dW2, *db2, *dal2, *dwo, *dbo;
+};
+// out[e] = sum of the G partials in workgroup order (seg_sum8's fixed tree)
+__global__ __launch_bounds__(256) void din_att_bwd_fin(const float* __restrict__ part, int G, const AttBwdArgs a,
+                                                       const AttBwdOut o) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= a.P) return;
+  const float v = seg_sum8(0, G, [&](int64_t g) { return part[g * a.P + e]; });
+  if (e < a.pW2) o.dW1[e - a.pW1] = v;
+  else if (e < a.pA1) o.dW2[e - a.pW2] = v;
+  else if (e < a.pA2) o.dal1[e - a.pA1] = v;
+  else if (e < a.pB1) o.dal2[e - a.pA2] = v;
+  else if (e < a.pB2) o.db1[e - a.pB1] = v;
+  else if (e < a.pWo) o.db2[e - a.pB2] = v;
+  else if (e < a.pBo) o.dwo[e - a.pWo] = v;
+  else o.dbo[0] = v;
+}
+
+// geometry; false when the dims do not fit (T, K0, h1, h2 <= 128 and the LDS)
+// vectors per thread of a [T, X] block (X % 4 == 0) read as float4 by 512 threads
+static int att_bwd_nv(int T, int X) { return (T * X / 4 + 511) / 512; }
+static bool att_bwd_geom(int64_t B, int T, int K0, int h1, int h2, AttBwdArgs& a, int& G) {
+  if (B < 0 || T < 1 || T > 128 || K0 < 4 || K0 > 128 || h1 < 4 || h1 > 128 || h2 < 4 || h2 > 128) return false;
+  if (K0 % 4 || h1 % 4 || h2 % 4) return false;  // float4 rows
+  if (att_bwd_nv(T, K0) > 4 || att_bwd_nv(T, h1) > 4 || att_bwd_nv(T, h2) > 4) return false;
+  auto r16 = [](int v) { return (v + 15) / 16 * 16; };
+  a.B = B;
+  a.T = T;
+  a.K0 = K0;
+  a.h1 = h1;
+  a.h2 = h2;
+  a.Rp = r16(T);
+  a.K0p = r16(K0);
+  a.h1p = r16(h1);
+  a.h2p = r16(h2);
+  a.sW1 = a.h1p + 1;
+  a.sW2 = a.h2p + 1;
+  a.sH0 = a.K0p + 1;
+  a.sY1 = a.h1p + 1;
+  a.sZ2 = a.h2p + 1;
+  int o = 0;
+  a.oW1 = o;
+  o += a.K0p * a.sW1;
+  a.oW2 = o;
+  o += a.h1p * a.sW2;
+  a.oH0 = o;
+  o += a.Rp * a.sH0;
+  a.oY1 = o;
+  o += a.Rp * a.sY1;
+  a.oZ1 = o;
+  o += a.Rp * a.sY1;
+  a.oZ2 = o;
+  o += a.Rp * a.sZ2;
+  a.oDS = o;
+  o += a.Rp;
+  a.oWo = o;
+  o += a.h2p;
+  a.lds_floats = o;
+  if ((size_t)o * sizeof(float) > 160 * 1024) return false;
+  int64_t p = 0;
+  a.pW1 = p;
+  p += (int64_t)K0 * h1;
+  a.pW2 = p;
+  p += (int64_t)h1 * h2;
+  a.pA1 = p;
+  p += (int64_t)T * h1;
+  a.pA2 = p;
+  p += (int64_t)T * h2;
+  a.pB1 = p;
+  p += h1;
+  a.pB2 = p;
+  p += h2;
+  a.pWo = p;
+  p += h2;
+  a.pBo = p;
+  p += 1;
+  a.P = p;
+  G = (int)std::max<int64_t>(1, std::min<int64_t>(B, 256));
+  return true;
+}
+
 }  // namespace rs
 
 using namespace rs;
@@ -464,6 +1024,126 @@ extern "C" int rs_prelu_rows_bwd(const float* z, const float* dy, int64_t M, int
   // dalpha[p, c] = column (p*N + c) sum of prod viewed as [M/period, period*N]
   const int64_t W = (int64_t)period * N;
   return rs_col_sum_split(prod, W, M / period, W, dalpha, ws + pb, workspace_bytes - pb, stream);
+}
+
+extern "C" int rs_din_att_prelu_fwd(const float* h0, const float* W1, const float* b1, const float* alpha1,
+                                    const float* W2, const float* b2, const float* alpha2, const float* wo,
+                                    const float* bo, int64_t batch, int T, int K0, int h1, int h2, float* z1, float* z2,
+                                    float* score, rs_stream_t stream) {
+  AttBwdArgs g{};
+  int G = 0;
+  RS_REQUIRE(att_bwd_geom(batch, T, K0, h1, h2, g, G),
+             "rs_din_att_prelu_fwd: unsupported shape (T, K0, h1, h2 <= 128, multiples of 4, the rows in LDS)");
+  RS_REQUIRE(h0 && W1 && b1 && alpha1 && W2 && b2 && alpha2 && wo && bo && z1 && z2 && score,
+             "rs_din_att_prelu_fwd: null pointer");
+  RS_REQUIRE(reinterpret_cast<uintptr_t>(h0) % 16 == 0, "rs_din_att_prelu_fwd: h0 16-B aligned");
+  if (batch == 0) return RS_OK;
+  AttFwdArgs a{};
+  a.h0 = h0;
+  a.W1 = W1;
+  a.b1 = b1;
+  a.al1 = alpha1;
+  a.W2 = W2;
+  a.b2 = b2;
+  a.al2 = alpha2;
+  a.wo = wo;
+  a.bo = bo;
+  a.B = batch;
+  a.T = T;
+  a.K0 = K0;
+  a.h1 = h1;
+  a.h2 = h2;
+  a.Rp = g.Rp;
+  a.K0p = g.K0p;
+  a.h1p = g.h1p;
+  a.h2p = g.h2p;
+  a.sW1 = g.h1p + 1;
+  a.sW2 = g.h2p + 1;
+  a.sH0 = g.K0p + 1;
+  a.sY1 = g.h1p + 1;
+  a.sP = g.h2p + 1;
+  int o = 0;
+  a.oW1 = o;
+  o += a.K0p * a.sW1;
+  a.oW2 = o;
+  o += a.h1p * a.sW2;
+  a.oH0 = o;
+  o += a.Rp * a.sH0;
+  a.oY1 = o;
+  o += a.Rp * a.sY1;
+  a.oP = o;
+  o += a.Rp * a.sP;
+  a.lds_floats = o;
+  a.z1 = z1;
+  a.z2 = z2;
+  a.score = score;
+  auto slots = [](int tiles) { return (tiles + AB_NW - 1) / AB_NW; };
+  const int SA = slots((a.Rp >> 4) * (a.h1p >> 4)), SB = slots((a.Rp >> 4) * (a.h2p >> 4));
+  const size_t lds = (size_t)o * sizeof(float);
+  hipStream_t st = as_stream(stream);
+  auto go = [&](auto fn) {
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    fn<<<(unsigned)G, 512, lds, st>>>(a);
+  };
+  if (SA <= 5 && SB <= 3 && att_bwd_nv(T, K0) <= 2)
+    go(din_att_fwd_kernel<5, 3, 2>);
+  else
+    go(din_att_fwd_kernel<8, 8, 4>);
+  return launch_status("rs_din_att_prelu_fwd");
+}
+
+extern "C" int64_t rs_din_att_prelu_bwd_workspace_size(int64_t batch, int T, int K0, int h1, int h2) {
+  AttBwdArgs a{};
+  int G = 0;
+  if (!att_bwd_geom(batch, T, K0, h1, h2, a, G)) return -1;
+  return (int64_t)G * a.P * (int64_t)sizeof(float);
+}
+
+extern "C" int rs_din_att_prelu_bwd(const float* h0, const float* z1, const float* z2, const float* ds, const float* W1,
+                                    const float* W2, const float* alpha1, const float* alpha2, const float* wo,
+                                    int64_t batch, int T, int K0, int h1, int h2, float* dh0, float* dW1, float* db1,
+                                    float* dalpha1, float* dW2, float* db2, float* dalpha2, float* dwo, float* dbo,
+                                    void* workspace, int64_t workspace_bytes, rs_stream_t stream) {
+  AttBwdArgs a{};
+  int G = 0;
+  RS_REQUIRE(att_bwd_geom(batch, T, K0, h1, h2, a, G),
+             "rs_din_att_prelu_bwd: unsupported shape (T, K0, h1, h2 <= 128 and the sample's rows in LDS)");
+  RS_REQUIRE(h0 && z1 && z2 && ds && W1 && W2 && alpha1 && alpha2 && wo && dh0 && dW1 && db1 && dalpha1 && dW2 &&
+                 db2 && dalpha2 && dwo && dbo && workspace,
+             "rs_din_att_prelu_bwd: null pointer");
+  RS_REQUIRE(workspace_bytes >= (int64_t)G * a.P * (int64_t)sizeof(float), "rs_din_att_prelu_bwd: workspace too small");
+  for (const void* p : {(const void*)h0, (const void*)z1, (const void*)z2, (const void*)alpha1, (const void*)alpha2,
+                        (const void*)wo})
+    RS_REQUIRE(reinterpret_cast<uintptr_t>(p) % 16 == 0, "rs_din_att_prelu_bwd: h0, z1, z2, alphas, wo 16-B aligned");
+  hipStream_t st = as_stream(stream);
+  a.h0 = h0;
+  a.z1 = z1;
+  a.z2 = z2;
+  a.ds = ds;
+  a.W1 = W1;
+  a.W2 = W2;
+  a.al1 = alpha1;
+  a.al2 = alpha2;
+  a.wo = wo;
+  a.dh0 = dh0;
+  a.part = static_cast<float*>(workspace);
+  const size_t lds = (size_t)a.lds_floats * sizeof(float);
+  auto slots = [](int tiles) { return (tiles + AB_NW - 1) / AB_NW; };
+  const int SA = slots((a.Rp >> 4) * (a.h1p >> 4)), SB = slots((a.h1p >> 4) * (a.h2p >> 4)),
+            SC = slots((a.K0p >> 4) * (a.h1p >> 4));
+  auto go = [&](auto fn) {
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    fn<<<(unsigned)G, 512, lds, st>>>(a);
+  };
+  // fewer slots / vectors = fewer live registers: the (80, 40) default at
+  // T <= 112 (K0 = 32) takes the small instance; the general one spills
+  if (SA <= 5 && SB <= 2 && SC <= 2 && att_bwd_nv(T, K0) <= 2 && att_bwd_nv(T, h1) <= 4 && att_bwd_nv(T, h2) <= 2)
+    go(din_att_bwd_kernel<5, 2, 2, 2, 4, 2>);
+  else
+    go(din_att_bwd_kernel<8, 8, 8, 4, 4, 4>);
+  const AttBwdOut o{dW1, db1, dalpha1, dW2, db2, dalpha2, dwo, dbo};
+  din_att_bwd_fin<<<(unsigned)((a.P + 255) / 256), 256, 0, st>>>(a.part, G, a, o);
+  return launch_status("rs_din_att_prelu_bwd");
 }
 
 extern "C" int rs_masked_softmax_pool(const float* score, const void* hist, int hist_kind, int64_t hist_stride,

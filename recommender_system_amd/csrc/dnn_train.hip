@@ -214,6 +214,33 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ w, const f
     w[i] -= lr * (g[i] + 2.f * l2 * w[i]);
 }
 
+// The same update over up to SGD_MT tensors in one launch: tensor j owns
+// blocks [first[j], first[j+1]) of 1024 elements (4 per thread).
+constexpr int SGD_MT = 32;
+struct SgdMulti {
+  float* w[SGD_MT];
+  const float* g[SGD_MT];
+  int64_t n[SGD_MT];
+  float l2[SGD_MT];
+  int first[SGD_MT + 1];
+  int count;
+  float lr;
+};
+__global__ __launch_bounds__(256) void sgd_multi_kernel(const SgdMulti a) {
+  const int blk = blockIdx.x;
+  int j = 0;
+  while (j + 1 < a.count && blk >= a.first[j + 1]) ++j;  // uniform, <= 32 steps
+  float* __restrict__ w = a.w[j];
+  const float* __restrict__ g = a.g[j];
+  const int64_t base = (int64_t)(blk - a.first[j]) * 1024 + threadIdx.x;
+  const float lr = a.lr, l2 = a.l2[j];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t i = base + 256 * u;
+    if (i < a.n[j]) w[i] -= lr * (g[i] + 2.f * l2 * w[i]);
+  }
+}
+
 // DeepFM head: z = c_fm*fm + c_dnn*dnn, g = (sigmoid(z) - t)/B, outputs
 // g_fm = c_fm*g, g_dnn = c_dnn*g (dL/dfm, dL/ddnn) and the BCE loss.
 __global__ __launch_bounds__(256) void head_grad_kernel(const float* __restrict__ fm, const float* __restrict__ dnn,
@@ -780,6 +807,47 @@ extern "C" int rs_sgd_update(float* w, const float* grad, int64_t n, float lr, f
   RS_REQUIRE(w && grad && n > 0, "rs_sgd_update: bad arguments");
   sgd_kernel<<<(unsigned)std::min<int64_t>((n + 255) / 256, 8192), 256, 0, as_stream(stream)>>>(w, grad, n, lr, l2);
   return launch_status("rs_sgd_update");
+}
+
+extern "C" int rs_sgd_update_multi(int count, float* const* w, const float* const* grad, const int64_t* n,
+                                   const float* l2, float lr, rs_stream_t stream) {
+  if (count == 0) return RS_OK;
+  RS_REQUIRE(count > 0 && w && grad && n && l2, "rs_sgd_update_multi: bad arguments");
+  for (int j = 0; j < count; ++j)
+    RS_REQUIRE(w[j] && grad[j] && n[j] >= 0 && n[j] < (1ll << 40), "rs_sgd_update_multi: bad tensor %d", j);
+  hipStream_t st = as_stream(stream);
+  for (int j0 = 0; j0 < count;) {
+    SgdMulti a{};
+    a.lr = lr;
+    int blocks = 0;
+    // pack tensors while the grid stays below 2^30 blocks; one huge tensor
+    // goes alone through sgd_kernel's grid-stride loop
+    while (j0 < count && a.count < SGD_MT) {
+      const int64_t nb = (n[j0] + 1023) / 1024;
+      if (nb > (1 << 20)) {
+        if (a.count == 0) {
+          sgd_kernel<<<8192, 256, 0, st>>>(w[j0], grad[j0], n[j0], lr, l2[j0]);
+          ++j0;
+          continue;
+        }
+        break;
+      }
+      if (nb > 0) {
+        a.w[a.count] = w[j0];
+        a.g[a.count] = grad[j0];
+        a.n[a.count] = n[j0];
+        a.l2[a.count] = l2[j0];
+        a.first[a.count] = blocks;
+        blocks += (int)nb;
+        ++a.count;
+      }
+      ++j0;
+    }
+    if (a.count == 0) continue;
+    a.first[a.count] = blocks;
+    sgd_multi_kernel<<<(unsigned)blocks, 256, 0, st>>>(a);
+  }
+  return launch_status("rs_sgd_update_multi");
 }
 
 extern "C" int rs_bce_prob_grad(const float* pred, int64_t pred_stride, const float* labels, int64_t batch, float* g,

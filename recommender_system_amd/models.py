@@ -83,10 +83,17 @@ def _dnn_backward(layers, acts, delta, gw, emp, st, outs=None):
     return grads, delta
 
 
-def _dnn_apply(grads, lr, st, l2=0.0):
+def _dnn_updates(grads, l2=0.0):
+    """[(w, grad, n, l2)] of Dense layers' kernels and biases (for
+    _lib.sgd_update_multi)."""
+    out = []
     for L, dW, db in grads:
-        call("rs_sgd_update", ptr(L.kernel), ptr(dW), dW.numel(), float(lr), float(l2), st)
-        call("rs_sgd_update", ptr(L.bias), ptr(db), db.numel(), float(lr), float(l2), st)
+        out.extend([(L.kernel, dW, dW.numel(), l2), (L.bias, db, db.numel(), l2)])
+    return out
+
+
+def _dnn_apply(grads, lr, st, l2=0.0):
+    _lib.sgd_update_multi(_dnn_updates(grads, l2), lr, st)
 
 
 def _embedding_sgd(model, ids, dx, ldx, lr, st):
@@ -277,10 +284,8 @@ class DeepFM(KerasModule):
         dw1, dv, dw0 = emp(d), emp(d, kfm), emp(1)
         call("rs_fm_param_grads", ptr(x), d, ptr(s), ptr(fm.v), B, d, kfm, ptr(g_fm), ptr(dw1), ptr(dv), ptr(dw0), st)
         # updates (every gradient above used the pre-step weights)
-        _dnn_apply(grads, lr, st)
-        call("rs_sgd_update", ptr(fm.w1), ptr(dw1), d, float(lr), float(fm.reg_w), st)
-        call("rs_sgd_update", ptr(fm.v), ptr(dv), d * kfm, float(lr), float(fm.reg_b), st)
-        call("rs_sgd_update", ptr(fm.w0), ptr(dw0), 1, float(lr), 0.0, st)
+        _lib.sgd_update_multi(_dnn_updates(grads) + [(fm.w1, dw1, d, fm.reg_w), (fm.v, dv, d * kfm, fm.reg_b),
+                                                     (fm.w0, dw0, 1, 0.0)], lr, st)
         _embedding_sgd(self, ids, dx, d, lr, st)
         self._weights_changed()  # packed operand images of the old weights are stale
         return loss
@@ -447,12 +452,10 @@ class DCN(KerasModule):
             call("rs_gemm", 1, 0, d, 1, B, 1.0, ptr(xl), d, ptr(sl[l]), 1, 0.0, ptr(dWc[l]), 1, None, 0, *gw, st)
             call("rs_col_sum", ptr(deltas[l]), d, B, d, ptr(dBc[l]), st)
         # updates
-        _dnn_apply(grads, lr, st)
-        call("rs_sgd_update", ptr(out.kernel), ptr(dWo), dz_n, float(lr), 0.0, st)
-        call("rs_sgd_update", ptr(out.bias), ptr(dbo), 1, float(lr), 0.0, st)
+        upd = _dnn_updates(grads) + [(out.kernel, dWo, dz_n, 0.0), (out.bias, dbo, 1, 0.0)]
         for l in range(Lc):
-            call("rs_sgd_update", ptr(cl.cross_weight[l]), ptr(dWc[l]), d, float(lr), float(cl.reg_w), st)
-            call("rs_sgd_update", ptr(cl.cross_bias[l]), ptr(dBc[l]), d, float(lr), float(cl.reg_b), st)
+            upd += [(cl.cross_weight[l], dWc[l], d, cl.reg_w), (cl.cross_bias[l], dBc[l], d, cl.reg_b)]
+        _lib.sgd_update_multi(upd, lr, st)
         _embedding_sgd(self, ids, dx, d, lr, st)
         self.__dict__["_keep"] = (W, Bc)  # stream-ordered lifetime of the stacked operands
         self._weights_changed()
@@ -651,9 +654,10 @@ class PNN(KerasModule):
             dW = emp(*op.W.shape)
             call("rs_outer_product_bwd", ptr(x), w, ptr(delta) + 4 * o0, w, ptr(op.W), F, k, B, ptr(de), F * k, st)
             call("rs_outer_product_w_grad", ptr(x), w, ptr(delta) + 4 * o0, w, F, k, B, ptr(dW), st)
-        _dnn_apply(grads, lr, st)
+        upd = _dnn_updates(grads)
         if dW is not None:
-            call("rs_sgd_update", ptr(self.outer_product_layer.W), ptr(dW), dW.numel(), float(lr), 0.0, st)
+            upd.append((self.outer_product_layer.W, dW, dW.numel(), 0.0))
+        _lib.sgd_update_multi(upd, lr, st)
         ws_n = _lib.lib().rs_embedding_sgd_workspace_size(B * F)
         ws = self.__dict__.get("_emb_ws")
         if ws is None or ws.numel() < ws_n:
@@ -673,6 +677,11 @@ class DIN(TowerMixin, KerasModule):
     id, :73,77-79).  Behaviour features are taken in sparse-column order; their
     embeddings are concatenated along k and the mask comes from the first
     (:80)."""
+
+    # train_step: the two-layer PReLU attention unit's forward and backward as
+    # one launch each (rs_din_att_prelu_fwd / _bwd; False: the layer-by-layer
+    # kernels; both are tested vs the oracle)
+    fused_att_train = True
 
     def __init__(self, feature_columns, behavior_feature_list, att_hidden_units=(80, 40),
                  dnn_hidden_units=(256, 128, 64), att_attention="prelu", dnn_activation="prelu", dnn_dropout=0.0,
@@ -778,7 +787,7 @@ class DIN(TowerMixin, KerasModule):
           DNN and the output logit;
           backward: rs_head_grad, per Dense layer split-K rs_gemm / rs_col_sum
           / rs_prelu_rows_bwd, rs_bn_train_bwd, rs_masked_softmax_pool_bwd,
-          rs_din_att_concat_bwd; then rs_sgd_update of every dense parameter
+          rs_din_att_concat_bwd; then one rs_sgd_update_multi over every dense parameter
           and row-sparse rs_embedding_sgd of the behaviour tables (history
           rows, then candidates) and the other sparse tables.
         Dropout (after the DNN, :93) runs as the identity (see
@@ -815,6 +824,12 @@ class DIN(TowerMixin, KerasModule):
         need += [lb.rs_prelu_rows_bwd_workspace_size(B, L.units, 1) for L in self.dense_layer]
         need += [lb.rs_dice_train_workspace_size(M, 4 * K)] if att.activation == "dice" else []
         need += [lb.rs_dice_train_workspace_size(B, L.units) for L in self.dense_layer if L.activation == "dice"]
+        # the PReLU unit with two hidden layers (the reference default (80, 40)):
+        # rs_din_att_prelu_bwd when its shape fits; otherwise layer by layer
+        att_fused = (self.fused_att_train and att.activation == "prelu" and len(att.kernels) == 2
+                     and lb.rs_din_att_prelu_bwd_workspace_size(B, T, 4 * K, *att.kernels[1].shape) >= 0)
+        if att_fused:
+            need.append(lb.rs_din_att_prelu_bwd_workspace_size(B, T, 4 * K, *att.kernels[1].shape))
         gws = _gemm_ws(self, max(need))
         gw = (ptr(gws), gws.numel())
 
@@ -835,22 +850,29 @@ class DIN(TowerMixin, KerasModule):
                  ptr(d.moving_variance), ptr(mu), ptr(vr), ptr(y), *gw, st)
             return (mu, vr), y
 
-        for W, b, al in zip(att.kernels, att.biases, att.alphas):
-            n = W.shape[1]
-            z, y = emp(M, n), emp(M, n)
-            call("rs_dense_fwd", ptr(att_in[-1]), att_in[-1].stride(0), ptr(W), ptr(b), None, _lib.ACT[None],
-                 ptr(z), n, M, W.shape[0], n, st)
-            call("rs_prelu_rows_fwd", ptr(z), M, n, ptr(al), T, ptr(y), st)
-            att_pre.append(z)
-            att_in.append(y)
-        for d in att.dice:  # att_attention 'dice': Dice layers on the 4k-wide concat, no Dense
-            saved, y = dice_fwd(d, att_in[-1], M, 4 * K)
-            att_pre.append(saved)
-            att_in.append(y)
         score = emp(M)
-        hl = att_in[-1]
-        call("rs_dense_fwd", ptr(hl), hl.stride(0), ptr(att.out_kernel), ptr(att.out_bias), None, _lib.ACT[None],
-             ptr(score), 1, M, hl.shape[1], 1, st)
+        if att_fused:  # the unit's forward in one launch, z1 / z2 kept
+            (W1, W2), (b1, b2), (al1, al2) = att.kernels, att.biases, att.alphas
+            att_pre = [emp(M, W1.shape[1]), emp(M, W2.shape[1])]
+            call("rs_din_att_prelu_fwd", ptr(h0), ptr(W1), ptr(b1), ptr(al1), ptr(W2), ptr(b2), ptr(al2),
+                 ptr(att.out_kernel), ptr(att.out_bias), B, T, 4 * K, W1.shape[1], W2.shape[1], ptr(att_pre[0]),
+                 ptr(att_pre[1]), ptr(score), st)
+        else:
+            for W, b, al in zip(att.kernels, att.biases, att.alphas):
+                n = W.shape[1]
+                z, y = emp(M, n), emp(M, n)
+                call("rs_dense_fwd", ptr(att_in[-1]), att_in[-1].stride(0), ptr(W), ptr(b), None, _lib.ACT[None],
+                     ptr(z), n, M, W.shape[0], n, st)
+                call("rs_prelu_rows_fwd", ptr(z), M, n, ptr(al), T, ptr(y), st)
+                att_pre.append(z)
+                att_in.append(y)
+            for d in att.dice:  # att_attention 'dice': Dice layers on the 4k-wide concat, no Dense
+                saved, y = dice_fwd(d, att_in[-1], M, 4 * K)
+                att_pre.append(saved)
+                att_in.append(y)
+            hl = att_in[-1]
+            call("rs_dense_fwd", ptr(hl), hl.stride(0), ptr(att.out_kernel), ptr(att.out_bias), None,
+                 _lib.ACT[None], ptr(score), 1, M, hl.shape[1], 1, st)
         a = emp(B, T)
         h_first = hists[0]
         call("rs_masked_softmax_pool", ptr(score), ptr(h_first), _lib.id_kind(h_first), h_first.stride(0), ptr(seq),
@@ -933,17 +955,27 @@ class DIN(TowerMixin, KerasModule):
         ds, dseq = emp(M), emp(M, K)
         call("rs_masked_softmax_pool_bwd", ptr(a), ptr(h_first), _lib.id_kind(h_first), h_first.stride(0), ptr(seq),
              ptr(dx), width, B, T, K, ptr(ds), ptr(dseq), st)
-        dh3 = dense_back(att.out_kernel, att.out_bias, hl, ds.view(M, 1), M)
-        for li in reversed(range(len(att.kernels))):
-            dz = prelu_back(att_pre[li], dh3, att.alphas[li], T, M)
-            dh3 = dense_back(att.kernels[li], att.biases[li], att_in[li], dz, M)
+        if att_fused:
+            # the whole attention-unit backward in one launch (+ its partial sums)
+            (W1, W2), (b1, b2), (al1, al2) = att.kernels, att.biases, att.alphas
+            h1, h2 = W2.shape
+            dh3 = emp(M, 4 * K)
+            gr = [emp(4 * K, h1), emp(h1), emp(T, h1), emp(h1, h2), emp(h2), emp(T, h2), emp(h2), emp(1)]
+            call("rs_din_att_prelu_bwd", ptr(h0), ptr(att_pre[0]), ptr(att_pre[1]), ptr(ds), ptr(W1), ptr(W2),
+                 ptr(al1), ptr(al2), ptr(att.out_kernel), B, T, 4 * K, h1, h2, ptr(dh3), *[ptr(v) for v in gr], *gw,
+                 st)
+            updates.extend(zip([W1, b1, al1, W2, b2, al2, att.out_kernel, att.out_bias], gr))
+        else:
+            dh3 = dense_back(att.out_kernel, att.out_bias, hl, ds.view(M, 1), M)
+            for li in reversed(range(len(att.kernels))):
+                dz = prelu_back(att_pre[li], dh3, att.alphas[li], T, M)
+                dh3 = dense_back(att.kernels[li], att.biases[li], att_in[li], dz, M)
         for li in reversed(range(len(att.dice))):
             dh3 = dice_back(att.dice[li], att_in[li], att_pre[li], dh3, M, 4 * K)
         call("rs_din_att_concat_bwd", ptr(dh3), ptr(item), ptr(seq), B, T, K, ptr(dx) + 4 * K, width, ptr(dseq), st)
 
         # ---- SGD
-        for w, gr in updates:
-            call("rs_sgd_update", ptr(w), ptr(gr), gr.numel(), float(lr), 0.0, st)
+        _lib.sgd_update_multi([(w, gr, gr.numel(), 0.0) for w, gr in updates], lr, st)
         ws_n = _lib.lib().rs_embedding_sgd_workspace_size(M)
         ws = self.__dict__.get("_emb_ws")
         if ws is None or ws.numel() < ws_n:
@@ -1062,9 +1094,7 @@ class NFM(TowerMixin, KerasModule):
              delta.stride(0), ptr(dx), D, ptr(dgam), ptr(dbet), st)
         de = emp(B, F * k)
         call("rs_bi_interaction_bwd", ptr(rows), F * k, ptr(dx) + 4 * self.nd, D, F, k, B, ptr(de), F * k, st)
-        _dnn_apply(grads, lr, st)
-        call("rs_sgd_update", ptr(bn.gamma), ptr(dgam), D, float(lr), 0.0, st)
-        call("rs_sgd_update", ptr(bn.beta), ptr(dbet), D, float(lr), 0.0, st)
+        _lib.sgd_update_multi(_dnn_updates(grads) + [(bn.gamma, dgam, D, 0.0), (bn.beta, dbet, D, 0.0)], lr, st)
         ws_n = _lib.lib().rs_embedding_sgd_workspace_size(B * F)
         ws = self.__dict__.get("_emb_ws")
         if ws is None or ws.numel() < ws_n:
@@ -1107,7 +1137,7 @@ class FFM(KerasModule):
         every row of w / v (layer/interaction.py:131-139), plain SGD:
           rs_ffm_train_fwd (per sample: Fm, z, g and the shared gradient row
           G = g (T - Fm)), rs_gemm / rs_col_sum (the dense rows' and w0's
-          gradients), rs_l2_decay (every row of w and v), rs_sgd_update (dense
+          gradients), rs_l2_decay (every row of w and v), rs_sgd_update_multi (dense
           rows, w0) and rs_embedding_sgd_strided (each looked-up row of v
           gets its sample's G, of w its g; duplicates summed in lookup order).
         Out-of-range ids train nothing (tf.one_hot's zero row).  Every
@@ -1140,10 +1170,8 @@ class FFM(KerasModule):
         # l2 on every row (old weights), then the data gradients
         call("rs_l2_decay", ptr(L.v), L.v.numel(), float(lr), float(L.v_reg), st)
         call("rs_l2_decay", ptr(L.w), L.w.numel(), float(lr), float(L.w_reg), st)
-        if nd:
-            call("rs_sgd_update", ptr(L.v), ptr(dvd), nd * E, float(lr), 0.0, st)
-            call("rs_sgd_update", ptr(L.w), ptr(dwd), nd, float(lr), 0.0, st)
-        call("rs_sgd_update", ptr(L.w0), ptr(dw0), 1, float(lr), 0.0, st)
+        _lib.sgd_update_multi(([(L.v, dvd, nd * E, 0.0), (L.w, dwd, nd, 0.0)] if nd else []) + [(L.w0, dw0, 1, 0.0)],
+                              lr, st)
         n_sparse = L.feature_num - nd
         ws_n = _lib.lib().rs_embedding_sgd_workspace_size(B * F)
         ws = self.__dict__.get("_emb_ws")

@@ -190,9 +190,9 @@ class HipShardOps:
 
     def apply(self, sh, grad, lr, reg_w, reg_v):
         d, kfm, st = sh.d, sh.kfm, _lib.stream()
-        call("rs_sgd_update", ptr(sh.w1), ptr(grad), d, float(lr), float(reg_w), st)
-        call("rs_sgd_update", ptr(sh.v), ptr(grad) + 4 * d, d * kfm, float(lr), float(reg_v), st)
-        call("rs_sgd_update", ptr(sh.w0), ptr(grad) + 4 * d * (1 + kfm), 1, float(lr), 0.0, st)
+        g = ptr(grad)
+        _lib.sgd_update_multi([(sh.w1, g, d, reg_w), (sh.v, g + 4 * d, d * kfm, reg_v),
+                               (sh.w0, g + 4 * d * (1 + kfm), 1, 0.0)], lr, st)
         sh.prepare()
 
     # -- row protocol of ShardedDeepFM (rs_shard_row_route / rs_gather_rows / rs_deepfm_fwd)
@@ -292,12 +292,12 @@ class HipShardOps:
         """SGD of the replicated parameters from the (all-reduced) flat
         gradient: l2(w_reg) on w1, l2(v_reg) on v (FMLayer), none elsewhere."""
         sh, st = model.emb, _lib.stream()
+        upd = []
         for (L, _), (dW, db) in zip(tb["layers"], tb["dnn_views"]):
-            call("rs_sgd_update", ptr(L.kernel), ptr(dW), dW.numel(), float(lr), 0.0, st)
-            call("rs_sgd_update", ptr(L.bias), ptr(db), db.numel(), float(lr), 0.0, st)
-        call("rs_sgd_update", ptr(sh.w1), ptr(tb["dw1"]), sh.d, float(lr), float(model.reg_w), st)
-        call("rs_sgd_update", ptr(sh.v), ptr(tb["dv"]), sh.d * sh.kfm, float(lr), float(model.reg_v), st)
-        call("rs_sgd_update", ptr(sh.w0), ptr(tb["dw0"]), 1, float(lr), 0.0, st)
+            upd += [(L.kernel, dW, dW.numel(), 0.0), (L.bias, db, db.numel(), 0.0)]
+        upd += [(sh.w1, tb["dw1"], sh.d, model.reg_w), (sh.v, tb["dv"], sh.d * sh.kfm, model.reg_v),
+                (sh.w0, tb["dw0"], 1, 0.0)]
+        _lib.sgd_update_multi(upd, lr, st)
         sh.prepare()
         model.dnn._weights_changed()
 
@@ -461,7 +461,7 @@ class ShardedEmbeddingFM:
           rs_embedding_sgd           -> row-sparse SGD of my shard (duplicates
                                         summed in global lookup order)
           all_reduce(dw1, dv, dw0)   -> replicated FM parameters stay identical (RCCL)
-          rs_sgd_update x3, rs_fm_prepare
+          rs_sgd_update_multi, rs_fm_prepare
         Every gradient comes from the pre-step weights.  Returns the per-sample
         losses of the local batch (before the step) if ``return_loss``."""
         B = ids.shape[0]
@@ -844,7 +844,7 @@ class ShardedDeepFM:
           rs_scatter_rows -> dL/drow into the row-exchange slot layout
           all_to_all(row gradients)  (RCCL; the reverse of the row exchange)
           owner: rs_embedding_sgd of the shard on the ids it served
-          all_reduce(flat gradient)  (RCCL) -> rs_sgd_update of the replicas
+          all_reduce(flat gradient)  (RCCL) -> rs_sgd_update_multi of the replicas
         Every gradient comes from the pre-step weights; every rank's update of
         the replicated parameters is identical.  Returns the per-sample losses
         of the local batch (before the step) if ``return_loss``."""

@@ -226,26 +226,36 @@ def _assert_update_close(got, ref, before, rtol=2e-3, what=""):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("att_hidden,dnn_hidden,nb,k,B,T,att_act,dnn_act", [
-    ((80, 40), (256, 128, 64), 1, 8, 256, 20, "prelu", "prelu"),   # the reference defaults
-    ((80, 40), (64, 32), 2, 8, 192, 30, "prelu", "prelu"),         # item + category behaviour features (K = 16)
-    ((32,), (16,), 2, 4, 64, 7, "prelu", "prelu"),                 # one attention layer, small ragged T
-    ((80, 40), (64, 32), 1, 8, 256, 20, "prelu", "dice"),          # dnn_activation='dice'
-    ((80, 40), (64, 32), 2, 8, 128, 30, "dice", "dice"),           # att_attention='dice' too
+@pytest.mark.parametrize("att_hidden,dnn_hidden,nb,k,B,T,att_act,dnn_act,fused", [
+    ((80, 40), (256, 128, 64), 1, 8, 256, 20, "prelu", "prelu", True),   # the reference defaults
+    ((80, 40), (256, 128, 64), 1, 8, 256, 20, "prelu", "prelu", False),  # ... attention unit layer by layer
+    ((80, 40), (64, 32), 2, 8, 192, 30, "prelu", "prelu", True),         # item + category features (K = 16)
+    ((80, 40), (64, 32), 1, 8, 40, 100, "prelu", "prelu", True),         # config 4's T = 100 (Rp = 112)
+    ((56, 24), (16,), 1, 8, 30, 128, "prelu", "prelu", True),            # T = 128, widths with pads
+    ((80, 40), (64, 32), 1, 8, 300, 7, "prelu", "prelu", True),          # T = 7: one row tile, > 256 samples
+    ((32,), (16,), 2, 4, 64, 7, "prelu", "prelu", True),                 # one attention layer, small ragged T
+    ((80, 40), (64, 32), 1, 8, 256, 20, "prelu", "dice", True),          # dnn_activation='dice'
+    ((80, 40), (64, 32), 2, 8, 128, 30, "dice", "dice", True),           # att_attention='dice' too
 ])
-def test_din_train_steps_match_oracle(gpu, att_hidden, dnn_hidden, nb, k, B, T, att_act, dnn_act):
+def test_din_train_steps_match_oracle(gpu, att_hidden, dnn_hidden, nb, k, B, T, att_act, dnn_act, fused):
     """DIN.train_step (compile_fit on DIN in training mode: batch-statistics
     BatchNormalization with moving averages, PReLU attention over [T, h]
     alphas, masked softmax pool, PReLU DNN, SGD + row-sparse embedding SGD)
     == oracle.din_train_step (pinned by finite differences) over 3 steps with
     small vocabularies (repeated rows, candidates inside the histories), a
     fully padded history row and non-trivial parameters.  Parameters and the
-    per-step updates are compared at 2e-3 of their scale."""
+    per-step updates are compared at 2e-3 of their scale.  ``fused``: the
+    two-layer PReLU attention's backward as one rs_din_att_prelu_bwd launch
+    and its forward as one rs_din_att_prelu_fwd launch (False: layer by layer)."""
     from recommender_system_amd import DIN
     rng = np.random.default_rng(B + T + nb)
     cols, behaviour = din_columns(nb, k, item_vocab=40, cate_vocab=9, user_vocab=17)
     model = DIN(cols, behaviour, att_hidden_units=att_hidden, dnn_hidden_units=dnn_hidden, att_attention=att_act,
                 dnn_activation=dnn_act, seed=3)
+    model.fused_att_train = fused
+    if fused and att_act == "prelu" and len(att_hidden) == 2:  # the shape takes the fused kernel
+        from recommender_system_amd import _lib
+        assert _lib.lib().rs_din_att_prelu_bwd_workspace_size(B, T, 4 * k * nb, *att_hidden) > 0
     inputs = din_inputs(rng, cols, behaviour, B, T)
     model(inputs)
     randomize(model, rng)

@@ -431,6 +431,26 @@ def test_col_sum_split_matches_numpy(gpu, M, N):
 
 
 @pytest.mark.gpu
+def test_sgd_update_multi_matches_single(gpu):
+    """rs_sgd_update_multi over 40 tensors (two launches of <= 32; sizes 0, 1,
+    ragged, multi-block; the single-tensor path past 2^20 blocks is not run) == one
+    rs_sgd_update per tensor, bitwise (same expression per element)."""
+    from recommender_system_amd import _lib
+    rng = np.random.default_rng(5)
+    sizes = [0, 1, 3, 1023, 1024, 1025, 70000] + [int(s) for s in rng.integers(1, 5000, 33)]
+    ws = [torch.as_tensor(rng.standard_normal(max(n, 1)).astype(np.float32), device=gpu) for n in sizes]
+    gs = [torch.as_tensor(rng.standard_normal(max(n, 1)).astype(np.float32), device=gpu) for n in sizes]
+    l2 = [float(v) for v in rng.uniform(0, 0.1, len(sizes))]
+    ref = [w.clone() for w in ws]
+    st = _lib.stream()
+    for w, g, n, c in zip(ref, gs, sizes, l2):
+        _lib.call("rs_sgd_update", w.data_ptr(), g.data_ptr(), n, 0.05, c, st)
+    _lib.sgd_update_multi([(w, g, n, c) for w, g, n, c in zip(ws, gs, sizes, l2)], 0.05, st)
+    for j, (a, b) in enumerate(zip(ws, ref)):
+        assert torch.equal(a, b), j
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("M,N", [(1, 5), (300, 16), (20000, 64)])
 def test_dice_train_fwd_bwd_match_oracle(gpu, M, N):
     """rs_dice_train_fwd / _bwd (Dice under fit: batch statistics, the
