@@ -433,7 +433,8 @@ int rs_gemm(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
             rs_stream_t stream);
 int rs_col_sum(const float* A, int64_t lda, int64_t M, int64_t N, float* out,
                rs_stream_t stream);
-/* rs_col_sum over many rows: slices of 256 rows summed into a workspace of
+/* rs_col_sum over many rows: slices of 256 rows (fewer, down to 16, when
+ * that leaves < 64 slices) summed into a workspace of
  * rs_col_sum_workspace_size(M, N) bytes, then the slices in order
  * (deterministic); without room (or one slice) it is rs_col_sum.           */
 int64_t rs_col_sum_workspace_size(int64_t M, int64_t N);

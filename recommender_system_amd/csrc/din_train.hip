@@ -906,6 +906,16 @@ __global__ __launch_bounds__(256) void din_att_bwd_fin(const float* __restrict__
 }
 
 // geometry; false when the dims do not fit (T, K0, h1, h2 <= 128 and the LDS)
+// LDS row strides for the two MFMA operand patterns of ds_read_b32 (32 banks
+// per 32-lane group): "rows": 16 rows x 2 consecutive columns per group
+// (operand[(16t + l16) * S + k + lg]) is conflict-free for S = 2 * odd;
+// "cols": 2 rows x 16 columns (operand[(k + lg) * S + 16t + l16]) for
+// S = 16 (mod 32).  Arrays read both ways take the "rows" stride.
+static int lds_stride_rows(int n) { return (n + 3) / 4 * 4 + 2; }
+static int lds_stride_cols(int n) {
+  const int v = (n + 15) / 32 * 32 + 16;
+  return v >= n ? v : v + 32;
+}
 // vectors per thread of a [T, X] block (X % 4 == 0) read as float4 by 512 threads
 static int att_bwd_nv(int T, int X) { return (T * X / 4 + 511) / 512; }
 static bool att_bwd_geom(int64_t B, int T, int K0, int h1, int h2, AttBwdArgs& a, int& G) {
@@ -922,11 +932,11 @@ static bool att_bwd_geom(int64_t B, int T, int K0, int h1, int h2, AttBwdArgs& a
   a.K0p = r16(K0);
   a.h1p = r16(h1);
   a.h2p = r16(h2);
-  a.sW1 = a.h1p + 1;
-  a.sW2 = a.h2p + 1;
-  a.sH0 = a.K0p + 1;
-  a.sY1 = a.h1p + 1;
-  a.sZ2 = a.h2p + 1;
+  a.sW1 = lds_stride_rows(a.h1p);  // (dh0: rows)
+  a.sW2 = lds_stride_rows(a.h2p);  // (dy1: rows)
+  a.sH0 = lds_stride_cols(a.K0p);  // (dW1: cols)
+  a.sY1 = lds_stride_rows(a.h1p);  // y1 (dW2: cols) and z1 / dz1 (rows and cols) share it
+  a.sZ2 = lds_stride_rows(a.h2p);  // dz2: rows and cols
   int o = 0;
   a.oW1 = o;
   o += a.K0p * a.sW1;
@@ -1057,10 +1067,10 @@ extern "C" int rs_din_att_prelu_fwd(const float* h0, const float* W1, const floa
   a.K0p = g.K0p;
   a.h1p = g.h1p;
   a.h2p = g.h2p;
-  a.sW1 = g.h1p + 1;
-  a.sW2 = g.h2p + 1;
-  a.sH0 = g.K0p + 1;
-  a.sY1 = g.h1p + 1;
+  a.sW1 = lds_stride_cols(g.h1p);  // z1 product B: cols
+  a.sW2 = lds_stride_cols(g.h2p);  // z2 product B: cols
+  a.sH0 = lds_stride_rows(g.K0p);  // z1 product A: rows
+  a.sY1 = lds_stride_rows(g.h1p);  // z2 product A: rows
   a.sP = g.h2p + 1;
   int o = 0;
   a.oW1 = o;

@@ -170,17 +170,19 @@ __global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ 
   if (threadIdx.x == 0) out[n] = red[0];
 }
 
-// Split column sums (rs_col_sum_split): slice s of CS_R rows -> part[s][n]
+// Split column sums (rs_col_sum_split): slice s of R rows -> part[s][n]
 // (64 columns x 4 row lanes per block, the lanes combined in order), then
-// out[n] = the slices in order (seg_sum8).  Deterministic for a given shape.
+// out[n] = the slices in order (seg_sum8).  R = 256 rows, halved (down to 16)
+// while there would be fewer than 64 slices, so a short matrix still spreads
+// over the chip.  Deterministic for a given shape.
 constexpr int CS_R = 256;
 __global__ __launch_bounds__(256) void col_sum_part_kernel(const float* __restrict__ A, int64_t lda, int64_t M, int N,
-                                                           float* __restrict__ part) {
+                                                           int R, float* __restrict__ part) {
   __shared__ float red[4][64];
   const int c = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int n = blockIdx.x * 64 + c;
-  const int64_t m0 = (int64_t)blockIdx.y * CS_R;
-  const int64_t m1 = m0 + CS_R < M ? m0 + CS_R : M;
+  const int64_t m0 = (int64_t)blockIdx.y * R;
+  const int64_t m1 = m0 + R < M ? m0 + R : M;
   float acc = 0.f;
   if (n < N)
     for (int64_t m = m0 + rl; m < m1; m += 4) acc += A[m * lda + n];
@@ -770,7 +772,12 @@ extern "C" int rs_col_sum(const float* A, int64_t lda, int64_t M, int64_t N, flo
   return launch_status("rs_col_sum");
 }
 
-static int64_t col_sum_slices(int64_t M) { return (M + CS_R - 1) / CS_R; }
+static int col_sum_rows(int64_t M) {
+  int R = CS_R;
+  while (R > 16 && (M + R - 1) / R < 64) R >>= 1;
+  return R;
+}
+static int64_t col_sum_slices(int64_t M) { return (M + col_sum_rows(M) - 1) / col_sum_rows(M); }
 
 extern "C" int64_t rs_col_sum_workspace_size(int64_t M, int64_t N) {
   if (M < 0 || N < 0) return -1;
@@ -786,7 +793,8 @@ static void col_sum_launch(const float* A, int64_t lda, int64_t M, int64_t N, fl
     return;
   }
   float* part = static_cast<float*>(ws);
-  col_sum_part_kernel<<<dim3((unsigned)((N + 63) / 64), (unsigned)S), 256, 0, st>>>(A, lda, M, (int)N, part);
+  col_sum_part_kernel<<<dim3((unsigned)((N + 63) / 64), (unsigned)S), 256, 0, st>>>(A, lda, M, (int)N,
+                                                                                   col_sum_rows(M), part);
   if (S >= 64 && N <= (1 << 20))
     col_sum_fin_wave<<<(unsigned)((N + 3) / 4), 256, 0, st>>>(part, (int)S, (int)N, out);
   else
