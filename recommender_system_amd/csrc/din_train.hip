@@ -889,12 +889,19 @@ __global__ __launch_bounds__(512) void din_att_fwd_kernel(const AttFwdArgs a) {
 struct AttBwdOut {
   float *dW1, *db1, *dal1, *dW2, *db2, *dal2, *dwo, *dbo;
 };
-// out[e] = sum of the G partials in workgroup order (seg_sum8's fixed tree)
+// out[e] = the G partials in a fixed order: a block takes 64 consecutive
+// elements (coalesced rows of the partials) x 4 lanes of workgroups (g = q
+// mod 4, each in seg_sum8's tree), the 4 lane sums added in order
 __global__ __launch_bounds__(256) void din_att_bwd_fin(const float* __restrict__ part, int G, const AttBwdArgs a,
                                                        const AttBwdOut o) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= a.P) return;
-  const float v = seg_sum8(0, G, [&](int64_t g) { return part[g * a.P + e]; });
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + c;
+  const int ng = G > q ? (G - q + 3) / 4 : 0;
+  red[q][c] = e < a.P ? seg_sum8(0, ng, [&](int64_t i) { return part[(q + 4 * i) * a.P + e]; }) : 0.f;
+  __syncthreads();
+  if (q != 0 || e >= a.P) return;
+  const float v = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
   if (e < a.pW2) o.dW1[e - a.pW1] = v;
   else if (e < a.pA1) o.dW2[e - a.pW2] = v;
   else if (e < a.pA2) o.dal1[e - a.pA1] = v;
@@ -1152,7 +1159,7 @@ extern "C" int rs_din_att_prelu_bwd(const float* h0, const float* z1, const floa
   else
     go(din_att_bwd_kernel<8, 8, 8, 4, 4, 4>);
   const AttBwdOut o{dW1, db1, dalpha1, dW2, db2, dalpha2, dwo, dbo};
-  din_att_bwd_fin<<<(unsigned)((a.P + 255) / 256), 256, 0, st>>>(a.part, G, a, o);
+  din_att_bwd_fin<<<(unsigned)((a.P + 63) / 64), 256, 0, st>>>(a.part, G, a, o);
   return launch_status("rs_din_att_prelu_bwd");
 }
 
