@@ -582,11 +582,13 @@ __global__ __launch_bounds__(256) void emb_piece_kernel(const uint32_t* __restri
   if (p >= n) return;
   uint32_t r;
   float s;
-  if (seg_piece(key, n, C, p, k, f, [&](int64_t q) {
-        const int64_t j = val[q];
-        const int64_t b = j / F;
-        const int cc = (int)(j - b * F);
-        return grad[b * ldg + (int64_t)cc * gfs + f];
+  // 32 gathers in flight per round: a hot row's chunk-long piece (the padding
+  // id of a DIN history) is 8 dependent rounds, not 32 (positions < 2^31)
+  if (seg_piece<32>(key, n, C, p, k, f, [&](int64_t q) {
+        const uint32_t j = val[q];
+        const uint32_t b = j / (uint32_t)F;
+        const int cc = (int)(j - b * (uint32_t)F);
+        return grad[(int64_t)b * ldg + (int64_t)cc * gfs + f];
       }, part_first, part_last, r, s))
     table[(int64_t)r * k + f] -= lr * s;
 }

@@ -163,6 +163,35 @@ __device__ __forceinline__ float seg_sum8(int64_t p, int64_t e, G get) {
   for (int u = 0; q < e; ++q, ++u) a[u] += get(q);
   return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
+// The same with U (a power of two >= 8) partial sums: U loads in flight per
+// round for sums whose every term is a dependent gather (index, then value);
+// the partials combined in a fixed pairwise tree.
+template <int U, class G>
+__device__ __forceinline__ float seg_sum_u(int64_t p, int64_t e, G get) {
+  if constexpr (U == 8) {
+    return seg_sum8(p, e, get);
+  } else {
+    float a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = 0.f;
+    int64_t q = p;
+    for (; q + U <= e; q += U) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = get(q + u);
+#pragma unroll
+      for (int u = 0; u < U; ++u) a[u] += v[u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (q + u < e) a[u] += get(q + u);
+#pragma unroll
+    for (int w = U / 2; w >= 1; w >>= 1)
+#pragma unroll
+      for (int u = 0; u < w; ++u) a[u] = a[u] + a[u + w];
+    return a[0];
+  }
+}
 
 // Chunked segment sums over sorted keys (row-sparse SGD with hot rows): a
 // segment is cut into PIECES at the fixed chunk boundaries (multiples of C
@@ -185,7 +214,7 @@ __device__ __forceinline__ int64_t seg_end_in(const uint32_t* __restrict__ key, 
   }
   return lo;
 }
-template <class G>
+template <int U = 8, class G>
 __device__ __forceinline__ bool seg_piece(const uint32_t* __restrict__ key, int64_t n, int64_t C, int64_t p, int W,
                                           int f, G get, float* __restrict__ part_first,
                                           float* __restrict__ part_last, uint32_t& r, float& sum) {
@@ -196,7 +225,7 @@ __device__ __forceinline__ bool seg_piece(const uint32_t* __restrict__ key, int6
   if (!head && p != c * C) return false;
   const int64_t cend = (c + 1) * C < n ? (c + 1) * C : n;
   const int64_t e = seg_end_in(key, p, cend, r);
-  const float s = seg_sum8(p, e, get);
+  const float s = seg_sum_u<U>(p, e, get);
   const bool crosses = e == cend && cend < n && key[cend] == r;
   if (head && !crosses) {
     sum = s;
