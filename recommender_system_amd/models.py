@@ -494,9 +494,16 @@ class DCN(KerasModule):
             n = _lib.lib().rs_cross_prepared_size(d, L + 1)
             cross = torch.empty(n, dtype=torch.float32, device=self._dev)
             call("rs_cross_prepare", ptr(W), ptr(Bb), d, L + 1, ptr(cross), _lib.stream())
-            wo2 = out.kernel[d:].reshape(-1, 1)                       # [out_dim, 1]
-            wf = (last.kernel @ wo2).contiguous()                     # [h_last, 1]
-            bf = (last.bias.reshape(1, -1) @ wo2).reshape(1) + out.bias.reshape(1)
+            # fold on rs_dense_fwd: wf = last.kernel @ wo2, bf = last.bias @ wo2 + out.bias
+            wo2 = out.kernel[d:].reshape(-1, 1).contiguous()          # [out_dim, 1]
+            h_last, od = last.kernel.shape
+            kern = last.kernel.contiguous()
+            wf = torch.empty(h_last, 1, dtype=torch.float32, device=self._dev)
+            bf = torch.empty(1, dtype=torch.float32, device=self._dev)
+            st = _lib.stream()
+            call("rs_dense_fwd", ptr(kern), od, ptr(wo2), None, None, _lib.ACT[None], ptr(wf), 1, h_last, od, 1, st)
+            call("rs_dense_fwd", ptr(last.bias), od, ptr(wo2), ptr(out.bias), None, _lib.ACT[None], ptr(bf), 1, 1, od, 1,
+                 st)
             ks = [l.kernel for l in hidden] + [wf]
             bs = [l.bias for l in hidden] + [bf.contiguous()]
             als = [l.alpha for l in hidden] + [None]
