@@ -5,6 +5,14 @@
 
 #include "rs_common.hpp"
 
+// Dataflow hand-off between whole-column layers: a layer whose predecessor
+// kept whole columns per wave (S == 1) starts without a workgroup barrier;
+// each of its k-groups waits on the LDS ready flag of the predecessor tile it
+// reads (see mlp_tower_tile).
+#ifndef MLP_FLOW
+#define MLP_FLOW 0
+#endif
+
 namespace rs {
 
 constexpr int MLP_MAXL = 8;
@@ -48,7 +56,7 @@ static bool mlp_geom(int L, const int* dims, MlpGeom& g) {
   // Row stride = 8 (mod 64) dwords: the four 16-lane groups of each
   // ds_read_b128 (rows l&15, k-slot l>>4) then hit 16 distinct bank slots.
   g.rs = rup(maxw, 64) + 8;
-  g.lds = (size_t)(32 * g.rs + MLP_NW * 256 + g.ptot + MLP_MAXL * 64) * sizeof(float);
+  g.lds = (size_t)(32 * g.rs + MLP_NW * 256 + g.ptot + (MLP_FLOW ? MLP_MAXL * 64 : 0)) * sizeof(float);
   return g.lds <= 160 * 1024;
 }
 
@@ -111,13 +119,6 @@ __device__ __forceinline__ MlpItem mlp_item(int item, int T, int G, int S) {
 #endif
 #ifndef MLP_ACC2
 #define MLP_ACC2 0
-#endif
-// Dataflow hand-off between whole-column layers: a layer whose predecessor
-// kept whole columns per wave (S == 1) starts without a workgroup barrier;
-// each of its k-groups waits on the LDS ready flag of the predecessor tile it
-// reads (see mlp_tower_tile).
-#ifndef MLP_FLOW
-#define MLP_FLOW 0
 #endif
 constexpr int MLP_R = MLP_RING;  // B-fragment ring slots (the deepest D)
 __device__ __forceinline__ void mlp_ring_fill(floatx4 (&ring)[MLP_R], const floatx4* bp, int g0, int g1) {
