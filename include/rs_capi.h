@@ -52,9 +52,32 @@ enum rs_act {
   RS_ACT_SIGMOID = 3
 };
 
+/* Bits of the device error flag (int, caller-owned, zero it before use):
+ * kernels OR these in; the host layer raises IndexError for RS_FLAG_BAD_ID
+ * (TF's InvalidArgumentError on an out-of-range Embedding id) and RSError for
+ * any other bit. */
+enum rs_flag {
+  RS_FLAG_BAD_ID = 1  /* an id outside [0, vocab) (its row read as zeros) */
+};
+
+/* Runtime tuning options (process-wide, host side; read when a kernel is
+ * launched, so a captured hipGraph keeps the value it was captured with). */
+enum rs_option {
+  RS_OPT_EMBED_FM_KERNEL = 0, /* rs_embed_fm_fwd kernel (id inputs, no x_out): 0 = MFMA K-split,
+                                 1 = VALU/DPP persistent 8-sample tiles, 2 / 3 = MFMA persistent
+                                 16-sample tiles (2 / 1 resident per CU); shapes a kernel does not
+                                 cover run the K-split one.  See DESIGN.md 4.1                    */
+  RS_OPT_COUNT = 1
+};
+
 /* ------------------------------------------------------------------ meta */
 const char* rs_version(void);
 const char* rs_last_error_string(void);
+/* Set option `option` to `value`; returns the previous value, or -1 for an
+ * unknown option / out-of-range value (then nothing changes). */
+int rs_set_option(int option, int value);
+/* Current value of `option`, or -1 for an unknown option. */
+int rs_get_option(int option);
 
 /* --------------------------------------------------------- embedding (a3)
  * Replaces EmbedLayer.call (layer/core.py:273-280) + the dense/sparse concat of

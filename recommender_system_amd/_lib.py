@@ -25,6 +25,8 @@ F = C.c_float
 SIGNATURES = {
     "rs_version": (C.c_char_p, []),
     "rs_last_error_string": (C.c_char_p, []),
+    "rs_set_option": (I, [I, I]),
+    "rs_get_option": (I, [I]),
     "rs_embed_gather": (I, [P, I, L, P, L, I, P, P, P, I, I, P, L, L, P, P]),
     "rs_fm_prepared_size": (L, [I, I, I, I]),
     "rs_fm_prepare": (I, [P, P, I, I, I, I, P, P]),
@@ -131,6 +133,8 @@ SIGNATURES = {
 }
 
 ID_I32, ID_I64, ID_F32 = 0, 1, 2
+FLAG_BAD_ID = 1  # rs_flag bit of the device error flag
+OPT_EMBED_FM_KERNEL = 0  # rs_option
 ACT = {None: 0, "linear": 0, "relu": 1, "prelu": 2, "sigmoid": 3}
 
 _lock = threading.Lock()
@@ -195,6 +199,14 @@ def sgd_update_multi(updates, lr, st) -> None:
     ns = (C.c_int64 * cnt)(*[int(u[2]) for u in updates])
     l2 = (C.c_float * cnt)(*[float(u[3]) for u in updates])
     call("rs_sgd_update_multi", cnt, ws, gs, ns, l2, float(lr), st)
+
+
+def set_option(option: int, value: int) -> int:
+    """rs_set_option: returns the previous value; raises on an unknown option."""
+    prev = lib().rs_set_option(int(option), int(value))
+    if prev < 0:
+        raise RSError(lib().rs_last_error_string().decode())
+    return prev
 
 
 def stream(device=None) -> int:

@@ -22,7 +22,26 @@ int launch_status(const char* what) {
   }
   return RS_OK;
 }
+
+// option values and their valid ranges [lo, hi]
+static int g_opt[RS_OPT_COUNT] = {0};
+static const int g_opt_hi[RS_OPT_COUNT] = {3};
+int opt(int option) { return (option >= 0 && option < RS_OPT_COUNT) ? g_opt[option] : 0; }
 }  // namespace rs
+
+extern "C" int rs_set_option(int option, int value) {
+  if (option < 0 || option >= RS_OPT_COUNT || value < 0 || value > rs::g_opt_hi[option]) {
+    rs::set_error("rs_set_option: unknown option %d or value %d out of range", option, value);
+    return -1;
+  }
+  const int prev = rs::g_opt[option];
+  rs::g_opt[option] = value;
+  return prev;
+}
+
+extern "C" int rs_get_option(int option) {
+  return (option >= 0 && option < RS_OPT_COUNT) ? rs::g_opt[option] : -1;
+}
 
 extern "C" const char* rs_version(void) { return "recommender_system_amd 0.1.0 (gfx950)"; }
 extern "C" const char* rs_last_error_string(void) { return rs::g_err; }

@@ -23,43 +23,12 @@
 //     logit = (x@w1 + w0) + 0.5*(sum_f s_f^2 - sum_i x_i^2 |v_i|^2).
 #include <stdlib.h>
 
+#include "embed_fm.hpp"
 #include "mlp_tower.hpp"
 #include "rs_common.hpp"
 #include "shard_route.hpp"
 
 namespace rs {
-
-// ----------------------------------------------------------- packed layout
-struct FmGeom {
-  int nd, F, k, kfm, d;
-  bool mfma;
-  int KV, NT, DB;
-  int64_t dense_rec, field_rec, field_base, size;
-};
-
-static FmGeom fm_geom(int nd, int F, int k, int kfm) {
-  FmGeom g{};
-  g.nd = nd;
-  g.F = F;
-  g.k = k;
-  g.kfm = kfm;
-  g.d = nd + F * k;
-  const bool kv_ok = (F == 0) || (k % 4 == 0 && (k == 4 || k == 8 || k == 16 || k == 32 || k == 64));
-  g.mfma = kv_ok && kfm >= 1 && kfm + 1 <= 32;
-  if (g.mfma) {
-    g.KV = (F == 0) ? 4 : k / 4;
-    g.NT = (kfm + 1 + 15) / 16;
-    g.DB = (nd + 3) / 4;
-    g.dense_rec = (int64_t)g.NT * 64 + 4;
-    g.field_rec = (int64_t)g.NT * 64 * g.KV + 4 * g.KV;
-    g.field_base = (int64_t)g.DB * g.dense_rec;
-    g.size = g.field_base + (int64_t)F * g.field_rec;
-  } else {
-    // generic path: [w1 (d) | v (d*kfm) | |v_i|^2 (d)]
-    g.size = (int64_t)g.d * (kfm + 2);
-  }
-  return g;
-}
 
 __device__ __forceinline__ float fm_bval(const float* w1, const float* v, int d, int kfm, int e, int colg) {
   if (e >= d) return 0.f;
@@ -128,34 +97,6 @@ __global__ void fm_prepare_generic(const float* __restrict__ w1, const float* __
     out[idx] = val;
   }
 }
-
-// ----------------------------------------------------------- arguments
-struct EmbedFmArgs {
-  const void* ids;
-  int64_t id_stride;
-  const float* dense;
-  int64_t dense_stride;
-  int nd;
-  const float* table;
-  const int64_t* offs;
-  const int64_t* vocab;
-  int F;
-  int k;
-  const float* prep;
-  const float* w0;
-  int kfm;
-  float* logit;
-  float* x_out;
-  int64_t batch;
-  int* err;
-  int DB;
-  int64_t dense_rec, field_rec, field_base;
-  int64_t owner_rows;       // KIND 4: rows of the owner's shard (ids are local rows, -1 = absent)
-  int pw;                   // KIND 4: floats per partial record (logit -> partial records)
-  int64_t pstride;          // KIND 4: floats between consecutive samples' partial records
-  unsigned long long* dbg;  // diagnostic builds only (RS_DIAG_STAMPS): phase stamps
-  int ablate;               // diagnostic builds only: bit0 no MFMA, bit1 no B loads, bit2 no combine
-};
 
 // Phase stamps (s_memrealtime, 100 MHz) for the diagnostic library built by
 // scripts/build_diag.sh; compiled out of librs_hip.so.
@@ -832,6 +773,8 @@ static int run_embed_fm(EmbedFmArgs a, const FmGeom& g, int kind, hipStream_t st
       launch_embed_fm_k<3>(a, 4, g.NT, st);
     } else if (kind == 3) {
       launch_embed_fm_k<3>(a, g.KV, g.NT, st);
+    } else if (launch_embed_fm_tiles(a, g, kind, opt(RS_OPT_EMBED_FM_KERNEL), st)) {
+      // the persistent tile kernels (embed_fm_tiles.hip), when selected and the shape fits
     } else {
       with_id_kind(kind, [&](auto K) { launch_embed_fm_k<decltype(K)::value>(a, g.KV, g.NT, st); });
     }

@@ -5,14 +5,6 @@
 
 #include "rs_common.hpp"
 
-// Dataflow hand-off between whole-column layers: a layer whose predecessor
-// kept whole columns per wave (S == 1) starts without a workgroup barrier;
-// each of its k-groups waits on the LDS ready flag of the predecessor tile it
-// reads (see mlp_tower_tile).
-#ifndef MLP_FLOW
-#define MLP_FLOW 0
-#endif
-
 namespace rs {
 
 constexpr int MLP_MAXL = 8;
@@ -56,7 +48,7 @@ static bool mlp_geom(int L, const int* dims, MlpGeom& g) {
   // Row stride = 8 (mod 64) dwords: the four 16-lane groups of each
   // ds_read_b128 (rows l&15, k-slot l>>4) then hit 16 distinct bank slots.
   g.rs = rup(maxw, 64) + 8;
-  g.lds = (size_t)(32 * g.rs + MLP_NW * 256 + g.ptot + (MLP_FLOW ? MLP_MAXL * 64 : 0)) * sizeof(float);
+  g.lds = (size_t)(32 * g.rs + MLP_NW * 256 + g.ptot) * sizeof(float);
   return g.lds <= 160 * 1024;
 }
 
@@ -126,38 +118,11 @@ __device__ __forceinline__ void mlp_ring_fill(floatx4 (&ring)[MLP_R], const floa
   for (int u = 0; u < MLP_R; ++u) ring[u] = bp[(int64_t)min(g0 + u, g1 - 1) * 64];
 }
 
-// Ready mask of the predecessor's output tiles (bit j = tile j published):
-// one flag per lane, one ballot; spins with s_sleep, bounded (a flag never
-// published would be a bug: the bound turns a hang into wrong output).
-struct MlpWait {
-  const int* fl;  // predecessor's per-tile ready flags (nullptr: barrier-ordered)
-  int G;
-  uint64_t mask;
-};
-__device__ __forceinline__ void mlp_wait_group(MlpWait& wt, int j) {
-  if (!wt.fl) return;
-  int spins = 0;
-  while (!((wt.mask >> j) & 1ull)) {
-    const int lane = threadIdx.x & 63;
-    const int v = lane < wt.G ? __hip_atomic_load(wt.fl + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 1;
-    wt.mask = __ballot(v != 0);
-    if ((wt.mask >> j) & 1ull) break;
-    if (++spins > (1 << 20)) {
-      wt.mask = ~0ull;
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
 template <int D>
 __device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[MLP_R], const float* __restrict__ ap,
-                                          const floatx4* __restrict__ bp, int g0, int g1, floatx4& acc,
-                                          MlpWait& wt) {
+                                          const floatx4* __restrict__ bp, int g0, int g1, floatx4& acc) {
   // A fragments are read one group ahead so the LDS latency hides behind
   // the previous group's MFMAs
-  mlp_wait_group(wt, g0);
   floatx4 an = *reinterpret_cast<const floatx4*>(ap + 16 * g0);
 #if MLP_ACC2
   // two accumulation chains (k-steps 0,2 / 1,3 of every group): half the
@@ -168,7 +133,6 @@ __device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[MLP_R], const float* _
 #pragma unroll
     for (int u = 0; u < D; ++u) {
       const floatx4 av = an;
-      mlp_wait_group(wt, min(g + u + 1, g1 - 1));
       an = *reinterpret_cast<const floatx4*>(ap + 16 * min(g + u + 1, g1 - 1));
       __builtin_amdgcn_sched_barrier(0);
 #if MLP_ACC2
@@ -196,17 +160,17 @@ __device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[MLP_R], const float* _
 }
 
 __device__ __forceinline__ void mlp_mac(floatx4 (&ring)[MLP_R], const float* ap, const floatx4* bp, int g0, int g1,
-                                        floatx4& acc, MlpWait& wt) {
+                                        floatx4& acc) {
   const int n = g1 - g0;  // wave-uniform
   if constexpr (MLP_R >= 9) {
-    if (n % 9 == 0) return mlp_mac_d<9>(ring, ap, bp, g0, g1, acc, wt);
-    if (n % 8 == 0) return mlp_mac_d<8>(ring, ap, bp, g0, g1, acc, wt);
-    if (n % 6 == 0) return mlp_mac_d<6>(ring, ap, bp, g0, g1, acc, wt);
+    if (n % 9 == 0) return mlp_mac_d<9>(ring, ap, bp, g0, g1, acc);
+    if (n % 8 == 0) return mlp_mac_d<8>(ring, ap, bp, g0, g1, acc);
+    if (n % 6 == 0) return mlp_mac_d<6>(ring, ap, bp, g0, g1, acc);
   }
   // (a 4-deep ring gets a full vmcnt(0) at its loop head from the compiler)
-  if (n % 3 == 0) mlp_mac_d<3>(ring, ap, bp, g0, g1, acc, wt);
-  else if (n % 2 == 0) mlp_mac_d<2>(ring, ap, bp, g0, g1, acc, wt);
-  else mlp_mac_d<1>(ring, ap, bp, g0, g1, acc, wt);
+  if (n % 3 == 0) mlp_mac_d<3>(ring, ap, bp, g0, g1, acc);
+  else if (n % 2 == 0) mlp_mac_d<2>(ring, ap, bp, g0, g1, acc);
+  else mlp_mac_d<1>(ring, ap, bp, g0, g1, acc);
 }
 
 // The tower on a 16-row tile whose input is already in LDS buf0 (barrier not
@@ -221,27 +185,12 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
-  // per (layer, output tile) ready flags after the bias/alpha block; zeroed
-  // before the first barrier (nothing touches them earlier)
-  int* flags = reinterpret_cast<int*>(par + a.ptot);
-  if (MLP_FLOW)
-    for (int i = threadIdx.x; i < MLP_MAXL * 64; i += NW * 64) flags[i] = 0;
   float* in = smem;
   float* out = smem + 16 * RS;
-  int Sprev = 0;
   for (int l = 0; l < a.L; ++l) {
     const int T = a.Np[l] >> 4, G = a.Kp[l] >> 4;
     const int S = mlp_slices(T, G, NW);
-    // Barrier-free hand-off when the predecessor kept whole columns: every
-    // k-group of this layer is one predecessor tile, published by its flag.
-    // Write-after-read on `out` (the predecessor's input) is safe: a wave of
-    // this layer writes `out` only after all predecessor tiles are ready,
-    // i.e. after every predecessor item finished reading it (S == 1 items
-    // span all k-groups; S > 1 items write `red` and meet at a barrier).
-    const bool flow = MLP_FLOW && l > 0 && Sprev == 1;
-    if (!flow) __syncthreads();
-    MlpWait wt{flow ? flags + (l - 1) * 64 : nullptr, G, 0ull};
-    const bool publish = MLP_FLOW && S == 1 && l + 1 < a.L;
+    __syncthreads();
     MLP_STAMP(2 + 2 * l);
     const floatx4* W = reinterpret_cast<const floatx4*>(a.prep + a.off[l]) + lane;
     const float* bias = par + a.poff[l];
@@ -275,15 +224,10 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
       const floatx4* bp = W + (int64_t)it.t * G * 64;
       if (item != w) mlp_ring_fill(ring, bp, it.g0, it.g1);
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-      mlp_mac(ring, ap, bp, it.g0, it.g1, acc, wt);
+      mlp_mac(ring, ap, bp, it.g0, it.g1, acc);
       if (S == 1) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) finish(4 * (lane >> 4) + r, 16 * it.t + (lane & 15), acc[r]);
-        if (publish) {
-          // the tile's LDS writes complete before its flag (release)
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          if (lane == 0) __hip_atomic_fetch_add(flags + l * 64 + it.t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
       } else {
         *reinterpret_cast<floatx4*>(red + item * 256 + lane * 4) = acc;
       }
@@ -312,7 +256,6 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
     float* tmp = in;
     in = out;
     out = tmp;
-    Sprev = S;
   }
   MLP_STAMP(15);
 }

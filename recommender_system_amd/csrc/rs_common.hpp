@@ -64,9 +64,14 @@ inline void with_id_kind(int kind, Fn&& f) {
   }
 }
 
-__device__ __forceinline__ void flag_error(int* err_flag) {
-  if (err_flag) __hip_atomic_store(err_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Device error flag: RS_FLAG_BAD_ID (an id outside [0, vocab)) unless another
+// code is given; codes are or-ed, so one flag carries every kind seen.
+__device__ __forceinline__ void flag_error(int* err_flag, int code = RS_FLAG_BAD_ID) {
+  if (err_flag) __hip_atomic_fetch_or(err_flag, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// Runtime tuning options (rs_set_option); read on the host at launch time.
+int opt(int option);
 
 template <int N>
 struct VecF;
@@ -135,8 +140,6 @@ struct Chunk {
   }
 };
 
-// Sum over the 16 lanes of a DPP row (lanes 16r..16r+15); every lane of the
-// row receives the total.  Four row_ror steps, VALU only.
 // Sorted-segment helpers for the deterministic scatter-adds (embedding SGD,
 // FM training, dedup gradients): the end of key r's segment starting at p
 // (binary search: keys are sorted), and the segment's sum of get(q) with 8
@@ -253,6 +256,8 @@ inline int64_t seg_chunk(int W) {
   return C;
 }
 
+// Sum over the 16 lanes of a DPP row (lanes 16r..16r+15); every lane of the
+// row receives the total.  Four row_ror steps, VALU only.
 __device__ __forceinline__ float row16_sum(float x) {
   x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xF, 0xF, false));
   x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x124, 0xF, 0xF, false));

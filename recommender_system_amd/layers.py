@@ -66,14 +66,18 @@ def _ids_tensor(ids, device):
 
 
 class _ErrFlag:
-    """Device int flag set by kernels on an out-of-range id."""
+    """Device int flag the kernels OR rs_flag bits into: an out-of-range id
+    (IndexError, as TF's Embedding raises) or a kernel-internal failure."""
 
     def __init__(self, device):
         self.t = torch.zeros(1, dtype=torch.int32, device=device)
 
     def check(self, what):
-        if int(self.t.item()) != 0:
+        v = int(self.t.item())
+        if v != 0:
             self.t.zero_()
+            if v & ~_lib.FLAG_BAD_ID:
+                raise _lib.RSError(f"{what}: kernel error flag {v:#x}")
             raise IndexError(f"{what}: embedding id out of range (indices must be in [0, vocab))")
 
 

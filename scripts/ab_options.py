@@ -1,0 +1,108 @@
+"""A/B timing of a runtime option (rs_set_option) on one workload, values
+alternated in rounds so drift on the box hits every arm; each arm is
+graph-replayed (the option is read at capture time).
+
+  python scripts/ab_options.py --option mlp_flow --workload deepfm
+  python scripts/ab_options.py --option embed_fm_kernel --workload embed_fm --batch 16384
+
+Prints one JSON line: per value the median us per launch and the max scaled
+difference of its output against value 0's.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+OPTS = {"embed_fm_kernel": 0}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--option", default="embed_fm_kernel", choices=sorted(OPTS))
+    ap.add_argument("--values", default="0,1")
+    ap.add_argument("--workload", default="deepfm", choices=["deepfm", "dcn", "embed_fm"])
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--vocab", type=float, default=1e7)
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--chunk", type=int, default=64)
+    ap.add_argument("--pool", type=int, default=64)
+    args = ap.parse_args()
+    import recommender_system_amd as rs
+    from recommender_system_amd import _lib
+
+    dev = torch.device("cuda")
+    B, F, k, nd = args.batch, 26, 16, 13
+    V = int(args.vocab) if args.workload == "embed_fm" else int(1e6)
+    cols = [[{"feat": f"I{i + 1}"} for i in range(nd)],
+            [{"feat": f"C{i + 1}", "feat_onehot_dim": V, "embed_dim": k} for i in range(F)]]
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    NP = args.pool
+    ids = torch.randint(0, V, (NP, B, F), generator=g, device=dev, dtype=torch.int32)
+    dense = torch.rand(NP, B, nd, generator=g, device=dev)
+    if args.workload == "dcn":
+        m = rs.DCN(cols, [256, 128, 64], 1, "relu", layer_num=3, embed_dim=k, seed=3, device=dev)
+
+        def fn(i):
+            outs[i % NP] = m.forward_fused((dense[i % NP], ids[i % NP]), check_ids=False)
+    else:
+        m = rs.DeepFM(cols, 10, 1e-4, 1e-4, [256, 128, 64], 1, "relu", embed_dim=k, seed=3, device=dev)
+        if args.workload == "deepfm":
+            def fn(i):
+                outs[i % NP] = m.forward_fused((dense[i % NP], ids[i % NP]), check_ids=False)
+        else:
+            def fn(i):
+                outs[i % NP] = m.fm_logit((dense[i % NP], ids[i % NP]), check_ids=False)
+    outs = {}  # step -> output tensor of the last call (graph memory after capture)
+    opt = OPTS[args.option]
+    values = [int(v) for v in args.values.split(",")]
+    graphs, res = {}, {}
+    for v in values:
+        _lib.set_option(opt, v)
+        for i in range(NP):
+            fn(i)
+        torch.cuda.synchronize()
+        gr = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(gr, stream=s):
+                for i in range(args.chunk):
+                    fn(i)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        gr.replay()
+        torch.cuda.synchronize()
+        res[v] = {"out": torch.cat([outs[i % NP] for i in range(max(0, args.chunk - NP), args.chunk)]).clone(), "us": []}
+        graphs[v] = gr
+    _lib.set_option(opt, 0)
+    for r in range(args.rounds):
+        for v in (values if r % 2 == 0 else values[::-1]):
+            gr = graphs[v]
+            gr.replay()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                gr.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            res[v]["us"].append(e0.elapsed_time(e1) * 1e3 / (10 * args.chunk))
+    base = res[values[0]]["out"]
+    rms = float(base.pow(2).mean().sqrt())
+    line = {"option": args.option, "workload": args.workload, "batch": B,
+            "us_per_launch_median": {v: float(np.median(res[v]["us"])) for v in values},
+            "us_per_launch_all": {v: [round(x, 3) for x in res[v]["us"]] for v in values},
+            "max_scaled_diff_vs_first": {v: float(((res[v]["out"] - base).abs() / base.abs().clamp_min(rms)).max())
+                                         for v in values}}
+    print(json.dumps(line))
+
+
+if __name__ == "__main__":
+    main()

@@ -70,3 +70,21 @@ def test_signature_arity_matches_header():
         name, params = m.group(1), m.group(2).strip()
         n = 0 if params in ("", "void") else len(params.split(","))
         assert len(_lib.SIGNATURES[name][1]) == n, f"{name}: header has {n} params"
+
+
+def test_runtime_options():
+    """rs_set_option / rs_get_option: known options round-trip, unknown ones
+    and out-of-range values are refused without changing anything."""
+    lib = _lib.lib()
+    opt = _lib.OPT_EMBED_FM_KERNEL
+    cur = lib.rs_get_option(opt)
+    assert cur >= 0
+    for v in range(4):
+        assert lib.rs_set_option(opt, v) >= 0
+        assert lib.rs_get_option(opt) == v
+    assert lib.rs_set_option(opt, cur) == 3
+    assert lib.rs_set_option(opt, 7) == -1 and lib.rs_get_option(opt) == cur
+    assert lib.rs_get_option(99) == -1
+    assert lib.rs_set_option(-1, 0) == -1 and b"unknown option" in lib.rs_last_error_string()
+    with pytest.raises(_lib.RSError):
+        _lib.set_option(99, 1)

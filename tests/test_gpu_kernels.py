@@ -100,6 +100,74 @@ def test_embed_fm_fused(gpu, k, kfm, F, nd, B):
     assert err.item() == 0
 
 
+# the rs_embed_fm_fwd kernel variants (RS_OPT_EMBED_FM_KERNEL): 0 = K-split
+# MFMA, 1 = VALU/DPP tiles, 2 / 3 = pipelined MFMA tiles (2 / 1 per CU).
+# Shapes a variant does not cover fall back to the K-split kernel; the cases
+# below include several tiles per workgroup (B past 256 or 512 tiles), ragged
+# tails, batch 1, odd F, F at each kernel's limit and every id dtype.
+@pytest.fixture
+def embed_fm_variant(request, gpu):
+    from recommender_system_amd import _lib
+    prev = _lib.set_option(_lib.OPT_EMBED_FM_KERNEL, request.param)
+    yield request.param
+    _lib.set_option(_lib.OPT_EMBED_FM_KERNEL, prev)
+
+
+@pytest.mark.parametrize("embed_fm_variant", [0, 1, 2, 3], indirect=True)
+@pytest.mark.parametrize("k,kfm,F,nd,B,idt", [
+    (16, 10, 26, 13, 9000, "i32"),   # headline shape, several tiles per workgroup
+    (16, 10, 26, 13, 1, "i64"),
+    (16, 10, 27, 13, 300, "f32"),    # odd F
+    (16, 8, 30, 32, 2071, "i32"),    # VALU limits: F 30, nd 32
+    (16, 10, 32, 13, 77, "i64"),     # MFMA-tile limit F = 32
+    (8, 10, 26, 13, 4113, "i32"),    # k = 8 (MFMA tiles KV 2; VALU falls back)
+    (16, 16, 20, 5, 130, "i32"),     # two MFMA column tiles
+    (16, 10, 5, 0, 33, "i32"),       # no dense block
+])
+def test_embed_fm_kernel_variants(gpu, embed_fm_variant, k, kfm, F, nd, B, idt):
+    from recommender_system_amd import _lib
+    rng = np.random.default_rng(B + F + k + kfm)
+    vocabs = rng.integers(2, 3000, size=F).tolist()
+    offs, offs_d, voc_d = _layout(vocabs, gpu)
+    d = nd + F * k
+    table = rng.uniform(-0.05, 0.05, size=(sum(vocabs), k)).astype(np.float32)
+    w1 = (rng.standard_normal((d, 1)) * 0.05).astype(np.float32)
+    v = (rng.standard_normal((d, kfm)) * 0.05).astype(np.float32)
+    w0 = np.array([-0.031], np.float32)
+    ids = random_ids(rng, B, vocabs)
+    ids[0] = np.asarray(vocabs) - 1
+    dense = rng.random((B, nd)).astype(np.float32)
+    prep = torch.empty(_lib.lib().rs_fm_prepared_size(nd, F, k, kfm), device=gpu)
+    w1_d, v_d, w0_d = _t(w1, gpu), _t(v, gpu), _t(w0, gpu)
+    _lib.call("rs_fm_prepare", w1_d.data_ptr(), v_d.data_ptr(), nd, F, k, kfm, prep.data_ptr(), 0)
+    kind, dt = {"i32": (0, torch.int32), "i64": (1, torch.int64), "f32": (2, torch.float32)}[idt]
+    ids_d, dense_d, tab_d = _t(ids, gpu, dt), _t(dense, gpu), _t(table, gpu)
+    logit = torch.full((B,), 99.0, device=gpu)
+    err = torch.zeros(1, dtype=torch.int32, device=gpu)
+
+    def run(ids_t):
+        _lib.call("rs_embed_fm_fwd", ids_t.data_ptr(), kind, ids_t.stride(0),
+                  dense_d.data_ptr() if nd else None, nd, nd, tab_d.data_ptr(), offs_d.data_ptr(),
+                  voc_d.data_ptr(), F, k, prep.data_ptr(), w0_d.data_ptr(), kfm, logit.data_ptr(), None, B,
+                  err.data_ptr(), 0)
+        torch.cuda.synchronize()
+
+    run(ids_d)
+    tables = [table[o:o + vv] for o, vv in zip(offs, vocabs)]
+    x = np.concatenate([dense, O.embed_layer(ids, tables, np.float64)], 1)
+    assert_scaled_close(logit, O.fm_layer(x, w0, w1, v)[:, 0], what=f"embed_fm variant {embed_fm_variant}")
+    assert err.item() == 0
+    bad = ids.copy()
+    bad[B - 1, F - 1] = vocabs[F - 1]  # the last sample's last field: out of range
+    run(_t(bad, gpu, dt))
+    assert err.item() != 0
+    err.zero_()
+    bad[B - 1, F - 1] = 0
+    bad[B // 2, 0] = -1
+    run(_t(bad, gpu, dt))
+    assert err.item() != 0
+
+
 def test_embed_fm_packed_float_X_and_oor(gpu):
     """Packed X[B,39] float ids (Keras int32 truncation) and the OOR flag."""
     from recommender_system_amd import DeepFM
@@ -649,7 +717,8 @@ def test_full_size_table_addressing(gpu):
     assert_scaled_close(xin, pref, what="PNN both @16.6 GB")
 
 
-def test_headline_shape_full_size(gpu):
+@pytest.mark.parametrize("embed_fm_variant", [0, 1, 2, 3], indirect=True)
+def test_headline_shape_full_size(gpu, embed_fm_variant):
     """The headline configuration itself (BASELINE metric: batch 4096, 26 x
     1e7 x 16 fp32 table = 16.6 GB, uniform int32 ids over the full range):
     rs_embed_fm_fwd (the benched kernel, DeepFM.fm_logit) and the fused DeepFM
