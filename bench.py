@@ -300,6 +300,8 @@ def bench_hotpath(args, world, rank):
         result["ms_per_step"] = dt / args.steps * 1e3
         result["roofline"] = {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                               "frac": achieved / PEAK_HBM, "traffic": _pmc_traffic(),
+                              "traffic_source": "profiles/pmc_embed_fm.json (rocprofv3 PMC pass of this kernel at "
+                                                "this shape: TCC_EA0_RDREQ x 128 B + WRITE_SIZE per launch)",
                               "kernel": "embed_fm_mfma", "kernel_ms": kern_ms,
                               "kernel_ms_source": "HIP events around the graph-replayed timed region / steps "
                                                   "(kernel + back-to-back dispatch boundary)",
@@ -380,13 +382,20 @@ def bench_hotpath(args, world, rank):
             result["cpu_baseline"] = cb
         else:
             result["cpu_baseline"] = None
+        # config 5 at world 1 with the exchange forced (RCCL self-exchange): the
+        # same workload as the driver's N > 1 lines, so the 1 -> N curve has an anchor
+        if not args.no_config5:
+            _world1_group()
+            c5, _ = bench_sharded_deepfm(args, 1, 0, lite=True)
+            c5["note"] = ("BASELINE config 5 at N = 1: ShardedDeepFM forward on the 1e8-row table with the row "
+                          "exchange forced through RCCL (self-exchange), B 4096 - the workload of the N > 1 lines")
+            result["config5_n1"] = c5
     else:
         res, V5 = bench_sharded_deepfm(args, world, rank)
         result.update(res)
         result["vocab_per_field"] = V5
         if not args.deepfm_only:
             result["fm_hotpath_sharded"] = bench_sharded_fm(args, world, rank, vocabs, dense_pool)
-        result["cpu_baseline"] = None
     return result
 
 
@@ -519,7 +528,69 @@ def bench_sharded_fm(args, world, rank, vocabs, dense_pool):
         "world1_no_exchange": local}
 
 
-def bench_sharded_deepfm(args, world, rank):
+def _cpu_leg_config5(args, world, rank, model, dense_pool, ids_pool, out, B, n_batches=4):
+    """cpu_baseline of config 5 on rank 0: the oracle's numpy fp32 DeepFM
+    (model/deepFM.py:23-31 restated; TF not installed) on rank 0's batches,
+    with the embedding rows copied from the shards — every rank runs the
+    sharded forward of those batches (the exchange is collective), rank 0 reads
+    each lookup's row out of its row-exchange buffer (got[slot_of]) — and
+    max_scaled_diff_vs_gpu against rank 0's GPU output of the same batch."""
+    if not args.cpu_baseline:
+        return None
+    rb = model._rbufs(B, dedup=False)
+    host = []
+    for j in range(n_batches):
+        model.forward((dense_pool[j], ids_pool[j]), check=False, out=out)
+        torch.cuda.synchronize()
+        if rank == 0:
+            emb = rb["got"][rb["slot_of"].reshape(-1).long()].reshape(B, model.F, model.k)
+            host.append((dense_pool[j].cpu().numpy(), emb.cpu().numpy(), out.cpu().numpy().copy()))
+    _barrier(world)
+    if rank != 0:
+        return None
+    from oracle import ctr_oracle as O
+    c = lambda t: t.detach().cpu().numpy()
+    p = {"w0": c(model.emb.w0), "w1": c(model.emb.w1), "v": c(model.emb.v),
+         "dnn_hidden": [(c(l.kernel), c(l.bias)) for l in model.dnn.hidden_layer],
+         "dnn_out": (c(model.dnn.output_layer.kernel), c(model.dnn.output_layer.bias))}
+    ids = np.tile(np.arange(B, dtype=np.int64)[:, None], (1, model.F))
+    n, first, t0 = 0, None, time.perf_counter()
+    while n < 64 and (time.perf_counter() - t0) < args.cpu_budget:
+        dense, emb, g = host[n % len(host)]
+        p["tables"] = [emb[:, f, :] for f in range(model.F)]
+        y, _, _ = O.deepfm(None, p, dt=np.float32, inputs=(dense, ids))
+        if first is None:
+            first = (np.asarray(y, np.float64), g)
+        n += 1
+    dt = time.perf_counter() - t0
+    ref, g = first
+    return {"value": n * B / dt, "unit": "samples/s", "cores": _cpu_threads(), "kind": "port",
+            "sample": f"{n} batches x {B} samples of rank 0 (of {world}): numpy fp32 DeepFM forward (the reference "
+                      f"TF graph restated; TF not installed) - EmbedLayer gather, FMLayer, DNNLayer "
+                      f"429-256-128-64-1, sigmoid; the batch's rows copied from the shards (via rank 0's row "
+                      f"exchange) into per-field host tables of the batch's own rows",
+            "max_scaled_diff_vs_gpu": float(np.max(np.abs(g.reshape(ref.shape) - ref) / np.abs(ref)))}
+
+
+def _world1_group():
+    """A one-rank RCCL process group for the config-5 anchor inside the
+    default N = 1 run (the driver's 1 -> N curve then has a same-workload
+    point); MASTER_ADDR 127.0.0.1, a free port unless MASTER_PORT is set."""
+    import socket
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in os.environ:
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(so.getsockname()[1])
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+
+
+def bench_sharded_deepfm(args, world, rank, lite=False):
     """BASELINE config 5 (the N>1 value, and --sharded at N=1): DeepFM forward
     with ONE 1e8-row table (26 fields x 3,846,154 rows x 16 fp32 = 6.4 GB)
     row-sharded over the ranks, B = 4096 local samples per rank (weak
@@ -573,6 +644,25 @@ def bench_sharded_deepfm(args, world, rank):
 
     fdt, fslot_ms = _timed_graph(finish, args.steps, 2, world, chunk=16)
     fin_ms = _max_over_ranks(fslot_ms, world)
+    flops = B * 2 * (429 * 256 + 256 * 128 + 128 * 64 + 64)
+    ms = dt / args.steps * 1e3
+    S = model.emb.slot_stride
+    roof = {"bound": "mfma", "achieved": flops / (fin_ms * 1e-3) / 1e12, "peak": PEAK_F32 / 1e12,
+            "unit": "TFLOP/s", "frac": flops / (fin_ms * 1e-3) / PEAK_F32, "traffic": None,
+            "kernel": "deepfm_fused (rs_deepfm_fwd from the row-exchange buffer)",
+            "kernel_ms": fin_ms, "dnn_flop_per_launch": flops,
+            "kernel_ms_source": "HIP events around graph-replayed launches of the fused kernel alone"}
+    exch = {"protocol": "field-range row records: rs_shard_row_route, RCCL all-to-all of row ids, "
+                        "owner rs_gather_rows, RCCL all-to-all of rows, rs_deepfm_fwd with ids = slot_of",
+            "timing": timing, "rows_per_rank": model.emb.rows_per_rank,
+            "owner_field_ranges": model.emb.owner_field_ranges, "slots_per_sample_per_owner": S,
+            "id_bytes_per_rank_each_way": world * B * S * 4,
+            "row_bytes_per_rank_each_way": world * B * S * k * 4,
+            "exchange_ms_per_step": ms - fin_ms}
+    cpu = _cpu_leg_config5(args, world, rank, model, dense_pool, ids_pool, out, B)
+    if lite:
+        return {"samples_per_s": world * args.steps * B / dt, "ms_per_step": ms, "roofline": roof,
+                "exchange": exch, "cpu_baseline": cpu}, V
     # secondary: the deduplicated exchange on Zipf(1.2) ids (hot rows repeat:
     # each owner receives every distinct row once per rank) and the training
     # step (forward exchange, local backward, reverse all-to-all of dL/drow,
@@ -604,7 +694,7 @@ def bench_sharded_deepfm(args, world, rank):
 
     def train(i):
         j = i % npool
-        model.train_step((dense_pool[j], ids_pool[j]), labels[j], lr=0.01, check=False, dropout=False)
+        model.train_step((dense_pool[j], ids_pool[j]), labels[j], lr=0.01, check=False)
 
     nt = max(10, args.steps // 4)
     tdt, _ = _timed(train, nt, 2, world, events=False)
@@ -619,22 +709,8 @@ def bench_sharded_deepfm(args, world, rank):
                  "timing": "HIP graph replay",
                  "note": "world 1 without the RCCL self-exchange (ShardedDeepFM.forward -> rs_deepfm_fwd on the "
                          "shard); the exchange line above is the comparison"}
-    flops = B * 2 * (429 * 256 + 256 * 128 + 128 * 64 + 64)
-    ms = dt / args.steps * 1e3
-    S = model.emb.slot_stride
-    res = {"value": world * args.steps * B / dt, "ms_per_step": ms,
-           "roofline": {"bound": "mfma", "achieved": flops / (fin_ms * 1e-3) / 1e12, "peak": PEAK_F32 / 1e12,
-                        "unit": "TFLOP/s", "frac": flops / (fin_ms * 1e-3) / PEAK_F32, "traffic": None,
-                        "kernel": "deepfm_fused (rs_deepfm_fwd from the row-exchange buffer)",
-                        "kernel_ms": fin_ms, "dnn_flop_per_launch": flops,
-                        "kernel_ms_source": "HIP events around graph-replayed launches of the fused kernel alone"},
-           "exchange": {"protocol": "field-range row records: rs_shard_row_route, RCCL all-to-all of row ids, "
-                                    "owner rs_gather_rows, RCCL all-to-all of rows, rs_deepfm_fwd with ids = slot_of",
-                        "timing": timing, "rows_per_rank": model.emb.rows_per_rank,
-                        "owner_field_ranges": model.emb.owner_field_ranges, "slots_per_sample_per_owner": S,
-                        "id_bytes_per_rank_each_way": world * B * S * 4,
-                        "row_bytes_per_rank_each_way": world * B * S * k * 4,
-                        "exchange_ms_per_step": ms - fin_ms},
+    res = {"value": world * args.steps * B / dt, "ms_per_step": ms, "roofline": roof, "exchange": exch,
+           "cpu_baseline": cpu,
            "zipf_ids": {"distinct_lookup_fraction": distinct,
                         "field_range_records": {"samples_per_s": world * nz * B / zdt, "ms_per_step": zdt / nz * 1e3,
                                                 "row_bytes_per_rank_each_way": world * B * S * k * 4},
@@ -1260,7 +1336,7 @@ def bench_fm_train(args, world, rank):
     lab = (torch.rand(16, B, device=dev) < 0.25).to(torch.float32)
 
     def step_dfm(i):
-        dfm.train_step((dense_pool[i % 16], ids_pool[i % 16]), lab[i % 16], lr=0.01, check_ids=False, dropout=False)
+        dfm.train_step((dense_pool[i % 16], ids_pool[i % 16]), lab[i % 16], lr=0.01, check_ids=False)
 
     n_d = max(10, args.steps // 5)
     dtd, _ = _timed_graph(step_dfm, n_d, args.warmup, world, chunk=16)
@@ -1269,7 +1345,7 @@ def bench_fm_train(args, world, rank):
     dcn = rs.DCN(cols, [256, 128, 64], 1, "relu", 3, embed_dim=16, seed=SEED, device=dev)
 
     def step_dcn(i):
-        dcn.train_step((dense_pool[i % 16], ids_pool[i % 16]), lab[i % 16], lr=0.01, check_ids=False, dropout=False)
+        dcn.train_step((dense_pool[i % 16], ids_pool[i % 16]), lab[i % 16], lr=0.01, check_ids=False)
 
     dtc, _ = _timed_graph(step_dcn, n_d, args.warmup, world, chunk=16)
     return _line("FM training samples/sec @ batch 4096, 26 x 1e6 one-hot columns, k 16 (SGD + l2, compile_fit)",
@@ -1355,6 +1431,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--deepfm-only", dest="deepfm_only", action="store_true",
                     help="sharded: skip the secondary FM hot-path protocols")
+    ap.add_argument("--no-config5", dest="no_config5", action="store_true",
+                    help="N=1: skip the nested config-5 anchor (config5_n1)")
     ap.add_argument("--sharded", action="store_true",
                     help="time the row-sharded exchange path even at world 1 (N=1 point of the sharded curve)")
     args = ap.parse_args()
@@ -1368,6 +1446,7 @@ def main():
         return
     if args.config == "deepfm1e6":
         args.vocab = 1e6
+        args.no_config5 = True
     elif args.config != "hotpath":
         raise SystemExit(f"unknown --config {args.config}")
     res = bench_hotpath(args, world, rank)
@@ -1379,7 +1458,10 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": ({"workload": "deepfm_embed_fm_hotpath", "global_batch": args.batch, "batch_per_gpu": args.batch,
                         "sparse_fields": 26, "vocab_per_field": int(args.vocab), "embed_dim": 16, "fm_k": 10,
-                        "dense_features": 13, "ids": "int32 uniform per field", "parallelism": "dp1"}
+                        "dense_features": 13, "ids": "int32 uniform per field", "parallelism": "dp1",
+                        "value_kind": "embed + FM logit (DeepFM's EmbedLayer + concat + FMLayer; no DNN, no "
+                                      "sigmoid) - the full DeepFM forward is deepfm_forward, config 5 at N = 1 "
+                                      "is config5_n1"}
                        if world == 1 and not args.sharded else
                        {"workload": "deepfm_forward_rowsharded_1e8 (BASELINE config 5)",
                         "global_batch": args.batch * world, "batch_per_gpu": args.batch, "sparse_fields": 26,
@@ -1388,8 +1470,8 @@ def main():
                         "ids": "int32 uniform per field", "parallelism": f"dp{world}+rowshard{world}"}),
             "roofline": res["roofline"], "cpu_baseline": res["cpu_baseline"],
         }
-        for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "exchange", "train_step", "fm_hotpath_sharded",
-                    "world1_no_exchange"):
+        for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "config5_n1", "exchange", "train_step",
+                    "fm_hotpath_sharded", "world1_no_exchange"):
             if key in res:
                 line[key] = res[key]
         _emit(line)

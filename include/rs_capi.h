@@ -428,6 +428,18 @@ int rs_fm_train_step(const void* ids, int id_kind, int64_t id_stride,
                      float lr, float l2_w, float l2_v, void* workspace,
                      float* loss, int* err_flag, rs_stream_t stream);
 
+/* rs_dropout: DNNLayer's Dropout(rate) in training (layer/interaction.py:35,44;
+ * active under compile_fit's model.fit, utils/compile_fit.py:14), in place on
+ * x[rows, cols] (row stride ld): x <- keep ? x / (1 - rate) : 0 with
+ * keep = u >= rate, u from Philox4x32-10 (key = seed, counter =
+ * (offset + row*cols + col) / 4, word (offset + e) % 4, u = (word >> 8) 2^-24).
+ * offset % 4 == 0; callers advance it by 4*ceil(rows*cols/4) per draw.  The
+ * same (seed, offset) applied to dL/dx is the backward (the mask is never
+ * stored).  TF's own draws cannot be reproduced; oracle.dropout_multiplier
+ * restates this generator exactly.                                          */
+int rs_dropout(float* x, int64_t ld, int64_t rows, int64_t cols, float rate,
+               uint64_t seed, uint64_t offset, rs_stream_t stream);
+
 /* DeepFM training (model/deepFM.py + utils/compile_fit.py; the host layer
  * DeepFM.train_step composes these with rs_embed_gather / rs_dense_fwd /
  * rs_fm_fwd):

@@ -569,13 +569,81 @@ def ffm_train_step(dense, ids, t, w0, w, v, onehot_dims, lr, l2_w, l2_v, dt=np.f
     return (w0 - lr * g.sum(keepdims=True)[:1], w - lr * dw, v - lr * dv), loss
 
 
-def deepfm_train_step(dense, ids, t, p, lr, l2_w, l2_v, nd=13, act="relu", dt=np.float64):
+def _dnn_train_acts(x, layers, act, masks, dt):
+    """DNNLayer.call in training (layer/interaction.py:40-46): Dense +
+    activation, then Dropout (masks[i] or the identity) per hidden layer."""
+    acts = [x]
+    for i, (W, b) in enumerate(layers[:-1]):
+        a = activation(acts[-1] @ W + b, act)
+        acts.append(a * np.asarray(masks[i], dt) if masks is not None else a)
+    return acts
+
+
+def _dnn_train_bwd(delta, layers, acts, act, masks, lr):
+    """Backward of _dnn_train_acts + the output Dense: returns the SGD-updated
+    layers and dL/dx.  Through hidden layer i: ReLU' = [a > 0] (a after the
+    dropout: zero where dropped) and the dropout multiplier masks[i]."""
+    new_layers = [None] * len(layers)
+    for li in reversed(range(len(layers))):
+        W, b = layers[li]
+        dW, db = acts[li].T @ delta, delta.sum(0)
+        prev = delta @ W.T
+        if li > 0 and act == "relu":
+            prev = prev * (acts[li] > 0)
+        if li > 0 and masks is not None:
+            prev = prev * np.asarray(masks[li - 1], prev.dtype)
+        new_layers[li] = (W - lr * dW, b - lr * db)
+        delta = prev
+    return new_layers, delta
+
+
+_PHILOX_M = (np.uint64(0xD2511F53), np.uint64(0xCD9E8D57))
+_PHILOX_W = (np.uint32(0x9E3779B9), np.uint32(0xBB67AE85))
+
+
+def philox4x32_10(ctr, seed):
+    """Philox4x32-10 (Salmon et al., SC'11) on counters ctr (uint64 array,
+    words (lo, hi, 0, 0)) with the 64-bit key seed: returns [n, 4] uint32."""
+    ctr = np.asarray(ctr, np.uint64)
+    c = [(ctr & np.uint64(0xFFFFFFFF)).astype(np.uint32), (ctr >> np.uint64(32)).astype(np.uint32),
+         np.zeros(ctr.shape, np.uint32), np.zeros(ctr.shape, np.uint32)]
+    k0, k1 = np.uint32(seed & 0xFFFFFFFF), np.uint32((seed >> 32) & 0xFFFFFFFF)
+    with np.errstate(over="ignore"):
+        for _ in range(10):
+            p0 = _PHILOX_M[0] * c[0].astype(np.uint64)
+            p1 = _PHILOX_M[1] * c[2].astype(np.uint64)
+            c = [(p1 >> np.uint64(32)).astype(np.uint32) ^ c[1] ^ k0, (p1 & np.uint64(0xFFFFFFFF)).astype(np.uint32),
+                 (p0 >> np.uint64(32)).astype(np.uint32) ^ c[3] ^ k1, (p0 & np.uint64(0xFFFFFFFF)).astype(np.uint32)]
+            k0 = np.uint32(k0 + _PHILOX_W[0])
+            k1 = np.uint32(k1 + _PHILOX_W[1])
+    return np.stack(c, axis=-1)
+
+
+def dropout_multiplier(rows, cols, rate, seed, offset, dt=np.float64):
+    """DNNLayer's Dropout(rate) in training (layer/interaction.py:35,44;
+    tf.nn.dropout: keep = u >= rate, kept values scaled by 1/(1-rate)) with
+    the build's counter-based draws (rs_dropout): element e = row*cols + col
+    takes word (offset+e) % 4 of Philox4x32-10(counter (offset+e)//4, key
+    seed), u = (word >> 8) 2^-24.  Returns the [rows, cols] multiplier
+    keep / (1 - rate) (the fp32 scale, as the kernel applies it)."""
+    e = np.uint64(offset) + np.arange(rows * cols, dtype=np.uint64)
+    words = philox4x32_10(e >> np.uint64(2), int(seed))
+    w = words[np.arange(e.size), (e & np.uint64(3)).astype(np.int64)]
+    u = (w >> np.uint32(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    scale = np.float32(1.0) / (np.float32(1.0) - np.float32(rate))
+    return np.where(u >= np.float32(rate), scale, np.float32(0.0)).astype(dt).reshape(rows, cols)
+
+
+def deepfm_train_step(dense, ids, t, p, lr, l2_w, l2_v, nd=13, act="relu", dt=np.float64, masks=None):
     """One SGD step of compile_fit on DeepFM (model/deepFM.py:23-31,
     utils/compile_fit.py:9-15), backpropagated by hand: z = 0.5 (fm + dnn),
     g = (sigmoid(z) - t)/B; DNN layers by the chain rule (ReLU' = [a > 0]);
     FM w.r.t. x: w1 + v s - x |v|^2 per feature; w1 / v with their l2
     terms; embedding rows by scatter-add (np.add.at) of dL/dx's sparse block.
     p: {"tables", "w0", "w1", "v", "dnn_hidden": [(W, b)], "dnn_out": (W, b)}.
+    masks: DNNLayer's Dropout in training — per hidden layer the [B, h]
+    multiplier keep / (1 - rate) applied after its activation (and to the
+    gradient flowing back through it), or None (Dropout as the identity).
     Returns (new p, per-sample losses before the step)."""
     dense = np.asarray(dense, dt)
     ids = cast_ids(ids)
@@ -586,25 +654,14 @@ def deepfm_train_step(dense, ids, t, p, lr, l2_w, l2_v, nd=13, act="relu", dt=np
     w0, w1, v = (np.array(p[n], dt) for n in ("w0", "w1", "v"))
     layers = [(np.array(W, dt), np.array(b, dt)) for W, b in p["dnn_hidden"]] + \
              [(np.array(p["dnn_out"][0], dt), np.array(p["dnn_out"][1], dt))]
-    acts = [x]
-    for W, b in layers[:-1]:
-        acts.append(activation(acts[-1] @ W + b, act))
+    acts = _dnn_train_acts(x, layers, act, masks, dt)
     dnn = (acts[-1] @ layers[-1][0] + layers[-1][1])[:, 0]
     fm = fm_layer(x, w0, w1, v, dt)[:, 0]
     z = 0.5 * (fm + dnn)
     g = (sigmoid(z) - t) / x.shape[0]
     gf = gd = 0.5 * g
     loss = np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z)))
-    delta = gd[:, None]
-    new_layers = [None] * len(layers)
-    for li in reversed(range(len(layers))):
-        W, b = layers[li]
-        dW, db = acts[li].T @ delta, delta.sum(0)
-        prev = delta @ W.T
-        if li > 0 and act == "relu":
-            prev = prev * (acts[li] > 0)
-        new_layers[li] = (W - lr * dW, b - lr * db)
-        delta = prev
+    new_layers, delta = _dnn_train_bwd(gd[:, None], layers, acts, act, masks, lr)
     s = x @ v
     dx = delta + gf[:, None] * (w1[:, 0][None, :] + s @ v.T - x * np.sum(v * v, axis=1)[None, :])
     dw1 = x.T @ gf[:, None]
@@ -1002,18 +1059,21 @@ def nfm_train_step(dense, ids, t, p, lr, momentum=0.99, dt=np.float64):
     return new, loss
 
 
-def deepfm_loss(dense, ids, t, p, l2_w, l2_v, nd=13, dt=np.float64):
+def deepfm_loss(dense, ids, t, p, l2_w, l2_v, nd=13, dt=np.float64, masks=None):
     """compile_fit's objective on DeepFM: mean BCE(t, sigmoid(0.5(fm+dnn)))
-    + l2_w |w1|^2 + l2_v |v|^2."""
+    + l2_w |w1|^2 + l2_v |v|^2 (masks: fixed dropout multipliers, or None)."""
     _, fm, x = deepfm(None, p, nd, dt, inputs=(dense, ids))
-    dnn = dnn_layer(x, p["dnn_hidden"], p["dnn_out"], "relu", dt)
+    layers = [(np.asarray(W, dt), np.asarray(b, dt)) for W, b in p["dnn_hidden"]] + \
+             [(np.asarray(p["dnn_out"][0], dt), np.asarray(p["dnn_out"][1], dt))]
+    acts = _dnn_train_acts(x, layers, "relu", masks, dt)
+    dnn = acts[-1] @ layers[-1][0] + layers[-1][1]
     z = 0.5 * (fm + dnn)[:, 0]
     t = np.asarray(t, dt)
     ce = np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z)))
     return np.mean(ce) + l2_w * np.sum(np.asarray(p["w1"], dt) ** 2) + l2_v * np.sum(np.asarray(p["v"], dt) ** 2)
 
 
-def dcn_train_step(dense, ids, t, p, lr, reg_w, reg_b, nd=13, act="relu", dt=np.float64):
+def dcn_train_step(dense, ids, t, p, lr, reg_w, reg_b, nd=13, act="relu", dt=np.float64, masks=None):
     """One SGD step of compile_fit on DCN (model/dcn.py:24-34,
     utils/compile_fit.py:9-15), backpropagated by hand.  logit = [x_L | dnn]
     Wo + bo, g = (sigmoid(logit) - t)/B; CrossNet (layer/interaction.py:75-83)
@@ -1021,7 +1081,8 @@ def dcn_train_step(dense, ids, t, p, lr, reg_w, reg_b, nd=13, act="relu", dt=np.
     delta_L = dL/dx_L, s_l = x0 . delta_{l+1}, dw_l = sum_b s_l x_l,
     db_l = sum_b delta_{l+1}, delta_l = delta_{l+1} + s_l w_l, dL/dx0 +=
     delta_0 + sum_l g_l delta_{l+1}; l2(reg) adds 2 reg w.  DNNLayer's
-    Dropout is taken as the identity.  Returns (new p, losses before the step)."""
+    Dropout: masks as in deepfm_train_step (None = the identity).  Returns
+    (new p, losses before the step)."""
     dense = np.asarray(dense, dt)
     ids = cast_ids(ids)
     t = np.asarray(t, dt)
@@ -1038,9 +1099,7 @@ def dcn_train_step(dense, ids, t, p, lr, reg_w, reg_b, nd=13, act="relu", dt=np.
         xs.append(xl)
     layers = [(np.array(W, dt), np.array(b, dt)) for W, b in p["dnn_hidden"]] + \
              [(np.array(p["dnn_out"][0], dt), np.array(p["dnn_out"][1], dt))]
-    acts = [x]
-    for W, b in layers[:-1]:
-        acts.append(activation(acts[-1] @ W + b, act))
+    acts = _dnn_train_acts(x, layers, act, masks, dt)
     dnn = acts[-1] @ layers[-1][0] + layers[-1][1]
     z = np.concatenate([xl, dnn], axis=1)
     Wo, bo = np.array(p["out_kernel"], dt), np.array(p["out_bias"], dt)
@@ -1049,17 +1108,7 @@ def dcn_train_step(dense, ids, t, p, lr, reg_w, reg_b, nd=13, act="relu", dt=np.
     g = (sigmoid(logit) - t) / B
     dz = g[:, None] @ Wo.T
     out = {"out_kernel": Wo - lr * (z.T @ g[:, None]), "out_bias": bo - lr * g.sum(keepdims=True)}
-    delta = dz[:, d:]
-    new_layers = [None] * len(layers)
-    for li in reversed(range(len(layers))):
-        W, b = layers[li]
-        dW, db = acts[li].T @ delta, delta.sum(0)
-        prev = delta @ W.T
-        if li > 0 and act == "relu":
-            prev = prev * (acts[li] > 0)
-        new_layers[li] = (W - lr * dW, b - lr * db)
-        delta = prev
-    dx = delta
+    new_layers, dx = _dnn_train_bwd(dz[:, d:], layers, acts, act, masks, lr)
     dc = dz[:, :d]
     new_w, new_b = [None] * len(ws), [None] * len(ws)
     for l in reversed(range(len(ws))):
@@ -1076,13 +1125,17 @@ def dcn_train_step(dense, ids, t, p, lr, reg_w, reg_b, nd=13, act="relu", dt=np.
     return out, loss
 
 
-def dcn_loss(dense, ids, t, p, reg_w, reg_b, nd=13, dt=np.float64):
+def dcn_loss(dense, ids, t, p, reg_w, reg_b, nd=13, dt=np.float64, masks=None):
     """compile_fit's objective on DCN: mean BCE(t, DCN.call) + reg_w sum |w_l|^2
-    + reg_b sum |b_l|^2 (the Keras l2 regularisers)."""
+    + reg_b sum |b_l|^2 (the Keras l2 regularisers); masks: fixed dropout
+    multipliers of DNNLayer, or None."""
     q = dict(p, act=p.get("act", "relu"))
     x = np.concatenate([np.asarray(dense, dt), embed_layer(ids, p["tables"], dt)], axis=1)
-    z = np.concatenate([cross_layer(x, p["cross_w"], p["cross_b"], dt),
-                        dnn_layer(x, p["dnn_hidden"], p["dnn_out"], q["act"], dt)], axis=1)
+    layers = [(np.asarray(W, dt), np.asarray(b, dt)) for W, b in p["dnn_hidden"]] + \
+             [(np.asarray(p["dnn_out"][0], dt), np.asarray(p["dnn_out"][1], dt))]
+    acts = _dnn_train_acts(x, layers, q["act"], masks, dt)
+    z = np.concatenate([cross_layer(x, p["cross_w"], p["cross_b"], dt), acts[-1] @ layers[-1][0] + layers[-1][1]],
+                       axis=1)
     logit = (z @ np.asarray(p["out_kernel"], dt) + np.asarray(p["out_bias"], dt))[:, 0]
     t = np.asarray(t, dt)
     ce = np.maximum(logit, 0) - logit * t + np.log1p(np.exp(-np.abs(logit)))

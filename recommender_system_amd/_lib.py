@@ -20,6 +20,7 @@ P = C.c_void_p
 I = C.c_int
 L = C.c_int64
 F = C.c_float
+U64 = C.c_uint64
 
 # name -> (restype, argtypes); must match include/rs_capi.h and include/rs_batchio.h
 SIGNATURES = {
@@ -78,6 +79,7 @@ SIGNATURES = {
     "rs_gemm_workspace_size": (L, [L, L, L]),
     "rs_gemm": (I, [I, I, L, L, L, F, P, L, P, L, F, P, L, P, L, P, L, P]),
     "rs_col_sum": (I, [P, L, L, L, P, P]),
+    "rs_dropout": (I, [P, L, L, L, F, U64, U64, P]),
     "rs_sgd_update": (I, [P, P, L, F, F, P]),
     "rs_sgd_update_multi": (I, [I, P, P, P, P, F, P]),
     "rs_head_grad": (I, [P, P, P, L, F, F, P, P, P, P]),

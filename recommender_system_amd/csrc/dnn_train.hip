@@ -1080,3 +1080,67 @@ extern "C" int rs_cross_train_bwd(const float* x0, int64_t ldx, int d, int n_lay
                                                                               lddxl, deltas, s, dx, lddx);
   return launch_status("rs_cross_train_bwd");
 }
+
+// ------------------------------------------------------------------ dropout
+// Inverted dropout of DNNLayer (layer/interaction.py:35,44: Dropout(0.2)
+// after every hidden layer, active under compile_fit's model.fit,
+// utils/compile_fit.py:14): x <- x * keep / (1 - rate), keep = (u >= rate)
+// as tf.nn.dropout.  TF's own random draws cannot be reproduced, so the mask
+// comes from a counter-based generator: Philox4x32-10 (Salmon et al., SC'11)
+// with key = seed and counter = (offset + e) / 4 for element e = row * cols +
+// col of the call; word (offset + e) % 4 of the block gives
+// u = (word >> 8) * 2^-24.  The same (seed, offset) regenerates the mask, so
+// the backward multiplies dL/dx by the same keep / (1 - rate) without storing
+// it; oracle.dropout_multiplier restates it bit for bit.
+namespace rs {
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n1 = (uint32_t)p1;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1, n3 = (uint32_t)p0;
+    c[0] = n0;
+    c[1] = n1;
+    c[2] = n2;
+    c[3] = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+// one thread per 4-element counter block of the call's [rows, cols] range
+__global__ __launch_bounds__(256) void dropout_kernel(float* __restrict__ x, int64_t ld, int64_t rows, int64_t cols,
+                                                      float rate, float scale, uint32_t k0, uint32_t k1,
+                                                      uint64_t offset) {
+  const int64_t n = rows * cols, nblk = (n + 3) >> 2;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nblk; q += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t ctr = (offset >> 2) + (uint64_t)q;
+    uint32_t c[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u};
+    philox4x32_10(c, k0, k1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t e = 4 * q + j;
+      if (e < n) {
+        const float u = (float)(c[j] >> 8) * (1.0f / 16777216.0f);
+        const int64_t r = e / cols, col = e - r * cols;
+        float* p = x + r * ld + col;
+        *p = u >= rate ? *p * scale : 0.f;
+      }
+    }
+  }
+}
+}  // namespace rs
+
+extern "C" int rs_dropout(float* x, int64_t ld, int64_t rows, int64_t cols, float rate, uint64_t seed,
+                          uint64_t offset, rs_stream_t stream) {
+  if (rows == 0 || cols == 0) return RS_OK;
+  RS_REQUIRE(x && rows > 0 && cols > 0 && ld >= cols, "rs_dropout: bad arguments");
+  RS_REQUIRE(rate >= 0.f && rate < 1.f, "rs_dropout: rate must be in [0, 1)");
+  RS_REQUIRE(offset % 4 == 0, "rs_dropout: offset must be a multiple of 4");
+  const int64_t nblk = (rows * cols + 3) / 4;
+  const int grid = (int)std::min<int64_t>((nblk + 255) / 256, 8192);
+  dropout_kernel<<<grid, 256, 0, as_stream(stream)>>>(x, ld, rows, cols, rate, 1.0f / (1.0f - rate), (uint32_t)seed,
+                                                      (uint32_t)(seed >> 32), offset);
+  return launch_status("rs_dropout");
+}

@@ -59,12 +59,14 @@ def _subseed(gen):
     return int(torch.randint(0, 2 ** 31, (1,), generator=gen))
 
 
-def _dnn_backward(layers, acts, delta, gw, emp, st, outs=None):
+def _dnn_backward(layers, acts, delta, gw, emp, st, outs=None, drop=None):
     """Backward through Dense layers (relu or linear hidden activations):
     delta = dL/d(pre-activation) of the top layer; returns the (layer, dW, db)
     gradients and dL/d(acts[0]).  dW = a_in^T delta (split-K rs_gemm), db =
     column sums, delta_below = (delta W^T) [a_in > 0] (mask epilogue).
-    outs: optional [(dW, db)] per layer to write into (contiguous views)."""
+    outs: optional [(dW, db)] per layer to write into (contiguous views).
+    drop: (_Dropout, rate, offsets) of the forward's hidden-layer dropout
+    draws — delta_below is multiplied by the same keep / (1 - rate)."""
     B = acts[0].shape[0]
     grads = []
     for li in reversed(range(len(layers))):
@@ -79,6 +81,9 @@ def _dnn_backward(layers, acts, delta, gw, emp, st, outs=None):
         prev = emp(B, K_in)
         call("rs_gemm", 0, 1, B, K_in, N_out, 1.0, ptr(delta), delta.stride(0), ptr(L.kernel), N_out, 0.0,
              ptr(prev), K_in, ptr(a_in) if relu_below else None, a_in.stride(0), *gw, st)
+        if drop is not None and li > 0:
+            rng, rate, offs = drop
+            rng.redraw(prev, rate, offs[li - 1], st)
         delta = prev
     return grads, delta
 
@@ -116,21 +121,75 @@ def _check_train_tower(name, dnn):
         raise NotImplementedError(f"{name}.train_step: 'relu' or linear hidden layers only")
 
 
+class _Dropout:
+    """DNNLayer's Dropout(rate) in training steps (layer/interaction.py:35,44;
+    active under compile_fit's model.fit, utils/compile_fit.py:14): inverted
+    dropout with counter-based masks (rs_dropout: Philox4x32-10, key = seed,
+    one counter per 4 elements).  Every draw takes the next `offset` range, so
+    masks differ across layers and steps and the backward regenerates a
+    draw's mask from its (seed, offset) instead of storing it.  TF's own draws
+    cannot be reproduced; oracle.dropout_multiplier restates this generator.
+    (A captured hipGraph replays the offsets it was captured with.)"""
+
+    def __init__(self, seed):
+        self.seed = int(seed) & (2 ** 64 - 1)
+        self.offset = 0
+
+    def draw(self, t, rate, st):
+        """Apply a fresh mask to t [rows, cols] in place; returns its offset."""
+        off = self.offset
+        self.redraw(t, rate, off, st)
+        self.offset += (t.shape[0] * t.shape[1] + 3) // 4 * 4
+        return off
+
+    def redraw(self, t, rate, offset, st):
+        call("rs_dropout", ptr(t), t.stride(0), t.shape[0], t.shape[1], float(rate), self.seed, int(offset), st)
+
+
+def _dropout_rate(dnn, dropout):
+    """The rate a training step applies: DNNLayer's own (Keras' fit runs the
+    Dropout layers in training mode) unless dropout=False turns it off, or a
+    float overrides it."""
+    if dropout is False:
+        return 0.0
+    if dropout is None or dropout is True:
+        return float(getattr(dnn, "dropout", 0) or 0)
+    return float(dropout)
+
+
+def _dropout_rng(model):
+    rng = model.__dict__.get("_drop_rng")
+    if rng is None:
+        rng = model.__dict__["_drop_rng"] = _Dropout(_subseed(model._gen) * 2654435761 + 97)
+    return rng
+
+
+def _dnn_train_forward(model, dnn, x, rate, st):
+    """Hidden layers of DNNLayer in training: Dense + activation, then the
+    dropout draw (rate > 0).  Returns (acts, drop) for _dnn_backward."""
+    acts, offs = [x], []
+    rng = _dropout_rng(model) if rate > 0 else None
+    for layer in dnn.hidden_layer:
+        a = layer(acts[-1])
+        if rng is not None:
+            offs.append(rng.draw(a, rate, st))
+        acts.append(a)
+    return acts, ((rng, rate, offs) if rng is not None else None)
+
+
 _DROPOUT_WARNED = set()
 
 
-def _dropout_notice(name, dnn, dropout):
-    """The training steps run DNNLayer's Dropout (layer/interaction.py:44) as
-    the identity: its masks are TF's own random draws, so no parity with the
-    reference's fit exists to test.  A layer with rate > 0 trained this way
-    optimises the no-dropout objective: say so once, unless the caller
-    passed dropout=False to acknowledge it."""
-    if dropout is False or not getattr(dnn, "dropout", 0):
+def _dropout_notice(name, layer, dropout):
+    """NFM / DIN (whose Dropout rates default to 0, model/nfm.py:13,
+    model/din.py:18) run a Dropout rate > 0 as the identity in their training
+    steps: say so once, unless dropout=False acknowledges it."""
+    if dropout is False or not getattr(layer, "dropout", 0):
         return
     if name not in _DROPOUT_WARNED:
         _DROPOUT_WARNED.add(name)
         import warnings
-        warnings.warn(f"{name}.train_step: DNNLayer dropout={dnn.dropout} is applied as the identity (no dropout "
+        warnings.warn(f"{name}.train_step: dropout={layer.dropout} is applied as the identity (no dropout "
                       f"masks); pass dropout=False to silence", RuntimeWarning, stacklevel=3)
 
 
@@ -251,7 +310,11 @@ class DeepFM(KerasModule):
         Forward with saved activations (rs_embed_gather, rs_dense_fwd,
         rs_fm_fwd), backward through rs_gemm / rs_col_sum / rs_fm_x_grad /
         rs_fm_param_grads, all gradients from the pre-step weights, then the
-        updates.  Supports output_dim 1 and 'relu' / linear hidden layers."""
+        updates.  Supports output_dim 1 and 'relu' / linear hidden layers.
+        DNNLayer's Dropout runs in training mode as under Keras' fit (rate =
+        the layer's, 0.2 by default; dropout=False turns it off): inverted
+        dropout with counter-based masks (rs_dropout), the same masks in the
+        backward."""
         dense, ids = _split_criteo(inputs, self.nd, self._dev)
         labels = _to_device_f32(labels, self._dev).reshape(-1)
         e, fm, dnn = self.embed_layer, self.fm, self.dnn
@@ -259,15 +322,13 @@ class DeepFM(KerasModule):
         if dnn.output_layer.units != 1:
             raise NotImplementedError("DeepFM.train_step: output_dim 1 only")
         _check_train_tower("DeepFM", dnn)
-        _dropout_notice("DeepFM", dnn, dropout)
+        rate = _dropout_rate(dnn, dropout)
         B, dev, st = ids.shape[0], self._dev, _lib.stream()
         d, kfm = self.nd + e.n_fields * e.k, fm.k
         emp = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=dev)
         # forward, keeping what the backward needs
         x = e.gather(ids, dense, check_ids=check_ids)
-        acts = [x]
-        for layer in dnn.hidden_layer:
-            acts.append(layer(acts[-1]))
+        acts, drop = _dnn_train_forward(self, dnn, x, rate, st)
         dnn_out = dnn.output_layer(acts[-1])
         fm_out = fm(x)
         s = emp(B, kfm)
@@ -278,7 +339,7 @@ class DeepFM(KerasModule):
         g_fm, g_dnn = emp(B), emp(B)
         loss = emp(B) if return_loss else None
         call("rs_head_grad", ptr(fm_out), ptr(dnn_out), ptr(labels), B, 0.5, 0.5, ptr(g_fm), ptr(g_dnn), ptr(loss), st)
-        grads, delta = _dnn_backward(layers, acts, g_dnn.view(B, 1), gw, emp, st)
+        grads, delta = _dnn_backward(layers, acts, g_dnn.view(B, 1), gw, emp, st, drop=drop)
         dx = delta  # [B, d]: the DNN's gradient w.r.t. x; the FM's is added next
         call("rs_fm_x_grad", ptr(x), d, ptr(s), ptr(fm.w1), ptr(fm.v), B, d, kfm, ptr(g_fm), ptr(dx), d, st)
         dw1, dv, dw0 = emp(d), emp(d, kfm), emp(1)
@@ -399,12 +460,12 @@ class DCN(KerasModule):
         x_1..x_L and x_l . w_l) and rs_cross_train_bwd (delta_l recursion);
         dw_l = x_l^T s_l and the Dense grads through rs_gemm, db_l / Dense
         biases through rs_col_sum, the looked-up rows by rs_embedding_sgd.
-        DNNLayer's Dropout is the identity (rate 0): its masks are random
-        draws TF does not expose, so no dropout parity exists to test."""
+        DNNLayer's Dropout runs in training mode (counter-based masks,
+        rs_dropout; dropout=False turns it off), as DeepFM.train_step."""
         dense, ids = _split_criteo(inputs, self.nd, self._dev)
         labels = _to_device_f32(labels, self._dev).reshape(-1)
         e, cl, dnn, out = self.embed_layer, self.cross_layer, self.dense_layer, self.output_layer
-        _dropout_notice("DCN", dnn, dropout)
+        rate = _dropout_rate(dnn, dropout)
         _check_train_tower("DCN", dnn)
         B, d, dev, st = ids.shape[0], self.d, self._dev, _lib.stream()
         od, Lc = dnn.output_layer.units, cl.layer_num
@@ -424,9 +485,7 @@ class DCN(KerasModule):
             call("rs_cross_train_fwd", ptr(x), d, d, Lc, ptr(W), ptr(Bc), B, ptr(xs), ptr(gl), ptr(zc), dz_n, st)
         else:
             zc[:, :d].copy_(x)
-        acts = [x]
-        for layer in dnn.hidden_layer:
-            acts.append(layer(acts[-1]))
+        acts, drop = _dnn_train_forward(self, dnn, x, rate, st)
         dnn.output_layer(acts[-1], out=zc[:, d:])
         logit = emp(B)
         call("rs_dense_fwd", ptr(zc), dz_n, ptr(out.kernel), ptr(out.bias), None, 0, ptr(logit), 1, B, dz_n, 1, st)
@@ -439,7 +498,7 @@ class DCN(KerasModule):
         call("rs_col_sum", ptr(g), 1, B, 1, ptr(dbo), st)
         call("rs_gemm", 0, 1, B, dz_n, 1, 1.0, ptr(g), 1, ptr(out.kernel), 1, 0.0, ptr(dzc), dz_n, None, 0, *gw, st)
         # DNN backward from dzc[:, d:], then the CrossNet's from dzc[:, :d]
-        grads, dx = _dnn_backward(layers, acts, dzc[:, d:], gw, emp, st)
+        grads, dx = _dnn_backward(layers, acts, dzc[:, d:], gw, emp, st, drop=drop)
         if Lc:
             deltas, sl = emp(Lc, B, d), emp(Lc, B)
         else:

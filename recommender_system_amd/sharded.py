@@ -213,14 +213,16 @@ class HipShardOps:
         return _hip_deepfm(self, model, ids, sh.table_shard, sh.offsets, sh.vocab, dense, out)
 
     # -- training of ShardedDeepFM (row protocol + reverse row exchange)
-    def deepfm_grads(self, model, got, rb, dense, labels, scale, tb, loss):
+    def deepfm_grads(self, model, got, rb, dense, labels, scale, tb, loss, drop=None):
         """This rank's share of the DeepFM step: x = [dense | rows from the
         exchange buffer] (rs_embed_gather with ids = slot_of), forward with
         saved activations (rs_dense_fwd, rs_fm_fwd, s = x@v on rs_gemm),
         g = scale (sigmoid(z) - t) (rs_head_grad_scaled, scale = 1/(world B)),
         the DNN backward (split-K rs_gemm, rs_col_sum) and the FM gradients
         (rs_fm_x_grad, rs_fm_param_grads) into the views of tb's flat
-        gradient; returns dL/dx [B, d]."""
+        gradient; returns dL/dx [B, d].  drop = (_Dropout, rate, offsets):
+        DNNLayer's Dropout draws of the hidden layers (rs_dropout), reused in
+        the backward."""
         from .models import _dnn_backward
         sh, st = model.emb, _lib.stream()
         B, d, kfm = dense.shape[0], sh.d, sh.kfm
@@ -230,8 +232,11 @@ class HipShardOps:
         dnn = model.dnn
         layers = list(dnn.hidden_layer) + [dnn.output_layer]
         acts = [x]
-        for layer in dnn.hidden_layer:
-            acts.append(layer(acts[-1]))
+        for i, layer in enumerate(dnn.hidden_layer):
+            a = layer(acts[-1])
+            if drop is not None:
+                drop[0].redraw(a, drop[1], drop[2][i], st)
+            acts.append(a)
         dnn_out = dnn.output_layer(acts[-1])
         fm_out = tb["fm"]
         # FMLayer on the dense x: its own packed image (nd = d, no fields)
@@ -244,7 +249,7 @@ class HipShardOps:
         call("rs_head_grad_scaled", ptr(fm_out), ptr(dnn_out), ptr(labels), B, 0.5, 0.5, float(scale), ptr(g_fm),
              ptr(g_dnn), ptr(loss), st)
         emp = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=self.device)
-        _, dx = _dnn_backward(layers, acts, g_dnn.view(B, 1), gw, emp, st, outs=tb["dnn_views"])
+        _, dx = _dnn_backward(layers, acts, g_dnn.view(B, 1), gw, emp, st, outs=tb["dnn_views"], drop=drop)
         call("rs_fm_x_grad", ptr(x), d, ptr(s), ptr(sh.w1), ptr(sh.v), B, d, kfm, ptr(g_fm), ptr(dx), d, st)
         call("rs_fm_param_grads", ptr(x), d, ptr(s), ptr(sh.v), B, d, kfm, ptr(g_fm), ptr(tb["dw1"]), ptr(tb["dv"]),
              ptr(tb["dw0"]), st)
@@ -659,6 +664,11 @@ class ShardedEmbeddingFM:
     __call__ = forward
 
 
+def dropout_seed(seed, rank):
+    """Seed of rank `rank`'s Dropout generator in ShardedDeepFM.train_step."""
+    return ((int(seed) * 1000003 + 7919 * (int(rank) + 1)) * 2654435761) & (2 ** 64 - 1)
+
+
 class ShardedDeepFM:
     """DeepFM (model/deepFM.py:15-31) with its embedding table row-sharded over
     a process group: BASELINE config 5.  ``forward(inputs) -> [B,1]``
@@ -708,6 +718,8 @@ class ShardedDeepFM:
         self.dnn = DNNLayer(hidden_units, output_dim, activation, device=self.device, seed=seed * 7919 + 11)
         self.dnn.build(sh.d)
         self._in_rows = None
+        self._seed = int(seed or 0)
+        self._drop_rng = None
         # world 1: run the row protocol anyway (route, serve, finish; the
         # exchange is the identity) instead of the direct table path
         self.force_rows = False
@@ -831,6 +843,25 @@ class ShardedDeepFM:
             self._train_bufs = tb
         return tb
 
+    def _dropout(self):
+        """The rank's Dropout generator (rs_dropout): seeded from the model
+        seed and the rank (dropout_seed), so ranks draw independent masks."""
+        from .models import _Dropout
+        if getattr(self, "_drop_rng", None) is None:
+            self._drop_rng = _Dropout(dropout_seed(self._seed, self.rank))
+        return self._drop_rng
+
+    def _draws(self, B, rate):
+        """(generator, rate, offsets): the next dropout draw of every hidden
+        layer for a local batch of B (None at rate 0)."""
+        if rate <= 0:
+            return None
+        rng, offs = self._dropout(), []
+        for L in self.dnn.hidden_layer:
+            offs.append(rng.offset)
+            rng.offset += (B * L.units + 3) // 4 * 4
+        return rng, rate, offs
+
     def train_step(self, inputs, labels, lr=0.01, return_loss=False, check=True, dropout=None):
         """One SGD step of compile_fit (utils/compile_fit.py:9-15: SGD(lr),
         binary cross-entropy on sigmoid(0.5 (FM + DNN)), FMLayer's l2
@@ -846,12 +877,14 @@ class ShardedDeepFM:
           owner: rs_embedding_sgd of the shard on the ids it served
           all_reduce(flat gradient)  (RCCL) -> rs_sgd_update_multi of the replicas
         Every gradient comes from the pre-step weights; every rank's update of
-        the replicated parameters is identical.  Returns the per-sample losses
-        of the local batch (before the step) if ``return_loss``."""
-        from .models import _split_criteo, _dropout_notice
+        the replicated parameters is identical.  DNNLayer's Dropout runs in
+        training mode (rate = the layer's, dropout=False turns it off) with
+        counter-based masks drawn per rank (_dropout).  Returns the per-sample
+        losses of the local batch (before the step) if ``return_loss``."""
+        from .models import _split_criteo, _dropout_rate
         from .layers import _to_device_f32
         sh = self.emb
-        _dropout_notice("ShardedDeepFM", self.dnn, dropout)
+        rate = _dropout_rate(self.dnn, dropout)
         if self.dnn.output_layer.units != 1 or any(l.activation not in (None, "linear", "relu")
                                                    for l in self.dnn.hidden_layer):
             raise NotImplementedError("ShardedDeepFM.train_step: output_dim 1, 'relu' / linear hidden layers")
@@ -873,7 +906,8 @@ class ShardedDeepFM:
             got = rb["got"]
             dist.all_to_all_single(got, reply, group=self.group)
         loss = torch.empty(B, dtype=torch.float32, device=self.device) if return_loss else None
-        dx = self.ops.deepfm_grads(self, got, rb, dense, labels, 1.0 / (W * B), tb, loss)
+        drop = self._draws(B, rate)  # this rank's draws: one offset range per hidden layer
+        dx = self.ops.deepfm_grads(self, got, rb, dense, labels, 1.0 / (W * B), tb, loss, drop=drop)
         if rb["dedup"]:
             gsend = self.ops.dedup_grads(self, dx, rb)  # one row per distinct row
         else:

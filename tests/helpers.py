@@ -56,3 +56,15 @@ def dnn_params(dnn):
     hidden = [(l.kernel.detach().cpu().numpy(), l.bias.detach().cpu().numpy()) for l in dnn.hidden_layer]
     out = (dnn.output_layer.kernel.detach().cpu().numpy(), dnn.output_layer.bias.detach().cpu().numpy())
     return hidden, out
+
+
+def dropout_masks(seed, offset, B, widths, rate):
+    """The dropout multipliers a training step draws for its hidden layers
+    (models._Dropout / rs_dropout: one offset range per layer, in order), as
+    the oracle's generator restates them; returns (masks, next offset)."""
+    from oracle import ctr_oracle as O
+    masks, off = [], int(offset)
+    for h in widths:
+        masks.append(O.dropout_multiplier(B, h, rate, seed, off))
+        off += (B * h + 3) // 4 * 4
+    return masks, off

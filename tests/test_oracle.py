@@ -214,6 +214,86 @@ def test_deepfm_train_step_gradient_matches_finite_differences():
     check(p["dnn_out"][1], new["dnn_out"][1], (0,))
 
 
+def test_philox_known_answers_and_dropout_multiplier():
+    """The dropout generator (rs_dropout / oracle.dropout_multiplier) is
+    Philox4x32-10: Random123's known-answer vectors, restated with Python ints
+    here, and the vectorised oracle agree; the multiplier keeps ~1 - rate of
+    the elements at scale 1/(1-rate), and a draw depends on (seed, offset)."""
+    M0, M1, W0, W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
+
+    def ph(c, k0, k1):
+        for _ in range(10):
+            p0, p1 = M0 * c[0], M1 * c[2]
+            c = [(p1 >> 32) ^ c[1] ^ k0, p1 & 0xFFFFFFFF, (p0 >> 32) ^ c[3] ^ k1, p0 & 0xFFFFFFFF]
+            k0, k1 = (k0 + W0) & 0xFFFFFFFF, (k1 + W1) & 0xFFFFFFFF
+        return c
+
+    assert ph([0, 0, 0, 0], 0, 0) == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    assert ph([0xFFFFFFFF] * 4, 0xFFFFFFFF, 0xFFFFFFFF) == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+    assert ph([0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344], 0xA4093822, 0x299F31D0) == \
+        [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+    seed = (0xBEEF << 32) | 0x1234
+    ctr = np.array([0, 1, 2 ** 32 + 5], np.uint64)
+    got = O.philox4x32_10(ctr, seed)
+    for i, c in enumerate(ctr.tolist()):
+        assert got[i].tolist() == ph([c & 0xFFFFFFFF, c >> 32, 0, 0], seed & 0xFFFFFFFF, seed >> 32)
+    m = O.dropout_multiplier(512, 300, 0.2, seed, 8)
+    assert set(np.unique(m).tolist()) == {0.0, 1.25}
+    assert abs(float((m == 0).mean()) - 0.2) < 0.005
+    assert not np.array_equal(m, O.dropout_multiplier(512, 300, 0.2, seed, 8 + 4 * 512 * 75))
+    np.testing.assert_array_equal(m.reshape(-1)[4:], O.dropout_multiplier(1, 512 * 300 - 4, 0.2, seed, 12)[0])
+
+
+def test_train_steps_with_dropout_match_finite_differences():
+    """deepfm_train_step / dcn_train_step with DNNLayer dropout masks (fixed
+    multipliers, as one training step draws them) == central differences of
+    the objective with the same masks: the gradient flows through kept units
+    scaled by 1/(1-rate) and stops at dropped ones."""
+    rng = np.random.default_rng(21)
+    nd, k, kfm = 2, 3, 2
+    vocab = [3, 2]
+    B = 5
+    tables = [rng.normal(size=(v_, k)) * 0.5 for v_ in vocab]
+    d = nd + len(vocab) * k
+    hidden = [(rng.normal(size=(d, 6)), rng.normal(size=6) * 0.1), (rng.normal(size=(6, 4)), rng.normal(size=4) * 0.1)]
+    masks = [O.dropout_multiplier(B, 6, 0.3, 77, 0), O.dropout_multiplier(B, 4, 0.3, 77, 32)]
+    assert all((mk == 0).any() and (mk > 0).any() for mk in masks)
+    dense = rng.random((B, nd))
+    ids = np.array([[0, 1], [2, 1], [0, 0], [1, 1], [2, 0]])
+    t = np.array([1.0, 0.0, 1.0, 0.0, 1.0])
+    eps = 1e-6
+    p = {"tables": tables, "w0": np.array([0.1]), "w1": rng.normal(size=(d, 1)), "v": rng.normal(size=(d, kfm)),
+         "dnn_hidden": hidden, "dnn_out": (rng.normal(size=(4, 1)), np.array([0.05]))}
+    new, _ = O.deepfm_train_step(dense, ids, t, p, 1.0, 1e-2, 3e-2, nd=nd, masks=masks)
+    q = {"tables": [tb.copy() for tb in tables], "cross_w": [rng.normal(size=(d, 1)) * 0.3 for _ in range(2)],
+         "cross_b": [rng.normal(size=(d, 1)) * 0.3 for _ in range(2)],
+         "dnn_hidden": [(W.copy(), b.copy()) for W, b in hidden], "dnn_out": (rng.normal(size=(4, 2)), np.zeros(2)),
+         "out_kernel": rng.normal(size=(d + 2, 1)) * 0.3, "out_bias": np.array([0.05])}
+    newq, _ = O.dcn_train_step(dense, ids, t, q, 1.0, 1e-2, 3e-2, nd=nd, masks=masks)
+
+    def check(loss, arr, new_arr, idx):
+        keep = arr[idx]
+        arr[idx] = keep + eps
+        lp = loss()
+        arr[idx] = keep - eps
+        lm = loss()
+        arr[idx] = keep
+        assert abs((lp - lm) / (2 * eps) - (arr[idx] - new_arr[idx])) < 1e-6, idx
+
+    fl = lambda: O.deepfm_loss(dense, ids, t, p, 1e-2, 3e-2, nd=nd, masks=masks)
+    gl = lambda: O.dcn_loss(dense, ids, t, q, 1e-2, 3e-2, nd=nd, masks=masks)
+    for li in range(2):
+        for idx in [(0, 0), (2, 1), (5, 3)]:
+            check(fl, p["dnn_hidden"][li][0], new["dnn_hidden"][li][0], idx)
+            check(gl, q["dnn_hidden"][li][0], newq["dnn_hidden"][li][0], idx)
+        check(fl, p["dnn_hidden"][li][1], new["dnn_hidden"][li][1], (3,))
+    for idx in [(0, 0), (2, 2), (1, 1)]:
+        check(fl, p["tables"][0], new["tables"][0], idx)
+        check(gl, q["tables"][0], newq["tables"][0], idx)
+    check(fl, p["dnn_out"][0], new["dnn_out"][0], (2, 0))
+    check(gl, q["dnn_out"][0], newq["dnn_out"][0], (1, 1))
+
+
 def test_dcn_train_step_gradient_matches_finite_differences():
     """oracle.dcn_train_step's hand backprop (CrossNet delta recursion, DNN,
     output Dense, embedding scatter-add) == central differences of

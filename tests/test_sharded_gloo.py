@@ -148,7 +148,7 @@ class CpuOps:
         return rb["gsend"]
 
     # training of ShardedDeepFM (fp64 inside, fp32 buffers like the device path)
-    def deepfm_grads(self, model, got, rb, dense, labels, scale, tb, loss):
+    def deepfm_grads(self, model, got, rb, dense, labels, scale, tb, loss, drop=None):
         so = rb["slot_of"].numpy().astype(np.int64)
         B = so.shape[0]
         x = np.concatenate([np.asarray(dense, np.float64), got.numpy().astype(np.float64)[so].reshape(B, -1)], 1)
@@ -156,9 +156,14 @@ class CpuOps:
         sh = model.emb
         layers = [(c(l.kernel), c(l.bias)) for l in model.dnn.hidden_layer]
         layers.append((c(model.dnn.output_layer.kernel), c(model.dnn.output_layer.bias)))
+        masks = None
+        if drop is not None:  # the rank's draws, restated by the oracle's generator
+            rng, rate, offs = drop
+            masks = [O.dropout_multiplier(B, W_.shape[1], rate, rng.seed, o) for (W_, _), o in zip(layers, offs)]
         acts = [x]
-        for W_, b_ in layers[:-1]:
-            acts.append(np.maximum(acts[-1] @ W_ + b_, 0.0))
+        for i, (W_, b_) in enumerate(layers[:-1]):
+            a = np.maximum(acts[-1] @ W_ + b_, 0.0)
+            acts.append(a * masks[i] if masks is not None else a)
         dnn = (acts[-1] @ layers[-1][0] + layers[-1][1])[:, 0]
         w0, w1, v = c(sh.w0), c(sh.w1), c(sh.v)
         z = 0.5 * (O.fm_layer(x, w0, w1, v)[:, 0] + dnn)
@@ -172,7 +177,11 @@ class CpuOps:
             dW.copy_(torch.as_tensor(acts[li].T @ delta))
             db.copy_(torch.as_tensor(delta.sum(0)))
             prev = delta @ layers[li][0].T
-            delta = prev * (acts[li] > 0) if li > 0 else prev
+            if li > 0:
+                prev = prev * (acts[li] > 0)
+                if masks is not None:
+                    prev = prev * masks[li - 1]
+            delta = prev
         s = x @ v
         dx = delta + gf[:, None] * (w1[:, 0][None, :] + s @ v.T - x * np.sum(v * v, 1)[None, :])
         tb["dw1"].copy_(torch.as_tensor((x.T @ gf[:, None])[:, 0]))
@@ -472,7 +481,16 @@ def _deepfm_worker(rank, world, port, vocabs, k, B, q, dedup=None):
         dist.destroy_process_group()
 
 
-def _deepfm_train_worker(rank, world, port, vocabs, k, B, q, dedup=None):
+def _global_masks(seed, world, offset, B, widths, rate):
+    """Dropout multipliers of the global batch: every rank's own draws
+    (sharded.dropout_seed), stacked in rank order."""
+    from recommender_system_amd.sharded import dropout_seed
+    from tests.helpers import dropout_masks
+    per = [dropout_masks(dropout_seed(seed, r), offset, B, widths, rate)[0] for r in range(world)]
+    return [np.concatenate([per[r][i] for r in range(world)]) for i in range(len(widths))]
+
+
+def _deepfm_train_worker(rank, world, port, vocabs, k, B, q, dedup=None, drop=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -496,10 +514,12 @@ def _deepfm_train_worker(rank, world, port, vocabs, k, B, q, dedup=None):
             for b_ in batch:
                 b_[1][:3, 1] = 0  # repeated rows inside and across ranks
             dense, ids, t = batch[rank]
+            off = m._dropout().offset
             loss = m.train_step((torch.as_tensor(dense), torch.as_tensor(ids)), torch.as_tensor(t), lr=lr,
-                                return_loss=True)
+                                return_loss=True, dropout=None if drop else False)
             gd, gi, gt = (np.concatenate([b_[j] for b_ in batch]) for j in range(3))
-            p, ce = O.deepfm_train_step(gd, gi, gt, p, lr, 1e-3, 2e-3, nd=nd)
+            masks = _global_masks(3, world, off, B, [32, 16], 0.2) if drop else None
+            p, ce = O.deepfm_train_step(gd, gi, gt, p, lr, 1e-3, 2e-3, nd=nd, masks=masks)
             ok = ok and np.allclose(loss.numpy(), ce[rank * B:(rank + 1) * B], rtol=1e-5, atol=1e-6)
             dist.all_gather_object(shards, m.table_shard.numpy().copy())
             ok = ok and np.allclose(np.concatenate(shards), np.concatenate(p["tables"]), rtol=1e-5, atol=1e-6)
@@ -518,8 +538,8 @@ def _deepfm_train_worker(rank, world, port, vocabs, k, B, q, dedup=None):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,dedup", [(2, None), (3, None), (2, 1.0), (3, 0.01)])
-def test_sharded_deepfm_train_step_gloo(world, dedup):
+@pytest.mark.parametrize("world,dedup,drop", [(2, None, True), (3, None, False), (2, 1.0, False), (3, 0.01, True)])
+def test_sharded_deepfm_train_step_gloo(world, dedup, drop):
     """ShardedDeepFM.train_step over gloo (world 2, 3): forward row exchange,
     each rank's local DeepFM backward scaled to the global batch, the REVERSE
     all-to-all of dL/drow to the owners (row-sparse SGD of each shard,
@@ -529,12 +549,14 @@ def test_sharded_deepfm_train_step_gloo(world, dedup):
     dedup: the distinct-row exchange (each owner gets every distinct row
     once per rank, row gradients summed at the requester); 0.01 = a tiny
     capacity that overflows, so every step falls back (collectively) to
-    the field-range records and must still be exact."""
+    the field-range records and must still be exact.  drop: DNNLayer's
+    Dropout(0.2) in training mode, each rank drawing its own masks (the
+    oracle gets the same multipliers, stacked in rank order)."""
     vocabs = [50, 7, 300, 1, 120, 33]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_deepfm_train_worker, args=(r, world, port, vocabs, 4, 19, q, dedup))
+    procs = [ctx.Process(target=_deepfm_train_worker, args=(r, world, port, vocabs, 4, 19, q, dedup, drop))
              for r in range(world)]
     for p_ in procs:
         p_.start()
@@ -1052,7 +1074,7 @@ def test_gpu_rccl_self_exchange(gpu):
     assert r.returncode == 0 and "RCCL OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
 
 
-def _simulated_deepfm_train(models, batches, labels, lr):
+def _simulated_deepfm_train(models, batches, labels, lr, rate=0.0):
     """One ShardedDeepFM.train_step of every rank of a simulated world on one
     GPU, step by step: the forward row exchange (block transposes), every
     rank's deepfm_grads + rs_scatter_rows, the reverse all-to-all of the row
@@ -1076,7 +1098,7 @@ def _simulated_deepfm_train(models, batches, labels, lr):
     losses = []
     for m, rb, tb, (dense, _), t in zip(models, rbs, tbs, batches, labels):
         losses.append(torch.empty(B, device=dense.device))
-        dx = m.ops.deepfm_grads(m, rb["got"], rb, dense, t, 1.0 / (W * B), tb, losses[-1])
+        dx = m.ops.deepfm_grads(m, rb["got"], rb, dense, t, 1.0 / (W * B), tb, losses[-1], drop=m._draws(B, rate))
         if rb["dedup"]:
             m.ops.dedup_grads(m, dx, rb)
         else:
@@ -1095,10 +1117,11 @@ def _simulated_deepfm_train(models, batches, labels, lr):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,B,k,dedup", [(1, 300, 16, None), (2, 200, 16, None), (3, 129, 8, None),
-                                             (8, 128, 16, None), (1, 300, 16, 1.0), (3, 129, 8, 1.0),
-                                             (8, 128, 16, 1.0)])
-def test_gpu_sharded_deepfm_train_simulated_world(gpu, world, B, k, dedup):
+@pytest.mark.parametrize("world,B,k,dedup,drop", [(1, 300, 16, None, True), (2, 200, 16, None, False),
+                                                  (3, 129, 8, None, True), (8, 128, 16, None, True),
+                                                  (1, 300, 16, 1.0, False), (3, 129, 8, 1.0, False),
+                                                  (8, 128, 16, 1.0, True)])
+def test_gpu_sharded_deepfm_train_simulated_world(gpu, world, B, k, dedup, drop):
     """ShardedDeepFM.train_step's HIP path (rs_embed_gather from the exchange
     buffer, rs_dense_fwd / rs_fm_fwd with saved activations,
     rs_head_grad_scaled, the rs_gemm DNN backward, rs_fm_x_grad /
@@ -1108,7 +1131,9 @@ def test_gpu_sharded_deepfm_train_simulated_world(gpu, world, B, k, dedup):
     and simulated worlds 2 / 3 / 8, 2 steps with rows repeated within and
     across ranks: every shard, w0 / w1 / v and every DNN layer equal
     O.deepfm_train_step on the concatenated global batch.  dedup: the
-    distinct-row exchange (rs_shard_dedup_route / rs_shard_dedup_grad)."""
+    distinct-row exchange (rs_shard_dedup_route / rs_shard_dedup_grad).
+    drop: DNNLayer's Dropout(0.2) in training, each rank's own rs_dropout
+    draws (the oracle gets the same multipliers)."""
     from recommender_system_amd.sharded import ShardedDeepFM
     from tests.helpers import assert_scaled_close
     rng = np.random.default_rng(world * 13 + k)
@@ -1134,13 +1159,16 @@ def test_gpu_sharded_deepfm_train_simulated_world(gpu, world, B, k, dedup):
             batches.append((torch.as_tensor(rng.random((B, nd)), dtype=torch.float32, device=gpu),
                             torch.as_tensor(ids, device=gpu)))
             labels.append(torch.as_tensor(rng.integers(0, 2, B), dtype=torch.float32, device=gpu))
+        off = models[0]._dropout().offset
         if world == 1:
-            losses = [models[0].train_step(batches[0], labels[0], lr=lr, return_loss=True)]
+            losses = [models[0].train_step(batches[0], labels[0], lr=lr, return_loss=True,
+                                           dropout=None if drop else False)]
         else:
-            losses = _simulated_deepfm_train(models, batches, labels, lr)
+            losses = _simulated_deepfm_train(models, batches, labels, lr, 0.2 if drop else 0.0)
         cat = lambda xs: np.concatenate([x.cpu().numpy() for x in xs])
+        masks = _global_masks(9, world, off, B, [64, 32], 0.2) if drop else None
         p, ce = O.deepfm_train_step(cat([b_[0] for b_ in batches]), cat([b_[1] for b_ in batches]), cat(labels), p,
-                                    lr, rw, rv, nd=nd)
+                                    lr, rw, rv, nd=nd, masks=masks)
         assert_scaled_close(cat(losses), ce, what=f"step {step} loss")
         full = np.concatenate([m.table_shard.cpu().numpy() for m in models])
         assert_scaled_close(full, np.concatenate(p["tables"]), what=f"step {step} tables")

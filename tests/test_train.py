@@ -91,16 +91,21 @@ def test_compile_fit_on_bundled_sample(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,k,hidden,vmax,id_dtype", [(32, 8, [256, 128, 64], 5, np.int32),
-                                                      (300, 16, [24, 12], 50, np.int64),
-                                                      (7, 4, [], 3, np.int32)])
-def test_deepfm_train_steps_match_oracle(gpu, B, k, hidden, vmax, id_dtype):
-    """DeepFM.train_step (gather, saved activations, rs_gemm backward, FM
-    gradients, l2, SGD, row-sparse embedding scatter-add) == the oracle's
-    hand backprop (pinned by finite differences) over 3 steps, with many
-    repeated rows; the fused forward then runs on the trained weights."""
+@pytest.mark.parametrize("B,k,hidden,vmax,id_dtype,drop", [(32, 8, [256, 128, 64], 5, np.int32, 0.2),
+                                                           (32, 8, [256, 128, 64], 5, np.int32, False),
+                                                           (300, 16, [24, 12], 50, np.int64, 0.2),
+                                                           (301, 16, [24, 12], 50, np.int64, False),
+                                                           (7, 4, [], 3, np.int32, 0.2)])
+def test_deepfm_train_steps_match_oracle(gpu, B, k, hidden, vmax, id_dtype, drop):
+    """DeepFM.train_step (gather, saved activations, DNNLayer's Dropout in
+    training mode, rs_gemm backward, FM gradients, l2, SGD, row-sparse
+    embedding scatter-add) == the oracle's hand backprop (pinned by finite
+    differences) fed the same dropout multipliers, over 3 steps, with many
+    repeated rows; the fused forward then runs on the trained weights.
+    drop: the DNNLayer rate (the reference default 0.2) or False (off)."""
     import recommender_system_amd as rs
-    from tests.helpers import criteo_columns, dnn_params, tables_of
+    from recommender_system_amd import models as M
+    from tests.helpers import criteo_columns, dnn_params, dropout_masks, tables_of
     rng = np.random.default_rng(B + k)
     vocab = rng.integers(1, vmax, 26)
     m = rs.DeepFM(criteo_columns(vocab, embed_dim=k), 10, 1e-3, 2e-3, hidden, 1, "relu", embed_dim=k, seed=2)
@@ -116,12 +121,15 @@ def test_deepfm_train_steps_match_oracle(gpu, B, k, hidden, vmax, id_dtype):
 
     p = {kk: vv for kk, vv in params().items()}
     lr = 0.5
+    assert m.dnn.dropout == 0.2  # DNNLayer's default (layer/interaction.py:30)
+    dr = M._dropout_rng(m)
     for step in range(3):
         dense = rng.random((B, 13)).astype(np.float32)
         ids = np.stack([rng.integers(0, v_, B) for v_ in vocab], 1).astype(id_dtype)
         t = rng.integers(0, 2, B).astype(np.float32)
-        loss = m.train_step((dense, ids), t, lr=lr, return_loss=True)
-        p, ce = O.deepfm_train_step(dense, ids, t, p, lr, 1e-3, 2e-3)
+        masks = dropout_masks(dr.seed, dr.offset, B, hidden, 0.2)[0] if drop else None
+        loss = m.train_step((dense, ids), t, lr=lr, return_loss=True, dropout=None if drop else False)
+        p, ce = O.deepfm_train_step(dense, ids, t, p, lr, 1e-3, 2e-3, masks=masks)
         got = params()
         assert_scaled_close(loss, ce, what=f"step {step} loss")
         for c in range(26):
@@ -148,9 +156,10 @@ def test_compile_fit_deepfm_on_bundled_sample(gpu):
     import os
 
     import recommender_system_amd as rs
+    from recommender_system_amd import models as M
     from recommender_system_amd.dataset import criteo_compact, features_dict
     from recommender_system_amd.train import compile_fit
-    from tests.helpers import dnn_params, tables_of
+    from tests.helpers import dnn_params, dropout_masks, tables_of
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "criteo_train_1w.txt.gz")
     dense, ids, label, _ = criteo_compact(path)
     cols = features_dict(path)
@@ -159,10 +168,14 @@ def test_compile_fit_deepfm_on_bundled_sample(gpu):
     p = {"tables": tables_of(m.embed_layer), "w0": m.fm.w0.cpu().numpy(), "w1": m.fm.w1.cpu().numpy(),
          "v": m.fm.v.cpu().numpy(), "dnn_hidden": hid, "dnn_out": out}
     N = 160
+    dr = M._dropout_rng(m)  # fit runs DNNLayer's Dropout(0.2): the oracle gets the same draws
+    seed, off = dr.seed, dr.offset
     compile_fit(m, dense[:N], ids[:N], label[:N], batch_size=32, epochs=1, sgd=0.01)
     d32 = dense[:N].astype(np.float32)
     for r0 in range(0, N, 32):
-        p, _ = O.deepfm_train_step(d32[r0:r0 + 32], ids[r0:r0 + 32], label[r0:r0 + 32], p, 0.01, 1e-4, 1e-4)
+        masks, off = dropout_masks(seed, off, 32, [64, 32], 0.2)
+        p, _ = O.deepfm_train_step(d32[r0:r0 + 32], ids[r0:r0 + 32], label[r0:r0 + 32], p, 0.01, 1e-4, 1e-4,
+                                   masks=masks)
     assert_scaled_close(m.fm.v, p["v"], what="DeepFM compile_fit v")
     for c in (0, 7, 25):
         assert_scaled_close(m.embed_layer.field_table(c), p["tables"][c], what=f"DeepFM compile_fit table {c}")
@@ -183,16 +196,19 @@ def _dcn_params(m):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,k,hidden,od,L,vmax,id_dtype", [(32, 8, [64, 32], 4, 3, 5, np.int32),
-                                                           (300, 16, [24], 1, 2, 50, np.int64),
-                                                           (7, 4, [], 2, 0, 3, np.int32)])
-def test_dcn_train_steps_match_oracle(gpu, B, k, hidden, od, L, vmax, id_dtype):
-    """DCN.train_step (rs_cross_train_fwd / _bwd, output Dense and DNN through
-    rs_gemm / rs_col_sum, CrossLayer l2, SGD, row-sparse embedding update) ==
-    the oracle's hand backprop (pinned by finite differences) over 3 steps;
-    the fused forward then runs on the trained weights."""
+@pytest.mark.parametrize("B,k,hidden,od,L,vmax,id_dtype,drop", [(32, 8, [64, 32], 4, 3, 5, np.int32, 0.2),
+                                                                (33, 8, [64, 32], 4, 3, 5, np.int32, False),
+                                                                (300, 16, [24], 1, 2, 50, np.int64, 0.2),
+                                                                (7, 4, [], 2, 0, 3, np.int32, 0.2)])
+def test_dcn_train_steps_match_oracle(gpu, B, k, hidden, od, L, vmax, id_dtype, drop):
+    """DCN.train_step (rs_cross_train_fwd / _bwd, DNNLayer's Dropout in
+    training mode, output Dense and DNN through rs_gemm / rs_col_sum,
+    CrossLayer l2, SGD, row-sparse embedding update) == the oracle's hand
+    backprop (pinned by finite differences) fed the same dropout multipliers
+    over 3 steps; the fused forward then runs on the trained weights."""
     import recommender_system_amd as rs
-    from tests.helpers import criteo_columns
+    from recommender_system_amd import models as M
+    from tests.helpers import criteo_columns, dropout_masks
     rng = np.random.default_rng(B + k + L)
     vocab = rng.integers(1, vmax, 26)
     m = rs.DCN(criteo_columns(vocab, embed_dim=k), hidden, od, "relu", layer_num=L, reg_w=1e-3, reg_b=2e-3,
@@ -204,12 +220,14 @@ def test_dcn_train_steps_match_oracle(gpu, B, k, hidden, od, L, vmax, id_dtype):
         m.output_layer.bias.uniform_(-0.1, 0.1)
     p = _dcn_params(m)
     lr = 0.5
+    dr = M._dropout_rng(m)
     for step in range(3):
         dense = rng.random((B, 13)).astype(np.float32)
         ids = np.stack([rng.integers(0, v_, B) for v_ in vocab], 1).astype(id_dtype)
         t = rng.integers(0, 2, B).astype(np.float32)
-        loss = m.train_step((dense, ids), t, lr=lr, return_loss=True)
-        p, ce = O.dcn_train_step(dense, ids, t, p, lr, 1e-3, 2e-3)
+        masks = dropout_masks(dr.seed, dr.offset, B, hidden, 0.2)[0] if drop else None
+        loss = m.train_step((dense, ids), t, lr=lr, return_loss=True, dropout=None if drop else False)
+        p, ce = O.dcn_train_step(dense, ids, t, p, lr, 1e-3, 2e-3, masks=masks)
         got = _dcn_params(m)
         assert_scaled_close(loss, ce, what=f"step {step} loss")
         for c in range(26):
@@ -235,18 +253,24 @@ def test_compile_fit_dcn_on_bundled_sample(gpu):
     import os
 
     import recommender_system_amd as rs
+    from recommender_system_amd import models as M
     from recommender_system_amd.dataset import criteo_compact, features_dict
     from recommender_system_amd.train import compile_fit
+    from tests.helpers import dropout_masks
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "criteo_train_1w.txt.gz")
     dense, ids, label, _ = criteo_compact(path)
     cols = features_dict(path)
     m = rs.DCN(cols, [64, 32], 1, "relu", 3, seed=5)
     p = _dcn_params(m)
     N = 160
+    dr = M._dropout_rng(m)  # fit runs DNNLayer's Dropout(0.2): the oracle gets the same draws
+    seed, off = dr.seed, dr.offset
     compile_fit(m, dense[:N], ids[:N], label[:N], batch_size=32, epochs=1, sgd=0.01)
     d32 = dense[:N].astype(np.float32)
     for r0 in range(0, N, 32):
-        p, _ = O.dcn_train_step(d32[r0:r0 + 32], ids[r0:r0 + 32], label[r0:r0 + 32], p, 0.01, 1e-4, 1e-4)
+        masks, off = dropout_masks(seed, off, 32, [64, 32], 0.2)
+        p, _ = O.dcn_train_step(d32[r0:r0 + 32], ids[r0:r0 + 32], label[r0:r0 + 32], p, 0.01, 1e-4, 1e-4,
+                                masks=masks)
     got = _dcn_params(m)
     for l in range(3):
         assert_scaled_close(got["cross_w"][l], p["cross_w"][l], what=f"DCN compile_fit w{l}")
@@ -287,30 +311,25 @@ def test_rs_gemm_mfma_matches_torch(gpu, ta, tb, M, N, K):
 
 
 @pytest.mark.gpu
-def test_train_step_dropout_notice(gpu):
-    """DNNLayer's Dropout is the identity in the training steps: a model with
-    rate > 0 gets one RuntimeWarning saying so; dropout=False acknowledges it
-    (no warning); rate 0 never warns."""
-    import warnings
-    import recommender_system_amd as rs
-    from recommender_system_amd import models as M
-    from tests.helpers import criteo_columns
-    rng = np.random.default_rng(0)
-    vocab = [5] * 26
-    B = 8
-    dense = rng.random((B, 13)).astype(np.float32)
-    ids = np.stack([rng.integers(0, 5, B) for _ in vocab], 1)
-    t = rng.integers(0, 2, B).astype(np.float32)
-    m = rs.DeepFM(criteo_columns(vocab, embed_dim=8), 4, 1e-4, 1e-4, [16], 1, "relu", embed_dim=8, seed=1)
-    m.dnn.dropout = 0.2
-    M._DROPOUT_WARNED.discard("DeepFM")
-    with warnings.catch_warnings(record=True) as w:
-        warnings.simplefilter("always")
-        m.train_step((dense, ids), t, lr=0.01, dropout=False)
-        assert not [x for x in w if issubclass(x.category, RuntimeWarning)]
-        m.train_step((dense, ids), t, lr=0.01)
-        m.train_step((dense, ids), t, lr=0.01)
-        assert len([x for x in w if "dropout" in str(x.message)]) == 1
+@pytest.mark.parametrize("rows,cols,ld,rate,offset", [(4096, 256, 256, 0.2, 0), (33, 7, 9, 0.5, 1236),
+                                                      (1, 3, 3, 0.2, 4), (300, 24, 24, 0.0, 8)])
+def test_rs_dropout_matches_oracle_generator(gpu, rows, cols, ld, rate, offset):
+    """rs_dropout == oracle.dropout_multiplier bit for bit (Philox4x32-10
+    draws, keep = u >= rate, scale 1/(1-rate)) on a strided tensor, padding
+    columns untouched; applying it again with the same (seed, offset) is the
+    backward (keep^2 = keep, one more scale)."""
+    from recommender_system_amd import _lib
+    g = torch.Generator(device="cpu").manual_seed(rows + cols)
+    x0 = torch.randn(rows, ld, generator=g)
+    x = x0.clone().to(gpu)
+    seed = 0x1234_5678_9ABC_DEF0
+    _lib.call("rs_dropout", x.data_ptr(), ld, rows, cols, rate, seed, offset, _lib.stream())
+    m = O.dropout_multiplier(rows, cols, rate, seed, offset, np.float32)
+    ref = x0.numpy().copy()
+    ref[:, :cols] = ref[:, :cols] * m
+    np.testing.assert_array_equal(x.cpu().numpy(), ref)
+    if rate > 0 and rows * cols > 1000:
+        assert abs(float((m == 0).mean()) - rate) < 0.01
 
 
 @pytest.mark.gpu
