@@ -152,6 +152,8 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   // A row, so they never touch valid outputs.
   const int64_t b = bt < a.batch ? bt : a.batch - 1;
   const int d = a.nd + a.F * a.k;
+  // w0 is requested now, not behind the rows (a dependent load at the end)
+  const float w0v = OWNER ? 0.f : a.w0[0];
 
   floatx4 acc[NT];
 #pragma unroll
@@ -438,7 +440,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       }
       return;
     }
-    const float fm = (lin + a.w0[0]) + 0.5f * t;
+    const float fm = (lin + w0v) + 0.5f * t;
     if (col == 0 && smp < TS && bb < a.batch && a.logit) a.logit[bb] = fm;
     if constexpr (TW) {
       if (col == 0) fmlog[smp] = fm;
