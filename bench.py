@@ -632,6 +632,27 @@ def bench_sharded_deepfm(args, world, rank, lite=False):
     else:
         dt, _ = _timed(step, args.steps, 0, world, events=False)
         timing = f"eager launches ({why})"
+    # pipelined stream (sharded.py pipe_step): batch t+1's route, id
+    # all-to-all, owner gather and row all-to-all on a side stream while
+    # batch t's fused kernel runs; two buffer slots, hub fork / join per step
+    outs = [torch.empty(B, 1, device=dev) for _ in range(2)]
+
+    def pstep(i):
+        j, jn = i % npool, (i + 1) % npool
+        model.pipe_step((dense_pool[j], outs[i % 2], i % 2), (ids_pool[jn], (i + 1) % 2))
+
+    model.pipe_prologue(ids_pool[0], 0)
+    for i in range(args.warmup):
+        pstep(i)
+    torch.cuda.synchronize()
+    pgraphed, pwhy = _graph_capturable(pstep, 0, count=2)
+    model.pipe_prologue(ids_pool[0], 0)
+    if pgraphed:
+        pdt, _ = _timed_graph(pstep, args.steps, 0, world, chunk=npool)
+        ptiming = "HIP graph replay (RCCL captured, two streams)"
+    else:
+        pdt, _ = _timed(pstep, args.steps, 0, world, events=False)
+        ptiming = f"eager launches ({pwhy})"
     f = model.ops.bad_flag()
     dist.all_reduce(f, op=dist.ReduceOp.MAX)
     if bool(f.item()):
@@ -645,7 +666,8 @@ def bench_sharded_deepfm(args, world, rank, lite=False):
     fdt, fslot_ms = _timed_graph(finish, args.steps, 2, world, chunk=16)
     fin_ms = _max_over_ranks(fslot_ms, world)
     flops = B * 2 * (429 * 256 + 256 * 128 + 128 * 64 + 64)
-    ms = dt / args.steps * 1e3
+    ms = pdt / args.steps * 1e3
+    ums = dt / args.steps * 1e3
     S = model.emb.slot_stride
     roof = {"bound": "mfma", "achieved": flops / (fin_ms * 1e-3) / 1e12, "peak": PEAK_F32 / 1e12,
             "unit": "TFLOP/s", "frac": flops / (fin_ms * 1e-3) / PEAK_F32, "traffic": None,
@@ -658,11 +680,16 @@ def bench_sharded_deepfm(args, world, rank, lite=False):
             "owner_field_ranges": model.emb.owner_field_ranges, "slots_per_sample_per_owner": S,
             "id_bytes_per_rank_each_way": world * B * S * 4,
             "row_bytes_per_rank_each_way": world * B * S * k * 4,
-            "exchange_ms_per_step": ms - fin_ms}
+            "exchange_ms_per_step_unpipelined": ums - fin_ms}
+    per_batch = {"samples_per_s": world * args.steps * B / dt, "ms_per_step": ums, "timing": timing,
+                 "note": "ShardedDeepFM.forward per batch: route, all-to-all ids, gather, all-to-all rows, "
+                         "rs_deepfm_fwd in sequence (the comparison for the pipelined value)"}
+    pipe = {"protocol": "sharded.py pipe_step: batch t+1's exchange on a side stream beside batch t's "
+                        "rs_deepfm_fwd (two buffer slots, fork / join on the step's stream)", "timing": ptiming}
     cpu = _cpu_leg_config5(args, world, rank, model, dense_pool, ids_pool, out, B)
     if lite:
-        return {"samples_per_s": world * args.steps * B / dt, "ms_per_step": ms, "roofline": roof,
-                "exchange": exch, "cpu_baseline": cpu}, V
+        return {"samples_per_s": world * args.steps * B / pdt, "ms_per_step": ms, "pipelined": pipe,
+                "per_batch": per_batch, "roofline": roof, "exchange": exch, "cpu_baseline": cpu}, V
     # secondary: the deduplicated exchange on Zipf(1.2) ids (hot rows repeat:
     # each owner receives every distinct row once per rank) and the training
     # step (forward exchange, local backward, reverse all-to-all of dL/drow,
@@ -709,8 +736,8 @@ def bench_sharded_deepfm(args, world, rank, lite=False):
                  "timing": "HIP graph replay",
                  "note": "world 1 without the RCCL self-exchange (ShardedDeepFM.forward -> rs_deepfm_fwd on the "
                          "shard); the exchange line above is the comparison"}
-    res = {"value": world * args.steps * B / dt, "ms_per_step": ms, "roofline": roof, "exchange": exch,
-           "cpu_baseline": cpu,
+    res = {"value": world * args.steps * B / pdt, "ms_per_step": ms, "pipelined": pipe, "per_batch": per_batch,
+           "roofline": roof, "exchange": exch, "cpu_baseline": cpu,
            "zipf_ids": {"distinct_lookup_fraction": distinct,
                         "field_range_records": {"samples_per_s": world * nz * B / zdt, "ms_per_step": zdt / nz * 1e3,
                                                 "row_bytes_per_rank_each_way": world * B * S * k * 4},
@@ -1416,6 +1443,8 @@ def _emit(line):
 
 def main():
     global _RESULT_OUT
+    import faulthandler
+    faulthandler.enable()  # a native crash prints the Python stack
     sys.stdout.flush()
     _RESULT_OUT = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
@@ -1470,8 +1499,8 @@ def main():
                         "ids": "int32 uniform per field", "parallelism": f"dp{world}+rowshard{world}"}),
             "roofline": res["roofline"], "cpu_baseline": res["cpu_baseline"],
         }
-        for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "config5_n1", "exchange", "train_step",
-                    "fm_hotpath_sharded", "world1_no_exchange"):
+        for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "config5_n1", "pipelined", "per_batch",
+                    "exchange", "train_step", "fm_hotpath_sharded", "world1_no_exchange"):
             if key in res:
                 line[key] = res[key]
         _emit(line)

@@ -801,6 +801,97 @@ class ShardedDeepFM:
                 self.route(ids, rb)
         return rb
 
+    # -- pipelined forward: batch t+1's exchange beside batch t's fused kernel
+    def _pipe_bufs(self, B, slot):
+        """Row-exchange buffers of pipeline slot 0 / 1 (field-range records)."""
+        key = f"_pipe_bufs{slot}"
+        rb = getattr(self, key, None)
+        if rb is None or rb["B"] != B:
+            saved = getattr(self, "_row_bufs", None)
+            self._row_bufs = None
+            rb = self._rbufs(B, dedup=False)
+            self._row_bufs = saved
+            setattr(self, key, rb)
+        return rb
+
+    def exchange(self, ids, rb):
+        """Steps 1-4 of forward into rb: route, all-to-all of the row ids, the
+        owner's gather, all-to-all of the rows; rb["rows"] = the rows' buffer."""
+        self.route(ids, rb)
+        recv = rb["send"]
+        if self.emb.exchanges:
+            recv = rb["recv"]
+            dist.all_to_all_single(recv, rb["send"], group=self.group)
+        reply = got = self.serve(recv, rb["reply"])
+        if self.emb.exchanges:
+            got = rb["got"]
+            dist.all_to_all_single(got, reply, group=self.group)
+        rb["rows"] = got
+        return rb
+
+    def pipe_prologue(self, ids, slot=0):
+        """Exchange of the first batch of a pipelined stream into `slot`."""
+        return self.exchange(ids, self._pipe_bufs(ids.shape[0], slot))
+
+    def pipe_step(self, cur, nxt=None, side=None):
+        """One step of the pipelined forward (config 5, model/deepFM.py:23-31
+        over the row-sharded table): rs_deepfm_fwd of batch t = cur = (dense,
+        out, slot) from the rows its exchange left in `slot`, while batch
+        t+1's exchange (nxt = (ids, slot'), route + two all-to-alls + the
+        owner gather) runs into the other slot.  The collectives stay on the
+        current stream and the kernel goes to a side stream that forks from
+        and joins it every step (hub topology: RCCL collectives captured on a
+        side stream crash hipGraph capture on this runtime, the capture
+        stream's do not); the slot the exchange writes was last read by step
+        t-1's kernel, which the previous join ordered before it.  Every rank
+        must run the same steps (the collectives)."""
+        dense, out, slot = cur
+        if self.device.type != "cuda":  # CPU test doubles: the same steps, in order
+            rb = self._pipe_bufs(dense.shape[0], slot)
+            self.finish(dense, rb["rows"], rb, out)
+            if nxt is not None:
+                self.exchange(nxt[0], self._pipe_bufs(nxt[0].shape[0], nxt[1]))
+            return out
+        rb = self._pipe_bufs(dense.shape[0], slot)
+        if nxt is None:
+            self.finish(dense, rb["rows"], rb, out)
+            return out
+        main = torch.cuda.current_stream(self.device)
+        side = side or self._side_stream()
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self.finish(dense, rb["rows"], rb, out)
+        ids_n, slot_n = nxt
+        self.exchange(ids_n, self._pipe_bufs(ids_n.shape[0], slot_n))
+        main.wait_stream(side)
+        return out
+
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.device)
+        return self._side
+
+    def forward_stream(self, batches, check=True):
+        """DeepFM outputs of a sequence of local batches [(dense, ids), ...],
+        pipelined: batch t+1's exchange overlaps batch t's fused kernel.
+        Every rank must pass the same number of batches."""
+        from .models import _split_criteo
+        batches = [_split_criteo(b, self.nd, self.device) for b in batches]
+        outs = [torch.empty(d.shape[0], 1, dtype=torch.float32, device=self.device) for d, _ in batches]
+        if not batches:
+            return outs
+        self.exchange(batches[0][1], self._pipe_bufs(batches[0][1].shape[0], 0))
+        for t, (dense, _) in enumerate(batches):
+            nxt = (batches[t + 1][1], (t + 1) % 2) if t + 1 < len(batches) else None
+            self.pipe_step((dense, outs[t], t % 2), nxt)
+        if check:
+            f = self.ops.bad_flag()
+            if self.world > 1:
+                dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
+            if bool(f.item()):
+                raise IndexError("sharded DeepFM: embedding id out of range")
+        return outs
+
     def serve(self, recv, reply):
         """Step 3 (owner): rows of the received record words (-1 -> zero row)."""
         return self.ops.gather_rows_into(self.emb.table_shard, recv, reply)

@@ -476,6 +476,14 @@ def _deepfm_worker(rank, world, port, vocabs, k, B, q, dedup=None):
             rows = m.emb.offsets.numpy()[None, :] + ids
             ok = ok and np.array_equal(ops.last_emb, full[rows.reshape(-1)].astype(np.float64))
             ok = ok and bool(np.all(np.abs(y - ref) <= 1e-5 * np.abs(ref)))
+        # the pipelined stream (batch t+1's exchange beside batch t's forward,
+        # two buffer slots) gives every batch the per-batch forward's output
+        batches = [(torch.as_tensor(rng.random((B, nd)).astype(np.float32)),
+                    torch.as_tensor(np.stack([rng.integers(0, v, B) for v in vocabs], 1).astype(np.int32)))
+                   for _ in range(3)]
+        outs = m.forward_stream(batches)
+        for (d_, i_), o_ in zip(batches, outs):
+            ok = ok and np.array_equal(o_.numpy(), m.forward((d_, i_)).numpy())
         q.put((rank, bool(ok), m.emb.owner_field_ranges))
     finally:
         dist.destroy_process_group()
@@ -1229,3 +1237,41 @@ def test_gpu_dedup_route_matches_reference(gpu, world, cap_frac):
         assert models[0]._rbufs(B)["n"] <= models[0]._rbufs(B, dedup=False)["n"]
     for m in models:
         assert int(m.ops.err.item()) == 0
+
+
+@pytest.mark.gpu
+def test_gpu_sharded_deepfm_pipelined(gpu):
+    """ShardedDeepFM.forward_stream / pipe_step (batch t+1's route + owner
+    gather on a side stream beside batch t's rs_deepfm_fwd, two buffer
+    slots, hub fork / join) == the per-batch forward bit for bit, eager and
+    replayed from a hipGraph; world 1 with the row protocol forced."""
+    from recommender_system_amd.sharded import ShardedDeepFM
+    rng = np.random.default_rng(5)
+    vocabs = [int(v) for v in rng.integers(1, 400, 26)]
+    m = ShardedDeepFM(_deepfm_columns(vocabs, 13, 16), 10, 1e-4, 1e-4, [64, 32], 1, "relu", embed_dim=16,
+                      device=gpu, seed=9, world=1, rank=0)
+    m.force_rows = True
+    B, T = 300, 4
+    batches = [(torch.rand(B, 13, device=gpu),
+                torch.as_tensor(np.stack([rng.integers(0, v, B) for v in vocabs], 1).astype(np.int32), device=gpu))
+               for _ in range(T)]
+    ref = [m.forward(b).clone() for b in batches]
+    for o, r in zip(m.forward_stream(batches), ref):
+        assert torch.equal(o, r)
+    outs = [torch.full((B, 1), 7.0, device=gpu) for _ in range(T)]
+    m.pipe_prologue(batches[0][1], 0)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for t in range(T):
+                m.pipe_step((batches[t][0], outs[t], t % 2), (batches[t + 1][1], (t + 1) % 2) if t + 1 < T else None)
+    torch.cuda.current_stream().wait_stream(s)
+    m.pipe_prologue(batches[0][1], 0)
+    g.replay()
+    torch.cuda.synchronize()
+    for o, r in zip(outs, ref):
+        assert torch.equal(o, r)
+    assert int(m.ops.err.item()) == 0
