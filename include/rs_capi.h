@@ -57,7 +57,9 @@ enum rs_act {
  * (TF's InvalidArgumentError on an out-of-range Embedding id) and RSError for
  * any other bit. */
 enum rs_flag {
-  RS_FLAG_BAD_ID = 1  /* an id outside [0, vocab) (its row read as zeros) */
+  RS_FLAG_BAD_ID = 1, /* an id outside [0, vocab) (its row read as zeros)               */
+  RS_FLAG_LAYOUT = 2  /* field row ranges overlap or decrease where a kernel needs the
+                         concatenated-table layout (offset_c + vocab_c <= offset_{c+1}) */
 };
 
 /* Runtime tuning options (process-wide, host side; read when a kernel is
@@ -808,8 +810,13 @@ int rs_shard_field_route(const void* ids, int id_kind, int64_t id_stride,
  * u, the reply row of lookup (b, c) after the row all-to-all (rs_deepfm_fwd
  * with ids = slot_of, vocab world*cap, reads the exchange buffer unchanged);
  * -1 for a bad id (*err_flag) or a distinct row past `cap` (*overflow_flag:
- * the caller redoes the step without dedup).  One stable radix sort of
- * (global row, lookup) + a scan of the segment heads; deterministic.
+ * the caller redoes the step without dedup).  The lookups are ordered by
+ * (global row, lookup) and the segment heads numbered; deterministic.  For
+ * batch <= 16384 and n_fields <= 1024 one workgroup per field sorts its
+ * lookups in LDS (the concatenated table's fields occupy increasing,
+ * disjoint row ranges, so the per-field orders concatenate to the global
+ * one; field_offsets[c] + field_vocab[c] > field_offsets[c+1] sets
+ * RS_FLAG_LAYOUT); larger batches use a device-wide radix sort.
  * rs_shard_dedup_grad (backward, same workspace, after the route of the same
  * step): dst[slot] = sum of the gradient rows grad[b*grad_stride + c*k ..]
  * of every lookup of that distinct row, in lookup order (in fixed chunk

@@ -135,7 +135,7 @@ SIGNATURES = {
 }
 
 ID_I32, ID_I64, ID_F32 = 0, 1, 2
-FLAG_BAD_ID = 1  # rs_flag bit of the device error flag
+FLAG_BAD_ID, FLAG_LAYOUT = 1, 2  # rs_flag bits of the device error flag
 OPT_EMBED_FM_KERNEL = 0  # rs_option
 ACT = {None: 0, "linear": 0, "relu": 1, "prelu": 2, "sigmoid": 3}
 

@@ -130,7 +130,7 @@ __global__ void fm_prepare_generic(const float* __restrict__ w1, const float* __
 // on it, closed by sigmoid(c0*dnn + c1*fm) (model/deepFM.py:24-30).
 // TS: samples per workgroup (16 = one MFMA row tile; 8 = the tile's rows
 // 8..15 repeat rows 0..7, two workgroups per CU at batch 4096)
-template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, int TS = 16>
+template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, int TS = 16, bool PF = false>
 __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArgs* tw, const int tile) {
   static_assert(TS == 16 || (TS == 8 && !TW && KIND != 4), "8-sample tiles: plain FM kernel only");
   // MC > 0: field slots per wave and pass (owner kernels with few fields)
@@ -240,57 +240,90 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       }
     }
   }
-  if (a.F == 0 || coop) load_dense();
-  if (coop) __syncthreads();
-  RS_STAMP(9);
-
-  // ---- fields c = cg + j*NW + w; slots past F re-read field F-1 and add 0
-  for (int cg = 0; cg < a.F; cg += NW * MAXC) {
-    // one slot per wave: a wave with no field left in this pass stops (a
-    // wave-uniform exit; nothing after the loop needs its slot)
-    if (MAXC == 1 && cg + w >= a.F) break;
+  // ---- fields c = cg + j*NW + w; slots past F re-read field F-1 and add 0.
+  // A pass = its B fragments and |v_e|^2 (launch constants), then its rows,
+  // then the MFMAs.  The first two passes' B fragments are requested here,
+  // inside the id trip (L2 hits, done before the ids arrive), and their norms
+  // computed while the first rows are in flight, so a pass's work after its
+  // rows arrive is its MFMAs and one FMA per element.
+  struct Pass {
     int cj[MAXC];
+    bool ok[MAXC];
+    typename I::raw_t rid[MAXC];
+    Chunk<KV> xs[MAXC];
+    Chunk<KV> bw[MAXC][NT];
+    float nrm[MAXC][KV];
+  };
+  auto issue_b = [&](int cg, Pass& P) {
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int c = cg + j * NW + w;
+      P.cj[j] = c < a.F ? c : a.F - 1;
+      const float* rec = a.prep + a.field_base + (int64_t)P.cj[j] * a.field_rec;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+#ifdef RS_DIAG_STAMPS
+        if (a.ablate & 2) { P.bw[j][nt].zero(); P.bw[j][nt].v[0] = (float)P.cj[j]; continue; }
+#endif
+        // lanes of the zero-padded columns (> kfm) load nothing
+        if (nt * 16 + s <= a.kfm) P.bw[j][nt].load(rec + (int64_t)(nt * 64 + lane) * KV);
+        else P.bw[j][nt].zero();
+      }
+    }
+  };
+  auto norms = [&](Pass& P) {
+    // |v_e|^2 for this lane's element e: the B lanes of DPP row kk hold
+    // v[e][0..15] — the same row as the A lane that holds x_e.
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j)
+#pragma unroll
+      for (int tp = 0; tp < KV; ++tp) {
+        float sq = 0.f;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const float bv = nt * 16 + s < a.kfm ? P.bw[j][nt].v[tp] : 0.f;
+          sq = fmaf(bv, bv, sq);
+        }
+        P.nrm[j][tp] = row16_sum(sq);
+      }
+  };
+  const int wv = threadIdx.x >> 6;
+  auto issue_rows = [&](int cg, Pass& P) {
     int64_t offc[MAXC], vocc[MAXC];
     // Field metadata through the VECTOR path (wave index taken from the raw
     // thread id, not readfirstlane, so these are not scalar loads): issued
     // with the ids, no dependent K$-miss round trip on the critical path.
-    const int wv = threadIdx.x >> 6;
-    typename I::raw_t rid[MAXC];
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
-      const int c = cg + j * NW + w;
-      cj[j] = c < a.F ? c : a.F - 1;
       if constexpr (KIND != 3) {
         if (OWNER) {
           offc[j] = 0;
           vocc[j] = a.owner_rows;
-          rid[j] = coop ? lid[s % TS][cj[j]] : I::load(a.ids, b * a.id_stride + cj[j]);
+          P.rid[j] = coop ? lid[s % TS][P.cj[j]] : I::load(a.ids, b * a.id_stride + P.cj[j]);
         } else if (coop) {
-          offc[j] = lmeta[0][cj[j]];
-          vocc[j] = lmeta[1][cj[j]];
-          rid[j] = lid[s % TS][cj[j]];
+          offc[j] = lmeta[0][P.cj[j]];
+          vocc[j] = lmeta[1][P.cj[j]];
+          P.rid[j] = lid[s % TS][P.cj[j]];
         } else {
           const int cv = min(cg + j * NW + wv, a.F - 1);
           offc[j] = a.offs[cv];
           vocc[j] = a.vocab[cv];
-          rid[j] = I::load(a.ids, b * a.id_stride + cj[j]);
+          P.rid[j] = I::load(a.ids, b * a.id_stride + P.cj[j]);
         }
       }
     }
     if (cg == 0 && !coop && a.F > 0) load_dense();
     RS_STAMP(6);
     // row gather: KV consecutive floats of the sample's row per lane
-    Chunk<KV> xs[MAXC];
-    bool ok[MAXC];
     int64_t row[MAXC];
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
       if constexpr (KIND == 3) {
-        row[j] = b * a.F + cj[j];
-        ok[j] = true;
+        row[j] = b * a.F + P.cj[j];
+        P.ok[j] = true;
       } else {
         int64_t id;
-        ok[j] = I::decode(rid[j], vocc[j], id);
+        P.ok[j] = I::decode(P.rid[j], vocc[j], id);
         row[j] = offc[j] + id;
       }
     }
@@ -299,65 +332,86 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
 #ifdef RS_DIAG_STAMPS
-      if ((a.ablate & 8) && cg + j * NW + w >= a.F) { xs[j].zero(); continue; }
+      if ((a.ablate & 8) && cg + j * NW + w >= a.F) { P.xs[j].zero(); continue; }
 #endif
-      xs[j].load_nt(a.table + row[j] * a.k + KV * kk);
+      P.xs[j].load_nt(a.table + row[j] * a.k + KV * kk);
     }
-    // B fragments; lanes of the zero-padded columns (> kfm) load nothing.
-    Chunk<KV> bw[MAXC][NT];
-#pragma unroll
-    for (int j = 0; j < MAXC; ++j) {
-      const float* rec = a.prep + a.field_base + (int64_t)cj[j] * a.field_rec;
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-#ifdef RS_DIAG_STAMPS
-        if (a.ablate & 2) { bw[j][nt].zero(); bw[j][nt].v[0] = (float)cj[j]; continue; }
-        if ((a.ablate & 8) && cg + j * NW + w >= a.F) { bw[j][nt].zero(); continue; }
-#endif
-        if (nt * 16 + s <= a.kfm) bw[j][nt].load(rec + (int64_t)(nt * 64 + lane) * KV);
-        else bw[j][nt].zero();
-      }
-    }
-    RS_USE(xs[MAXC - 1].v[KV - 1]);
-    RS_USE(bw[MAXC - 1][0].v[KV - 1]);
+  };
+  auto consume = [&](int cg, Pass& P) {
+    RS_USE(P.xs[MAXC - 1].v[KV - 1]);
+    RS_USE(P.bw[MAXC - 1][0].v[KV - 1]);
     RS_STAMP(2);
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
       const bool live = cg + j * NW + w < a.F;
-      if constexpr (OWNER) bad |= live && !ok[j] && rid[j] != -1;
-      else bad |= live && !ok[j];
-      const bool use = live && ok[j];
+      if constexpr (OWNER) bad |= live && !P.ok[j] && P.rid[j] != -1;
+      else bad |= live && !P.ok[j];
+      const bool use = live && P.ok[j];
 #pragma unroll
       for (int tp = 0; tp < KV; ++tp) {
-        const float xv = use ? xs[j].v[tp] : 0.f;
+        const float xv = use ? P.xs[j].v[tp] : 0.f;
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
 #ifdef RS_DIAG_STAMPS
-          if (a.ablate & 1) { acc[nt][0] += xv * bw[j][nt].v[tp]; continue; }
+          if (a.ablate & 1) { acc[nt][0] += xv * P.bw[j][nt].v[tp]; continue; }
 #endif
-          acc[nt] = mfma16x16x4(xv, bw[j][nt].v[tp], acc[nt]);
+          acc[nt] = mfma16x16x4(xv, P.bw[j][nt].v[tp], acc[nt]);
         }
-        // |v_e|^2 for this lane's element e: the B lanes of DPP row kk hold
-        // v[e][0..15] — the same row as the A lane that holds x_e.
-        float sq = 0.f;
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          const float bv = nt * 16 + s < a.kfm ? bw[j][nt].v[tp] : 0.f;
-          sq = fmaf(bv, bv, sq);
-        }
-        qn = fmaf(xv * xv, row16_sum(sq), qn);
+        qn = fmaf(xv * xv, P.nrm[j][tp], qn);
       }
       if constexpr (TW) {
         if (live) {
-          float* xo = tsm + s * xrs + cj[j] * a.k + KV * kk;
+          float* xo = tsm + s * xrs + P.cj[j] * a.k + KV * kk;
 #pragma unroll
-          for (int tp = 0; tp < KV; ++tp) xo[tp] = ok[j] ? xs[j].v[tp] : 0.f;
+          for (int tp = 0; tp < KV; ++tp) xo[tp] = P.ok[j] ? P.xs[j].v[tp] : 0.f;
         }
       } else if (a.x_out && live && valid) {
-        float* xo = a.x_out + b * d + a.nd + cj[j] * a.k + KV * kk;
+        float* xo = a.x_out + b * d + a.nd + P.cj[j] * a.k + KV * kk;
 #pragma unroll
-        for (int tp = 0; tp < KV; ++tp) xo[tp] = ok[j] ? xs[j].v[tp] : 0.f;
+        for (int tp = 0; tp < KV; ++tp) xo[tp] = P.ok[j] ? P.xs[j].v[tp] : 0.f;
       }
+    }
+  };
+  // one slot per wave: a wave with no field left in a pass stops there (a
+  // wave-uniform exit; nothing after the loop needs its slot)
+  auto has_pass = [&](int cg) { return cg < a.F && !(MAXC == 1 && cg + w >= a.F); };
+  constexpr int PS = NW * MAXC;  // fields per pass
+  // PF: B fragments of the first two passes ride the id trip (registers: two
+  // passes only where they are few; larger rows load theirs per pass).
+  // Measured (scripts/ab, profiles/r3_ab_prefetch_*.json): 14.51 vs 15.30 us
+  // at batch 16384 (4 tiles per CU), 6.15 vs 6.13 at 4096 (1 tile per CU)
+  constexpr bool PRE = PF && KV * MAXC * NT <= 8;
+  Pass P0, P1;
+  if (PRE) {
+    if (has_pass(0)) issue_b(0, P0);
+    if (has_pass(PS)) issue_b(PS, P1);
+  }
+  if (a.F == 0 || coop) load_dense();
+  if (coop) __syncthreads();
+  RS_STAMP(9);
+  if (PRE) {
+    if (has_pass(0)) {
+      issue_rows(0, P0);
+      norms(P0);
+      if (has_pass(PS)) norms(P1);
+      consume(0, P0);
+      if (has_pass(PS)) {
+        issue_rows(PS, P1);
+        consume(PS, P1);
+        for (int cg = 2 * PS; has_pass(cg); cg += PS) {
+          issue_b(cg, P0);
+          issue_rows(cg, P0);
+          norms(P0);
+          consume(cg, P0);
+        }
+      }
+    }
+  } else {
+    for (int cg = 0; has_pass(cg); cg += PS) {
+      issue_b(cg, P0);
+      issue_rows(cg, P0);
+      norms(P0);
+      consume(cg, P0);
     }
   }
 
@@ -450,9 +504,9 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   if constexpr (TW) mlp_tower_tile<NW>(*tw, tsm, (int64_t)tile * 16, ring, fmlog);
 }
 
-template <int KV, int NT, int NW, int KIND, int MC, int TS = 16>
+template <int KV, int NT, int NW, int KIND, int MC, int TS = 16, bool PF = false>
 __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
-  embed_fm_body<KV, NT, NW, KIND, false, MC, TS>(a, nullptr, blockIdx.x);
+  embed_fm_body<KV, NT, NW, KIND, false, MC, TS, PF>(a, nullptr, blockIdx.x);
 }
 
 // ---- sharded FM, partial protocol: combine (requester side) as a block part
@@ -737,7 +791,9 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st) {
 #endif
   constexpr int TS = RS_EMBED_TS;
   const int grid = (int)((a.batch + TS - 1) / TS);
-  if (a.F <= 32) embed_fm_mfma<KV, NT, 16, KIND, 1, TS><<<grid, 16 * 64, 0, st>>>(a);
+  // several tiles per CU: prefetch the first passes' B fragments (PF)
+  if (a.F <= 32 && grid > 512) embed_fm_mfma<KV, NT, 16, KIND, 1, TS, true><<<grid, 16 * 64, 0, st>>>(a);
+  else if (a.F <= 32) embed_fm_mfma<KV, NT, 16, KIND, 1, TS><<<grid, 16 * 64, 0, st>>>(a);
   else embed_fm_mfma<KV, NT, 16, KIND, 0, TS><<<grid, 16 * 64, 0, st>>>(a);
 }
 

@@ -312,6 +312,10 @@ class HipShardOps:
         self.err.zero_()
         return v
 
+    def clear_flags(self):
+        """Restart the sticky id flag (a checked step reports its own ids)."""
+        self.err.zero_()
+
     def check(self):
         if int(self.err.item()):
             self.err.zero_()
@@ -788,9 +792,17 @@ class ShardedDeepFM:
     def _routed(self, ids, check):
         """Route the batch; with dedup and ``check``, a capacity overflow on
         any rank (collective decision: one host sync) reroutes it through the
-        field-range records, so the step stays exact."""
+        field-range records, so the step stays exact.  check=False with
+        dedup < 1 is approximate: lookups past the capacity get slot -1, read
+        a zero row (and set the sticky id flag) and drop their row gradient.
+        Both flags restart here (device memsets, no sync), so an unchecked
+        step never leaves a false IndexError or fallback to a checked one."""
         B = ids.shape[0]
         rb = self._rbufs(B)
+        if rb["dedup"]:
+            rb["overflow"].zero_()
+        if check:
+            self.ops.clear_flags()
         self.route(ids, rb)
         if rb["dedup"] and check:
             f = self.ops.overflow_flag(rb)

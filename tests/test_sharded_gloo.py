@@ -333,6 +333,9 @@ class CpuOps:
     def bad_flag(self):
         return torch.zeros(1, dtype=torch.int32)
 
+    def clear_flags(self):
+        pass
+
 
 def _free_port():
     s = socket.socket()
@@ -1196,18 +1199,20 @@ def test_gpu_sharded_deepfm_train_simulated_world(gpu, world, B, k, dedup, drop)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,cap_frac", [(1, 1.0), (3, 1.0), (8, 1.0), (8, 0.05)])
-def test_gpu_dedup_route_matches_reference(gpu, world, cap_frac):
+@pytest.mark.parametrize("world,cap_frac,B", [(1, 1.0, 256), (3, 1.0, 256), (8, 1.0, 4096), (8, 0.05, 256),
+                                               (2, 1.0, 17000)])
+def test_gpu_dedup_route_matches_reference(gpu, world, cap_frac, B):
     """rs_shard_dedup_route == the numpy double (distinct rows per owner in
     row order, slot_of, -1 padding), Zipf-like ids with many repeats; a
     capacity below the distinct count raises the overflow flag; then the
     forward through the deduplicated exchange (simulated world) equals
-    O.deepfm."""
+    O.deepfm.  B <= 16384: the per-field LDS sort path; 17000: the
+    device-wide radix sort."""
     from recommender_system_amd.sharded import ShardedDeepFM
     from tests.helpers import assert_rel_close
     rng = np.random.default_rng(world * 5 + 3)
     vocabs = [int(v) for v in rng.integers(1, 3000, 26)]
-    B, k, nd = 256, 16, 13
+    k, nd = 16, 13
     cols = _deepfm_columns(vocabs, nd, k)
     models = [ShardedDeepFM(cols, 10, 1e-4, 1e-4, [64, 32], 1, "relu", embed_dim=k, device=gpu, seed=4,
                             world=world, rank=r, dedup=cap_frac) for r in range(world)]
@@ -1233,10 +1238,41 @@ def test_gpu_dedup_route_matches_reference(gpu, world, cap_frac):
         for r in range(world):
             ref = _compact_deepfm_reference(models, batches[r][0].cpu().numpy(), batches[r][1].cpu().numpy())
             assert_rel_close(outs[r], ref, what=f"rank {r}")
-        # fewer words than the field-range records whenever ids repeat
-        assert models[0]._rbufs(B)["n"] <= models[0]._rbufs(B, dedup=False)["n"]
+        # fewer rows on the wire than the field-range records whenever ids
+        # repeat (the capacity itself is rounded up to 64 words per owner)
+        for m in models:
+            assert int((m._rbufs(B)["send"] >= 0).sum().item()) < B * 26
     for m in models:
         assert int(m.ops.err.item()) == 0
+
+
+@pytest.mark.gpu
+def test_gpu_dedup_unchecked_overflow_leaves_no_stale_flags(gpu):
+    """An unchecked forward (check=False) whose distinct rows overflow a small
+    dedup capacity leaves the overflow and id flags set; the next checked
+    forward restarts both, so it neither raises a false IndexError nor takes
+    the fallback, and equals the exact forward."""
+    from recommender_system_amd.sharded import ShardedDeepFM
+    from tests.helpers import assert_rel_close
+    rng = np.random.default_rng(31)
+    vocabs = [int(v) for v in rng.integers(500, 3000, 26)]
+    m = ShardedDeepFM(_deepfm_columns(vocabs, 13, 16), 10, 1e-4, 1e-4, [64, 32], 1, "relu", embed_dim=16,
+                      device=gpu, seed=3, world=1, rank=0, dedup=0.05)
+    m.force_rows = True
+    B = 512
+    wide = torch.as_tensor(np.stack([rng.integers(0, v, B) for v in vocabs], 1).astype(np.int32), device=gpu)
+    dense = torch.rand(B, 13, device=gpu)
+    m.forward((dense, wide), check=False)
+    torch.cuda.synchronize()
+    assert int(m._rbufs(B)["overflow"].item()) > 0  # slot -1 lookups (they also set the id flag)
+    few = torch.zeros(B, 26, dtype=torch.int32, device=gpu)  # one distinct row per field: fits
+    got = m.forward((dense, few)).clone()
+    assert int(m.ops.err.item()) == 0
+    m2 = ShardedDeepFM(_deepfm_columns(vocabs, 13, 16), 10, 1e-4, 1e-4, [64, 32], 1, "relu", embed_dim=16,
+                       device=gpu, seed=3, world=1, rank=0)
+    m2.force_rows = True
+    exp = m2.forward((dense, few))
+    assert_rel_close(got.cpu().numpy(), exp.cpu().numpy(), what="checked dedup forward after an overflow")
 
 
 @pytest.mark.gpu
