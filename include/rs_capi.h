@@ -810,19 +810,21 @@ int rs_shard_field_route(const void* ids, int id_kind, int64_t id_stride,
  * u, the reply row of lookup (b, c) after the row all-to-all (rs_deepfm_fwd
  * with ids = slot_of, vocab world*cap, reads the exchange buffer unchanged);
  * -1 for a bad id (*err_flag) or a distinct row past `cap` (*overflow_flag:
- * the caller redoes the step without dedup).  The lookups are ordered by
- * (global row, lookup) and the segment heads numbered; deterministic.  For
- * batch <= 16384 and n_fields <= 1024 one workgroup per field sorts its
- * lookups in LDS (the concatenated table's fields occupy increasing,
- * disjoint row ranges, so the per-field orders concatenate to the global
- * one; field_offsets[c] + field_vocab[c] > field_offsets[c+1] sets
- * RS_FLAG_LAYOUT); larger batches use a device-wide radix sort.
+ * the caller redoes the step without dedup).  For
+ * batch <= 4096, n_fields <= 1024 and world <= 4096, one workgroup per
+ * field dedups its lookups in an LDS hash table and numbers each owner's
+ * distinct rows field by field in order of first occurrence (the
+ * concatenated table's fields occupy increasing, disjoint row ranges;
+ * field_offsets[c] + field_vocab[c] > field_offsets[c+1] sets
+ * RS_FLAG_LAYOUT), and a second launch scatters — no sort; larger batches
+ * use a device-wide radix sort and number the rows in row order.  Either
+ * way the numbering is deterministic.
  * rs_shard_dedup_grad (backward, same workspace, after the route of the same
  * step): dst[slot] = sum of the gradient rows grad[b*grad_stride + c*k ..]
- * of every lookup of that distinct row, in lookup order (in fixed chunk
- * pieces, so hot rows stay parallel; it overwrites the route's scratch slabs,
- * not its sorted keys) — one gradient row per distinct row travels back to
- * its owner.  Workspace: rs_shard_dedup_workspace_size(batch*n_fields,
+ * of every lookup of that distinct row, in lookup order (the lookups grouped
+ * by row first — on the hash path by a per-field launch of its own — then
+ * summed in fixed chunk pieces, so hot rows stay parallel) — one gradient
+ * row per distinct row travels back to its owner.  Workspace: rs_shard_dedup_workspace_size(batch*n_fields,
  * world) bytes.                                                            */
 int64_t rs_shard_dedup_workspace_size(int64_t n_lookups, int world);
 int rs_shard_dedup_route(const void* ids, int id_kind, int64_t id_stride,

@@ -1198,16 +1198,46 @@ def test_gpu_sharded_deepfm_train_simulated_world(gpu, world, B, k, dedup, drop)
         assert int(m.ops.err.item()) == 0
 
 
+def _check_dedup_route(sh, ids, cap, send, slot_of):
+    """What the dedup route promises, whatever order it numbers the distinct
+    rows in: owner o's words [0, n_o) are n_o = min(distinct, cap) distinct
+    local rows it owns (all of them when they fit), the rest -1; every lookup's
+    slot holds its own row (-1 only past the capacity).  Returns overflow."""
+    rpr, world = sh.rows_per_rank, sh.world
+    rows = (sh.offsets.cpu().numpy()[None, :] + ids.astype(np.int64)).reshape(-1)
+    owner = np.minimum(rows // rpr, world - 1)
+    send = send.astype(np.int64)
+    slot = slot_of.reshape(-1).astype(np.int64)
+    over = False
+    for o in range(world):
+        need = np.unique(rows[owner == o])
+        n_o = min(need.size, cap)
+        words = send[o * cap:(o + 1) * cap]
+        assert np.all(words[n_o:] == -1)
+        got = words[:n_o] + o * rpr
+        assert np.unique(got).size == n_o and np.isin(got, need).all()
+        over |= need.size > cap
+        mine = owner == o
+        ok = slot[mine] >= 0
+        assert need.size > cap or ok.all()
+        s = slot[mine][ok]
+        assert np.all(s // cap == o)
+        np.testing.assert_array_equal(send[s] + o * rpr, rows[mine][ok])
+    return over
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,cap_frac,B", [(1, 1.0, 256), (3, 1.0, 256), (8, 1.0, 4096), (8, 0.05, 256),
-                                               (2, 1.0, 17000)])
+                                               (2, 1.0, 3000), (1, 1.0, 4096), (2, 1.0, 17000)])
 def test_gpu_dedup_route_matches_reference(gpu, world, cap_frac, B):
     """rs_shard_dedup_route == the numpy double (distinct rows per owner in
     row order, slot_of, -1 padding), Zipf-like ids with many repeats; a
     capacity below the distinct count raises the overflow flag; then the
     forward through the deduplicated exchange (simulated world) equals
-    O.deepfm.  B <= 16384: the per-field LDS sort path; 17000: the
-    device-wide radix sort."""
+    O.deepfm.  B <= 4096: the per-field hash path (rows numbered by first
+    occurrence: checked by what the route promises, and run twice for
+    determinism); 17000: the device-wide radix sort (row order: equal to the
+    numpy double word for word)."""
     from recommender_system_amd.sharded import ShardedDeepFM
     from tests.helpers import assert_rel_close
     rng = np.random.default_rng(world * 5 + 3)
@@ -1229,8 +1259,16 @@ def test_gpu_dedup_route_matches_reference(gpu, world, cap_frac, B):
         over = bool(m.ops.overflow_flag(rb).item())
         assert over == bool(getattr(cpu, "dedup_overflow", False)), (over, cap_frac)
         cpu.dedup_overflow = False
-        np.testing.assert_array_equal(rb["send"].cpu().numpy(), ref["send"].numpy())
-        np.testing.assert_array_equal(rb["slot_of"].cpu().numpy(), ref["slot_of"].numpy())
+        send, slot_of = rb["send"].cpu().numpy(), rb["slot_of"].cpu().numpy()
+        assert _check_dedup_route(m.emb, ids, rb["cap"], send, slot_of) == over
+        if B > 4096:
+            np.testing.assert_array_equal(send, ref["send"].numpy())
+            np.testing.assert_array_equal(slot_of, ref["slot_of"].numpy())
+        else:
+            m.route(batches[-1][1], rb)
+            m.ops.overflow_flag(rb)
+            np.testing.assert_array_equal(rb["send"].cpu().numpy(), send)
+            np.testing.assert_array_equal(rb["slot_of"].cpu().numpy(), slot_of)
         if cap_frac < 0.1:
             assert over
     if cap_frac >= 0.1:
