@@ -715,11 +715,26 @@ def bench_sharded_deepfm(args, world, rank, lite=False):
             m.forward((dense_pool[j], zipf_pool[j]), check=False, out=out)
         return st
 
-    zdt, _ = _timed(step_zipf(model), max(10, args.steps // 2), 2, world, events=False)
-    ddt, _ = _timed(step_zipf(dmodel), max(10, args.steps // 2), 2, world, events=False)
+    nz = max(10, args.steps // 2)
+    zfn, dfn = step_zipf(model), step_zipf(dmodel)
+    for i in range(2):
+        zfn(i)
+        dfn(i)
+    torch.cuda.synchronize()
+    zg, zwhy = _graph_capturable(zfn, 0)
+    dg, dwhy = _graph_capturable(dfn, 0)
+    if zg and dg:  # both replayed from HIP graphs (collective decision)
+        zdt, _ = _timed_graph(zfn, nz, 2, world, chunk=16)
+        ddt, _ = _timed_graph(dfn, nz, 2, world, chunk=16)
+        ztiming = "HIP graph replay (RCCL captured)"
+    else:
+        zdt, _ = _timed(zfn, nz, 2, world, events=False)
+        ddt, _ = _timed(dfn, nz, 2, world, events=False)
+        ztiming = f"eager launches ({zwhy or dwhy})"
+    zedt, _ = _timed(zfn, nz, 2, world, events=False)
+    dedt, _ = _timed(dfn, nz, 2, world, events=False)
     over += dmodel.ops.overflow_flag(dmodel._rbufs(B))
     dist.all_reduce(over, op=dist.ReduceOp.MAX)
-    nz = max(10, args.steps // 2)
     distinct = float(np.mean([sum(len(np.unique((model.emb.offsets[None, :].cpu().numpy() +
                                                  zipf_pool[j].cpu().numpy().astype(np.int64))[:, c]))
                                   for c in range(F)) for j in range(2)])) / (B * F)
@@ -747,13 +762,16 @@ def bench_sharded_deepfm(args, world, rank, lite=False):
            "roofline": roof, "exchange": exch, "cpu_baseline": cpu,
            "zipf_ids": {"distinct_lookup_fraction": distinct,
                         "field_range_records": {"samples_per_s": world * nz * B / zdt, "ms_per_step": zdt / nz * 1e3,
+                                                "ms_per_step_eager": zedt / nz * 1e3,
                                                 "row_bytes_per_rank_each_way": world * B * S * k * 4},
                         "dedup": {"samples_per_s": world * nz * B / ddt, "ms_per_step": ddt / nz * 1e3,
+                                  "ms_per_step_eager": dedt / nz * 1e3,
                                   "capacity_fraction": 0.5, "overflow_seen": bool(over.item()),
                                   "row_bytes_per_rank_each_way": dmodel._rbufs(B)["n"] * k * 4},
-                        "timing": "eager launches (the dedup route's radix sort is not graph-captured here)",
-                        "note": "Zipf(1.2) ids per field, clipped to the vocab; dedup = rs_shard_dedup_route: "
-                                "each owner receives each distinct row once per rank"},
+                        "timing": ztiming,
+                        "note": "Zipf(1.2) ids per field, clipped to the vocab; dedup = rs_shard_dedup_route (per-field "
+                                "LDS hash, first-occurrence numbering, no sort): each owner receives each distinct "
+                                "row once per rank"},
            "train_step": {"samples_per_s": world * nt * B / tdt, "ms_per_step": tdt / nt * 1e3,
                           "timing": "eager launches",
                           "note": "ShardedDeepFM.train_step: row exchange, local DeepFM backward (rs_gemm), "
