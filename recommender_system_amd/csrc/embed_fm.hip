@@ -791,8 +791,13 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st) {
 #endif
   constexpr int TS = RS_EMBED_TS;
   const int grid = (int)((a.batch + TS - 1) / TS);
-  // several tiles per CU: prefetch the first passes' B fragments (PF)
-  if (a.F <= 32 && grid > 512) embed_fm_mfma<KV, NT, 16, KIND, 1, TS, true><<<grid, 16 * 64, 0, st>>>(a);
+  // several tiles per CU: prefetch the first passes' B fragments (PF) and
+  // use fewer waves per tile, so more tiles share a CU (one field slot per
+  // wave and pass): 8 waves up to 1024 tiles, 4 beyond (scripts/ab A/B,
+  // graph slots: 13.0 -> 11.4 us at B 12288, 14.5 -> 13.5 at 16384, 27.0 ->
+  // 22.9 at 32768, 50.7 -> 42.7 at 65536; profiles/r3_ab_nw*.json)
+  if (a.F <= 32 && grid > 1024) embed_fm_mfma<KV, NT, 4, KIND, 1, TS, true><<<grid, 4 * 64, 0, st>>>(a);
+  else if (a.F <= 32 && grid > 512) embed_fm_mfma<KV, NT, 8, KIND, 1, TS, true><<<grid, 8 * 64, 0, st>>>(a);
   else if (a.F <= 32) embed_fm_mfma<KV, NT, 16, KIND, 1, TS><<<grid, 16 * 64, 0, st>>>(a);
   else embed_fm_mfma<KV, NT, 16, KIND, 0, TS><<<grid, 16 * 64, 0, st>>>(a);
 }

@@ -123,6 +123,9 @@ def embed_fm_variant(request, gpu):
     (8, 10, 26, 13, 4113, "i32"),    # k = 8 (MFMA tiles KV 2; VALU falls back)
     (16, 16, 20, 5, 130, "i32"),     # two MFMA column tiles
     (16, 10, 5, 0, 33, "i32"),       # no dense block
+    (16, 10, 26, 13, 16500, "i32"),  # > 1024 tiles: the 4-wave K-split tiles
+    (8, 10, 26, 40, 17001, "i64"),   # 4 waves, k 8, more dense k-steps (10) than waves
+    (16, 16, 20, 5, 12000, "f32"),   # 8 waves, two column tiles
 ])
 def test_embed_fm_kernel_variants(gpu, embed_fm_variant, k, kfm, F, nd, B, idt):
     from recommender_system_amd import _lib
