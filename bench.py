@@ -277,15 +277,16 @@ def bench_hotpath(args, world, rank):
         err = torch.zeros(1, dtype=torch.int32, device=dev)
         lib = _lib.lib()
         tptr, optr, vptr = e.table.data_ptr(), e.field_offsets.data_ptr(), e.field_vocab.data_ptr()
+        hoff, hvoc = e.host_meta()  # the field metadata also as kernel arguments (DeepFM.fm_logit's entry)
         pptr, w0ptr, lptr, eptr = prep.data_ptr(), model.fm.w0.data_ptr(), logit.data_ptr(), err.data_ptr()
 
         def step(i):
             j = i % ids_pool.shape[0]
             ids, dense = ids_pool[j], dense_pool[j]
-            st = lib.rs_embed_fm_fwd(ids.data_ptr(), 0, F, dense.data_ptr(), nd, nd, tptr, optr, vptr, F, k, pptr,
-                                     w0ptr, kfm, lptr, None, B, eptr, _lib.stream())
+            st = lib.rs_embed_fm_fwd_hm(ids.data_ptr(), 0, F, dense.data_ptr(), nd, nd, tptr, optr, vptr, hoff, hvoc,
+                                        F, k, pptr, w0ptr, kfm, lptr, None, B, eptr, _lib.stream())
             if st:
-                _lib.check(st, "rs_embed_fm_fwd")
+                _lib.check(st, "rs_embed_fm_fwd_hm")
 
         # value: the K timed steps replayed from HIP graphs (no host launch cost)
         dt, slot_ms = _timed_graph(step, args.steps, args.warmup, world)
@@ -320,10 +321,11 @@ def bench_hotpath(args, world, rank):
             def step_s(i, ns=ns, logits=logits):
                 j = i % ids_pool.shape[0]
                 ids, dense = ids_pool[j], dense_pool[j]
-                st = lib.rs_embed_fm_fwd(ids.data_ptr(), 0, F, dense.data_ptr(), nd, nd, tptr, optr, vptr, F, k,
-                                         pptr, w0ptr, kfm, logits[i % ns].data_ptr(), None, B, eptr, _lib.stream())
+                st = lib.rs_embed_fm_fwd_hm(ids.data_ptr(), 0, F, dense.data_ptr(), nd, nd, tptr, optr, vptr, hoff,
+                                            hvoc, F, k, pptr, w0ptr, kfm, logits[i % ns].data_ptr(), None, B, eptr,
+                                            _lib.stream())
                 if st:
-                    _lib.check(st, "rs_embed_fm_fwd")
+                    _lib.check(st, "rs_embed_fm_fwd_hm")
 
             n = max(ns * 32, (args.steps // ns) * ns)
             t = _timed_graph_streams(step_s, n, ns, world)
@@ -337,10 +339,10 @@ def bench_hotpath(args, world, rank):
 
         def step_z(i):
             ids, dense = zipf_pool[i % 16], dense_pool[i % 64]
-            st = lib.rs_embed_fm_fwd(ids.data_ptr(), 0, F, dense.data_ptr(), nd, nd, tptr, optr, vptr, F, k, pptr,
-                                     w0ptr, kfm, zlogit.data_ptr(), None, B, eptr, _lib.stream())
+            st = lib.rs_embed_fm_fwd_hm(ids.data_ptr(), 0, F, dense.data_ptr(), nd, nd, tptr, optr, vptr, hoff, hvoc,
+                                        F, k, pptr, w0ptr, kfm, zlogit.data_ptr(), None, B, eptr, _lib.stream())
             if st:
-                _lib.check(st, "rs_embed_fm_fwd")
+                _lib.check(st, "rs_embed_fm_fwd_hm")
 
         dtz, slotz = _timed_graph(step_z, args.steps, args.warmup, world)
         uniq = float(np.mean([len(np.unique(zipf_pool[j].cpu().numpy())) for j in range(4)])) / (B * F)

@@ -118,6 +118,22 @@ int rs_embed_fm_fwd(const void* ids, int id_kind, int64_t id_stride,
                     const float* prepared, const float* w0, int kfm,
                     float* logit, float* x_out, int64_t batch, int* err_flag,
                     rs_stream_t stream);
+/* The same with the field metadata also given on the HOST (read at call
+ * time, copied into the launch: graph capture keeps the values of the
+ * capturing call).  For n_fields <= 32 and batch <= 8192 the kernel then
+ * reads (offset, vocab) through scalar kernel-argument loads and each wave
+ * loads its own fields' ids — no workgroup id tile, no barrier; otherwise
+ * (or with a kernel option other than 0 set) it is rs_embed_fm_fwd.  The
+ * host arrays must equal the device ones.                                    */
+int rs_embed_fm_fwd_hm(const void* ids, int id_kind, int64_t id_stride,
+                       const float* dense, int64_t dense_stride, int nd,
+                       const float* table, const int64_t* field_offsets,
+                       const int64_t* field_vocab,
+                       const int64_t* field_offsets_host,
+                       const int64_t* field_vocab_host, int n_fields, int k,
+                       const float* prepared, const float* w0, int kfm,
+                       float* logit, float* x_out, int64_t batch, int* err_flag,
+                       rs_stream_t stream);
 
 /* FMLayer on an arbitrary dense x[B,n] (layer/interaction.py:106-114), e.g.
  * the FM model's one-hot input (model/fm.py:19-23).  `prepared` comes from

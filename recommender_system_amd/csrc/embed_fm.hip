@@ -130,8 +130,9 @@ __global__ void fm_prepare_generic(const float* __restrict__ w1, const float* __
 // on it, closed by sigmoid(c0*dnn + c1*fm) (model/deepFM.py:24-30).
 // TS: samples per workgroup (16 = one MFMA row tile; 8 = the tile's rows
 // 8..15 repeat rows 0..7, two workgroups per CU at batch 4096)
-template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, int TS = 16, bool PF = false>
-__device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArgs* tw, const int tile) {
+template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, int TS = 16, bool PF = false, bool KA = false>
+__device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArgs* tw, const int tile,
+                                              const FieldMeta* km = nullptr) {
   static_assert(TS == 16 || (TS == 8 && !TW && KIND != 4), "8-sample tiles: plain FM kernel only");
   // MC > 0: field slots per wave and pass (owner kernels with few fields)
   constexpr int MAXC0 = MC > 0 ? MC : 128 / (NW * KV);
@@ -217,9 +218,9 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   __shared__ typename I::raw_t lid[16][FMAX];
   __shared__ int64_t lmeta[2][FMAX];
 #ifdef RS_DIAG_STAMPS
-  const bool coop = (KIND != 3) && a.F <= FMAX && !(a.ablate & 16);  // bit 16: per-wave id loads
+  const bool coop = !KA && (KIND != 3) && a.F <= FMAX && !(a.ablate & 16);  // bit 16: per-wave id loads
 #else
-  const bool coop = (KIND != 3) && a.F <= FMAX;
+  const bool coop = !KA && (KIND != 3) && a.F <= FMAX;
 #endif
   if (coop) {
     const int64_t b0 = (int64_t)tile * TS;
@@ -304,6 +305,10 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
           offc[j] = lmeta[0][P.cj[j]];
           vocc[j] = lmeta[1][P.cj[j]];
           P.rid[j] = lid[s % TS][P.cj[j]];
+        } else if constexpr (KA) {  // kernarg metadata: scalar loads, wave-uniform field
+          offc[j] = km->off[P.cj[j]];
+          vocc[j] = km->voc[P.cj[j]];
+          P.rid[j] = I::load(a.ids, b * a.id_stride + P.cj[j]);
         } else {
           const int cv = min(cg + j * NW + wv, a.F - 1);
           offc[j] = a.offs[cv];
@@ -507,6 +512,14 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 template <int KV, int NT, int NW, int KIND, int MC, int TS = 16, bool PF = false>
 __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
   embed_fm_body<KV, NT, NW, KIND, false, MC, TS, PF>(a, nullptr, blockIdx.x);
+}
+
+// the field metadata by value (rs_embed_fm_fwd_hm): each wave loads its own
+// fields' ids and reads (offset, vocab) through scalar kernarg loads — no LDS
+// id tile, no barrier, no per-wave metadata loads from one hot L2 line
+template <int KV, int NT, int KIND>
+__global__ __launch_bounds__(16 * 64) void embed_fm_mfma_ka(EmbedFmArgs a, FieldMeta m) {
+  embed_fm_body<KV, NT, 16, KIND, false, 1, 16, false, true>(a, nullptr, blockIdx.x, &m);
 }
 
 // ---- sharded FM, partial protocol: combine (requester side) as a block part
@@ -780,7 +793,7 @@ static int grid_for(int64_t work, int block, int cap = 2048) {
 }
 
 template <int KV, int NT, int KIND>
-static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st) {
+static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st, const FieldMeta* hm) {
   // 16 waves per 16-sample tile (measured against 4, 8 and 13 waves), one
   // field slot per wave and pass: the headline's 26 fields take two passes
   // (16 + 10), 6.05 us per launch against 6.54 with both in one pass (2 slots
@@ -796,6 +809,13 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st) {
   // wave and pass): 8 waves up to 1024 tiles, 4 beyond (scripts/ab A/B,
   // graph slots: 13.0 -> 11.4 us at B 12288, 14.5 -> 13.5 at 16384, 27.0 ->
   // 22.9 at 32768, 50.7 -> 42.7 at 65536; profiles/r3_ab_nw*.json)
+  // host field metadata given (rs_embed_fm_fwd_hm), up to 2 tiles per CU:
+  // the kernarg-metadata kernel (6.92 -> 6.50 us at B 4096, 6.10 -> 5.78 at
+  // 2048; profiles/r3_ab_kernarg_meta_{4096,2048}.json)
+  if (hm && a.F <= 32 && grid <= 512 && KIND != 3) {
+    embed_fm_mfma_ka<KV, NT, KIND><<<grid, 16 * 64, 0, st>>>(a, *hm);
+    return;
+  }
   if (a.F <= 32 && grid > 1024) embed_fm_mfma<KV, NT, 4, KIND, 1, TS, true><<<grid, 4 * 64, 0, st>>>(a);
   else if (a.F <= 32 && grid > 512) embed_fm_mfma<KV, NT, 8, KIND, 1, TS, true><<<grid, 8 * 64, 0, st>>>(a);
   else if (a.F <= 32) embed_fm_mfma<KV, NT, 16, KIND, 1, TS><<<grid, 16 * 64, 0, st>>>(a);
@@ -803,28 +823,30 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st) {
 }
 
 template <int KIND>
-static void launch_embed_fm_k(const EmbedFmArgs& a, int KV, int NT, hipStream_t st) {
+static void launch_embed_fm_k(const EmbedFmArgs& a, int KV, int NT, hipStream_t st,
+                              const FieldMeta* hm = nullptr) {
   if (NT == 1) {
     switch (KV) {
-      case 1: launch_embed_fm3<1, 1, KIND>(a, st); break;
-      case 2: launch_embed_fm3<2, 1, KIND>(a, st); break;
-      case 4: launch_embed_fm3<4, 1, KIND>(a, st); break;
-      case 8: launch_embed_fm3<8, 1, KIND>(a, st); break;
-      default: launch_embed_fm3<16, 1, KIND>(a, st); break;
+      case 1: launch_embed_fm3<1, 1, KIND>(a, st, hm); break;
+      case 2: launch_embed_fm3<2, 1, KIND>(a, st, hm); break;
+      case 4: launch_embed_fm3<4, 1, KIND>(a, st, hm); break;
+      case 8: launch_embed_fm3<8, 1, KIND>(a, st, hm); break;
+      default: launch_embed_fm3<16, 1, KIND>(a, st, hm); break;
     }
   } else {
     switch (KV) {
-      case 1: launch_embed_fm3<1, 2, KIND>(a, st); break;
-      case 2: launch_embed_fm3<2, 2, KIND>(a, st); break;
-      case 4: launch_embed_fm3<4, 2, KIND>(a, st); break;
-      case 8: launch_embed_fm3<8, 2, KIND>(a, st); break;
-      default: launch_embed_fm3<16, 2, KIND>(a, st); break;
+      case 1: launch_embed_fm3<1, 2, KIND>(a, st, hm); break;
+      case 2: launch_embed_fm3<2, 2, KIND>(a, st, hm); break;
+      case 4: launch_embed_fm3<4, 2, KIND>(a, st, hm); break;
+      case 8: launch_embed_fm3<8, 2, KIND>(a, st, hm); break;
+      default: launch_embed_fm3<16, 2, KIND>(a, st, hm); break;
     }
   }
 }
 
 // kind: RS_ID_* or 3 (rows already gathered)
-static int run_embed_fm(EmbedFmArgs a, const FmGeom& g, int kind, hipStream_t st, const char* what) {
+static int run_embed_fm(EmbedFmArgs a, const FmGeom& g, int kind, hipStream_t st, const char* what,
+                        const FieldMeta* hm = nullptr) {
   if (a.batch == 0) return RS_OK;
   if (g.mfma) {
     a.DB = g.DB;
@@ -839,7 +861,7 @@ static int run_embed_fm(EmbedFmArgs a, const FmGeom& g, int kind, hipStream_t st
     } else if (launch_embed_fm_tiles(a, g, kind, opt(RS_OPT_EMBED_FM_KERNEL), st)) {
       // the persistent tile kernels (embed_fm_tiles.hip), when selected and the shape fits
     } else {
-      with_id_kind(kind, [&](auto K) { launch_embed_fm_k<decltype(K)::value>(a, g.KV, g.NT, st); });
+      with_id_kind(kind, [&](auto K) { launch_embed_fm_k<decltype(K)::value>(a, g.KV, g.NT, st, hm); });
     }
   } else {
     if (a.F > 1024) {
@@ -913,6 +935,51 @@ extern "C" int rs_embed_fm_fwd(const void* ids, int id_kind, int64_t id_stride, 
   a.batch = batch;
   a.err = err_flag;
   return run_embed_fm(a, g, id_kind, as_stream(stream), "rs_embed_fm_fwd");
+}
+
+extern "C" int rs_embed_fm_fwd_hm(const void* ids, int id_kind, int64_t id_stride, const float* dense,
+                                  int64_t dense_stride, int nd, const float* table, const int64_t* field_offsets,
+                                  const int64_t* field_vocab, const int64_t* field_offsets_host,
+                                  const int64_t* field_vocab_host, int n_fields, int k, const float* prepared,
+                                  const float* w0, int kfm, float* logit, float* x_out, int64_t batch,
+                                  int* err_flag, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(field_offsets_host && field_vocab_host, "rs_embed_fm_fwd_hm: host metadata missing");
+  if (n_fields > 32 || opt(RS_OPT_EMBED_FM_KERNEL) != 0)
+    return rs_embed_fm_fwd(ids, id_kind, id_stride, dense, dense_stride, nd, table, field_offsets, field_vocab,
+                           n_fields, k, prepared, w0, kfm, logit, x_out, batch, err_flag, stream);
+  RS_REQUIRE(batch >= 0 && nd >= 0 && n_fields >= 0 && kfm >= 1, "rs_embed_fm_fwd_hm: bad shape");
+  RS_REQUIRE(prepared && w0 && logit, "rs_embed_fm_fwd_hm: null pointer");
+  RS_REQUIRE(nd == 0 || dense, "rs_embed_fm_fwd_hm: dense is null");
+  RS_REQUIRE(n_fields == 0 || (ids && table && field_offsets && field_vocab && k >= 1),
+             "rs_embed_fm_fwd_hm: sparse inputs missing");
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_embed_fm_fwd_hm: bad id_kind");
+  RS_REQUIRE(k % 4 != 0 || (uintptr_t)table % 16 == 0, "rs_embed_fm_fwd_hm: table must be 16-B aligned");
+  FieldMeta m{};
+  for (int c = 0; c < n_fields; ++c) {
+    m.off[c] = field_offsets_host[c];
+    m.voc[c] = field_vocab_host[c];
+  }
+  const FmGeom g = fm_geom(nd, n_fields, k, kfm);
+  EmbedFmArgs a{};
+  a.ids = ids;
+  a.id_stride = id_stride;
+  a.dense = dense;
+  a.dense_stride = dense_stride;
+  a.nd = nd;
+  a.table = table;
+  a.offs = field_offsets;
+  a.vocab = field_vocab;
+  a.F = n_fields;
+  a.k = k;
+  a.prep = prepared;
+  a.w0 = w0;
+  a.kfm = kfm;
+  a.logit = logit;
+  a.x_out = x_out;
+  a.batch = batch;
+  a.err = err_flag;
+  return run_embed_fm(a, g, id_kind, as_stream(stream), "rs_embed_fm_fwd_hm", &m);
 }
 
 #ifdef RS_DIAG_STAMPS

@@ -67,6 +67,13 @@ struct EmbedFmArgs {
   int ablate;               // diagnostic builds only: bit0 no MFMA, bit1 no B loads, bit2 no combine
 };
 
+// Field metadata by value in the kernarg (diagnostic build -DRS_DIAG_KARG:
+// the per-wave id path reads it through scalar loads, no LDS id tile)
+struct FieldMeta {
+  int64_t off[32];
+  int64_t voc[32];
+};
+
 // Launches of embed_fm_tiles.hip (rs_embed_fm_fwd, id kinds 0..2): returns
 // false when the shape / option has no kernel there (the caller then runs the
 // K-split kernel of embed_fm.hip).

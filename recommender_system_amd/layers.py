@@ -139,6 +139,11 @@ class EmbedLayer(KerasModule):
     like the reference (which ignores feat['embed_dim'] and uses k).
     """
 
+    def host_meta(self):
+        """(offsets, vocab) as host int64 arrays (addresses), for the entry
+        points that take the field metadata by value."""
+        return C.addressof(self._host_offsets), C.addressof(self._host_vocab)
+
     def __init__(self, sparse_feature_columns, k=8, device=None, seed=None):
         super().__init__(device, seed)
         self.k = int(k)
@@ -151,6 +156,10 @@ class EmbedLayer(KerasModule):
         self.total_rows = sum(self.vocab_sizes)
         self.register_buffer("field_offsets", torch.tensor(offs, dtype=torch.int64, device=self._dev))
         self.register_buffer("field_vocab", torch.tensor(self.vocab_sizes, dtype=torch.int64, device=self._dev))
+        # host copies of the same metadata (rs_embed_fm_fwd_hm: kernel arguments)
+        F = max(self.n_fields, 1)
+        self._host_offsets = (C.c_int64 * F)(*offs[:self.n_fields])
+        self._host_vocab = (C.c_int64 * F)(*self.vocab_sizes)
         table = torch.empty(self.total_rows, self.k, dtype=torch.float32, device=self._dev)
         if table.is_cuda:
             g = torch.Generator(device=table.device)

@@ -294,9 +294,10 @@ class DeepFM(KerasModule):
         e = self.embed_layer
         prep = self.fm.prepared(self.nd, e.n_fields, e.k)
         logit = torch.empty(B, 1, dtype=torch.float32, device=self._dev)
-        call("rs_embed_fm_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), self.nd,
-             ptr(e.table), ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, e.k, ptr(prep), ptr(self.fm.w0),
-             self.fm.k, ptr(logit), ptr(x_out), B, ptr(self._err.t), _lib.stream())
+        hoff, hvoc = e.host_meta()
+        call("rs_embed_fm_fwd_hm", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), self.nd,
+             ptr(e.table), ptr(e.field_offsets), ptr(e.field_vocab), hoff, hvoc, e.n_fields, e.k, ptr(prep),
+             ptr(self.fm.w0), self.fm.k, ptr(logit), ptr(x_out), B, ptr(self._err.t), _lib.stream())
         if check_ids:
             self._err.check("DeepFM")
         return logit

@@ -171,6 +171,72 @@ def test_embed_fm_kernel_variants(gpu, embed_fm_variant, k, kfm, F, nd, B, idt):
     assert err.item() != 0
 
 
+@pytest.mark.parametrize("k,kfm,F,nd,B,idt,with_x", [
+    (16, 10, 26, 13, 4096, "i32", False),   # the headline: kernarg-metadata kernel
+    (16, 10, 26, 13, 8192, "i64", True),    # two tiles per CU, x emitted
+    (16, 10, 32, 13, 300, "f32", False),    # F at the kernarg limit
+    (8, 10, 26, 40, 1000, "i32", True),     # k 8, more dense k-steps than fit one per wave
+    (16, 16, 20, 5, 130, "i32", False),     # two MFMA column tiles
+    (16, 10, 26, 13, 9000, "i32", False),   # > 512 tiles: the device-metadata kernel
+    (16, 10, 33, 13, 64, "i32", False),     # F > 32: the device-metadata kernel
+])
+def test_embed_fm_host_meta(gpu, k, kfm, F, nd, B, idt, with_x):
+    """rs_embed_fm_fwd_hm (field metadata also as kernel arguments, per-wave
+    id loads, no id tile) == rs_embed_fm_fwd bit for bit (logit and x) and ==
+    the oracle; an out-of-range id sets the flag."""
+    import ctypes as C
+    from recommender_system_amd import _lib
+    rng = np.random.default_rng(B * 7 + F)
+    vocabs = rng.integers(2, 5000, size=F).tolist()
+    offs, offs_d, voc_d = _layout(vocabs, gpu)
+    hoff = (C.c_int64 * F)(*offs)
+    hvoc = (C.c_int64 * F)(*vocabs)
+    d = nd + F * k
+    table = rng.uniform(-0.05, 0.05, size=(sum(vocabs), k)).astype(np.float32)
+    w1 = (rng.standard_normal((d, 1)) * 0.05).astype(np.float32)
+    v = (rng.standard_normal((d, kfm)) * 0.05).astype(np.float32)
+    w0 = np.array([0.017], np.float32)
+    ids = random_ids(rng, B, vocabs)
+    ids[0] = np.asarray(vocabs) - 1
+    dense = rng.random((B, nd)).astype(np.float32)
+    prep = torch.empty(_lib.lib().rs_fm_prepared_size(nd, F, k, kfm), device=gpu)
+    w1_d, v_d, w0_d = _t(w1, gpu), _t(v, gpu), _t(w0, gpu)
+    _lib.call("rs_fm_prepare", w1_d.data_ptr(), v_d.data_ptr(), nd, F, k, kfm, prep.data_ptr(), 0)
+    kind, dt = {"i32": (0, torch.int32), "i64": (1, torch.int64), "f32": (2, torch.float32)}[idt]
+    dense_d, tab_d = _t(dense, gpu), _t(table, gpu)
+    err = torch.zeros(1, dtype=torch.int32, device=gpu)
+
+    def run(ids_np, hm):
+        ids_t = _t(ids_np, gpu, dt)
+        logit = torch.full((B,), 99.0, device=gpu)
+        x = torch.full((B, d), 7.0, device=gpu) if with_x else None
+        common = [ids_t.data_ptr(), kind, ids_t.stride(0), dense_d.data_ptr() if nd else None, nd, nd,
+                  tab_d.data_ptr(), offs_d.data_ptr(), voc_d.data_ptr()]
+        tail = [F, k, prep.data_ptr(), w0_d.data_ptr(), kfm, logit.data_ptr(), None if x is None else x.data_ptr(), B,
+                err.data_ptr(), 0]
+        if hm:
+            _lib.call("rs_embed_fm_fwd_hm", *common, C.addressof(hoff), C.addressof(hvoc), *tail)
+        else:
+            _lib.call("rs_embed_fm_fwd", *common, *tail)
+        torch.cuda.synchronize()
+        return logit, x
+
+    ref_logit, ref_x = run(ids, False)
+    assert err.item() == 0
+    got_logit, got_x = run(ids, True)
+    assert err.item() == 0
+    assert torch.equal(got_logit, ref_logit)
+    if with_x:
+        assert torch.equal(got_x, ref_x)
+    tables = [table[o:o + vv] for o, vv in zip(offs, vocabs)]
+    x64 = np.concatenate([dense, O.embed_layer(ids, tables, np.float64)], 1)
+    assert_scaled_close(got_logit, O.fm_layer(x64, w0, w1, v)[:, 0], what="embed_fm host meta")
+    bad = ids.copy()
+    bad[B - 1, F - 1] = vocabs[F - 1]
+    run(bad, True)
+    assert err.item() != 0
+
+
 def test_embed_fm_packed_float_X_and_oor(gpu):
     """Packed X[B,39] float ids (Keras int32 truncation) and the OOR flag."""
     from recommender_system_amd import DeepFM
