@@ -354,6 +354,20 @@ int rs_deepfm_fwd(const void* ids, int id_kind, int64_t id_stride,
                   const float* mlp_prepared, float c0, float c1, float* out,
                   float* fm_logit, int64_t batch, int* err_flag,
                   rs_stream_t stream);
+/* rs_deepfm_fwd with the field metadata also on the host (kernel arguments
+ * for n_fields <= 32, as rs_embed_fm_fwd_hm; the host arrays must equal the
+ * device ones).                                                             */
+int rs_deepfm_fwd_hm(const void* ids, int id_kind, int64_t id_stride,
+                     const float* dense, int64_t dense_stride, int nd,
+                     const float* table, const int64_t* field_offsets,
+                     const int64_t* field_vocab,
+                     const int64_t* field_offsets_host,
+                     const int64_t* field_vocab_host, int n_fields, int k,
+                     const float* fm_prepared, const float* w0, int kfm,
+                     int n_layers, const int* dims, const int* acts,
+                     const float* mlp_prepared, float c0, float c1, float* out,
+                     float* fm_logit, int64_t batch, int* err_flag,
+                     rs_stream_t stream);
 
 /* Dense + PReLU whose alpha is [alpha_rows, N], row m using alpha row
  * m % alpha_rows: Keras Dense(N, activation=PReLU()) on a 3-D input

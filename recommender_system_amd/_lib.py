@@ -61,6 +61,7 @@ SIGNATURES = {
     "rs_mlp_fwd": (I, [P, L, I, P, P, P, P, L, I, P, F, F, L, P]),
     "rs_deepfm_fused_ok": (I, [I, I, I, I, I, P]),
     "rs_deepfm_fwd": (I, [P, I, L, P, L, I, P, P, P, I, I, P, P, I, I, P, P, P, F, F, P, P, L, P, P]),
+    "rs_deepfm_fwd_hm": (I, [P, I, L, P, L, I, P, P, P, P, P, I, I, P, P, I, I, P, P, P, F, F, P, P, L, P, P]),
     "rs_affine_act": (I, [P, L, P, P, P, I, P, L, L, I, P]),
     "rs_sigmoid_combine": (I, [P, P, F, F, P, L, P]),
     "rs_dice_fwd": (I, [P, L, P, P, F, P, P, L, L, I, P]),

@@ -517,9 +517,9 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
 // the field metadata by value (rs_embed_fm_fwd_hm): each wave loads its own
 // fields' ids and reads (offset, vocab) through scalar kernarg loads — no LDS
 // id tile, no barrier, no per-wave metadata loads from one hot L2 line
-template <int KV, int NT, int KIND>
-__global__ __launch_bounds__(16 * 64) void embed_fm_mfma_ka(EmbedFmArgs a, FieldMeta m) {
-  embed_fm_body<KV, NT, 16, KIND, false, 1, 16, false, true>(a, nullptr, blockIdx.x, &m);
+template <int KV, int NT, int NW, int KIND, bool PF>
+__global__ __launch_bounds__(NW * 64) void embed_fm_mfma_ka(EmbedFmArgs a, FieldMeta m) {
+  embed_fm_body<KV, NT, NW, KIND, false, 1, 16, PF, true>(a, nullptr, blockIdx.x, &m);
 }
 
 // ---- sharded FM, partial protocol: combine (requester side) as a block part
@@ -611,6 +611,11 @@ __global__ __launch_bounds__(NW * 64) void shard_fm_pipe(EmbedFmArgs a, PipeArgs
 template <int KV, int KIND>
 __global__ __launch_bounds__(16 * 64) void deepfm_fused(EmbedFmArgs a, MlpArgs t) {
   embed_fm_body<KV, 1, 16, KIND, true, 1>(a, &t, blockIdx.x);
+}
+// ... with the field metadata by value (rs_deepfm_fwd_hm; see embed_fm_mfma_ka)
+template <int KV, int KIND>
+__global__ __launch_bounds__(16 * 64) void deepfm_fused_ka(EmbedFmArgs a, MlpArgs t, FieldMeta m) {
+  embed_fm_body<KV, 1, 16, KIND, true, 1, 16, false, true>(a, &t, blockIdx.x, &m);
 }
 
 // Generic fallback (any k / kfm): one 256-thread workgroup per sample.
@@ -812,8 +817,12 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st, const FieldMe
   // host field metadata given (rs_embed_fm_fwd_hm), up to 2 tiles per CU:
   // the kernarg-metadata kernel (6.92 -> 6.50 us at B 4096, 6.10 -> 5.78 at
   // 2048; profiles/r3_ab_kernarg_meta_{4096,2048}.json)
-  if (hm && a.F <= 32 && grid <= 512 && KIND != 3) {
-    embed_fm_mfma_ka<KV, NT, KIND><<<grid, 16 * 64, 0, st>>>(a, *hm);
+  // with the ids loaded per wave, the first passes' B fragments beside them
+  // pay at 4096 too (6.61 -> 6.39 us, profiles/r3_ab_kernarg_pf_4096.json);
+  // above 512 tiles the device-metadata kernels stay faster (14.26 vs 13.48
+  // us at 16384, 47.5 vs 42.6 at 65536; profiles/r3_ab_kernarg_allgrids_*)
+  if (hm && a.F <= 32 && KIND != 3 && grid <= 512) {
+    embed_fm_mfma_ka<KV, NT, 16, KIND, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
     return;
   }
   if (a.F <= 32 && grid > 1024) embed_fm_mfma<KV, NT, 4, KIND, 1, TS, true><<<grid, 4 * 64, 0, st>>>(a);
@@ -1434,14 +1443,18 @@ static bool deepfm_geom(int nd, int n_fields, int k, int kfm, int n_layers, cons
 }
 
 template <int KV, int KIND>
-static void launch_deepfm(const EmbedFmArgs& a, const MlpArgs& t, size_t lds, hipStream_t st) {
-  static size_t lds_set = 64 * 1024;  // opt in to exactly what is needed beyond the default
-  if (lds > lds_set) {
-    (void)hipFuncSetAttribute((const void*)deepfm_fused<KV, KIND>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    lds_set = lds;
+static void launch_deepfm(const EmbedFmArgs& a, const MlpArgs& t, size_t lds, hipStream_t st,
+                          const FieldMeta* hm) {
+  static size_t lds_set[2] = {64 * 1024, 64 * 1024};  // opt in to exactly what is needed beyond the default
+  const int ka = hm && a.F <= 32 ? 1 : 0;
+  if (lds > lds_set[ka]) {
+    (void)hipFuncSetAttribute(ka ? (const void*)deepfm_fused_ka<KV, KIND> : (const void*)deepfm_fused<KV, KIND>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    lds_set[ka] = lds;
   }
-  deepfm_fused<KV, KIND><<<(unsigned)((a.batch + 15) / 16), 16 * 64, lds, st>>>(a, t);
+  const unsigned grid = (unsigned)((a.batch + 15) / 16);
+  if (ka) deepfm_fused_ka<KV, KIND><<<grid, 16 * 64, lds, st>>>(a, t, *hm);
+  else deepfm_fused<KV, KIND><<<grid, 16 * 64, lds, st>>>(a, t);
 }
 }  // namespace rs
 
@@ -1451,12 +1464,11 @@ extern "C" int rs_deepfm_fused_ok(int nd, int n_fields, int k, int kfm, int n_la
   return dims && deepfm_geom(nd, n_fields, k, kfm, n_layers, dims, fg, mg) ? 1 : 0;
 }
 
-extern "C" int rs_deepfm_fwd(const void* ids, int id_kind, int64_t id_stride, const float* dense,
-                             int64_t dense_stride, int nd, const float* table, const int64_t* field_offsets,
-                             const int64_t* field_vocab, int n_fields, int k, const float* fm_prepared,
-                             const float* w0, int kfm, int n_layers, const int* dims, const int* acts,
-                             const float* mlp_prepared, float c0, float c1, float* out, float* fm_logit,
-                             int64_t batch, int* err_flag, rs_stream_t stream) {
+static int deepfm_run(const void* ids, int id_kind, int64_t id_stride, const float* dense, int64_t dense_stride,
+                      int nd, const float* table, const int64_t* field_offsets, const int64_t* field_vocab,
+                      int n_fields, int k, const float* fm_prepared, const float* w0, int kfm, int n_layers,
+                      const int* dims, const int* acts, const float* mlp_prepared, float c0, float c1, float* out,
+                      float* fm_logit, int64_t batch, int* err_flag, rs_stream_t stream, const FieldMeta* hm) {
   if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   FmGeom fg;
   MlpGeom mg;
@@ -1501,8 +1513,38 @@ extern "C" int rs_deepfm_fwd(const void* ids, int id_kind, int64_t id_stride, co
   hipStream_t st = as_stream(stream);
   with_id_kind(id_kind, [&](auto K) {
     constexpr int KIND = decltype(K)::value;
-    if (fg.KV == 2) launch_deepfm<2, KIND>(a, t, mg.lds, st);
-    else launch_deepfm<4, KIND>(a, t, mg.lds, st);
+    if (fg.KV == 2) launch_deepfm<2, KIND>(a, t, mg.lds, st, hm);
+    else launch_deepfm<4, KIND>(a, t, mg.lds, st, hm);
   });
   return launch_status("rs_deepfm_fwd");
+}
+
+extern "C" int rs_deepfm_fwd(const void* ids, int id_kind, int64_t id_stride, const float* dense,
+                             int64_t dense_stride, int nd, const float* table, const int64_t* field_offsets,
+                             const int64_t* field_vocab, int n_fields, int k, const float* fm_prepared,
+                             const float* w0, int kfm, int n_layers, const int* dims, const int* acts,
+                             const float* mlp_prepared, float c0, float c1, float* out, float* fm_logit,
+                             int64_t batch, int* err_flag, rs_stream_t stream) {
+  return deepfm_run(ids, id_kind, id_stride, dense, dense_stride, nd, table, field_offsets, field_vocab, n_fields, k,
+                    fm_prepared, w0, kfm, n_layers, dims, acts, mlp_prepared, c0, c1, out, fm_logit, batch, err_flag,
+                    stream, nullptr);
+}
+
+extern "C" int rs_deepfm_fwd_hm(const void* ids, int id_kind, int64_t id_stride, const float* dense,
+                                int64_t dense_stride, int nd, const float* table, const int64_t* field_offsets,
+                                const int64_t* field_vocab, const int64_t* field_offsets_host,
+                                const int64_t* field_vocab_host, int n_fields, int k, const float* fm_prepared,
+                                const float* w0, int kfm, int n_layers, const int* dims, const int* acts,
+                                const float* mlp_prepared, float c0, float c1, float* out, float* fm_logit,
+                                int64_t batch, int* err_flag, rs_stream_t stream) {
+  RS_REQUIRE(batch == 0 || (field_offsets_host && field_vocab_host), "rs_deepfm_fwd_hm: host metadata missing");
+  FieldMeta m{};
+  const bool use = n_fields <= 32 && batch > 0;
+  for (int c = 0; use && c < n_fields; ++c) {
+    m.off[c] = field_offsets_host[c];
+    m.voc[c] = field_vocab_host[c];
+  }
+  return deepfm_run(ids, id_kind, id_stride, dense, dense_stride, nd, table, field_offsets, field_vocab, n_fields, k,
+                    fm_prepared, w0, kfm, n_layers, dims, acts, mlp_prepared, c0, c1, out, fm_logit, batch, err_flag,
+                    stream, use ? &m : nullptr);
 }

@@ -387,10 +387,11 @@ class DeepFM(KerasModule):
         n = len(dims) - 1
         acts = [_lib.ACT[l.activation] for l in self.dnn._layers()]
         out = torch.empty(B, 1, dtype=torch.float32, device=self._dev)
-        call("rs_deepfm_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), self.nd,
-             ptr(e.table), ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, e.k, ptr(prep), ptr(self.fm.w0),
-             self.fm.k, n, (C.c_int * (n + 1))(*dims), (C.c_int * n)(*acts), ptr(mlp), 0.5, 0.5, ptr(out),
-             ptr(fm_logit), B, ptr(self._err.t), _lib.stream())
+        hoff, hvoc = e.host_meta()
+        call("rs_deepfm_fwd_hm", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), self.nd,
+             ptr(e.table), ptr(e.field_offsets), ptr(e.field_vocab), hoff, hvoc, e.n_fields, e.k, ptr(prep),
+             ptr(self.fm.w0), self.fm.k, n, (C.c_int * (n + 1))(*dims), (C.c_int * n)(*acts), ptr(mlp), 0.5, 0.5,
+             ptr(out), ptr(fm_logit), B, ptr(self._err.t), _lib.stream())
         if check_ids:
             self._err.check("DeepFM")
         return out

@@ -205,12 +205,17 @@ class HipShardOps:
 
     def deepfm_rows(self, model, got, rb, dense, out):
         """DeepFM forward with lookup (b, c)'s row at got[slot_of[b, c]]."""
-        return _hip_deepfm(self, model, rb["slot_of"], got, rb["zoff"], rb["nslots"], dense, out)
+        hm = rb.get("hmeta")
+        if hm is None:  # the exchange layout's metadata on the host: offsets 0, n slots per field
+            F = model.F
+            hm = rb["hmeta"] = ((C.c_int64 * F)(*([0] * F)), (C.c_int64 * F)(*([int(rb["n"])] * F)))
+        return _hip_deepfm(self, model, rb["slot_of"], got, rb["zoff"], rb["nslots"], dense, out, hm)
 
     def deepfm_table(self, model, ids, dense, out):
         """World 1: the DeepFM forward on the (whole-table) shard itself."""
         sh = model.emb
-        return _hip_deepfm(self, model, ids, sh.table_shard, sh.offsets, sh.vocab, dense, out)
+        return _hip_deepfm(self, model, ids, sh.table_shard, sh.offsets, sh.vocab, dense, out,
+                           (sh.host_offsets, sh.host_vocab))
 
     # -- training of ShardedDeepFM (row protocol + reverse row exchange)
     def deepfm_grads(self, model, got, rb, dense, labels, scale, tb, loss, drop=None):
@@ -347,6 +352,9 @@ class ShardedEmbeddingFM:
         self.row_range = (lo, hi)
         self.offsets = torch.tensor(offs, dtype=torch.int64, device=self.device)
         self.vocab = torch.tensor(self.vocab_sizes, dtype=torch.int64, device=self.device)
+        nf = max(len(offs), 1)  # host copies (the fused kernels' kernel-argument metadata)
+        self.host_offsets = (C.c_int64 * nf)(*offs[:len(self.vocab_sizes)])
+        self.host_vocab = (C.c_int64 * nf)(*self.vocab_sizes)
         self.table_shard = torch.empty(max(hi - lo, 0), self.k, dtype=torch.float32, device=self.device)
         if table_init:
             g = torch.Generator(device=self.device)
@@ -1079,16 +1087,18 @@ def _deepfm_fused_ok(model):
     return bool(_lib.lib().rs_deepfm_fused_ok(model.nd, model.F, model.k, model.kfm, n, dims))
 
 
-def _hip_deepfm(ops, model, ids, table, offs, vocab, dense, out):
-    """rs_deepfm_fwd (one launch) or, for shapes it does not take, the fused
+def _hip_deepfm(ops, model, ids, table, offs, vocab, dense, out, hmeta):
+    """rs_deepfm_fwd_hm (one launch; hmeta = the (offsets, vocab) host arrays
+    equal to offs / vocab) or, for shapes it does not take, the fused
     gather+FM kernel emitting x + the tower / per-layer DNN."""
     sh = model.emb
     if _deepfm_fused_ok(model):
         n, dims, acts = _deepfm_tower_args(model)
         mlp = model.dnn.prepared(model.fused_rows())
-        call("rs_deepfm_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), model.nd,
-             ptr(table), ptr(offs), ptr(vocab), model.F, model.k, ptr(sh.prepared), ptr(sh.w0), model.kfm, n, dims,
-             acts, ptr(mlp), 0.5, 0.5, ptr(out), None, ids.shape[0], ptr(ops.err), _lib.stream())
+        call("rs_deepfm_fwd_hm", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), model.nd,
+             ptr(table), ptr(offs), ptr(vocab), C.addressof(hmeta[0]), C.addressof(hmeta[1]), model.F, model.k,
+             ptr(sh.prepared), ptr(sh.w0), model.kfm, n, dims, acts, ptr(mlp), 0.5, 0.5, ptr(out), None,
+             ids.shape[0], ptr(ops.err), _lib.stream())
         return out
     from .layers import sigmoid_combine
     B = ids.shape[0]

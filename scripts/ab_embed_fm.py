@@ -16,6 +16,9 @@ def bind(path):
     lib = C.CDLL(path)
     P, L, I = C.c_void_p, C.c_int64, C.c_int
     lib.rs_embed_fm_fwd.argtypes = [P, I, L, P, L, I, P, P, P, I, I, P, P, I, P, P, L, P, P]
+    lib.has_hm = hasattr(lib, "rs_embed_fm_fwd_hm")
+    if lib.has_hm:  # the host-metadata entry (the product's headline path)
+        lib.rs_embed_fm_fwd_hm.argtypes = [P, I, L, P, L, I, P, P, P, P, P, I, I, P, P, I, P, P, L, P, P]
     lib.rs_fm_prepare.argtypes = [P, P, I, I, I, I, P, P]
     lib.rs_fm_prepared_size.restype = L
     lib.rs_fm_prepared_size.argtypes = [I, I, I, I]
@@ -37,6 +40,8 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     offs = torch.arange(F, dtype=torch.int64, device=dev) * V
     voc = torch.full((F,), V, dtype=torch.int64, device=dev)
+    hoff = (C.c_int64 * F)(*[c * V for c in range(F)])
+    hvoc = (C.c_int64 * F)(*([V] * F))
     NP = 64
     pool = torch.randint(0, V, (NP, B, F), dtype=torch.int32, device=dev)
     dense = torch.rand(NP, B, nd, device=dev)
@@ -49,6 +54,12 @@ def main():
 
         def fn(i, lib=lib, prep=prep, logit=logit):
             j = i % NP
+            if lib.has_hm and not os.environ.get("AB_NO_HM"):
+                lib.rs_embed_fm_fwd_hm(pool[j].data_ptr(), 0, F, dense[j].data_ptr(), nd, nd, table.data_ptr(),
+                                       offs.data_ptr(), voc.data_ptr(), C.addressof(hoff), C.addressof(hvoc), F, k,
+                                       prep.data_ptr(), w0.data_ptr(), kfm, logit[j].data_ptr(), None, B,
+                                       err.data_ptr(), torch.cuda.current_stream().cuda_stream)
+                return
             lib.rs_embed_fm_fwd(pool[j].data_ptr(), 0, F, dense[j].data_ptr(), nd, nd, table.data_ptr(),
                                 offs.data_ptr(), voc.data_ptr(), F, k, prep.data_ptr(), w0.data_ptr(), kfm,
                                 logit[j].data_ptr(), None, B, err.data_ptr(), torch.cuda.current_stream().cuda_stream)
