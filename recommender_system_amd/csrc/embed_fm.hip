@@ -251,6 +251,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     int cj[MAXC];
     bool ok[MAXC];
     typename I::raw_t rid[MAXC];
+    int64_t off[MAXC], voc[MAXC];
     Chunk<KV> xs[MAXC];
     Chunk<KV> bw[MAXC][NT];
     float nrm[MAXC][KV];
@@ -289,8 +290,10 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       }
   };
   const int wv = threadIdx.x >> 6;
-  auto issue_rows = [&](int cg, Pass& P) {
-    int64_t offc[MAXC], vocc[MAXC];
+  // a pass's ids and field metadata (issue_rows takes them from here)
+  auto fetch_ids = [&](int cg, Pass& P) {
+    int64_t* offc = P.off;
+    int64_t* vocc = P.voc;
     // Field metadata through the VECTOR path (wave index taken from the raw
     // thread id, not readfirstlane, so these are not scalar loads): issued
     // with the ids, no dependent K$-miss round trip on the critical path.
@@ -318,6 +321,11 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       }
     }
     if (cg == 0 && !coop && a.F > 0) load_dense();
+  };
+  auto issue_rows = [&](int cg, Pass& P, bool fetched) {
+    if (!fetched) fetch_ids(cg, P);
+    const int64_t* offc = P.off;
+    const int64_t* vocc = P.voc;
     RS_STAMP(6);
     // row gather: KV consecutive floats of the sample's row per lane
     int64_t row[MAXC];
@@ -394,18 +402,26 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   if (a.F == 0 || coop) load_dense();
   if (coop) __syncthreads();
   RS_STAMP(9);
+#ifndef RS_EARLY_IDS
+#define RS_EARLY_IDS 1
+#endif
   if (PRE) {
     if (has_pass(0)) {
-      issue_rows(0, P0);
+      // both passes' ids requested together: the second pass's id trip is
+      // not serialised behind the first pass's rows and MFMAs
+      fetch_ids(0, P0);
+      const bool two = has_pass(PS);
+      if (RS_EARLY_IDS && two) fetch_ids(PS, P1);
+      issue_rows(0, P0, true);
       norms(P0);
-      if (has_pass(PS)) norms(P1);
+      if (two) norms(P1);
       consume(0, P0);
-      if (has_pass(PS)) {
-        issue_rows(PS, P1);
+      if (two) {
+        issue_rows(PS, P1, RS_EARLY_IDS);
         consume(PS, P1);
         for (int cg = 2 * PS; has_pass(cg); cg += PS) {
           issue_b(cg, P0);
-          issue_rows(cg, P0);
+          issue_rows(cg, P0, false);
           norms(P0);
           consume(cg, P0);
         }
@@ -414,7 +430,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   } else {
     for (int cg = 0; has_pass(cg); cg += PS) {
       issue_b(cg, P0);
-      issue_rows(cg, P0);
+      issue_rows(cg, P0, false);
       norms(P0);
       consume(cg, P0);
     }
