@@ -412,6 +412,9 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       fetch_ids(0, P0);
       const bool two = has_pass(PS);
       if (RS_EARLY_IDS && two) fetch_ids(PS, P1);
+      // (the second pass's rows stay behind the first pass's MFMAs: issuing
+      // them with the first pass's was slower, 6.19 vs 5.82 us at 4096 —
+      // the r1 finding that two row bursts beat one, again)
       issue_rows(0, P0, true);
       norms(P0);
       if (two) norms(P1);
@@ -837,6 +840,7 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st, const FieldMe
   // pay at 4096 too (6.61 -> 6.39 us, profiles/r3_ab_kernarg_pf_4096.json);
   // above 512 tiles the device-metadata kernels stay faster (14.26 vs 13.48
   // us at 16384, 47.5 vs 42.6 at 65536; profiles/r3_ab_kernarg_allgrids_*)
+  // 16 waves (13: 6.20 us, 9: 6.78 vs 5.76 at 4096; profiles/r3_ab_kernarg_waves_4096.json)
   if (hm && a.F <= 32 && KIND != 3 && grid <= 512) {
     embed_fm_mfma_ka<KV, NT, 16, KIND, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
     return;
