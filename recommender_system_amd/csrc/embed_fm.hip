@@ -839,7 +839,8 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st, const FieldMe
   // with the ids loaded per wave, the first passes' B fragments beside them
   // pay at 4096 too (6.61 -> 6.39 us, profiles/r3_ab_kernarg_pf_4096.json);
   // above 512 tiles the device-metadata kernels stay faster (14.26 vs 13.48
-  // us at 16384, 47.5 vs 42.6 at 65536; profiles/r3_ab_kernarg_allgrids_*)
+  // us at 16384, 47.5 vs 42.6 at 65536, still 14.34 vs 13.54 / 47.8 vs 42.6
+  // with both passes' ids requested together; profiles/r3_ab_kernarg_*)
   // 16 waves (13: 6.20 us, 9: 6.78 vs 5.76 at 4096; profiles/r3_ab_kernarg_waves_4096.json)
   if (hm && a.F <= 32 && KIND != 3 && grid <= 512) {
     embed_fm_mfma_ka<KV, NT, 16, KIND, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
