@@ -408,7 +408,8 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   if (PRE) {
     if (has_pass(0)) {
       // both passes' ids requested together: the second pass's id trip is
-      // not serialised behind the first pass's rows and MFMAs
+      // not serialised behind the first pass's rows and MFMAs (after the B
+      // fragments: ids first was slower, 5.95 vs 5.75 us at 4096)
       fetch_ids(0, P0);
       const bool two = has_pass(PS);
       if (RS_EARLY_IDS && two) fetch_ids(PS, P1);
