@@ -492,6 +492,22 @@ int rs_dropout(float* x, int64_t ld, int64_t rows, int64_t cols, float rate,
  *  summed over duplicate rows in lookup order (stable sort + segmented sum:
  *  Keras' IndexedSlices scatter-add); workspace:
  *  rs_embedding_sgd_workspace_size(batch * n_fields) bytes.                 */
+/* rs_sort_pairs_u32: stable ascending sort of (key, val) pairs by the low
+ *  `bits` bits of key (LSD radix, 8 bits a pass; equal keys keep their input
+ *  order), the grouping step of every row-sparse scatter-add here
+ *  (rs_embedding_sgd, rs_fm_train_step, rs_shard_dedup_route beyond 4096
+ *  samples) — Keras' IndexedSlices accumulation groups the same rows
+ *  (utils/compile_fit.py:9-15 via SGD on the Embedding); in != out,
+ *  workspace: rs_sort_pairs_workspace_size(n) bytes.
+ * rs_inclusive_sum_i32: out[i] = in[0] + ... + in[i] (in == out allowed),
+ *  workspace: rs_inclusive_sum_workspace_size(n) bytes.                    */
+int64_t rs_sort_pairs_workspace_size(int64_t n);
+int rs_sort_pairs_u32(const uint32_t* key_in, const uint32_t* val_in,
+                      uint32_t* key_out, uint32_t* val_out, int64_t n,
+                      int bits, void* workspace, rs_stream_t stream);
+int64_t rs_inclusive_sum_workspace_size(int64_t n);
+int rs_inclusive_sum_i32(const int32_t* in, int32_t* out, int64_t n,
+                         void* workspace, rs_stream_t stream);
 int64_t rs_gemm_workspace_size(int64_t M, int64_t N, int64_t K);
 int rs_gemm(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
             float alpha, const float* A, int64_t lda, const float* B,

@@ -69,6 +69,10 @@ SIGNATURES = {
     "rs_shard_bucketize": (I, [P, I, L, P, P, I, L, L, I, P, P, P, P, P, P]),
     "rs_shard_slot_bucketize": (I, [P, I, L, P, P, I, L, L, I, I, P, P, P, P, P, P, P]),
     "rs_gather_rows": (I, [P, L, I, P, L, P, P, P]),
+    "rs_sort_pairs_workspace_size": (L, [L]),
+    "rs_sort_pairs_u32": (I, [P, P, P, P, L, I, P, P]),
+    "rs_inclusive_sum_workspace_size": (L, [L]),
+    "rs_inclusive_sum_i32": (I, [P, P, L, P, P]),
     "rs_unpermute_rows": (I, [P, P, I, L, P, P]),
     "rs_rows_fm_fwd": (I, [P, P, L, I, I, I, P, P, I, P, L, P]),
     "rs_cb_write": (I, [C.c_char_p, L, I, I, I, P, P, P, P, P]),

@@ -10,7 +10,7 @@
 //   z = 0.5 (FM(x) + DNN(x)),  p = sigmoid(z),  L = mean_b BCE(t_b, p_b)
 //   + l2(reg_w) |w1|^2 + l2(reg_b) |v|^2 (FMLayer.build); Dense layers and
 //   embeddings carry no regulariser; SGD(lr): w -= lr dL/dw.
-#include <hipcub/hipcub.hpp>
+#include "radix_sort.hpp"
 
 #include "rs_common.hpp"
 
@@ -990,12 +990,7 @@ extern "C" int rs_shard_owner_fm_grad(const int32_t* recv, int64_t rec_stride, i
   return launch_status("rs_shard_owner_fm_grad");
 }
 
-static int64_t emb_sort_bytes(int64_t n) {
-  size_t sb = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sb, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                           (uint32_t*)nullptr, (int)(n > 0 ? n : 1));
-  return (int64_t)sb;
-}
+static int64_t emb_sort_bytes(int64_t n) { return sort_pairs_ws_bytes(n); }
 
 extern "C" int64_t rs_embedding_sgd_workspace_size(int64_t n_lookups) {
   if (n_lookups < 0) return -1;
@@ -1029,9 +1024,7 @@ extern "C" int rs_embedding_sgd_strided(float* table, int64_t n_rows, int k, con
   // so it still sorts after every valid row
   int bits = 1;
   while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)n_rows) ++bits;
-  size_t sb = (size_t)emb_sort_bytes(n);
-  const hipError_t e = hipcub::DeviceRadixSort::SortPairs(ws + 5 * slab, sb, key_in, key_out, val_in, val_out, (int)n,
-                                                          0, bits, st);
+  const hipError_t e = sort_pairs_u32(key_in, val_in, key_out, val_out, n, bits, ws + 5 * slab, st);
   if (e != hipSuccess) {
     set_error("rs_embedding_sgd: radix sort failed: %s", hipGetErrorString(e));
     return RS_ERR_HIP;

@@ -19,8 +19,7 @@
 // its lookups (stable sort order = lookup order: deterministic) into its
 // send slot, so the reverse all-to-all carries one gradient row per distinct
 // row and owner.
-#include <hipcub/hipcub.hpp>
-
+#include "radix_sort.hpp"
 #include "rs_common.hpp"
 
 namespace rs {
@@ -37,13 +36,9 @@ static int64_t dd_al(int64_t x) { return (x + 255) / 256 * 256; }
 
 static DedupWs dedup_ws(int64_t n, int world) {
   DedupWs w{};
-  const int nn = (int)(n > 0 ? n : 1);
-  size_t sb = 0, cb = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sb, (uint32_t*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr,
-                                           (int32_t*)nullptr, nn);
-  (void)hipcub::DeviceScan::InclusiveSum(nullptr, cb, (int32_t*)nullptr, (int32_t*)nullptr, nn);
-  w.sort_bytes = sb;
-  w.scan_bytes = cb;
+  const int64_t sb = sort_pairs_ws_bytes(n), cb = scan_ws_bytes(n);
+  w.sort_bytes = (size_t)sb;
+  w.scan_bytes = (size_t)cb;
   int64_t o = 0;
   w.key_in = o; o = dd_al(o + n * 4);
   w.key_out = o; o = dd_al(o + n * 4);
@@ -704,11 +699,11 @@ extern "C" int rs_shard_dedup_route(const void* ids, int id_kind, int64_t id_str
   const uint64_t rows = (uint64_t)world * (uint64_t)rows_per_rank;
   int bits = 1;
   while (bits < 32 && ((uint64_t)1 << bits) <= rows) ++bits;
-  size_t sb = w.sort_bytes, cb = w.scan_bytes;
-  e = hipcub::DeviceRadixSort::SortPairs(ws + w.sort, sb, key_in, key_out, val_in, val_out, (int)n, 0, bits, st);
+  e = sort_pairs_u32(key_in, reinterpret_cast<const uint32_t*>(val_in), key_out, reinterpret_cast<uint32_t*>(val_out),
+                     n, bits, ws + w.sort, st);
   if (e == hipSuccess) {
     dedup_heads<<<g, 256, 0, st>>>(key_out, n, head);
-    e = hipcub::DeviceScan::InclusiveSum(ws + w.scan, cb, head, incl, (int)n, st);
+    e = inclusive_sum_i32(head, incl, n, ws + w.scan, st);
   }
   if (e != hipSuccess) {
     set_error("rs_shard_dedup_route: sort/scan failed: %s", hipGetErrorString(e));

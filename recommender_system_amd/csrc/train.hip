@@ -22,11 +22,10 @@
 //   w1  -= lr * (G1 + 2 lw w1),   v -= lr * (Gv + 2 lv v)       (every row)
 // The decay touches every row (as Keras' dense regulariser gradient does);
 // G is non-zero only on the nd dense rows and the rows the batch looked up.
-// Sparse rows: per-lookup contributions are sorted by row (hipCUB radix sort,
-// stable) and each row's contributions are summed in lookup order, in chunk
+// Sparse rows: per-lookup contributions are sorted by row (the hand-written
+// stable radix sort, radix_sort.hip) and each row's contributions are summed in lookup order, in chunk
 // pieces added in chunk order, so the result is bitwise reproducible.
-#include <hipcub/hipcub.hpp>
-
+#include "radix_sort.hpp"
 #include "rs_common.hpp"
 
 namespace rs {
@@ -359,10 +358,8 @@ static int64_t al256(int64_t x) { return (x + 255) / 256 * 256; }
 static TrainWs train_ws(int64_t batch, int n_fields, int k, int nd) {
   TrainWs w{};
   const int64_t n = batch * n_fields;
-  size_t sb = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sb, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                           (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(n > 0 ? n : 1));
-  w.sort_bytes = sb;
+  const int64_t sb = sort_pairs_ws_bytes(n);
+  w.sort_bytes = (size_t)sb;
   int64_t o = 0;
   w.g = o; o = al256(o + batch * 4);
   w.s = o; o = al256(o + batch * k * 4);
@@ -424,9 +421,7 @@ extern "C" int rs_fm_train_step(const void* ids, int id_kind, int64_t id_stride,
   if (n > 0) {
     int bits = 1;
     while (bits < 32 && ((uint64_t)1 << bits) < (uint64_t)n_rows) ++bits;
-    size_t sb = w.sort_bytes;
-    const hipError_t e = hipcub::DeviceRadixSort::SortPairs(ws + w.sort, sb, a.key_in, a.key_out, a.val_in,
-                                                            a.val_out, (int)n, 0, bits, st);
+    const hipError_t e = sort_pairs_u32(a.key_in, a.val_in, a.key_out, a.val_out, n, bits, ws + w.sort, st);
     if (e != hipSuccess) {
       set_error("rs_fm_train_step: radix sort failed: %s", hipGetErrorString(e));
       return RS_ERR_HIP;
