@@ -69,7 +69,11 @@ enum rs_option {
                                  1 = VALU/DPP persistent 8-sample tiles, 2 / 3 = MFMA persistent
                                  16-sample tiles (2 / 1 resident per CU); shapes a kernel does not
                                  cover run the K-split one.  See DESIGN.md 4.1                    */
-  RS_OPT_COUNT = 1
+  RS_OPT_MLP_UNROLL = 1,      /* fused MLP towers (rs_mlp_fwd, rs_deepfm_fwd, rs_dcn_fwd): 1 (the
+                                 default) = the k-group loop of the common layer widths fully
+                                 unrolled (no loop-head wait on the weight ring), 0 = the looped
+                                 form.  See DESIGN.md 4.5                                         */
+  RS_OPT_COUNT = 2
 };
 
 /* ------------------------------------------------------------------ meta */

@@ -67,6 +67,7 @@ struct MlpArgs {
   float c0, c1;
   int64_t M;
   unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_mlp_set_dbg)
+  int unroll;               // RS_OPT_MLP_UNROLL at launch
 };
 #define MLP_STAMP(i)                                                                              \
   do {                                                                                            \
@@ -159,9 +160,46 @@ __device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[MLP_R], const float* _
 #endif
 }
 
+// The same contraction over exactly N k-groups, fully unrolled: straight-line
+// code, so the compiler waits on each ring slot's own load (vmcnt(D-1)-style)
+// instead of draining the ring at a loop head (the looped form's back-edge
+// gets a full vmcnt(0) every D groups).
+template <int N, int D>
+__device__ __forceinline__ void mlp_mac_u(floatx4 (&ring)[MLP_R], const float* __restrict__ ap,
+                                          const floatx4* __restrict__ bp, int g0, floatx4& acc) {
+  static_assert(N % D == 0 && D <= MLP_R, "unrolled contraction: D | N, D <= ring");
+  const int g1 = g0 + N;
+  floatx4 an = *reinterpret_cast<const floatx4*>(ap + 16 * g0);
+#pragma unroll
+  for (int i = 0; i < N; i += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int g = g0 + i;
+      const floatx4 av = an;
+      an = *reinterpret_cast<const floatx4*>(ap + 16 * min(g + u + 1, g1 - 1));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = mfma16x16x4(av[j], ring[u][j], acc);
+      ring[u] = bp[(int64_t)min(g + u + D, g1 - 1) * 64];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
 __device__ __forceinline__ void mlp_mac(floatx4 (&ring)[MLP_R], const float* ap, const floatx4* bp, int g0, int g1,
-                                        floatx4& acc) {
+                                        floatx4& acc, int unroll = 0) {
   const int n = g1 - g0;  // wave-uniform
+  if (unroll) {  // the DeepFM / DCN tower widths (429|432 -> 256 -> 128 -> 64 -> head)
+    switch (n) {
+      // ring depth by the ring's size (MLP_RING >= 9: 9 / 8 / 8 / 4 groups ahead)
+      case 27: return mlp_mac_u<27, (MLP_R >= 9 ? 9 : 3)>(ring, ap, bp, g0, acc);
+      case 16: return mlp_mac_u<16, (MLP_R >= 9 ? 8 : 2)>(ring, ap, bp, g0, acc);
+      case 8: return mlp_mac_u<8, (MLP_R >= 9 ? 8 : 2)>(ring, ap, bp, g0, acc);
+      case 4: return mlp_mac_u<4, (MLP_R >= 9 ? 4 : 2)>(ring, ap, bp, g0, acc);
+      case 1: return mlp_mac_u<1, 1>(ring, ap, bp, g0, acc);
+      default: break;
+    }
+  }
   if constexpr (MLP_R >= 9) {
     if (n % 9 == 0) return mlp_mac_d<9>(ring, ap, bp, g0, g1, acc);
     if (n % 8 == 0) return mlp_mac_d<8>(ring, ap, bp, g0, g1, acc);
@@ -224,7 +262,7 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
       const floatx4* bp = W + (int64_t)it.t * G * 64;
       if (item != w) mlp_ring_fill(ring, bp, it.g0, it.g1);
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-      mlp_mac(ring, ap, bp, it.g0, it.g1, acc);
+      mlp_mac(ring, ap, bp, it.g0, it.g1, acc, a.unroll);
       if (S == 1) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) finish(4 * (lane >> 4) + r, 16 * it.t + (lane & 15), acc[r]);
@@ -291,6 +329,7 @@ inline bool mlp_fill_args(const MlpGeom& g, const int* acts, const float* prepar
   a.L = g.L;
   a.K0 = g.K[0];
   a.rs = g.rs;
+  a.unroll = opt(RS_OPT_MLP_UNROLL);
   return true;
 }
 

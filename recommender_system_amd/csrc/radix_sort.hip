@@ -5,30 +5,38 @@
 // so the sort must be stable), and the dedup route's large-batch path numbers
 // distinct rows by a scan of segment heads.
 //
-// One pass per 8 key bits, three launches each:
-//   radix_hist     one workgroup per 4096-pair tile: digit counts in LDS
-//                  (order-free atomics), written digit-major hist[d][tile];
-//   radix_scan     one workgroup: exclusive scan of hist in place (digit-major
-//                  order = every tile's start for each digit, tiles in order);
-//   radix_scatter  the tile again: each pair's rank among equal digits in tile
-//                  order — per 64-lane batch the lanes with the same digit are
-//                  found by 8 ballots (no LDS atomics, so the rank is the
-//                  pair's position, not an arrival order), wave-private digit
-//                  counters carry the rank across a wave's batches and a sum
-//                  over the earlier waves' counters across waves.
-// Tile order inside a workgroup: pair e = (wave * 16 + r) * 64 + lane, the
-// 16 r-batches of a wave consecutive, so loads are coalesced and the rank
-// order is the input order.  Bytes per pass: 8 B read twice + 8 B written per
-// pair (HBM-bound work; a pass over the 106,496 lookups of a B 4096 x 26
-// batch is ~2.6 MB).
+// One pass per 8 key bits, over tiles of 256 threads x RX_ITEMS pairs, three
+// launches a pass:
+//   radix_hist      the tile's digit counts in LDS (order-free atomics),
+//                   written digit-major hist[d][tile];
+//   radix_row_scan  one workgroup per digit scans its row in place (tiles in
+//                   order) and writes the row total;
+//   radix_scatter   the tile's start for each digit (the row totals scanned
+//                   over the 256 digits in the workgroup + the tile's row
+//                   prefix), then each pair's rank among equal digits in tile
+//                   order: per 64-lane batch the lanes with the same digit are
+//                   found by 8 ballots (no LDS atomics, so the rank is the
+//                   pair's position, not an arrival order), wave-private digit
+//                   counters carry the rank across a wave's batches and a sum
+//                   over the earlier waves' counters across waves.
+// Tile order inside a workgroup: pair e = (wave * RX_ITEMS + r) * 64 + lane,
+// a wave's batches consecutive, so loads are coalesced and the rank order is
+// the input order.  Bytes per pass: 8 B read twice + 8 B written per pair
+// (HBM-bound integer work; ~2.6 MB a pass for the 106,496 lookups of a B 4096
+// x 26 batch).  Tile size and the row-scan split were chosen by
+// scripts/ab_sort.py against hipCUB on one box (profiles/r3_ab_sort.jsonl):
+// 52 vs 51 us at 106,496 pairs, 134 vs 143 us at 1,703,936.
 #include "radix_sort.hpp"
 #include "rs_common.hpp"
 
 namespace rs {
 
 constexpr int RX_T = 256;              // threads per workgroup
-constexpr int RX_R = 16;               // pairs per lane
-constexpr int RX_TILE = RX_T * RX_R;   // 4096 pairs per tile
+#ifndef RX_ITEMS
+#define RX_ITEMS 8
+#endif
+constexpr int RX_R = RX_ITEMS;         // pairs per lane
+constexpr int RX_TILE = RX_T * RX_R;   // pairs per tile
 constexpr int RX_D = 8;                // digit bits
 constexpr int RX_ND = 1 << RX_D;       // digits
 
@@ -104,12 +112,44 @@ __global__ __launch_bounds__(1024) void rx_scan_one(T* __restrict__ a, const T* 
   if (carry_out && threadIdx.x == 0) carry_out[0] = (T)total;
 }
 
+// many tiles: one workgroup per digit scans its row of the count table in
+// place (exclusive, tiles in order) and writes the row total; the scatter
+// then adds the totals of the digits below (its own 256-entry scan)
+__global__ __launch_bounds__(RX_T) void radix_row_scan(uint32_t* __restrict__ hist, int64_t ntile,
+                                                       uint32_t* __restrict__ rowsum) {
+  __shared__ uint32_t red[RX_T / 64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t* row = hist + (int64_t)blockIdx.x * ntile;
+  const int64_t per = (ntile + RX_T - 1) / RX_T;
+  const int64_t lo = (int64_t)t * per, hi = lo + per < ntile ? lo + per : ntile;
+  uint32_t s = 0;
+  for (int64_t i = lo; i < hi; ++i) s += row[i];
+  uint32_t inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) red[w] = inc;
+  __syncthreads();
+  uint32_t run = inc - s;
+  for (int ww = 0; ww < w; ++ww) run += red[ww];
+  for (int64_t i = lo; i < hi; ++i) {
+    const uint32_t x = row[i];
+    row[i] = run;
+    run += x;
+  }
+  if (t == RX_T - 1) rowsum[blockIdx.x] = run;
+}
+
 __global__ __launch_bounds__(RX_T) void radix_scatter(const uint32_t* __restrict__ kin,
                                                       const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
                                                       uint32_t* __restrict__ vout, int64_t n, int shift,
-                                                      const uint32_t* __restrict__ hist, int64_t ntile) {
+                                                      const uint32_t* __restrict__ hist, int64_t ntile,
+                                                      const uint32_t* __restrict__ rowsum) {
   __shared__ uint32_t cnt[RX_T / 64][RX_ND];
   __shared__ uint32_t gb[RX_ND];
+  __shared__ uint32_t red[RX_T / 64];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint32_t k[RX_R], v[RX_R];
   int dg[RX_R];
@@ -122,7 +162,25 @@ __global__ __launch_bounds__(RX_T) void radix_scatter(const uint32_t* __restrict
     dg[r] = ok ? (int)((k[r] >> shift) & (RX_ND - 1)) : RX_ND;
   }
   for (int i = t; i < (RX_T / 64) * RX_ND; i += RX_T) (&cnt[0][0])[i] = 0;
-  for (int d = t; d < RX_ND; d += RX_T) gb[d] = hist[(int64_t)d * ntile + blockIdx.x];
+  {
+    // thread d: digit d's total over all tiles (rowsum) and its count over
+    // the tiles before this one (the scanned row); the tile's start = (totals
+    // of the digits below d) + that prefix
+    static_assert(RX_T == RX_ND, "one thread per digit");
+    const uint32_t tot = rowsum[t];
+    const uint32_t pre = hist[(int64_t)t * ntile + blockIdx.x];
+    uint32_t inc = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) red[w] = inc;
+    __syncthreads();
+    uint32_t below = inc - tot;
+    for (int ww = 0; ww < w; ++ww) below += red[ww];
+    gb[t] = below + pre;
+  }
   __syncthreads();
   // rank inside the wave: lanes with the same digit (and present) in batch r
   int occ[RX_R];
@@ -157,13 +215,14 @@ __global__ __launch_bounds__(RX_T) void radix_scatter(const uint32_t* __restrict
 }
 
 struct RxWs {
-  int64_t hist, tk, tv, total;
+  int64_t hist, rowsum, tk, tv, total;
 };
 static RxWs rx_ws(int64_t n) {
   RxWs w{};
   const int64_t ntile = (n + RX_TILE - 1) / RX_TILE;
   int64_t o = 0;
   w.hist = o; o = rx_al(o + ntile * RX_ND * 4);
+  w.rowsum = o; o = rx_al(o + RX_ND * 4);
   w.tk = o; o = rx_al(o + n * 4);
   w.tv = o; o = rx_al(o + n * 4);
   w.total = o;
@@ -180,6 +239,7 @@ hipError_t sort_pairs_u32(const uint32_t* key_in, const uint32_t* val_in, uint32
   const RxWs w = rx_ws(n);
   uint8_t* base = static_cast<uint8_t*>(ws);
   uint32_t* hist = reinterpret_cast<uint32_t*>(base + w.hist);
+  uint32_t* rowsum = reinterpret_cast<uint32_t*>(base + w.rowsum);
   uint32_t* tk = reinterpret_cast<uint32_t*>(base + w.tk);
   uint32_t* tv = reinterpret_cast<uint32_t*>(base + w.tv);
   const int64_t ntile = (n + RX_TILE - 1) / RX_TILE;
@@ -193,8 +253,8 @@ hipError_t sort_pairs_u32(const uint32_t* key_in, const uint32_t* val_in, uint32
     uint32_t* dk = to_out ? key_out : tk;
     uint32_t* dv = to_out ? val_out : tv;
     radix_hist<<<(unsigned)ntile, RX_T, 0, st>>>(sk, n, p * RX_D, hist, ntile);
-    rx_scan_one<true, uint32_t><<<1, 1024, 0, st>>>(hist, hist, ntile * RX_ND, nullptr);
-    radix_scatter<<<(unsigned)ntile, RX_T, 0, st>>>(sk, sv, dk, dv, n, p * RX_D, hist, ntile);
+    radix_row_scan<<<RX_ND, RX_T, 0, st>>>(hist, ntile, rowsum);
+    radix_scatter<<<(unsigned)ntile, RX_T, 0, st>>>(sk, sv, dk, dv, n, p * RX_D, hist, ntile, rowsum);
     sk = dk;
     sv = dv;
   }

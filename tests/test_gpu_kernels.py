@@ -455,12 +455,22 @@ def _tower_ref(x, layers):
     return x
 
 
+# the fused towers' k-group contraction (RS_OPT_MLP_UNROLL): 0 = looped,
+# 1 = fully unrolled for the common layer widths (27 / 16 / 8 / 4 / 1 groups)
+@pytest.fixture(params=[0, 1])
+def mlp_unroll(request, gpu):
+    from recommender_system_amd import _lib
+    prev = _lib.set_option(_lib.OPT_MLP_UNROLL, request.param)
+    yield request.param
+    _lib.set_option(_lib.OPT_MLP_UNROLL, prev)
+
+
 @pytest.mark.parametrize("M,K,hidden,out,act", [(4096, 429, [256, 128, 64], 1, "relu"),
                                                 (1000, 741, [256, 128, 64], 1, "relu"),
                                                 (37, 37, [50, 3], 7, "prelu"),
                                                 (1, 1024, [1024], 16, "relu"),
                                                 (130, 20, [16, 16, 16, 16, 16, 16, 16], 2, "sigmoid")])
-def test_dnn_tower(gpu, M, K, hidden, out, act):
+def test_dnn_tower(gpu, mlp_unroll, M, K, hidden, out, act):
     from recommender_system_amd import DNNLayer
     rng = np.random.default_rng(M + K)
     x = torch.tensor(rng.standard_normal((M, K)).astype(np.float32), device="cuda")
@@ -522,7 +532,7 @@ def test_dnn_tower_head_strided_and_permuted(gpu):
 # ----------------------------------------------- fused DeepFM (rs_deepfm_fwd)
 @pytest.mark.parametrize("k,B,id_dtype,hidden", [(16, 4096, np.int32, [256, 128, 64]), (8, 1000, np.int64, [256, 128, 64]),
                                                  (16, 33, np.int32, [40, 24]), (8, 1, np.int64, [16])])
-def test_deepfm_fused(gpu, k, B, id_dtype, hidden):
+def test_deepfm_fused(gpu, mlp_unroll, k, B, id_dtype, hidden):
     """One-launch DeepFM == two-launch path == fp64 oracle; the optional FM
     logit output matches the standalone FM kernel."""
     from recommender_system_amd import DeepFM
@@ -706,7 +716,7 @@ def test_pnn_modes_fused(gpu, mode, k, B, id_dtype):
                                                            (8, 2, [40, 24], 3, 37, np.int64),
                                                            (4, 0, [16], 1, 5, np.int32),
                                                            (16, 20, [32], 2, 100, np.int64)])
-def test_dcn_fused(gpu, k, L, hidden, out_dim, B, id_dtype):
+def test_dcn_fused(gpu, mlp_unroll, k, L, hidden, out_dim, B, id_dtype):
     """One-launch DCN == the layer-by-layer path == the fp64 oracle."""
     from recommender_system_amd import DCN
     from tests.helpers import criteo_columns, dnn_params, tables_of

@@ -37,6 +37,7 @@ def _expect(keys, vals, bits):
     (1, 1, 2), (63, 7, 100), (4095, 12, 4000), (4096, 16, 60000), (4097, 20, 1 << 20),
     (106_496, 25, 26_000_000),      # one B 4096 x 26 batch of lookups, 26 x 1e6 rows
     (300_001, 32, 1 << 32),         # full-width keys, ragged last tile
+    (1_703_936, 25, 26_000_000),    # B 65536 x 26: the scan-launch path (many tiles)
     (50_000, 9, 3),                 # very few distinct keys: long equal runs, stability
 ])
 def test_sort_pairs_matches_stable_argsort(gpu, n, bits, span):
