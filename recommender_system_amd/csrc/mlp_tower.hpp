@@ -91,8 +91,11 @@ struct MlpItem {
 // k-slices per output tile: layers with >= 4 tiles keep whole columns per
 // wave (no partial-sum exchange: measured faster than filling all 16 waves);
 // narrow layers (the 64->1 head) split K over the idle waves.
+#ifndef MLP_SPLIT_T
+#define MLP_SPLIT_T 4  // layers with fewer output tiles than this split K over the idle waves
+#endif
 __device__ __forceinline__ int mlp_slices(int T, int G, int NW) {
-  if (T >= 4) return 1;
+  if (T >= MLP_SPLIT_T) return 1;
   const int S = NW / T;
   return S < 1 ? 1 : (S > G ? G : S);
 }
@@ -196,6 +199,7 @@ __device__ __forceinline__ void mlp_mac(floatx4 (&ring)[MLP_R], const float* ap,
       case 16: return mlp_mac_u<16, (MLP_R >= 9 ? 8 : 2)>(ring, ap, bp, g0, acc);
       case 8: return mlp_mac_u<8, (MLP_R >= 9 ? 8 : 2)>(ring, ap, bp, g0, acc);
       case 4: return mlp_mac_u<4, (MLP_R >= 9 ? 4 : 2)>(ring, ap, bp, g0, acc);
+      case 2: return mlp_mac_u<2, 2>(ring, ap, bp, g0, acc);
       case 1: return mlp_mac_u<1, 1>(ring, ap, bp, g0, acc);
       default: break;
     }

@@ -1,5 +1,5 @@
 """Fixed-count launches for PMC collection (run under rocprofv3 --pmc):
-  * rs_embed_fm_fwd at the headline shape (B=4096, 26 x 1e7 x 16, int32 ids),
+  * rs_embed_fm_fwd_hm (the bench's entry) at the headline shape (B=4096, 26 x 1e7 x 16, int32 ids),
     50 launches over a pool of 16 batches;
   * the calibration probe (diagnostic library): random 64-B rows and line
     pairs, known byte counts (1,703,936 rows x 64 B, + 8-B row indices).
@@ -30,11 +30,14 @@ pool = [torch.randint(0, V, (B, F), dtype=torch.int32, device=dev) for _ in rang
 dense = torch.rand(B, nd, device=dev)
 logit = torch.empty(B, device=dev)
 torch.cuda.synchronize()
+hoff = (C.c_int64 * F)(*[c * V for c in range(F)])
+hvoc = (C.c_int64 * F)(*([V] * F))
 for i in range(128):  # 64-batch rotation as in bench.py: rows not MALL-resident between uses
     ids = pool[i % 64]
-    _lib.call("rs_embed_fm_fwd", ids.data_ptr(), 0, F, dense.data_ptr(), nd, nd, table.data_ptr(), offs.data_ptr(),
-              voc.data_ptr(), F, k, prep.data_ptr(), w0.data_ptr(), kfm, logit.data_ptr(), None, B, None,
-              _lib.stream())
+    # the bench's entry (field metadata as kernel arguments: embed_fm_mfma_ka)
+    _lib.call("rs_embed_fm_fwd_hm", ids.data_ptr(), 0, F, dense.data_ptr(), nd, nd, table.data_ptr(),
+              offs.data_ptr(), voc.data_ptr(), C.addressof(hoff), C.addressof(hvoc), F, k, prep.data_ptr(),
+              w0.data_ptr(), kfm, logit.data_ptr(), None, B, None, _lib.stream())
 torch.cuda.synchronize()
 diag = os.path.join(ROOT, "recommender_system_amd", "librs_hip_diag.so")
 if os.path.exists(diag):
