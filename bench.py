@@ -72,6 +72,21 @@ def _dist_setup(args):
     return world, rank
 
 
+def _host_wait_mode(mode):
+    """How the host waits for the device (hipSetDeviceFlags, before the device
+    is first used): '' = the runtime's default, 'spin' = busy-wait
+    (hipDeviceScheduleSpin), 'yield' = hipDeviceScheduleYield.  Diagnostic
+    A/B of the synchronisation latency inside the timed region."""
+    flags = {"": None, "spin": 1, "yield": 2}[mode]
+    if flags is None:
+        return
+    import ctypes
+    with open("/proc/self/maps") as f:  # the HIP runtime torch loaded
+        path = next(l.split()[-1] for l in f if "libamdhip64.so" in l)
+    rc = ctypes.CDLL(path).hipSetDeviceFlags(ctypes.c_uint(flags))
+    print(f"bench: hipSetDeviceFlags({flags}) -> {rc}", file=sys.stderr)
+
+
 def _barrier(world):
     if world > 1 or _dist_on():
         import torch.distributed as dist
@@ -1492,6 +1507,7 @@ def main():
     ap.add_argument("--sharded", action="store_true",
                     help="time the row-sharded exchange path even at world 1 (N=1 point of the sharded curve)")
     args = ap.parse_args()
+    _host_wait_mode(os.environ.get("RS_BENCH_SYNC", ""))
     world, rank = _dist_setup(args)
     other = {"dcn": bench_dcn, "din": bench_din, "pnn": bench_pnn, "nfm": bench_nfm, "afm": bench_afm,
              "ffm": bench_ffm, "io": bench_io, "fm_train": bench_fm_train}
