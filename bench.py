@@ -74,12 +74,14 @@ def _dist_setup(args):
 
 def _host_wait_mode(mode):
     """How the host waits for the device (hipSetDeviceFlags, before the device
-    is first used): '' = the runtime's default, 'spin' = busy-wait
-    (hipDeviceScheduleSpin), 'yield' = hipDeviceScheduleYield.  Diagnostic
-    A/B of the synchronisation latency inside the timed region."""
-    flags = {"": None, "spin": 1, "yield": 2}[mode]
-    if flags is None:
-        return
+    is first used; RS_BENCH_SYNC): 'spin' (the default) = busy-wait
+    (hipDeviceScheduleSpin), as a latency-bound serving loop would set it;
+    'default' = the runtime's own choice; 'yield' = hipDeviceScheduleYield.
+    The synchronisations around the timed region return sooner: +3 % on the
+    20-step line (profiles/r3_sync_mode_ab.jsonl)."""
+    flags = {"": None, "default": None, "spin": 1, "yield": 2}[mode]
+    if flags is None or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return  # multi-rank runs keep the runtime's default (the flag is per device, set before its first use)
     import ctypes
     with open("/proc/self/maps") as f:  # the HIP runtime torch loaded
         path = next(l.split()[-1] for l in f if "libamdhip64.so" in l)
@@ -1507,7 +1509,7 @@ def main():
     ap.add_argument("--sharded", action="store_true",
                     help="time the row-sharded exchange path even at world 1 (N=1 point of the sharded curve)")
     args = ap.parse_args()
-    _host_wait_mode(os.environ.get("RS_BENCH_SYNC", ""))
+    _host_wait_mode(os.environ.get("RS_BENCH_SYNC", "spin"))
     world, rank = _dist_setup(args)
     other = {"dcn": bench_dcn, "din": bench_din, "pnn": bench_pnn, "nfm": bench_nfm, "afm": bench_afm,
              "ffm": bench_ffm, "io": bench_io, "fm_train": bench_fm_train}
@@ -1543,6 +1545,7 @@ def main():
                         "value_kind": (f"{res.get('value_kind')}: the faster of the per-batch forward and the "
                                        "pipelined stream (both nested below)")}),
             "roofline": res["roofline"], "cpu_baseline": res["cpu_baseline"],
+            "host_wait": os.environ.get("RS_BENCH_SYNC", "spin") if world == 1 else "default",
         }
         for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "config5_n1", "pipelined", "per_batch",
                     "exchange", "train_step", "fm_hotpath_sharded", "world1_no_exchange"):
