@@ -167,6 +167,9 @@ __device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[MLP_R], const float* _
 // code, so the compiler waits on each ring slot's own load (vmcnt(D-1)-style)
 // instead of draining the ring at a loop head (the looped form's back-edge
 // gets a full vmcnt(0) every D groups).
+#ifndef MLP_SMALL_D
+#define MLP_SMALL_D 2  // groups ahead in the 16 / 8 / 4-group layers (a divisor of 4, <= MLP_RING)
+#endif
 template <int N, int D>
 __device__ __forceinline__ void mlp_mac_u(floatx4 (&ring)[MLP_R], const float* __restrict__ ap,
                                           const floatx4* __restrict__ bp, int g0, floatx4& acc) {
@@ -196,9 +199,9 @@ __device__ __forceinline__ void mlp_mac(floatx4 (&ring)[MLP_R], const float* ap,
     switch (n) {
       // ring depth by the ring's size (MLP_RING >= 9: 9 / 8 / 8 / 4 groups ahead)
       case 27: return mlp_mac_u<27, (MLP_R >= 9 ? 9 : 3)>(ring, ap, bp, g0, acc);
-      case 16: return mlp_mac_u<16, (MLP_R >= 9 ? 8 : 2)>(ring, ap, bp, g0, acc);
-      case 8: return mlp_mac_u<8, (MLP_R >= 9 ? 8 : 2)>(ring, ap, bp, g0, acc);
-      case 4: return mlp_mac_u<4, (MLP_R >= 9 ? 4 : 2)>(ring, ap, bp, g0, acc);
+      case 16: return mlp_mac_u<16, (MLP_R >= 9 ? 8 : MLP_SMALL_D)>(ring, ap, bp, g0, acc);
+      case 8: return mlp_mac_u<8, (MLP_R >= 9 ? 8 : MLP_SMALL_D)>(ring, ap, bp, g0, acc);
+      case 4: return mlp_mac_u<4, (MLP_R >= 9 ? 4 : MLP_SMALL_D)>(ring, ap, bp, g0, acc);
       case 2: return mlp_mac_u<2, 2>(ring, ap, bp, g0, acc);
       case 1: return mlp_mac_u<1, 1>(ring, ap, bp, g0, acc);
       default: break;

@@ -25,7 +25,7 @@ def main():
     bs = [(torch.rand(dims[i + 1], generator=g) * 0.1).to(dev) for i in range(n)]
     NP = 64
     x = torch.rand(NP, B, dims[0], device=dev)
-    names = [v for v in "ABC" if os.path.exists(os.path.join(ROOT, "scripts", "ab", f"librs_tower_{v}.so"))]
+    names = [v for v in "ABCD" if os.path.exists(os.path.join(ROOT, "scripts", "ab", f"librs_tower_{v}.so"))]
     graphs, outs, res = {}, {}, {}
     for name in names:
         lib = C.CDLL(os.path.join(ROOT, "scripts", "ab", f"librs_tower_{name}.so"))
