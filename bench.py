@@ -9,13 +9,16 @@ Default (N=1) workload — the configuration the metric is quoted on:
   one rs_embed_fm_fwd launch over one batch.
 
   N>1 (driver: torch.distributed.run, one rank per GPU) and --sharded at
-  N=1: BASELINE config 5 — the full DeepFM forward with ONE 1e8-row table
-  (26 x 3,846,154 x 16 fp32) row-sharded over the ranks
-  (recommender_system_amd/sharded.py ShardedDeepFM: RCCL all-to-all of row
-  ids and of rows, then the fused DeepFM kernel from the exchange buffer),
-  4096 local samples per rank (weak scaling).  value = N*4096 /
-  max-over-ranks step time.  The headline hot path sharded the same way
-  (26 x 1e7 table, FM partial protocol) is nested as `fm_hotpath_sharded`.
+  N=1: the SAME workload (26 x 1e7 x 16 table, embed + FM logit, 4096 local
+  samples per rank: weak scaling) with the table row-sharded over the ranks
+  (recommender_system_amd/sharded.py ShardedEmbeddingFM, pipelined partial
+  protocol: per batch one RCCL all-to-all of [row ids | FM partials] records
+  + one rs_shard_fm_pipe launch).  value = N*4096 / max-over-ranks step
+  time; its roofline is the pipe kernel's (per-rank algorithmic bytes, the
+  exchange records listed separately).  BASELINE config 5 (the DeepFM
+  forward on a 1e8-row table, row-sharded, RCCL all-to-all of row ids and of
+  rows, then the fused DeepFM kernel) is nested as `config5` (at N=1:
+  `config5_n1`).
 
 Also measured (nested in the JSON line, not `value`):
   * `roofline`: the fused gather+FM kernel's algorithmic bytes per launch
@@ -228,6 +231,71 @@ def _timed_graph_streams(fn, steps, n_streams, world):
     return _max_over_ranks(time.perf_counter() - t0, world)
 
 
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _device_state():
+    """Clocks, power and temperature of the GPU this rank runs on, read from
+    sysfs in-process (no exec): the DRM card whose PCI address matches torch's
+    current device.  `sclk` / `mclk` = the active DPM level (the line marked
+    '*'); power in W, temperature in C.  Box-to-box spread in the numbers
+     is read against these."""
+    import glob
+    st = {}
+    try:
+        p = torch.cuda.get_device_properties(torch.cuda.current_device())
+        want = "%04x:%02x:%02x" % (getattr(p, "pci_domain_id", 0), p.pci_bus_id, p.pci_device_id)
+    except Exception as e:  # noqa: BLE001 - the state is informative only
+        return {"error": f"{type(e).__name__}: {e}"[:120]}
+    for dev in sorted(glob.glob("/sys/class/drm/card[0-9]*/device")):
+        if not os.path.basename(os.path.realpath(dev)).startswith(want):
+            continue
+        st["card"] = os.path.basename(os.path.dirname(dev))
+        st["pci"] = os.path.basename(os.path.realpath(dev))
+        for key, name in (("sclk", "pp_dpm_sclk"), ("mclk", "pp_dpm_mclk"), ("fclk", "pp_dpm_fclk")):
+            txt = _read(os.path.join(dev, name))
+            if txt:
+                act = [l.split(":", 1)[1].replace("*", "").strip() for l in txt.splitlines() if "*" in l]
+                st[key] = act[0] if act else None
+                st[key + "_levels"] = len(txt.splitlines())
+        st["perf_level"] = _read(os.path.join(dev, "power_dpm_force_performance_level"))
+        st["busy_percent"] = _read(os.path.join(dev, "gpu_busy_percent"))
+        for hw in glob.glob(os.path.join(dev, "hwmon", "hwmon*")):
+            for key, name, scale in (("power_cap_W", "power1_cap", 1e-6), ("power_avg_W", "power1_average", 1e-6),
+                                     ("power_W", "power1_input", 1e-6), ("sclk_MHz", "freq1_input", 1e-6),
+                                     ("mclk_MHz", "freq2_input", 1e-6), ("temp_edge_C", "temp1_input", 1e-3),
+                                     ("temp_hotspot_C", "temp2_input", 1e-3), ("temp_mem_C", "temp3_input", 1e-3)):
+                v = _read(os.path.join(hw, name))
+                if v is not None:
+                    try:
+                        st[key] = round(int(v) * scale, 1)
+                    except ValueError:
+                        pass
+        break
+    if not st:
+        st["note"] = f"no /sys/class/drm card with PCI address {want}"
+    return st
+
+
+def _empty_kernel_slot(world):
+    """Per-launch slot time of an empty 256 x 256 kernel replayed back to back
+    from a hipGraph (dispatch + end of kernel + barrier: the box's floor under
+    every graph-replayed step), in us."""
+    from recommender_system_amd import _lib
+    lib = _lib.lib()
+
+    def step(i):
+        _lib.check(lib.rs_diag_empty(256, 256, _lib.stream()), "rs_diag_empty")
+
+    _, slot = _timed_graph(step, 256, 8, world, chunk=64)
+    return round(slot * 1e3, 3)
+
+
 def _pool(B, vocabs, nd, n_pool, device, dtype=torch.int32):
     g = torch.Generator(device=device)
     g.manual_seed(SEED)
@@ -407,14 +475,27 @@ def bench_hotpath(args, world, rank):
             _world1_group()
             c5, _ = bench_sharded_deepfm(args, 1, 0, lite=True)
             c5["note"] = ("BASELINE config 5 at N = 1: ShardedDeepFM forward on the 1e8-row table with the row "
-                          "exchange forced through RCCL (self-exchange), B 4096 - the workload of the N > 1 lines")
+                          "exchange forced through RCCL (self-exchange), B 4096 - the config5 field of the N > 1 "
+                          "lines")
             result["config5_n1"] = c5
+            # the N > 1 value's own protocol at world 1 (RCCL self-exchange):
+            # what row-sharding costs on one GPU
+            sfm, _, _ = bench_sharded_fm(args, 1, 0, vocabs, dense_pool, lite=True)
+            sfm["note"] = ("the N > 1 value's protocol (row-sharded FM, pipelined partials) at world 1 with the "
+                           "RCCL self-exchange forced - not what a world-1 job runs (it calls the unsharded "
+                           "kernel, the value above)")
+            result["fm_hotpath_sharded_n1"] = sfm
     else:
-        res, V5 = bench_sharded_deepfm(args, world, rank)
+        # N > 1 (and --sharded at N = 1): the metric's own workload, the
+        # 26 x 1e7 table row-sharded over the ranks, B local samples per rank
+        res, _, _ = bench_sharded_fm(args, world, rank, vocabs, dense_pool)
         result.update(res)
-        result["vocab_per_field"] = V5
-        if not args.deepfm_only:
-            result["fm_hotpath_sharded"] = bench_sharded_fm(args, world, rank, vocabs, dense_pool)
+        result["value"] = res["samples_per_s"]
+        # BASELINE config 5 (the DeepFM forward on the 1e8-row table) nested
+        if not args.no_config5:
+            c5, V5 = bench_sharded_deepfm(args, world, rank)
+            c5["vocab_per_field"] = V5
+            result["config5"] = c5
     return result
 
 
@@ -436,19 +517,21 @@ def _graph_capturable(fn, first, begin=None, end=None, count=1):
     return bool(t.item()), why
 
 
-def bench_sharded_fm(args, world, rank, vocabs, dense_pool):
-    """The headline hot path (embedding lookup + FM logit, 26 x 1e7 x 16) with
-    the table row-sharded over the ranks, each rank B local samples (weak
-    scaling); nested in the N>1 line as `fm_hotpath_sharded`.  Timed protocol:
-    owner-side FM partials, pipelined (sharded.py ``pipe_step``): per batch t,
-    ONE RCCL all-to-all carrying [row ids of t | FM partials of t-1], then ONE
-    launch (rs_shard_fm_pipe) doing combine of t-1 | owner FM partials of t
-    over its field range | field route of t+1.  Also timed: the same protocol
-    unpipelined (``forward``: two all-to-alls per batch), the fixed-capacity
-    ROW exchange (``forward_slots``, every lookup's 64-B row back to the
-    requester) and the data-parallel training step.  Steps are replayed from
-    HIP graphs when RCCL capture works on every rank (decided collectively),
-    eager otherwise; the all-to-alls run at world 1 too (RCCL self-exchange)."""
+def bench_sharded_fm(args, world, rank, vocabs, dense_pool, lite=False):
+    """The headline workload (embedding lookup + FM logit, 26 x 1e7 x 16, B
+    local samples per rank) with the table ROW-SHARDED over the ranks (weak
+    scaling): the N > 1 line's `value`, and at N = 1 (forced RCCL
+    self-exchange) the nested anchor `fm_hotpath_sharded_n1`.  Timed protocol
+    (the value): owner-side FM partials, pipelined (sharded.py ``pipe_step``):
+    per batch t ONE RCCL all-to-all carrying [row ids of t | FM partials of
+    t-1], then ONE launch (rs_shard_fm_pipe) doing combine of t-1 | owner FM
+    partials of t over its field range | field route of t+1.  Beside it: the
+    pipe kernel alone (the roofline's kernel time), the unpipelined protocol
+    (``forward``: two all-to-alls per batch) and, unless ``lite``, the
+    cpu_baseline on rank 0; --extras adds the ROW exchange (``forward_slots``)
+    and the data-parallel training step.  Steps are replayed from HIP graphs
+    when RCCL capture works on every rank (decided collectively), eager
+    otherwise."""
     import torch.distributed as dist
     from recommender_system_amd.sharded import ShardedEmbeddingFM
     B, F, k = args.batch, len(vocabs), 16
@@ -490,25 +573,83 @@ def bench_sharded_fm(args, world, rank, vocabs, dense_pool):
 
     sh.pipe_route(ids_pool[0])  # prologue of the stream: batch 0's row ids
     dt, step_ms, timing = run(pipelined)
+    # the pipe kernel alone, on this rank's last received records (no
+    # exchange: the same owner / route / combine work every launch)
+    sb = sh._sbufs(B)
+
+    def pipe_only(i):
+        j = i % npool
+        sh.ops.pipe(sh, sb["recv"], sb["send"], prev=(dense_pool[j], outs[0]), cur=ids_pool[j],
+                    nxt=(dense_pool[j], ids_pool[j]))
+
+    _, kslot = _timed_graph(pipe_only, args.steps, 2, world, chunk=16)
+    kern_ms = _max_over_ranks(kslot, world)
     udt, ustep_ms, utiming = run(per_batch(sh.forward))
     f = sh.ops.bad_flag()  # any bad id during the timed steps?
-    dist.all_reduce(f, op=dist.ReduceOp.MAX)
+    if world > 1 or _dist_on():
+        dist.all_reduce(f, op=dist.ReduceOp.MAX)
     if bool(f.item()):
         raise RuntimeError("sharded bench: bad ids during timing")
-    # reference point: the same step with the row exchange
-    rdt, rstep_ms, rtiming = run(per_batch(sh.forward_slots))
-    fl = sh.ops.flags(sh._bufs(B))
-    dist.all_reduce(fl, op=dist.ReduceOp.MAX)
-    bufs = sh._bufs(B)
-    # data-parallel training step on the sharded table (sharded.py train_step)
-    labels = (torch.rand(npool, B, generator=g, device=dev) < 0.25).to(torch.float32)
+    S, P = sh.slot_stride, sh.partial_width
+    alg = B * 1824 + 18880
+    rec_bytes = world * B * (S + P) * 4
+    roof = {"bound": "hbm", "achieved": alg / (kern_ms * 1e-3) / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+            "frac": alg / (kern_ms * 1e-3) / PEAK_HBM, "traffic": None,
+            "traffic_note": "no PMC pass on the driver's multi-GPU run; the N = 1 line's traffic is the unsharded "
+                            "kernel's",
+            "kernel": "shard_fm_pipe (rs_shard_fm_pipe: combine t-1 | owner FM partials of t | field route t+1)",
+            "kernel_ms": kern_ms,
+            "kernel_ms_source": "HIP events around graph-replayed launches of the pipe kernel alone on this rank's "
+                                "received records (no exchange), max over ranks",
+            "algorithmic_bytes_per_launch": alg,
+            "algorithmic_bytes_note": "per rank and step: the headline's 1,824 B/sample (ids 104, dense 52, rows "
+                                      "1,664, logit 4) x B local samples + 18,880 B of FM parameters - under uniform "
+                                      "ids an owner reads B x F rows of 64 B on average; the exchange records are "
+                                      "listed separately",
+            "exchange_record_bytes_per_rank_each_way": rec_bytes,
+            "record_bytes_per_launch": 2 * rec_bytes,
+            "achieved_incl_records": (alg + 2 * rec_bytes) / (kern_ms * 1e-3) / 1e9,
+            "step_ms": dt / args.steps * 1e3,
+            "step_frac": alg / (dt / args.steps) / PEAK_HBM}
+    res = {
+        "samples_per_s": world * args.steps * B / dt, "ms_per_step": dt / args.steps * 1e3,
+        "slot_ms": step_ms,
+        "protocol": "owner-side FM partials, pipelined: ONE RCCL all-to-all of [row ids of t | FM partials of t-1] "
+                    "records + ONE launch (combine t-1 | owner FM partials of t over its field range | field route "
+                    "of t+1) per batch; fixed sizes, no host sync",
+        "timing": timing, "roofline": roof, "lookups_per_rank": B * F, "rows_per_rank": sh.rows_per_rank,
+        "owner_field_ranges": sh.owner_field_ranges, "bytes_per_rank_each_way": rec_bytes,
+        "unpipelined": {"samples_per_s": world * args.steps * B / udt, "ms_per_step": udt / args.steps * 1e3,
+                        "timing": utiming, "id_bytes_per_rank_each_way": world * B * S * 4,
+                        "partial_bytes_per_rank_each_way": world * B * P * 4,
+                        "note": "forward(): route, all-to-all ids, owner partials, all-to-all partials, combine"}}
+    if lite:
+        return res, sh, ids_pool
+    res["cpu_baseline"] = _cpu_leg_fm_sharded(args, world, rank, sh, dense_pool, ids_pool, B)
+    if args.extras:
+        # reference point: the same step with the row exchange
+        rdt, _, rtiming = run(per_batch(sh.forward_slots))
+        fl = sh.ops.flags(sh._bufs(B))
+        dist.all_reduce(fl, op=dist.ReduceOp.MAX)
+        bufs = sh._bufs(B)
+        # data-parallel training step on the sharded table (sharded.py train_step)
+        labels = (torch.rand(npool, B, generator=g, device=dev) < 0.25).to(torch.float32)
 
-    def train(i):
-        j = i % npool
-        sh.train_step(dense_pool[j], ids_pool[j], labels[j], lr=0.01, check=False)
+        def train(i):
+            j = i % npool
+            sh.train_step(dense_pool[j], ids_pool[j], labels[j], lr=0.01, check=False)
 
-    tdt, tstep_ms, ttiming = run(train)
-    local = None
+        tdt, _, ttiming = run(train)
+        res["rows_protocol"] = {"samples_per_s": world * args.steps * B / rdt, "ms_per_step": rdt / args.steps * 1e3,
+                                "timing": rtiming, "slots_per_peer": bufs["cap"],
+                                "row_bytes_per_rank_each_way": world * bufs["cap"] * k * 4,
+                                "overflow_during_timing": bool(fl[1].item()),
+                                "note": "fixed-capacity row exchange (forward_slots): rows back to the requester"}
+        res["train_step"] = {"samples_per_s": world * args.steps * B / tdt, "ms_per_step": tdt / args.steps * 1e3,
+                             "timing": ttiming,
+                             "note": "ShardedEmbeddingFM.train_step: partial-protocol forward (2 all-to-alls) + "
+                                     "combine_grad, all-gather of [s | g] records, owner row grads + row-sparse SGD "
+                                     "of the shard, all-reduce of the FM parameter grads, SGD + l2"}
     if world == 1:
         # the same pipelined step without the RCCL self-exchange (what a world-1
         # job runs: sharded.py skips the all-to-alls unless forced)
@@ -516,35 +657,51 @@ def bench_sharded_fm(args, world, rank, vocabs, dense_pool):
         sh.pipe_route(ids_pool[0])
         ldt, lstep_ms, ltiming = run(pipelined)
         sh._force_exchange = True
-        local = {"samples_per_s": args.steps * B / ldt, "ms_per_step": ldt / args.steps * 1e3,
-                 "slot_ms": lstep_ms, "timing": ltiming,
-                 "note": "world 1 without the self-exchange: rs_shard_fm_pipe alone per batch (the records "
-                         "alternate between two buffers); the RCCL lines above are the comparison"}
-    S, P = sh.slot_stride, sh.partial_width
-    alg = B * 1824 + 18880
-    return {
-        "samples_per_s": world * args.steps * B / dt, "ms_per_step": dt / args.steps * 1e3,
-        "protocol": "owner-side FM partials, pipelined: ONE RCCL all-to-all of [row ids of t | FM partials of t-1] "
-                    "records + ONE launch (combine t-1 | owner FM partials of t over its field range | field route "
-                    "of t+1) per batch; fixed sizes, no host sync",
-        "timing": timing, "lookups_per_rank": B * F, "rows_per_rank": sh.rows_per_rank,
-        "owner_field_ranges": sh.owner_field_ranges, "bytes_per_rank_each_way": world * B * (S + P) * 4,
-        "hbm_frac_vs_unsharded_bytes": alg / (step_ms * 1e-3) / PEAK_HBM,
-        "unpipelined": {"samples_per_s": world * args.steps * B / udt, "ms_per_step": udt / args.steps * 1e3,
-                        "timing": utiming, "id_bytes_per_rank_each_way": world * B * S * 4,
-                        "partial_bytes_per_rank_each_way": world * B * P * 4,
-                        "note": "forward(): route, all-to-all ids, owner partials, all-to-all partials, combine"},
-        "rows_protocol": {"samples_per_s": world * args.steps * B / rdt, "ms_per_step": rdt / args.steps * 1e3,
-                          "timing": rtiming, "slots_per_peer": bufs["cap"],
-                          "row_bytes_per_rank_each_way": world * bufs["cap"] * k * 4,
-                          "overflow_during_timing": bool(fl[1].item()),
-                          "note": "fixed-capacity row exchange (forward_slots): rows back to the requester"},
-        "train_step": {"samples_per_s": world * args.steps * B / tdt, "ms_per_step": tdt / args.steps * 1e3,
-                       "timing": ttiming,
-                       "note": "ShardedEmbeddingFM.train_step: partial-protocol forward (2 all-to-alls) + "
-                               "combine_grad, all-gather of [s | g] records, owner row grads + row-sparse SGD "
-                               "of the shard, all-reduce of the FM parameter grads, SGD + l2"},
-        "world1_no_exchange": local}
+        res["world1_no_exchange"] = {
+            "samples_per_s": args.steps * B / ldt, "ms_per_step": ldt / args.steps * 1e3, "slot_ms": lstep_ms,
+            "timing": ltiming, "note": "world 1 without the self-exchange: rs_shard_fm_pipe alone per batch (the "
+                                       "records alternate between two buffers); the RCCL lines above are the comparison"}
+    return res, sh, ids_pool
+
+
+def _cpu_leg_fm_sharded(args, world, rank, sh, dense_pool, ids_pool, B, n_batches=4):
+    """cpu_baseline of the sharded headline line on rank 0: the oracle's numpy
+    fp32 EmbedLayer + concat + FMLayer (layer/core.py:273-280,
+    layer/interaction.py:106-114 restated; TF not installed) on rank 0's
+    batches.  The rows come from the shards through the exact row exchange
+    (``lookup``, collective), and the first batch's logits are compared with
+    rank 0's GPU output of the same batch (``forward``, collective)."""
+    if not args.cpu_baseline:
+        return None
+    out = torch.empty(B, 1, device=sh.device)
+    host = []
+    for j in range(n_batches):
+        sh.forward(dense_pool[j], ids_pool[j], check=False, out=out)
+        emb = sh.lookup(ids_pool[j])
+        torch.cuda.synchronize()
+        if rank == 0:
+            host.append((dense_pool[j].cpu().numpy(), emb.reshape(B, -1).cpu().numpy(), out.cpu().numpy().copy()))
+    _barrier(world)
+    if rank != 0:
+        return None
+    from oracle import ctr_oracle as O
+    w0, w1, v = (t.detach().cpu().numpy() for t in (sh.w0, sh.w1, sh.v))
+    n, first, t0 = 0, None, time.perf_counter()
+    while n < 64 and (time.perf_counter() - t0) < args.cpu_budget:
+        dense, emb, gout = host[n % len(host)]
+        y = O.fm_layer(np.concatenate([dense, emb], axis=-1), w0, w1, v, dt=np.float32)
+        if first is None:
+            first = (np.asarray(y, np.float64), gout)
+        n += 1
+    dt = time.perf_counter() - t0
+    ref, gout = first
+    rms = float(np.sqrt(np.mean(ref ** 2)))
+    return {"value": n * B / dt, "unit": "samples/s", "cores": _cpu_threads(), "kind": "port",
+            "sample": f"{n} batches x {B} samples of rank 0 (of {world}): numpy fp32 EmbedLayer + concat + FMLayer "
+                      f"(the reference TF graph restated; TF not installed); the batch's rows copied from the "
+                      f"shards through the exact row exchange",
+            "max_scaled_diff_vs_gpu": float(np.max(np.abs(gout.reshape(ref.shape) - ref) /
+                                                   np.maximum(np.abs(ref), rms)))}
 
 
 def _cpu_leg_config5(args, world, rank, model, dense_pool, ids_pool, out, B, n_batches=4):
@@ -610,8 +767,8 @@ def _world1_group():
 
 
 def bench_sharded_deepfm(args, world, rank, lite=False):
-    """BASELINE config 5 (the N>1 value, and --sharded at N=1): DeepFM forward
-    with ONE 1e8-row table (26 fields x 3,846,154 rows x 16 fp32 = 6.4 GB)
+    """BASELINE config 5 (nested as `config5` in the N > 1 line and as
+    `config5_n1` at N = 1): DeepFM forward with ONE 1e8-row table (26 fields x 3,846,154 rows x 16 fp32 = 6.4 GB)
     row-sharded over the ranks, B = 4096 local samples per rank (weak
     scaling), DNN 429-256-128-64-1, FM k 10.  One step = ShardedDeepFM.forward
     on one batch: rs_shard_row_route -> RCCL all-to-all of row ids ->
@@ -651,27 +808,34 @@ def bench_sharded_deepfm(args, world, rank, lite=False):
     else:
         dt, _ = _timed(step, args.steps, 0, world, events=False)
         timing = f"eager launches ({why})"
-    # pipelined stream (sharded.py pipe_step): batch t+1's route, id
-    # all-to-all, owner gather and row all-to-all on a side stream while
-    # batch t's fused kernel runs; two buffer slots, hub fork / join per step
-    outs = [torch.empty(B, 1, device=dev) for _ in range(2)]
+    pipe = None
+    if args.config5_pipelined:
+        # pipelined stream (sharded.py pipe_step): batch t+1's route, id
+        # all-to-all, owner gather and row all-to-all on a side stream while
+        # batch t's fused kernel runs; two buffer slots, hub fork / join per
+        # step.  Measured slower than the per-batch forward on one GPU
+        # (DESIGN.md 4.6), so only on request.
+        outs = [torch.empty(B, 1, device=dev) for _ in range(2)]
 
-    def pstep(i):
-        j, jn = i % npool, (i + 1) % npool
-        model.pipe_step((dense_pool[j], outs[i % 2], i % 2), (ids_pool[jn], (i + 1) % 2))
+        def pstep(i):
+            j, jn = i % npool, (i + 1) % npool
+            model.pipe_step((dense_pool[j], outs[i % 2], i % 2), (ids_pool[jn], (i + 1) % 2))
 
-    model.pipe_prologue(ids_pool[0], 0)
-    for i in range(args.warmup):
-        pstep(i)
-    torch.cuda.synchronize()
-    pgraphed, pwhy = _graph_capturable(pstep, 0, count=2)
-    model.pipe_prologue(ids_pool[0], 0)
-    if pgraphed:
-        pdt, _ = _timed_graph(pstep, args.steps, 0, world, chunk=npool)
-        ptiming = "HIP graph replay (RCCL captured, two streams)"
-    else:
-        pdt, _ = _timed(pstep, args.steps, 0, world, events=False)
-        ptiming = f"eager launches ({pwhy})"
+        model.pipe_prologue(ids_pool[0], 0)
+        for i in range(args.warmup):
+            pstep(i)
+        torch.cuda.synchronize()
+        pgraphed, pwhy = _graph_capturable(pstep, 0, count=2)
+        model.pipe_prologue(ids_pool[0], 0)
+        if pgraphed:
+            pdt, _ = _timed_graph(pstep, args.steps, 0, world, chunk=npool)
+            ptiming = "HIP graph replay (RCCL captured, two streams)"
+        else:
+            pdt, _ = _timed(pstep, args.steps, 0, world, events=False)
+            ptiming = f"eager launches ({pwhy})"
+        pipe = {"protocol": "sharded.py pipe_step: batch t+1's exchange on a side stream beside batch t's "
+                            "rs_deepfm_fwd (two buffer slots, fork / join on the step's stream)", "timing": ptiming,
+                "samples_per_s": world * args.steps * B / pdt, "ms_per_step": pdt / args.steps * 1e3}
     f = model.ops.bad_flag()
     dist.all_reduce(f, op=dist.ReduceOp.MAX)
     if bool(f.item()):
@@ -685,12 +849,10 @@ def bench_sharded_deepfm(args, world, rank, lite=False):
     fdt, fslot_ms = _timed_graph(finish, args.steps, 2, world, chunk=16)
     fin_ms = _max_over_ranks(fslot_ms, world)
     flops = B * 2 * (429 * 256 + 256 * 128 + 128 * 64 + 64)
-    # value: the faster of the two complete protocols (same outputs per
-    # batch); value_kind names which one it is
-    best_dt = min(dt, pdt)
-    kind = "pipelined" if pdt < dt else "per_batch"
-    ms = best_dt / args.steps * 1e3
-    ums = dt / args.steps * 1e3
+    # value: the per-batch forward (the pipelined stream rides along when
+    # asked for, never as the value)
+    kind = "per_batch"
+    ms = ums = dt / args.steps * 1e3
     S = model.emb.slot_stride
     roof = {"bound": "mfma", "achieved": flops / (fin_ms * 1e-3) / 1e12, "peak": PEAK_F32 / 1e12,
             "unit": "TFLOP/s", "frac": flops / (fin_ms * 1e-3) / PEAK_F32, "traffic": None,
@@ -707,14 +869,13 @@ def bench_sharded_deepfm(args, world, rank, lite=False):
     per_batch = {"samples_per_s": world * args.steps * B / dt, "ms_per_step": ums, "timing": timing,
                  "note": "ShardedDeepFM.forward per batch: route, all-to-all ids, gather, all-to-all rows, "
                          "rs_deepfm_fwd in sequence (the comparison for the pipelined value)"}
-    pipe = {"protocol": "sharded.py pipe_step: batch t+1's exchange on a side stream beside batch t's "
-                        "rs_deepfm_fwd (two buffer slots, fork / join on the step's stream)", "timing": ptiming,
-            "samples_per_s": world * args.steps * B / pdt, "ms_per_step": pdt / args.steps * 1e3}
     cpu = _cpu_leg_config5(args, world, rank, model, dense_pool, ids_pool, out, B)
+    res = {"samples_per_s": world * args.steps * B / dt, "ms_per_step": ms, "value_kind": kind,
+           "per_batch": per_batch, "roofline": roof, "exchange": exch, "cpu_baseline": cpu}
+    if pipe is not None:
+        res["pipelined"] = pipe
     if lite:
-        return {"samples_per_s": world * args.steps * B / best_dt, "ms_per_step": ms, "value_kind": kind,
-                "pipelined": pipe,
-                "per_batch": per_batch, "roofline": roof, "exchange": exch, "cpu_baseline": cpu}, V
+        return res, V
     # secondary: the deduplicated exchange on Zipf(1.2) ids (hot rows repeat:
     # each owner receives every distinct row once per rank) and the training
     # step (forward exchange, local backward, reverse all-to-all of dL/drow,
@@ -757,46 +918,43 @@ def bench_sharded_deepfm(args, world, rank, lite=False):
     distinct = float(np.mean([sum(len(np.unique((model.emb.offsets[None, :].cpu().numpy() +
                                                  zipf_pool[j].cpu().numpy().astype(np.int64))[:, c]))
                                   for c in range(F)) for j in range(2)])) / (B * F)
-    labels = (torch.rand(npool, B, generator=g, device=dev) < 0.25).to(torch.float32)
+    res["zipf_ids"] = {"distinct_lookup_fraction": distinct,
+                       "field_range_records": {"samples_per_s": world * nz * B / zdt, "ms_per_step": zdt / nz * 1e3,
+                                               "ms_per_step_eager": zedt / nz * 1e3,
+                                               "row_bytes_per_rank_each_way": world * B * S * k * 4},
+                       "dedup": {"samples_per_s": world * nz * B / ddt, "ms_per_step": ddt / nz * 1e3,
+                                 "ms_per_step_eager": dedt / nz * 1e3,
+                                 "capacity_fraction": 0.5, "overflow_seen": bool(over.item()),
+                                 "row_bytes_per_rank_each_way": dmodel._rbufs(B)["n"] * k * 4},
+                       "timing": ztiming,
+                       "note": "Zipf(1.2) ids per field, clipped to the vocab; dedup = rs_shard_dedup_route (per-field "
+                               "LDS hash, first-occurrence numbering, no sort): each owner receives each distinct "
+                               "row once per rank"}
+    if args.extras:
+        labels = (torch.rand(npool, B, generator=g, device=dev) < 0.25).to(torch.float32)
 
-    def train(i):
-        j = i % npool
-        model.train_step((dense_pool[j], ids_pool[j]), labels[j], lr=0.01, check=False)
+        def train(i):
+            j = i % npool
+            model.train_step((dense_pool[j], ids_pool[j]), labels[j], lr=0.01, check=False)
 
-    nt = max(10, args.steps // 4)
-    tdt, _ = _timed(train, nt, 2, world, events=False)
-    local = None
+        nt = max(10, args.steps // 4)
+        tdt, _ = _timed(train, nt, 2, world, events=False)
+        res["train_step"] = {"samples_per_s": world * nt * B / tdt, "ms_per_step": tdt / nt * 1e3,
+                             "timing": "eager launches",
+                             "note": "ShardedDeepFM.train_step: row exchange, local DeepFM backward (rs_gemm), "
+                                     "rs_scatter_rows + reverse all-to-all of dL/drow, owner rs_embedding_sgd, "
+                                     "all-reduce of the flat replicated gradient, SGD"}
     if world == 1:
         # what a world-1 job runs: no self-exchange, the fused DeepFM straight
         # from the (whole-table) shard
         model.emb._force_exchange = False
         ldt, lslot_ms = _timed_graph(step, args.steps, 2, world, chunk=16)
         model.emb._force_exchange = True
-        local = {"samples_per_s": args.steps * B / ldt, "ms_per_step": ldt / args.steps * 1e3, "slot_ms": lslot_ms,
-                 "timing": "HIP graph replay",
-                 "note": "world 1 without the RCCL self-exchange (ShardedDeepFM.forward -> rs_deepfm_fwd on the "
-                         "shard); the exchange line above is the comparison"}
-    res = {"value": world * args.steps * B / best_dt, "ms_per_step": ms, "value_kind": kind, "pipelined": pipe,
-           "per_batch": per_batch,
-           "roofline": roof, "exchange": exch, "cpu_baseline": cpu,
-           "zipf_ids": {"distinct_lookup_fraction": distinct,
-                        "field_range_records": {"samples_per_s": world * nz * B / zdt, "ms_per_step": zdt / nz * 1e3,
-                                                "ms_per_step_eager": zedt / nz * 1e3,
-                                                "row_bytes_per_rank_each_way": world * B * S * k * 4},
-                        "dedup": {"samples_per_s": world * nz * B / ddt, "ms_per_step": ddt / nz * 1e3,
-                                  "ms_per_step_eager": dedt / nz * 1e3,
-                                  "capacity_fraction": 0.5, "overflow_seen": bool(over.item()),
-                                  "row_bytes_per_rank_each_way": dmodel._rbufs(B)["n"] * k * 4},
-                        "timing": ztiming,
-                        "note": "Zipf(1.2) ids per field, clipped to the vocab; dedup = rs_shard_dedup_route (per-field "
-                                "LDS hash, first-occurrence numbering, no sort): each owner receives each distinct "
-                                "row once per rank"},
-           "train_step": {"samples_per_s": world * nt * B / tdt, "ms_per_step": tdt / nt * 1e3,
-                          "timing": "eager launches",
-                          "note": "ShardedDeepFM.train_step: row exchange, local DeepFM backward (rs_gemm), "
-                                  "rs_scatter_rows + reverse all-to-all of dL/drow, owner rs_embedding_sgd, "
-                                  "all-reduce of the flat replicated gradient, SGD"},
-           "world1_no_exchange": local}
+        res["world1_no_exchange"] = {
+            "samples_per_s": args.steps * B / ldt, "ms_per_step": ldt / args.steps * 1e3, "slot_ms": lslot_ms,
+            "timing": "HIP graph replay",
+            "note": "world 1 without the RCCL self-exchange (ShardedDeepFM.forward -> rs_deepfm_fwd on the "
+                    "shard); the exchange line above is the comparison"}
     return res, V
 
 
@@ -1502,12 +1660,14 @@ def main():
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
-    ap.add_argument("--deepfm-only", dest="deepfm_only", action="store_true",
-                    help="sharded: skip the secondary FM hot-path protocols")
+    ap.add_argument("--extras", action="store_true",
+                    help="N > 1 / --sharded: also time the row-exchange protocol and the sharded training steps")
+    ap.add_argument("--config5-pipelined", dest="config5_pipelined", action="store_true",
+                    help="also time config 5's pipelined stream (slower than the per-batch forward on one GPU)")
     ap.add_argument("--no-config5", dest="no_config5", action="store_true",
-                    help="N=1: skip the nested config-5 anchor (config5_n1)")
+                    help="skip the nested config-5 line (config5_n1 at N = 1, config5 at N > 1)")
     ap.add_argument("--sharded", action="store_true",
-                    help="time the row-sharded exchange path even at world 1 (N=1 point of the sharded curve)")
+                    help="time the N > 1 line's row-sharded protocol even at world 1 (RCCL self-exchange)")
     args = ap.parse_args()
     _host_wait_mode(os.environ.get("RS_BENCH_SYNC", "spin"))
     world, rank = _dist_setup(args)
@@ -1523,32 +1683,41 @@ def main():
         args.no_config5 = True
     elif args.config != "hotpath":
         raise SystemExit(f"unknown --config {args.config}")
+    dev_state = {"before": _device_state()}
+    empty_slot = _empty_kernel_slot(world)
     res = bench_hotpath(args, world, rank)
+    dev_state["after"] = _device_state()
     if rank == 0:
         line = {
             "metric": "CTR forward samples/sec @ batch 4096, 26 sparse×1e7 vocab, dim 16; %HBM roofline",
             "value": res["value"], "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": res["ms_per_step"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": ({"workload": "deepfm_embed_fm_hotpath", "global_batch": args.batch, "batch_per_gpu": args.batch,
-                        "sparse_fields": 26, "vocab_per_field": int(args.vocab), "embed_dim": 16, "fm_k": 10,
-                        "dense_features": 13, "ids": "int32 uniform per field", "parallelism": "dp1",
-                        "value_kind": "embed + FM logit (DeepFM's EmbedLayer + concat + FMLayer; no DNN, no "
-                                      "sigmoid) - the full DeepFM forward is deepfm_forward, config 5 at N = 1 "
-                                      "is config5_n1"}
-                       if world == 1 and not args.sharded else
-                       {"workload": "deepfm_forward_rowsharded_1e8 (BASELINE config 5)",
-                        "global_batch": args.batch * world, "batch_per_gpu": args.batch, "sparse_fields": 26,
-                        "vocab_per_field": res["vocab_per_field"], "table_rows": 26 * res["vocab_per_field"],
-                        "embed_dim": 16, "fm_k": 10, "dnn": [256, 128, 64, 1], "dense_features": 13,
-                        "ids": "int32 uniform per field", "parallelism": f"dp{world}+rowshard{world}",
-                        "value_kind": (f"{res.get('value_kind')}: the faster of the per-batch forward and the "
-                                       "pipelined stream (both nested below)")}),
+            "config": {"workload": "deepfm_embed_fm_hotpath", "global_batch": args.batch * world,
+                       "batch_per_gpu": args.batch, "sparse_fields": 26, "vocab_per_field": int(args.vocab),
+                       "embed_dim": 16, "fm_k": 10, "dense_features": 13, "ids": "int32 uniform per field"},
             "roofline": res["roofline"], "cpu_baseline": res["cpu_baseline"],
             "host_wait": os.environ.get("RS_BENCH_SYNC", "spin") if world == 1 else "default",
+            "device_state": dev_state, "empty_kernel_slot_us": empty_slot,
         }
-        for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "config5_n1", "pipelined", "per_batch",
-                    "exchange", "train_step", "fm_hotpath_sharded", "world1_no_exchange"):
+        if world == 1 and not args.sharded:
+            line["config"].update({
+                "parallelism": "dp1",
+                "value_kind": "embed + FM logit (DeepFM's EmbedLayer + concat + FMLayer; no DNN, no sigmoid), one "
+                              "unsharded rs_embed_fm_fwd launch per batch - the full DeepFM forward is "
+                              "deepfm_forward, config 5 at N = 1 is config5_n1, the N > 1 protocol at world 1 is "
+                              "fm_hotpath_sharded_n1"})
+        else:
+            line["config"].update({
+                "parallelism": f"dp{world}+rowshard{world}",
+                "table_rows_per_rank": res["rows_per_rank"],
+                "value_kind": "embed + FM logit of the same workload with the 26 x 1e7 table row-sharded over the "
+                              "ranks: per batch ONE RCCL all-to-all of [row ids t | FM partials t-1] + ONE "
+                              "rs_shard_fm_pipe launch (sharded.py pipe_step); config 5 (the DeepFM forward on the "
+                              "1e8-row table) is nested as config5"})
+        for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "config5_n1", "fm_hotpath_sharded_n1",
+                    "config5", "protocol", "timing", "slot_ms", "unpipelined", "rows_protocol", "train_step",
+                    "owner_field_ranges", "bytes_per_rank_each_way", "world1_no_exchange"):
             if key in res:
                 line[key] = res[key]
         _emit(line)

@@ -84,6 +84,11 @@ const char* rs_last_error_string(void);
 int rs_set_option(int option, int value);
 /* Current value of `option`, or -1 for an unknown option. */
 int rs_get_option(int option);
+/* Diagnostic (no reference counterpart): launch an empty kernel of `grid`
+ * workgroups x `block` threads on `stream`.  bench.py replays it from a
+ * hipGraph to record the box's dependent-launch slot time beside its
+ * numbers. */
+int rs_diag_empty(int grid, int block, rs_stream_t stream);
 
 /* --------------------------------------------------------- embedding (a3)
  * Replaces EmbedLayer.call (layer/core.py:273-280) + the dense/sparse concat of

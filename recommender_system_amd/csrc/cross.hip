@@ -493,20 +493,12 @@ extern "C" int rs_embed_cross_fwd(const void* ids, int id_kind, int64_t id_strid
   with_id_kind(id_kind, [&](auto K) {
     constexpr int KIND = decltype(K)::value;
     if (g.NT == 1) {
-      static size_t set1 = 64 * 1024;
-      if (lds > set1) {
-        (void)hipFuncSetAttribute((const void*)embed_cross<1, KIND>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        set1 = lds;
-      }
+      static LdsAttr set1;
+      lds_attr(set1, (const void*)embed_cross<1, KIND>, lds);
       embed_cross<1, KIND><<<grid, NW * 64, lds, st>>>(a, e);
     } else {
-      static size_t set2 = 64 * 1024;
-      if (lds > set2) {
-        (void)hipFuncSetAttribute((const void*)embed_cross<2, KIND>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        set2 = lds;
-      }
+      static LdsAttr set2;
+      lds_attr(set2, (const void*)embed_cross<2, KIND>, lds);
       embed_cross<2, KIND><<<grid, NW * 64, lds, st>>>(a, e);
     }
   });
@@ -561,18 +553,12 @@ extern "C" int rs_dcn_fwd(const void* ids, int id_kind, int64_t id_stride, const
   with_id_kind(id_kind, [&](auto K) {
     constexpr int KIND = decltype(K)::value;
     if (g.NT == 1) {
-      static size_t set1 = 64 * 1024;
-      if (lds > set1) {
-        (void)hipFuncSetAttribute((const void*)dcn_fused<1, KIND>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        set1 = lds;
-      }
+      static LdsAttr set1;
+      lds_attr(set1, (const void*)dcn_fused<1, KIND>, lds);
       dcn_fused<1, KIND><<<grid, 16 * 64, lds, st>>>(a, e, t);
     } else {
-      static size_t set2 = 64 * 1024;
-      if (lds > set2) {
-        (void)hipFuncSetAttribute((const void*)dcn_fused<2, KIND>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        set2 = lds;
-      }
+      static LdsAttr set2;
+      lds_attr(set2, (const void*)dcn_fused<2, KIND>, lds);
       dcn_fused<2, KIND><<<grid, 16 * 64, lds, st>>>(a, e, t);
     }
   });

@@ -128,12 +128,10 @@ __global__ void fm_prepare_generic(const float* __restrict__ w1, const float* __
 // TW: fused DeepFM — x goes to an LDS tile ([emb F*k | dense nd | 0-pad],
 // row stride tw->rs) instead of x_out, and the DNN tower of mlp_tower.hpp runs
 // on it, closed by sigmoid(c0*dnn + c1*fm) (model/deepFM.py:24-30).
-// TS: samples per workgroup (16 = one MFMA row tile; 8 = the tile's rows
-// 8..15 repeat rows 0..7, two workgroups per CU at batch 4096)
-template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, int TS = 16, bool PF = false, bool KA = false>
+// A workgroup owns one 16-sample MFMA row tile.
+template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, bool PF = false, bool KA = false>
 __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArgs* tw, const int tile,
                                               const FieldMeta* km = nullptr) {
-  static_assert(TS == 16 || (TS == 8 && !TW && KIND != 4), "8-sample tiles: plain FM kernel only");
   // MC > 0: field slots per wave and pass (owner kernels with few fields)
   constexpr int MAXC0 = MC > 0 ? MC : 128 / (NW * KV);
   constexpr int MAXC = MAXC0 < 1 ? 1 : (MAXC0 > 8 ? 8 : MAXC0);
@@ -146,11 +144,10 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int s = lane & 15;   // A: sample row of the tile; B/C: column
   const int kk = lane >> 4;  // k-slot
-  const int64_t bt = (int64_t)tile * TS + (s % TS);
-  const bool valid = s < TS && bt < a.batch;
-  // Padded lanes of the last tile recompute the last sample (and with TS = 8
-  // rows 8..15 repeat rows 0..7): an MFMA output row depends only on its own
-  // A row, so they never touch valid outputs.
+  const int64_t bt = (int64_t)tile * 16 + s;
+  const bool valid = bt < a.batch;
+  // Padded lanes of the last tile recompute the last sample: an MFMA output
+  // row depends only on its own A row, so they never touch valid outputs.
   const int64_t b = bt < a.batch ? bt : a.batch - 1;
   const int d = a.nd + a.F * a.k;
   // w0 is requested now, not behind the rows (a dependent load at the end)
@@ -223,8 +220,8 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   const bool coop = !KA && (KIND != 3) && a.F <= FMAX;
 #endif
   if (coop) {
-    const int64_t b0 = (int64_t)tile * TS;
-    for (int t = threadIdx.x; t < TS * a.F; t += NW * 64) {
+    const int64_t b0 = (int64_t)tile * 16;
+    for (int t = threadIdx.x; t < 16 * a.F; t += NW * 64) {
       const int ss = t / a.F, c = t - ss * a.F;
       const int64_t bb = b0 + ss < a.batch ? b0 + ss : a.batch - 1;
       const auto idv = I::load(a.ids, bb * a.id_stride + c);
@@ -303,11 +300,11 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
         if (OWNER) {
           offc[j] = 0;
           vocc[j] = a.owner_rows;
-          P.rid[j] = coop ? lid[s % TS][P.cj[j]] : I::load(a.ids, b * a.id_stride + P.cj[j]);
+          P.rid[j] = coop ? lid[s][P.cj[j]] : I::load(a.ids, b * a.id_stride + P.cj[j]);
         } else if (coop) {
           offc[j] = lmeta[0][P.cj[j]];
           vocc[j] = lmeta[1][P.cj[j]];
-          P.rid[j] = lid[s % TS][P.cj[j]];
+          P.rid[j] = lid[s][P.cj[j]];
         } else if constexpr (KA) {  // kernarg metadata: scalar loads, wave-uniform field
           offc[j] = km->off[P.cj[j]];
           vocc[j] = km->voc[P.cj[j]];
@@ -402,9 +399,6 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   if (a.F == 0 || coop) load_dense();
   if (coop) __syncthreads();
   RS_STAMP(9);
-#ifndef RS_EARLY_IDS
-#define RS_EARLY_IDS 1
-#endif
   if (PRE) {
     if (has_pass(0)) {
       // both passes' ids requested together: the second pass's id trip is
@@ -412,7 +406,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       // fragments: ids first was slower, 5.95 vs 5.75 us at 4096)
       fetch_ids(0, P0);
       const bool two = has_pass(PS);
-      if (RS_EARLY_IDS && two) fetch_ids(PS, P1);
+      if (two) fetch_ids(PS, P1);
       // (the second pass's rows stay behind the first pass's MFMAs: issuing
       // them with the first pass's was slower, 6.19 vs 5.82 us at 4096 —
       // the r1 finding that two row bursts beat one, again)
@@ -421,7 +415,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       if (two) norms(P1);
       consume(0, P0);
       if (two) {
-        issue_rows(PS, P1, RS_EARLY_IDS);
+        issue_rows(PS, P1, true);
         consume(PS, P1);
         for (int cg = 2 * PS; has_pass(cg); cg += PS) {
           issue_b(cg, P0);
@@ -505,7 +499,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       t += __shfl_xor(t, 16);
       lin += __shfl_xor(lin, 16);
     }
-    const int64_t bb = (int64_t)tile * TS + smp;
+    const int64_t bb = (int64_t)tile * 16 + smp;
     if constexpr (OWNER) {
       // partial record: column sums as they stand, the q term row-summed
       float q = col < NW ? qs[col][smp] : 0.f;
@@ -520,7 +514,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       return;
     }
     const float fm = (lin + w0v) + 0.5f * t;
-    if (col == 0 && smp < TS && bb < a.batch && a.logit) a.logit[bb] = fm;
+    if (col == 0 && bb < a.batch && a.logit) a.logit[bb] = fm;
     if constexpr (TW) {
       if (col == 0) fmlog[smp] = fm;
     }
@@ -529,9 +523,9 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   if constexpr (TW) mlp_tower_tile<NW>(*tw, tsm, (int64_t)tile * 16, ring, fmlog);
 }
 
-template <int KV, int NT, int NW, int KIND, int MC, int TS = 16, bool PF = false>
+template <int KV, int NT, int NW, int KIND, int MC, bool PF = false>
 __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
-  embed_fm_body<KV, NT, NW, KIND, false, MC, TS, PF>(a, nullptr, blockIdx.x);
+  embed_fm_body<KV, NT, NW, KIND, false, MC, PF>(a, nullptr, blockIdx.x);
 }
 
 // the field metadata by value (rs_embed_fm_fwd_hm): each wave loads its own
@@ -539,7 +533,7 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
 // id tile, no barrier, no per-wave metadata loads from one hot L2 line
 template <int KV, int NT, int NW, int KIND, bool PF>
 __global__ __launch_bounds__(NW * 64) void embed_fm_mfma_ka(EmbedFmArgs a, FieldMeta m) {
-  embed_fm_body<KV, NT, NW, KIND, false, 1, 16, PF, true>(a, nullptr, blockIdx.x, &m);
+  embed_fm_body<KV, NT, NW, KIND, false, 1, PF, true>(a, nullptr, blockIdx.x, &m);
 }
 
 // ---- sharded FM, partial protocol: combine (requester side) as a block part
@@ -635,7 +629,7 @@ __global__ __launch_bounds__(16 * 64) void deepfm_fused(EmbedFmArgs a, MlpArgs t
 // ... with the field metadata by value (rs_deepfm_fwd_hm; see embed_fm_mfma_ka)
 template <int KV, int KIND>
 __global__ __launch_bounds__(16 * 64) void deepfm_fused_ka(EmbedFmArgs a, MlpArgs t, FieldMeta m) {
-  embed_fm_body<KV, 1, 16, KIND, true, 1, 16, false, true>(a, &t, blockIdx.x, &m);
+  embed_fm_body<KV, 1, 16, KIND, true, 1, false, true>(a, &t, blockIdx.x, &m);
 }
 
 // Generic fallback (any k / kfm): one 256-thread workgroup per sample.
@@ -824,11 +818,7 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st, const FieldMe
   // (16 + 10), 6.05 us per launch against 6.54 with both in one pass (2 slots
   // per wave) — the second pass's row requests queue behind a shorter first
   // wave of 256 rows per CU.  More than 32 fields: 2 slots per pass.
-#ifndef RS_EMBED_TS
-#define RS_EMBED_TS 16
-#endif
-  constexpr int TS = RS_EMBED_TS;
-  const int grid = (int)((a.batch + TS - 1) / TS);
+  const int grid = (int)((a.batch + 15) / 16);
   // several tiles per CU: prefetch the first passes' B fragments (PF) and
   // use fewer waves per tile, so more tiles share a CU (one field slot per
   // wave and pass): 8 waves up to 1024 tiles, 4 beyond (scripts/ab A/B,
@@ -847,10 +837,10 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st, const FieldMe
     embed_fm_mfma_ka<KV, NT, 16, KIND, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
     return;
   }
-  if (a.F <= 32 && grid > 1024) embed_fm_mfma<KV, NT, 4, KIND, 1, TS, true><<<grid, 4 * 64, 0, st>>>(a);
-  else if (a.F <= 32 && grid > 512) embed_fm_mfma<KV, NT, 8, KIND, 1, TS, true><<<grid, 8 * 64, 0, st>>>(a);
-  else if (a.F <= 32) embed_fm_mfma<KV, NT, 16, KIND, 1, TS><<<grid, 16 * 64, 0, st>>>(a);
-  else embed_fm_mfma<KV, NT, 16, KIND, 0, TS><<<grid, 16 * 64, 0, st>>>(a);
+  if (a.F <= 32 && grid > 1024) embed_fm_mfma<KV, NT, 4, KIND, 1, true><<<grid, 4 * 64, 0, st>>>(a);
+  else if (a.F <= 32 && grid > 512) embed_fm_mfma<KV, NT, 8, KIND, 1, true><<<grid, 8 * 64, 0, st>>>(a);
+  else if (a.F <= 32) embed_fm_mfma<KV, NT, 16, KIND, 1><<<grid, 16 * 64, 0, st>>>(a);
+  else embed_fm_mfma<KV, NT, 16, KIND, 0><<<grid, 16 * 64, 0, st>>>(a);
 }
 
 template <int KIND>
@@ -1467,13 +1457,9 @@ static bool deepfm_geom(int nd, int n_fields, int k, int kfm, int n_layers, cons
 template <int KV, int KIND>
 static void launch_deepfm(const EmbedFmArgs& a, const MlpArgs& t, size_t lds, hipStream_t st,
                           const FieldMeta* hm) {
-  static size_t lds_set[2] = {64 * 1024, 64 * 1024};  // opt in to exactly what is needed beyond the default
+  static LdsAttr lds_set[2];  // opt in to exactly what is needed beyond the default
   const int ka = hm && a.F <= 32 ? 1 : 0;
-  if (lds > lds_set[ka]) {
-    (void)hipFuncSetAttribute(ka ? (const void*)deepfm_fused_ka<KV, KIND> : (const void*)deepfm_fused<KV, KIND>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    lds_set[ka] = lds;
-  }
+  lds_attr(lds_set[ka], ka ? (const void*)deepfm_fused_ka<KV, KIND> : (const void*)deepfm_fused<KV, KIND>, lds);
   const unsigned grid = (unsigned)((a.batch + 15) / 16);
   if (ka) deepfm_fused_ka<KV, KIND><<<grid, 16 * 64, lds, st>>>(a, t, *hm);
   else deepfm_fused<KV, KIND><<<grid, 16 * 64, lds, st>>>(a, t);

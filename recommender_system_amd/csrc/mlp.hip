@@ -161,12 +161,8 @@ extern "C" int rs_mlp_fwd(const float* x, int64_t x_stride, int n_layers, const 
   a.M = batch;
   a.dbg = g_mlp_dbg;
   const size_t lds = g.lds;
-  static size_t lds_set = 64 * 1024;  // opt in to exactly what is needed beyond the default
-  if (lds > lds_set) {
-    (void)hipFuncSetAttribute((const void*)mlp_tower<MLP_NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    lds_set = lds;
-  }
+  static LdsAttr lds_set;  // opt in to exactly what is needed beyond the default
+  lds_attr(lds_set, (const void*)mlp_tower<MLP_NW>, lds);
   const int64_t grid = (batch + 15) / 16;
   RS_REQUIRE(grid < (1ll << 31), "rs_mlp_fwd: batch too large");
   mlp_tower<MLP_NW><<<(unsigned)grid, MLP_NW * 64, lds, as_stream(stream)>>>(a);

@@ -91,9 +91,7 @@ struct MlpItem {
 // k-slices per output tile: layers with >= 4 tiles keep whole columns per
 // wave (no partial-sum exchange: measured faster than filling all 16 waves);
 // narrow layers (the 64->1 head) split K over the idle waves.
-#ifndef MLP_SPLIT_T
-#define MLP_SPLIT_T 4  // layers with fewer output tiles than this split K over the idle waves
-#endif
+constexpr int MLP_SPLIT_T = 4;  // layers with fewer output tiles than this split K over the idle waves
 __device__ __forceinline__ int mlp_slices(int T, int G, int NW) {
   if (T >= MLP_SPLIT_T) return 1;
   const int S = NW / T;
@@ -110,13 +108,7 @@ __device__ __forceinline__ MlpItem mlp_item(int item, int T, int G, int S) {
 // the ring D deep, refilling the slot it just consumed with group g + D, so
 // every MFMA's weights were requested D groups (4D MFMAs) earlier.  D | (g1-g0)
 // keeps it branch-free; refills past g1 are clamped in-bounds re-reads.
-#ifndef MLP_RING
-#define MLP_RING 4
-#endif
-#ifndef MLP_ACC2
-#define MLP_ACC2 0
-#endif
-constexpr int MLP_R = MLP_RING;  // B-fragment ring slots (the deepest D)
+constexpr int MLP_R = 4;  // B-fragment ring slots (the deepest D; a 9-slot ring measured slower)
 __device__ __forceinline__ void mlp_ring_fill(floatx4 (&ring)[MLP_R], const floatx4* bp, int g0, int g1) {
 #pragma unroll
   for (int u = 0; u < MLP_R; ++u) ring[u] = bp[(int64_t)min(g0 + u, g1 - 1) * 64];
@@ -128,26 +120,14 @@ __device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[MLP_R], const float* _
   // A fragments are read one group ahead so the LDS latency hides behind
   // the previous group's MFMAs
   floatx4 an = *reinterpret_cast<const floatx4*>(ap + 16 * g0);
-#if MLP_ACC2
-  // two accumulation chains (k-steps 0,2 / 1,3 of every group): half the
-  // dependent-MFMA latency per wave; summed once at the end
-  floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
-#endif
   for (int g = g0; g < g1; g += D) {
 #pragma unroll
     for (int u = 0; u < D; ++u) {
       const floatx4 av = an;
       an = *reinterpret_cast<const floatx4*>(ap + 16 * min(g + u + 1, g1 - 1));
       __builtin_amdgcn_sched_barrier(0);
-#if MLP_ACC2
-      acc = mfma16x16x4(av[0], ring[u][0], acc);
-      acc1 = mfma16x16x4(av[1], ring[u][1], acc1);
-      acc = mfma16x16x4(av[2], ring[u][2], acc);
-      acc1 = mfma16x16x4(av[3], ring[u][3], acc1);
-#else
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc = mfma16x16x4(av[j], ring[u][j], acc);
-#endif
       // refill the slot in place right after its MFMAs and pin it there: left
       // alone the scheduler sinks every refill to the end of the iteration
       // (or copies in-flight registers), which drains the ring each pass
@@ -155,12 +135,6 @@ __device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[MLP_R], const float* _
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-#if MLP_ACC2
-  acc[0] += acc1[0];
-  acc[1] += acc1[1];
-  acc[2] += acc1[2];
-  acc[3] += acc1[3];
-#endif
 }
 
 // The same contraction over exactly N k-groups, fully unrolled: straight-line
@@ -197,20 +171,14 @@ __device__ __forceinline__ void mlp_mac(floatx4 (&ring)[MLP_R], const float* ap,
   const int n = g1 - g0;  // wave-uniform
   if (unroll) {  // the DeepFM / DCN tower widths (429|432 -> 256 -> 128 -> 64 -> head)
     switch (n) {
-      // ring depth by the ring's size (MLP_RING >= 9: 9 / 8 / 8 / 4 groups ahead)
-      case 27: return mlp_mac_u<27, (MLP_R >= 9 ? 9 : 3)>(ring, ap, bp, g0, acc);
-      case 16: return mlp_mac_u<16, (MLP_R >= 9 ? 8 : MLP_SMALL_D)>(ring, ap, bp, g0, acc);
-      case 8: return mlp_mac_u<8, (MLP_R >= 9 ? 8 : MLP_SMALL_D)>(ring, ap, bp, g0, acc);
-      case 4: return mlp_mac_u<4, (MLP_R >= 9 ? 4 : MLP_SMALL_D)>(ring, ap, bp, g0, acc);
+      case 27: return mlp_mac_u<27, 3>(ring, ap, bp, g0, acc);
+      case 16: return mlp_mac_u<16, MLP_SMALL_D>(ring, ap, bp, g0, acc);
+      case 8: return mlp_mac_u<8, MLP_SMALL_D>(ring, ap, bp, g0, acc);
+      case 4: return mlp_mac_u<4, MLP_SMALL_D>(ring, ap, bp, g0, acc);
       case 2: return mlp_mac_u<2, 2>(ring, ap, bp, g0, acc);
       case 1: return mlp_mac_u<1, 1>(ring, ap, bp, g0, acc);
       default: break;
     }
-  }
-  if constexpr (MLP_R >= 9) {
-    if (n % 9 == 0) return mlp_mac_d<9>(ring, ap, bp, g0, g1, acc);
-    if (n % 8 == 0) return mlp_mac_d<8>(ring, ap, bp, g0, g1, acc);
-    if (n % 6 == 0) return mlp_mac_d<6>(ring, ap, bp, g0, g1, acc);
   }
   // (a 4-deep ring gets a full vmcnt(0) at its loop head from the compiler)
   if (n % 3 == 0) mlp_mac_d<3>(ring, ap, bp, g0, g1, acc);

@@ -262,7 +262,7 @@ hipError_t sort_pairs_u32(const uint32_t* key_in, const uint32_t* val_in, uint32
 }
 
 // ---- inclusive scan: per-tile sums, one-workgroup scan of the sums, per-tile
-// scan from its carry (tile = 4096 values, 16 per thread)
+// scan from its carry (tile = RX_TILE values: RX_T threads x RX_R per thread)
 __global__ __launch_bounds__(RX_T) void scan_tile_sums(const int32_t* __restrict__ in, int64_t n,
                                                        int32_t* __restrict__ sums) {
   __shared__ int32_t red[RX_T / 64];

@@ -20,6 +20,21 @@ int launch_status(const char* what);
 
 inline hipStream_t as_stream(rs_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// A kernel's dynamic-LDS opt-in (hipFuncSetAttribute) beyond the 64 KiB
+// default, per device: set[d] = the largest size set so far on device d (only
+// successful calls are recorded; a failure is retried at the next launch,
+// whose own launch status then reports it).
+struct LdsAttr {
+  size_t set[64] = {};
+};
+inline void lds_attr(LdsAttr& s, const void* kern, size_t lds) {
+  if (lds <= 64 * 1024) return;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (lds <= s.set[dev]) return;
+  if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess) s.set[dev] = lds;
+}
+
 #define RS_REQUIRE(cond, ...)            \
   do {                                   \
     if (!(cond)) {                       \

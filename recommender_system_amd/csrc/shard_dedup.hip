@@ -673,11 +673,8 @@ extern "C" int rs_shard_dedup_route(const void* ids, int id_kind, int64_t id_str
     with_id_kind(id_kind, [&](auto K) {
       constexpr int KI = decltype(K)::value;
       auto go = [&](auto kern) {
-        static bool lds_set[3][3] = {};
-        if (!lds_set[KI][LW]) {
-          (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-          lds_set[KI][LW] = true;
-        }
+        static LdsAttr lds_set[3][3];
+        lds_attr(lds_set[KI][LW], (const void*)kern, lds);
         kern<<<n_fields, T, lds, st>>>(ids, id_stride, field_offsets, field_vocab, n_fields, batch, rows_per_rank,
                                        world, key_in, val_in, cnt, strad, err_flag, ws + w.incl);
       };
@@ -743,11 +740,8 @@ extern "C" int rs_shard_dedup_grad(const float* grad, int64_t grad_stride, int n
     uint32_t* ko = reinterpret_cast<uint32_t*>(ws + w.key_out);
     int32_t* vo = reinterpret_cast<int32_t*>(ws + w.val_out);
     auto go = [&](auto kern) {
-      static bool lds_set[3] = {};
-      if (!lds_set[LW]) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        lds_set[LW] = true;
-      }
+      static LdsAttr lds_set[3];
+      lds_attr(lds_set[LW], (const void*)kern, lds);
       kern<<<n_fields, N2 / DH_KPL, lds, st>>>(rowg, fuh, n_fields, batch, cnt, ko, vo);
     };
     if (LW == 0) go(dedup_group_f<0>);

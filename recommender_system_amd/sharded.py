@@ -42,6 +42,21 @@ from . import _lib
 from ._lib import call, ptr
 
 
+def raise_flag(f, what, group=None, world=1):
+    """Raise for the rs_flag bits in the device flag `f` (reduced by MAX over
+    the group first when world > 1, so every rank takes the same branch):
+    RS_FLAG_LAYOUT (or any unknown bit) -> RSError, RS_FLAG_BAD_ID ->
+    IndexError (TF's InvalidArgumentError on an out-of-range Embedding id)."""
+    if world > 1:
+        dist.all_reduce(f, op=dist.ReduceOp.MAX, group=group)
+    bits = int(f.item())
+    if bits & ~_lib.FLAG_BAD_ID:
+        raise _lib.RSError(f"{what}: device error flag {bits:#x} (RS_FLAG_LAYOUT: the table's field row ranges "
+                           "overlap or decrease)")
+    if bits:
+        raise IndexError(f"{what}: embedding id out of range")
+
+
 class HipShardOps:
     """Local per-rank steps on librs_hip.so kernels."""
 
@@ -93,8 +108,8 @@ class HipShardOps:
         return logit
 
     def flags(self, bufs):
-        """[out-of-range id seen, slot overflow seen] (device tensor; resets)."""
-        v = torch.stack([self.err[0], bufs["overflow"][0]]).clamp_(max=1)
+        """[rs_flag bits of the id flag, slot overflow seen] (device tensor; resets)."""
+        v = torch.stack([self.err[0], bufs["overflow"][0].clamp(max=1)])
         self.err.zero_()
         bufs["overflow"].zero_()
         return v
@@ -312,8 +327,10 @@ class HipShardOps:
         model.dnn._weights_changed()
 
     def bad_flag(self):
-        """[out-of-range id seen] (device tensor; resets)."""
-        v = self.err.clamp(max=1)
+        """The device error flag's rs_flag bits (device tensor; resets):
+        RS_FLAG_BAD_ID for an out-of-range id, RS_FLAG_LAYOUT for a table
+        layout the dedup route cannot use."""
+        v = self.err.clone()
         self.err.zero_()
         return v
 
@@ -322,9 +339,7 @@ class HipShardOps:
         self.err.zero_()
 
     def check(self):
-        if int(self.err.item()):
-            self.err.zero_()
-            raise IndexError("sharded lookup: embedding id out of range")
+        raise_flag(self.bad_flag(), "sharded lookup")
 
 
 class ShardedEmbeddingFM:
@@ -417,6 +432,8 @@ class ShardedEmbeddingFM:
         peer), no overflow case, no host sync unless ``check``."""
         B = ids.shape[0]
         pb = self._pbufs(B)
+        if check:
+            self.ops.clear_flags()  # a checked step reports its own ids only
         exchange = self.world > 1 or self._force_exchange
         send = self.ops.field_route(self, ids, pb["send"])
         recv = send
@@ -430,11 +447,7 @@ class ShardedEmbeddingFM:
         logit = out if out is not None else torch.empty(B, 1, dtype=torch.float32, device=self.device)
         logit = self.ops.combine(self, part, dense, logit)
         if check:
-            f = self.ops.bad_flag()
-            if self.world > 1:
-                dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
-            if bool(f.item()):
-                raise IndexError("sharded lookup: embedding id out of range")
+            raise_flag(self.ops.bad_flag(), "sharded lookup", self.group, self.world)
         return logit
 
     # -- training: compile_fit's SGD on the FM logit, data parallel
@@ -484,6 +497,8 @@ class ShardedEmbeddingFM:
         B = ids.shape[0]
         W = self.world
         pb, tb = self._pbufs(B), self._tbufs(B)
+        if check:
+            self.ops.clear_flags()
         exchange = W > 1 or self._force_exchange
         send = self.ops.field_route(self, ids, pb["send"])
         recv = send
@@ -508,11 +523,7 @@ class ShardedEmbeddingFM:
             dist.all_reduce(grad, group=self.group)
         self.ops.apply(self, grad, lr, reg_w, reg_v)
         if check:
-            f = self.ops.bad_flag()
-            if W > 1:
-                dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
-            if bool(f.item()):
-                raise IndexError("sharded lookup: embedding id out of range")
+            raise_flag(self.ops.bad_flag(), "sharded lookup", self.group, W)
         return loss
 
     # -- the pipelined partial protocol: one all-to-all per batch
@@ -567,6 +578,8 @@ class ShardedEmbeddingFM:
         must pass the same number of batches.  Returns [logit [B,1] per batch]."""
         n = len(batches)
         outs = [torch.empty(ids.shape[0], 1, dtype=torch.float32, device=self.device) for _, ids in batches]
+        if check:
+            self.ops.clear_flags()
         if n:
             self.pipe_route(batches[0][1])
         for t in range(n + 1):
@@ -575,11 +588,7 @@ class ShardedEmbeddingFM:
             nxt = batches[t + 1] if t + 1 < n else None
             self.pipe_step(prev, cur, nxt)
         if check:
-            f = self.ops.bad_flag()
-            if self.world > 1:
-                dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
-            if bool(f.item()):
-                raise IndexError("sharded lookup: embedding id out of range")
+            raise_flag(self.ops.bad_flag(), "sharded lookup", self.group, self.world)
         return outs
 
     # -- the fixed-capacity row exchange (returns rows; forward_slots)
@@ -656,6 +665,8 @@ class ShardedEmbeddingFM:
         every lookup come back to the requester: EmbedLayer semantics).
         check=True: one host sync at the end of the step; a slot overflow is
         redone exactly, a bad id raises."""
+        if check:
+            self.ops.clear_flags()
         got, slot_of = self.exchange_slots(ids)
         bufs = self._bufs(ids.shape[0])
         logit = self.ops.slots_fm(got, slot_of, dense, self.F, self.k, self.prepared, self.w0, self.kfm, bufs,
@@ -666,9 +677,9 @@ class ShardedEmbeddingFM:
             f = self.ops.flags(bufs)
             if self.world > 1:
                 dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
-            bad, overflow = (bool(x) for x in f.tolist())
+            bad, overflow = f.tolist()
             if bad:
-                raise IndexError("sharded lookup: embedding id out of range")
+                raise_flag(torch.tensor([bad]), "sharded lookup")
             if overflow:
                 return self.forward_exact(dense, ids)
         return logit
@@ -900,16 +911,14 @@ class ShardedDeepFM:
         outs = [torch.empty(d.shape[0], 1, dtype=torch.float32, device=self.device) for d, _ in batches]
         if not batches:
             return outs
+        if check:
+            self.ops.clear_flags()  # an earlier unchecked step may have left the sticky flag set
         self.exchange(batches[0][1], self._pipe_bufs(batches[0][1].shape[0], 0))
         for t, (dense, _) in enumerate(batches):
             nxt = (batches[t + 1][1], (t + 1) % 2) if t + 1 < len(batches) else None
             self.pipe_step((dense, outs[t], t % 2), nxt)
         if check:
-            f = self.ops.bad_flag()
-            if self.world > 1:
-                dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
-            if bool(f.item()):
-                raise IndexError("sharded DeepFM: embedding id out of range")
+            raise_flag(self.ops.bad_flag(), "sharded DeepFM", self.group, self.world)
         return outs
 
     def serve(self, recv, reply):
@@ -1032,11 +1041,7 @@ class ShardedDeepFM:
             dist.all_reduce(tb["flat"], group=self.group)
         self.ops.deepfm_apply(self, tb, lr)
         if check:
-            f = self.ops.bad_flag()
-            if W > 1:
-                dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
-            if bool(f.item()):
-                raise IndexError("sharded DeepFM: embedding id out of range")
+            raise_flag(self.ops.bad_flag(), "sharded DeepFM", self.group, W)
         return loss
 
     def forward(self, inputs, check=True, out=None):
@@ -1049,6 +1054,8 @@ class ShardedDeepFM:
         B = ids.shape[0]
         if out is None:
             out = torch.empty(B, 1, dtype=torch.float32, device=self.device)
+        if check:
+            self.ops.clear_flags()
         if not sh.exchanges and not self.force_rows and isinstance(self.ops, HipShardOps):
             self.ops.deepfm_table(self, ids, dense, out)  # world 1: the shard is the whole table
         else:
@@ -1063,11 +1070,7 @@ class ShardedDeepFM:
                 dist.all_to_all_single(got, reply, group=self.group)
             self.finish(dense, got, rb, out)
         if check:
-            f = self.ops.bad_flag()
-            if self.world > 1:
-                dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
-            if bool(f.item()):
-                raise IndexError("sharded DeepFM: embedding id out of range")
+            raise_flag(self.ops.bad_flag(), "sharded DeepFM", self.group, self.world)
         return out
 
     __call__ = forward
