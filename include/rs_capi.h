@@ -67,7 +67,10 @@ enum rs_flag {
 enum rs_option {
   RS_OPT_EMBED_FM_KERNEL = 0, /* rs_embed_fm_fwd kernel (id inputs, no x_out): 0 = MFMA K-split,
                                  1 = VALU/DPP persistent 8-sample tiles, 2 / 3 = MFMA persistent
-                                 16-sample tiles (2 / 1 resident per CU); shapes a kernel does not
+                                 16-sample tiles (2 / 1 resident per CU); rs_embed_fm_fwd_hm at
+                                 k = 16: 4 / 5 / 6 = the K-split kernel with rows loaded by 4
+                                 adjacent lanes each (second pass after the first's MFMAs / on
+                                 its rows' arrival / with the first); shapes a kernel does not
                                  cover run the K-split one.  See DESIGN.md 4.1                    */
   RS_OPT_MLP_UNROLL = 1,      /* fused MLP towers (rs_mlp_fwd, rs_deepfm_fwd, rs_dcn_fwd): 1 (the
                                  default) = the k-group loop of the common layer widths fully

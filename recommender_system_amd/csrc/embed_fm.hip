@@ -105,7 +105,7 @@ __global__ void fm_prepare_generic(const float* __restrict__ w1, const float* __
   do {                                                                                       \
     __builtin_amdgcn_sched_barrier(0);                                                       \
     if (a.dbg && lane == 0)                                                                  \
-      a.dbg[((int64_t)blockIdx.x * NW + w) * 12 + (i)] = __builtin_amdgcn_s_memrealtime();  \
+      a.dbg[((int64_t)blockIdx.x * NW + w) * 16 + (i)] = __builtin_amdgcn_s_memrealtime();  \
     __builtin_amdgcn_sched_barrier(0);                                                       \
   } while (0)
 #define RS_USE(x) asm volatile("" ::"v"(x))
@@ -129,9 +129,20 @@ __global__ void fm_prepare_generic(const float* __restrict__ w1, const float* __
 // row stride tw->rs) instead of x_out, and the DNN tower of mlp_tower.hpp runs
 // on it, closed by sigmoid(c0*dnn + c1*fm) (model/deepFM.py:24-30).
 // A workgroup owns one 16-sample MFMA row tile.
-template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, bool PF = false, bool KA = false>
+// QV (kernarg kernel, k = 16 only): 0 = rows loaded in the MFMA A layout
+// (lane = sample + 16 chunk: a 16-lane quarter-wave touches 16 rows); 1..3 =
+// rows loaded with 4 ADJACENT lanes per row (lane = 4 sample + chunk: a
+// quarter-wave touches 4 whole rows) and moved to the A layout in registers
+// (swap_hi4 / swap_lo4: 4 v_permlane*_swap + 16 DPP/select per field; MFMA
+// row r then holds sample ((r & 3) << 2) | (r >> 2), the B fragments take the
+// matching element order by swap_hi4).  The second pass's rows are requested
+// 1: after the first pass's MFMAs, 2: when the first pass's rows have
+// arrived, 3: with the first pass's.
+template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, bool PF = false, bool KA = false, int QV = 0>
 __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArgs* tw, const int tile,
                                               const FieldMeta* km = nullptr) {
+  constexpr bool QL = QV > 0;
+  static_assert(!QL || (KV == 4 && KA && !TW && KIND < 3), "adjacent-lane rows: kernarg FM kernel, k = 16");
   // MC > 0: field slots per wave and pass (owner kernels with few fields)
   constexpr int MAXC0 = MC > 0 ? MC : 128 / (NW * KV);
   constexpr int MAXC = MAXC0 < 1 ? 1 : (MAXC0 > 8 ? 8 : MAXC0);
@@ -142,13 +153,19 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int s = lane & 15;   // A: sample row of the tile; B/C: column
+  const int s = lane & 15;   // A: row of the tile; B/C: column
   const int kk = lane >> 4;  // k-slot
-  const int64_t bt = (int64_t)tile * 16 + s;
+  const int sm = QL ? (((s & 3) << 2) | (s >> 2)) : s;  // the sample of MFMA row s
+  const int64_t bt = (int64_t)tile * 16 + sm;
   const bool valid = bt < a.batch;
   // Padded lanes of the last tile recompute the last sample: an MFMA output
   // row depends only on its own A row, so they never touch valid outputs.
   const int64_t b = bt < a.batch ? bt : a.batch - 1;
+  // the sample / chunk whose row piece this lane LOADS (QL: lane = 4 sample + chunk)
+  const int64_t btl = QL ? (int64_t)tile * 16 + (lane >> 2) : bt;
+  const bool valid_ld = btl < a.batch;
+  const int64_t bl = btl < a.batch ? btl : a.batch - 1;
+  const int qc = QL ? (lane & 3) : kk;
   const int d = a.nd + a.F * a.k;
   // w0 is requested now, not behind the rows (a dependent load at the end)
   const float w0v = OWNER ? 0.f : a.w0[0];
@@ -271,6 +288,19 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     }
   };
   auto norms = [&](Pass& P) {
+    if constexpr (QL) {
+      // B fragment lane (kk, col) register t: v[4 kk + t] -> v[4 t + kk], the
+      // element order of the A values after swap_hi4 / swap_lo4
+#pragma unroll
+      for (int j = 0; j < MAXC; ++j)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          float t4[4] = {P.bw[j][nt].v[0], P.bw[j][nt].v[1], P.bw[j][nt].v[2], P.bw[j][nt].v[3]};
+          swap_hi4(t4);
+#pragma unroll
+          for (int tp = 0; tp < 4; ++tp) P.bw[j][nt].v[tp] = t4[tp];
+        }
+    }
     // |v_e|^2 for this lane's element e: the B lanes of DPP row kk hold
     // v[e][0..15] — the same row as the A lane that holds x_e.
 #pragma unroll
@@ -308,7 +338,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
         } else if constexpr (KA) {  // kernarg metadata: scalar loads, wave-uniform field
           offc[j] = km->off[P.cj[j]];
           vocc[j] = km->voc[P.cj[j]];
-          P.rid[j] = I::load(a.ids, b * a.id_stride + P.cj[j]);
+          P.rid[j] = I::load(a.ids, bl * a.id_stride + P.cj[j]);
         } else {
           const int cv = min(cg + j * NW + wv, a.F - 1);
           offc[j] = a.offs[cv];
@@ -323,7 +353,8 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     if (!fetched) fetch_ids(cg, P);
     const int64_t* offc = P.off;
     const int64_t* vocc = P.voc;
-    RS_STAMP(6);
+    if (cg == 0) RS_STAMP(6);
+    else RS_STAMP(10);
     // row gather: KV consecutive floats of the sample's row per lane
     int64_t row[MAXC];
 #pragma unroll
@@ -338,25 +369,46 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       }
     }
     RS_USE(row[MAXC - 1]);
-    RS_STAMP(1);
+    if (cg == 0) RS_STAMP(1);
+    else RS_STAMP(11);
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
 #ifdef RS_DIAG_STAMPS
       if ((a.ablate & 8) && cg + j * NW + w >= a.F) { P.xs[j].zero(); continue; }
 #endif
-      P.xs[j].load_nt(a.table + row[j] * a.k + KV * kk);
+      P.xs[j].load_nt(a.table + row[j] * a.k + KV * qc);
     }
   };
   auto consume = [&](int cg, Pass& P) {
     RS_USE(P.xs[MAXC - 1].v[KV - 1]);
     RS_USE(P.bw[MAXC - 1][0].v[KV - 1]);
-    RS_STAMP(2);
+    if (cg == 0) RS_STAMP(2);
+    else RS_STAMP(12);
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
       const bool live = cg + j * NW + w < a.F;
       if constexpr (OWNER) bad |= live && !P.ok[j] && P.rid[j] != -1;
       else bad |= live && !P.ok[j];
       const bool use = live && P.ok[j];
+      if constexpr (QL) {
+        float x4[4];
+#pragma unroll
+        for (int tp = 0; tp < 4; ++tp) x4[tp] = use ? P.xs[j].v[tp] : 0.f;
+        if (a.x_out && live && valid_ld) {  // before the exchange: one 64-B row per lane quad
+          float* xo = a.x_out + bl * d + a.nd + P.cj[j] * a.k + 4 * qc;
+#pragma unroll
+          for (int tp = 0; tp < 4; ++tp) xo[tp] = x4[tp];
+        }
+        swap_hi4(x4);
+        swap_lo4(x4, lane);
+#pragma unroll
+        for (int tp = 0; tp < 4; ++tp) {
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(x4[tp], P.bw[j][nt].v[tp], acc[nt]);
+          qn = fmaf(x4[tp] * x4[tp], P.nrm[j][tp], qn);
+        }
+        continue;
+      }
 #pragma unroll
       for (int tp = 0; tp < KV; ++tp) {
         const float xv = use ? P.xs[j].v[tp] : 0.f;
@@ -381,6 +433,9 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
         for (int tp = 0; tp < KV; ++tp) xo[tp] = P.ok[j] ? P.xs[j].v[tp] : 0.f;
       }
     }
+    RS_USE(acc[0][0]);
+    if (cg == 0) RS_STAMP(13);
+    else RS_STAMP(14);
   };
   // one slot per wave: a wave with no field left in a pass stops there (a
   // wave-uniform exit; nothing after the loop needs its slot)
@@ -411,11 +466,16 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       // them with the first pass's was slower, 6.19 vs 5.82 us at 4096 —
       // the r1 finding that two row bursts beat one, again)
       issue_rows(0, P0, true);
+      if (QV == 3 && two) issue_rows(PS, P1, true);
       norms(P0);
       if (two) norms(P1);
+      if (QV == 2 && two) {
+        asm volatile("" ::"v"(P0.xs[0].v[KV - 1]));  // the first pass's rows have arrived
+        issue_rows(PS, P1, true);
+      }
       consume(0, P0);
       if (two) {
-        issue_rows(PS, P1, true);
+        if (QV < 2) issue_rows(PS, P1, true);
         consume(PS, P1);
         for (int cg = 2 * PS; has_pass(cg); cg += PS) {
           issue_b(cg, P0);
@@ -465,7 +525,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   }
   RS_USE(acc[0][0]);
   RS_STAMP(3);
-  if (__any(bad && valid) && lane == 0) flag_error(a.err);
+  if (__any(bad && valid_ld) && lane == 0) flag_error(a.err);
 
 #ifdef RS_DIAG_STAMPS
   if (a.ablate & 4) {
@@ -499,7 +559,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       t += __shfl_xor(t, 16);
       lin += __shfl_xor(lin, 16);
     }
-    const int64_t bb = (int64_t)tile * 16 + smp;
+    const int64_t bb = (int64_t)tile * 16 + (QL ? (((smp & 3) << 2) | (smp >> 2)) : smp);
     if constexpr (OWNER) {
       // partial record: column sums as they stand, the q term row-summed
       float q = col < NW ? qs[col][smp] : 0.f;
@@ -531,9 +591,9 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
 // the field metadata by value (rs_embed_fm_fwd_hm): each wave loads its own
 // fields' ids and reads (offset, vocab) through scalar kernarg loads — no LDS
 // id tile, no barrier, no per-wave metadata loads from one hot L2 line
-template <int KV, int NT, int NW, int KIND, bool PF>
+template <int KV, int NT, int NW, int KIND, bool PF, int QV = 0>
 __global__ __launch_bounds__(NW * 64) void embed_fm_mfma_ka(EmbedFmArgs a, FieldMeta m) {
-  embed_fm_body<KV, NT, NW, KIND, false, 1, PF, true>(a, nullptr, blockIdx.x, &m);
+  embed_fm_body<KV, NT, NW, KIND, false, 1, PF, true, QV>(a, nullptr, blockIdx.x, &m);
 }
 
 // ---- sharded FM, partial protocol: combine (requester side) as a block part
@@ -834,6 +894,14 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st, const FieldMe
   // with both passes' ids requested together; profiles/r3_ab_kernarg_*)
   // 16 waves (13: 6.20 us, 9: 6.78 vs 5.76 at 4096; profiles/r3_ab_kernarg_waves_4096.json)
   if (hm && a.F <= 32 && KIND != 3 && grid <= 512) {
+    if constexpr (KV == 4 && KIND < 3) {
+      switch (opt(RS_OPT_EMBED_FM_KERNEL)) {  // adjacent-lane row loads (embed_fm_body QV)
+        case 4: embed_fm_mfma_ka<KV, NT, 16, KIND, true, 1><<<grid, 16 * 64, 0, st>>>(a, *hm); return;
+        case 5: embed_fm_mfma_ka<KV, NT, 16, KIND, true, 2><<<grid, 16 * 64, 0, st>>>(a, *hm); return;
+        case 6: embed_fm_mfma_ka<KV, NT, 16, KIND, true, 3><<<grid, 16 * 64, 0, st>>>(a, *hm); return;
+        default: break;
+      }
+    }
     embed_fm_mfma_ka<KV, NT, 16, KIND, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
     return;
   }
@@ -966,7 +1034,8 @@ extern "C" int rs_embed_fm_fwd_hm(const void* ids, int id_kind, int64_t id_strid
                                   int* err_flag, rs_stream_t stream) {
   if (batch == 0) return RS_OK;
   RS_REQUIRE(field_offsets_host && field_vocab_host, "rs_embed_fm_fwd_hm: host metadata missing");
-  if (n_fields > 32 || opt(RS_OPT_EMBED_FM_KERNEL) != 0)
+  const int variant = opt(RS_OPT_EMBED_FM_KERNEL);
+  if (n_fields > 32 || (variant >= 1 && variant <= 3))
     return rs_embed_fm_fwd(ids, id_kind, id_stride, dense, dense_stride, nd, table, field_offsets, field_vocab,
                            n_fields, k, prepared, w0, kfm, logit, x_out, batch, err_flag, stream);
   RS_REQUIRE(batch >= 0 && nd >= 0 && n_fields >= 0 && kfm >= 1, "rs_embed_fm_fwd_hm: bad shape");
@@ -1130,6 +1199,12 @@ extern "C" int rs_diag_embed_fm_fwd(const void* ids, int id_kind, int64_t id_str
   a.batch = batch;
   a.dbg = dbg;
   a.ablate = getenv("RS_ABLATE") ? atoi(getenv("RS_ABLATE")) : 0;
+  if (getenv("RS_DIAG_HM") && n_fields <= 32) {  // the kernarg-metadata kernel (rs_embed_fm_fwd_hm)
+    FieldMeta m{};
+    (void)hipMemcpy(m.off, field_offsets, n_fields * sizeof(int64_t), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(m.voc, field_vocab, n_fields * sizeof(int64_t), hipMemcpyDeviceToHost);
+    return run_embed_fm(a, g, id_kind, as_stream(stream), "rs_diag_embed_fm_fwd", &m);
+  }
   return run_embed_fm(a, g, id_kind, as_stream(stream), "rs_diag_embed_fm_fwd");
 }
 #endif

@@ -41,7 +41,10 @@ def main():
     dense_rec, field_rec = 64 + 4, 64 * 4 + 16
     field_base = DB * dense_rec
     NP = 64
-    for B in (4096, 16384):
+    hmv = [int(x) for x in os.environ.get("DIAG_HM_VARIANTS", "").split(",") if x]
+    hoff = (C.c_int64 * F)(*[c * V for c in range(F)])
+    hvoc = (C.c_int64 * F)(*([V] * F))
+    for B in [int(x) for x in os.environ.get("DIAG_BATCHES", "4096,16384").split(",")]:
         pool = torch.randint(0, V, (NP, B, F), dtype=torch.int32, device=dev)
         dense = torch.rand(NP, B, nd, device=dev)
         out = torch.empty(B * F, device=dev)
@@ -62,6 +65,15 @@ def main():
                                                         nd, table.data_ptr(), offs.data_ptr(), voc.data_ptr(), F, k,
                                                         prep.data_ptr(), w0.data_ptr(), kfm, logit.data_ptr(), None, B,
                                                         err.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        for hv in hmv:  # the product's headline entry (kernarg metadata), RS_OPT_EMBED_FM_KERNEL = hv
+            def hm_fn(i, hv=hv):
+                _lib.set_option(_lib.OPT_EMBED_FM_KERNEL, hv)
+                lib.rs_embed_fm_fwd_hm(pool[i % NP].data_ptr(), 0, F, dense[i % NP].data_ptr(), nd, nd,
+                                       table.data_ptr(), offs.data_ptr(), voc.data_ptr(), C.addressof(hoff),
+                                       C.addressof(hvoc), F, k, prep.data_ptr(), w0.data_ptr(), kfm, logit.data_ptr(),
+                                       None, B, err.data_ptr(), torch.cuda.current_stream().cuda_stream)
+                _lib.set_option(_lib.OPT_EMBED_FM_KERNEL, 0)
+            fns[f"hm{hv}"] = hm_fn
         # correctness of the ablations that keep the arithmetic (bits 0, 4, 5 only)
         chk = {}
         fns["embed_fm"](0)

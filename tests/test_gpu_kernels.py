@@ -179,11 +179,17 @@ def test_embed_fm_kernel_variants(gpu, embed_fm_variant, k, kfm, F, nd, B, idt):
     (16, 16, 20, 5, 130, "i32", False),     # two MFMA column tiles
     (16, 10, 26, 13, 9000, "i32", False),   # > 512 tiles: the device-metadata kernel
     (16, 10, 33, 13, 64, "i32", False),     # F > 32: the device-metadata kernel
+    (16, 10, 26, 13, 4093, "i64", True),    # ragged last tile, x emitted
+    (16, 10, 17, 0, 50, "f32", False),      # no dense block, one pass + a partial pass
 ])
-def test_embed_fm_host_meta(gpu, k, kfm, F, nd, B, idt, with_x):
+@pytest.mark.parametrize("variant", [0, 4, 5, 6])
+def test_embed_fm_host_meta(gpu, k, kfm, F, nd, B, idt, with_x, variant):
     """rs_embed_fm_fwd_hm (field metadata also as kernel arguments, per-wave
     id loads, no id tile) == rs_embed_fm_fwd bit for bit (logit and x) and ==
-    the oracle; an out-of-range id sets the flag."""
+    the oracle; an out-of-range id sets the flag.  Variants 4 / 5 / 6
+    (RS_OPT_EMBED_FM_KERNEL; k = 16: rows loaded by 4 adjacent lanes, moved
+    to the MFMA layout in registers, so the MFMA element order differs):
+    x bit for bit, the logit within the fp32 tolerance of the oracle."""
     import ctypes as C
     from recommender_system_amd import _lib
     rng = np.random.default_rng(B * 7 + F)
@@ -223,18 +229,28 @@ def test_embed_fm_host_meta(gpu, k, kfm, F, nd, B, idt, with_x):
 
     ref_logit, ref_x = run(ids, False)
     assert err.item() == 0
-    got_logit, got_x = run(ids, True)
-    assert err.item() == 0
-    assert torch.equal(got_logit, ref_logit)
-    if with_x:
-        assert torch.equal(got_x, ref_x)
-    tables = [table[o:o + vv] for o, vv in zip(offs, vocabs)]
-    x64 = np.concatenate([dense, O.embed_layer(ids, tables, np.float64)], 1)
-    assert_scaled_close(got_logit, O.fm_layer(x64, w0, w1, v)[:, 0], what="embed_fm host meta")
-    bad = ids.copy()
-    bad[B - 1, F - 1] = vocabs[F - 1]
-    run(bad, True)
-    assert err.item() != 0
+    prev = _lib.set_option(_lib.OPT_EMBED_FM_KERNEL, variant)
+    try:
+        got_logit, got_x = run(ids, True)
+        assert err.item() == 0
+        if variant == 0 or k != 16:
+            assert torch.equal(got_logit, ref_logit)
+        if with_x:
+            assert torch.equal(got_x, ref_x)
+        tables = [table[o:o + vv] for o, vv in zip(offs, vocabs)]
+        x64 = np.concatenate([dense, O.embed_layer(ids, tables, np.float64)], 1)
+        assert_scaled_close(got_logit, O.fm_layer(x64, w0, w1, v)[:, 0], what=f"embed_fm host meta v{variant}")
+        bad = ids.copy()
+        bad[B - 1, F - 1] = vocabs[F - 1]
+        run(bad, True)
+        assert err.item() != 0
+        err.zero_()
+        bad = ids.copy()
+        bad[B // 2, 0] = -1
+        run(bad, True)
+        assert err.item() != 0
+    finally:
+        _lib.set_option(_lib.OPT_EMBED_FM_KERNEL, prev)
 
 
 def test_embed_fm_packed_float_X_and_oor(gpu):
