@@ -76,7 +76,14 @@ enum rs_option {
                                  default) = the k-group loop of the common layer widths fully
                                  unrolled (no loop-head wait on the weight ring), 0 = the looped
                                  form.  See DESIGN.md 4.5                                         */
-  RS_OPT_COUNT = 2
+  RS_OPT_GATHER_ROWS = 2,     /* rs_gather_rows at k = 16: 0 = 256-thread workgroups, 4 lanes per
+                                 row; 1 = 64-thread workgroups; 2 = two rows per lane quad in
+                                 flight; 3 = 2 with write-through (sc1) row stores.  DESIGN.md 4.6 */
+  RS_OPT_SHARD_ROUTE = 3,     /* rs_shard_field_route / rs_shard_row_route / the route part of
+                                 rs_shard_fm_pipe: 0 (the default) = one thread per lookup with
+                                 the field metadata staged in LDS, 1 = one thread per record word
+                                 (the round-3 form).  Same words either way.  DESIGN.md 4.6        */
+  RS_OPT_COUNT = 4
 };
 
 /* ------------------------------------------------------------------ meta */

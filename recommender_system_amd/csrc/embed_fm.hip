@@ -665,6 +665,7 @@ __device__ __forceinline__ void fm_combine_part(const CombineArgs& c, int blk, i
 // all-to-all.  Any part may be empty.
 struct PipeArgs {
   int owner_blocks, route_blocks, combine_blocks;
+  int route_lookup;  // 1: lookup_route_part (one thread per lookup), 0: field_route_part
   RouteArgs r;
   CombineArgs c;
 };
@@ -675,7 +676,9 @@ __global__ __launch_bounds__(NW * 64) void shard_fm_pipe(EmbedFmArgs a, PipeArgs
   if (bid < p.owner_blocks) {
     embed_fm_body<KV, NT, NW, 4, false, MC>(a, nullptr, bid);
   } else if (bid < p.owner_blocks + p.route_blocks) {
-    field_route_part<NW * 64>(p.r, bid - p.owner_blocks, p.route_blocks);
+    __shared__ RouteLds L;
+    if (p.route_lookup) lookup_route_part<NW * 64>(p.r, bid - p.owner_blocks, p.route_blocks, L);
+    else field_route_part<NW * 64>(p.r, bid - p.owner_blocks, p.route_blocks);
   } else {
     fm_combine_part<NW * 64>(p.c, bid - p.owner_blocks - p.route_blocks, p.combine_blocks);
   }
@@ -1222,7 +1225,10 @@ template <int KV, int NT, int NW, int MC>
 static void launch_pipe4(const EmbedFmArgs& a, PipeArgs p, hipStream_t st) {
   const int T = NW * 64;
   p.owner_blocks = a.F > 0 ? (int)((a.batch + 15) / 16) : 0;
-  if (p.route_blocks) p.route_blocks = (int)std::min<int64_t>((p.r.total + T - 1) / T, 4096);
+  if (p.route_blocks) {
+    const int64_t items = p.route_lookup ? (int64_t)p.r.batch * p.r.n_fields : p.r.total;
+    p.route_blocks = (int)std::min<int64_t>((items + T - 1) / T, 4096);
+  }
   if (p.combine_blocks) p.combine_blocks = (int)std::min<int64_t>((p.c.batch * 16 + T - 1) / T, 4096);
   const int grid = p.owner_blocks + p.route_blocks + p.combine_blocks;
   if (grid) shard_fm_pipe<KV, NT, NW, MC><<<grid, T, 0, st>>>(a, p);
@@ -1393,6 +1399,10 @@ extern "C" int rs_shard_fm_pipe(const int32_t* recv, int field_lo, int n_owned, 
     p.route_blocks = 1;
     p.r = RouteArgs{ids_next, id_kind, id_stride, field_offsets, field_vocab, rows_per_rank, owner_fields,
                     slot_stride, (int)batch, R, send, err_flag, (int64_t)world * batch * slot_stride};
+    p.r.n_fields = n_fields;
+    p.r.world = world;
+    p.route_lookup = opt(RS_OPT_SHARD_ROUTE) == 0 && n_fields <= RT_MAXF && world <= RT_MAXW &&
+                     batch * n_fields < ((int64_t)1 << 31);
   }
   if (logit_prev) {
     p.combine_blocks = 1;
