@@ -197,6 +197,19 @@ int rs_embed_cross_fwd(const void* ids, int id_kind, int64_t id_stride,
                        int n_layers, const float* prepared, float* out,
                        int64_t out_stride, int64_t batch, int* err_flag,
                        rs_stream_t stream);
+/* The same with the fields' (offset, vocab) also on the host: at k = 16 and
+ * <= 32 fields they travel as kernel arguments and the rows come in through
+ * the headline kernel's front end (per-wave field ids, no id tile; DESIGN.md
+ * 4.2); otherwise identical to rs_embed_cross_fwd.  Bit-identical outputs. */
+int rs_embed_cross_fwd_hm(const void* ids, int id_kind, int64_t id_stride,
+                          const float* dense, int64_t dense_stride, int nd,
+                          const float* table, const int64_t* field_offsets,
+                          const int64_t* field_vocab,
+                          const int64_t* field_offsets_host,
+                          const int64_t* field_vocab_host, int n_fields, int k,
+                          int n_layers, const float* prepared, float* out,
+                          int64_t out_stride, int64_t batch, int* err_flag,
+                          rs_stream_t stream);
 
 /* Fused DCN forward (model/dcn.py:24-34) in one launch: x0 in LDS, CrossNet
  * folded into its contraction, the DNN tower on the same tile, head
@@ -216,6 +229,16 @@ int rs_dcn_fwd(const void* ids, int id_kind, int64_t id_stride,
                const float* cross_prepared, int n_layers, const int* dims,
                const int* acts, const float* mlp_prepared, float* out,
                int64_t batch, int* err_flag, rs_stream_t stream);
+/* rs_dcn_fwd with host field metadata (kernel-argument front end, as
+ * rs_embed_cross_fwd_hm).  Bit-identical outputs. */
+int rs_dcn_fwd_hm(const void* ids, int id_kind, int64_t id_stride,
+                  const float* dense, int64_t dense_stride, int nd,
+                  const float* table, const int64_t* field_offsets,
+                  const int64_t* field_vocab, const int64_t* field_offsets_host,
+                  const int64_t* field_vocab_host, int n_fields, int k,
+                  int n_cross, const float* cross_prepared, int n_layers,
+                  const int* dims, const int* acts, const float* mlp_prepared,
+                  float* out, int64_t batch, int* err_flag, rs_stream_t stream);
 
 /* ----------------------------------------------- PNN inner product (a11)
  * InnerProductLayer.call (layer/interaction.py:170-183) on e[B,F,k]:
@@ -231,6 +254,15 @@ int rs_embed_inner_fwd(const void* ids, int id_kind, int64_t id_stride,
                        const int64_t* field_vocab, int n_fields, int k,
                        float* out, int64_t out_stride, int64_t batch,
                        int* err_flag, rs_stream_t stream);
+/* rs_embed_inner_fwd with host field metadata (kernel-argument front end at
+ * k = 16, <= 32 fields).  Bit-identical outputs. */
+int rs_embed_inner_fwd_hm(const void* ids, int id_kind, int64_t id_stride,
+                          const float* table, const int64_t* field_offsets,
+                          const int64_t* field_vocab,
+                          const int64_t* field_offsets_host,
+                          const int64_t* field_vocab_host, int n_fields, int k,
+                          float* out, int64_t out_stride, int64_t batch,
+                          int* err_flag, rs_stream_t stream);
 
 /* OuterProductLayer (layer/interaction.py:186-215): out[b,p] =
  * sum_{a,j} e[b,row_p,j] W[a,p,j] e[b,col_p,a] with W the Keras weight
@@ -252,6 +284,15 @@ int rs_embed_product_fwd(const void* ids, int id_kind, int64_t id_stride,
                          int inner, const float* outer_prepared, float* out,
                          int64_t out_stride, int64_t batch, int* err_flag,
                          rs_stream_t stream);
+/* rs_embed_product_fwd with host field metadata (as rs_embed_inner_fwd_hm). */
+int rs_embed_product_fwd_hm(const void* ids, int id_kind, int64_t id_stride,
+                            const float* table, const int64_t* field_offsets,
+                            const int64_t* field_vocab,
+                            const int64_t* field_offsets_host,
+                            const int64_t* field_vocab_host, int n_fields, int k,
+                            int inner, const float* outer_prepared, float* out,
+                            int64_t out_stride, int64_t batch, int* err_flag,
+                            rs_stream_t stream);
 
 /* ---------------------------------------------- DIN attention unit (a13)
  * Attention.call (layer/interaction.py:369-406), 'prelu' mode:

@@ -40,14 +40,18 @@ SIGNATURES = {
     "rs_cross_prepare": (I, [P, P, I, I, P, P]),
     "rs_cross_fwd": (I, [P, L, I, I, P, P, L, L, P]),
     "rs_embed_cross_fwd": (I, [P, I, L, P, L, I, P, P, P, I, I, I, P, P, L, L, P, P]),
+    "rs_embed_cross_fwd_hm": (I, [P, I, L, P, L, I, P, P, P, P, P, I, I, I, P, P, L, L, P, P]),
     "rs_dcn_fused_ok": (I, [I, I, I, I, I, P]),
     "rs_dcn_fwd": (I, [P, I, L, P, L, I, P, P, P, I, I, I, P, I, P, P, P, P, L, P, P]),
+    "rs_dcn_fwd_hm": (I, [P, I, L, P, L, I, P, P, P, P, P, I, I, I, P, I, P, P, P, P, L, P, P]),
     "rs_inner_product_fwd": (I, [P, I, I, P, L, L, P]),
     "rs_embed_inner_fwd": (I, [P, I, L, P, P, P, I, I, P, L, L, P, P]),
+    "rs_embed_inner_fwd_hm": (I, [P, I, L, P, P, P, P, P, I, I, P, L, L, P, P]),
     "rs_outer_prepared_size": (L, [I, I]),
     "rs_outer_prepare": (I, [P, I, I, P, P]),
     "rs_outer_product_fwd": (I, [P, I, I, P, P, L, L, P]),
     "rs_embed_product_fwd": (I, [P, I, L, P, P, P, I, I, I, P, P, L, L, P, P]),
+    "rs_embed_product_fwd_hm": (I, [P, I, L, P, P, P, P, P, I, I, I, P, P, L, L, P, P]),
     "rs_din_attention_fwd": (I, [P, P, P, P, I, I, P, P, P, I, P, P, P, I, P, P, P, L, P]),
     "rs_din_attention_dice_fwd": (I, [P, P, P, P, I, I, I, P, P, P, F, P, P, P, L, P]),
     "rs_din_prepared_size": (L, [I, I, I, I]),

@@ -13,6 +13,7 @@
 // 2*d*4 bytes per sample; MFMA utilisation is at most L/16 by construction.
 #include "mlp_tower.hpp"
 #include "rs_common.hpp"
+#include "tile_gather.hpp"
 
 namespace rs {
 
@@ -217,13 +218,14 @@ struct EmbedCrossArgs {
 
 constexpr int EC_FMAX = 128;
 
-template <int NT, int KIND>
-__global__ __launch_bounds__(16 * 64) void embed_cross(CrossArgs a, EmbedCrossArgs e) {
+// KA: the field metadata by value (rs_embed_cross_fwd_hm, k = 16, <= 32
+// fields): the headline kernel's front end (tile_gather.hpp) instead of the
+// cooperative id tile.
+template <int NT, int KIND, bool KA>
+__device__ __forceinline__ void embed_cross_body(const CrossArgs& a, const EmbedCrossArgs& e, const FieldMeta* km) {
   constexpr int NW = 16;
   typedef Ids<KIND> I;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ typename I::raw_t lid[16][EC_FMAX];
-  __shared__ int64_t lmeta[2][EC_FMAX];
   float* tile = smem;
   float* cs = smem + ((16 * a.d + 3) / 4) * 4;
   float* alpha = cs + NW * 16 * (NT * 16 + 1);
@@ -232,6 +234,26 @@ __global__ __launch_bounds__(16 * 64) void embed_cross(CrossArgs a, EmbedCrossAr
   const int64_t b0 = (int64_t)blockIdx.x * 16;
   const int rows = (int)((a.batch - b0) < 16 ? (a.batch - b0) : 16);
   const int F = e.F;
+  if constexpr (KA) {
+    {  // dense columns (wave w: sample w), requested beside the ids
+      const int64_t bb = b0 + (w < rows ? w : rows - 1);
+      for (int j = lane; j < e.nd; j += 64) tile[w * a.d + j] = w < rows ? e.dense[bb * e.dense_stride + j] : 0.f;
+    }
+    const bool bad = gather_tile_k16<NW, KIND>(e.ids, e.id_stride, e.table, km, F, b0, rows,
+                                               [&](int s, int c, int q, floatx4 x) {
+                                                 float* p = tile + s * a.d + e.nd + c * 16 + 4 * q;
+                                                 p[0] = x[0];
+                                                 p[1] = x[1];
+                                                 p[2] = x[2];
+                                                 p[3] = x[3];
+                                               });
+    if (__any(bad) && lane == 0) flag_error(e.err);
+    __syncthreads();
+    cross_tile<NT, NW>(a, tile, cs, alpha, b0, rows);
+    return;
+  } else {
+  __shared__ typename I::raw_t lid[16][EC_FMAX];
+  __shared__ int64_t lmeta[2][EC_FMAX];
 
   for (int t = tid; t < 16 * F; t += NW * 64) {
     const int ss = t / F, c = t - ss * F;
@@ -286,6 +308,16 @@ __global__ __launch_bounds__(16 * 64) void embed_cross(CrossArgs a, EmbedCrossAr
   if (__any(bad) && lane == 0) flag_error(e.err);
   __syncthreads();
   cross_tile<NT, NW>(a, tile, cs, alpha, b0, rows);
+  }
+}
+
+template <int NT, int KIND>
+__global__ __launch_bounds__(16 * 64) void embed_cross(CrossArgs a, EmbedCrossArgs e) {
+  embed_cross_body<NT, KIND, false>(a, e, nullptr);
+}
+template <int NT, int KIND>
+__global__ __launch_bounds__(16 * 64) void embed_cross_ka(CrossArgs a, EmbedCrossArgs e, FieldMeta m) {
+  embed_cross_body<NT, KIND, true>(a, e, &m);
 }
 
 // Fused DCN forward (model/dcn.py:24-34) in ONE launch: x0 = [dense |
@@ -295,13 +327,12 @@ __global__ __launch_bounds__(16 * 64) void embed_cross(CrossArgs a, EmbedCrossAr
 // branch's logit is alpha_L (x0.w_o) + beta_L.w_o = alpha_L g_L + h_L, x_L is
 // never formed); the DNN tower on the same tile with its last layer folded
 // with the output Dense's DNN half; head sigmoid(dnn + cross).
-template <int NT, int KIND>
-__global__ __launch_bounds__(16 * 64) void dcn_fused(CrossArgs a, EmbedCrossArgs e, MlpArgs t) {
+template <int NT, int KIND, bool KA>
+__device__ __forceinline__ void dcn_fused_body(const CrossArgs& a, const EmbedCrossArgs& e, const MlpArgs& t,
+                                               const FieldMeta* km) {
   constexpr int NW = 16;
   typedef Ids<KIND> I;
   extern __shared__ __attribute__((aligned(16))) float tsm[];
-  __shared__ typename I::raw_t lid[16][EC_FMAX];
-  __shared__ int64_t lmeta[2][EC_FMAX];
   constexpr int CW = NT * 16 + 1;
   __shared__ float cs[NW * 16 * CW];
   __shared__ float xlog[16];
@@ -317,6 +348,25 @@ __global__ __launch_bounds__(16 * 64) void dcn_fused(CrossArgs a, EmbedCrossArgs
   mlp_first_fill<NW>(t, ring);
   float* par = tsm + 32 * RS + NW * 256;
   for (int i = tid; i < t.ptot; i += NW * 64) par[i] = t.prep[t.wtot + i];
+  if constexpr (KA) {
+    {  // dense columns + zero padding of the tile row (wave w: sample w)
+      const int64_t bb = b0 + (w < rows ? w : rows - 1);
+      for (int j = lane; j < e.nd; j += 64) tsm[w * RS + j] = w < rows ? e.dense[bb * e.dense_stride + j] : 0.f;
+      for (int j = d + lane; j < t.Kp[0]; j += 64) tsm[w * RS + j] = 0.f;
+    }
+    const bool bad = gather_tile_k16<NW, KIND>(e.ids, e.id_stride, e.table, km, F, b0, rows,
+                                               [&](int sm, int c, int q, floatx4 x) {
+                                                 float* p = tsm + sm * RS + e.nd + c * 16 + 4 * q;
+                                                 p[0] = x[0];
+                                                 p[1] = x[1];
+                                                 p[2] = x[2];
+                                                 p[3] = x[3];
+                                               });
+    if (__any(bad) && lane == 0) flag_error(e.err);
+    __syncthreads();
+  } else {
+  __shared__ typename I::raw_t lid[16][EC_FMAX];
+  __shared__ int64_t lmeta[2][EC_FMAX];
   for (int t0 = tid; t0 < 16 * F; t0 += NW * 64) {
     const int ss = t0 / F, c = t0 - ss * F;
     lid[ss][c] = I::load(e.ids, (b0 + (ss < rows ? ss : rows - 1)) * e.id_stride + c);
@@ -367,6 +417,7 @@ __global__ __launch_bounds__(16 * 64) void dcn_fused(CrossArgs a, EmbedCrossArgs
   }
   if (__any(bad) && lane == 0) flag_error(e.err);
   __syncthreads();
+  }
 
   // CrossNet contraction G = X0 @ [w_0 .. w_{L-1}, w_o[:d]] (a.L = L + 1 columns)
   floatx4 acc[NT];
@@ -412,6 +463,15 @@ __global__ __launch_bounds__(16 * 64) void dcn_fused(CrossArgs a, EmbedCrossArgs
   }
   // (the tower's first barrier publishes xlog and the tile)
   mlp_tower_tile<NW>(t, tsm, b0, ring, xlog);
+}
+
+template <int NT, int KIND>
+__global__ __launch_bounds__(16 * 64) void dcn_fused(CrossArgs a, EmbedCrossArgs e, MlpArgs t) {
+  dcn_fused_body<NT, KIND, false>(a, e, t, nullptr);
+}
+template <int NT, int KIND>
+__global__ __launch_bounds__(16 * 64) void dcn_fused_ka(CrossArgs a, EmbedCrossArgs e, MlpArgs t, FieldMeta m) {
+  dcn_fused_body<NT, KIND, true>(a, e, t, &m);
 }
 
 }  // namespace rs
@@ -465,11 +525,22 @@ extern "C" int rs_cross_fwd(const float* x0, int64_t x_stride, int d, int n_laye
   return launch_status("rs_cross_fwd");
 }
 
-extern "C" int rs_embed_cross_fwd(const void* ids, int id_kind, int64_t id_stride, const float* dense,
-                                  int64_t dense_stride, int nd, const float* table, const int64_t* field_offsets,
-                                  const int64_t* field_vocab, int n_fields, int k, int n_layers,
-                                  const float* prepared, float* out, int64_t out_stride, int64_t batch,
-                                  int* err_flag, rs_stream_t stream) {
+namespace rs {
+// host field metadata -> FieldMeta for the kernarg front end (k = 16, <= 32 fields), else null
+static const FieldMeta* host_meta(FieldMeta& m, const int64_t* off_h, const int64_t* voc_h, int n_fields, int k) {
+  if (!off_h || !voc_h || k != 16 || n_fields < 1 || n_fields > 32) return nullptr;
+  for (int c = 0; c < n_fields; ++c) {
+    m.off[c] = off_h[c];
+    m.voc[c] = voc_h[c];
+  }
+  return &m;
+}
+
+static int embed_cross_run(const void* ids, int id_kind, int64_t id_stride, const float* dense,
+                           int64_t dense_stride, int nd, const float* table, const int64_t* field_offsets,
+                           const int64_t* field_vocab, int n_fields, int k, int n_layers, const float* prepared,
+                           float* out, int64_t out_stride, int64_t batch, int* err_flag, rs_stream_t stream,
+                           const FieldMeta* hm) {
   if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(ids && table && field_offsets && field_vocab && prepared && out, "rs_embed_cross_fwd: null pointer");
   RS_REQUIRE(nd == 0 || dense, "rs_embed_cross_fwd: dense is null");
@@ -492,7 +563,15 @@ extern "C" int rs_embed_cross_fwd(const void* ids, int id_kind, int64_t id_strid
   hipStream_t st = as_stream(stream);
   with_id_kind(id_kind, [&](auto K) {
     constexpr int KIND = decltype(K)::value;
-    if (g.NT == 1) {
+    if (hm && g.NT == 1) {
+      static LdsAttr setk1;
+      lds_attr(setk1, (const void*)embed_cross_ka<1, KIND>, lds);
+      embed_cross_ka<1, KIND><<<grid, NW * 64, lds, st>>>(a, e, *hm);
+    } else if (hm) {
+      static LdsAttr setk2;
+      lds_attr(setk2, (const void*)embed_cross_ka<2, KIND>, lds);
+      embed_cross_ka<2, KIND><<<grid, NW * 64, lds, st>>>(a, e, *hm);
+    } else if (g.NT == 1) {
       static LdsAttr set1;
       lds_attr(set1, (const void*)embed_cross<1, KIND>, lds);
       embed_cross<1, KIND><<<grid, NW * 64, lds, st>>>(a, e);
@@ -503,6 +582,30 @@ extern "C" int rs_embed_cross_fwd(const void* ids, int id_kind, int64_t id_strid
     }
   });
   return launch_status("rs_embed_cross_fwd");
+}
+}  // namespace rs
+
+extern "C" int rs_embed_cross_fwd(const void* ids, int id_kind, int64_t id_stride, const float* dense,
+                                  int64_t dense_stride, int nd, const float* table, const int64_t* field_offsets,
+                                  const int64_t* field_vocab, int n_fields, int k, int n_layers,
+                                  const float* prepared, float* out, int64_t out_stride, int64_t batch,
+                                  int* err_flag, rs_stream_t stream) {
+  return embed_cross_run(ids, id_kind, id_stride, dense, dense_stride, nd, table, field_offsets, field_vocab,
+                         n_fields, k, n_layers, prepared, out, out_stride, batch, err_flag, stream, nullptr);
+}
+
+extern "C" int rs_embed_cross_fwd_hm(const void* ids, int id_kind, int64_t id_stride, const float* dense,
+                                     int64_t dense_stride, int nd, const float* table,
+                                     const int64_t* field_offsets, const int64_t* field_vocab,
+                                     const int64_t* field_offsets_host, const int64_t* field_vocab_host,
+                                     int n_fields, int k, int n_layers, const float* prepared, float* out,
+                                     int64_t out_stride, int64_t batch, int* err_flag, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(field_offsets_host && field_vocab_host, "rs_embed_cross_fwd_hm: host metadata missing");
+  FieldMeta m;
+  return embed_cross_run(ids, id_kind, id_stride, dense, dense_stride, nd, table, field_offsets, field_vocab,
+                         n_fields, k, n_layers, prepared, out, out_stride, batch, err_flag, stream,
+                         host_meta(m, field_offsets_host, field_vocab_host, n_fields, k));
 }
 
 namespace rs {
@@ -520,11 +623,12 @@ extern "C" int rs_dcn_fused_ok(int nd, int n_fields, int k, int n_cross, int n_l
   return dims && dcn_geom(nd, n_fields, k, n_cross, n_layers, dims, mg) ? 1 : 0;
 }
 
-extern "C" int rs_dcn_fwd(const void* ids, int id_kind, int64_t id_stride, const float* dense, int64_t dense_stride,
-                          int nd, const float* table, const int64_t* field_offsets, const int64_t* field_vocab,
-                          int n_fields, int k, int n_cross, const float* cross_prepared, int n_layers,
-                          const int* dims, const int* acts, const float* mlp_prepared, float* out, int64_t batch,
-                          int* err_flag, rs_stream_t stream) {
+namespace rs {
+static int dcn_run(const void* ids, int id_kind, int64_t id_stride, const float* dense, int64_t dense_stride,
+                   int nd, const float* table, const int64_t* field_offsets, const int64_t* field_vocab,
+                   int n_fields, int k, int n_cross, const float* cross_prepared, int n_layers, const int* dims,
+                   const int* acts, const float* mlp_prepared, float* out, int64_t batch, int* err_flag,
+                   rs_stream_t stream, const FieldMeta* hm) {
   if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   MlpGeom mg;
   RS_REQUIRE(dims && acts, "rs_dcn_fwd: null dims/acts");
@@ -552,7 +656,15 @@ extern "C" int rs_dcn_fwd(const void* ids, int id_kind, int64_t id_stride, const
   hipStream_t st = as_stream(stream);
   with_id_kind(id_kind, [&](auto K) {
     constexpr int KIND = decltype(K)::value;
-    if (g.NT == 1) {
+    if (hm && g.NT == 1) {
+      static LdsAttr setk1;
+      lds_attr(setk1, (const void*)dcn_fused_ka<1, KIND>, lds);
+      dcn_fused_ka<1, KIND><<<grid, 16 * 64, lds, st>>>(a, e, t, *hm);
+    } else if (hm) {
+      static LdsAttr setk2;
+      lds_attr(setk2, (const void*)dcn_fused_ka<2, KIND>, lds);
+      dcn_fused_ka<2, KIND><<<grid, 16 * 64, lds, st>>>(a, e, t, *hm);
+    } else if (g.NT == 1) {
       static LdsAttr set1;
       lds_attr(set1, (const void*)dcn_fused<1, KIND>, lds);
       dcn_fused<1, KIND><<<grid, 16 * 64, lds, st>>>(a, e, t);
@@ -563,4 +675,29 @@ extern "C" int rs_dcn_fwd(const void* ids, int id_kind, int64_t id_stride, const
     }
   });
   return launch_status("rs_dcn_fwd");
+}
+}  // namespace rs
+
+extern "C" int rs_dcn_fwd(const void* ids, int id_kind, int64_t id_stride, const float* dense, int64_t dense_stride,
+                          int nd, const float* table, const int64_t* field_offsets, const int64_t* field_vocab,
+                          int n_fields, int k, int n_cross, const float* cross_prepared, int n_layers,
+                          const int* dims, const int* acts, const float* mlp_prepared, float* out, int64_t batch,
+                          int* err_flag, rs_stream_t stream) {
+  return dcn_run(ids, id_kind, id_stride, dense, dense_stride, nd, table, field_offsets, field_vocab, n_fields, k,
+                 n_cross, cross_prepared, n_layers, dims, acts, mlp_prepared, out, batch, err_flag, stream, nullptr);
+}
+
+extern "C" int rs_dcn_fwd_hm(const void* ids, int id_kind, int64_t id_stride, const float* dense,
+                             int64_t dense_stride, int nd, const float* table, const int64_t* field_offsets,
+                             const int64_t* field_vocab, const int64_t* field_offsets_host,
+                             const int64_t* field_vocab_host, int n_fields, int k, int n_cross,
+                             const float* cross_prepared, int n_layers, const int* dims, const int* acts,
+                             const float* mlp_prepared, float* out, int64_t batch, int* err_flag,
+                             rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(field_offsets_host && field_vocab_host, "rs_dcn_fwd_hm: host metadata missing");
+  FieldMeta m;
+  return dcn_run(ids, id_kind, id_stride, dense, dense_stride, nd, table, field_offsets, field_vocab, n_fields, k,
+                 n_cross, cross_prepared, n_layers, dims, acts, mlp_prepared, out, batch, err_flag, stream,
+                 host_meta(m, field_offsets_host, field_vocab_host, n_fields, k));
 }

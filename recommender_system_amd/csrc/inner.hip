@@ -8,6 +8,7 @@
 // e_j from LDS.  Output column p enumerates pairs (i<j) in the reference's
 // row-major order: p(i,j) = i*(2F-i-1)/2 + (j-i-1).
 #include "rs_common.hpp"
+#include "tile_gather.hpp"
 
 namespace rs {
 
@@ -137,13 +138,15 @@ constexpr int IP_SMAX = 16;
 constexpr int IP_NW = 16, IP_NT = IP_NW * 64;  // 16 waves: one sample per wave in the Gram phase
 constexpr int IP_FMAX = 64;
 
-template <int K, int KIND>
-__global__ __launch_bounds__(IP_NT) void inner_fast(InnerArgs a) {
+// KA (inner_fast_ka, rs_embed_inner_fwd_hm / rs_embed_product_fwd_hm: K = 16,
+// <= 32 fields, 16 samples per workgroup): the rows come in through the
+// headline kernel's front end (tile_gather.hpp: field metadata as kernel
+// arguments, per-wave field ids, no id tile or barrier before the rows).
+template <int K, int KIND, bool KA>
+__device__ __forceinline__ void inner_fast_body(const InnerArgs& a, const FieldMeta* km) {
   constexpr int KQ = K / 4;
   typedef Ids<KIND == 3 ? 0 : KIND> I;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ typename I::raw_t lid[IP_SMAX][IP_FMAX];
-  __shared__ int64_t lmeta[2][IP_FMAX];
   const int F = a.F, P = F * (F - 1) / 2, S = a.S;
   const int SS = F * K + 4;                    // sample stride: +4 dwords spreads the Gram reads over banks
   const int Pi = a.want_inner ? P : 0, Po = a.outer_img ? P : 0, PP = Pi + Po;
@@ -154,6 +157,19 @@ __global__ __launch_bounds__(IP_NT) void inner_fast(InnerArgs a) {
   const int nvalid = (int)(a.batch - b0 < S ? a.batch - b0 : S);
   IP_STAMP(0);
 
+  if constexpr (KA) {
+    static_assert(K == 16 && KIND != 3, "kernarg front end: gathered rows, k = 16");
+    const bool bad = gather_tile_k16<IP_NW, KIND>(a.ids, a.id_stride, a.table, km, F, b0, nvalid,
+                                                  [&](int s, int c, int q, floatx4 x) {
+                                                    *reinterpret_cast<floatx4*>(tile + s * SS + c * 16 + 4 * q) = x;
+                                                  });
+    IP_STAMP(1);
+    if (__any(bad) && (tid & 63) == 0) flag_error(a.err);
+    __syncthreads();
+    IP_STAMP(2);
+  } else {
+  __shared__ typename I::raw_t lid[IP_SMAX][IP_FMAX];
+  __shared__ int64_t lmeta[2][IP_FMAX];
   if constexpr (KIND != 3) {
     for (int t = tid; t < S * F; t += IP_NT) {
       const int s = t / F, c = t - s * F;
@@ -218,6 +234,7 @@ __global__ __launch_bounds__(IP_NT) void inner_fast(InnerArgs a) {
   if (bad) flag_error(a.err);
   __syncthreads();
   IP_STAMP(2);
+  }
 
   // Gram matrix per sample on MFMA: G = E E^T with E [F x K] from the LDS
   // tile, 16x16 blocks (bi <= bj) of v_mfma_f32_16x16x4_f32.  Lane l holds
@@ -401,6 +418,15 @@ __global__ __launch_bounds__(IP_NT) void inner_fast(InnerArgs a) {
   IP_STAMP(4);
 }
 
+template <int K, int KIND>
+__global__ __launch_bounds__(IP_NT) void inner_fast(InnerArgs a) {
+  inner_fast_body<K, KIND, false>(a, nullptr);
+}
+template <int KIND>
+__global__ __launch_bounds__(IP_NT) void inner_fast_ka(InnerArgs a, FieldMeta m) {
+  inner_fast_body<16, KIND, true>(a, &m);
+}
+
 template <int KIND>
 static void launch_inner_fast_k(const InnerArgs& a, size_t lds, unsigned grid, hipStream_t st) {
   switch (a.k) {
@@ -412,7 +438,7 @@ static void launch_inner_fast_k(const InnerArgs& a, size_t lds, unsigned grid, h
   }
 }
 
-static int launch_inner(InnerArgs a, hipStream_t st, const char* what) {
+static int launch_inner(InnerArgs a, hipStream_t st, const char* what, const FieldMeta* hm = nullptr) {
   if (a.batch == 0) return RS_OK;
   const bool fast_k = a.k == 4 || a.k == 8 || a.k == 16 || a.k == 32 || a.k == 64;
   if (fast_k && a.F >= 2 && a.F <= IP_FMAX) {
@@ -431,6 +457,13 @@ static int launch_inner(InnerArgs a, hipStream_t st, const char* what) {
     const unsigned grid = (unsigned)((a.batch + S - 1) / S);
     if (a.ids == nullptr) {
       launch_inner_fast_k<3>(a, lds, grid, st);
+    } else if (hm && a.k == 16 && a.F <= 32 && S == IP_SMAX) {
+      with_id_kind(a.id_kind, [&](auto K) {
+        constexpr int KIND = decltype(K)::value;
+        static LdsAttr set[3];
+        lds_attr(set[KIND], (const void*)inner_fast_ka<KIND>, lds);
+        inner_fast_ka<KIND><<<grid, IP_NT, lds, st>>>(a, *hm);
+      });
     } else {
       with_id_kind(a.id_kind, [&](auto K) { launch_inner_fast_k<decltype(K)::value>(a, lds, grid, st); });
     }
@@ -516,6 +549,93 @@ extern "C" int rs_inner_product_fwd(const float* emb, int n_fields, int k, float
   a.want_inner = 1;
   a.batch = batch;
   return launch_inner(a, as_stream(stream), "rs_inner_product_fwd");
+}
+
+namespace rs {
+static const FieldMeta* inner_host_meta(FieldMeta& m, const int64_t* off_h, const int64_t* voc_h, int n_fields,
+                                        int k) {
+  if (!off_h || !voc_h || k != 16 || n_fields < 1 || n_fields > 32) return nullptr;
+  for (int c = 0; c < n_fields; ++c) {
+    m.off[c] = off_h[c];
+    m.voc[c] = voc_h[c];
+  }
+  return &m;
+}
+}  // namespace rs
+
+extern "C" int rs_embed_inner_fwd_hm(const void* ids, int id_kind, int64_t id_stride, const float* table,
+                                     const int64_t* field_offsets, const int64_t* field_vocab,
+                                     const int64_t* field_offsets_host, const int64_t* field_vocab_host,
+                                     int n_fields, int k, float* out, int64_t out_stride, int64_t batch,
+                                     int* err_flag, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(field_offsets_host && field_vocab_host, "rs_embed_inner_fwd_hm: host metadata missing");
+  RS_REQUIRE(ids && table && field_offsets && field_vocab && out, "rs_embed_inner_fwd_hm: null pointer");
+  RS_REQUIRE(n_fields >= 1 && k >= 1 && k <= 64 && batch >= 0, "rs_embed_inner_fwd_hm: bad shape (k<=64)");
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_embed_inner_fwd_hm: bad id_kind");
+  RS_REQUIRE(out_stride >= (int64_t)n_fields * k + (int64_t)n_fields * (n_fields - 1) / 2,
+             "rs_embed_inner_fwd_hm: out_stride too small");
+  RS_REQUIRE(k % 4 != 0 || (uintptr_t)table % 16 == 0, "rs_embed_inner_fwd_hm: table must be 16-B aligned");
+  InnerArgs a{};
+  a.dbg = g_inner_dbg;
+  a.ids = ids;
+  a.id_kind = id_kind;
+  a.id_stride = id_stride;
+  a.table = table;
+  a.offs = field_offsets;
+  a.vocab = field_vocab;
+  a.F = n_fields;
+  a.k = k;
+  a.out = out;
+  a.out_stride = out_stride;
+  a.inner_off = n_fields * k;
+  a.write_flat = 1;
+  a.want_inner = 1;
+  a.batch = batch;
+  a.err = err_flag;
+  FieldMeta m;
+  return launch_inner(a, as_stream(stream), "rs_embed_inner_fwd_hm",
+                      inner_host_meta(m, field_offsets_host, field_vocab_host, n_fields, k));
+}
+
+extern "C" int rs_embed_product_fwd_hm(const void* ids, int id_kind, int64_t id_stride, const float* table,
+                                       const int64_t* field_offsets, const int64_t* field_vocab,
+                                       const int64_t* field_offsets_host, const int64_t* field_vocab_host,
+                                       int n_fields, int k, int inner, const float* outer_prepared, float* out,
+                                       int64_t out_stride, int64_t batch, int* err_flag, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(field_offsets_host && field_vocab_host, "rs_embed_product_fwd_hm: host metadata missing");
+  RS_REQUIRE(ids && table && field_offsets && field_vocab && out, "rs_embed_product_fwd_hm: null pointer");
+  RS_REQUIRE(inner || outer_prepared, "rs_embed_product_fwd_hm: nothing to compute (inner=0, no outer weights)");
+  RS_REQUIRE(rs_outer_prepared_size(n_fields, k) > 0,
+             "rs_embed_product_fwd_hm: need 2..%d fields and k in {4,8,16,32,64}", IP_FMAX);
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32 && batch >= 0, "rs_embed_product_fwd_hm: bad ids");
+  const int P = n_fields * (n_fields - 1) / 2;
+  RS_REQUIRE(out_stride >= (int64_t)n_fields * k + (inner ? P : 0) + (outer_prepared ? P : 0),
+             "rs_embed_product_fwd_hm: out_stride too small");
+  RS_REQUIRE((uintptr_t)table % 16 == 0, "rs_embed_product_fwd_hm: table must be 16-B aligned");
+  InnerArgs a{};
+  a.dbg = g_inner_dbg;
+  a.ids = ids;
+  a.id_kind = id_kind;
+  a.id_stride = id_stride;
+  a.table = table;
+  a.offs = field_offsets;
+  a.vocab = field_vocab;
+  a.F = n_fields;
+  a.k = k;
+  a.out = out;
+  a.out_stride = out_stride;
+  a.write_flat = 1;
+  a.want_inner = inner ? 1 : 0;
+  a.inner_off = n_fields * k;
+  a.outer_img = outer_prepared;
+  a.outer_off = n_fields * k + (inner ? P : 0);
+  a.batch = batch;
+  a.err = err_flag;
+  FieldMeta m;
+  return launch_inner(a, as_stream(stream), "rs_embed_product_fwd_hm",
+                      inner_host_meta(m, field_offsets_host, field_vocab_host, n_fields, k));
 }
 
 extern "C" int rs_embed_inner_fwd(const void* ids, int id_kind, int64_t id_stride, const float* table,

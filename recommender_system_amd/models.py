@@ -443,9 +443,10 @@ class DCN(KerasModule):
         if out is None:
             out = torch.empty(B, self.d, dtype=torch.float32, device=self._dev)
         prep = self.cross_layer.prepared(self.d)
-        call("rs_embed_cross_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), self.nd,
-             ptr(e.table), ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, e.k, self.cross_layer.layer_num,
-             ptr(prep), ptr(out), out.stride(0), B, ptr(self._err.t), _lib.stream())
+        hoff, hvoc = e.host_meta()  # field metadata also by value (the kernel-argument front end)
+        call("rs_embed_cross_fwd_hm", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0),
+             self.nd, ptr(e.table), ptr(e.field_offsets), ptr(e.field_vocab), hoff, hvoc, e.n_fields, e.k,
+             self.cross_layer.layer_num, ptr(prep), ptr(out), out.stride(0), B, ptr(self._err.t), _lib.stream())
         if check_ids:
             self._err.check("DCN")
         return out
@@ -587,10 +588,11 @@ class DCN(KerasModule):
         cross, mlp, dims, acts, _ = self._fused_params()
         n = len(dims) - 1
         out = torch.empty(B, 1, dtype=torch.float32, device=self._dev)
-        call("rs_dcn_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), self.nd,
-             ptr(e.table), ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, e.k, self.cross_layer.layer_num,
-             ptr(cross), n, (C.c_int * (n + 1))(*dims), (C.c_int * n)(*acts), ptr(mlp), ptr(out), B,
-             ptr(self._err.t), _lib.stream())
+        hoff, hvoc = e.host_meta()
+        call("rs_dcn_fwd_hm", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(dense), dense.stride(0), self.nd,
+             ptr(e.table), ptr(e.field_offsets), ptr(e.field_vocab), hoff, hvoc, e.n_fields, e.k,
+             self.cross_layer.layer_num, ptr(cross), n, (C.c_int * (n + 1))(*dims), (C.c_int * n)(*acts), ptr(mlp),
+             ptr(out), B, ptr(self._err.t), _lib.stream())
         if check_ids:
             self._err.check("DCN")
         return out
@@ -652,15 +654,16 @@ class PNN(KerasModule):
         e = self.embed_layer
         B = ids.shape[0]
         out = torch.empty(B, self.width, dtype=torch.float32, device=self._dev)
+        hoff, hvoc = e.host_meta()  # field metadata also by value (the kernel-argument front end)
         if self.mode == "inner":
-            call("rs_embed_inner_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(e.table),
-                 ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, e.k, ptr(out), out.stride(0), B,
+            call("rs_embed_inner_fwd_hm", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(e.table),
+                 ptr(e.field_offsets), ptr(e.field_vocab), hoff, hvoc, e.n_fields, e.k, ptr(out), out.stride(0), B,
                  ptr(self._err.t), _lib.stream())
         else:
-            call("rs_embed_product_fwd", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(e.table),
-                 ptr(e.field_offsets), ptr(e.field_vocab), e.n_fields, e.k, 1 if self.mode == "both" else 0,
-                 ptr(self.outer_product_layer.prepared()), ptr(out), out.stride(0), B, ptr(self._err.t),
-                 _lib.stream())
+            call("rs_embed_product_fwd_hm", ptr(ids), _lib.id_kind(ids), ids.stride(0), ptr(e.table),
+                 ptr(e.field_offsets), ptr(e.field_vocab), hoff, hvoc, e.n_fields, e.k,
+                 1 if self.mode == "both" else 0, ptr(self.outer_product_layer.prepared()), ptr(out), out.stride(0),
+                 B, ptr(self._err.t), _lib.stream())
         if check_ids:
             self._err.check("PNN")
         return out

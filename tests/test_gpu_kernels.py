@@ -834,3 +834,90 @@ def test_headline_shape_full_size(gpu, embed_fm_variant):
     hidden, out = dnn_params(m.dnn)
     ref = 1.0 / (1.0 + np.exp(-(0.5 * (fm + O.dnn_layer(x, hidden, out)))))
     assert_rel_close(m((dense, ids)), ref, what="DeepFM fused, headline shape")
+
+
+# ------------- kernel-argument front end of the DCN / PNN kernels (the _hm entries)
+@pytest.mark.parametrize("F,B,id_dtype", [(26, 4096, np.int32), (26, 333, np.int64), (20, 17, np.float32),
+                                          (32, 1, np.int32), (9, 64, np.int64)])
+def test_hm_front_end_bit_identical(gpu, F, B, id_dtype):
+    """rs_embed_cross_fwd_hm / rs_dcn_fwd_hm / rs_embed_inner_fwd_hm /
+    rs_embed_product_fwd_hm (k = 16: field metadata as kernel arguments, the
+    rows gathered by the headline kernel's per-wave front end) write exactly
+    what the cooperative-id-tile kernels write (rs_embed_cross_fwd, ...), and
+    flag an out-of-range id of a valid sample."""
+    import ctypes as C
+    from recommender_system_amd import DCN, PNN, _lib
+    from tests.helpers import criteo_columns
+    rng = np.random.default_rng(F * 1000 + B)
+    vocabs = rng.integers(2, 3000, size=F)
+    cols = criteo_columns(vocabs, embed_dim=16)
+    m = DCN(cols, [64, 32], 1, "relu", layer_num=3, embed_dim=16, seed=2)
+    p = PNN(cols, "both", [32], 1, embed_dim=16, seed=3)
+    ids_np = random_ids(rng, B, vocabs, np.int64)
+    dt = {np.int32: torch.int32, np.int64: torch.int64, np.float32: torch.float32}[id_dtype]
+    ids = torch.as_tensor(ids_np, device=gpu).to(dt)
+    kind = _lib.id_kind(ids)
+    dense = torch.rand(B, 13, device=gpu)
+    err = torch.zeros(1, dtype=torch.int32, device=gpu)
+    st = _lib.stream()
+
+    def both(entry, args_before, args_after, out):
+        outs = []
+        for hm in (False, True):
+            out.fill_(7.0)
+            if hm:
+                _lib.call(entry + "_hm", *args_before, *args_hm, *args_after)
+            else:
+                _lib.call(entry, *args_before, *args_after)
+            torch.cuda.synchronize()
+            outs.append(out.clone())
+        return outs
+
+    e = m.embed_layer
+    hoff, hvoc = e.host_meta()
+    args_hm = (hoff, hvoc)
+    d = m.d
+    xl = torch.empty(B, d, device=gpu)
+    prep = m.cross_layer.prepared(d)
+    a, b = both("rs_embed_cross_fwd", (ids.data_ptr(), kind, ids.stride(0), dense.data_ptr(), 13, 13, e.table.data_ptr(),
+                                       e.field_offsets.data_ptr(), e.field_vocab.data_ptr()),
+                (F, 16, 3, prep.data_ptr(), xl.data_ptr(), d, B, err.data_ptr(), st), xl)
+    assert torch.equal(a, b) and int(err.item()) == 0
+    cross, mlp, dims, acts, _ = m._fused_params()
+    n = len(dims) - 1
+    y = torch.empty(B, 1, device=gpu)
+    a, b = both("rs_dcn_fwd", (ids.data_ptr(), kind, ids.stride(0), dense.data_ptr(), 13, 13, e.table.data_ptr(),
+                               e.field_offsets.data_ptr(), e.field_vocab.data_ptr()),
+                (F, 16, 3, cross.data_ptr(), n, (C.c_int * (n + 1))(*dims), (C.c_int * n)(*acts), mlp.data_ptr(),
+                 y.data_ptr(), B, err.data_ptr(), st), y)
+    assert torch.equal(a, b) and int(err.item()) == 0
+    pe = p.embed_layer
+    hoff, hvoc = pe.host_meta()
+    args_hm = (hoff, hvoc)
+    P = F * (F - 1) // 2
+    z = torch.empty(B, F * 16 + P, device=gpu)
+    a, b = both("rs_embed_inner_fwd", (ids.data_ptr(), kind, ids.stride(0), pe.table.data_ptr(),
+                                       pe.field_offsets.data_ptr(), pe.field_vocab.data_ptr()),
+                (F, 16, z.data_ptr(), z.stride(0), B, err.data_ptr(), st), z)
+    assert torch.equal(a, b) and int(err.item()) == 0
+    z2 = torch.empty(B, F * 16 + 2 * P, device=gpu)
+    a, b = both("rs_embed_product_fwd", (ids.data_ptr(), kind, ids.stride(0), pe.table.data_ptr(),
+                                         pe.field_offsets.data_ptr(), pe.field_vocab.data_ptr()),
+                (F, 16, 1, p.outer_product_layer.prepared().data_ptr(), z2.data_ptr(), z2.stride(0), B,
+                 err.data_ptr(), st), z2)
+    assert torch.equal(a, b) and int(err.item()) == 0
+    bad = ids_np.copy()
+    bad[B - 1, F - 1] = vocabs[F - 1]
+    bad_t = torch.as_tensor(bad, device=gpu).to(dt)
+    for entry, extra in (("rs_embed_cross_fwd_hm", None), ("rs_embed_inner_fwd_hm", None)):
+        err.zero_()
+        if entry == "rs_embed_cross_fwd_hm":
+            _lib.call(entry, bad_t.data_ptr(), kind, bad_t.stride(0), dense.data_ptr(), 13, 13, e.table.data_ptr(),
+                      e.field_offsets.data_ptr(), e.field_vocab.data_ptr(), *e.host_meta(), F, 16, 3, prep.data_ptr(),
+                      xl.data_ptr(), d, B, err.data_ptr(), st)
+        else:
+            _lib.call(entry, bad_t.data_ptr(), kind, bad_t.stride(0), pe.table.data_ptr(), pe.field_offsets.data_ptr(),
+                      pe.field_vocab.data_ptr(), *pe.host_meta(), F, 16, z.data_ptr(), z.stride(0), B, err.data_ptr(),
+                      st)
+        torch.cuda.synchronize()
+        assert int(err.item()) != 0, entry
