@@ -67,23 +67,15 @@ enum rs_flag {
 enum rs_option {
   RS_OPT_EMBED_FM_KERNEL = 0, /* rs_embed_fm_fwd kernel (id inputs, no x_out): 0 = MFMA K-split,
                                  1 = VALU/DPP persistent 8-sample tiles, 2 / 3 = MFMA persistent
-                                 16-sample tiles (2 / 1 resident per CU); rs_embed_fm_fwd_hm at
-                                 k = 16: 4 / 5 / 6 = the K-split kernel with rows loaded by 4
-                                 adjacent lanes each (second pass after the first's MFMAs / on
-                                 its rows' arrival / with the first); shapes a kernel does not
-                                 cover run the K-split one.  See DESIGN.md 4.1                    */
+                                 16-sample tiles (2 / 1 resident per CU); 4 = rs_embed_fm_fwd_hm's
+                                 K-split kernel with the last-wave finish (no combine barrier;
+                                 bit-identical); shapes a kernel does not cover run the K-split
+                                 one.  See DESIGN.md 4.1                                          */
   RS_OPT_MLP_UNROLL = 1,      /* fused MLP towers (rs_mlp_fwd, rs_deepfm_fwd, rs_dcn_fwd): 1 (the
                                  default) = the k-group loop of the common layer widths fully
                                  unrolled (no loop-head wait on the weight ring), 0 = the looped
                                  form.  See DESIGN.md 4.5                                         */
-  RS_OPT_GATHER_ROWS = 2,     /* rs_gather_rows at k = 16: 0 = 256-thread workgroups, 4 lanes per
-                                 row; 1 = 64-thread workgroups; 2 = two rows per lane quad in
-                                 flight; 3 = 2 with write-through (sc1) row stores.  DESIGN.md 4.6 */
-  RS_OPT_SHARD_ROUTE = 3,     /* rs_shard_field_route / rs_shard_row_route / the route part of
-                                 rs_shard_fm_pipe: 0 (the default) = one thread per lookup with
-                                 the field metadata staged in LDS, 1 = one thread per record word
-                                 (the round-3 form).  Same words either way.  DESIGN.md 4.6        */
-  RS_OPT_COUNT = 4
+  RS_OPT_COUNT = 2
 };
 
 /* ------------------------------------------------------------------ meta */

@@ -149,8 +149,6 @@ ID_I32, ID_I64, ID_F32 = 0, 1, 2
 FLAG_BAD_ID, FLAG_LAYOUT = 1, 2  # rs_flag bits of the device error flag
 OPT_EMBED_FM_KERNEL = 0  # rs_option
 OPT_MLP_UNROLL = 1
-OPT_GATHER_ROWS = 2
-OPT_SHARD_ROUTE = 3
 ACT = {None: 0, "linear": 0, "relu": 1, "prelu": 2, "sigmoid": 3}
 
 _lock = threading.Lock()

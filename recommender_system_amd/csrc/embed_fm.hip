@@ -129,20 +129,16 @@ __global__ void fm_prepare_generic(const float* __restrict__ w1, const float* __
 // row stride tw->rs) instead of x_out, and the DNN tower of mlp_tower.hpp runs
 // on it, closed by sigmoid(c0*dnn + c1*fm) (model/deepFM.py:24-30).
 // A workgroup owns one 16-sample MFMA row tile.
-// QV (kernarg kernel, k = 16 only): 0 = rows loaded in the MFMA A layout
-// (lane = sample + 16 chunk: a 16-lane quarter-wave touches 16 rows); 1..3 =
-// rows loaded with 4 ADJACENT lanes per row (lane = 4 sample + chunk: a
-// quarter-wave touches 4 whole rows) and moved to the A layout in registers
-// (swap_hi4 / swap_lo4: 4 v_permlane*_swap + 16 DPP/select per field; MFMA
-// row r then holds sample ((r & 3) << 2) | (r >> 2), the B fragments take the
-// matching element order by swap_hi4).  The second pass's rows are requested
-// 1: after the first pass's MFMAs, 2: when the first pass's rows have
-// arrived, 3: with the first pass's.
-template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, bool PF = false, bool KA = false, int QV = 0>
+// LF (FM logit kernels): the cross-wave combine without a workgroup barrier —
+// every wave writes its partial tile (one b128 per lane) and its per-row q
+// partials to its own LDS slot and counts itself in an LDS counter; the LAST
+// wave to arrive sums the slots in wave order and finishes the tile's logits
+// (the others exit).  The sums run in the same order as the barrier form, so
+// the logits are bit-identical.
+template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, bool PF = false, bool KA = false, bool LF = false>
 __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArgs* tw, const int tile,
                                               const FieldMeta* km = nullptr) {
-  constexpr bool QL = QV > 0;
-  static_assert(!QL || (KV == 4 && KA && !TW && KIND < 3), "adjacent-lane rows: kernarg FM kernel, k = 16");
+  static_assert(!LF || (!TW && KIND != 4), "last-wave finish: FM logit kernels");
   // MC > 0: field slots per wave and pass (owner kernels with few fields)
   constexpr int MAXC0 = MC > 0 ? MC : 128 / (NW * KV);
   constexpr int MAXC = MAXC0 < 1 ? 1 : (MAXC0 > 8 ? 8 : MAXC0);
@@ -150,22 +146,17 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   constexpr bool OWNER = KIND == 4;
   __shared__ float cs[NW][16][NT * 16 + 1];
   __shared__ float qs[NW][16];
+  __shared__ int lf_arrived;  // LF: waves done with their partial tiles
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int s = lane & 15;   // A: row of the tile; B/C: column
+  const int s = lane & 15;   // A: sample row of the tile; B/C: column
   const int kk = lane >> 4;  // k-slot
-  const int sm = QL ? (((s & 3) << 2) | (s >> 2)) : s;  // the sample of MFMA row s
-  const int64_t bt = (int64_t)tile * 16 + sm;
+  const int64_t bt = (int64_t)tile * 16 + s;
   const bool valid = bt < a.batch;
   // Padded lanes of the last tile recompute the last sample: an MFMA output
   // row depends only on its own A row, so they never touch valid outputs.
   const int64_t b = bt < a.batch ? bt : a.batch - 1;
-  // the sample / chunk whose row piece this lane LOADS (QL: lane = 4 sample + chunk)
-  const int64_t btl = QL ? (int64_t)tile * 16 + (lane >> 2) : bt;
-  const bool valid_ld = btl < a.batch;
-  const int64_t bl = btl < a.batch ? btl : a.batch - 1;
-  const int qc = QL ? (lane & 3) : kk;
   const int d = a.nd + a.F * a.k;
   // w0 is requested now, not behind the rows (a dependent load at the end)
   const float w0v = OWNER ? 0.f : a.w0[0];
@@ -288,19 +279,6 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     }
   };
   auto norms = [&](Pass& P) {
-    if constexpr (QL) {
-      // B fragment lane (kk, col) register t: v[4 kk + t] -> v[4 t + kk], the
-      // element order of the A values after swap_hi4 / swap_lo4
-#pragma unroll
-      for (int j = 0; j < MAXC; ++j)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          float t4[4] = {P.bw[j][nt].v[0], P.bw[j][nt].v[1], P.bw[j][nt].v[2], P.bw[j][nt].v[3]};
-          swap_hi4(t4);
-#pragma unroll
-          for (int tp = 0; tp < 4; ++tp) P.bw[j][nt].v[tp] = t4[tp];
-        }
-    }
     // |v_e|^2 for this lane's element e: the B lanes of DPP row kk hold
     // v[e][0..15] — the same row as the A lane that holds x_e.
 #pragma unroll
@@ -338,7 +316,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
         } else if constexpr (KA) {  // kernarg metadata: scalar loads, wave-uniform field
           offc[j] = km->off[P.cj[j]];
           vocc[j] = km->voc[P.cj[j]];
-          P.rid[j] = I::load(a.ids, bl * a.id_stride + P.cj[j]);
+          P.rid[j] = I::load(a.ids, b * a.id_stride + P.cj[j]);
         } else {
           const int cv = min(cg + j * NW + wv, a.F - 1);
           offc[j] = a.offs[cv];
@@ -376,7 +354,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 #ifdef RS_DIAG_STAMPS
       if ((a.ablate & 8) && cg + j * NW + w >= a.F) { P.xs[j].zero(); continue; }
 #endif
-      P.xs[j].load_nt(a.table + row[j] * a.k + KV * qc);
+      P.xs[j].load_nt(a.table + row[j] * a.k + KV * kk);
     }
   };
   auto consume = [&](int cg, Pass& P) {
@@ -390,25 +368,6 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       if constexpr (OWNER) bad |= live && !P.ok[j] && P.rid[j] != -1;
       else bad |= live && !P.ok[j];
       const bool use = live && P.ok[j];
-      if constexpr (QL) {
-        float x4[4];
-#pragma unroll
-        for (int tp = 0; tp < 4; ++tp) x4[tp] = use ? P.xs[j].v[tp] : 0.f;
-        if (a.x_out && live && valid_ld) {  // before the exchange: one 64-B row per lane quad
-          float* xo = a.x_out + bl * d + a.nd + P.cj[j] * a.k + 4 * qc;
-#pragma unroll
-          for (int tp = 0; tp < 4; ++tp) xo[tp] = x4[tp];
-        }
-        swap_hi4(x4);
-        swap_lo4(x4, lane);
-#pragma unroll
-        for (int tp = 0; tp < 4; ++tp) {
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(x4[tp], P.bw[j][nt].v[tp], acc[nt]);
-          qn = fmaf(x4[tp] * x4[tp], P.nrm[j][tp], qn);
-        }
-        continue;
-      }
 #pragma unroll
       for (int tp = 0; tp < KV; ++tp) {
         const float xv = use ? P.xs[j].v[tp] : 0.f;
@@ -454,28 +413,34 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   if (a.F == 0 || coop) load_dense();
   if (coop) __syncthreads();
   RS_STAMP(9);
+  // LF: the finish counter starts at 0, behind one workgroup barrier that
+  // every wave passes (in the PRE schedule with its ids already in flight)
+  auto lf_init = [&]() {
+    if constexpr (LF) {
+      if (threadIdx.x == 0) lf_arrived = 0;
+      __syncthreads();
+    }
+  };
   if (PRE) {
-    if (has_pass(0)) {
+    const bool one = has_pass(0), two = one && has_pass(PS);
+    if (one) {
       // both passes' ids requested together: the second pass's id trip is
       // not serialised behind the first pass's rows and MFMAs (after the B
       // fragments: ids first was slower, 5.95 vs 5.75 us at 4096)
       fetch_ids(0, P0);
-      const bool two = has_pass(PS);
       if (two) fetch_ids(PS, P1);
+    }
+    lf_init();
+    if (one) {
       // (the second pass's rows stay behind the first pass's MFMAs: issuing
       // them with the first pass's was slower, 6.19 vs 5.82 us at 4096 —
       // the r1 finding that two row bursts beat one, again)
       issue_rows(0, P0, true);
-      if (QV == 3 && two) issue_rows(PS, P1, true);
       norms(P0);
       if (two) norms(P1);
-      if (QV == 2 && two) {
-        asm volatile("" ::"v"(P0.xs[0].v[KV - 1]));  // the first pass's rows have arrived
-        issue_rows(PS, P1, true);
-      }
       consume(0, P0);
       if (two) {
-        if (QV < 2) issue_rows(PS, P1, true);
+        issue_rows(PS, P1, true);
         consume(PS, P1);
         for (int cg = 2 * PS; has_pass(cg); cg += PS) {
           issue_b(cg, P0);
@@ -486,6 +451,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       }
     }
   } else {
+    lf_init();
     for (int cg = 0; has_pass(cg); cg += PS) {
       issue_b(cg, P0);
       issue_rows(cg, P0, false);
@@ -525,7 +491,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   }
   RS_USE(acc[0][0]);
   RS_STAMP(3);
-  if (__any(bad && valid_ld) && lane == 0) flag_error(a.err);
+  if (__any(bad && valid) && lane == 0) flag_error(a.err);
 
 #ifdef RS_DIAG_STAMPS
   if (a.ablate & 4) {
@@ -533,6 +499,54 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     return;
   }
 #endif
+  if constexpr (LF) {
+    // ---- last-wave finish: partial tile + per-row q partials to this wave's
+    // slot, count in; the last wave sums the slots in wave order (as the
+    // barrier form below: bit-identical) and writes the tile's logits.
+    __shared__ floatx4 lf_acc[NT][NW][64];
+    __shared__ floatx4 lf_q[NW][4];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) lf_acc[nt][w][lane] = acc[nt];
+    qn += __shfl_xor(qn, 16);
+    qn += __shfl_xor(qn, 32);
+    if (lane < 16) reinterpret_cast<float*>(&lf_q[w][0])[lane] = qn;
+    int old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(&lf_arrived, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != NW - 1) return;
+    RS_STAMP(7);
+    floatx4 v[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      v[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) {
+        const floatx4 pv = lf_acc[nt][ww][lane];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[nt][i] += pv[i];
+      }
+    }
+    const floatx4 q4 = lf_q[s < NW ? s : 0][kk];  // wave s's q partials of rows 4 kk .. 4 kk + 3
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float t = 0.f, lin = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int col = nt * 16 + s;
+        float tt = col < a.kfm ? v[nt][i] * v[nt][i] : 0.f;  // s_f^2
+        if (col < NW) tt -= q4[i];                           // - sum_i x_i^2 |v_i|^2 (wave partials)
+        float ll = col == a.kfm ? v[nt][i] : 0.f;            // x@w1
+        tt = row16_sum(tt);
+        ll = row16_sum(ll);
+        t = nt == 0 ? tt : t + tt;
+        lin = nt == 0 ? ll : lin + ll;
+      }
+      const int64_t bb = (int64_t)tile * 16 + 4 * kk + i;
+      if (s == 0 && bb < a.batch && a.logit) a.logit[bb] = (lin + w0v) + 0.5f * t;
+    }
+    RS_STAMP(4);
+    return;
+  }
   // ---- combine the NW partial tiles: thread (sample, column) sums the waves'
   // partials; the per-sample reductions over columns are DPP row sums.
 #pragma unroll
@@ -559,7 +573,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       t += __shfl_xor(t, 16);
       lin += __shfl_xor(lin, 16);
     }
-    const int64_t bb = (int64_t)tile * 16 + (QL ? (((smp & 3) << 2) | (smp >> 2)) : smp);
+    const int64_t bb = (int64_t)tile * 16 + smp;
     if constexpr (OWNER) {
       // partial record: column sums as they stand, the q term row-summed
       float q = col < NW ? qs[col][smp] : 0.f;
@@ -591,9 +605,9 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
 // the field metadata by value (rs_embed_fm_fwd_hm): each wave loads its own
 // fields' ids and reads (offset, vocab) through scalar kernarg loads — no LDS
 // id tile, no barrier, no per-wave metadata loads from one hot L2 line
-template <int KV, int NT, int NW, int KIND, bool PF, int QV = 0>
+template <int KV, int NT, int NW, int KIND, bool PF, bool LF = false>
 __global__ __launch_bounds__(NW * 64) void embed_fm_mfma_ka(EmbedFmArgs a, FieldMeta m) {
-  embed_fm_body<KV, NT, NW, KIND, false, 1, PF, true, QV>(a, nullptr, blockIdx.x, &m);
+  embed_fm_body<KV, NT, NW, KIND, false, 1, PF, true, LF>(a, nullptr, blockIdx.x, &m);
 }
 
 // ---- sharded FM, partial protocol: combine (requester side) as a block part
@@ -665,7 +679,6 @@ __device__ __forceinline__ void fm_combine_part(const CombineArgs& c, int blk, i
 // all-to-all.  Any part may be empty.
 struct PipeArgs {
   int owner_blocks, route_blocks, combine_blocks;
-  int route_lookup;  // 1: lookup_route_part (one thread per lookup), 0: field_route_part
   RouteArgs r;
   CombineArgs c;
 };
@@ -676,9 +689,7 @@ __global__ __launch_bounds__(NW * 64) void shard_fm_pipe(EmbedFmArgs a, PipeArgs
   if (bid < p.owner_blocks) {
     embed_fm_body<KV, NT, NW, 4, false, MC>(a, nullptr, bid);
   } else if (bid < p.owner_blocks + p.route_blocks) {
-    __shared__ RouteLds L;
-    if (p.route_lookup) lookup_route_part<NW * 64>(p.r, bid - p.owner_blocks, p.route_blocks, L);
-    else field_route_part<NW * 64>(p.r, bid - p.owner_blocks, p.route_blocks);
+    field_route_part<NW * 64>(p.r, bid - p.owner_blocks, p.route_blocks);
   } else {
     fm_combine_part<NW * 64>(p.c, bid - p.owner_blocks - p.route_blocks, p.combine_blocks);
   }
@@ -897,13 +908,9 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st, const FieldMe
   // with both passes' ids requested together; profiles/r3_ab_kernarg_*)
   // 16 waves (13: 6.20 us, 9: 6.78 vs 5.76 at 4096; profiles/r3_ab_kernarg_waves_4096.json)
   if (hm && a.F <= 32 && KIND != 3 && grid <= 512) {
-    if constexpr (KV == 4 && KIND < 3) {
-      switch (opt(RS_OPT_EMBED_FM_KERNEL)) {  // adjacent-lane row loads (embed_fm_body QV)
-        case 4: embed_fm_mfma_ka<KV, NT, 16, KIND, true, 1><<<grid, 16 * 64, 0, st>>>(a, *hm); return;
-        case 5: embed_fm_mfma_ka<KV, NT, 16, KIND, true, 2><<<grid, 16 * 64, 0, st>>>(a, *hm); return;
-        case 6: embed_fm_mfma_ka<KV, NT, 16, KIND, true, 3><<<grid, 16 * 64, 0, st>>>(a, *hm); return;
-        default: break;
-      }
+    if (!a.x_out && opt(RS_OPT_EMBED_FM_KERNEL) == 4) {  // last-wave finish (embed_fm_body LF)
+      embed_fm_mfma_ka<KV, NT, 16, KIND, true, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
+      return;
     }
     embed_fm_mfma_ka<KV, NT, 16, KIND, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
     return;
@@ -1225,10 +1232,7 @@ template <int KV, int NT, int NW, int MC>
 static void launch_pipe4(const EmbedFmArgs& a, PipeArgs p, hipStream_t st) {
   const int T = NW * 64;
   p.owner_blocks = a.F > 0 ? (int)((a.batch + 15) / 16) : 0;
-  if (p.route_blocks) {
-    const int64_t items = p.route_lookup ? (int64_t)p.r.batch * p.r.n_fields : p.r.total;
-    p.route_blocks = (int)std::min<int64_t>((items + T - 1) / T, 4096);
-  }
+  if (p.route_blocks) p.route_blocks = (int)std::min<int64_t>((p.r.total + T - 1) / T, 4096);
   if (p.combine_blocks) p.combine_blocks = (int)std::min<int64_t>((p.c.batch * 16 + T - 1) / T, 4096);
   const int grid = p.owner_blocks + p.route_blocks + p.combine_blocks;
   if (grid) shard_fm_pipe<KV, NT, NW, MC><<<grid, T, 0, st>>>(a, p);
@@ -1399,10 +1403,6 @@ extern "C" int rs_shard_fm_pipe(const int32_t* recv, int field_lo, int n_owned, 
     p.route_blocks = 1;
     p.r = RouteArgs{ids_next, id_kind, id_stride, field_offsets, field_vocab, rows_per_rank, owner_fields,
                     slot_stride, (int)batch, R, send, err_flag, (int64_t)world * batch * slot_stride};
-    p.r.n_fields = n_fields;
-    p.r.world = world;
-    p.route_lookup = opt(RS_OPT_SHARD_ROUTE) == 0 && n_fields <= RT_MAXF && world <= RT_MAXW &&
-                     batch * n_fields < ((int64_t)1 << 31);
   }
   if (logit_prev) {
     p.combine_blocks = 1;

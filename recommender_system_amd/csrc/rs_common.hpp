@@ -281,41 +281,6 @@ __device__ __forceinline__ float row16_sum(float x) {
   return x;
 }
 
-// Register/lane bit exchanges for 4 registers v[0..3] (register index bits
-// r1 r0) of a wave (lane bits l5..l0):
-//   swap_hi:  l5 <-> r1 (v_permlane32_swap), then l4 <-> r0 (v_permlane16_swap)
-//   swap_lo:  l0 <-> r0, then l1 <-> r1 (DPP quad permutes + selects)
-// The value at (lane L, register R) moves to the lane / register with those
-// bits exchanged.  Used to turn rows loaded with 4 ADJACENT lanes per row
-// (lane = 4 sample + chunk: one 64-B row per lane quad, the memory-friendly
-// layout) into the v_mfma_f32_16x16x4_f32 A layout (lane = row + 16 k-slot).
-__device__ __forceinline__ void swap_hi4(float (&v)[4]) {
-  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0]), __float_as_uint(v[2]), false, false);
-  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[1]), __float_as_uint(v[3]), false, false);
-  const auto c = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
-  const auto d = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
-  v[0] = __uint_as_float(c[0]);
-  v[1] = __uint_as_float(c[1]);
-  v[2] = __uint_as_float(d[0]);
-  v[3] = __uint_as_float(d[1]);
-}
-__device__ __forceinline__ float dpp_quad_xor1(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float dpp_quad_xor2(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));
-}
-__device__ __forceinline__ void swap_lo4(float (&v)[4], int lane) {
-  const bool b0 = lane & 1, b1 = lane & 2;
-  const float t0 = dpp_quad_xor1(v[1]), t1 = dpp_quad_xor1(v[0]), t2 = dpp_quad_xor1(v[3]), t3 = dpp_quad_xor1(v[2]);
-  const float n0 = b0 ? t0 : v[0], n1 = b0 ? v[1] : t1, n2 = b0 ? t2 : v[2], n3 = b0 ? v[3] : t3;
-  const float u0 = dpp_quad_xor2(n2), u1 = dpp_quad_xor2(n3), u2 = dpp_quad_xor2(n0), u3 = dpp_quad_xor2(n1);
-  v[0] = b1 ? u0 : n0;
-  v[1] = b1 ? u1 : n1;
-  v[2] = b1 ? n2 : u2;
-  v[3] = b1 ? n3 : u3;
-}
-
 __device__ __forceinline__ floatx4 mfma16x16x4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }

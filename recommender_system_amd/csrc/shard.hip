@@ -302,10 +302,7 @@ __global__ __launch_bounds__(SP_THREADS) void shard_slot_onepass(ShardArgs a, ui
 __global__ __launch_bounds__(256) void shard_field_route(RouteArgs a) {
   field_route_part<256>(a, blockIdx.x, gridDim.x);
 }
-__global__ __launch_bounds__(256) void shard_lookup_route(RouteArgs a) {
-  __shared__ RouteLds L;
-  lookup_route_part<256>(a, blockIdx.x, gridDim.x, L);
-}
+
 
 template <int VW>
 __global__ void gather_rows_kernel(const float* __restrict__ table, int64_t n_rows, int k,
@@ -363,52 +360,10 @@ __global__ __launch_bounds__(256) void gather_rows_k16(const float* __restrict__
   reinterpret_cast<floatx4*>(out)[idx] = x;
 }
 
-// k = 16, U rows per lane quad (U loads in flight per lane), NTH threads per
-// workgroup; WT: row stores written through (sc1) instead of left dirty in L2
-template <int U, int NTH, bool WT>
-__global__ __launch_bounds__(NTH) void gather_rows_k16u(const float* __restrict__ table, int64_t n_rows,
-                                                        const int32_t* __restrict__ rows, int n,
-                                                        float* __restrict__ out, int* err) {
-  const int quads = (n + U - 1) / U;  // quad g handles rows g, g + quads, ...
-  const int idx = blockIdx.x * NTH + threadIdx.x;
-  const int g = idx >> 2, q = idx & 3;
-  if (g >= quads) return;
-  int64_t r[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) r[u] = g + u * quads < n ? (int64_t)rows[g + u * quads] : -1;
-  floatx4 x[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    x[u] = floatx4{0.f, 0.f, 0.f, 0.f};
-    if (r[u] >= 0 && r[u] < n_rows) x[u] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(table + r[u] * 16) + q);
-    else if (r[u] != -1 && q == 0) flag_error(err);
-  }
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int i = g + u * quads;
-    if (i >= n) break;
-    floatx4* d = reinterpret_cast<floatx4*>(out) + (int64_t)i * 4 + q;
-    if constexpr (WT) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(d), "v"(x[u]) : "memory");
-    else *d = x[u];
-  }
-}
-
 static unsigned sh_grid(int64_t work) {
   int64_t g = (work + 255) / 256;
   if (g > 8192) g = 8192;
   return (unsigned)(g < 1 ? 1 : g);
-}
-
-// The route launch: one thread per lookup (RS_OPT_SHARD_ROUTE 0, shapes it
-// covers) or one per record word.
-static void launch_route(RouteArgs& a, int n_fields, int world, hipStream_t st) {
-  a.n_fields = n_fields;
-  a.world = world;
-  const int64_t n = (int64_t)a.batch * n_fields;
-  if (opt(RS_OPT_SHARD_ROUTE) == 0 && n_fields <= RT_MAXF && world <= RT_MAXW && n < ((int64_t)1 << 31))
-    shard_lookup_route<<<sh_grid(n), 256, 0, st>>>(a);
-  else
-    shard_field_route<<<sh_grid(a.total), 256, 0, st>>>(a);
 }
 
 }  // namespace rs
@@ -506,7 +461,7 @@ extern "C" int rs_shard_field_route(const void* ids, int id_kind, int64_t id_str
   const int64_t total = (int64_t)world * batch * slot_stride;
   RouteArgs a{ids, id_kind, id_stride, field_offsets, field_vocab, rows_per_rank, owner_fields, slot_stride,
               (int)batch, rec_stride, send, err_flag, total};
-  launch_route(a, n_fields, world, as_stream(stream));
+  shard_field_route<<<sh_grid(total), 256, 0, as_stream(stream)>>>(a);
   return launch_status("rs_shard_field_route");
 }
 
@@ -527,7 +482,7 @@ extern "C" int rs_shard_row_route(const void* ids, int id_kind, int64_t id_strid
   const int64_t total = (int64_t)world * batch * slot_stride;
   RouteArgs a{ids, id_kind, id_stride, field_offsets, field_vocab, rows_per_rank, owner_fields, slot_stride,
               (int)batch, slot_stride, send, err_flag, total, slot_of, n_fields};
-  launch_route(a, n_fields, world, as_stream(stream));
+  shard_field_route<<<sh_grid(total), 256, 0, as_stream(stream)>>>(a);
   return launch_status("rs_shard_row_route");
 }
 
@@ -538,13 +493,7 @@ extern "C" int rs_gather_rows(const float* table, int64_t n_rows, int k, const i
   RS_REQUIRE(k >= 1 && n >= 0 && n_rows >= 0, "rs_gather_rows: bad shape");
   if (n == 0) return RS_OK;
   hipStream_t st = as_stream(stream);
-  const int gv = opt(RS_OPT_GATHER_ROWS);
-  if (k == 16 && n < (1 << 29) && (uintptr_t)table % 16 == 0 && (uintptr_t)out % 16 == 0 && gv != 0) {
-    const int64_t quads = gv == 1 ? n : (n + 1) / 2;
-    if (gv == 1) gather_rows_k16u<1, 64, false><<<(unsigned)((quads * 4 + 63) / 64), 64, 0, st>>>(table, n_rows, rows, (int)n, out, err_flag);
-    else if (gv == 2) gather_rows_k16u<2, 256, false><<<(unsigned)((quads * 4 + 255) / 256), 256, 0, st>>>(table, n_rows, rows, (int)n, out, err_flag);
-    else gather_rows_k16u<2, 256, true><<<(unsigned)((quads * 4 + 255) / 256), 256, 0, st>>>(table, n_rows, rows, (int)n, out, err_flag);
-  } else if (k == 16 && n < (1 << 29) && (uintptr_t)table % 16 == 0 && (uintptr_t)out % 16 == 0)
+  if (k == 16 && n < (1 << 29) && (uintptr_t)table % 16 == 0 && (uintptr_t)out % 16 == 0)
     gather_rows_k16<<<(unsigned)((n * 4 + 255) / 256), 256, 0, st>>>(table, n_rows, rows, (int)n, out, err_flag);
   else if (k % 4 == 0 && (uintptr_t)table % 16 == 0 && (uintptr_t)out % 16 == 0)
     gather_rows_kernel<4><<<sh_grid(n * (k / 4)), 256, 0, st>>>(table, n_rows, k, rows, n, out, err_flag);

@@ -1394,79 +1394,3 @@ def test_gpu_sharded_deepfm_pipelined(gpu):
     for o, r in zip(outs, ref):
         assert torch.equal(o, r)
     assert int(m.ops.err.item()) == 0
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("world,vocab_hi,B,idt", [(1, 5000, 300, torch.int32), (2, 5000, 257, torch.int64),
-                                                  (3, 4000, 100, torch.float32), (8, 3000, 4096, torch.int32),
-                                                  (40, 2, 64, torch.int32)])
-def test_gpu_route_variants_write_the_same_words(gpu, world, vocab_hi, B, idt):
-    """rs_shard_field_route / rs_shard_row_route (and so the pipe kernel's
-    route part) in both forms (RS_OPT_SHARD_ROUTE 0: one thread per lookup
-    with the metadata in LDS; 1: one thread per record word) write the same
-    words: every row-id word, the partial words left alone, slot_of, and the
-    flag on bad ids.  world 40 over a 26..52-row table leaves owners with no
-    field at all (their words are all -1)."""
-    from recommender_system_amd import _lib
-    from recommender_system_amd.sharded import ShardedEmbeddingFM
-    rng = np.random.default_rng(world * 31 + B)
-    vocabs = [int(v) for v in rng.integers(1, vocab_hi + 1, 26)]
-    sh = ShardedEmbeddingFM(vocabs, 16, 13, 10, device=gpu, seed=2, table_init=False, world=world, rank=0)
-    ids = np.stack([rng.integers(0, v, B) for v in vocabs], 1)
-    ids[0] = np.array(vocabs) - 1
-    ids[1, 3] = vocabs[3]  # out of range
-    ids[2, 5] = -1
-    ids_t = torch.as_tensor(ids, device=gpu).to(idt)
-    S, R = sh.slot_stride, sh.slot_stride + 5
-    got = {}
-    prev = _lib.set_option(_lib.OPT_SHARD_ROUTE, 0)
-    try:
-        for v in (0, 1):
-            _lib.set_option(_lib.OPT_SHARD_ROUTE, v)
-            sh.ops.err.zero_()
-            send = torch.full((world * B * R,), 7, dtype=torch.int32, device=gpu)
-            sh.ops.field_route(sh, ids_t, send, rec=R)
-            rsend = torch.full((world * B * S,), 7, dtype=torch.int32, device=gpu)
-            slot_of = torch.full((B * 26,), 7, dtype=torch.int32, device=gpu)
-            sh.ops.row_route(sh, ids_t, rsend, slot_of)
-            torch.cuda.synchronize()
-            got[v] = (send.cpu(), rsend.cpu(), slot_of.cpu(), int(sh.ops.err.item()))
-    finally:
-        _lib.set_option(_lib.OPT_SHARD_ROUTE, prev)
-    for a, b in zip(got[0][:3], got[1][:3]):
-        assert torch.equal(a, b)
-    assert got[0][3] == got[1][3] == _lib.FLAG_BAD_ID
-    send = got[0][0].view(world * B, R)
-    assert bool((send[:, S:] == 7).all()) and not bool((send[:, :S] == 7).any())
-    sh.ops.err.zero_()
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
-@pytest.mark.parametrize("n", [1, 777, 106_497])
-def test_gpu_gather_rows_variants(gpu, variant, n):
-    """rs_gather_rows at k = 16 in every RS_OPT_GATHER_ROWS form: row r of the
-    table for every word, a zero row for -1 (no flag) and for an out-of-range
-    row (flag set)."""
-    from recommender_system_amd import _lib
-    from recommender_system_amd.sharded import HipShardOps
-    rng = np.random.default_rng(n + variant)
-    table = torch.randn(50_000, 16, device=gpu)
-    rows = rng.integers(0, table.shape[0], n).astype(np.int32)
-    if n > 1:
-        rows[n // 2] = -1
-    ops = HipShardOps(gpu)
-    prev = _lib.set_option(_lib.OPT_GATHER_ROWS, variant)
-    try:
-        out = ops.gather_rows(table, torch.as_tensor(rows, device=gpu))
-        torch.cuda.synchronize()
-        exp = table[torch.as_tensor(np.maximum(rows, 0), device=gpu).long()].clone()
-        exp[torch.as_tensor(rows < 0, device=gpu)] = 0
-        assert torch.equal(out, exp) and int(ops.err.item()) == 0
-        bad = rows.copy()
-        bad[-1] = table.shape[0]
-        out = ops.gather_rows(table, torch.as_tensor(bad, device=gpu))
-        torch.cuda.synchronize()
-        assert int(ops.err.item()) != 0 and not bool(out[-1].any())
-    finally:
-        _lib.set_option(_lib.OPT_GATHER_ROWS, prev)
