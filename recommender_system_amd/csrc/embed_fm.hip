@@ -181,6 +181,10 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   RS_STAMP(0);
   RS_USE(b);
   RS_STAMP(5);
+  if constexpr (TW) {
+    const MlpArgs& a = *tw;  // MLP_STAMP reads a.dbg
+    MLP_STAMP(0);
+  }
   // fused tower: its layer-0 weights, the bias/alpha block and the x tile's
   // zero padding do not depend on the ids; issue them first
   extern __shared__ float tsm[];
@@ -594,7 +598,13 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     }
   }
   RS_STAMP(4);
-  if constexpr (TW) mlp_tower_tile<NW>(*tw, tsm, (int64_t)tile * 16, ring, fmlog);
+  if constexpr (TW) {
+    {
+      const MlpArgs& a = *tw;
+      MLP_STAMP(1);
+    }
+    mlp_tower_tile<NW>(*tw, tsm, (int64_t)tile * 16, ring, fmlog);
+  }
 }
 
 template <int KV, int NT, int NW, int KIND, int MC, bool PF = false>
@@ -1582,6 +1592,7 @@ static int deepfm_run(const void* ids, int id_kind, int64_t id_stride, const flo
   t.c0 = c0;
   t.c1 = c1;
   t.M = batch;
+  t.dbg = mlp_diag_dbg();
   EmbedFmArgs a{};
   a.ids = ids;
   a.id_stride = id_stride;

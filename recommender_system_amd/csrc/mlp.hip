@@ -104,6 +104,9 @@ using namespace rs;
 
 static unsigned long long* g_mlp_dbg = nullptr;
 extern "C" void rs_diag_mlp_set_dbg(unsigned long long* p) { g_mlp_dbg = p; }
+namespace rs {
+unsigned long long* mlp_diag_dbg() { return g_mlp_dbg; }  // the fused towers' stamps too (deepfm_run)
+}  // namespace rs
 
 extern "C" int64_t rs_mlp_prepared_size(int n_layers, const int* dims) {
   MlpGeom g;

@@ -287,6 +287,9 @@ __device__ __forceinline__ void mlp_first_fill(const MlpArgs& a, floatx4 (&ring)
   }
 }
 
+// Diagnostics: the per-wave stamp buffer set by rs_diag_mlp_set_dbg (null = off).
+unsigned long long* mlp_diag_dbg();
+
 // Host: fill the tower part of MlpArgs from a validated geometry.
 inline bool mlp_fill_args(const MlpGeom& g, const int* acts, const float* prepared, MlpArgs& a) {
   for (int l = 0; l < g.L; ++l) {
