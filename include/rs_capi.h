@@ -75,7 +75,11 @@ enum rs_option {
                                  default) = the k-group loop of the common layer widths fully
                                  unrolled (no loop-head wait on the weight ring), 0 = the looped
                                  form.  See DESIGN.md 4.5                                         */
-  RS_OPT_COUNT = 2
+  RS_OPT_DEEPFM_KERNEL = 2,   /* rs_deepfm_fwd_hm at the Criteo shape (k 16, 26 fields, 256-unit
+                                 first layer): 0 (the default) = split wave roles (loaders +
+                                 layer-0 compute waves, deepfm_ws), 1 = one role per wave (gather
+                                 + FM, then the tower).  See DESIGN.md 4.5                       */
+  RS_OPT_COUNT = 3
 };
 
 /* ------------------------------------------------------------------ meta */

@@ -716,6 +716,213 @@ __global__ __launch_bounds__(16 * 64) void deepfm_fused_ka(EmbedFmArgs a, MlpArg
   embed_fm_body<KV, 1, 16, KIND, true, 1, false, true>(a, &t, blockIdx.x, &m);
 }
 
+// ---- Fused DeepFM with split wave roles (deepfm_ws; rs_deepfm_fwd_hm at the
+// Criteo shape: k = 16, 26 fields, 1..16 dense features, a first hidden layer
+// of 241..256 units).  The tower's first layer is the bulk of the MFMA work
+// and only needs each field's 16 columns of the tile, so it need not wait for
+// the whole gather: waves 0..7 LOAD — ids, then the rows in two bursts
+// (fields 0..15, 16..25) into the LDS tile, the FM partial tiles on the way,
+// the dense block — and count each burst in an LDS counter; waves 8..15
+// COMPUTE layer 0 (two 16-column output tiles each, k-groups in arrival
+// order: the dense group first, then the fields) with their weight ring
+// streaming from the start and waiting only on the counters.  Their vector
+// memory queue holds weights only, so no row load sits in front of a weight
+// wait.  The FM partials of the loaders meet by the last-wave finish; layers
+// 1.. run as mlp_tower_tile on all 16 waves.  Every spin is bounded.
+constexpr int WS_NL = 8;
+
+__device__ __forceinline__ void lds_wait_ge(int* p, int v) {
+  for (int spins = 0; __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v; ++spins) {
+    if (spins > (1 << 22)) break;  // a logic error must end the kernel, never hang it
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+__device__ __forceinline__ void lds_signal(int* p) {
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int KIND, int G>
+__global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, FieldMeta m) {
+  typedef Ids<KIND> I;
+  constexpr int NW = 16, F = G - 1, MF = (F + WS_NL - 1) / WS_NL;
+  static_assert(F <= 32 && MF <= 4, "deepfm_ws: <= 32 fields");
+  extern __shared__ float tsm[];
+  __shared__ floatx4 lf_acc[WS_NL][64];
+  __shared__ floatx4 lf_q[WS_NL][4];
+  __shared__ float fmlog[16];
+  __shared__ int cnt[4];  // dense k-steps written | loaders past burst 0 | past burst 1 | FM partials in
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int s = lane & 15, kk = lane >> 4;
+  const int64_t bt = (int64_t)blockIdx.x * 16 + s;
+  const bool valid = bt < a.batch;
+  const int64_t b = valid ? bt : a.batch - 1;
+  const int RS = t.rs;
+  float* par = tsm + 32 * RS + NW * 256;
+  floatx4 ring[MLP_R];
+  if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
+  if (w < WS_NL) {
+    // ================================ loader
+    const int l = w;
+    const float w0v = a.w0[0];
+    const int dw = l - (WS_NL - a.DB);  // dense k-steps on the last DB loaders (fewest fields)
+    const bool has_dense = dw >= 0;
+    float dx = 0.f, drec = 0.f, dn = 0.f;
+    if (has_dense) {
+      const int e = 4 * dw + kk;
+      dx = a.dense[b * a.dense_stride + (e < a.nd ? e : 0)];
+      const float* rec = a.prep + (int64_t)dw * a.dense_rec;
+      drec = rec[lane];
+      dn = rec[64 + kk];
+    }
+    typename I::raw_t rid[MF];
+    floatx4 bw[MF];
+#pragma unroll
+    for (int p = 0; p < MF; ++p) {
+      const int c = l + WS_NL * p;
+      bw[p] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (c < F) {
+        rid[p] = I::load(a.ids, b * a.id_stride + c);
+        if (s <= a.kfm) bw[p] = *reinterpret_cast<const floatx4*>(a.prep + a.field_base + (int64_t)c * a.field_rec + lane * 4);
+      }
+    }
+    for (int i = threadIdx.x; i < t.ptot; i += WS_NL * 64) par[i] = t.prep[t.wtot + i];
+    __syncthreads();  // the counters start at 0 (the compute waves pass the same barrier)
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    float qn = 0.f;
+    if (has_dense) {  // the dense group of the tile: dense columns + the zero padding up to 16
+      const int e = 4 * dw + kk;
+      const float x = e < a.nd ? dx : 0.f;
+      acc = mfma16x16x4(x, drec, acc);
+      qn = fmaf(x * x, dn, qn);
+      tsm[s * RS + F * 16 + e] = x;
+      lds_signal(&cnt[0]);
+    }
+    float nrm[MF][4];
+#pragma unroll
+    for (int p = 0; p < MF; ++p)
+#pragma unroll
+      for (int tp = 0; tp < 4; ++tp) nrm[p][tp] = row16_sum(s < a.kfm ? bw[p][tp] * bw[p][tp] : 0.f);
+    bool bad = false;
+#pragma unroll
+    for (int burst = 0; burst < 2; ++burst) {
+      floatx4 xs[2];
+      bool ok[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int p = 2 * burst + q, c = l + WS_NL * p;
+        ok[q] = false;
+        if (p < MF && c < F) {
+          int64_t id;
+          ok[q] = I::decode(rid[p], m.voc[c], id);
+          xs[q] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(a.table + (m.off[c] + id) * 16) + kk);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int p = 2 * burst + q, c = l + WS_NL * p;
+        if (p < MF && c < F) {
+          bad |= !ok[q];
+          const floatx4 x = ok[q] ? xs[q] : floatx4{0.f, 0.f, 0.f, 0.f};
+          *reinterpret_cast<floatx4*>(tsm + s * RS + c * 16 + 4 * kk) = x;
+#pragma unroll
+          for (int tp = 0; tp < 4; ++tp) {
+            acc = mfma16x16x4(x[tp], bw[p][tp], acc);
+            qn = fmaf(x[tp] * x[tp], nrm[p][tp], qn);
+          }
+        }
+      }
+      lds_signal(&cnt[1 + burst]);
+    }
+    if (__any(bad && valid) && lane == 0) flag_error(a.err);
+    // FM: last-wave finish over the loaders' partial tiles (wave order)
+    lf_acc[l][lane] = acc;
+    qn += __shfl_xor(qn, 16);
+    qn += __shfl_xor(qn, 32);
+    if (lane < 16) reinterpret_cast<float*>(&lf_q[l][0])[lane] = qn;
+    int old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(&cnt[3], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old == WS_NL - 1) {
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ww = 0; ww < WS_NL; ++ww) {
+        const floatx4 pv = lf_acc[ww][lane];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] += pv[i];
+      }
+      const floatx4 q4 = lf_q[s < WS_NL ? s : 0][kk];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float tt = s < a.kfm ? v[i] * v[i] : 0.f;
+        if (s < WS_NL) tt -= q4[i];
+        float ll = s == a.kfm ? v[i] : 0.f;
+        tt = row16_sum(tt);
+        ll = row16_sum(ll);
+        const float fm = (ll + w0v) + 0.5f * tt;
+        const int64_t bb = (int64_t)blockIdx.x * 16 + 4 * kk + i;
+        if (s == 0) {
+          fmlog[4 * kk + i] = fm;
+          if (bb < a.batch && a.logit) a.logit[bb] = fm;
+        }
+      }
+    }
+  } else {
+    // ================================ layer 0 compute
+    const int c8 = w - WS_NL;
+    const floatx4* W0 = reinterpret_cast<const floatx4*>(t.prep + t.off[0]) + lane + (int64_t)c8 * G * 64;
+    const floatx4* W1 = W0 + (int64_t)WS_NL * G * 64;  // output tile c8 + 8
+    // k-group order: the dense group (G - 1) first, then fields 0 .. F-1
+    auto grp = [](int i) { return i == 0 ? G - 1 : i - 1; };
+    floatx4 r0[3], r1[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      r0[u] = W0[(int64_t)grp(u) * 64];
+      r1[u] = W1[(int64_t)grp(u) * 64];
+    }
+    __syncthreads();  // the counters start at 0
+    const float* ap = tsm + s * RS + 4 * kk;
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    lds_wait_ge(&cnt[0], a.DB);
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      if (i == 1) lds_wait_ge(&cnt[1], WS_NL);       // fields 0..15 in the tile
+      if (i == 1 + 2 * WS_NL) lds_wait_ge(&cnt[2], WS_NL);  // fields 16..
+      const int u = i % 3;
+      const floatx4 av = *reinterpret_cast<const floatx4*>(ap + 16 * grp(i));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc0 = mfma16x16x4(av[j], r0[u][j], acc0);
+        acc1 = mfma16x16x4(av[j], r1[u][j], acc1);
+      }
+      const int nx = i + 3 < G ? i + 3 : G - 1;
+      r0[u] = W0[(int64_t)grp(nx) * 64];
+      r1[u] = W1[(int64_t)grp(nx) * 64];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const float* bias = par + t.poff[0];
+    const float* alpha = bias + t.Np[0];
+    float* out = tsm + 16 * RS;  // layer 0 -> buf1
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * kk + r, col0 = 16 * c8 + s, col1 = col0 + 16 * WS_NL;
+      out[row * RS + col0] = mlp_act(acc0[r] + bias[col0], t.act[0], alpha[col0]);
+      out[row * RS + col1] = mlp_act(acc1[r] + bias[col1], t.act[0], alpha[col1]);
+    }
+  }
+  {  // layer 1's first weights (this wave's first item of it, if any)
+    const int T1 = t.Np[1] >> 4, G1 = t.Kp[1] >> 4;
+    const int S1 = mlp_slices(T1, G1, NW);
+    if (w < T1 * S1) {
+      const MlpItem it = mlp_item(w, T1, G1, S1);
+      mlp_ring_fill(ring, reinterpret_cast<const floatx4*>(t.prep + t.off[1]) + lane + (int64_t)it.t * G1 * 64,
+                    it.g0, it.g1);
+    }
+  }
+  mlp_tower_tile<NW>(t, tsm, (int64_t)blockIdx.x * 16, ring, fmlog, 1);
+}
+
 // Generic fallback (any k / kfm): one 256-thread workgroup per sample.
 __device__ __forceinline__ float block_sum(float v, float* red) {
 #pragma unroll
@@ -1549,13 +1756,32 @@ static bool deepfm_geom(int nd, int n_fields, int k, int kfm, int n_layers, cons
   return dims[0] == nd + n_fields * k && dims[n_layers] == 1 && mg.lds <= 120 * 1024;
 }
 
+// deepfm_ws covers: kernel-argument metadata, k = 16, 26 fields, 13..16 dense
+// features (one k-group of dense + padding, written whole by the 4 dense
+// loaders), a first hidden layer of 241..256
+// units (16 output tiles: two per compute wave), >= 2 layers whose second has
+// >= 8 output tiles (its items start on the loader waves)
+static bool deepfm_ws_ok(const EmbedFmArgs& a, const MlpArgs& t, const FieldMeta* hm, int KV) {
+  return hm && KV == 4 && a.F == 26 && a.nd >= 13 && a.nd <= 16 && a.DB == 4 && t.L >= 2 &&
+         t.Np[0] == 256 && t.Kp[0] == 16 * (a.F + 1) && (t.Np[1] >> 4) >= WS_NL &&
+         opt(RS_OPT_DEEPFM_KERNEL) == 0;
+}
+
 template <int KV, int KIND>
 static void launch_deepfm(const EmbedFmArgs& a, const MlpArgs& t, size_t lds, hipStream_t st,
                           const FieldMeta* hm) {
+  const unsigned grid = (unsigned)((a.batch + 15) / 16);
+  if constexpr (KV == 4) {
+    if (deepfm_ws_ok(a, t, hm, KV)) {
+      static LdsAttr ws_set;
+      lds_attr(ws_set, (const void*)deepfm_ws<KIND, 27>, lds);
+      deepfm_ws<KIND, 27><<<grid, 16 * 64, lds, st>>>(a, t, *hm);
+      return;
+    }
+  }
   static LdsAttr lds_set[2];  // opt in to exactly what is needed beyond the default
   const int ka = hm && a.F <= 32 ? 1 : 0;
   lds_attr(lds_set[ka], ka ? (const void*)deepfm_fused_ka<KV, KIND> : (const void*)deepfm_fused<KV, KIND>, lds);
-  const unsigned grid = (unsigned)((a.batch + 15) / 16);
   if (ka) deepfm_fused_ka<KV, KIND><<<grid, 16 * 64, lds, st>>>(a, t, *hm);
   else deepfm_fused<KV, KIND><<<grid, 16 * 64, lds, st>>>(a, t);
 }

@@ -189,18 +189,20 @@ __device__ __forceinline__ void mlp_mac(floatx4 (&ring)[MLP_R], const float* ap,
 // The tower on a 16-row tile whose input is already in LDS buf0 (barrier not
 // yet taken) and whose layer-0 ring was filled by the caller.  smem layout:
 // buf0 [16][rs] | buf1 [16][rs] | red [NW][256] | par [ptot] (loaded here).
+// l0 > 0: layers 0 .. l0-1 were computed by the caller (layer l0's input is
+// in buf (l0 & 1), its ring filled).
 template <int NW>
 __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, int64_t m0, floatx4 (&ring)[MLP_R],
-                                               const float* extra_lds = nullptr) {
+                                               const float* extra_lds = nullptr, int l0 = 0) {
   const int RS = a.rs;
   float* red = smem + 32 * RS;
   float* par = red + NW * 256;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
-  float* in = smem;
-  float* out = smem + 16 * RS;
-  for (int l = 0; l < a.L; ++l) {
+  float* in = (l0 & 1) ? smem + 16 * RS : smem;
+  float* out = (l0 & 1) ? smem : smem + 16 * RS;
+  for (int l = l0; l < a.L; ++l) {
     const int T = a.Np[l] >> 4, G = a.Kp[l] >> 4;
     const int S = mlp_slices(T, G, NW);
     __syncthreads();

@@ -1,6 +1,8 @@
 """Per-wave s_memtime stamps (shader cycles) of the fused DeepFM kernel
 (rs_deepfm_fwd_hm: gather + FM + DNN tower + head, one launch; diagnostic hook
-rs_diag_mlp_set_dbg, compiled into the product library behind a null check):
+rs_diag_mlp_set_dbg, compiled into the product library behind a null check;
+DIAG_DEEPFM_OPT = RS_OPT_DEEPFM_KERNEL, default 1 — the split-role form 0
+stamps only the layers after its first):
   0 entry, 1 gather + FM combine done (tower about to start), 2+2l layer l
   after its barrier, 3+2l layer l's contraction done, 15 end.
 Prints the median over workgroups of each phase (relative to the workgroup's
@@ -35,6 +37,7 @@ def main():
     dbg = torch.zeros(nwg * 16 * 16, dtype=torch.int64, device=dev)
     lib = _lib.lib()
     lib.rs_diag_mlp_set_dbg.argtypes = [C.c_void_p]
+    _lib.set_option(_lib.OPT_DEEPFM_KERNEL, int(os.environ.get("DIAG_DEEPFM_OPT", "1")))
     for i in range(40):
         m.forward_fused((dense[i % NP], ids[i % NP]), check_ids=False)
     torch.cuda.synchronize()
@@ -49,7 +52,7 @@ def main():
         names[2 + 2 * l] = f"l{l}_start"
         names[3 + 2 * l] = f"l{l}_mac_done"
     names[15] = "end"
-    out = {"B": B, "V": V, "phases_cycles": {}}
+    out = {"B": B, "V": V, "deepfm_kernel_option": int(os.environ.get("DIAG_DEEPFM_OPT", "1")), "phases_cycles": {}}
     for j, n in names.items():
         rel = d[:, :, j] - t0
         out["phases_cycles"][n] = {"median_wave": int(np.median(rel)), "slowest_wave": int(np.median(rel.max(axis=1)))}

@@ -919,3 +919,49 @@ def test_hm_front_end_bit_identical(gpu, F, B, id_dtype):
                       st)
         torch.cuda.synchronize()
         assert int(err.item()) != 0, entry
+
+
+# --------------------------- fused DeepFM kernel forms (RS_OPT_DEEPFM_KERNEL)
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("B,id_dtype,hidden,nd", [(4096, np.int32, [256, 128, 64], 13), (4093, np.int64, [248, 160, 8], 13),
+                                                  (33, np.float32, [256, 128], 16), (1, np.int32, [256, 128, 64], 13),
+                                                  (300, np.int32, [256, 128, 64], 9)])
+def test_deepfm_kernel_forms(gpu, variant, B, id_dtype, hidden, nd):
+    """rs_deepfm_fwd_hm in both forms — 0: split wave roles (loader waves
+    gather the rows and the FM while compute waves run the first layer as the
+    fields land; the Criteo shape), 1: one role per wave — == the fp64
+    oracle (post-sigmoid 1e-5 relative), the FM logit output too, and an
+    out-of-range id raises.  Shapes outside the split form's (nd 9 here) run
+    the one-role kernel under both values."""
+    from recommender_system_amd import DeepFM, _lib
+    from tests.helpers import criteo_columns, dnn_params, tables_of
+    rng = np.random.default_rng(B + nd)
+    vocabs = rng.integers(2, 5000, size=26)
+    m = DeepFM(criteo_columns(vocabs, n_dense=nd, embed_dim=16), 10, 1e-4, 1e-4, hidden, 1, "relu", embed_dim=16,
+               seed=9)
+    with torch.no_grad():
+        for l in m.dnn._layers():
+            l.bias.uniform_(-0.1, 0.1)
+        m.embed_layer.table.mul_(10.0)  # O(0.5) rows: the tower and the FM both matter
+    ids = random_ids(rng, B, vocabs, np.int64)
+    ids[0] = vocabs - 1
+    dense = rng.random((B, nd)).astype(np.float32)
+    ids_t = torch.as_tensor(ids, device=gpu).to({np.int32: torch.int32, np.int64: torch.int64,
+                                                 np.float32: torch.float32}[id_dtype])
+    prev = _lib.set_option(_lib.OPT_DEEPFM_KERNEL, variant)
+    try:
+        fm = torch.empty(B, 1, device="cuda")
+        y = m.forward_fused((torch.as_tensor(dense, device=gpu), ids_t), fm_logit=fm)
+        torch.cuda.synchronize()
+        hidden_p, out_p = dnn_params(m.dnn)
+        p = {"tables": tables_of(m.embed_layer), "w0": m.fm.w0.cpu().numpy(), "w1": m.fm.w1.cpu().numpy(),
+             "v": m.fm.v.cpu().numpy(), "dnn_hidden": hidden_p, "dnn_out": out_p}
+        ref, ref_fm, _ = O.deepfm(None, p, nd=nd, inputs=(dense, ids))
+        assert_rel_close(y, ref, what=f"DeepFM kernel form {variant}")
+        assert_scaled_close(fm, ref_fm, what=f"DeepFM kernel form {variant} fm logit")
+        bad = ids_t.clone()
+        bad[B - 1, 25] = int(vocabs[25])
+        with pytest.raises(IndexError):
+            m.forward_fused((torch.as_tensor(dense, device=gpu), bad))
+    finally:
+        _lib.set_option(_lib.OPT_DEEPFM_KERNEL, prev)
