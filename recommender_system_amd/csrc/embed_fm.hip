@@ -760,6 +760,10 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
   const int RS = t.rs;
   float* par = tsm + 32 * RS + NW * 256;
   floatx4 ring[MLP_R];
+  {
+    const MlpArgs& a = t;  // MLP_STAMP reads a.dbg (diagnostic hook)
+    MLP_STAMP(0);
+  }
   if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
   if (w < WS_NL) {
     // ================================ loader
@@ -910,6 +914,10 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
       out[row * RS + col0] = mlp_act(acc0[r] + bias[col0], t.act[0], alpha[col0]);
       out[row * RS + col1] = mlp_act(acc1[r] + bias[col1], t.act[0], alpha[col1]);
     }
+  }
+  {
+    const MlpArgs& a = t;
+    MLP_STAMP(1);  // loader: rows + FM done; compute wave: layer 0 done
   }
   {  // layer 1's first weights (this wave's first item of it, if any)
     const int T1 = t.Np[1] >> 4, G1 = t.Kp[1] >> 4;
