@@ -809,13 +809,15 @@ def _dice_train_bwd(dy, z, alpha, eps, saved):
     return dx, dalpha
 
 
-def _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt, att_act="prelu", dnn_act="prelu"):
+def _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt, att_act="prelu", dnn_act="prelu",
+                       drop_mask=None):
     """DIN.call (model/din.py:56-95) with training=True (Keras fit): the
     BatchNormalization normalises with the batch's own mean and (biased)
     variance, and so do the Dice layers' BatchNormalizations (the fit's
     training flag reaches every nested layer call).  att / dnn activation
     'prelu' (the reference defaults) or 'dice'.  Returns every intermediate
-    the hand backward needs."""
+    the hand backward needs.  drop_mask: the Dropout after the DNN
+    (model/din.py:93) as a fixed [B, h] multiplier, or None (the identity)."""
     c = {}
     dense_in = np.concatenate([cast_inputs(inputs[f], dt).reshape(-1, 1) for f in dense_feats], -1) \
         if dense_feats else None
@@ -868,23 +870,25 @@ def _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt,
             yz, saved = _dice_train(z, al[0], al[3], dt)
             dsaved.append(saved)
             acts.append(yz)
-    logit = (acts[-1] @ np.asarray(p["out"][0], dt) + np.asarray(p["out"][1], dt))[:, 0]
-    c.update(seq=seq, item=item, mask=mask, q=q, att_pre=att_pre, att_in=att_in, a=a, x=x, bmu=bmu, bvar=bvar,
+    top = acts[-1] * np.asarray(drop_mask, dt) if drop_mask is not None else acts[-1]
+    logit = (top @ np.asarray(p["out"][0], dt) + np.asarray(p["out"][1], dt))[:, 0]
+    c.update(top=top, seq=seq, item=item, mask=mask, q=q, att_pre=att_pre, att_in=att_in, a=a, x=x, bmu=bmu, bvar=bvar,
              xhat=xhat, pre=pre, acts=acts, dsaved=dsaved, logit=logit, B=B, T=T, K=K, nd=0 if dense_in is None else
              dense_in.shape[1], other_sparse=other_sparse)
     return c
 
 
 def din_loss(inputs, t, p, dense_feats, sparse_feats, behavior_feats, dt=np.float64, att_act="prelu",
-             dnn_act="prelu"):
+             dnn_act="prelu", drop_mask=None):
     """compile_fit's objective on DIN (training-mode forward): mean BCE."""
-    z = _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt, att_act, dnn_act)["logit"]
+    z = _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt, att_act, dnn_act,
+                           drop_mask)["logit"]
     t = np.asarray(t, dt).reshape(-1)
     return np.mean(np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z))))
 
 
 def din_train_step(inputs, t, p, dense_feats, sparse_feats, behavior_feats, lr, momentum=0.99, dt=np.float64,
-                   att_act="prelu", dnn_act="prelu"):
+                   att_act="prelu", dnn_act="prelu", drop_mask=None):
     """One SGD step of compile_fit on DIN (utils/compile_fit.py:9-15; model/
     din.py:56-95, att 'prelu', dnn 'prelu'), backpropagated by hand:
     BCE on the sigmoid's logit (g = (sigmoid(z) - t)/B); Dense + PReLU layers
@@ -896,8 +900,10 @@ def din_train_step(inputs, t, p, dense_feats, sparse_feats, behavior_feats, lr, 
     (dq sums over T); embedding rows by scatter-add.  No regularisers.
     Dice (att / dnn 'dice'): training-mode batch statistics in the forward,
     the batch-norm backward inside its gradient, its moving averages moved
-    like the BN's.  Returns (new p, per-sample losses before the step)."""
-    c = _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt, att_act, dnn_act)
+    like the BN's.  drop_mask: the Dropout after the DNN (din.py:93) as a
+    fixed [B, h] multiplier (dL/d(dnn out) = dL/d(dropped) * mask), or None.
+    Returns (new p, per-sample losses before the step)."""
+    c = _din_train_forward(inputs, p, dense_feats, sparse_feats, behavior_feats, dt, att_act, dnn_act, drop_mask)
     B, T, K = c["B"], c["T"], c["K"]
     t = np.asarray(t, dt).reshape(-1)
     z = c["logit"]
@@ -906,8 +912,10 @@ def din_train_step(inputs, t, p, dense_feats, sparse_feats, behavior_feats, lr, 
     new = {"sparse_tables": {f: np.array(v, dt) for f, v in p["sparse_tables"].items()},
            "seq_tables": {f: np.array(v, dt) for f, v in p["seq_tables"].items()}}
     Wo, bo = (np.asarray(v, dt) for v in p["out"])
-    new["out"] = (Wo - lr * (c["acts"][-1].T @ g[:, None]), bo - lr * g.sum(keepdims=True))
+    new["out"] = (Wo - lr * (c["top"].T @ g[:, None]), bo - lr * g.sum(keepdims=True))
     dh = g[:, None] @ Wo.T
+    if drop_mask is not None:
+        dh = dh * np.asarray(drop_mask, dt)
     new_dnn = [None] * len(p["dnn"])
     for li in reversed(range(len(p["dnn"]))):
         W, b = (np.asarray(v, dt) for v in p["dnn"][li][:2])
@@ -984,7 +992,7 @@ def din_train_step(inputs, t, p, dense_feats, sparse_feats, behavior_feats, lr, 
     return new, loss
 
 
-def _nfm_train_forward(dense, ids, p, dt):
+def _nfm_train_forward(dense, ids, p, dt, masks=None):
     tables = [np.asarray(tb, dt) for tb in p["tables"]]
     k = tables[0].shape[1]
     flat = embed_layer(cast_ids(ids), tables, dt)
@@ -994,21 +1002,23 @@ def _nfm_train_forward(dense, ids, p, dt):
     mu, var = x.mean(0), x.var(0)
     xhat = (x - mu) / np.sqrt(var + eps)
     acts = [xhat * np.asarray(g_, dt) + np.asarray(b_, dt)]
-    for W, b in p["dnn_hidden"]:
-        acts.append(activation(acts[-1] @ np.asarray(W, dt) + np.asarray(b, dt), p.get("act", "relu")))
+    for i, (W, b) in enumerate(p["dnn_hidden"]):  # DNNLayer: Dense, then Dropout (masks[i] or the identity)
+        a = activation(acts[-1] @ np.asarray(W, dt) + np.asarray(b, dt), p.get("act", "relu"))
+        acts.append(a * np.asarray(masks[i], dt) if masks is not None else a)
     acts.append(acts[-1] @ np.asarray(p["dnn_out"][0], dt) + np.asarray(p["dnn_out"][1], dt))
     logit = (acts[-1] @ np.asarray(p["out"][0], dt) + np.asarray(p["out"][1], dt))[:, 0]
     return dict(e=e, x=x, mu=mu, var=var, xhat=xhat, acts=acts, logit=logit)
 
 
-def nfm_loss(dense, ids, t, p, dt=np.float64):
-    """compile_fit's objective on NFM (training-mode BatchNormalization)."""
-    z = _nfm_train_forward(dense, ids, p, dt)["logit"]
+def nfm_loss(dense, ids, t, p, dt=np.float64, masks=None):
+    """compile_fit's objective on NFM (training-mode BatchNormalization;
+    masks: fixed dropout multipliers, or None)."""
+    z = _nfm_train_forward(dense, ids, p, dt, masks)["logit"]
     t = np.asarray(t, dt).reshape(-1)
     return np.mean(np.maximum(z, 0) - z * t + np.log1p(np.exp(-np.abs(z))))
 
 
-def nfm_train_step(dense, ids, t, p, lr, momentum=0.99, dt=np.float64):
+def nfm_train_step(dense, ids, t, p, lr, momentum=0.99, dt=np.float64, masks=None):
     """One SGD step of compile_fit on NFM (utils/compile_fit.py:9-15;
     model/nfm.py:22-33 with 3-D embeddings, training=True): BCE on the
     sigmoid's logit; output Dense(1) and the DNNLayer (relu hidden, linear
@@ -1017,9 +1027,12 @@ def nfm_train_step(dense, ids, t, p, lr, momentum=0.99, dt=np.float64):
     Bi-Interaction 0.5((sum_f e_f)^2 - sum_f e_f^2) gives de_f = dbi (S - e_f),
     S = sum_f e_f; embedding rows by scatter-add.  No regularisers.
     p: tables, bn (gamma, beta, mean, var, eps), dnn_hidden [(W, b)],
-    dnn_out (W, b), out (W, b).  Returns (new p, per-sample losses)."""
+    dnn_out (W, b), out (W, b).  masks: DNNLayer's Dropout (interaction.py:
+    44) in training, per hidden layer a [B, h] multiplier (None = the
+    identity); the backward multiplies dL/d(hidden out) by it.
+    Returns (new p, per-sample losses)."""
     ids = cast_ids(ids)
-    c = _nfm_train_forward(dense, ids, p, dt)
+    c = _nfm_train_forward(dense, ids, p, dt, masks)
     t = np.asarray(t, dt).reshape(-1)
     z = c["logit"]
     B = z.shape[0]
@@ -1038,6 +1051,8 @@ def nfm_train_step(dense, ids, t, p, lr, momentum=0.99, dt=np.float64):
         prev = delta @ W.T
         if 0 < li <= nh and p.get("act", "relu") == "relu":  # acts[li] = relu output of hidden layer li-1
             prev = prev * (acts[li] > 0)
+        if 0 < li <= nh and masks is not None:
+            prev = prev * np.asarray(masks[li - 1], dt)
         delta = prev
     gam, bet, mu0, var0, eps = p["bn"]
     gam, bet = np.asarray(gam, dt), np.asarray(bet, dt)

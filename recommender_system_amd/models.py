@@ -81,7 +81,7 @@ def _dnn_backward(layers, acts, delta, gw, emp, st, outs=None, drop=None):
         prev = emp(B, K_in)
         call("rs_gemm", 0, 1, B, K_in, N_out, 1.0, ptr(delta), delta.stride(0), ptr(L.kernel), N_out, 0.0,
              ptr(prev), K_in, ptr(a_in) if relu_below else None, a_in.stride(0), *gw, st)
-        if drop is not None and li > 0:
+        if drop is not None and 0 < li <= len(drop[2]):  # acts[li] is dropped hidden output li-1
             rng, rate, offs = drop
             rng.redraw(prev, rate, offs[li - 1], st)
         delta = prev
@@ -129,7 +129,9 @@ class _Dropout:
     masks differ across layers and steps and the backward regenerates a
     draw's mask from its (seed, offset) instead of storing it.  TF's own draws
     cannot be reproduced; oracle.dropout_multiplier restates this generator.
-    (A captured hipGraph replays the offsets it was captured with.)"""
+    The offsets live on the host, so a captured hipGraph would replay the
+    masks it was captured with: draw() refuses stream capture (train with
+    dropout=False, or eagerly, to capture)."""
 
     def __init__(self, seed):
         self.seed = int(seed) & (2 ** 64 - 1)
@@ -137,6 +139,9 @@ class _Dropout:
 
     def draw(self, t, rate, st):
         """Apply a fresh mask to t [rows, cols] in place; returns its offset."""
+        if t.is_cuda and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("dropout in a captured graph would replay one mask every step; "
+                               "pass dropout=False to capture a training step")
         off = self.offset
         self.redraw(t, rate, off, st)
         self.offset += (t.shape[0] * t.shape[1] + 3) // 4 * 4
@@ -175,22 +180,6 @@ def _dnn_train_forward(model, dnn, x, rate, st):
             offs.append(rng.draw(a, rate, st))
         acts.append(a)
     return acts, ((rng, rate, offs) if rng is not None else None)
-
-
-_DROPOUT_WARNED = set()
-
-
-def _dropout_notice(name, layer, dropout):
-    """NFM / DIN (whose Dropout rates default to 0, model/nfm.py:13,
-    model/din.py:18) run a Dropout rate > 0 as the identity in their training
-    steps: say so once, unless dropout=False acknowledges it."""
-    if dropout is False or not getattr(layer, "dropout", 0):
-        return
-    if name not in _DROPOUT_WARNED:
-        _DROPOUT_WARNED.add(name)
-        import warnings
-        warnings.warn(f"{name}.train_step: dropout={layer.dropout} is applied as the identity (no dropout "
-                      f"masks); pass dropout=False to silence", RuntimeWarning, stacklevel=3)
 
 
 def _gemm_ws(model, nbytes):
@@ -861,11 +850,13 @@ class DIN(TowerMixin, KerasModule):
           rs_din_att_concat_bwd; then one rs_sgd_update_multi over every dense parameter
           and row-sparse rs_embedding_sgd of the behaviour tables (history
           rows, then candidates) and the other sparse tables.
-        Dropout (after the DNN, :93) runs as the identity (see
-        _dropout_notice).  Returns per-sample losses (before the step) if
+        Dropout(dnn_dropout) after the DNN (:93) runs in training mode: one
+        rs_dropout draw on the last DNN output, the same mask regenerated on
+        its gradient (dropout=False turns it off, a float overrides the
+        rate).  Returns per-sample losses (before the step) if
         ``return_loss``."""
         att, bn = self.att_layer, self.bn_layer
-        _dropout_notice("DIN", self, dropout)
+        rate = _dropout_rate(self, dropout)
         dev, st = self._dev, _lib.stream()
         nb = len(self.seq_feats)
         hists = [_ids_tensor(inputs[f["feat"]], dev) for f in self.seq_feats]
@@ -975,6 +966,9 @@ class DIN(TowerMixin, KerasModule):
                 dsaved.append(None)
             pre.append(z)
             acts.append(y)
+        if rate > 0:  # in place: the backward reads the layers' pre-activations, and BN's input, only
+            rng = _dropout_rng(self)
+            drop_off = rng.draw(acts[-1], rate, st)
         out = self.out_layer
         logit = emp(B)
         call("rs_dense_fwd", ptr(acts[-1]), acts[-1].stride(0), ptr(out.kernel), ptr(out.bias), None,
@@ -1012,6 +1006,8 @@ class DIN(TowerMixin, KerasModule):
             return dx
 
         dh = dense_back(out.kernel, out.bias, acts[-1], g.view(B, 1), B)
+        if rate > 0:
+            rng.redraw(dh, rate, drop_off, st)
         for li in reversed(range(len(self.dense_layer))):
             L = self.dense_layer[li]
             if L.activation == "dice":
@@ -1131,10 +1127,13 @@ class NFM(TowerMixin, KerasModule):
           (rs_dense_fwd, logit), rs_head_grad, the DNN backward (rs_gemm /
           rs_col_sum), rs_bn_train_bwd, rs_bi_interaction_bwd (de_f = dbi
           (S - e_f)), SGD of the dense parameters and row-sparse
-          rs_embedding_sgd.  Dropout as the identity (_dropout_notice).
+          rs_embedding_sgd.  DNNLayer's Dropout after each hidden layer
+          (layer/interaction.py:44) runs in training mode as in
+          DeepFM.train_step (counter-based rs_dropout masks, regenerated in
+          the backward; dropout=False turns it off, a float overrides the rate).
         Returns per-sample losses (before the step) if ``return_loss``."""
         dnn = self.dnn_layers
-        _dropout_notice("NFM", dnn, dropout)
+        rate = _dropout_rate(dnn, dropout)
         _check_train_tower("NFM", dnn)
         dense, ids = _split_criteo(inputs, self.nd, self._dev)
         labels = _to_device_f32(labels, self._dev).reshape(-1)
@@ -1148,9 +1147,8 @@ class NFM(TowerMixin, KerasModule):
         call("rs_bn_train_fwd", ptr(x), D, B, D, ptr(bn.gamma), ptr(bn.beta), bn.epsilon, 0.99, ptr(bn.moving_mean),
              ptr(bn.moving_variance), ptr(mean), ptr(var), ptr(y0), D, st)
         layers = self._layers()
-        acts = [y0]
-        for L in layers[:-1]:
-            acts.append(L(acts[-1]))
+        acts, drop = _dnn_train_forward(self, dnn, y0, rate, st)
+        acts.append(dnn.output_layer(acts[-1]))
         logit = emp(B)
         call("rs_dense_fwd", ptr(acts[-1]), acts[-1].stride(0), ptr(out.kernel), ptr(out.bias), None,
              _lib.ACT[None], ptr(logit), 1, B, out.kernel.shape[0], 1, st)
@@ -1159,7 +1157,7 @@ class NFM(TowerMixin, KerasModule):
         call("rs_head_grad", ptr(logit), ptr(logit), ptr(labels), B, 1.0, 0.0, ptr(g), ptr(g0), ptr(loss), st)
         gws = _gemm_ws(self, max(_lib.lib().rs_gemm_workspace_size(L.kernel.shape[0], L.kernel.shape[1], B)
                                  for L in layers))
-        grads, delta = _dnn_backward(layers, acts, g.view(B, 1), (ptr(gws), gws.numel()), emp, st)
+        grads, delta = _dnn_backward(layers, acts, g.view(B, 1), (ptr(gws), gws.numel()), emp, st, drop=drop)
         dx, dgam, dbet = emp(B, D), emp(D), emp(D)
         call("rs_bn_train_bwd", ptr(x), D, B, D, ptr(mean), ptr(var), ptr(bn.gamma), bn.epsilon, ptr(delta),
              delta.stride(0), ptr(dx), D, ptr(dgam), ptr(dbet), st)

@@ -5,5 +5,5 @@
 set -e
 cd "$(dirname "$0")/.."
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DRS_DIAG_STAMPS -I include -I recommender_system_amd/csrc \
-  recommender_system_amd/csrc/embed_fm.hip recommender_system_amd/csrc/embed_fm_tiles.hip recommender_system_amd/csrc/capi.cpp \
+  recommender_system_amd/csrc/embed_fm.hip recommender_system_amd/csrc/embed_fm_tiles.hip recommender_system_amd/csrc/mlp.hip recommender_system_amd/csrc/capi.cpp \
   -o recommender_system_amd/librs_hip_diag.so

@@ -226,18 +226,20 @@ def _assert_update_close(got, ref, before, rtol=2e-3, what=""):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("att_hidden,dnn_hidden,nb,k,B,T,att_act,dnn_act,fused", [
-    ((80, 40), (256, 128, 64), 1, 8, 256, 20, "prelu", "prelu", True),   # the reference defaults
-    ((80, 40), (256, 128, 64), 1, 8, 256, 20, "prelu", "prelu", False),  # ... attention unit layer by layer
-    ((80, 40), (64, 32), 2, 8, 192, 30, "prelu", "prelu", True),         # item + category features (K = 16)
-    ((80, 40), (64, 32), 1, 8, 40, 100, "prelu", "prelu", True),         # config 4's T = 100 (Rp = 112)
-    ((56, 24), (16,), 1, 8, 30, 128, "prelu", "prelu", True),            # T = 128, widths with pads
-    ((80, 40), (64, 32), 1, 8, 300, 7, "prelu", "prelu", True),          # T = 7: one row tile, > 256 samples
-    ((32,), (16,), 2, 4, 64, 7, "prelu", "prelu", True),                 # one attention layer, small ragged T
-    ((80, 40), (64, 32), 1, 8, 256, 20, "prelu", "dice", True),          # dnn_activation='dice'
-    ((80, 40), (64, 32), 2, 8, 128, 30, "dice", "dice", True),           # att_attention='dice' too
+@pytest.mark.parametrize("att_hidden,dnn_hidden,nb,k,B,T,att_act,dnn_act,fused,rate", [
+    ((80, 40), (256, 128, 64), 1, 8, 256, 20, "prelu", "prelu", True, 0.0),   # the reference defaults
+    ((80, 40), (256, 128, 64), 1, 8, 256, 20, "prelu", "prelu", True, 0.2),   # ... with dnn_dropout=0.2
+    ((80, 40), (64, 32), 1, 8, 256, 20, "prelu", "dice", True, 0.2),          # dropout after a Dice DNN
+    ((80, 40), (256, 128, 64), 1, 8, 256, 20, "prelu", "prelu", False, 0.0),  # ... attention unit layer by layer
+    ((80, 40), (64, 32), 2, 8, 192, 30, "prelu", "prelu", True, 0.0),         # item + category features (K = 16)
+    ((80, 40), (64, 32), 1, 8, 40, 100, "prelu", "prelu", True, 0.0),         # config 4's T = 100 (Rp = 112)
+    ((56, 24), (16,), 1, 8, 30, 128, "prelu", "prelu", True, 0.0),            # T = 128, widths with pads
+    ((80, 40), (64, 32), 1, 8, 300, 7, "prelu", "prelu", True, 0.0),          # T = 7: one row tile, > 256 samples
+    ((32,), (16,), 2, 4, 64, 7, "prelu", "prelu", True, 0.0),                 # one attention layer, small ragged T
+    ((80, 40), (64, 32), 1, 8, 256, 20, "prelu", "dice", True, 0.0),          # dnn_activation='dice'
+    ((80, 40), (64, 32), 2, 8, 128, 30, "dice", "dice", True, 0.0),           # att_attention='dice' too
 ])
-def test_din_train_steps_match_oracle(gpu, att_hidden, dnn_hidden, nb, k, B, T, att_act, dnn_act, fused):
+def test_din_train_steps_match_oracle(gpu, att_hidden, dnn_hidden, nb, k, B, T, att_act, dnn_act, fused, rate):
     """DIN.train_step (compile_fit on DIN in training mode: batch-statistics
     BatchNormalization with moving averages, PReLU attention over [T, h]
     alphas, masked softmax pool, PReLU DNN, SGD + row-sparse embedding SGD)
@@ -246,12 +248,16 @@ def test_din_train_steps_match_oracle(gpu, att_hidden, dnn_hidden, nb, k, B, T, 
     fully padded history row and non-trivial parameters.  Parameters and the
     per-step updates are compared at 2e-3 of their scale.  ``fused``: the
     two-layer PReLU attention's backward as one rs_din_att_prelu_bwd launch
-    and its forward as one rs_din_att_prelu_fwd launch (False: layer by layer)."""
+    and its forward as one rs_din_att_prelu_fwd launch (False: layer by layer).
+    ``rate``: DIN(dnn_dropout=rate) — the Dropout after the DNN (din.py:93)
+    in training mode, the oracle fed the same multiplier."""
     from recommender_system_amd import DIN
+    from recommender_system_amd import models as M
+    from tests.helpers import dropout_masks
     rng = np.random.default_rng(B + T + nb)
     cols, behaviour = din_columns(nb, k, item_vocab=40, cate_vocab=9, user_vocab=17)
     model = DIN(cols, behaviour, att_hidden_units=att_hidden, dnn_hidden_units=dnn_hidden, att_attention=att_act,
-                dnn_activation=dnn_act, seed=3)
+                dnn_activation=dnn_act, dnn_dropout=rate, seed=3)
     model.fused_att_train = fused
     if fused and att_act == "prelu" and len(att_hidden) == 2:  # the shape takes the fused kernel
         from recommender_system_amd import _lib
@@ -268,8 +274,13 @@ def test_din_train_steps_match_oracle(gpu, att_hidden, dnn_hidden, nb, k, B, T, 
         inputs = din_inputs(rng, cols, behaviour, B, T)
         t = rng.integers(0, 2, B).astype(np.float32)
         before = _flat_params(_din_train_params(model))
+        drop_mask = None
+        if rate:
+            dr = M._dropout_rng(model)
+            drop_mask = dropout_masks(dr.seed, dr.offset, B, [dnn_hidden[-1]], rate)[0][0]
         loss = model.train_step(inputs, t, lr=lr, return_loss=True)
-        p, ce = O.din_train_step(inputs, t, p, dense_f, sparse_f, beh, lr, att_act=att_act, dnn_act=dnn_act)
+        p, ce = O.din_train_step(inputs, t, p, dense_f, sparse_f, beh, lr, att_act=att_act, dnn_act=dnn_act,
+                                 drop_mask=drop_mask)
         got = _flat_params(_din_train_params(model))
         ref = _flat_params(p)
         assert_scaled_close(loss, ce, rtol=1e-4, what=f"step {step} loss")

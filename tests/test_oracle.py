@@ -642,6 +642,62 @@ def test_nfm_train_step_gradient_matches_finite_differences():
         check(p["bn"][j], new["bn"][j], idx)
 
 
+def test_nfm_din_train_steps_with_dropout_match_finite_differences():
+    """oracle.nfm_train_step / din_train_step with fixed dropout multipliers
+    (NFM: after each hidden layer, interaction.py:44; DIN: after the DNN,
+    din.py:93) == central differences of the same masked objective."""
+    rng = np.random.default_rng(33)
+    k, vocab, nd = 3, [3, 2, 4], 2
+    D = nd + k
+    p = {"tables": [rng.normal(size=(v_, k)) * 0.7 for v_ in vocab],
+         "bn": (1 + 0.1 * rng.normal(size=D), 0.1 * rng.normal(size=D), np.zeros(D), np.ones(D), 1e-3),
+         "dnn_hidden": [(rng.normal(size=(D, 5)) * 0.5, rng.normal(size=5) * 0.1),
+                        (rng.normal(size=(5, 4)) * 0.5, rng.normal(size=4) * 0.1)],
+         "dnn_out": (rng.normal(size=(4, 2)) * 0.5, rng.normal(size=2) * 0.1),
+         "out": (rng.normal(size=(2, 1)), np.array([0.1]))}
+    ids = np.array([[0, 1, 3], [2, 1, 0], [0, 0, 3], [1, 1, 2], [2, 0, 1]])
+    dense = rng.random((5, nd))
+    t = np.array([1.0, 0.0, 1.0, 0.0, 1.0])
+    masks = [O.dropout_multiplier(5, w, 0.3, 11, off) for w, off in ((5, 0), (4, 28))]
+    assert any((m_ == 0).any() for m_ in masks)
+    new, _ = O.nfm_train_step(dense, ids, t, p, 1.0, masks=masks)
+    eps = 1e-6
+
+    def check(loss_fn, arr, new_arr, idx):
+        keep = arr[idx]
+        arr[idx] = keep + eps
+        lp = loss_fn()
+        arr[idx] = keep - eps
+        lm = loss_fn()
+        arr[idx] = keep
+        fd = (lp - lm) / (2 * eps)
+        assert abs(fd - (arr[idx] - new_arr[idx])) < 1e-6 * max(1.0, abs(fd)), (idx, fd)
+
+    nl = lambda: O.nfm_loss(dense, ids, t, p, masks=masks)
+    for c, idx in [(0, (0, 0)), (2, (3, 0))]:
+        check(nl, p["tables"][c], new["tables"][c], idx)
+    for li in range(2):
+        check(nl, p["dnn_hidden"][li][0], new["dnn_hidden"][li][0], (1, 2))
+        check(nl, p["dnn_hidden"][li][1], new["dnn_hidden"][li][1], (3,))
+    check(nl, p["dnn_out"][0], new["dnn_out"][0], (1, 1))
+    check(nl, p["bn"][0], new["bn"][0], (2,))
+
+    inputs, t, p, dense_f, sparse_f, beh = _din_small(rng)
+    B = len(t)
+    h = np.asarray(p["dnn"][-1][0]).shape[1]
+    mask = O.dropout_multiplier(B, h, 0.4, 5, 0)
+    assert (mask == 0).any()
+    new, _ = O.din_train_step(inputs, t, p, dense_f, sparse_f, beh, 1.0, drop_mask=mask)
+    dl = lambda: O.din_loss(inputs, t, p, dense_f, sparse_f, beh, drop_mask=mask)
+    check(dl, p["out"][0], new["out"][0], (1, 0))
+    for li in range(len(p["dnn"])):
+        check(dl, p["dnn"][li][0], new["dnn"][li][0], (0, 1))
+        check(dl, p["dnn"][li][2], new["dnn"][li][2], (1,))
+    f = beh[0]
+    check(dl, p["seq_tables"][f], new["seq_tables"][f], (2, 1))
+    check(dl, p["bn"][0], new["bn"][0], (2,))
+
+
 def test_ffm_train_step_gradient_matches_finite_differences():
     """oracle.ffm_train_step (compile_fit on FFM: BCE + l2(w_reg) on w + l2(v_reg)
     on v, the field-aware interaction's G = g (T - Fm)) == central differences

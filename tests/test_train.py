@@ -311,6 +311,27 @@ def test_rs_gemm_mfma_matches_torch(gpu, ta, tb, M, N, K):
 
 
 @pytest.mark.gpu
+def test_dropout_refuses_graph_capture(gpu):
+    """A dropout draw inside hipGraph capture raises (its offset is a host
+    counter, so every replay would reuse the captured mask); outside a
+    capture it advances the offset."""
+    from recommender_system_amd import models as M
+    rng = M._Dropout(7)
+    t = torch.ones(64, 32, device="cuda")
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            with pytest.raises(RuntimeError, match="captured graph"):
+                rng.draw(t, 0.2, s.cuda_stream)
+    torch.cuda.current_stream().wait_stream(s)
+    assert rng.offset == 0
+    rng.draw(t, 0.2, torch.cuda.current_stream().cuda_stream)
+    assert rng.offset == 64 * 32
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("rows,cols,ld,rate,offset", [(4096, 256, 256, 0.2, 0), (33, 7, 9, 0.5, 1236),
                                                       (1, 3, 3, 0.2, 4), (300, 24, 24, 0.0, 8)])
 def test_rs_dropout_matches_oracle_generator(gpu, rows, cols, ld, rate, offset):
@@ -539,18 +560,23 @@ def test_outer_product_bwd_matches_oracle(gpu, B, F, k):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,k,hidden", [(64, 8, [32, 16]), (300, 16, [256, 128, 64])])
-def test_nfm_train_steps_match_oracle(gpu, B, k, hidden):
+@pytest.mark.parametrize("B,k,hidden,rate", [(64, 8, [32, 16], 0.0), (300, 16, [256, 128, 64], 0.0),
+                                             (64, 8, [32, 16], 0.3), (300, 16, [256, 128, 64], 0.3)])
+def test_nfm_train_steps_match_oracle(gpu, B, k, hidden, rate):
     """NFM.train_step (compile_fit on NFM: training-mode BatchNormalization,
     the DNNLayer + output Dense backward, the Bi-Interaction backward,
     row-sparse embedding SGD) == oracle.nfm_train_step (pinned by finite
     differences) over 3 steps with repeated rows; the inference forward then
-    runs on the trained weights and the moved BN averages."""
+    runs on the trained weights and the moved BN averages.  rate > 0:
+    NFM(dropout=rate) — DNNLayer's Dropout after each hidden layer in
+    training mode, the oracle fed the same multipliers (rs_dropout's
+    generator, restated by oracle.dropout_multiplier)."""
     import recommender_system_amd as rs
-    from tests.helpers import criteo_columns, dnn_params, tables_of
+    from recommender_system_amd import models as M
+    from tests.helpers import criteo_columns, dnn_params, dropout_masks, tables_of
     rng = np.random.default_rng(B + k + 5)
     vocab = rng.integers(1, 200, 26)
-    m = rs.NFM(criteo_columns(vocab, embed_dim=k), hidden, 1, embed_dim=k, seed=6)
+    m = rs.NFM(criteo_columns(vocab, embed_dim=k), hidden, 1, dropout=rate, embed_dim=k, seed=6)
     with torch.no_grad():
         m.emb_layers.table.mul_(4.0)
 
@@ -569,8 +595,12 @@ def test_nfm_train_steps_match_oracle(gpu, B, k, hidden):
         ids = np.stack([rng.integers(0, v_, B) for v_ in vocab], 1).astype(np.int32)
         ids[:7, 3] = 0  # repeated rows
         t = rng.integers(0, 2, B).astype(np.float32)
+        masks = None
+        if rate:
+            dr = M._dropout_rng(m)
+            masks = dropout_masks(dr.seed, dr.offset, B, hidden, rate)[0]
         loss = m.train_step((dense, ids), t, lr=lr, return_loss=True)
-        p, ce = O.nfm_train_step(dense, ids, t, p, lr)
+        p, ce = O.nfm_train_step(dense, ids, t, p, lr, masks=masks)
         got = params()
         assert_scaled_close(loss, ce, what=f"step {step} loss")
         for c_ in range(26):
