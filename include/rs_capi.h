@@ -527,6 +527,15 @@ int rs_fm_train_step(const void* ids, int id_kind, int64_t id_stride,
  * restates this generator exactly.                                          */
 int rs_dropout(float* x, int64_t ld, int64_t rows, int64_t cols, float rate,
                uint64_t seed, uint64_t offset, rs_stream_t stream);
+/* rs_dropout_at: the same draw at offset *base + offset, with the base read
+ * on the device (a per-generator counter in device memory), so a captured
+ * hipGraph replays fresh masks; rs_dropout_advance adds inc (a multiple of 4)
+ * to *base on the stream — the training steps call it once, after the
+ * backward's redraws, with the step's total.                                */
+int rs_dropout_at(float* x, int64_t ld, int64_t rows, int64_t cols, float rate,
+                  uint64_t seed, const uint64_t* base, uint64_t offset,
+                  rs_stream_t stream);
+int rs_dropout_advance(uint64_t* base, uint64_t inc, rs_stream_t stream);
 
 /* DeepFM training (model/deepFM.py + utils/compile_fit.py; the host layer
  * DeepFM.train_step composes these with rs_embed_gather / rs_dense_fwd /

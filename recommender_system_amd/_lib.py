@@ -91,6 +91,8 @@ SIGNATURES = {
     "rs_gemm": (I, [I, I, L, L, L, F, P, L, P, L, F, P, L, P, L, P, L, P]),
     "rs_col_sum": (I, [P, L, L, L, P, P]),
     "rs_dropout": (I, [P, L, L, L, F, U64, U64, P]),
+    "rs_dropout_at": (I, [P, L, L, L, F, U64, P, U64, P]),
+    "rs_dropout_advance": (I, [P, U64, P]),
     "rs_sgd_update": (I, [P, P, L, F, F, P]),
     "rs_sgd_update_multi": (I, [I, P, P, P, P, F, P]),
     "rs_head_grad": (I, [P, P, P, L, F, F, P, P, P, P]),

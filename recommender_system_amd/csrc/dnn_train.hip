@@ -1102,10 +1102,12 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
   }
 }
 
-// one thread per 4-element counter block of the call's [rows, cols] range
+// one thread per 4-element counter block of the call's [rows, cols] range;
+// base (rs_dropout_at): the offset is *base + offset, read on the device
 __global__ __launch_bounds__(256) void dropout_kernel(float* __restrict__ x, int64_t ld, int64_t rows, int64_t cols,
                                                       float rate, float scale, uint32_t k0, uint32_t k1,
-                                                      uint64_t offset) {
+                                                      uint64_t offset, const uint64_t* __restrict__ base) {
+  if (base) offset += *base;
   const int64_t n = rows * cols, nblk = (n + 3) >> 2;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nblk; q += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t ctr = (offset >> 2) + (uint64_t)q;
@@ -1134,6 +1136,32 @@ extern "C" int rs_dropout(float* x, int64_t ld, int64_t rows, int64_t cols, floa
   const int64_t nblk = (rows * cols + 3) / 4;
   const int grid = (int)std::min<int64_t>((nblk + 255) / 256, 8192);
   dropout_kernel<<<grid, 256, 0, as_stream(stream)>>>(x, ld, rows, cols, rate, 1.0f / (1.0f - rate), (uint32_t)seed,
-                                                      (uint32_t)(seed >> 32), offset);
+                                                      (uint32_t)(seed >> 32), offset, nullptr);
   return launch_status("rs_dropout");
+}
+
+namespace rs {
+__global__ void dropout_advance_kernel(uint64_t* base, uint64_t inc) {
+  if (threadIdx.x == 0) base[0] += inc;
+}
+}  // namespace rs
+
+extern "C" int rs_dropout_at(float* x, int64_t ld, int64_t rows, int64_t cols, float rate, uint64_t seed,
+                             const uint64_t* base, uint64_t offset, rs_stream_t stream) {
+  if (rows == 0 || cols == 0) return RS_OK;
+  RS_REQUIRE(x && base && rows > 0 && cols > 0 && ld >= cols, "rs_dropout_at: bad arguments");
+  RS_REQUIRE(rate >= 0.f && rate < 1.f, "rs_dropout_at: rate must be in [0, 1)");
+  RS_REQUIRE(offset % 4 == 0, "rs_dropout_at: offset must be a multiple of 4");
+  const int64_t nblk = (rows * cols + 3) / 4;
+  const int grid = (int)std::min<int64_t>((nblk + 255) / 256, 8192);
+  dropout_kernel<<<grid, 256, 0, as_stream(stream)>>>(x, ld, rows, cols, rate, 1.0f / (1.0f - rate), (uint32_t)seed,
+                                                      (uint32_t)(seed >> 32), offset, base);
+  return launch_status("rs_dropout_at");
+}
+
+extern "C" int rs_dropout_advance(uint64_t* base, uint64_t inc, rs_stream_t stream) {
+  RS_REQUIRE(base && inc % 4 == 0, "rs_dropout_advance: bad arguments");
+  if (inc == 0) return RS_OK;
+  dropout_advance_kernel<<<1, 64, 0, as_stream(stream)>>>(base, inc);
+  return launch_status("rs_dropout_advance");
 }

@@ -85,6 +85,8 @@ def _dnn_backward(layers, acts, delta, gw, emp, st, outs=None, drop=None):
             rng, rate, offs = drop
             rng.redraw(prev, rate, offs[li - 1], st)
         delta = prev
+    if drop is not None:
+        drop[0].end_step(st)
     return grads, delta
 
 
@@ -124,31 +126,48 @@ def _check_train_tower(name, dnn):
 class _Dropout:
     """DNNLayer's Dropout(rate) in training steps (layer/interaction.py:35,44;
     active under compile_fit's model.fit, utils/compile_fit.py:14): inverted
-    dropout with counter-based masks (rs_dropout: Philox4x32-10, key = seed,
-    one counter per 4 elements).  Every draw takes the next `offset` range, so
-    masks differ across layers and steps and the backward regenerates a
-    draw's mask from its (seed, offset) instead of storing it.  TF's own draws
-    cannot be reproduced; oracle.dropout_multiplier restates this generator.
-    The offsets live on the host, so a captured hipGraph would replay the
-    masks it was captured with: draw() refuses stream capture (train with
-    dropout=False, or eagerly, to capture)."""
+    dropout with counter-based masks (rs_dropout_at: Philox4x32-10, key =
+    seed, one counter per 4 elements).  Every draw of a step takes the next
+    offset range relative to a counter in DEVICE memory, the backward
+    regenerates a draw's mask from the same (seed, counter + rel) instead of
+    storing it, and end_step() advances the counter on the stream by the
+    step's total — so a captured hipGraph of a training step draws fresh
+    masks on every replay.  TF's own draws cannot be reproduced;
+    oracle.dropout_multiplier restates this generator."""
 
-    def __init__(self, seed):
+    def __init__(self, seed, device=None):
         self.seed = int(seed) & (2 ** 64 - 1)
-        self.offset = 0
+        self.base = torch.zeros(1, dtype=torch.int64, device=device if device is not None else "cuda")
+        self.rel = 0
+
+    @property
+    def offset(self):
+        """The absolute offset the next draw takes (reads the device counter)."""
+        return int(self.base.item()) + self.rel
 
     def draw(self, t, rate, st):
-        """Apply a fresh mask to t [rows, cols] in place; returns its offset."""
-        if t.is_cuda and torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("dropout in a captured graph would replay one mask every step; "
-                               "pass dropout=False to capture a training step")
-        off = self.offset
+        """Apply a fresh mask to t [rows, cols] in place; returns its offset
+        relative to the step's counter."""
+        off = self.rel
         self.redraw(t, rate, off, st)
-        self.offset += (t.shape[0] * t.shape[1] + 3) // 4 * 4
+        self.rel += (t.shape[0] * t.shape[1] + 3) // 4 * 4
         return off
 
-    def redraw(self, t, rate, offset, st):
-        call("rs_dropout", ptr(t), t.stride(0), t.shape[0], t.shape[1], float(rate), self.seed, int(offset), st)
+    def take(self, n):
+        """Reserve the next n elements' range (a draw made elsewhere)."""
+        off = self.rel
+        self.rel += (int(n) + 3) // 4 * 4
+        return off
+
+    def redraw(self, t, rate, rel, st):
+        call("rs_dropout_at", ptr(t), t.stride(0), t.shape[0], t.shape[1], float(rate), self.seed, ptr(self.base),
+             int(rel), st)
+
+    def end_step(self, st):
+        """Advance the device counter past this step's draws."""
+        if self.rel:
+            call("rs_dropout_advance", ptr(self.base), int(self.rel), st)
+            self.rel = 0
 
 
 def _dropout_rate(dnn, dropout):
@@ -165,7 +184,7 @@ def _dropout_rate(dnn, dropout):
 def _dropout_rng(model):
     rng = model.__dict__.get("_drop_rng")
     if rng is None:
-        rng = model.__dict__["_drop_rng"] = _Dropout(_subseed(model._gen) * 2654435761 + 97)
+        rng = model.__dict__["_drop_rng"] = _Dropout(_subseed(model._gen) * 2654435761 + 97, model._dev)
     return rng
 
 
@@ -1008,6 +1027,7 @@ class DIN(TowerMixin, KerasModule):
         dh = dense_back(out.kernel, out.bias, acts[-1], g.view(B, 1), B)
         if rate > 0:
             rng.redraw(dh, rate, drop_off, st)
+            rng.end_step(st)
         for li in reversed(range(len(self.dense_layer))):
             L = self.dense_layer[li]
             if L.activation == "dice":

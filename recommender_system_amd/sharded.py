@@ -968,7 +968,7 @@ class ShardedDeepFM:
         seed and the rank (dropout_seed), so ranks draw independent masks."""
         from .models import _Dropout
         if getattr(self, "_drop_rng", None) is None:
-            self._drop_rng = _Dropout(dropout_seed(self._seed, self.rank))
+            self._drop_rng = _Dropout(dropout_seed(self._seed, self.rank), self.device)
         return self._drop_rng
 
     def _draws(self, B, rate):
@@ -978,8 +978,7 @@ class ShardedDeepFM:
             return None
         rng, offs = self._dropout(), []
         for L in self.dnn.hidden_layer:
-            offs.append(rng.offset)
-            rng.offset += (B * L.units + 3) // 4 * 4
+            offs.append(rng.take(B * L.units))
         return rng, rate, offs
 
     def train_step(self, inputs, labels, lr=0.01, return_loss=False, check=True, dropout=None):

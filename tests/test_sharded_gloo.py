@@ -159,7 +159,11 @@ class CpuOps:
         masks = None
         if drop is not None:  # the rank's draws, restated by the oracle's generator
             rng, rate, offs = drop
-            masks = [O.dropout_multiplier(B, W_.shape[1], rate, rng.seed, o) for (W_, _), o in zip(layers, offs)]
+            base = int(rng.base.item())  # offsets are relative to the generator's counter
+            masks = [O.dropout_multiplier(B, W_.shape[1], rate, rng.seed, base + o)
+                     for (W_, _), o in zip(layers, offs)]
+            rng.base += rng.rel  # end of the step (models._Dropout.end_step, on the host here)
+            rng.rel = 0
         acts = [x]
         for i, (W_, b_) in enumerate(layers[:-1]):
             a = np.maximum(acts[-1] @ W_ + b_, 0.0)

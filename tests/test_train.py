@@ -311,24 +311,50 @@ def test_rs_gemm_mfma_matches_torch(gpu, ta, tb, M, N, K):
 
 
 @pytest.mark.gpu
-def test_dropout_refuses_graph_capture(gpu):
-    """A dropout draw inside hipGraph capture raises (its offset is a host
-    counter, so every replay would reuse the captured mask); outside a
-    capture it advances the offset."""
+def test_dropout_counter_under_graph_replay(gpu):
+    """The dropout offset lives in device memory (rs_dropout_at /
+    rs_dropout_advance): a captured draw + advance replays a FRESH mask on
+    every replay, each equal to oracle.dropout_multiplier at the counter's
+    value, and a redraw at the same relative offset inside the step repeats
+    the step's mask (the backward's regeneration)."""
     from recommender_system_amd import models as M
     rng = M._Dropout(7)
-    t = torch.ones(64, 32, device="cuda")
+    rows, cols, rate = 64, 30, 0.25
+    x = torch.empty(rows, cols, device="cuda")
+    y = torch.empty(rows, cols, device="cuda")
+    st = lambda: torch.cuda.current_stream().cuda_stream
+
+    def step():
+        x.fill_(1.0)
+        y.fill_(1.0)
+        off = rng.draw(x, rate, st())
+        rng.redraw(y, rate, off, st())
+        rng.end_step(st())
+
+    step()  # eager, offset 0
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(x.cpu().numpy(), O.dropout_multiplier(rows, cols, rate, rng.seed, 0, np.float32))
+    n = (rows * cols + 3) // 4 * 4
+    assert rng.offset == n
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         with torch.cuda.graph(g, stream=s):
-            with pytest.raises(RuntimeError, match="captured graph"):
-                rng.draw(t, 0.2, s.cuda_stream)
+            step()
     torch.cuda.current_stream().wait_stream(s)
-    assert rng.offset == 0
-    rng.draw(t, 0.2, torch.cuda.current_stream().cuda_stream)
-    assert rng.offset == 64 * 32
+    torch.cuda.synchronize()
+    assert rng.offset == n  # capture ran nothing
+    seen = []
+    for r in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        ref = O.dropout_multiplier(rows, cols, rate, rng.seed, n * (r + 1), np.float32)
+        np.testing.assert_array_equal(x.cpu().numpy(), ref)
+        assert torch.equal(x, y)
+        seen.append(x.clone())
+    assert not torch.equal(seen[0], seen[1]) and not torch.equal(seen[1], seen[2])
+    assert rng.offset == 4 * n
 
 
 @pytest.mark.gpu
