@@ -67,10 +67,8 @@ enum rs_flag {
 enum rs_option {
   RS_OPT_EMBED_FM_KERNEL = 0, /* rs_embed_fm_fwd kernel (id inputs, no x_out): 0 = MFMA K-split,
                                  1 = VALU/DPP persistent 8-sample tiles, 2 / 3 = MFMA persistent
-                                 16-sample tiles (2 / 1 resident per CU); 4 = rs_embed_fm_fwd_hm's
-                                 K-split kernel with the last-wave finish (no combine barrier;
-                                 bit-identical); shapes a kernel does not cover run the K-split
-                                 one.  See DESIGN.md 4.1                                          */
+                                 16-sample tiles (2 / 1 resident per CU); shapes a kernel does
+                                 not cover run the K-split one.  See DESIGN.md 4.1                */
   RS_OPT_MLP_UNROLL = 1,      /* fused MLP towers (rs_mlp_fwd, rs_deepfm_fwd, rs_dcn_fwd): 1 (the
                                  default) = the k-group loop of the common layer widths fully
                                  unrolled (no loop-head wait on the weight ring), 0 = the looped
@@ -95,6 +93,10 @@ int rs_get_option(int option);
  * hipGraph to record the box's dependent-launch slot time beside its
  * numbers. */
 int rs_diag_empty(int grid, int block, rs_stream_t stream);
+/* rs_diag_wave_slots: every wave's HW_ID register (bits 3:0 wave slot, 5:4
+ * SIMD, 11:8 CU, 12 SH, 15:13 SE) into out[grid * block / 64], lds_bytes of
+ * dynamic LDS per workgroup — how a workgroup's waves spread over the SIMDs. */
+int rs_diag_wave_slots(int grid, int block, int lds_bytes, uint32_t* out, rs_stream_t stream);
 
 /* --------------------------------------------------------- embedding (a3)
  * Replaces EmbedLayer.call (layer/core.py:273-280) + the dense/sparse concat of

@@ -83,39 +83,75 @@ struct CrossArgs {
   int64_t batch;
 };
 
-// Phases (2)-(4) on a staged 16 x d tile of x0 (rows >= `rows` zero).
+// The B fragments of 8 of a wave's k-steps (t0, t0 + NW, ..): L2-resident
+// launch constants, so the fused kernels request the first 8 before their
+// gather (they arrive inside the id / row trips).
 template <int NT, int NW>
-__device__ __forceinline__ void cross_tile(const CrossArgs& a, float* tile, float* cs, float* alpha, int64_t b0,
-                                           int rows) {
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int s = lane & 15, kk = lane >> 4;
-  const int n = rows * a.d;
-  // (2) G = X0 @ W on MFMA, K split across the NW waves
-  floatx4 acc[NT];
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // the wave's k-steps are t = w + NW*i; their B fragments (L2-resident) are
-  // requested 8 steps at a time before any MFMA waits on them
-  for (int t0 = w; t0 < a.DB; t0 += 8 * NW) {
-    float bv[8][NT], xv[8];
+struct CrossB {
+  float v[8][NT];
+  __device__ __forceinline__ void load(const CrossArgs& a, int t0) {
+    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int t = min(t0 + u * NW, a.DB - 1);
       const float* rec = a.img + (int64_t)t * NT * 64;
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) bv[u][nt] = rec[nt * 64 + lane];
+      for (int nt = 0; nt < NT; ++nt) v[u][nt] = rec[nt * 64 + lane];
     }
+  }
+};
+
+// G = X0 @ W on MFMA, K split across the NW waves: the wave's k-steps are
+// t = w + NW*i, 8 at a time (B fragments requested before any MFMA waits on
+// them; the first 8 from `pre` when the caller prefetched them).  tile rows
+// are `ld` floats apart, columns >= a.d read as 0.
+template <int NT, int NW>
+__device__ __forceinline__ void cross_contract(const CrossArgs& a, const float* tile, int ld,
+                                               const CrossB<NT, NW>* pre, floatx4 (&acc)[NT]) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int s = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  auto step = [&](int t0, const CrossB<NT, NW>& B) {
+    float xv[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int e = 4 * (t0 + u * NW) + kk;
-      xv[u] = (t0 + u * NW < a.DB && e < a.d) ? tile[s * a.d + e] : 0.f;
+      xv[u] = (t0 + u * NW < a.DB && e < a.d) ? tile[s * ld + e] : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u)
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(xv[u], bv[u][nt], acc[nt]);
+      for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(xv[u], B.v[u][nt], acc[nt]);
+  };
+  if (w < a.DB) {
+    if (pre) {
+      step(w, *pre);
+    } else {
+      CrossB<NT, NW> B;
+      B.load(a, w);
+      step(w, B);
+    }
   }
+  for (int t0 = w + 8 * NW; t0 < a.DB; t0 += 8 * NW) {
+    CrossB<NT, NW> B;
+    B.load(a, t0);
+    step(t0, B);
+  }
+}
+
+// Phases (2)-(4) on a staged 16 x d tile of x0 (rows >= `rows` zero).
+template <int NT, int NW>
+__device__ __forceinline__ void cross_tile(const CrossArgs& a, float* tile, float* cs, float* alpha, int64_t b0,
+                                           int rows, const CrossB<NT, NW>* pre = nullptr) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int s = lane & 15, kk = lane >> 4;
+  const int n = rows * a.d;
+  // (2) G = X0 @ W on MFMA
+  floatx4 acc[NT];
+  cross_contract<NT, NW>(a, tile, a.d, pre, acc);
   constexpr int CW = NT * 16 + 1;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
@@ -235,6 +271,8 @@ __device__ __forceinline__ void embed_cross_body(const CrossArgs& a, const Embed
   const int rows = (int)((a.batch - b0) < 16 ? (a.batch - b0) : 16);
   const int F = e.F;
   if constexpr (KA) {
+    CrossB<NT, NW> pre;  // the contraction's first B fragments ride the gather's trips
+    pre.load(a, w);
     {  // dense columns (wave w: sample w), requested beside the ids
       const int64_t bb = b0 + (w < rows ? w : rows - 1);
       for (int j = lane; j < e.nd; j += 64) tile[w * a.d + j] = w < rows ? e.dense[bb * e.dense_stride + j] : 0.f;
@@ -249,7 +287,7 @@ __device__ __forceinline__ void embed_cross_body(const CrossArgs& a, const Embed
                                                });
     if (__any(bad) && lane == 0) flag_error(e.err);
     __syncthreads();
-    cross_tile<NT, NW>(a, tile, cs, alpha, b0, rows);
+    cross_tile<NT, NW>(a, tile, cs, alpha, b0, rows, &pre);
     return;
   } else {
   __shared__ typename I::raw_t lid[16][EC_FMAX];
@@ -348,6 +386,8 @@ __device__ __forceinline__ void dcn_fused_body(const CrossArgs& a, const EmbedCr
   mlp_first_fill<NW>(t, ring);
   float* par = tsm + 32 * RS + NW * 256;
   for (int i = tid; i < t.ptot; i += NW * 64) par[i] = t.prep[t.wtot + i];
+  CrossB<NT, NW> pre;  // KA: the contraction's first B fragments ride the gather's trips
+  if constexpr (KA) pre.load(a, w);
   if constexpr (KA) {
     {  // dense columns + zero padding of the tile row (wave w: sample w)
       const int64_t bb = b0 + (w < rows ? w : rows - 1);
@@ -421,27 +461,7 @@ __device__ __forceinline__ void dcn_fused_body(const CrossArgs& a, const EmbedCr
 
   // CrossNet contraction G = X0 @ [w_0 .. w_{L-1}, w_o[:d]] (a.L = L + 1 columns)
   floatx4 acc[NT];
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int t0 = w; t0 < a.DB; t0 += 8 * NW) {
-    float bv[8][NT], xv[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int tt = min(t0 + u * NW, a.DB - 1);
-      const float* rec = a.img + (int64_t)tt * NT * 64;
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) bv[u][nt] = rec[nt * 64 + lane];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int ee = 4 * (t0 + u * NW) + kk;
-      xv[u] = (t0 + u * NW < a.DB && ee < d) ? tsm[s * RS + ee] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(xv[u], bv[u][nt], acc[nt]);
-  }
+  cross_contract<NT, NW>(a, tsm, RS, KA ? &pre : nullptr, acc);
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll

@@ -129,16 +129,9 @@ __global__ void fm_prepare_generic(const float* __restrict__ w1, const float* __
 // row stride tw->rs) instead of x_out, and the DNN tower of mlp_tower.hpp runs
 // on it, closed by sigmoid(c0*dnn + c1*fm) (model/deepFM.py:24-30).
 // A workgroup owns one 16-sample MFMA row tile.
-// LF (FM logit kernels): the cross-wave combine without a workgroup barrier —
-// every wave writes its partial tile (one b128 per lane) and its per-row q
-// partials to its own LDS slot and counts itself in an LDS counter; the LAST
-// wave to arrive sums the slots in wave order and finishes the tile's logits
-// (the others exit).  The sums run in the same order as the barrier form, so
-// the logits are bit-identical.
-template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, bool PF = false, bool KA = false, bool LF = false>
+template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, bool PF = false, bool KA = false>
 __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArgs* tw, const int tile,
                                               const FieldMeta* km = nullptr) {
-  static_assert(!LF || (!TW && KIND != 4), "last-wave finish: FM logit kernels");
   // MC > 0: field slots per wave and pass (owner kernels with few fields)
   constexpr int MAXC0 = MC > 0 ? MC : 128 / (NW * KV);
   constexpr int MAXC = MAXC0 < 1 ? 1 : (MAXC0 > 8 ? 8 : MAXC0);
@@ -146,7 +139,6 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   constexpr bool OWNER = KIND == 4;
   __shared__ float cs[NW][16][NT * 16 + 1];
   __shared__ float qs[NW][16];
-  __shared__ int lf_arrived;  // LF: waves done with their partial tiles
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -226,10 +218,12 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   constexpr int FMAX = 128;
   __shared__ typename I::raw_t lid[16][FMAX];
   __shared__ int64_t lmeta[2][FMAX];
+  // (owner side, KIND 4: the local rows need no field metadata, so every
+  // wave loads its own ids — no id tile, no barrier before the rows)
 #ifdef RS_DIAG_STAMPS
-  const bool coop = !KA && (KIND != 3) && a.F <= FMAX && !(a.ablate & 16);  // bit 16: per-wave id loads
+  const bool coop = !KA && !OWNER && (KIND != 3) && a.F <= FMAX && !(a.ablate & 16);  // bit 16: per-wave id loads
 #else
-  const bool coop = !KA && (KIND != 3) && a.F <= FMAX;
+  const bool coop = !KA && !OWNER && (KIND != 3) && a.F <= FMAX;
 #endif
   if (coop) {
     const int64_t b0 = (int64_t)tile * 16;
@@ -417,14 +411,6 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   if (a.F == 0 || coop) load_dense();
   if (coop) __syncthreads();
   RS_STAMP(9);
-  // LF: the finish counter starts at 0, behind one workgroup barrier that
-  // every wave passes (in the PRE schedule with its ids already in flight)
-  auto lf_init = [&]() {
-    if constexpr (LF) {
-      if (threadIdx.x == 0) lf_arrived = 0;
-      __syncthreads();
-    }
-  };
   if (PRE) {
     const bool one = has_pass(0), two = one && has_pass(PS);
     if (one) {
@@ -434,7 +420,6 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       fetch_ids(0, P0);
       if (two) fetch_ids(PS, P1);
     }
-    lf_init();
     if (one) {
       // (the second pass's rows stay behind the first pass's MFMAs: issuing
       // them with the first pass's was slower, 6.19 vs 5.82 us at 4096 —
@@ -455,7 +440,6 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       }
     }
   } else {
-    lf_init();
     for (int cg = 0; has_pass(cg); cg += PS) {
       issue_b(cg, P0);
       issue_rows(cg, P0, false);
@@ -503,54 +487,6 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     return;
   }
 #endif
-  if constexpr (LF) {
-    // ---- last-wave finish: partial tile + per-row q partials to this wave's
-    // slot, count in; the last wave sums the slots in wave order (as the
-    // barrier form below: bit-identical) and writes the tile's logits.
-    __shared__ floatx4 lf_acc[NT][NW][64];
-    __shared__ floatx4 lf_q[NW][4];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) lf_acc[nt][w][lane] = acc[nt];
-    qn += __shfl_xor(qn, 16);
-    qn += __shfl_xor(qn, 32);
-    if (lane < 16) reinterpret_cast<float*>(&lf_q[w][0])[lane] = qn;
-    int old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(&lf_arrived, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-    old = __builtin_amdgcn_readfirstlane(old);
-    if (old != NW - 1) return;
-    RS_STAMP(7);
-    floatx4 v[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      v[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ww = 0; ww < NW; ++ww) {
-        const floatx4 pv = lf_acc[nt][ww][lane];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[nt][i] += pv[i];
-      }
-    }
-    const floatx4 q4 = lf_q[s < NW ? s : 0][kk];  // wave s's q partials of rows 4 kk .. 4 kk + 3
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float t = 0.f, lin = 0.f;
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const int col = nt * 16 + s;
-        float tt = col < a.kfm ? v[nt][i] * v[nt][i] : 0.f;  // s_f^2
-        if (col < NW) tt -= q4[i];                           // - sum_i x_i^2 |v_i|^2 (wave partials)
-        float ll = col == a.kfm ? v[nt][i] : 0.f;            // x@w1
-        tt = row16_sum(tt);
-        ll = row16_sum(ll);
-        t = nt == 0 ? tt : t + tt;
-        lin = nt == 0 ? ll : lin + ll;
-      }
-      const int64_t bb = (int64_t)tile * 16 + 4 * kk + i;
-      if (s == 0 && bb < a.batch && a.logit) a.logit[bb] = (lin + w0v) + 0.5f * t;
-    }
-    RS_STAMP(4);
-    return;
-  }
   // ---- combine the NW partial tiles: thread (sample, column) sums the waves'
   // partials; the per-sample reductions over columns are DPP row sums.
 #pragma unroll
@@ -615,9 +551,9 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
 // the field metadata by value (rs_embed_fm_fwd_hm): each wave loads its own
 // fields' ids and reads (offset, vocab) through scalar kernarg loads — no LDS
 // id tile, no barrier, no per-wave metadata loads from one hot L2 line
-template <int KV, int NT, int NW, int KIND, bool PF, bool LF = false>
+template <int KV, int NT, int NW, int KIND, bool PF>
 __global__ __launch_bounds__(NW * 64) void embed_fm_mfma_ka(EmbedFmArgs a, FieldMeta m) {
-  embed_fm_body<KV, NT, NW, KIND, false, 1, PF, true, LF>(a, nullptr, blockIdx.x, &m);
+  embed_fm_body<KV, NT, NW, KIND, false, 1, PF, true>(a, nullptr, blockIdx.x, &m);
 }
 
 // ---- sharded FM, partial protocol: combine (requester side) as a block part
@@ -697,7 +633,9 @@ template <int KV, int NT, int NW, int MC>
 __global__ __launch_bounds__(NW * 64) void shard_fm_pipe(EmbedFmArgs a, PipeArgs p) {
   const int bid = blockIdx.x;
   if (bid < p.owner_blocks) {
-    embed_fm_body<KV, NT, NW, 4, false, MC>(a, nullptr, bid);
+    // the headline kernel's schedule: B fragments of the first two passes and
+    // both passes' ids issued before the first rows (PF)
+    embed_fm_body<KV, NT, NW, 4, false, MC, true>(a, nullptr, bid);
   } else if (bid < p.owner_blocks + p.route_blocks) {
     field_route_part<NW * 64>(p.r, bid - p.owner_blocks, p.route_blocks);
   } else {
@@ -1133,10 +1071,6 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st, const FieldMe
   // with both passes' ids requested together; profiles/r3_ab_kernarg_*)
   // 16 waves (13: 6.20 us, 9: 6.78 vs 5.76 at 4096; profiles/r3_ab_kernarg_waves_4096.json)
   if (hm && a.F <= 32 && KIND != 3 && grid <= 512) {
-    if (!a.x_out && opt(RS_OPT_EMBED_FM_KERNEL) == 4) {  // last-wave finish (embed_fm_body LF)
-      embed_fm_mfma_ka<KV, NT, 16, KIND, true, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
-      return;
-    }
     embed_fm_mfma_ka<KV, NT, 16, KIND, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
     return;
   }

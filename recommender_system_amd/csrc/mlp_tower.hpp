@@ -141,9 +141,9 @@ __device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[MLP_R], const float* _
 // code, so the compiler waits on each ring slot's own load (vmcnt(D-1)-style)
 // instead of draining the ring at a loop head (the looped form's back-edge
 // gets a full vmcnt(0) every D groups).
-#ifndef MLP_SMALL_D
-#define MLP_SMALL_D 2  // groups ahead in the 16 / 8 / 4-group layers (a divisor of 4, <= MLP_RING)
-#endif
+// groups ahead in the 16 / 8 / 4-group layers: 2 (A/B of rs_mlp_fwd, B 4096:
+// 20.66 us vs 20.75 at 1 and 20.89 at 4; profiles/r4_ab_mlp_small_d.json)
+constexpr int MLP_SMALL_D = 2;
 template <int N, int D>
 __device__ __forceinline__ void mlp_mac_u(floatx4 (&ring)[MLP_R], const float* __restrict__ ap,
                                           const floatx4* __restrict__ bp, int g0, floatx4& acc) {

@@ -1,4 +1,6 @@
-"""Same-box timing of tower build variants (scripts/build_ab_tower.sh): the
+"""Same-box timing of tower build variants (scripts/ab/librs_tower_{A..D}.so,
+each `hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -I include
+-I recommender_system_amd/csrc <flags> csrc/mlp.hip csrc/capi.cpp`): the
 DeepFM DNN tower 429-256-128-64-1 with the sigmoid head (rs_mlp_fwd) at
 B 4096, graph-replayed (64 launches per replay), variants alternated, outputs
 compared bitwise with A.  Prints one JSON line."""

@@ -1,0 +1,35 @@
+"""Which SIMD each wave of a 1024-thread workgroup runs on (rs_diag_wave_slots:
+HW_ID per wave), at the tower's occupancy (one workgroup per CU through its
+LDS) and at a small one.  Prints one JSON line: per LDS size, the SIMD of
+waves 0..15 in the first workgroups and how often each wave -> SIMD pattern
+occurs."""
+import collections
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    from recommender_system_amd import _lib
+    grid = 256
+    res = {}
+    for lds in (4096, 80 * 1024):
+        out = torch.zeros(grid * 16, dtype=torch.int32, device="cuda")
+        _lib.call("rs_diag_wave_slots", grid, 1024, lds, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        hw = out.cpu().numpy().astype("uint32").reshape(grid, 16)
+        simd = (hw >> 4) & 3
+        slot = hw & 15
+        pats = collections.Counter(tuple(int(x) for x in r) for r in simd)
+        res[f"lds_{lds}"] = {"simd_of_wave_wg0": [int(x) for x in simd[0]], "slot_of_wave_wg0": [int(x) for x in slot[0]],
+                             "patterns": {",".join(map(str, k)): v for k, v in pats.most_common(4)},
+                             "waves_per_simd_wg0": [int((simd[0] == s).sum()) for s in range(4)]}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -182,13 +182,10 @@ def test_embed_fm_kernel_variants(gpu, embed_fm_variant, k, kfm, F, nd, B, idt):
     (16, 10, 26, 13, 4093, "i64", True),    # ragged last tile, x emitted
     (16, 10, 17, 0, 50, "f32", False),      # no dense block, one pass + a partial pass
 ])
-@pytest.mark.parametrize("variant", [0, 4])
-def test_embed_fm_host_meta(gpu, k, kfm, F, nd, B, idt, with_x, variant):
+def test_embed_fm_host_meta(gpu, k, kfm, F, nd, B, idt, with_x):
     """rs_embed_fm_fwd_hm (field metadata also as kernel arguments, per-wave
     id loads, no id tile) == rs_embed_fm_fwd bit for bit (logit and x) and ==
-    the oracle; an out-of-range id sets the flag.  Variant 4
-    (RS_OPT_EMBED_FM_KERNEL: the last-wave finish, no combine barrier) is
-    bit-identical too."""
+    the oracle; an out-of-range id sets the flag."""
     import ctypes as C
     from recommender_system_amd import _lib
     rng = np.random.default_rng(B * 7 + F)
@@ -228,27 +225,23 @@ def test_embed_fm_host_meta(gpu, k, kfm, F, nd, B, idt, with_x, variant):
 
     ref_logit, ref_x = run(ids, False)
     assert err.item() == 0
-    prev = _lib.set_option(_lib.OPT_EMBED_FM_KERNEL, variant)
-    try:
-        got_logit, got_x = run(ids, True)
-        assert err.item() == 0
-        assert torch.equal(got_logit, ref_logit)
-        if with_x:
-            assert torch.equal(got_x, ref_x)
-        tables = [table[o:o + vv] for o, vv in zip(offs, vocabs)]
-        x64 = np.concatenate([dense, O.embed_layer(ids, tables, np.float64)], 1)
-        assert_scaled_close(got_logit, O.fm_layer(x64, w0, w1, v)[:, 0], what=f"embed_fm host meta v{variant}")
-        bad = ids.copy()
-        bad[B - 1, F - 1] = vocabs[F - 1]
-        run(bad, True)
-        assert err.item() != 0
-        err.zero_()
-        bad = ids.copy()
-        bad[B // 2, 0] = -1
-        run(bad, True)
-        assert err.item() != 0
-    finally:
-        _lib.set_option(_lib.OPT_EMBED_FM_KERNEL, prev)
+    got_logit, got_x = run(ids, True)
+    assert err.item() == 0
+    assert torch.equal(got_logit, ref_logit)
+    if with_x:
+        assert torch.equal(got_x, ref_x)
+    tables = [table[o:o + vv] for o, vv in zip(offs, vocabs)]
+    x64 = np.concatenate([dense, O.embed_layer(ids, tables, np.float64)], 1)
+    assert_scaled_close(got_logit, O.fm_layer(x64, w0, w1, v)[:, 0], what="embed_fm host meta")
+    bad = ids.copy()
+    bad[B - 1, F - 1] = vocabs[F - 1]
+    run(bad, True)
+    assert err.item() != 0
+    err.zero_()
+    bad = ids.copy()
+    bad[B // 2, 0] = -1
+    run(bad, True)
+    assert err.item() != 0
 
 
 def test_embed_fm_packed_float_X_and_oor(gpu):
