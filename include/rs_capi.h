@@ -77,7 +77,12 @@ enum rs_option {
                                  first layer): 0 (the default) = split wave roles (loaders +
                                  layer-0 compute waves, deepfm_ws), 1 = one role per wave (gather
                                  + FM, then the tower).  See DESIGN.md 4.5                       */
-  RS_OPT_COUNT = 3
+  RS_OPT_WAVE_ORDER = 3,      /* fused towers: which waves take a layer's work items when there are
+                                 fewer items than waves (and the split-role DeepFM's roles): 0 =
+                                 waves 0, 1, 2 ..; 1 (the default) = interleaved over the CU's
+                                 SIMDs, for the hardware's placement of wave w of a 16-wave
+                                 workgroup on SIMD w / 4 (rs_diag_wave_slots).  See DESIGN.md 4.5 */
+  RS_OPT_COUNT = 4
 };
 
 /* ------------------------------------------------------------------ meta */

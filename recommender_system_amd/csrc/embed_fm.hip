@@ -691,6 +691,9 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
   __shared__ int cnt[4];  // dense k-steps written | loaders past burst 0 | past burst 1 | FM partials in
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // roles by the wave's SIMD-interleaved rank (RS_OPT_WAVE_ORDER): ranks
+  // 0..7 load, 8..15 compute — two of each on every SIMD
+  const int wr = mlp_wave_rank<NW>(w, t.worder);
   const int s = lane & 15, kk = lane >> 4;
   const int64_t bt = (int64_t)blockIdx.x * 16 + s;
   const bool valid = bt < a.batch;
@@ -703,9 +706,9 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     MLP_STAMP(0);
   }
   if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
-  if (w < WS_NL) {
+  if (wr < WS_NL) {
     // ================================ loader
-    const int l = w;
+    const int l = wr;
     const float w0v = a.w0[0];
     const int dw = l - (WS_NL - a.DB);  // dense k-steps on the last DB loaders (fewest fields)
     const bool has_dense = dw >= 0;
@@ -728,7 +731,7 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
         if (s <= a.kfm) bw[p] = *reinterpret_cast<const floatx4*>(a.prep + a.field_base + (int64_t)c * a.field_rec + lane * 4);
       }
     }
-    for (int i = threadIdx.x; i < t.ptot; i += WS_NL * 64) par[i] = t.prep[t.wtot + i];
+    for (int i = l * 64 + lane; i < t.ptot; i += WS_NL * 64) par[i] = t.prep[t.wtot + i];
     __syncthreads();  // the counters start at 0 (the compute waves pass the same barrier)
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
     float qn = 0.f;
@@ -811,7 +814,7 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     }
   } else {
     // ================================ layer 0 compute
-    const int c8 = w - WS_NL;
+    const int c8 = wr - WS_NL;
     const floatx4* W0 = reinterpret_cast<const floatx4*>(t.prep + t.off[0]) + lane + (int64_t)c8 * G * 64;
     const floatx4* W1 = W0 + (int64_t)WS_NL * G * 64;  // output tile c8 + 8
     // k-group order: the dense group (G - 1) first, then fields 0 .. F-1
@@ -860,8 +863,8 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
   {  // layer 1's first weights (this wave's first item of it, if any)
     const int T1 = t.Np[1] >> 4, G1 = t.Kp[1] >> 4;
     const int S1 = mlp_slices(T1, G1, NW);
-    if (w < T1 * S1) {
-      const MlpItem it = mlp_item(w, T1, G1, S1);
+    if (wr < T1 * S1) {
+      const MlpItem it = mlp_item(wr, T1, G1, S1);
       mlp_ring_fill(ring, reinterpret_cast<const floatx4*>(t.prep + t.off[1]) + lane + (int64_t)it.t * G1 * 64,
                     it.g0, it.g1);
     }

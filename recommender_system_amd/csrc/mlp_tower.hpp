@@ -68,6 +68,7 @@ struct MlpArgs {
   int64_t M;
   unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_mlp_set_dbg)
   int unroll;               // RS_OPT_MLP_UNROLL at launch
+  int worder;               // RS_OPT_WAVE_ORDER at launch
 };
 #define MLP_STAMP(i)                                                                              \
   do {                                                                                            \
@@ -100,6 +101,20 @@ __device__ __forceinline__ int mlp_slices(int T, int G, int NW) {
 __device__ __forceinline__ MlpItem mlp_item(int item, int T, int G, int S) {
   const int t = item % T, part = item / T;
   return MlpItem{t, part * G / S, (part + 1) * G / S};
+}
+
+// The wave's rank in the order that takes a layer's items (items r, r + NW,
+// ..): worder 1 interleaves the CU's SIMDs — the hardware puts wave w of an
+// NW-wave workgroup on SIMD w / (NW / 4) (rs_diag_wave_slots), so item order
+// = wave order would stack a layer with fewer items than waves (8 / 4 / 1
+// output tiles after the first) on one or two SIMDs.  A bijection of 0..NW-1.
+template <int NW>
+__device__ __forceinline__ int mlp_wave_rank(int w, int worder) {
+  if constexpr (NW % 4 == 0 && NW >= 8) {
+    constexpr int PER = NW / 4;
+    if (worder) return (w % PER) * 4 + w / PER;
+  }
+  return w;
 }
 
 // B fragments (1 KB per k-group per output tile) stream through a ring of 4
@@ -199,6 +214,7 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
   float* par = red + NW * 256;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = mlp_wave_rank<NW>(w, a.worder);
 
   float* in = (l0 & 1) ? smem + 16 * RS : smem;
   float* out = (l0 & 1) ? smem : smem + 16 * RS;
@@ -234,10 +250,10 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
     };
 
     const float* ap = in + (lane & 15) * RS + 4 * (lane >> 4);
-    for (int item = w; item < T * S; item += NW) {
+    for (int item = wr; item < T * S; item += NW) {
       const MlpItem it = mlp_item(item, T, G, S);
       const floatx4* bp = W + (int64_t)it.t * G * 64;
-      if (item != w) mlp_ring_fill(ring, bp, it.g0, it.g1);
+      if (item != wr) mlp_ring_fill(ring, bp, it.g0, it.g1);
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
       mlp_mac(ring, ap, bp, it.g0, it.g1, acc, a.unroll);
       if (S == 1) {
@@ -253,8 +269,8 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
     if (l + 1 < a.L) {
       const int T2 = a.Np[l + 1] >> 4, G2 = a.Kp[l + 1] >> 4;
       const int S2 = mlp_slices(T2, G2, NW);
-      if (w < T2 * S2) {
-        const MlpItem it = mlp_item(w, T2, G2, S2);
+      if (wr < T2 * S2) {
+        const MlpItem it = mlp_item(wr, T2, G2, S2);
         mlp_ring_fill(ring, reinterpret_cast<const floatx4*>(a.prep + a.off[l + 1]) + lane + (int64_t)it.t * G2 * 64,
                       it.g0, it.g1);
       }
@@ -282,8 +298,9 @@ __device__ __forceinline__ void mlp_first_fill(const MlpArgs& a, floatx4 (&ring)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int T = a.Np[0] >> 4, G = a.Kp[0] >> 4;
   const int S = mlp_slices(T, G, NW);
-  if (w < T * S) {
-    const MlpItem it = mlp_item(w, T, G, S);
+  const int wr = mlp_wave_rank<NW>(w, a.worder);
+  if (wr < T * S) {
+    const MlpItem it = mlp_item(wr, T, G, S);
     mlp_ring_fill(ring, reinterpret_cast<const floatx4*>(a.prep + a.off[0]) + lane + (int64_t)it.t * G * 64, it.g0,
                   it.g1);
   }
@@ -310,6 +327,7 @@ inline bool mlp_fill_args(const MlpGeom& g, const int* acts, const float* prepar
   a.K0 = g.K[0];
   a.rs = g.rs;
   a.unroll = opt(RS_OPT_MLP_UNROLL);
+  a.worder = opt(RS_OPT_WAVE_ORDER);
   return true;
 }
 

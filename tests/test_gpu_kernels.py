@@ -958,3 +958,48 @@ def test_deepfm_kernel_forms(gpu, variant, B, id_dtype, hidden, nd):
             m.forward_fused((torch.as_tensor(dense, device=gpu), bad))
     finally:
         _lib.set_option(_lib.OPT_DEEPFM_KERNEL, prev)
+
+
+# --------------------------- tower item order (RS_OPT_WAVE_ORDER)
+@pytest.mark.parametrize("B,hidden", [(4096, [256, 128, 64]), (333, [248, 160, 8]), (64, [256, 128])])
+def test_tower_wave_order_bit_identical(gpu, B, hidden):
+    """Which wave takes which work item of a layer (RS_OPT_WAVE_ORDER 0:
+    waves in order, 1: interleaved over the SIMDs) changes no arithmetic: the
+    fused DeepFM (both kernel forms), the fused DCN and rs_mlp_fwd give
+    bit-identical outputs under both orders (the oracle checks of each
+    kernel run under the default order elsewhere)."""
+    from recommender_system_amd import DCN, DeepFM, _lib
+    from tests.helpers import criteo_columns
+    rng = np.random.default_rng(B + len(hidden))
+    vocabs = rng.integers(2, 3000, size=26)
+    cols = criteo_columns(vocabs, embed_dim=16)
+    dfm = DeepFM(cols, 10, 1e-4, 1e-4, hidden, 1, "relu", embed_dim=16, seed=4)
+    dcn = DCN(cols, hidden, 1, "relu", 3, embed_dim=16, seed=4)
+    with torch.no_grad():
+        for l in dfm.dnn._layers() + dcn.dense_layer._layers():
+            l.bias.uniform_(-0.1, 0.1)
+        dfm.embed_layer.table.mul_(10.0)
+        dcn.embed_layer.table.mul_(10.0)
+    ids = torch.as_tensor(random_ids(rng, B, vocabs, np.int64), device=gpu).to(torch.int32)
+    dense = torch.as_tensor(rng.random((B, 13)).astype(np.float32), device=gpu)
+    x = torch.as_tensor(rng.uniform(-1, 1, (B, 429)).astype(np.float32), device=gpu)
+    outs = {}
+    prev_o = _lib.set_option(_lib.OPT_WAVE_ORDER, 0)
+    prev_k = _lib.lib().rs_get_option(_lib.OPT_DEEPFM_KERNEL)
+    try:
+        for order in (0, 1):
+            _lib.set_option(_lib.OPT_WAVE_ORDER, order)
+            for form in (0, 1):
+                _lib.set_option(_lib.OPT_DEEPFM_KERNEL, form)
+                outs[("deepfm", form, order)] = dfm.forward_fused((dense, ids)).clone()
+            outs[("dcn", order)] = dcn.forward_fused((dense, ids)).clone()
+            outs[("mlp", order)] = dfm.dnn(x).clone()
+        torch.cuda.synchronize()
+    finally:
+        _lib.set_option(_lib.OPT_WAVE_ORDER, prev_o)
+        _lib.set_option(_lib.OPT_DEEPFM_KERNEL, prev_k)
+    for form in (0, 1):
+        assert torch.equal(outs[("deepfm", form, 0)], outs[("deepfm", form, 1)]), f"deepfm form {form}"
+    assert torch.equal(outs[("dcn", 0)], outs[("dcn", 1)])
+    assert torch.equal(outs[("mlp", 0)], outs[("mlp", 1)])
+    assert not torch.equal(outs[("mlp", 1)], torch.zeros_like(outs[("mlp", 1)]))
