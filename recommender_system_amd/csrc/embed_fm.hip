@@ -142,6 +142,10 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // the wave's field slot: SIMD-interleaved (RS_OPT_WAVE_ORDER) so the
+  // two-field and the dense waves spread over the CU's SIMDs (the fused
+  // tower keeps wave order: its combine order is part of its results)
+  const int wf = TW ? w : mlp_wave_rank<NW>(w, a.worder);
   const int s = lane & 15;   // A: sample row of the tile; B/C: column
   const int kk = lane >> 4;  // k-slot
   const int64_t bt = (int64_t)tile * 16 + s;
@@ -196,7 +200,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   const bool dense_small = a.DB <= NW;
   // Dense k-steps go to the LAST waves: with F = 26 fields over 16 waves the
   // first F - NW waves already carry two fields.
-  const int dw = NW - 1 - w;                        // dense k-step of this wave
+  const int dw = NW - 1 - wf;                       // dense k-step of this wave
   const bool has_dense = dense_small && dw < a.DB;  // wave-uniform
   float dx = 0.f, dn = 0.f, drec[NT];
 #pragma unroll
@@ -262,7 +266,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   auto issue_b = [&](int cg, Pass& P) {
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
-      const int c = cg + j * NW + w;
+      const int c = cg + j * NW + wf;
       P.cj[j] = c < a.F ? c : a.F - 1;
       const float* rec = a.prep + a.field_base + (int64_t)P.cj[j] * a.field_rec;
 #pragma unroll
@@ -292,7 +296,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
         P.nrm[j][tp] = row16_sum(sq);
       }
   };
-  const int wv = threadIdx.x >> 6;
+  const int wv = TW ? (int)(threadIdx.x >> 6) : mlp_wave_rank<NW>((int)(threadIdx.x >> 6), a.worder);
   // a pass's ids and field metadata (issue_rows takes them from here)
   auto fetch_ids = [&](int cg, Pass& P) {
     int64_t* offc = P.off;
@@ -350,7 +354,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
 #ifdef RS_DIAG_STAMPS
-      if ((a.ablate & 8) && cg + j * NW + w >= a.F) { P.xs[j].zero(); continue; }
+      if ((a.ablate & 8) && cg + j * NW + wf >= a.F) { P.xs[j].zero(); continue; }
 #endif
       P.xs[j].load_nt(a.table + row[j] * a.k + KV * kk);
     }
@@ -362,7 +366,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     else RS_STAMP(12);
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
-      const bool live = cg + j * NW + w < a.F;
+      const bool live = cg + j * NW + wf < a.F;
       if constexpr (OWNER) bad |= live && !P.ok[j] && P.rid[j] != -1;
       else bad |= live && !P.ok[j];
       const bool use = live && P.ok[j];
@@ -396,7 +400,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   };
   // one slot per wave: a wave with no field left in a pass stops there (a
   // wave-uniform exit; nothing after the loop needs its slot)
-  auto has_pass = [&](int cg) { return cg < a.F && !(MAXC == 1 && cg + w >= a.F); };
+  auto has_pass = [&](int cg) { return cg < a.F && !(MAXC == 1 && cg + wf >= a.F); };
   constexpr int PS = NW * MAXC;  // fields per pass
   // PF: B fragments of the first two passes ride the id trip (registers: two
   // passes only where they are few; larger rows load theirs per pass).
@@ -1109,6 +1113,7 @@ static void launch_embed_fm_k(const EmbedFmArgs& a, int KV, int NT, hipStream_t 
 static int run_embed_fm(EmbedFmArgs a, const FmGeom& g, int kind, hipStream_t st, const char* what,
                         const FieldMeta* hm = nullptr) {
   if (a.batch == 0) return RS_OK;
+  a.worder = opt(RS_OPT_WAVE_ORDER);
   if (g.mfma) {
     a.DB = g.DB;
     a.dense_rec = g.dense_rec;
@@ -1413,7 +1418,9 @@ static void launch_pipe_kv(const EmbedFmArgs& a, const PipeArgs& p, int NT, hipS
   else launch_pipe4<KV, 2, 16, 0>(a, p, st);
 }
 
-static void launch_pipe(const EmbedFmArgs& a, const PipeArgs& p, const FmGeom& g, hipStream_t st) {
+static void launch_pipe(const EmbedFmArgs& a0, const PipeArgs& p, const FmGeom& g, hipStream_t st) {
+  EmbedFmArgs a = a0;
+  a.worder = opt(RS_OPT_WAVE_ORDER);
   switch (g.KV) {
     case 1: launch_pipe_kv<1>(a, p, g.NT, st); break;
     case 2: launch_pipe_kv<2>(a, p, g.NT, st); break;
