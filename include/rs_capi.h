@@ -77,11 +77,12 @@ enum rs_option {
                                  first layer): 0 (the default) = split wave roles (loaders +
                                  layer-0 compute waves, deepfm_ws), 1 = one role per wave (gather
                                  + FM, then the tower).  See DESIGN.md 4.5                       */
-  RS_OPT_WAVE_ORDER = 3,      /* fused towers: which waves take a layer's work items when there are
-                                 fewer items than waves (and the split-role DeepFM's roles): 0 =
-                                 waves 0, 1, 2 ..; 1 (the default) = interleaved over the CU's
-                                 SIMDs, for the hardware's placement of wave w of a 16-wave
-                                 workgroup on SIMD w / 4 (rs_diag_wave_slots).  See DESIGN.md 4.5 */
+  RS_OPT_MFMA_CHAINS = 3,     /* accumulation chains of the fp32 MFMA contractions (the fused
+                                 towers, the FM logit / DeepFM gather kernels, the CrossNet
+                                 contraction): 0 = one per output tile, 1 = four independent
+                                 chains per tile summed at the end (a dependent
+                                 v_mfma_f32_16x16x4_f32 waits ~100 cycles on its predecessor;
+                                 DESIGN.md 4.5).  Results differ from 0 in fp32 rounding only.  */
   RS_OPT_COUNT = 4
 };
 

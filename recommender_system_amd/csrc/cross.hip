@@ -81,6 +81,7 @@ struct CrossArgs {
   float* out;
   int64_t out_stride;
   int64_t batch;
+  int chains;  // RS_OPT_MFMA_CHAINS at launch
 };
 
 // The B fragments of 8 of a wave's k-steps (t0, t0 + NW, ..): L2-resident
@@ -107,12 +108,17 @@ struct CrossB {
 // are `ld` floats apart, columns >= a.d read as 0.
 template <int NT, int NW>
 __device__ __forceinline__ void cross_contract(const CrossArgs& a, const float* tile, int ld,
-                                               const CrossB<NT, NW>* pre, floatx4 (&acc)[NT]) {
+                                               const CrossB<NT, NW>* pre, floatx4 (&acc)[NT], int chains) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int s = lane & 15, kk = lane >> 4;
+  // accumulation chains (RS_OPT_MFMA_CHAINS): k-step u into chain u & 3, or
+  // all into chain 0
+  floatx4 ac[NT][4];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) ac[nt][c] = floatx4{0.f, 0.f, 0.f, 0.f};
   auto step = [&](int t0, const CrossB<NT, NW>& B) {
     float xv[8];
 #pragma unroll
@@ -123,7 +129,10 @@ __device__ __forceinline__ void cross_contract(const CrossArgs& a, const float* 
 #pragma unroll
     for (int u = 0; u < 8; ++u)
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(xv[u], B.v[u][nt], acc[nt]);
+      for (int nt = 0; nt < NT; ++nt) {
+        if (chains) ac[nt][u & 3] = mfma16x16x4(xv[u], B.v[u][nt], ac[nt][u & 3]);
+        else ac[nt][0] = mfma16x16x4(xv[u], B.v[u][nt], ac[nt][0]);
+      }
   };
   if (w < a.DB) {
     if (pre) {
@@ -139,6 +148,15 @@ __device__ __forceinline__ void cross_contract(const CrossArgs& a, const float* 
     B.load(a, t0);
     step(t0, B);
   }
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    if (chains) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[nt][i] = (ac[nt][0][i] + ac[nt][1][i]) + (ac[nt][2][i] + ac[nt][3][i]);
+    } else {
+      acc[nt] = ac[nt][0];
+    }
+  }
 }
 
 // Phases (2)-(4) on a staged 16 x d tile of x0 (rows >= `rows` zero).
@@ -151,7 +169,7 @@ __device__ __forceinline__ void cross_tile(const CrossArgs& a, float* tile, floa
   const int n = rows * a.d;
   // (2) G = X0 @ W on MFMA
   floatx4 acc[NT];
-  cross_contract<NT, NW>(a, tile, a.d, pre, acc);
+  cross_contract<NT, NW>(a, tile, a.d, pre, acc, a.chains);
   constexpr int CW = NT * 16 + 1;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
@@ -461,7 +479,7 @@ __device__ __forceinline__ void dcn_fused_body(const CrossArgs& a, const EmbedCr
 
   // CrossNet contraction G = X0 @ [w_0 .. w_{L-1}, w_o[:d]] (a.L = L + 1 columns)
   floatx4 acc[NT];
-  cross_contract<NT, NW>(a, tsm, RS, KA ? &pre : nullptr, acc);
+  cross_contract<NT, NW>(a, tsm, RS, KA ? &pre : nullptr, acc, a.chains);
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -530,7 +548,8 @@ extern "C" int rs_cross_fwd(const float* x0, int64_t x_stride, int d, int n_laye
   if (batch == 0) return RS_OK;
   const int L = n_layers;
   const CrossGeom g = cross_geom(d, L < 1 ? 1 : L);
-  CrossArgs a{x0, x_stride, d, L, g.DB, prepared, prepared + g.h_off, prepared + g.beta_off, out, out_stride, batch};
+  CrossArgs a{x0, x_stride, d, L, g.DB, prepared, prepared + g.h_off, prepared + g.beta_off, out, out_stride, batch,
+              opt(RS_OPT_MFMA_CHAINS)};
   constexpr int NW = 8;
   const size_t lds = (size_t)(((16 * d + 3) / 4) * 4 + NW * 16 * (g.NT * 16 + 1) + 16) * sizeof(float);
   const unsigned grid = (unsigned)((batch + 15) / 16);
@@ -575,7 +594,8 @@ static int embed_cross_run(const void* ids, int id_kind, int64_t id_stride, cons
   if (batch == 0) return RS_OK;
   const int L = n_layers;
   const CrossGeom g = cross_geom(d, L < 1 ? 1 : L);
-  CrossArgs a{nullptr, d, d, L, g.DB, prepared, prepared + g.h_off, prepared + g.beta_off, out, out_stride, batch};
+  CrossArgs a{nullptr, d, d, L, g.DB, prepared, prepared + g.h_off, prepared + g.beta_off, out, out_stride, batch,
+              opt(RS_OPT_MFMA_CHAINS)};
   EmbedCrossArgs e{ids, id_stride, dense, dense_stride, nd, n_fields, k, table, field_offsets, field_vocab, err_flag};
   constexpr int NW = 16;
   const size_t lds = (size_t)(((16 * d + 3) / 4) * 4 + NW * 16 * (g.NT * 16 + 1) + 16) * sizeof(float);
@@ -669,7 +689,7 @@ static int dcn_run(const void* ids, int id_kind, int64_t id_stride, const float*
   const int d = nd + n_fields * k, Lx = n_cross + 1;  // + the output Dense's cross column
   const CrossGeom g = cross_geom(d, Lx);
   CrossArgs a{nullptr, d, d, Lx, g.DB, cross_prepared, cross_prepared + g.h_off, cross_prepared + g.beta_off,
-              nullptr, 0, batch};
+              nullptr, 0, batch, opt(RS_OPT_MFMA_CHAINS)};
   EmbedCrossArgs e{ids, id_stride, dense, dense_stride, nd, n_fields, k, table, field_offsets, field_vocab, err_flag};
   const size_t lds = mg.lds;
   const unsigned grid = (unsigned)((batch + 15) / 16);

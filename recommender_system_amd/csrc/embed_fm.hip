@@ -142,10 +142,6 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // the wave's field slot: SIMD-interleaved (RS_OPT_WAVE_ORDER) so the
-  // two-field and the dense waves spread over the CU's SIMDs (the fused
-  // tower keeps wave order: its combine order is part of its results)
-  const int wf = TW ? w : mlp_wave_rank<NW>(w, a.worder);
   const int s = lane & 15;   // A: sample row of the tile; B/C: column
   const int kk = lane >> 4;  // k-slot
   const int64_t bt = (int64_t)tile * 16 + s;
@@ -157,9 +153,14 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   // w0 is requested now, not behind the rows (a dependent load at the end)
   const float w0v = OWNER ? 0.f : a.w0[0];
 
-  floatx4 acc[NT];
+  // accumulation chains (RS_OPT_MFMA_CHAINS): MFMA tp of a field slot into
+  // chain tp & 3, or all into chain 0 (the one-chain form); summed below
+  floatx4 ac[NT][4];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) ac[nt][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const bool chains = a.chains != 0;
   float qn = 0.f;
   bool bad = false;
 
@@ -200,7 +201,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   const bool dense_small = a.DB <= NW;
   // Dense k-steps go to the LAST waves: with F = 26 fields over 16 waves the
   // first F - NW waves already carry two fields.
-  const int dw = NW - 1 - wf;                       // dense k-step of this wave
+  const int dw = NW - 1 - w;                        // dense k-step of this wave
   const bool has_dense = dense_small && dw < a.DB;  // wave-uniform
   float dx = 0.f, dn = 0.f, drec[NT];
 #pragma unroll
@@ -266,7 +267,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   auto issue_b = [&](int cg, Pass& P) {
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
-      const int c = cg + j * NW + wf;
+      const int c = cg + j * NW + w;
       P.cj[j] = c < a.F ? c : a.F - 1;
       const float* rec = a.prep + a.field_base + (int64_t)P.cj[j] * a.field_rec;
 #pragma unroll
@@ -296,7 +297,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
         P.nrm[j][tp] = row16_sum(sq);
       }
   };
-  const int wv = TW ? (int)(threadIdx.x >> 6) : mlp_wave_rank<NW>((int)(threadIdx.x >> 6), a.worder);
+  const int wv = threadIdx.x >> 6;
   // a pass's ids and field metadata (issue_rows takes them from here)
   auto fetch_ids = [&](int cg, Pass& P) {
     int64_t* offc = P.off;
@@ -354,7 +355,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
 #ifdef RS_DIAG_STAMPS
-      if ((a.ablate & 8) && cg + j * NW + wf >= a.F) { P.xs[j].zero(); continue; }
+      if ((a.ablate & 8) && cg + j * NW + w >= a.F) { P.xs[j].zero(); continue; }
 #endif
       P.xs[j].load_nt(a.table + row[j] * a.k + KV * kk);
     }
@@ -366,7 +367,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     else RS_STAMP(12);
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
-      const bool live = cg + j * NW + wf < a.F;
+      const bool live = cg + j * NW + w < a.F;
       if constexpr (OWNER) bad |= live && !P.ok[j] && P.rid[j] != -1;
       else bad |= live && !P.ok[j];
       const bool use = live && P.ok[j];
@@ -376,9 +377,10 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
 #ifdef RS_DIAG_STAMPS
-          if (a.ablate & 1) { acc[nt][0] += xv * P.bw[j][nt].v[tp]; continue; }
+          if (a.ablate & 1) { ac[nt][0][0] += xv * P.bw[j][nt].v[tp]; continue; }
 #endif
-          acc[nt] = mfma16x16x4(xv, P.bw[j][nt].v[tp], acc[nt]);
+          if (chains) ac[nt][tp & 3] = mfma16x16x4(xv, P.bw[j][nt].v[tp], ac[nt][tp & 3]);
+          else ac[nt][0] = mfma16x16x4(xv, P.bw[j][nt].v[tp], ac[nt][0]);
         }
         qn = fmaf(xv * xv, P.nrm[j][tp], qn);
       }
@@ -394,13 +396,13 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
         for (int tp = 0; tp < KV; ++tp) xo[tp] = P.ok[j] ? P.xs[j].v[tp] : 0.f;
       }
     }
-    RS_USE(acc[0][0]);
+    RS_USE(ac[0][0][0]);
     if (cg == 0) RS_STAMP(13);
     else RS_STAMP(14);
   };
   // one slot per wave: a wave with no field left in a pass stops there (a
   // wave-uniform exit; nothing after the loop needs its slot)
-  auto has_pass = [&](int cg) { return cg < a.F && !(MAXC == 1 && cg + wf >= a.F); };
+  auto has_pass = [&](int cg) { return cg < a.F && !(MAXC == 1 && cg + w >= a.F); };
   constexpr int PS = NW * MAXC;  // fields per pass
   // PF: B fragments of the first two passes ride the id trip (registers: two
   // passes only where they are few; larger rows load theirs per pass).
@@ -457,7 +459,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     const int e = 4 * dw + kk;
     dx = e < a.nd ? dx : 0.f;
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(dx, drec[nt], acc[nt]);
+    for (int nt = 0; nt < NT; ++nt) ac[nt][0] = mfma16x16x4(dx, drec[nt], ac[nt][0]);
     qn = fmaf(dx * dx, dn, qn);
     if constexpr (TW) {
       if (e < a.nd) tsm[s * xrs + a.F * a.k + e] = dx;
@@ -472,13 +474,23 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       const float x = e < a.nd ? xv : 0.f;
       const float* rec = a.prep + (int64_t)t * a.dense_rec;
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16x16x4(x, rec[nt * 64 + lane], acc[nt]);
+      for (int nt = 0; nt < NT; ++nt) ac[nt][0] = mfma16x16x4(x, rec[nt * 64 + lane], ac[nt][0]);
       qn = fmaf(x * x, rec[NT * 64 + kk], qn);
       if constexpr (TW) {
         if (e < a.nd) tsm[s * xrs + a.F * a.k + e] = x;
       } else if (a.x_out && valid && e < a.nd) {
         a.x_out[b * d + e] = x;
       }
+    }
+  }
+  floatx4 acc[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    if (chains) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[nt][i] = (ac[nt][0][i] + ac[nt][1][i]) + (ac[nt][2][i] + ac[nt][3][i]);
+    } else {
+      acc[nt] = ac[nt][0];
     }
   }
   RS_USE(acc[0][0]);
@@ -695,9 +707,6 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
   __shared__ int cnt[4];  // dense k-steps written | loaders past burst 0 | past burst 1 | FM partials in
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // roles by the wave's SIMD-interleaved rank (RS_OPT_WAVE_ORDER): ranks
-  // 0..7 load, 8..15 compute — two of each on every SIMD
-  const int wr = mlp_wave_rank<NW>(w, t.worder);
   const int s = lane & 15, kk = lane >> 4;
   const int64_t bt = (int64_t)blockIdx.x * 16 + s;
   const bool valid = bt < a.batch;
@@ -710,9 +719,9 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     MLP_STAMP(0);
   }
   if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
-  if (wr < WS_NL) {
+  if (w < WS_NL) {
     // ================================ loader
-    const int l = wr;
+    const int l = w;
     const float w0v = a.w0[0];
     const int dw = l - (WS_NL - a.DB);  // dense k-steps on the last DB loaders (fewest fields)
     const bool has_dense = dw >= 0;
@@ -735,14 +744,17 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
         if (s <= a.kfm) bw[p] = *reinterpret_cast<const floatx4*>(a.prep + a.field_base + (int64_t)c * a.field_rec + lane * 4);
       }
     }
-    for (int i = l * 64 + lane; i < t.ptot; i += WS_NL * 64) par[i] = t.prep[t.wtot + i];
+    for (int i = threadIdx.x; i < t.ptot; i += WS_NL * 64) par[i] = t.prep[t.wtot + i];
     __syncthreads();  // the counters start at 0 (the compute waves pass the same barrier)
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    floatx4 ac[4];  // accumulation chains (RS_OPT_MFMA_CHAINS; one chain: ac[0] only)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) ac[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const bool chains = a.chains != 0;
     float qn = 0.f;
     if (has_dense) {  // the dense group of the tile: dense columns + the zero padding up to 16
       const int e = 4 * dw + kk;
       const float x = e < a.nd ? dx : 0.f;
-      acc = mfma16x16x4(x, drec, acc);
+      ac[0] = mfma16x16x4(x, drec, ac[0]);
       qn = fmaf(x * x, dn, qn);
       tsm[s * RS + F * 16 + e] = x;
       lds_signal(&cnt[0]);
@@ -776,7 +788,8 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
           *reinterpret_cast<floatx4*>(tsm + s * RS + c * 16 + 4 * kk) = x;
 #pragma unroll
           for (int tp = 0; tp < 4; ++tp) {
-            acc = mfma16x16x4(x[tp], bw[p][tp], acc);
+            if (chains) ac[tp] = mfma16x16x4(x[tp], bw[p][tp], ac[tp]);
+            else ac[0] = mfma16x16x4(x[tp], bw[p][tp], ac[0]);
             qn = fmaf(x[tp] * x[tp], nrm[p][tp], qn);
           }
         }
@@ -785,6 +798,11 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     }
     if (__any(bad && valid) && lane == 0) flag_error(a.err);
     // FM: last-wave finish over the loaders' partial tiles (wave order)
+    floatx4 acc = ac[0];
+    if (chains) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = (ac[0][i] + ac[1][i]) + (ac[2][i] + ac[3][i]);
+    }
     lf_acc[l][lane] = acc;
     qn += __shfl_xor(qn, 16);
     qn += __shfl_xor(qn, 32);
@@ -818,7 +836,7 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     }
   } else {
     // ================================ layer 0 compute
-    const int c8 = wr - WS_NL;
+    const int c8 = w - WS_NL;
     const floatx4* W0 = reinterpret_cast<const floatx4*>(t.prep + t.off[0]) + lane + (int64_t)c8 * G * 64;
     const floatx4* W1 = W0 + (int64_t)WS_NL * G * 64;  // output tile c8 + 8
     // k-group order: the dense group (G - 1) first, then fields 0 .. F-1
@@ -831,7 +849,10 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     }
     __syncthreads();  // the counters start at 0
     const float* ap = tsm + s * RS + 4 * kk;
-    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    // two output tiles; with RS_OPT_MFMA_CHAINS two chains each (MFMA j of a
+    // group into chain j & 1)
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc0b = acc0, acc1b = acc0;
+    const bool chains = t.chains != 0;
     lds_wait_ge(&cnt[0], a.DB);
 #pragma unroll
     for (int i = 0; i < G; ++i) {
@@ -840,15 +861,32 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
       const int u = i % 3;
       const floatx4 av = *reinterpret_cast<const floatx4*>(ap + 16 * grp(i));
       __builtin_amdgcn_sched_barrier(0);
+      if (chains) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc0 = mfma16x16x4(av[j], r0[u][j], acc0);
-        acc1 = mfma16x16x4(av[j], r1[u][j], acc1);
+        for (int j = 0; j < 4; j += 2) {
+          acc0 = mfma16x16x4(av[j], r0[u][j], acc0);
+          acc1 = mfma16x16x4(av[j], r1[u][j], acc1);
+          acc0b = mfma16x16x4(av[j + 1], r0[u][j + 1], acc0b);
+          acc1b = mfma16x16x4(av[j + 1], r1[u][j + 1], acc1b);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc0 = mfma16x16x4(av[j], r0[u][j], acc0);
+          acc1 = mfma16x16x4(av[j], r1[u][j], acc1);
+        }
       }
       const int nx = i + 3 < G ? i + 3 : G - 1;
       r0[u] = W0[(int64_t)grp(nx) * 64];
       r1[u] = W1[(int64_t)grp(nx) * 64];
       __builtin_amdgcn_sched_barrier(0);
+    }
+    if (chains) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc0[i] += acc0b[i];
+        acc1[i] += acc1b[i];
+      }
     }
     const float* bias = par + t.poff[0];
     const float* alpha = bias + t.Np[0];
@@ -867,8 +905,8 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
   {  // layer 1's first weights (this wave's first item of it, if any)
     const int T1 = t.Np[1] >> 4, G1 = t.Kp[1] >> 4;
     const int S1 = mlp_slices(T1, G1, NW);
-    if (wr < T1 * S1) {
-      const MlpItem it = mlp_item(wr, T1, G1, S1);
+    if (w < T1 * S1) {
+      const MlpItem it = mlp_item(w, T1, G1, S1);
       mlp_ring_fill(ring, reinterpret_cast<const floatx4*>(t.prep + t.off[1]) + lane + (int64_t)it.t * G1 * 64,
                     it.g0, it.g1);
     }
@@ -1113,7 +1151,7 @@ static void launch_embed_fm_k(const EmbedFmArgs& a, int KV, int NT, hipStream_t 
 static int run_embed_fm(EmbedFmArgs a, const FmGeom& g, int kind, hipStream_t st, const char* what,
                         const FieldMeta* hm = nullptr) {
   if (a.batch == 0) return RS_OK;
-  a.worder = opt(RS_OPT_WAVE_ORDER);
+  a.chains = opt(RS_OPT_MFMA_CHAINS);
   if (g.mfma) {
     a.DB = g.DB;
     a.dense_rec = g.dense_rec;
@@ -1420,7 +1458,7 @@ static void launch_pipe_kv(const EmbedFmArgs& a, const PipeArgs& p, int NT, hipS
 
 static void launch_pipe(const EmbedFmArgs& a0, const PipeArgs& p, const FmGeom& g, hipStream_t st) {
   EmbedFmArgs a = a0;
-  a.worder = opt(RS_OPT_WAVE_ORDER);
+  a.chains = opt(RS_OPT_MFMA_CHAINS);
   switch (g.KV) {
     case 1: launch_pipe_kv<1>(a, p, g.NT, st); break;
     case 2: launch_pipe_kv<2>(a, p, g.NT, st); break;
@@ -1792,6 +1830,7 @@ static int deepfm_run(const void* ids, int id_kind, int64_t id_stride, const flo
   a.dense_rec = fg.dense_rec;
   a.field_rec = fg.field_rec;
   a.field_base = fg.field_base;
+  a.chains = opt(RS_OPT_MFMA_CHAINS);
   hipStream_t st = as_stream(stream);
   with_id_kind(id_kind, [&](auto K) {
     constexpr int KIND = decltype(K)::value;

@@ -236,49 +236,6 @@ __device__ __forceinline__ void inner_fast_body(const InnerArgs& a, const FieldM
   IP_STAMP(2);
   }
 
-  // coalesced output rows [flat F*K | inner P | outer P] of the workgroup's
-  // contiguous block as float4 stores (scalar stores are issue-bound at
-  // ~4 B/clk/CU), in two passes: the chunks whose four columns are all flat
-  // leave right after the gather (their stores drain under the Gram MFMAs),
-  // the rest after the Gram barrier.
-  const int FK = a.write_flat ? F * K : 0;
-  const int W = FK + PP;
-  auto write_block = [&](bool flat_pass) {
-    float* ob = a.out + b0 * a.out_stride;
-    const int n = nvalid * W;
-    const int dq = 4 * IP_NT / W, dr = 4 * IP_NT - dq * W;
-    int f = 4 * tid, s0 = f / W, c0 = f - s0 * W;
-    for (; f < n; f += 4 * IP_NT) {
-      bool flat = true;
-      {
-        int cc = c0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          flat = flat && cc < FK;
-          if (++cc == W) cc = 0;
-        }
-      }
-      if (flat == flat_pass) {
-        floatx4 v;
-        int ss = s0, cc = c0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          v[q] = cc < FK ? tile[ss * SS + cc] : gram[ss * PP + (cc - FK)];
-          if (++cc == W) { cc = 0; ++ss; }
-        }
-        if (f + 4 <= n) {
-          *reinterpret_cast<floatx4*>(ob + f) = v;
-        } else {
-          for (int q = 0; q < n - f; ++q) ob[f + q] = v[q];
-        }
-      }
-      s0 += dq;
-      c0 += dr;
-      if (c0 >= W) { c0 -= W; ++s0; }
-    }
-  };
-  if (a.contig && FK > 0) write_block(true);
-
   // Gram matrix per sample on MFMA: G = E E^T with E [F x K] from the LDS
   // tile, 16x16 blocks (bi <= bj) of v_mfma_f32_16x16x4_f32.  Lane l holds
   // float4 E[16b + (l&15)][16grp + 4(l>>4) ..+3] — the A fragment of row block
@@ -421,9 +378,33 @@ __device__ __forceinline__ void inner_fast_body(const InnerArgs& a, const FieldM
   }
   __syncthreads();
   IP_STAMP(3);
+  // coalesced output rows [flat F*K | inner P | outer P]
+  const int FK = a.write_flat ? F * K : 0;
+  const int W = FK + PP;
   if (a.contig) {
-    // the workgroup's rows are one contiguous, 16-B aligned block
-    write_block(false);
+    // the workgroup's rows are one contiguous, 16-B aligned block: float4
+    // stores (scalar stores are issue-bound at ~4 B/clk/CU)
+    float* ob = a.out + b0 * a.out_stride;
+    const int n = nvalid * W;
+    const int dq = 4 * IP_NT / W, dr = 4 * IP_NT - dq * W;
+    int f = 4 * tid, s0 = f / W, c0 = f - s0 * W;
+    for (; f < n; f += 4 * IP_NT) {
+      floatx4 v;
+      int ss = s0, cc = c0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[q] = cc < FK ? tile[ss * SS + cc] : gram[ss * PP + (cc - FK)];
+        if (++cc == W) { cc = 0; ++ss; }
+      }
+      if (f + 4 <= n) {
+        *reinterpret_cast<floatx4*>(ob + f) = v;
+      } else {
+        for (int q = 0; q < n - f; ++q) ob[f + q] = v[q];
+      }
+      s0 += dq;
+      c0 += dr;
+      if (c0 >= W) { c0 -= W; ++s0; }
+    }
   } else {
   for (int s = 0; s < nvalid; ++s) {
     float* orow = a.out + (b0 + s) * a.out_stride;

@@ -68,7 +68,7 @@ struct MlpArgs {
   int64_t M;
   unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_mlp_set_dbg)
   int unroll;               // RS_OPT_MLP_UNROLL at launch
-  int worder;               // RS_OPT_WAVE_ORDER at launch
+  int chains;               // RS_OPT_MFMA_CHAINS at launch
 };
 #define MLP_STAMP(i)                                                                              \
   do {                                                                                            \
@@ -103,20 +103,6 @@ __device__ __forceinline__ MlpItem mlp_item(int item, int T, int G, int S) {
   return MlpItem{t, part * G / S, (part + 1) * G / S};
 }
 
-// The wave's rank in the order that takes a layer's items (items r, r + NW,
-// ..): worder 1 interleaves the CU's SIMDs — the hardware puts wave w of an
-// NW-wave workgroup on SIMD w / (NW / 4) (rs_diag_wave_slots), so item order
-// = wave order would stack a layer with fewer items than waves (8 / 4 / 1
-// output tiles after the first) on one or two SIMDs.  A bijection of 0..NW-1.
-template <int NW>
-__device__ __forceinline__ int mlp_wave_rank(int w, int worder) {
-  if constexpr (NW % 4 == 0 && NW >= 8) {
-    constexpr int PER = NW / 4;
-    if (worder) return (w % PER) * 4 + w / PER;
-  }
-  return w;
-}
-
 // B fragments (1 KB per k-group per output tile) stream through a ring of 4
 // registers.  mlp_ring_fill issues the first 4 groups of an item (it can run
 // before the barrier that publishes the item's A tile); mlp_mac<D> consumes
@@ -129,9 +115,37 @@ __device__ __forceinline__ void mlp_ring_fill(floatx4 (&ring)[MLP_R], const floa
   for (int u = 0; u < MLP_R; ++u) ring[u] = bp[(int64_t)min(g0 + u, g1 - 1) * 64];
 }
 
-template <int D>
+// CH = 4: MFMA j of every k-group accumulates into chain j (four independent
+// dependency chains, summed (c0 + c1) + (c2 + c3) at the end): a dependent
+// fp32 MFMA issues only ~100 cycles after its predecessor, so a single chain
+// leaves the pipe idle on a SIMD with one or two busy waves.
+template <int CH>
+struct MacAcc {
+  floatx4 c[CH];
+  __device__ __forceinline__ MacAcc() {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) c[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+  __device__ __forceinline__ void mac4(const floatx4& a, const floatx4& b) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j % CH] = mfma16x16x4(a[j], b[j], c[j % CH]);
+  }
+  __device__ __forceinline__ floatx4 sum() const {
+    if constexpr (CH == 1) {
+      return c[0];
+    } else {
+      floatx4 r;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = (c[0][i] + c[1][i]) + (c[2][i] + c[3][i]);
+      return r;
+    }
+  }
+};
+
+template <int D, int CH>
 __device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[MLP_R], const float* __restrict__ ap,
-                                          const floatx4* __restrict__ bp, int g0, int g1, floatx4& acc) {
+                                          const floatx4* __restrict__ bp, int g0, int g1, floatx4& out) {
+  MacAcc<CH> acc;
   // A fragments are read one group ahead so the LDS latency hides behind
   // the previous group's MFMAs
   floatx4 an = *reinterpret_cast<const floatx4*>(ap + 16 * g0);
@@ -141,8 +155,7 @@ __device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[MLP_R], const float* _
       const floatx4 av = an;
       an = *reinterpret_cast<const floatx4*>(ap + 16 * min(g + u + 1, g1 - 1));
       __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc = mfma16x16x4(av[j], ring[u][j], acc);
+      acc.mac4(av, ring[u]);
       // refill the slot in place right after its MFMAs and pin it there: left
       // alone the scheduler sinks every refill to the end of the iteration
       // (or copies in-flight registers), which drains the ring each pass
@@ -150,6 +163,7 @@ __device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[MLP_R], const float* _
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+  out = acc.sum();
 }
 
 // The same contraction over exactly N k-groups, fully unrolled: straight-line
@@ -159,10 +173,11 @@ __device__ __forceinline__ void mlp_mac_d(floatx4 (&ring)[MLP_R], const float* _
 // groups ahead in the 16 / 8 / 4-group layers: 2 (A/B of rs_mlp_fwd, B 4096:
 // 20.66 us vs 20.75 at 1 and 20.89 at 4; profiles/r4_ab_mlp_small_d.json)
 constexpr int MLP_SMALL_D = 2;
-template <int N, int D>
+template <int N, int D, int CH>
 __device__ __forceinline__ void mlp_mac_u(floatx4 (&ring)[MLP_R], const float* __restrict__ ap,
-                                          const floatx4* __restrict__ bp, int g0, floatx4& acc) {
+                                          const floatx4* __restrict__ bp, int g0, floatx4& out) {
   static_assert(N % D == 0 && D <= MLP_R, "unrolled contraction: D | N, D <= ring");
+  MacAcc<CH> acc;
   const int g1 = g0 + N;
   floatx4 an = *reinterpret_cast<const floatx4*>(ap + 16 * g0);
 #pragma unroll
@@ -173,32 +188,39 @@ __device__ __forceinline__ void mlp_mac_u(floatx4 (&ring)[MLP_R], const float* _
       const floatx4 av = an;
       an = *reinterpret_cast<const floatx4*>(ap + 16 * min(g + u + 1, g1 - 1));
       __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc = mfma16x16x4(av[j], ring[u][j], acc);
+      acc.mac4(av, ring[u]);
       ring[u] = bp[(int64_t)min(g + u + D, g1 - 1) * 64];
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+  out = acc.sum();
 }
 
-__device__ __forceinline__ void mlp_mac(floatx4 (&ring)[MLP_R], const float* ap, const floatx4* bp, int g0, int g1,
-                                        floatx4& acc, int unroll = 0) {
+template <int CH>
+__device__ __forceinline__ void mlp_mac_ch(floatx4 (&ring)[MLP_R], const float* ap, const floatx4* bp, int g0,
+                                           int g1, floatx4& acc, int unroll) {
   const int n = g1 - g0;  // wave-uniform
   if (unroll) {  // the DeepFM / DCN tower widths (429|432 -> 256 -> 128 -> 64 -> head)
     switch (n) {
-      case 27: return mlp_mac_u<27, 3>(ring, ap, bp, g0, acc);
-      case 16: return mlp_mac_u<16, MLP_SMALL_D>(ring, ap, bp, g0, acc);
-      case 8: return mlp_mac_u<8, MLP_SMALL_D>(ring, ap, bp, g0, acc);
-      case 4: return mlp_mac_u<4, MLP_SMALL_D>(ring, ap, bp, g0, acc);
-      case 2: return mlp_mac_u<2, 2>(ring, ap, bp, g0, acc);
-      case 1: return mlp_mac_u<1, 1>(ring, ap, bp, g0, acc);
+      case 27: return mlp_mac_u<27, 3, CH>(ring, ap, bp, g0, acc);
+      case 16: return mlp_mac_u<16, MLP_SMALL_D, CH>(ring, ap, bp, g0, acc);
+      case 8: return mlp_mac_u<8, MLP_SMALL_D, CH>(ring, ap, bp, g0, acc);
+      case 4: return mlp_mac_u<4, MLP_SMALL_D, CH>(ring, ap, bp, g0, acc);
+      case 2: return mlp_mac_u<2, 2, CH>(ring, ap, bp, g0, acc);
+      case 1: return mlp_mac_u<1, 1, CH>(ring, ap, bp, g0, acc);
       default: break;
     }
   }
   // (a 4-deep ring gets a full vmcnt(0) at its loop head from the compiler)
-  if (n % 3 == 0) mlp_mac_d<3>(ring, ap, bp, g0, g1, acc);
-  else if (n % 2 == 0) mlp_mac_d<2>(ring, ap, bp, g0, g1, acc);
-  else mlp_mac_d<1>(ring, ap, bp, g0, g1, acc);
+  if (n % 3 == 0) mlp_mac_d<3, CH>(ring, ap, bp, g0, g1, acc);
+  else if (n % 2 == 0) mlp_mac_d<2, CH>(ring, ap, bp, g0, g1, acc);
+  else mlp_mac_d<1, CH>(ring, ap, bp, g0, g1, acc);
+}
+
+__device__ __forceinline__ void mlp_mac(floatx4 (&ring)[MLP_R], const float* ap, const floatx4* bp, int g0, int g1,
+                                        floatx4& acc, int unroll = 0, int chains = 0) {
+  if (chains) mlp_mac_ch<4>(ring, ap, bp, g0, g1, acc, unroll);
+  else mlp_mac_ch<1>(ring, ap, bp, g0, g1, acc, unroll);
 }
 
 // The tower on a 16-row tile whose input is already in LDS buf0 (barrier not
@@ -214,7 +236,6 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
   float* par = red + NW * 256;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = mlp_wave_rank<NW>(w, a.worder);
 
   float* in = (l0 & 1) ? smem + 16 * RS : smem;
   float* out = (l0 & 1) ? smem : smem + 16 * RS;
@@ -250,12 +271,12 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
     };
 
     const float* ap = in + (lane & 15) * RS + 4 * (lane >> 4);
-    for (int item = wr; item < T * S; item += NW) {
+    for (int item = w; item < T * S; item += NW) {
       const MlpItem it = mlp_item(item, T, G, S);
       const floatx4* bp = W + (int64_t)it.t * G * 64;
-      if (item != wr) mlp_ring_fill(ring, bp, it.g0, it.g1);
+      if (item != w) mlp_ring_fill(ring, bp, it.g0, it.g1);
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-      mlp_mac(ring, ap, bp, it.g0, it.g1, acc, a.unroll);
+      mlp_mac(ring, ap, bp, it.g0, it.g1, acc, a.unroll, a.chains);
       if (S == 1) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) finish(4 * (lane >> 4) + r, 16 * it.t + (lane & 15), acc[r]);
@@ -269,8 +290,8 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
     if (l + 1 < a.L) {
       const int T2 = a.Np[l + 1] >> 4, G2 = a.Kp[l + 1] >> 4;
       const int S2 = mlp_slices(T2, G2, NW);
-      if (wr < T2 * S2) {
-        const MlpItem it = mlp_item(wr, T2, G2, S2);
+      if (w < T2 * S2) {
+        const MlpItem it = mlp_item(w, T2, G2, S2);
         mlp_ring_fill(ring, reinterpret_cast<const floatx4*>(a.prep + a.off[l + 1]) + lane + (int64_t)it.t * G2 * 64,
                       it.g0, it.g1);
       }
@@ -298,9 +319,8 @@ __device__ __forceinline__ void mlp_first_fill(const MlpArgs& a, floatx4 (&ring)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int T = a.Np[0] >> 4, G = a.Kp[0] >> 4;
   const int S = mlp_slices(T, G, NW);
-  const int wr = mlp_wave_rank<NW>(w, a.worder);
-  if (wr < T * S) {
-    const MlpItem it = mlp_item(wr, T, G, S);
+  if (w < T * S) {
+    const MlpItem it = mlp_item(w, T, G, S);
     mlp_ring_fill(ring, reinterpret_cast<const floatx4*>(a.prep + a.off[0]) + lane + (int64_t)it.t * G * 64, it.g0,
                   it.g1);
   }
@@ -327,7 +347,7 @@ inline bool mlp_fill_args(const MlpGeom& g, const int* acts, const float* prepar
   a.K0 = g.K[0];
   a.rs = g.rs;
   a.unroll = opt(RS_OPT_MLP_UNROLL);
-  a.worder = opt(RS_OPT_WAVE_ORDER);
+  a.chains = opt(RS_OPT_MFMA_CHAINS);
   return true;
 }
 

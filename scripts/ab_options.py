@@ -19,7 +19,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-OPTS = {"embed_fm_kernel": 0, "mlp_unroll": 1, "deepfm_kernel": 2, "wave_order": 3}
+OPTS = {"embed_fm_kernel": 0, "mlp_unroll": 1, "deepfm_kernel": 2, "mfma_chains": 3}
 
 
 def main():

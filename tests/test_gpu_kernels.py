@@ -960,16 +960,16 @@ def test_deepfm_kernel_forms(gpu, variant, B, id_dtype, hidden, nd):
         _lib.set_option(_lib.OPT_DEEPFM_KERNEL, prev)
 
 
-# --------------------------- tower item order (RS_OPT_WAVE_ORDER)
+# --------------------------- MFMA accumulation chains (RS_OPT_MFMA_CHAINS)
 @pytest.mark.parametrize("B,hidden", [(4096, [256, 128, 64]), (333, [248, 160, 8]), (64, [256, 128])])
-def test_tower_wave_order_bit_identical(gpu, B, hidden):
-    """Which wave takes which work item of a layer (RS_OPT_WAVE_ORDER 0:
-    waves in order, 1: interleaved over the SIMDs) changes no arithmetic: the
-    fused DeepFM (both kernel forms), the fused DCN and rs_mlp_fwd give
-    bit-identical outputs under both orders (the oracle checks of each
-    kernel run under the default order elsewhere)."""
+def test_mfma_chains_match(gpu, B, hidden):
+    """Four independent accumulation chains per output tile (RS_OPT_MFMA_CHAINS
+    1) change only the fp32 summation order: the fused DeepFM (both kernel
+    forms) == the fp64 oracle, and the FM logit kernel, the fused DCN, the
+    CrossNet kernel and rs_mlp_fwd agree with the one-chain form within fp32
+    rounding."""
     from recommender_system_amd import DCN, DeepFM, _lib
-    from tests.helpers import criteo_columns
+    from tests.helpers import criteo_columns, dnn_params, tables_of
     rng = np.random.default_rng(B + len(hidden))
     vocabs = rng.integers(2, 3000, size=26)
     cols = criteo_columns(vocabs, embed_dim=16)
@@ -980,26 +980,38 @@ def test_tower_wave_order_bit_identical(gpu, B, hidden):
             l.bias.uniform_(-0.1, 0.1)
         dfm.embed_layer.table.mul_(10.0)
         dcn.embed_layer.table.mul_(10.0)
-    ids = torch.as_tensor(random_ids(rng, B, vocabs, np.int64), device=gpu).to(torch.int32)
-    dense = torch.as_tensor(rng.random((B, 13)).astype(np.float32), device=gpu)
+    ids_np = random_ids(rng, B, vocabs, np.int64)
+    ids = torch.as_tensor(ids_np, device=gpu).to(torch.int32)
+    dense_np = rng.random((B, 13)).astype(np.float32)
+    dense = torch.as_tensor(dense_np, device=gpu)
     x = torch.as_tensor(rng.uniform(-1, 1, (B, 429)).astype(np.float32), device=gpu)
     outs = {}
-    prev_o = _lib.set_option(_lib.OPT_WAVE_ORDER, 0)
-    prev_k = _lib.lib().rs_get_option(_lib.OPT_DEEPFM_KERNEL)
+    lib = _lib.lib()
+    prev_c, prev_k = lib.rs_get_option(_lib.OPT_MFMA_CHAINS), lib.rs_get_option(_lib.OPT_DEEPFM_KERNEL)
     try:
-        for order in (0, 1):
-            _lib.set_option(_lib.OPT_WAVE_ORDER, order)
+        for ch in (0, 1):
+            _lib.set_option(_lib.OPT_MFMA_CHAINS, ch)
             for form in (0, 1):
                 _lib.set_option(_lib.OPT_DEEPFM_KERNEL, form)
-                outs[("deepfm", form, order)] = dfm.forward_fused((dense, ids)).clone()
-            outs[("dcn", order)] = dcn.forward_fused((dense, ids)).clone()
-            outs[("mlp", order)] = dfm.dnn(x).clone()
+                fm = torch.empty(B, 1, device=gpu)
+                outs[("deepfm", form, ch)] = dfm.forward_fused((dense, ids), fm_logit=fm).clone()
+                outs[("fm", form, ch)] = fm.clone()
+            outs[("fm_logit", ch)] = dfm.fm_logit((dense, ids)).clone()
+            outs[("dcn", ch)] = dcn.forward_fused((dense, ids)).clone()
+            outs[("cross", ch)] = dcn.cross_fused((dense, ids)).clone()
+            outs[("mlp", ch)] = dfm.dnn(x).clone()
         torch.cuda.synchronize()
     finally:
-        _lib.set_option(_lib.OPT_WAVE_ORDER, prev_o)
+        _lib.set_option(_lib.OPT_MFMA_CHAINS, prev_c)
         _lib.set_option(_lib.OPT_DEEPFM_KERNEL, prev_k)
+    hidden_p, out_p = dnn_params(dfm.dnn)
+    p = {"tables": tables_of(dfm.embed_layer), "w0": dfm.fm.w0.cpu().numpy(), "w1": dfm.fm.w1.cpu().numpy(),
+         "v": dfm.fm.v.cpu().numpy(), "dnn_hidden": hidden_p, "dnn_out": out_p}
+    ref, ref_fm, _ = O.deepfm(None, p, nd=13, inputs=(dense_np, ids_np))
     for form in (0, 1):
-        assert torch.equal(outs[("deepfm", form, 0)], outs[("deepfm", form, 1)]), f"deepfm form {form}"
-    assert torch.equal(outs[("dcn", 0)], outs[("dcn", 1)])
-    assert torch.equal(outs[("mlp", 0)], outs[("mlp", 1)])
-    assert not torch.equal(outs[("mlp", 1)], torch.zeros_like(outs[("mlp", 1)]))
+        assert_rel_close(outs[("deepfm", form, 1)], ref, what=f"deepfm form {form}, four chains")
+        assert_scaled_close(outs[("fm", form, 1)], ref_fm, what=f"deepfm form {form} fm logit, four chains")
+    assert_scaled_close(outs[("fm_logit", 1)], outs[("fm_logit", 0)].cpu().numpy(), what="fm logit")
+    assert_rel_close(outs[("dcn", 1)], outs[("dcn", 0)].cpu().numpy(), what="dcn")
+    assert_scaled_close(outs[("cross", 1)], outs[("cross", 0)].cpu().numpy(), what="cross")
+    assert_scaled_close(outs[("mlp", 1)], outs[("mlp", 0)].cpu().numpy(), what="mlp")
