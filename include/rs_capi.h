@@ -103,6 +103,10 @@ int rs_diag_empty(int grid, int block, rs_stream_t stream);
  * SIMD, 11:8 CU, 12 SH, 15:13 SE) into out[grid * block / 64], lds_bytes of
  * dynamic LDS per workgroup — how a workgroup's waves spread over the SIMDs. */
 int rs_diag_wave_slots(int grid, int block, int lds_bytes, uint32_t* out, rs_stream_t stream);
+/* rs_diag_mfma_chain: every wave issues n v_mfma_f32_16x16x4_f32 as `chains`
+ * (1, 2, 4) independent accumulation chains; cyc[wave] = s_memtime cycles. */
+int rs_diag_mfma_chain(int grid, int block, int n, int chains, unsigned long long* cyc, float* sink,
+                       rs_stream_t stream);
 
 /* --------------------------------------------------------- embedding (a3)
  * Replaces EmbedLayer.call (layer/core.py:273-280) + the dense/sparse concat of

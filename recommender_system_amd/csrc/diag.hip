@@ -16,7 +16,49 @@ __global__ void diag_wave_slots_kernel(uint32_t* out) {
     out[(int64_t)blockIdx.x * (blockDim.x >> 6) + w] = hw;
   }
 }
+
+// MFMA issue timing: every wave runs n v_mfma_f32_16x16x4_f32 as `chains`
+// independent accumulation chains (1, 2 or 4) and lane 0 records the
+// s_memtime cycles they took; the result is stored so nothing is dropped.
+__global__ void diag_mfma_chain_kernel(int n, int chains, unsigned long long* cyc, float* sink) {
+  const int lane = threadIdx.x & 63;
+  float a = 1.0f + lane * 1e-3f, b = 0.5f - lane * 1e-3f;
+  floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  if (chains == 4) {
+    for (int i = 0; i < n; i += 4) {
+      c0 = mfma16x16x4(a, b, c0);
+      c1 = mfma16x16x4(a, b, c1);
+      c2 = mfma16x16x4(a, b, c2);
+      c3 = mfma16x16x4(a, b, c3);
+    }
+  } else if (chains == 2) {
+    for (int i = 0; i < n; i += 2) {
+      c0 = mfma16x16x4(a, b, c0);
+      c1 = mfma16x16x4(a, b, c1);
+    }
+  } else {
+    for (int i = 0; i < n; ++i) c0 = mfma16x16x4(a, b, c0);
+  }
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r += c0[i] + c1[i] + c2[i] + c3[i];
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  sink[blockIdx.x * blockDim.x + threadIdx.x] = r;
+  if (lane == 0) cyc[blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)] = t1 - t0;
+}
 }  // namespace rs
+
+extern "C" int rs_diag_mfma_chain(int grid, int block, int n, int chains, unsigned long long* cyc, float* sink,
+                                  rs_stream_t stream) {
+  if (grid < 1 || block < 64 || block > 1024 || block % 64 || n < 4 || n % 4 || !cyc || !sink ||
+      (chains != 1 && chains != 2 && chains != 4)) {
+    rs::set_error("rs_diag_mfma_chain: bad arguments");
+    return RS_ERR_ARG;
+  }
+  rs::diag_mfma_chain_kernel<<<grid, block, 0, (hipStream_t)stream>>>(n, chains, cyc, sink);
+  return rs::launch_status("rs_diag_mfma_chain");
+}
 
 // An empty launch: replayed back to back from a hipGraph it measures the
 // dependent-launch slot (dispatch + end-of-kernel + barrier) of the box.

@@ -38,6 +38,7 @@ def main():
     lib = _lib.lib()
     lib.rs_diag_mlp_set_dbg.argtypes = [C.c_void_p]
     _lib.set_option(_lib.OPT_DEEPFM_KERNEL, int(os.environ.get("DIAG_DEEPFM_OPT", "1")))
+    _lib.set_option(_lib.OPT_MFMA_CHAINS, int(os.environ.get("DIAG_CHAINS", "0")))
     for i in range(40):
         m.forward_fused((dense[i % NP], ids[i % NP]), check_ids=False)
     torch.cuda.synchronize()
@@ -52,7 +53,8 @@ def main():
         names[2 + 2 * l] = f"l{l}_start"
         names[3 + 2 * l] = f"l{l}_mac_done"
     names[15] = "end"
-    out = {"B": B, "V": V, "deepfm_kernel_option": int(os.environ.get("DIAG_DEEPFM_OPT", "1")), "phases_cycles": {}}
+    out = {"B": B, "V": V, "deepfm_kernel_option": int(os.environ.get("DIAG_DEEPFM_OPT", "1")),
+           "mfma_chains": int(os.environ.get("DIAG_CHAINS", "0")), "phases_cycles": {}}
     for j, n in names.items():
         rel = d[:, :, j] - t0
         out["phases_cycles"][n] = {"median_wave": int(np.median(rel)), "slowest_wave": int(np.median(rel.max(axis=1)))}
