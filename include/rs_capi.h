@@ -76,8 +76,7 @@ enum rs_option {
   RS_OPT_DEEPFM_KERNEL = 2,   /* rs_deepfm_fwd_hm at the Criteo shape (k 16, 26 fields, 256-unit
                                  first layer): 0 (the default) = split wave roles (loaders +
                                  layer-0 compute waves, deepfm_ws), 1 = one role per wave (gather
-                                 + FM, then the tower), 2 = split roles with the loaders taking
-                                 half of layer 0 once the rows are in.  See DESIGN.md 4.5        */
+                                 + FM, then the tower).  See DESIGN.md 4.5                       */
   RS_OPT_MFMA_CHAINS = 3,     /* accumulation chains of the fp32 MFMA contractions (the fused
                                  towers, the FM logit / DeepFM gather kernels, the CrossNet
                                  contraction): 0 = one per output tile, 1 = four independent

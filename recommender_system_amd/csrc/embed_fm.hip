@@ -695,11 +695,7 @@ __device__ __forceinline__ void lds_signal(int* p) {
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// SHARE (RS_OPT_DEEPFM_KERNEL 2): the compute waves take output tiles 0..7
-// of layer 0 (one each) and the loaders, once their rows and the FM are in,
-// take tiles 8..15 — four waves per SIMD on layer 0 after the gather instead
-// of two.
-template <int KIND, int G, bool SHARE>
+template <int KIND, int G>
 __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, FieldMeta m) {
   typedef Ids<KIND> I;
   constexpr int NW = 16, F = G - 1, MF = (F + WS_NL - 1) / WS_NL;
@@ -723,55 +719,6 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     MLP_STAMP(0);
   }
   if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
-  // ---- one 16-column output tile of layer 0 over all G k-groups (the dense
-  // group first, then the fields in arrival order), B fragments 3 groups
-  // ahead in r; `waits`: wait on the burst counters as the groups land
-  const floatx4* W0all = reinterpret_cast<const floatx4*>(t.prep + t.off[0]) + lane;
-  auto grp = [](int i) { return i == 0 ? G - 1 : i - 1; };
-  auto l0_fill = [&](int tile, floatx4 (&r)[3]) {
-    const floatx4* Wt = W0all + (int64_t)tile * G * 64;
-#pragma unroll
-    for (int u = 0; u < 3; ++u) r[u] = Wt[(int64_t)grp(u) * 64];
-  };
-  auto l0_tile = [&](int tile, floatx4 (&r)[3], bool waits) {
-    const floatx4* Wt = W0all + (int64_t)tile * G * 64;
-    const float* ap = tsm + s * RS + 4 * kk;
-    floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;  // chains (RS_OPT_MFMA_CHAINS): MFMA j into j & 1
-    const bool chains = t.chains != 0;
-    if (waits) lds_wait_ge(&cnt[0], a.DB);
-#pragma unroll
-    for (int i = 0; i < G; ++i) {
-      if (waits && i == 1) lds_wait_ge(&cnt[1], WS_NL);             // fields 0..15 in the tile
-      if (waits && i == 1 + 2 * WS_NL) lds_wait_ge(&cnt[2], WS_NL);  // fields 16..
-      const int u = i % 3;
-      const floatx4 av = *reinterpret_cast<const floatx4*>(ap + 16 * grp(i));
-      __builtin_amdgcn_sched_barrier(0);
-      if (chains) {
-        c0 = mfma16x16x4(av[0], r[u][0], c0);
-        c1 = mfma16x16x4(av[1], r[u][1], c1);
-        c0 = mfma16x16x4(av[2], r[u][2], c0);
-        c1 = mfma16x16x4(av[3], r[u][3], c1);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c0 = mfma16x16x4(av[j], r[u][j], c0);
-      }
-      const int nx = i + 3 < G ? i + 3 : G - 1;
-      r[u] = Wt[(int64_t)grp(nx) * 64];
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (chains) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) c0[i] += c1[i];
-    }
-    const float* bias = par + t.poff[0];
-    const float* alpha = bias + t.Np[0];
-    float* out = tsm + 16 * RS;  // layer 0 -> buf1
-#pragma unroll
-    for (int r2 = 0; r2 < 4; ++r2) {
-      const int row = 4 * kk + r2, col = 16 * tile + s;
-      out[row * RS + col] = mlp_act(c0[r2] + bias[col], t.act[0], alpha[col]);
-    }
-  };
   if (w < WS_NL) {
     // ================================ loader
     const int l = w;
@@ -848,9 +795,11 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
         }
       }
       lds_signal(&cnt[1 + burst]);
+      {
+        const MlpArgs& a = t;
+        MLP_STAMP(2 + burst);  // diagnostic hook: this loader's burst in
+      }
     }
-    floatx4 rl[3];
-    if constexpr (SHARE) l0_fill(WS_NL + l, rl);  // this loader's layer-0 tile, requested now
     if (__any(bad && valid) && lane == 0) flag_error(a.err);
     // FM: last-wave finish over the loaders' partial tiles (wave order)
     floatx4 acc = ac[0];
@@ -889,24 +838,13 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
         }
       }
     }
-    if constexpr (SHARE) {
-      lds_wait_ge(&cnt[0], a.DB);
-      lds_wait_ge(&cnt[2], WS_NL);  // every loader's rows are in the tile
-      l0_tile(WS_NL + l, rl, false);
-    }
-  } else if constexpr (SHARE) {
-    // ================================ layer 0 compute: one tile per wave
-    const int c8 = w - WS_NL;
-    floatx4 r0[3];
-    l0_fill(c8, r0);
-    __syncthreads();  // the counters start at 0
-    l0_tile(c8, r0, true);
   } else {
     // ================================ layer 0 compute
     const int c8 = w - WS_NL;
     const floatx4* W0 = reinterpret_cast<const floatx4*>(t.prep + t.off[0]) + lane + (int64_t)c8 * G * 64;
     const floatx4* W1 = W0 + (int64_t)WS_NL * G * 64;  // output tile c8 + 8
     // k-group order: the dense group (G - 1) first, then fields 0 .. F-1
+    auto grp = [](int i) { return i == 0 ? G - 1 : i - 1; };
     floatx4 r0[3], r1[3];
 #pragma unroll
     for (int u = 0; u < 3; ++u) {
@@ -922,8 +860,16 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     lds_wait_ge(&cnt[0], a.DB);
 #pragma unroll
     for (int i = 0; i < G; ++i) {
-      if (i == 1) lds_wait_ge(&cnt[1], WS_NL);       // fields 0..15 in the tile
-      if (i == 1 + 2 * WS_NL) lds_wait_ge(&cnt[2], WS_NL);  // fields 16..
+      if (i == 1) {
+        lds_wait_ge(&cnt[1], WS_NL);  // fields 0..15 in the tile
+        const MlpArgs& a = t;
+        MLP_STAMP(2);  // diagnostic hook: burst 0 seen
+      }
+      if (i == 1 + 2 * WS_NL) {
+        lds_wait_ge(&cnt[2], WS_NL);  // fields 16..
+        const MlpArgs& a = t;
+        MLP_STAMP(3);  // burst 1 seen
+      }
       const int u = i % 3;
       const floatx4 av = *reinterpret_cast<const floatx4*>(ap + 16 * grp(i));
       __builtin_amdgcn_sched_barrier(0);
@@ -1820,7 +1766,7 @@ static bool deepfm_geom(int nd, int n_fields, int k, int kfm, int n_layers, cons
 static bool deepfm_ws_ok(const EmbedFmArgs& a, const MlpArgs& t, const FieldMeta* hm, int KV) {
   return hm && KV == 4 && a.F == 26 && a.nd >= 13 && a.nd <= 16 && a.DB == 4 && t.L >= 2 &&
          t.Np[0] == 256 && t.Kp[0] == 16 * (a.F + 1) && (t.Np[1] >> 4) >= WS_NL &&
-         opt(RS_OPT_DEEPFM_KERNEL) != 1;
+         opt(RS_OPT_DEEPFM_KERNEL) == 0;
 }
 
 template <int KV, int KIND>
@@ -1829,14 +1775,9 @@ static void launch_deepfm(const EmbedFmArgs& a, const MlpArgs& t, size_t lds, hi
   const unsigned grid = (unsigned)((a.batch + 15) / 16);
   if constexpr (KV == 4) {
     if (deepfm_ws_ok(a, t, hm, KV)) {
-      static LdsAttr ws_set[2];
-      if (opt(RS_OPT_DEEPFM_KERNEL) == 2) {
-        lds_attr(ws_set[1], (const void*)deepfm_ws<KIND, 27, true>, lds);
-        deepfm_ws<KIND, 27, true><<<grid, 16 * 64, lds, st>>>(a, t, *hm);
-      } else {
-        lds_attr(ws_set[0], (const void*)deepfm_ws<KIND, 27, false>, lds);
-        deepfm_ws<KIND, 27, false><<<grid, 16 * 64, lds, st>>>(a, t, *hm);
-      }
+      static LdsAttr ws_set;
+      lds_attr(ws_set, (const void*)deepfm_ws<KIND, 27>, lds);
+      deepfm_ws<KIND, 27><<<grid, 16 * 64, lds, st>>>(a, t, *hm);
       return;
     }
   }

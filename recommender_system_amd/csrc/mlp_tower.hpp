@@ -239,7 +239,15 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
 
   float* in = (l0 & 1) ? smem + 16 * RS : smem;
   float* out = (l0 & 1) ? smem : smem + 16 * RS;
-  for (int l = l0; l < a.L; ++l) {
+  // A one-unit head after a layer that keeps whole columns per wave folds into
+  // that layer's epilogue: each wave dots its 16 activation columns with the
+  // head weights (a DPP row sum per sample) into red, and after one barrier
+  // 16 threads add the tiles' partials in tile order — no head layer of its
+  // own (ring fill, barrier, K-split reduction).
+  const int LH = a.L - 1;
+  const bool fhead = LH - 1 >= l0 && a.N[LH] == 1 && mlp_slices(a.Np[LH - 1] >> 4, a.Kp[LH - 1] >> 4, NW) == 1;
+  const int Lrun = fhead ? LH : a.L;
+  for (int l = l0; l < Lrun; ++l) {
     const int T = a.Np[l] >> 4, G = a.Kp[l] >> 4;
     const int S = mlp_slices(T, G, NW);
     __syncthreads();
@@ -271,13 +279,27 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
     };
 
     const float* ap = in + (lane & 15) * RS + 4 * (lane >> 4);
+    const bool head_here = fhead && l == LH - 1;
     for (int item = w; item < T * S; item += NW) {
       const MlpItem it = mlp_item(item, T, G, S);
       const floatx4* bp = W + (int64_t)it.t * G * 64;
       if (item != w) mlp_ring_fill(ring, bp, it.g0, it.g1);
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
       mlp_mac(ring, ap, bp, it.g0, it.g1, acc, a.unroll, a.chains);
-      if (S == 1) {
+      if (head_here) {
+        // head weight of this lane's column k: the packed head layer holds
+        // W[k][0] at lane 16 ((k & 15) >> 2), element k & 3, of k-group k >> 4
+        const int col = 16 * it.t + (lane & 15);
+        const float hw = col < Nl ? a.prep[a.off[LH] + ((int64_t)(col >> 4) * 64 + 16 * ((col & 15) >> 2)) * 4 +
+                                           (col & 3)]
+                                  : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float p = col < Nl ? mlp_act(acc[r] + bias[col], act, alpha[col]) * hw : 0.f;
+          p = row16_sum(p);
+          if ((lane & 15) == 0) red[it.t * 16 + 4 * (lane >> 4) + r] = p;
+        }
+      } else if (S == 1) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) finish(4 * (lane >> 4) + r, 16 * it.t + (lane & 15), acc[r]);
       } else {
@@ -308,6 +330,28 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
     float* tmp = in;
     in = out;
     out = tmp;
+  }
+  if (fhead) {
+    __syncthreads();
+    MLP_STAMP(2 + 2 * LH);
+    if (threadIdx.x < 16) {
+      const int row = threadIdx.x, T = a.Np[LH - 1] >> 4;
+      float z = 0.f;
+      for (int t = 0; t < T; ++t) z += red[t * 16 + row];
+      const float* hb = par + a.poff[LH];
+      float v = mlp_act(z + hb[0], a.act[LH], hb[a.Np[LH]]);
+      const int64_t m = m0 + row;
+      if (m < a.M) {
+        if (a.head == 0) {
+          a.y[m * a.ys] = v;
+        } else {
+          float zz = a.c0 * v;
+          if (extra_lds) zz = zz + a.c1 * extra_lds[row];
+          else if (a.extra) zz = zz + a.c1 * a.extra[m];
+          a.y[m * a.ys] = 1.0f / (1.0f + expf(-zz));
+        }
+      }
+    }
   }
   MLP_STAMP(15);
 }

@@ -52,16 +52,25 @@ def main():
     for l in range(4):
         names[2 + 2 * l] = f"l{l}_start"
         names[3 + 2 * l] = f"l{l}_mac_done"
+    if int(os.environ.get("DIAG_DEEPFM_OPT", "1")) == 0:  # split roles: slots 2 / 3 = burst 0 / 1 in
+        names[2], names[3] = "burst0_in", "burst1_in"
     names[15] = "end"
     out = {"B": B, "V": V, "deepfm_kernel_option": int(os.environ.get("DIAG_DEEPFM_OPT", "1")),
            "mfma_chains": int(os.environ.get("DIAG_CHAINS", "0")), "phases_cycles": {}}
     for j, n in names.items():
         rel = d[:, :, j] - t0
-        out["phases_cycles"][n] = {"median_wave": int(np.median(rel)), "slowest_wave": int(np.median(rel.max(axis=1)))}
-    kstart = d[:, :, 0].min()
+        ok = d[:, :, j] > 0  # waves that wrote this slot
+        if not ok.any():
+            continue
+        relm = np.where(ok, rel, np.nan)
+        out["phases_cycles"][n] = {"median_wave": int(np.nanmedian(relm)),
+                                   "slowest_wave": int(np.nanmedian(np.nanmax(relm, axis=1))),
+                                   "loaders_median": int(np.nanmedian(relm[:, :8])) if ok[:, :8].any() else None,
+                                   "compute_median": int(np.nanmedian(relm[:, 8:])) if ok[:, 8:].any() else None}
+    st0 = np.where(d[:, :, 0] > 0, d[:, :, 0], np.iinfo(np.int64).max).min(axis=1)  # per-WG first stamp
+    kstart = st0.min()
     out["kernel_span_cycles"] = int(d[:, :, 15].max() - kstart)
-    out["wg_start_spread_cycles"] = [int(np.percentile(d[:, :, 0].min(axis=1) - kstart, 50)),
-                                     int((d[:, :, 0].min(axis=1) - kstart).max())]
+    out["wg_start_spread_cycles"] = [int(np.percentile(st0 - kstart, 50)), int((st0 - kstart).max())]
     print(json.dumps(out))
 
 

@@ -915,15 +915,14 @@ def test_hm_front_end_bit_identical(gpu, F, B, id_dtype):
 
 
 # --------------------------- fused DeepFM kernel forms (RS_OPT_DEEPFM_KERNEL)
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("B,id_dtype,hidden,nd", [(4096, np.int32, [256, 128, 64], 13), (4093, np.int64, [248, 160, 8], 13),
                                                   (33, np.float32, [256, 128], 16), (1, np.int32, [256, 128, 64], 13),
                                                   (300, np.int32, [256, 128, 64], 9)])
 def test_deepfm_kernel_forms(gpu, variant, B, id_dtype, hidden, nd):
     """rs_deepfm_fwd_hm in its forms — 0: split wave roles (loader waves
     gather the rows and the FM while compute waves run the first layer as the
-    fields land; the Criteo shape), 1: one role per wave, 2: split roles with
-    the loaders taking half of the first layer after the gather — == the fp64
+    fields land; the Criteo shape), 1: one role per wave — == the fp64
     oracle (post-sigmoid 1e-5 relative), the FM logit output too, and an
     out-of-range id raises.  Shapes outside the split form's (nd 9 here) run
     the one-role kernel under both values."""
@@ -992,7 +991,7 @@ def test_mfma_chains_match(gpu, B, hidden):
     try:
         for ch in (0, 1):
             _lib.set_option(_lib.OPT_MFMA_CHAINS, ch)
-            for form in (0, 1, 2):
+            for form in (0, 1):
                 _lib.set_option(_lib.OPT_DEEPFM_KERNEL, form)
                 fm = torch.empty(B, 1, device=gpu)
                 outs[("deepfm", form, ch)] = dfm.forward_fused((dense, ids), fm_logit=fm).clone()
@@ -1009,7 +1008,7 @@ def test_mfma_chains_match(gpu, B, hidden):
     p = {"tables": tables_of(dfm.embed_layer), "w0": dfm.fm.w0.cpu().numpy(), "w1": dfm.fm.w1.cpu().numpy(),
          "v": dfm.fm.v.cpu().numpy(), "dnn_hidden": hidden_p, "dnn_out": out_p}
     ref, ref_fm, _ = O.deepfm(None, p, nd=13, inputs=(dense_np, ids_np))
-    for form in (0, 1, 2):
+    for form in (0, 1):
         assert_rel_close(outs[("deepfm", form, 1)], ref, what=f"deepfm form {form}, four chains")
         assert_scaled_close(outs[("fm", form, 1)], ref_fm, what=f"deepfm form {form} fm logit, four chains")
     assert_scaled_close(outs[("fm_logit", 1)], outs[("fm_logit", 0)].cpu().numpy(), what="fm logit")
