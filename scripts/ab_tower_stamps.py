@@ -70,8 +70,8 @@ def main():
         # taken within each XCD (workgroup i runs on XCD i mod 8)
         xcd = np.arange(nwg) % 8
         start = np.empty(nwg)
-        for x in range(8):
-            sel = xcd == x
+        for xc in range(8):
+            sel = xcd == xc
             start[sel] = t0[sel] - np.nanmin(t0[sel])
         dur = np.nanmax(d[:, :, 15], axis=1) - t0
         pct = lambda v: [int(np.nanpercentile(v, q)) for q in (0, 50, 90, 100)]
