@@ -160,9 +160,12 @@ __device__ __forceinline__ void cross_contract(const CrossArgs& a, const float* 
 }
 
 // Phases (2)-(4) on a staged 16 x d tile of x0 (rows >= `rows` zero).
+// beta: beta_L (a.beta, or its LDS copy when the caller staged one).
 template <int NT, int NW>
 __device__ __forceinline__ void cross_tile(const CrossArgs& a, float* tile, float* cs, float* alpha, int64_t b0,
-                                           int rows, const CrossB<NT, NW>* pre = nullptr) {
+                                           int rows, const CrossB<NT, NW>* pre = nullptr,
+                                           const float* beta = nullptr) {
+  if (!beta) beta = a.beta;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int s = lane & 15, kk = lane >> 4;
@@ -190,27 +193,39 @@ __device__ __forceinline__ void cross_tile(const CrossArgs& a, float* tile, floa
   }
   __syncthreads();
 
-  // (4) out = alpha * x0 + beta_L: float4 stores over the contiguous block
-  // (row/column tracked incrementally, no per-element division)
-  if (a.out_stride == a.d && ((uintptr_t)(a.out + b0 * a.d) % 16 == 0) && (a.d % 4 == 0)) {
+  // (4) out = alpha * x0 + beta_L.  The workgroup's rows are one contiguous
+  // block when out_stride == d (16-B aligned: b0 is a multiple of 16): float4
+  // stores over it, a chunk's four elements may straddle two rows (row /
+  // column tracked incrementally, no per-element division); scalar stores
+  // are issue-bound (~4 B/clk/CU), so they only take the strided case.
+  if (a.out_stride == a.d && ((uintptr_t)(a.out + b0 * a.d) % 16 == 0)) {
     floatx4* dst = reinterpret_cast<floatx4*>(a.out + b0 * a.d);
     const int n4 = n / 4;
     const int step = 4 * NW * 64, dq = step / a.d, dr = step - dq * a.d;
     int i = threadIdx.x, r = (4 * i) / a.d, j = 4 * i - r * a.d;
     for (; i < n4; i += NW * 64) {
-      const floatx4 x = reinterpret_cast<const floatx4*>(tile)[i];
-      const float al = alpha[r];
-      dst[i] = floatx4{fmaf(al, x[0], a.beta[j]), fmaf(al, x[1], a.beta[j + 1]), fmaf(al, x[2], a.beta[j + 2]),
-                       fmaf(al, x[3], a.beta[j + 3])};
+      const floatx4 x = reinterpret_cast<const floatx4*>(tile)[i];  // tile rows are d apart too
+      floatx4 v;
+      int rr = r, jj = j;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[q] = fmaf(alpha[rr], x[q], beta[jj]);
+        if (++jj == a.d) { jj = 0; ++rr; }
+      }
+      dst[i] = v;
       r += dq;
       j += dr;
       if (j >= a.d) { j -= a.d; ++r; }
+    }
+    for (int e = n4 * 4 + threadIdx.x; e < n; e += NW * 64) {  // a ragged last tile's tail
+      const int rr = e / a.d, jj = e - rr * a.d;
+      a.out[b0 * a.d + e] = fmaf(alpha[rr], tile[e], beta[jj]);
     }
   } else {
     for (int r = 0; r < rows; ++r) {
       float* orow = a.out + (b0 + r) * a.out_stride;
       const float al = alpha[r];
-      for (int j = threadIdx.x; j < a.d; j += NW * 64) orow[j] = fmaf(al, tile[r * a.d + j], a.beta[j]);
+      for (int j = threadIdx.x; j < a.d; j += NW * 64) orow[j] = fmaf(al, tile[r * a.d + j], beta[j]);
     }
   }
 }
@@ -291,6 +306,10 @@ __device__ __forceinline__ void embed_cross_body(const CrossArgs& a, const Embed
   if constexpr (KA) {
     CrossB<NT, NW> pre;  // the contraction's first B fragments ride the gather's trips
     pre.load(a, w);
+    // beta_L (sample-independent) rides them too: registers now, LDS after the gather
+    float* betal = alpha + 16;
+    const float bv0 = tid < a.d ? a.beta[tid] : 0.f;
+    const float bv1 = tid + NW * 64 < a.d ? a.beta[tid + NW * 64] : 0.f;
     {  // dense columns (wave w: sample w), requested beside the ids
       const int64_t bb = b0 + (w < rows ? w : rows - 1);
       for (int j = lane; j < e.nd; j += 64) tile[w * a.d + j] = w < rows ? e.dense[bb * e.dense_stride + j] : 0.f;
@@ -304,8 +323,10 @@ __device__ __forceinline__ void embed_cross_body(const CrossArgs& a, const Embed
                                                  p[3] = x[3];
                                                });
     if (__any(bad) && lane == 0) flag_error(e.err);
+    if (tid < a.d) betal[tid] = bv0;
+    if (tid + NW * 64 < a.d) betal[tid + NW * 64] = bv1;
     __syncthreads();
-    cross_tile<NT, NW>(a, tile, cs, alpha, b0, rows, &pre);
+    cross_tile<NT, NW>(a, tile, cs, alpha, b0, rows, &pre, a.d <= 2 * NW * 64 ? betal : a.beta);
     return;
   } else {
   __shared__ typename I::raw_t lid[16][EC_FMAX];
@@ -598,7 +619,9 @@ static int embed_cross_run(const void* ids, int id_kind, int64_t id_stride, cons
               opt(RS_OPT_MFMA_CHAINS)};
   EmbedCrossArgs e{ids, id_stride, dense, dense_stride, nd, n_fields, k, table, field_offsets, field_vocab, err_flag};
   constexpr int NW = 16;
-  const size_t lds = (size_t)(((16 * d + 3) / 4) * 4 + NW * 16 * (g.NT * 16 + 1) + 16) * sizeof(float);
+  // tile | contraction partials | alpha[16] | beta_L copy (the kernarg front end)
+  const size_t lds =
+      (size_t)(((16 * d + 3) / 4) * 4 + NW * 16 * (g.NT * 16 + 1) + 16 + ((d + 3) / 4) * 4) * sizeof(float);
   const unsigned grid = (unsigned)((batch + 15) / 16);
   hipStream_t st = as_stream(stream);
   with_id_kind(id_kind, [&](auto K) {
