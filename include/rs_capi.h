@@ -107,6 +107,9 @@ int rs_diag_wave_slots(int grid, int block, int lds_bytes, uint32_t* out, rs_str
  * (1, 2, 4) independent accumulation chains; cyc[wave] = s_memtime cycles. */
 int rs_diag_mfma_chain(int grid, int block, int n, int chains, unsigned long long* cyc, float* sink,
                        rs_stream_t stream);
+/* rs_diag_icache: 2048 FMAs per wave as a loop (unroll 0) or straight-line
+ * code (unroll 1), run twice in one launch; cyc[2 wave + pass] = cycles.     */
+int rs_diag_icache(int grid, int block, int unroll, unsigned long long* cyc, float* sink, rs_stream_t stream);
 
 /* --------------------------------------------------------- embedding (a3)
  * Replaces EmbedLayer.call (layer/core.py:273-280) + the dense/sparse concat of

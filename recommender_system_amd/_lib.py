@@ -31,6 +31,7 @@ SIGNATURES = {
     "rs_diag_empty": (I, [I, I, P]),
     "rs_diag_wave_slots": (I, [I, I, I, P, P]),
     "rs_diag_mfma_chain": (I, [I, I, I, I, P, P, P]),
+    "rs_diag_icache": (I, [I, I, I, P, P, P]),
     "rs_embed_gather": (I, [P, I, L, P, L, I, P, P, P, I, I, P, L, L, P, P]),
     "rs_fm_prepared_size": (L, [I, I, I, I]),
     "rs_fm_prepare": (I, [P, P, I, I, I, I, P, P]),

@@ -47,7 +47,54 @@ __global__ void diag_mfma_chain_kernel(int n, int chains, unsigned long long* cy
   sink[blockIdx.x * blockDim.x + threadIdx.x] = r;
   if (lane == 0) cyc[blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)] = t1 - t0;
 }
+
+// Instruction-fetch cost: 2048 FMAs on 8 independent accumulators as a loop
+// (8 per iteration, the body stays in the instruction cache) or straight-line
+// (fully unrolled, ~8 KB of code); cyc[wave] = {first pass, second pass} of
+// the same code in one launch.
+template <bool UNROLL>
+__global__ void diag_icache_kernel(float x, float y, unsigned long long* cyc, float* sink) {
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = x + i;
+  unsigned long long t[3];
+  for (int pass = 0; pass < 2; ++pass) {
+    t[pass] = __builtin_amdgcn_s_memtime();
+    if constexpr (UNROLL) {
+#pragma unroll
+      for (int i = 0; i < 2048; ++i) acc[i & 7] = fmaf(acc[i & 7], x, y);
+    } else {
+#pragma unroll 1
+      for (int i = 0; i < 2048; i += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = fmaf(acc[j], x, y);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  t[2] = __builtin_amdgcn_s_memtime();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r += acc[i];
+  sink[blockIdx.x * blockDim.x + threadIdx.x] = r;
+  if ((threadIdx.x & 63) == 0) {
+    const int64_t wv = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    cyc[2 * wv] = t[1] - t[0];
+    cyc[2 * wv + 1] = t[2] - t[1];
+  }
+}
 }  // namespace rs
+
+extern "C" int rs_diag_icache(int grid, int block, int unroll, unsigned long long* cyc, float* sink,
+                              rs_stream_t stream) {
+  if (grid < 1 || block < 64 || block > 1024 || block % 64 || !cyc || !sink) {
+    rs::set_error("rs_diag_icache: bad arguments");
+    return RS_ERR_ARG;
+  }
+  if (unroll) rs::diag_icache_kernel<true><<<grid, block, 0, (hipStream_t)stream>>>(1.0001f, 1e-4f, cyc, sink);
+  else rs::diag_icache_kernel<false><<<grid, block, 0, (hipStream_t)stream>>>(1.0001f, 1e-4f, cyc, sink);
+  return rs::launch_status("rs_diag_icache");
+}
 
 extern "C" int rs_diag_mfma_chain(int grid, int block, int n, int chains, unsigned long long* cyc, float* sink,
                                   rs_stream_t stream) {

@@ -31,6 +31,7 @@ lib.rs_diag_inner_set_dbg(None)
 d = dbg.cpu().numpy().reshape(-1, 16, 8)
 d = d[d[:, :, 0].min(axis=1) > 0]
 t0 = d[:, :, 0].min(axis=1, keepdims=True)
-rel = d[:, :, :5] - t0[:, :, None]
-for j, n in enumerate(["start", "rows_in_lds", "after_barrier", "gram_done", "end"]):
+rel = d[:, :, :6] - t0[:, :, None]
+for j, n in [(0, "start"), (1, "rows_in_lds"), (2, "after_barrier"), (5, "wave_gram_done"), (3, "gram_done"),
+             (4, "end")]:
     print(f"{n:14s} {int(np.median(rel[:, :, j])):8d} {int(np.median(rel[:, :, j].max(axis=1))):8d}")
