@@ -23,6 +23,8 @@
 //     logit = (x@w1 + w0) + 0.5*(sum_f s_f^2 - sum_i x_i^2 |v_i|^2).
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "embed_fm.hpp"
 #include "mlp_tower.hpp"
 #include "rs_common.hpp"
@@ -858,19 +860,9 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc0b = acc0, acc1b = acc0;
     const bool chains = t.chains != 0;
     lds_wait_ge(&cnt[0], a.DB);
-#pragma unroll
-    for (int i = 0; i < G; ++i) {
-      if (i == 1) {
-        lds_wait_ge(&cnt[1], WS_NL);  // fields 0..15 in the tile
-        const MlpArgs& a = t;
-        MLP_STAMP(2);  // diagnostic hook: burst 0 seen
-      }
-      if (i == 1 + 2 * WS_NL) {
-        lds_wait_ge(&cnt[2], WS_NL);  // fields 16..
-        const MlpArgs& a = t;
-        MLP_STAMP(3);  // burst 1 seen
-      }
-      const int u = i % 3;
+    // one k-group: MFMAs of ring slot U, then the slot refilled 3 groups ahead
+    auto step = [&](int i, auto U) {
+      constexpr int u = decltype(U)::value;
       const floatx4 av = *reinterpret_cast<const floatx4*>(ap + 16 * grp(i));
       __builtin_amdgcn_sched_barrier(0);
       if (chains) {
@@ -892,6 +884,49 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
       r0[u] = W0[(int64_t)grp(nx) * 64];
       r1[u] = W1[(int64_t)grp(nx) * 64];
       __builtin_amdgcn_sched_barrier(0);
+    };
+    using U0 = std::integral_constant<int, 0>;
+    using U1 = std::integral_constant<int, 1>;
+    using U2 = std::integral_constant<int, 2>;
+    auto wait_burst = [&](int which) {
+      lds_wait_ge(&cnt[1 + which], WS_NL);  // fields 0..15 / 16.. in the tile
+      const MlpArgs& a = t;
+      MLP_STAMP(2 + which);  // diagnostic hook: burst seen
+    };
+    constexpr int B1 = 1 + 2 * WS_NL;  // first group of the second burst
+    if (t.unroll) {
+      // straight-line (RS_OPT_MLP_UNROLL 1)
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        if (i == 1) wait_burst(0);
+        if (i == B1) wait_burst(1);
+        if (i % 3 == 0) step(i, U0{});
+        else if (i % 3 == 1) step(i, U1{});
+        else step(i, U2{});
+      }
+    } else {
+      // compact loops (three groups a trip, ring slots fixed per position):
+      // straight-line code of this length runs at instruction-fetch speed
+      // (every 64-B line a miss, the cache is cold each launch: DESIGN 10)
+      static_assert((B1 - 2) % 3 == 0 && (G - 1 - B1) % 3 == 0, "deepfm_ws: group / ring phase");
+      step(0, U0{});
+      wait_burst(0);
+      int i = 1;
+#pragma unroll 1
+      for (; i + 2 < B1; i += 3) {
+        step(i, U1{});
+        step(i + 1, U2{});
+        step(i + 2, U0{});
+      }
+      step(i, U1{});  // i = B1 - 1
+      wait_burst(1);
+#pragma unroll 1
+      for (i = B1; i + 2 < G; i += 3) {
+        step(i, U2{});
+        step(i + 1, U0{});
+        step(i + 2, U1{});
+      }
+      step(i, U2{});  // i = G - 1
     }
     if (chains) {
 #pragma unroll

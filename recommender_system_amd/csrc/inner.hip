@@ -376,6 +376,7 @@ __device__ __forceinline__ void inner_fast_body(const InnerArgs& a, const FieldM
       pair(wb, p + IP_NW);
     }
   }
+  IP_STAMP(5);  // this wave's Gram / outer pairs done (before the barrier)
   __syncthreads();
   IP_STAMP(3);
   // coalesced output rows [flat F*K | inner P | outer P]

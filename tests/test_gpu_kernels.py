@@ -919,7 +919,7 @@ def test_hm_front_end_bit_identical(gpu, F, B, id_dtype):
 @pytest.mark.parametrize("B,id_dtype,hidden,nd", [(4096, np.int32, [256, 128, 64], 13), (4093, np.int64, [248, 160, 8], 13),
                                                   (33, np.float32, [256, 128], 16), (1, np.int32, [256, 128, 64], 13),
                                                   (300, np.int32, [256, 128, 64], 9)])
-def test_deepfm_kernel_forms(gpu, variant, B, id_dtype, hidden, nd):
+def test_deepfm_kernel_forms(gpu, mlp_unroll, variant, B, id_dtype, hidden, nd):
     """rs_deepfm_fwd_hm in its forms — 0: split wave roles (loader waves
     gather the rows and the FM while compute waves run the first layer as the
     fields land; the Criteo shape), 1: one role per wave — == the fp64
