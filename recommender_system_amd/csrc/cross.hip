@@ -81,8 +81,15 @@ struct CrossArgs {
   float* out;
   int64_t out_stride;
   int64_t batch;
-  int chains;  // RS_OPT_MFMA_CHAINS at launch
+  int chains;               // RS_OPT_MFMA_CHAINS at launch
+  unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_cross_set_dbg)
 };
+static unsigned long long* g_cross_dbg = nullptr;  // rs_diag_cross_set_dbg
+#define CR_STAMP(i)                                                                                   \
+  do {                                                                                                \
+    if (a.dbg && (threadIdx.x & 63) == 0)                                                             \
+      a.dbg[((int64_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 
 // The B fragments of 8 of a wave's k-steps (t0, t0 + NW, ..): L2-resident
 // launch constants, so the fused kernels request the first 8 before their
@@ -178,7 +185,9 @@ __device__ __forceinline__ void cross_tile(const CrossArgs& a, float* tile, floa
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) cs[(w * 16 + kk * 4 + r) * CW + nt * 16 + s] = acc[nt][r];
+  CR_STAMP(3);
   __syncthreads();
+  CR_STAMP(4);
 
   // (3) per-sample recurrence alpha_{l+1} = alpha_l (1 + g_l) + h_l
   if (threadIdx.x < 16) {
@@ -192,6 +201,7 @@ __device__ __forceinline__ void cross_tile(const CrossArgs& a, float* tile, floa
     alpha[threadIdx.x] = al;
   }
   __syncthreads();
+  CR_STAMP(5);
 
   // (4) out = alpha * x0 + beta_L.  The workgroup's rows are one contiguous
   // block when out_stride == d (16-B aligned: b0 is a multiple of 16): float4
@@ -228,6 +238,7 @@ __device__ __forceinline__ void cross_tile(const CrossArgs& a, float* tile, floa
       for (int j = threadIdx.x; j < a.d; j += NW * 64) orow[j] = fmaf(al, tile[r * a.d + j], beta[j]);
     }
   }
+  CR_STAMP(6);
 }
 
 template <int NT, int NW>
@@ -304,6 +315,7 @@ __device__ __forceinline__ void embed_cross_body(const CrossArgs& a, const Embed
   const int rows = (int)((a.batch - b0) < 16 ? (a.batch - b0) : 16);
   const int F = e.F;
   if constexpr (KA) {
+    CR_STAMP(0);
     CrossB<NT, NW> pre;  // the contraction's first B fragments ride the gather's trips
     pre.load(a, w);
     // beta_L (sample-independent) rides them too: registers now, LDS after the gather
@@ -325,7 +337,9 @@ __device__ __forceinline__ void embed_cross_body(const CrossArgs& a, const Embed
     if (__any(bad) && lane == 0) flag_error(e.err);
     if (tid < a.d) betal[tid] = bv0;
     if (tid + NW * 64 < a.d) betal[tid + NW * 64] = bv1;
+    CR_STAMP(1);
     __syncthreads();
+    CR_STAMP(2);
     cross_tile<NT, NW>(a, tile, cs, alpha, b0, rows, &pre, a.d <= 2 * NW * 64 ? betal : a.beta);
     return;
   } else {
@@ -570,7 +584,7 @@ extern "C" int rs_cross_fwd(const float* x0, int64_t x_stride, int d, int n_laye
   const int L = n_layers;
   const CrossGeom g = cross_geom(d, L < 1 ? 1 : L);
   CrossArgs a{x0, x_stride, d, L, g.DB, prepared, prepared + g.h_off, prepared + g.beta_off, out, out_stride, batch,
-              opt(RS_OPT_MFMA_CHAINS)};
+              opt(RS_OPT_MFMA_CHAINS), g_cross_dbg};
   constexpr int NW = 8;
   const size_t lds = (size_t)(((16 * d + 3) / 4) * 4 + NW * 16 * (g.NT * 16 + 1) + 16) * sizeof(float);
   const unsigned grid = (unsigned)((batch + 15) / 16);
@@ -616,7 +630,7 @@ static int embed_cross_run(const void* ids, int id_kind, int64_t id_stride, cons
   const int L = n_layers;
   const CrossGeom g = cross_geom(d, L < 1 ? 1 : L);
   CrossArgs a{nullptr, d, d, L, g.DB, prepared, prepared + g.h_off, prepared + g.beta_off, out, out_stride, batch,
-              opt(RS_OPT_MFMA_CHAINS)};
+              opt(RS_OPT_MFMA_CHAINS), g_cross_dbg};
   EmbedCrossArgs e{ids, id_stride, dense, dense_stride, nd, n_fields, k, table, field_offsets, field_vocab, err_flag};
   constexpr int NW = 16;
   // tile | contraction partials | alpha[16] | beta_L copy (the kernarg front end)
@@ -712,7 +726,7 @@ static int dcn_run(const void* ids, int id_kind, int64_t id_stride, const float*
   const int d = nd + n_fields * k, Lx = n_cross + 1;  // + the output Dense's cross column
   const CrossGeom g = cross_geom(d, Lx);
   CrossArgs a{nullptr, d, d, Lx, g.DB, cross_prepared, cross_prepared + g.h_off, cross_prepared + g.beta_off,
-              nullptr, 0, batch, opt(RS_OPT_MFMA_CHAINS)};
+              nullptr, 0, batch, opt(RS_OPT_MFMA_CHAINS), g_cross_dbg};
   EmbedCrossArgs e{ids, id_stride, dense, dense_stride, nd, n_fields, k, table, field_offsets, field_vocab, err_flag};
   const size_t lds = mg.lds;
   const unsigned grid = (unsigned)((batch + 15) / 16);
@@ -764,3 +778,6 @@ extern "C" int rs_dcn_fwd_hm(const void* ids, int id_kind, int64_t id_stride, co
                  n_cross, cross_prepared, n_layers, dims, acts, mlp_prepared, out, batch, err_flag, stream,
                  host_meta(m, field_offsets_host, field_vocab_host, n_fields, k));
 }
+
+// diagnostics only: per-wave phase stamps of the CrossNet kernels (null = off)
+extern "C" void rs_diag_cross_set_dbg(unsigned long long* p) { rs::g_cross_dbg = p; }
