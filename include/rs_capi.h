@@ -77,13 +77,7 @@ enum rs_option {
                                  first layer): 0 (the default) = split wave roles (loaders +
                                  layer-0 compute waves, deepfm_ws), 1 = one role per wave (gather
                                  + FM, then the tower).  See DESIGN.md 4.5                       */
-  RS_OPT_MFMA_CHAINS = 3,     /* accumulation chains of the fp32 MFMA contractions (the fused
-                                 towers, the FM logit / DeepFM gather kernels, the CrossNet
-                                 contraction): 0 = one per output tile, 1 (the default) = four
-                                 independent chains per tile summed at the end (a dependent
-                                 v_mfma_f32_16x16x4_f32 waits ~100 cycles on its predecessor;
-                                 DESIGN.md 4.5).  Results differ from 0 in fp32 rounding only.  */
-  RS_OPT_COUNT = 4
+  RS_OPT_COUNT = 3
 };
 
 /* ------------------------------------------------------------------ meta */

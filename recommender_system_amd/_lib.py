@@ -155,7 +155,6 @@ FLAG_BAD_ID, FLAG_LAYOUT = 1, 2  # rs_flag bits of the device error flag
 OPT_EMBED_FM_KERNEL = 0  # rs_option
 OPT_MLP_UNROLL = 1
 OPT_DEEPFM_KERNEL = 2
-OPT_MFMA_CHAINS = 3
 ACT = {None: 0, "linear": 0, "relu": 1, "prelu": 2, "sigmoid": 3}
 
 _lock = threading.Lock()

@@ -81,7 +81,6 @@ struct CrossArgs {
   float* out;
   int64_t out_stride;
   int64_t batch;
-  int chains;               // RS_OPT_MFMA_CHAINS at launch
   unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_cross_set_dbg)
 };
 static unsigned long long* g_cross_dbg = nullptr;  // rs_diag_cross_set_dbg
@@ -115,12 +114,12 @@ struct CrossB {
 // are `ld` floats apart, columns >= a.d read as 0.
 template <int NT, int NW>
 __device__ __forceinline__ void cross_contract(const CrossArgs& a, const float* tile, int ld,
-                                               const CrossB<NT, NW>* pre, floatx4 (&acc)[NT], int chains) {
+                                               const CrossB<NT, NW>* pre, floatx4 (&acc)[NT]) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int s = lane & 15, kk = lane >> 4;
-  // accumulation chains (RS_OPT_MFMA_CHAINS): k-step u into chain u & 3, or
-  // all into chain 0
+  // four accumulation chains: k-step u into chain u & 3 (compile-time, no
+  // per-MFMA branch on a runtime flag)
   floatx4 ac[NT][4];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
@@ -137,8 +136,7 @@ __device__ __forceinline__ void cross_contract(const CrossArgs& a, const float* 
     for (int u = 0; u < 8; ++u)
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        if (chains) ac[nt][u & 3] = mfma16x16x4(xv[u], B.v[u][nt], ac[nt][u & 3]);
-        else ac[nt][0] = mfma16x16x4(xv[u], B.v[u][nt], ac[nt][0]);
+        ac[nt][u & 3] = mfma16x16x4(xv[u], B.v[u][nt], ac[nt][u & 3]);
       }
   };
   if (w < a.DB) {
@@ -156,14 +154,9 @@ __device__ __forceinline__ void cross_contract(const CrossArgs& a, const float* 
     step(t0, B);
   }
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    if (chains) {
+  for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[nt][i] = (ac[nt][0][i] + ac[nt][1][i]) + (ac[nt][2][i] + ac[nt][3][i]);
-    } else {
-      acc[nt] = ac[nt][0];
-    }
-  }
+    for (int i = 0; i < 4; ++i) acc[nt][i] = (ac[nt][0][i] + ac[nt][1][i]) + (ac[nt][2][i] + ac[nt][3][i]);
 }
 
 // Phases (2)-(4) on a staged 16 x d tile of x0 (rows >= `rows` zero).
@@ -179,7 +172,7 @@ __device__ __forceinline__ void cross_tile(const CrossArgs& a, float* tile, floa
   const int n = rows * a.d;
   // (2) G = X0 @ W on MFMA
   floatx4 acc[NT];
-  cross_contract<NT, NW>(a, tile, a.d, pre, acc, a.chains);
+  cross_contract<NT, NW>(a, tile, a.d, pre, acc);
   constexpr int CW = NT * 16 + 1;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
@@ -514,7 +507,7 @@ __device__ __forceinline__ void dcn_fused_body(const CrossArgs& a, const EmbedCr
 
   // CrossNet contraction G = X0 @ [w_0 .. w_{L-1}, w_o[:d]] (a.L = L + 1 columns)
   floatx4 acc[NT];
-  cross_contract<NT, NW>(a, tsm, RS, KA ? &pre : nullptr, acc, a.chains);
+  cross_contract<NT, NW>(a, tsm, RS, KA ? &pre : nullptr, acc);
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -584,7 +577,7 @@ extern "C" int rs_cross_fwd(const float* x0, int64_t x_stride, int d, int n_laye
   const int L = n_layers;
   const CrossGeom g = cross_geom(d, L < 1 ? 1 : L);
   CrossArgs a{x0, x_stride, d, L, g.DB, prepared, prepared + g.h_off, prepared + g.beta_off, out, out_stride, batch,
-              opt(RS_OPT_MFMA_CHAINS), g_cross_dbg};
+              g_cross_dbg};
   constexpr int NW = 8;
   const size_t lds = (size_t)(((16 * d + 3) / 4) * 4 + NW * 16 * (g.NT * 16 + 1) + 16) * sizeof(float);
   const unsigned grid = (unsigned)((batch + 15) / 16);
@@ -630,7 +623,7 @@ static int embed_cross_run(const void* ids, int id_kind, int64_t id_stride, cons
   const int L = n_layers;
   const CrossGeom g = cross_geom(d, L < 1 ? 1 : L);
   CrossArgs a{nullptr, d, d, L, g.DB, prepared, prepared + g.h_off, prepared + g.beta_off, out, out_stride, batch,
-              opt(RS_OPT_MFMA_CHAINS), g_cross_dbg};
+              g_cross_dbg};
   EmbedCrossArgs e{ids, id_stride, dense, dense_stride, nd, n_fields, k, table, field_offsets, field_vocab, err_flag};
   constexpr int NW = 16;
   // tile | contraction partials | alpha[16] | beta_L copy (the kernarg front end)
@@ -726,7 +719,7 @@ static int dcn_run(const void* ids, int id_kind, int64_t id_stride, const float*
   const int d = nd + n_fields * k, Lx = n_cross + 1;  // + the output Dense's cross column
   const CrossGeom g = cross_geom(d, Lx);
   CrossArgs a{nullptr, d, d, Lx, g.DB, cross_prepared, cross_prepared + g.h_off, cross_prepared + g.beta_off,
-              nullptr, 0, batch, opt(RS_OPT_MFMA_CHAINS), g_cross_dbg};
+              nullptr, 0, batch, g_cross_dbg};
   EmbedCrossArgs e{ids, id_stride, dense, dense_stride, nd, n_fields, k, table, field_offsets, field_vocab, err_flag};
   const size_t lds = mg.lds;
   const unsigned grid = (unsigned)((batch + 15) / 16);

@@ -155,14 +155,15 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   // w0 is requested now, not behind the rows (a dependent load at the end)
   const float w0v = OWNER ? 0.f : a.w0[0];
 
-  // accumulation chains (RS_OPT_MFMA_CHAINS): MFMA tp of a field slot into
-  // chain tp & 3, or all into chain 0 (the one-chain form); summed below
+  // four accumulation chains: MFMA tp of a field slot into chain tp & 3,
+  // summed below.  Fixed at compile time: the runtime switch this replaced
+  // put a scalar branch beside every MFMA and cost 6.01 vs 5.74 us per
+  // headline launch (cold instruction cache, profiles/r4_ab_ka_chains_compile_time.json)
   floatx4 ac[NT][4];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int c = 0; c < 4; ++c) ac[nt][c] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const bool chains = a.chains != 0;
   float qn = 0.f;
   bool bad = false;
 
@@ -381,8 +382,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 #ifdef RS_DIAG_STAMPS
           if (a.ablate & 1) { ac[nt][0][0] += xv * P.bw[j][nt].v[tp]; continue; }
 #endif
-          if (chains) ac[nt][tp & 3] = mfma16x16x4(xv, P.bw[j][nt].v[tp], ac[nt][tp & 3]);
-          else ac[nt][0] = mfma16x16x4(xv, P.bw[j][nt].v[tp], ac[nt][0]);
+          ac[nt][tp & 3] = mfma16x16x4(xv, P.bw[j][nt].v[tp], ac[nt][tp & 3]);
         }
         qn = fmaf(xv * xv, P.nrm[j][tp], qn);
       }
@@ -487,14 +487,9 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   }
   floatx4 acc[NT];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    if (chains) {
+  for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[nt][i] = (ac[nt][0][i] + ac[nt][1][i]) + (ac[nt][2][i] + ac[nt][3][i]);
-    } else {
-      acc[nt] = ac[nt][0];
-    }
-  }
+    for (int i = 0; i < 4; ++i) acc[nt][i] = (ac[nt][0][i] + ac[nt][1][i]) + (ac[nt][2][i] + ac[nt][3][i]);
   RS_USE(acc[0][0]);
   RS_STAMP(3);
   if (__any(bad && valid) && lane == 0) flag_error(a.err);
@@ -748,10 +743,9 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     }
     for (int i = threadIdx.x; i < t.ptot; i += WS_NL * 64) par[i] = t.prep[t.wtot + i];
     __syncthreads();  // the counters start at 0 (the compute waves pass the same barrier)
-    floatx4 ac[4];  // accumulation chains (RS_OPT_MFMA_CHAINS; one chain: ac[0] only)
+    floatx4 ac[4];  // four accumulation chains (MFMA tp into chain tp)
 #pragma unroll
     for (int c = 0; c < 4; ++c) ac[c] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const bool chains = a.chains != 0;
     float qn = 0.f;
     if (has_dense) {  // the dense group of the tile: dense columns + the zero padding up to 16
       const int e = 4 * dw + kk;
@@ -790,8 +784,7 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
           *reinterpret_cast<floatx4*>(tsm + s * RS + c * 16 + 4 * kk) = x;
 #pragma unroll
           for (int tp = 0; tp < 4; ++tp) {
-            if (chains) ac[tp] = mfma16x16x4(x[tp], bw[p][tp], ac[tp]);
-            else ac[0] = mfma16x16x4(x[tp], bw[p][tp], ac[0]);
+            ac[tp] = mfma16x16x4(x[tp], bw[p][tp], ac[tp]);
             qn = fmaf(x[tp] * x[tp], nrm[p][tp], qn);
           }
         }
@@ -804,11 +797,9 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     }
     if (__any(bad && valid) && lane == 0) flag_error(a.err);
     // FM: last-wave finish over the loaders' partial tiles (wave order)
-    floatx4 acc = ac[0];
-    if (chains) {
+    floatx4 acc;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] = (ac[0][i] + ac[1][i]) + (ac[2][i] + ac[3][i]);
-    }
+    for (int i = 0; i < 4; ++i) acc[i] = (ac[0][i] + ac[1][i]) + (ac[2][i] + ac[3][i]);
     lf_acc[l][lane] = acc;
     qn += __shfl_xor(qn, 16);
     qn += __shfl_xor(qn, 32);
@@ -855,30 +846,20 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     }
     __syncthreads();  // the counters start at 0
     const float* ap = tsm + s * RS + 4 * kk;
-    // two output tiles; with RS_OPT_MFMA_CHAINS two chains each (MFMA j of a
-    // group into chain j & 1)
+    // two output tiles, two chains each (MFMA j of a group into chain j & 1)
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc0b = acc0, acc1b = acc0;
-    const bool chains = t.chains != 0;
     lds_wait_ge(&cnt[0], a.DB);
     // one k-group: MFMAs of ring slot U, then the slot refilled 3 groups ahead
     auto step = [&](int i, auto U) {
       constexpr int u = decltype(U)::value;
       const floatx4 av = *reinterpret_cast<const floatx4*>(ap + 16 * grp(i));
       __builtin_amdgcn_sched_barrier(0);
-      if (chains) {
 #pragma unroll
-        for (int j = 0; j < 4; j += 2) {
-          acc0 = mfma16x16x4(av[j], r0[u][j], acc0);
-          acc1 = mfma16x16x4(av[j], r1[u][j], acc1);
-          acc0b = mfma16x16x4(av[j + 1], r0[u][j + 1], acc0b);
-          acc1b = mfma16x16x4(av[j + 1], r1[u][j + 1], acc1b);
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc0 = mfma16x16x4(av[j], r0[u][j], acc0);
-          acc1 = mfma16x16x4(av[j], r1[u][j], acc1);
-        }
+      for (int j = 0; j < 4; j += 2) {
+        acc0 = mfma16x16x4(av[j], r0[u][j], acc0);
+        acc1 = mfma16x16x4(av[j], r1[u][j], acc1);
+        acc0b = mfma16x16x4(av[j + 1], r0[u][j + 1], acc0b);
+        acc1b = mfma16x16x4(av[j + 1], r1[u][j + 1], acc1b);
       }
       const int nx = i + 3 < G ? i + 3 : G - 1;
       r0[u] = W0[(int64_t)grp(nx) * 64];
@@ -928,12 +909,10 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
       }
       step(i, U2{});  // i = G - 1
     }
-    if (chains) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        acc0[i] += acc0b[i];
-        acc1[i] += acc1b[i];
-      }
+    for (int i = 0; i < 4; ++i) {
+      acc0[i] += acc0b[i];
+      acc1[i] += acc1b[i];
     }
     const float* bias = par + t.poff[0];
     const float* alpha = bias + t.Np[0];
@@ -1198,7 +1177,6 @@ static void launch_embed_fm_k(const EmbedFmArgs& a, int KV, int NT, hipStream_t 
 static int run_embed_fm(EmbedFmArgs a, const FmGeom& g, int kind, hipStream_t st, const char* what,
                         const FieldMeta* hm = nullptr) {
   if (a.batch == 0) return RS_OK;
-  a.chains = opt(RS_OPT_MFMA_CHAINS);
   if (g.mfma) {
     a.DB = g.DB;
     a.dense_rec = g.dense_rec;
@@ -1505,7 +1483,6 @@ static void launch_pipe_kv(const EmbedFmArgs& a, const PipeArgs& p, int NT, hipS
 
 static void launch_pipe(const EmbedFmArgs& a0, const PipeArgs& p, const FmGeom& g, hipStream_t st) {
   EmbedFmArgs a = a0;
-  a.chains = opt(RS_OPT_MFMA_CHAINS);
   switch (g.KV) {
     case 1: launch_pipe_kv<1>(a, p, g.NT, st); break;
     case 2: launch_pipe_kv<2>(a, p, g.NT, st); break;
@@ -1877,7 +1854,6 @@ static int deepfm_run(const void* ids, int id_kind, int64_t id_stride, const flo
   a.dense_rec = fg.dense_rec;
   a.field_rec = fg.field_rec;
   a.field_base = fg.field_base;
-  a.chains = opt(RS_OPT_MFMA_CHAINS);
   hipStream_t st = as_stream(stream);
   with_id_kind(id_kind, [&](auto K) {
     constexpr int KIND = decltype(K)::value;

@@ -65,7 +65,6 @@ struct EmbedFmArgs {
   int64_t pstride;          // KIND 4: floats between consecutive samples' partial records
   unsigned long long* dbg;  // diagnostic builds only (RS_DIAG_STAMPS): phase stamps
   int ablate;               // diagnostic builds only: bit0 no MFMA, bit1 no B loads, bit2 no combine
-  int chains;               // RS_OPT_MFMA_CHAINS at launch
 };
 
 // Field metadata by value in the kernarg (diagnostic build -DRS_DIAG_KARG:

@@ -68,7 +68,6 @@ struct MlpArgs {
   int64_t M;
   unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_mlp_set_dbg)
   int unroll;               // RS_OPT_MLP_UNROLL at launch
-  int chains;               // RS_OPT_MFMA_CHAINS at launch
 };
 #define MLP_STAMP(i)                                                                              \
   do {                                                                                            \
@@ -217,10 +216,10 @@ __device__ __forceinline__ void mlp_mac_ch(floatx4 (&ring)[MLP_R], const float* 
   else mlp_mac_d<1, CH>(ring, ap, bp, g0, g1, acc);
 }
 
+// four accumulation chains (MFMA j of a k-group into chain j), compile-time
 __device__ __forceinline__ void mlp_mac(floatx4 (&ring)[MLP_R], const float* ap, const floatx4* bp, int g0, int g1,
-                                        floatx4& acc, int unroll = 0, int chains = 0) {
-  if (chains) mlp_mac_ch<4>(ring, ap, bp, g0, g1, acc, unroll);
-  else mlp_mac_ch<1>(ring, ap, bp, g0, g1, acc, unroll);
+                                        floatx4& acc, int unroll = 0) {
+  mlp_mac_ch<4>(ring, ap, bp, g0, g1, acc, unroll);
 }
 
 // The tower on a 16-row tile whose input is already in LDS buf0 (barrier not
@@ -285,7 +284,7 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
       const floatx4* bp = W + (int64_t)it.t * G * 64;
       if (item != w) mlp_ring_fill(ring, bp, it.g0, it.g1);
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-      mlp_mac(ring, ap, bp, it.g0, it.g1, acc, a.unroll, a.chains);
+      mlp_mac(ring, ap, bp, it.g0, it.g1, acc, a.unroll);
       if (head_here) {
         // head weight of this lane's column k: the packed head layer holds
         // W[k][0] at lane 16 ((k & 15) >> 2), element k & 3, of k-group k >> 4
@@ -391,7 +390,6 @@ inline bool mlp_fill_args(const MlpGeom& g, const int* acts, const float* prepar
   a.K0 = g.K[0];
   a.rs = g.rs;
   a.unroll = opt(RS_OPT_MLP_UNROLL);
-  a.chains = opt(RS_OPT_MFMA_CHAINS);
   return true;
 }
 

@@ -19,7 +19,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-OPTS = {"embed_fm_kernel": 0, "mlp_unroll": 1, "deepfm_kernel": 2, "mfma_chains": 3}
+OPTS = {"embed_fm_kernel": 0, "mlp_unroll": 1, "deepfm_kernel": 2}
 
 
 def main():
@@ -32,9 +32,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--chunk", type=int, default=64)
     ap.add_argument("--pool", type=int, default=64)
+    ap.add_argument("--lib", default=None, help="another build of librs_hip.so (build A/B: one process per build)")
     args = ap.parse_args()
     import recommender_system_amd as rs
     from recommender_system_amd import _lib
+    if args.lib:
+        from pathlib import Path
+        _lib._LIB_PATH = Path(args.lib).resolve()
 
     dev = torch.device("cuda")
     B, F, k, nd = args.batch, 26, 16, 13
@@ -96,7 +100,7 @@ def main():
             res[v]["us"].append(e0.elapsed_time(e1) * 1e3 / (10 * args.chunk))
     base = res[values[0]]["out"]
     rms = float(base.pow(2).mean().sqrt())
-    line = {"option": args.option, "workload": args.workload, "batch": B,
+    line = {"option": args.option, "workload": args.workload, "batch": B, "lib": args.lib,
             "us_per_launch_median": {v: float(np.median(res[v]["us"])) for v in values},
             "us_per_launch_all": {v: [round(x, 3) for x in res[v]["us"]] for v in values},
             "max_scaled_diff_vs_first": {v: float(((res[v]["out"] - base).abs() / base.abs().clamp_min(rms)).max())

@@ -12,9 +12,9 @@ A=${1:-}
 if [ -z "$A" ]; then A=$(mktemp -d)/embed_fm.hip; git show HEAD:recommender_system_amd/csrc/embed_fm.hip > "$A"; fi
 C=recommender_system_amd/csrc
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -I include -I $C"
-hipcc $F ${AFLAGS:-} "$A" $C/embed_fm_tiles.hip $C/capi.cpp -o scripts/ab/librs_ab_A.so &
-hipcc $F ${BFLAGS:-} $C/embed_fm.hip $C/embed_fm_tiles.hip $C/capi.cpp -o scripts/ab/librs_ab_B.so &
+hipcc $F ${AFLAGS:-} "$A" $C/embed_fm_tiles.hip $C/mlp.hip $C/capi.cpp -o scripts/ab/librs_ab_A.so &
+hipcc $F ${BFLAGS:-} $C/embed_fm.hip $C/embed_fm_tiles.hip $C/mlp.hip $C/capi.cpp -o scripts/ab/librs_ab_B.so &
 if [ -n "${CFLAGS:-}" ]; then
-  hipcc $F $CFLAGS $C/embed_fm.hip $C/embed_fm_tiles.hip $C/capi.cpp -o scripts/ab/librs_ab_C.so &
+  hipcc $F $CFLAGS $C/embed_fm.hip $C/embed_fm_tiles.hip $C/mlp.hip $C/capi.cpp -o scripts/ab/librs_ab_C.so &
 fi
 wait

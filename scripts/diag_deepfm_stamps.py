@@ -38,7 +38,6 @@ def main():
     lib = _lib.lib()
     lib.rs_diag_mlp_set_dbg.argtypes = [C.c_void_p]
     _lib.set_option(_lib.OPT_DEEPFM_KERNEL, int(os.environ.get("DIAG_DEEPFM_OPT", "1")))
-    _lib.set_option(_lib.OPT_MFMA_CHAINS, int(os.environ.get("DIAG_CHAINS", "0")))
     for i in range(40):
         m.forward_fused((dense[i % NP], ids[i % NP]), check_ids=False)
     torch.cuda.synchronize()
@@ -55,8 +54,7 @@ def main():
     if int(os.environ.get("DIAG_DEEPFM_OPT", "1")) == 0:  # split roles: slots 2 / 3 = burst 0 / 1 in
         names[2], names[3] = "burst0_in", "burst1_in"
     names[15] = "end"
-    out = {"B": B, "V": V, "deepfm_kernel_option": int(os.environ.get("DIAG_DEEPFM_OPT", "1")),
-           "mfma_chains": int(os.environ.get("DIAG_CHAINS", "0")), "phases_cycles": {}}
+    out = {"B": B, "V": V, "deepfm_kernel_option": int(os.environ.get("DIAG_DEEPFM_OPT", "1")), "phases_cycles": {}}
     for j, n in names.items():
         rel = d[:, :, j] - t0
         ok = d[:, :, j] > 0  # waves that wrote this slot
