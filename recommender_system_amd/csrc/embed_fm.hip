@@ -201,7 +201,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       tsm[r * xrs + d0 + (i - r * padw)] = 0.f;
     }
   }
-  const bool dense_small = a.DB <= NW;
+  const bool dense_small = KA || a.DB <= NW;  // (the kernarg kernel is launched for DB <= 16 only)
   // Dense k-steps go to the LAST waves: with F = 26 fields over 16 waves the
   // first F - NW waves already carry two fields.
   const int dw = NW - 1 - w;                        // dense k-step of this wave
@@ -263,6 +263,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     bool ok[MAXC];
     typename I::raw_t rid[MAXC];
     int64_t off[MAXC], voc[MAXC];
+    int64_t row[MAXC];  // decoded table rows (decode_rows)
     Chunk<KV> xs[MAXC];
     Chunk<KV> bw[MAXC][NT];
     float nrm[MAXC][KV];
@@ -333,35 +334,39 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     }
     if (cg == 0 && !coop && a.F > 0) load_dense();
   };
-  auto issue_rows = [&](int cg, Pass& P, bool fetched) {
-    if (!fetched) fetch_ids(cg, P);
-    const int64_t* offc = P.off;
-    const int64_t* vocc = P.voc;
+  // id -> table row (the ids must have arrived)
+  auto decode_rows = [&](int cg, Pass& P) {
     if (cg == 0) RS_STAMP(6);
     else RS_STAMP(10);
-    // row gather: KV consecutive floats of the sample's row per lane
-    int64_t row[MAXC];
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
       if constexpr (KIND == 3) {
-        row[j] = b * a.F + P.cj[j];
+        P.row[j] = b * a.F + P.cj[j];
         P.ok[j] = true;
       } else {
         int64_t id;
-        P.ok[j] = I::decode(P.rid[j], vocc[j], id);
-        row[j] = offc[j] + id;
+        P.ok[j] = I::decode(P.rid[j], P.voc[j], id);
+        P.row[j] = P.off[j] + id;
       }
     }
-    RS_USE(row[MAXC - 1]);
+    RS_USE(P.row[MAXC - 1]);
     if (cg == 0) RS_STAMP(1);
     else RS_STAMP(11);
+  };
+  // row gather: KV consecutive floats of the sample's row per lane
+  auto load_rows = [&](int cg, Pass& P) {
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
 #ifdef RS_DIAG_STAMPS
       if ((a.ablate & 8) && cg + j * NW + w >= a.F) { P.xs[j].zero(); continue; }
 #endif
-      P.xs[j].load_nt(a.table + row[j] * a.k + KV * kk);
+      P.xs[j].load_nt(a.table + P.row[j] * a.k + KV * kk);
     }
+  };
+  auto issue_rows = [&](int cg, Pass& P, bool fetched) {
+    if (!fetched) fetch_ids(cg, P);
+    decode_rows(cg, P);
+    load_rows(cg, P);
   };
   auto consume = [&](int cg, Pass& P) {
     RS_USE(P.xs[MAXC - 1].v[KV - 1]);
@@ -392,7 +397,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 #pragma unroll
           for (int tp = 0; tp < KV; ++tp) xo[tp] = P.ok[j] ? P.xs[j].v[tp] : 0.f;
         }
-      } else if (a.x_out && live && valid) {
+      } else if (!KA && a.x_out && live && valid) {  // (the kernarg kernel never emits x)
         float* xo = a.x_out + b * d + a.nd + P.cj[j] * a.k + KV * kk;
 #pragma unroll
         for (int tp = 0; tp < KV; ++tp) xo[tp] = P.ok[j] ? P.xs[j].v[tp] : 0.f;
@@ -435,11 +440,16 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       issue_rows(0, P0, true);
       norms(P0);
       if (two) norms(P1);
+      // the second pass's ids arrive with the first's: its row addresses are
+      // worked out while the first rows are in flight, so only the loads
+      // themselves sit between the first pass's MFMAs and the second trip
+      if (two) decode_rows(PS, P1);
       consume(0, P0);
       if (two) {
-        issue_rows(PS, P1, true);
+        load_rows(PS, P1);
         consume(PS, P1);
-        for (int cg = 2 * PS; has_pass(cg); cg += PS) {
+        // (a third pass: more than 2 x NW fields — never in the kernarg kernel, F <= 32)
+        for (int cg = 2 * PS; !KA && has_pass(cg); cg += PS) {
           issue_b(cg, P0);
           issue_rows(cg, P0, false);
           norms(P0);
@@ -465,7 +475,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     qn = fmaf(dx * dx, dn, qn);
     if constexpr (TW) {
       if (e < a.nd) tsm[s * xrs + a.F * a.k + e] = dx;
-    } else if (a.x_out && valid && e < a.nd) {
+    } else if (!KA && a.x_out && valid && e < a.nd) {
       a.x_out[b * d + e] = dx;
     }
   }
@@ -1141,7 +1151,9 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st, const FieldMe
   // us at 16384, 47.5 vs 42.6 at 65536, still 14.34 vs 13.54 / 47.8 vs 42.6
   // with both passes' ids requested together; profiles/r3_ab_kernarg_*)
   // 16 waves (13: 6.20 us, 9: 6.78 vs 5.76 at 4096; profiles/r3_ab_kernarg_waves_4096.json)
-  if (hm && a.F <= 32 && KIND != 3 && grid <= 512) {
+  // (the kernarg kernel is built lean: at most 2 x 16 fields, 16 dense k-steps,
+  // no x output — its straight-line code runs from a cold instruction cache)
+  if (hm && a.F <= 32 && KIND != 3 && grid <= 512 && a.DB <= 16 && !a.x_out) {
     embed_fm_mfma_ka<KV, NT, 16, KIND, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
     return;
   }
