@@ -432,6 +432,8 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       // fragments: ids first was slower, 5.95 vs 5.75 us at 4096)
       fetch_ids(0, P0);
       if (two) fetch_ids(PS, P1);
+    } else if (!coop && a.F > 0) {
+      load_dense();  // a wave with no field (F < NW) may still own a dense k-step
     }
     if (one) {
       // (the second pass's rows stay behind the first pass's MFMAs: issuing

@@ -181,11 +181,13 @@ def test_embed_fm_kernel_variants(gpu, embed_fm_variant, k, kfm, F, nd, B, idt):
     (16, 10, 33, 13, 64, "i32", False),     # F > 32: the device-metadata kernel
     (16, 10, 26, 13, 4093, "i64", True),    # ragged last tile, x emitted
     (16, 10, 17, 0, 50, "f32", False),      # no dense block, one pass + a partial pass
+    (16, 10, 9, 2, 333, "i32", False),      # fewer fields than waves, one dense k-step
 ])
 def test_embed_fm_host_meta(gpu, k, kfm, F, nd, B, idt, with_x):
     """rs_embed_fm_fwd_hm (field metadata also as kernel arguments, per-wave
     id loads, no id tile) == rs_embed_fm_fwd bit for bit (logit and x) and ==
-    the oracle; an out-of-range id sets the flag."""
+    the oracle; an out-of-range id sets the flag.  (F < 16 with a dense block:
+    the dense k-step belongs to a wave with no field.)"""
     import ctypes as C
     from recommender_system_amd import _lib
     rng = np.random.default_rng(B * 7 + F)
