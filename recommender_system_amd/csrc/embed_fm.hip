@@ -929,12 +929,14 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     const float* bias = par + t.poff[0];
     const float* alpha = bias + t.Np[0];
     float* out = tsm + 16 * RS;  // layer 0 -> buf1
+    with_act(t.act[0], [&](auto A) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = 4 * kk + r, col0 = 16 * c8 + s, col1 = col0 + 16 * WS_NL;
-      out[row * RS + col0] = mlp_act(acc0[r] + bias[col0], t.act[0], alpha[col0]);
-      out[row * RS + col1] = mlp_act(acc1[r] + bias[col1], t.act[0], alpha[col1]);
-    }
+      for (int r = 0; r < 4; ++r) {
+        const int row = 4 * kk + r, col0 = 16 * c8 + s, col1 = col0 + 16 * WS_NL;
+        out[row * RS + col0] = mlp_act_c<decltype(A)::value>(acc0[r] + bias[col0], alpha[col0]);
+        out[row * RS + col1] = mlp_act_c<decltype(A)::value>(acc1[r] + bias[col1], alpha[col1]);
+      }
+    });
   }
   {
     const MlpArgs& a = t;

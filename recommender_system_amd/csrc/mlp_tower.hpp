@@ -2,6 +2,7 @@
 // the fused DeepFM kernel (embed_fm.hip).  See mlp.hip for the design.
 #pragma once
 #include <algorithm>
+#include <type_traits>
 
 #include "rs_common.hpp"
 
@@ -75,12 +76,30 @@ struct MlpArgs {
       a.dbg[((int64_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
+template <int ACT>
+__device__ __forceinline__ float mlp_act_c(float v, float alpha) {
+  if constexpr (ACT == RS_ACT_RELU) return fmaxf(v, 0.f);
+  else if constexpr (ACT == RS_ACT_PRELU) return fmaxf(v, 0.f) + alpha * fminf(v, 0.f);
+  else if constexpr (ACT == RS_ACT_SIGMOID) return 1.0f / (1.0f + expf(-v));
+  else return v;
+}
 __device__ __forceinline__ float mlp_act(float v, int act, float alpha) {
   switch (act) {
-    case RS_ACT_RELU: return fmaxf(v, 0.f);
-    case RS_ACT_PRELU: return fmaxf(v, 0.f) + alpha * fminf(v, 0.f);
-    case RS_ACT_SIGMOID: return 1.0f / (1.0f + expf(-v));
+    case RS_ACT_RELU: return mlp_act_c<RS_ACT_RELU>(v, alpha);
+    case RS_ACT_PRELU: return mlp_act_c<RS_ACT_PRELU>(v, alpha);
+    case RS_ACT_SIGMOID: return mlp_act_c<RS_ACT_SIGMOID>(v, alpha);
     default: return v;
+  }
+}
+// f(std::integral_constant<int, act>): the activation switch taken once
+// around an epilogue, not per element inside it
+template <class Fn>
+__device__ __forceinline__ void with_act(int act, Fn&& f) {
+  switch (act) {
+    case RS_ACT_RELU: f(std::integral_constant<int, RS_ACT_RELU>()); break;
+    case RS_ACT_PRELU: f(std::integral_constant<int, RS_ACT_PRELU>()); break;
+    case RS_ACT_SIGMOID: f(std::integral_constant<int, RS_ACT_SIGMOID>()); break;
+    default: f(std::integral_constant<int, RS_ACT_NONE>()); break;
   }
 }
 
@@ -258,8 +277,8 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
     const bool last = l == a.L - 1;
     const int Nl = a.N[l];
 
-    auto finish = [&](int row, int col, float v) {
-      v = mlp_act(v + bias[col], act, alpha[col]);
+    auto finish = [&](auto A, int row, int col, float v) {
+      v = mlp_act_c<decltype(A)::value>(v + bias[col], alpha[col]);
       if (!last) {
         out[row * RS + col] = v;
       } else {
@@ -292,15 +311,19 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
         const float hw = col < Nl ? a.prep[a.off[LH] + ((int64_t)(col >> 4) * 64 + 16 * ((col & 15) >> 2)) * 4 +
                                            (col & 3)]
                                   : 0.f;
+        with_act(act, [&](auto A) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float p = col < Nl ? mlp_act(acc[r] + bias[col], act, alpha[col]) * hw : 0.f;
-          p = row16_sum(p);
-          if ((lane & 15) == 0) red[it.t * 16 + 4 * (lane >> 4) + r] = p;
-        }
+          for (int r = 0; r < 4; ++r) {
+            float p = col < Nl ? mlp_act_c<decltype(A)::value>(acc[r] + bias[col], alpha[col]) * hw : 0.f;
+            p = row16_sum(p);
+            if ((lane & 15) == 0) red[it.t * 16 + 4 * (lane >> 4) + r] = p;
+          }
+        });
       } else if (S == 1) {
+        with_act(act, [&](auto A) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) finish(4 * (lane >> 4) + r, 16 * it.t + (lane & 15), acc[r]);
+          for (int r = 0; r < 4; ++r) finish(A, 4 * (lane >> 4) + r, 16 * it.t + (lane & 15), acc[r]);
+        });
       } else {
         *reinterpret_cast<floatx4*>(red + item * 256 + lane * 4) = acc;
       }
@@ -319,12 +342,14 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
     }
     if (S > 1) {
       __syncthreads();
-      for (int e = threadIdx.x; e < T * 256; e += NW * 64) {
-        const int t = e >> 8, q = e & 255, ln = q >> 2, r = q & 3;
-        float v = 0.f;
-        for (int p = 0; p < S; ++p) v += red[(p * T + t) * 256 + q];
-        finish(4 * (ln >> 4) + r, 16 * t + (ln & 15), v);
-      }
+      with_act(act, [&](auto A) {
+        for (int e = threadIdx.x; e < T * 256; e += NW * 64) {
+          const int t = e >> 8, q = e & 255, ln = q >> 2, r = q & 3;
+          float v = 0.f;
+          for (int p = 0; p < S; ++p) v += red[(p * T + t) * 256 + q];
+          finish(A, 4 * (ln >> 4) + r, 16 * t + (ln & 15), v);
+        }
+      });
     }
     float* tmp = in;
     in = out;
