@@ -26,7 +26,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--option", default="embed_fm_kernel", choices=sorted(OPTS))
     ap.add_argument("--values", default="0,1")
-    ap.add_argument("--workload", default="deepfm", choices=["deepfm", "dcn", "embed_fm"])
+    ap.add_argument("--workload", default="deepfm", choices=["deepfm", "dcn", "cross", "embed_fm"])
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--vocab", type=float, default=1e7)
     ap.add_argument("--rounds", type=int, default=8)
@@ -50,11 +50,14 @@ def main():
     NP = args.pool
     ids = torch.randint(0, V, (NP, B, F), generator=g, device=dev, dtype=torch.int32)
     dense = torch.rand(NP, B, nd, generator=g, device=dev)
-    if args.workload == "dcn":
+    if args.workload in ("dcn", "cross"):
         m = rs.DCN(cols, [256, 128, 64], 1, "relu", layer_num=3, embed_dim=k, seed=3, device=dev)
 
         def fn(i):
-            outs[i % NP] = m.forward_fused((dense[i % NP], ids[i % NP]), check_ids=False)
+            if args.workload == "dcn":
+                outs[i % NP] = m.forward_fused((dense[i % NP], ids[i % NP]), check_ids=False)
+            else:  # the CrossNet output x_L (embed_cross)
+                outs[i % NP] = m.cross_fused((dense[i % NP], ids[i % NP]), check_ids=False)
     else:
         m = rs.DeepFM(cols, 10, 1e-4, 1e-4, [256, 128, 64], 1, "relu", embed_dim=k, seed=3, device=dev)
         if args.workload == "deepfm":
