@@ -70,11 +70,21 @@ struct MlpArgs {
   unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_mlp_set_dbg)
   int unroll;               // RS_OPT_MLP_UNROLL at launch
 };
+// Per-wave phase stamps (rs_diag_mlp_set_dbg) exist only in the diagnostic
+// build (scripts/build_diag.sh, -DRS_DIAG_STAMPS): the product's runtime
+// check of a.dbg at every stamp cost 2.5 % of the fused DeepFM and 1.5 % of
+// the fused DCN (instruction fetch; profiles/r4_ab_stamps_compiled_out.jsonl).
+#ifdef RS_DIAG_STAMPS
 #define MLP_STAMP(i)                                                                              \
   do {                                                                                            \
     if (a.dbg && (threadIdx.x & 63) == 0)                                                         \
       a.dbg[((int64_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+#else
+#define MLP_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
 
 template <int ACT>
 __device__ __forceinline__ float mlp_act_c(float v, float alpha) {

@@ -10,7 +10,7 @@ cd "$(dirname "$0")/.."
 mkdir -p scripts/ab
 rm -f scripts/ab/librs_tower_*.so
 C=recommender_system_amd/csrc
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -I include"
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DRS_DIAG_STAMPS -I include"  # (stamps for ab_tower_stamps.py)
 T=$(mktemp -d)
 for v in A B C D; do mkdir -p $T/$v; cp $C/mlp_tower.hpp $C/mlp.hip $T/$v/; done
 sed -i 's/ring\[u\] = bp\[(int64_t)min(g + u + D, g1 - 1) \* 64\];/ring[u] = bp[(int64_t)g0 * 64];/' $T/B/mlp_tower.hpp

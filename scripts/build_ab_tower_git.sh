@@ -9,7 +9,7 @@ REV=${1:-HEAD}
 mkdir -p scripts/ab
 rm -f scripts/ab/librs_tower_*.so
 C=recommender_system_amd/csrc
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -I include"
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DRS_DIAG_STAMPS -I include"  # (stamps for ab_tower_stamps.py)
 T=$(mktemp -d)
 for v in A B C D; do mkdir -p $T/$v; cp $C/mlp.hip $C/mlp_tower.hpp $T/$v/; done
 git show $REV:$C/mlp_tower.hpp > $T/A/mlp_tower.hpp

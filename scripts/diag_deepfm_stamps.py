@@ -10,6 +10,7 @@ first stamp), for the median wave and the slowest wave, and the span."""
 import ctypes as C
 import json
 import os
+from pathlib import Path
 import sys
 
 import numpy as np
@@ -22,6 +23,8 @@ sys.path.insert(0, ROOT)
 def main():
     import recommender_system_amd as rs
     from recommender_system_amd import _lib
+    # the MLP stamps exist only in the diagnostic build (scripts/build_diag.sh)
+    _lib._LIB_PATH = Path(ROOT) / "recommender_system_amd" / "librs_hip_diag.so"
     dev = torch.device("cuda")
     B, F, nd, k = int(os.environ.get("DIAG_B", "4096")), 26, 13, 16
     V = int(float(os.environ.get("DIAG_V", "1e6")))

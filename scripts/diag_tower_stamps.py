@@ -2,13 +2,18 @@
 rs_diag_mlp_set_dbg): median cycles of each phase across workgroups."""
 import ctypes as C
 import os
+from pathlib import Path
 import sys
 
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 from recommender_system_amd import DNNLayer, _lib  # noqa: E402
+
+# the MLP stamps exist only in the diagnostic build (scripts/build_diag.sh)
+_lib._LIB_PATH = Path(ROOT) / "recommender_system_amd" / "librs_hip_diag.so"
 
 B = int(os.environ.get("TOWER_B", "4096"))
 dims = [int(v) for v in os.environ.get("TOWER_DIMS", "429,256,128,64,1").split(",")]
