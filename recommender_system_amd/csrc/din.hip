@@ -134,12 +134,19 @@ struct DinArgs {
   int* err;
   unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_din_set_dbg)
 };
+// (phase stamps only in the diagnostic build, scripts/build_diag.sh)
+#ifdef RS_DIAG_STAMPS
 #define DIN_STAMP(i)                                                                                   \
   do {                                                                                                 \
     if (a.dbg && (threadIdx.x & 63) == 0)                                                              \
       a.dbg[(((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6)) * 8 + (i)] =     \
           __builtin_amdgcn_s_memtime();                                                                \
   } while (0)
+#else
+#define DIN_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
 
 
 // Keras PReLU max(0,x) + alpha*min(0,x) == x * (x < 0 ? alpha : 1) (one
@@ -185,9 +192,11 @@ __global__ __launch_bounds__(256, 4) void din_scores(DinArgs a) {  // 4 waves/SI
   const int col = lane & 15, kg = lane >> 4;
   const int t0 = blockIdx.x * 16;
   DIN_STAMP(0);
+#ifdef RS_DIAG_STAMPS
   if (a.dbg && (threadIdx.x & 63) == 0)
     a.dbg[(((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6)) * 8 + 6] =
         __builtin_amdgcn_s_memrealtime();
+#endif
 
   // ---- stage the tile's alphas and the W2^T image (shared by 16 samples)
   const float* pa1 = a.prep + g.a1 + (int64_t)t0 * (HT1 * 16);
@@ -342,9 +351,11 @@ __global__ __launch_bounds__(256, 4) void din_scores(DinArgs a) {  // 4 waves/SI
     ++cnt;
   }
   if (__any(bad) && lane == 0) flag_error(a.err);
+#ifdef RS_DIAG_STAMPS
   if (a.dbg && (threadIdx.x & 63) == 0)
     a.dbg[(((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6)) * 8 + 7] =
         __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // masked softmax over the T scores and out[b] = sum_t a_t * E[hist_t].

@@ -2,6 +2,7 @@
 T=100, k=8, (80, 40)): cycles from the workgroup's first stamp."""
 import ctypes as C
 import os
+from pathlib import Path
 import sys
 
 import numpy as np
@@ -9,6 +10,9 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from recommender_system_amd import Attention, _lib  # noqa: E402
+
+# the DIN stamps exist only in the diagnostic build (scripts/build_diag.sh)
+_lib._LIB_PATH = Path(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))) / "recommender_system_amd" / "librs_hip_diag.so"
 
 B, T, k, V = 2048, 100, 8, 63001
 layer = Attention((80, 40), "prelu", seed=1)
