@@ -33,11 +33,18 @@ struct InnerArgs {
   int* err;
   unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_inner_set_dbg)
 };
+// (phase stamps only in the diagnostic build, scripts/build_diag.sh)
+#ifdef RS_DIAG_STAMPS
 #define IP_STAMP(i)                                                                                   \
   do {                                                                                                \
     if (a.dbg && (threadIdx.x & 63) == 0)                                                             \
       a.dbg[((int64_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+#else
+#define IP_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
 
 __device__ __forceinline__ bool inner_decode(const void* ids, int kind, int64_t off, int64_t vocab, int64_t& id) {
   if (kind == RS_ID_F32) {

@@ -2,6 +2,7 @@
 bench shape (B=4096, 26 x 1e6, k=16): median cycles per phase."""
 import ctypes as C
 import os
+from pathlib import Path
 import sys
 
 import numpy as np
@@ -10,6 +11,9 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import recommender_system_amd as rs  # noqa: E402
 from recommender_system_amd import _lib  # noqa: E402
+
+# the inner-product stamps exist only in the diagnostic build (scripts/build_diag.sh)
+_lib._LIB_PATH = Path(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))) / "recommender_system_amd" / "librs_hip_diag.so"
 
 B, F, V, k = 4096, 26, 1_000_000, 16
 cols = [[{"feat": f"I{i}"} for i in range(13)],
