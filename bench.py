@@ -385,9 +385,14 @@ def bench_hotpath(args, world, rank):
         result["value"] = args.steps * B / dt
         result["ms_per_step"] = dt / args.steps * 1e3
         result["roofline"] = {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                              "frac": achieved / PEAK_HBM, "traffic": _pmc_traffic(),
-                              "traffic_source": "profiles/pmc_embed_fm.json (rocprofv3 PMC pass of this kernel at "
-                                                "this shape: TCC_EA0_RDREQ x 128 B + WRITE_SIZE per launch)",
+                              "frac": achieved / PEAK_HBM,
+                              # the PMC file was measured on the 26 x 1e7 table: other vocabularies
+                              # (--config deepfm1e6) have no pass of their own, so no traffic figure
+                              "traffic": _pmc_traffic() if int(args.vocab) == int(1e7) else None,
+                              "traffic_source": ("profiles/pmc_embed_fm.json (rocprofv3 PMC pass of this kernel at "
+                                                 "this shape: TCC_EA0_RDREQ x 128 B + WRITE_SIZE per launch)"
+                                                 if int(args.vocab) == int(1e7) else
+                                                 "none: no PMC pass at this vocabulary"),
                               "kernel": "embed_fm_mfma", "kernel_ms": kern_ms,
                               "kernel_ms_source": "HIP events around the graph-replayed timed region / steps "
                                                   "(kernel + back-to-back dispatch boundary)",

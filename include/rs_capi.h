@@ -58,12 +58,20 @@ enum rs_act {
  * any other bit. */
 enum rs_flag {
   RS_FLAG_BAD_ID = 1, /* an id outside [0, vocab) (its row read as zeros)               */
-  RS_FLAG_LAYOUT = 2  /* field row ranges overlap or decrease where a kernel needs the
+  RS_FLAG_LAYOUT = 2, /* field row ranges overlap or decrease where a kernel needs the
                          concatenated-table layout (offset_c + vocab_c <= offset_{c+1}) */
+  RS_FLAG_TIMEOUT = 4 /* a bounded in-kernel wait (a workgroup-internal hand-off) gave up:
+                         a kernel logic error — the launch's outputs are invalid and the
+                         host layer raises RSError instead of returning them               */
 };
 
-/* Runtime tuning options (process-wide, host side; read when a kernel is
- * launched, so a captured hipGraph keeps the value it was captured with). */
+/* Runtime tuning options (host side, read when a kernel is launched, so a
+ * captured hipGraph keeps the value it was captured with).  Options are
+ * THREAD-LOCAL: rs_set_option changes only the launches made by the calling
+ * host thread, every new thread starts from the defaults — no process-wide
+ * mutable state, so concurrent callers on different threads stay reentrant
+ * (SURVEY 8(b)).  They select between measured kernel forms for A/B work;
+ * results agree within the parity tolerance whatever the setting. */
 enum rs_option {
   RS_OPT_EMBED_FM_KERNEL = 0, /* rs_embed_fm_fwd kernel (id inputs, no x_out): 0 = MFMA K-split,
                                  1 = VALU/DPP persistent 8-sample tiles, 2 / 3 = MFMA persistent
@@ -76,8 +84,13 @@ enum rs_option {
   RS_OPT_DEEPFM_KERNEL = 2,   /* rs_deepfm_fwd_hm at the Criteo shape (k 16, 26 fields, 256-unit
                                  first layer): 0 (the default) = split wave roles (loaders +
                                  layer-0 compute waves, deepfm_ws), 1 = one role per wave (gather
-                                 + FM, then the tower).  See DESIGN.md 4.5                       */
-  RS_OPT_COUNT = 3
+                                 + FM, then the tower), 2 / 3 = every wave gathers two fields and
+                                 computes one layer-0 tile, split-K tower tail (deepfm_all; rows
+                                 requested before / after the first weights).  See DESIGN.md 4.5 */
+  RS_OPT_DIN_KERNEL = 3,      /* rs_din_attention_ids_fwd at the reference's (80, 40) widths: 0
+                                 (the default) = one launch (scores + softmax + pool, din_fused),
+                                 1 = two launches (din_scores, din_pool).  See DESIGN.md 4.4     */
+  RS_OPT_COUNT = 4
 };
 
 /* ------------------------------------------------------------------ meta */
@@ -98,7 +111,9 @@ int rs_diag_empty(int grid, int block, rs_stream_t stream);
  * dynamic LDS per workgroup — how a workgroup's waves spread over the SIMDs. */
 int rs_diag_wave_slots(int grid, int block, int lds_bytes, uint32_t* out, rs_stream_t stream);
 /* rs_diag_mfma_chain: every wave issues n v_mfma_f32_16x16x4_f32 as `chains`
- * (1, 2, 4) independent accumulation chains; cyc[wave] = s_memtime cycles. */
+ * (1, 2, 4) independent accumulation chains; cyc[3 wave + {0, 1, 2}] = its
+ * start / end s_memtime and its HW_ID (SIMD in bits 5:4), so the host can time
+ * each SIMD's window from its first wave's start to its last wave's end. */
 int rs_diag_mfma_chain(int grid, int block, int n, int chains, unsigned long long* cyc, float* sink,
                        rs_stream_t stream);
 /* rs_diag_icache: 2048 FMAs per wave as a loop (unroll 0) or straight-line
@@ -350,11 +365,15 @@ int rs_din_attention_gen_fwd(const float* query, const float* keys,
 
 /* DIN attention straight from behaviour ids (model/din.py:56-80 + Attention
  * 'prelu', layer/interaction.py:355-406): key = value = table[hist[b,t]],
- * query = table[cand[b]], mask = hist != 0.  Two launches: scores (MFMA, the
- * tile's PReLU alphas and W2 staged once per workgroup, layer 1 regrouped per
- * sample as q(Wq+Wd) + key(Wk-Wd+diag(q)Wp)) then the masked softmax pool.
+ * query = table[cand[b]], mask = hist != 0.  At the reference's (80, 40)
+ * widths ONE launch (din_fused: every position's PReLU alphas and W2 staged
+ * once per workgroup of 8 samples, layer 1 regrouped per sample as
+ * q(Wq+Wd) + key(Wk-Wd+diag(q)Wp), per-tile online-softmax partials merged
+ * per sample — the scores never reach HBM); other widths, or
+ * RS_OPT_DIN_KERNEL 1, two launches (scores, then the masked softmax pool).
  * prepared: rs_din_prepare (k in {4,8,16}, H1 <= 128, H2 <= 64); scores: a
- * caller-owned [B, T] fp32 workspace; out [B, k] with rows out_stride
+ * caller-owned [B, T] fp32 workspace (untouched by the one-launch form);
+ * out [B, k] with rows out_stride
  * floats apart (>= k: DIN.call writes straight into its concat).  T <= 1024.
  * OOR ids set *err_flag.                                                   */
 int64_t rs_din_prepared_size(int T, int k, int H1, int H2);

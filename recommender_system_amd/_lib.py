@@ -151,10 +151,23 @@ SIGNATURES = {
 }
 
 ID_I32, ID_I64, ID_F32 = 0, 1, 2
-FLAG_BAD_ID, FLAG_LAYOUT = 1, 2  # rs_flag bits of the device error flag
+FLAG_BAD_ID, FLAG_LAYOUT, FLAG_TIMEOUT = 1, 2, 4  # rs_flag bits of the device error flag
+_FLAG_NAMES = {FLAG_BAD_ID: "RS_FLAG_BAD_ID: an embedding id out of range",
+               FLAG_LAYOUT: "RS_FLAG_LAYOUT: the table's field row ranges overlap or decrease",
+               FLAG_TIMEOUT: "RS_FLAG_TIMEOUT: a bounded in-kernel wait gave up (kernel logic error; outputs invalid)"}
+
+
+def flag_names(bits: int) -> str:
+    """Human-readable list of the rs_flag bits set in `bits`."""
+    names = [n for b, n in _FLAG_NAMES.items() if bits & b]
+    unknown = bits & ~sum(_FLAG_NAMES)
+    if unknown:
+        names.append(f"unknown bits {unknown:#x}")
+    return "; ".join(names)
 OPT_EMBED_FM_KERNEL = 0  # rs_option
 OPT_MLP_UNROLL = 1
 OPT_DEEPFM_KERNEL = 2
+OPT_DIN_KERNEL = 3
 ACT = {None: 0, "linear": 0, "relu": 1, "prelu": 2, "sigmoid": 3}
 
 _lock = threading.Lock()

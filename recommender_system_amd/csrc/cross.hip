@@ -84,11 +84,19 @@ struct CrossArgs {
   unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_cross_set_dbg)
 };
 static unsigned long long* g_cross_dbg = nullptr;  // rs_diag_cross_set_dbg
+// Phase stamps only in the diagnostic build (scripts/build_diag.sh), like
+// MLP_STAMP / DIN_STAMP / IP_STAMP: no runtime check of a.dbg in the product.
+#ifdef RS_DIAG_STAMPS
 #define CR_STAMP(i)                                                                                   \
   do {                                                                                                \
     if (a.dbg && (threadIdx.x & 63) == 0)                                                             \
       a.dbg[((int64_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+#else
+#define CR_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
 
 // The B fragments of 8 of a wave's k-steps (t0, t0 + NW, ..): L2-resident
 // launch constants, so the fused kernels request the first 8 before their

@@ -18,12 +18,17 @@ __global__ void diag_wave_slots_kernel(uint32_t* out) {
 }
 
 // MFMA issue timing: every wave runs n v_mfma_f32_16x16x4_f32 as `chains`
-// independent accumulation chains (1, 2 or 4) and lane 0 records the
-// s_memtime cycles they took; the result is stored so nothing is dropped.
+// independent accumulation chains (1, 2 or 4); lane 0 records its start and
+// end s_memtime and its HW_ID, cyc[3 wave + {0, 1, 2}] — the host groups the
+// waves by (workgroup, SIMD) and divides each SIMD's window (first start to
+// last end) by the MFMAs issued on it.  (Round 4 divided one wave's own
+// window by the waves per SIMD, which assumed the waves ran in perfect
+// overlap and read faster than the 32-cycle issue rate.)
 __global__ void diag_mfma_chain_kernel(int n, int chains, unsigned long long* cyc, float* sink) {
   const int lane = threadIdx.x & 63;
   float a = 1.0f + lane * 1e-3f, b = 0.5f - lane * 1e-3f;
   floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
+  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);  // HW_REG_HW_ID
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   if (chains == 4) {
     for (int i = 0; i < n; i += 4) {
@@ -45,7 +50,12 @@ __global__ void diag_mfma_chain_kernel(int n, int chains, unsigned long long* cy
   for (int i = 0; i < 4; ++i) r += c0[i] + c1[i] + c2[i] + c3[i];
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   sink[blockIdx.x * blockDim.x + threadIdx.x] = r;
-  if (lane == 0) cyc[blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)] = t1 - t0;
+  if (lane == 0) {
+    const int64_t wv = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    cyc[3 * wv] = t0;
+    cyc[3 * wv + 1] = t1;
+    cyc[3 * wv + 2] = hw;
+  }
 }
 
 // Instruction-fetch cost: 2048 FMAs on 8 independent accumulators as a loop

@@ -402,6 +402,245 @@ __global__ __launch_bounds__(256) void din_pool(DinArgs a) {
   if (lane < k) a.out[b * a.ldo + lane] = v / sum;
 }
 
+// ---- One-launch DIN attention unit (din_fused; RS_OPT_DIN_KERNEL 0, the
+// default at the reference's (80, 40) widths): scores, masked softmax and the
+// pool in ONE kernel, no [B, T] score round trip through HBM and no second
+// launch.  One 16-wave workgroup per CU owns DF_SPW samples, ALL their
+// position tiles: the PReLU alphas of every position (a [NTT*16][HT*16]
+// slice of each layer) and the W2^T image are staged in LDS once per
+// workgroup; item (sample, tile) = one 16-position MFMA tile exactly as in
+// din_scores (layer 1 regrouped per sample, layer 1's accumulators are layer
+// 2's B operand), the wave's next item's ids and rows requested while the
+// current one computes.  Each item ends with its tile's online-softmax
+// partial {m_j = max s_t, l_j = sum e^(s_t - m_j), o_j = sum e^(s_t - m_j)
+// key_t} in LDS; after one barrier a wave per sample merges its tiles
+// (m = max m_j, weights e^(m_j - m)) and writes out[b] = o / l.  Items are
+// dealt round-robin to the waves (w, w + 16, ..): at 8 samples x 7 tiles
+// every SIMD runs 14 items.  Masking as the reference (din.py: hist != 0 ->
+// score -2^32 + 1 in fp32 = -4294967296): a fully masked row averages its
+// keys; an out-of-range id reads a zero row and sets the flag (din_pool's
+// rule).  Reference: layer/interaction.py:369-406, model/din.py:56-80.
+#ifdef RS_DIAG_STAMPS
+#define DF_STAMP(i)                                                                                            \
+  do {                                                                                                         \
+    if (a.dbg && (threadIdx.x & 63) == 0)                                                                      \
+      a.dbg[((int64_t)blockIdx.x * DF_NW + (threadIdx.x >> 6)) * 8 + (i)] = __builtin_amdgcn_s_memtime();      \
+  } while (0)
+#else
+#define DF_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+constexpr int DF_SPW = 8;     // samples per workgroup
+constexpr int DF_NW = 16;     // waves per workgroup
+constexpr int DF_MAXK = 16;   // embedding width (k) at most
+
+struct DfLayout {  // dynamic LDS (floats): a1s | a2s | w2s | part
+  int a1, a2, w2, part, total;
+};
+__host__ __device__ inline DfLayout df_layout(int NTT, int HT1, int HT2) {
+  DfLayout L;
+  L.a1 = 0;
+  L.a2 = L.a1 + NTT * 16 * (HT1 * 16 + 4);
+  L.w2 = L.a2 + NTT * 16 * (HT2 * 16 + 4);
+  L.part = L.w2 + HT2 * HT1 * 64 * 4;
+  L.total = L.part + DF_SPW * NTT * (2 + DF_MAXK);
+  return L;
+}
+
+template <int KS, int HT1, int HT2, int KIND>
+__global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
+  typedef Ids<KIND> I;
+  constexpr int K = 4 * KS;
+  const DinGeom& g = a.g;
+  const int NTT = g.NTT, T = g.T;
+  const DfLayout L = df_layout(NTT, HT1, HT2);
+  extern __shared__ float dsm[];
+  float* a1s = dsm + L.a1;  // [NTT*16][HT1*16 + 4]
+  float* a2s = dsm + L.a2;  // [NTT*16][HT2*16 + 4]
+  floatx4* w2s = reinterpret_cast<floatx4*>(dsm + L.w2);
+  float* part = dsm + L.part;  // [DF_SPW * NTT][2 + DF_MAXK]
+  __shared__ floatx4 b1s[HT1 * 4], b2s[HT2 * 4], w3s[HT2 * 4];
+  constexpr int A1W = HT1 * 16 + 4, A2W = HT2 * 16 + 4;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = lane & 15, kg = lane >> 4;
+  const int64_t s0 = (int64_t)blockIdx.x * DF_SPW;
+  const int nsmp = (int)min<int64_t>(DF_SPW, a.batch - s0);
+  const int nitems = nsmp * NTT;
+  DF_STAMP(0);
+
+  // the wave's items: it = w + 16 m  ->  (sample it / NTT, tile it % NTT)
+  auto item_ids = [&](int it, typename I::raw_t& craw, typename I::raw_t& hraw) {
+    const int itc = it < nitems ? it : nitems - 1;  // clamped: loads stay in bounds, results unused
+    const int si = itc / NTT, j = itc - si * NTT;
+    const int64_t b = s0 + si;
+    const int t = 16 * j + col;
+    craw = I::load(a.cand, b * a.cand_stride);
+    hraw = I::load(a.hist, b * a.hist_stride + (t < T ? t : 0));
+  };
+  auto item_rows = [&](typename I::raw_t craw, typename I::raw_t hraw, float (&q)[KS], float (&kv)[KS]) {
+    int64_t cid, hid;
+    I::decode(craw, a.vocab, cid);
+    I::decode(hraw, a.vocab, hid);
+    din_row<KS>(a.table, cid, kg, q);
+    din_row<KS>(a.table, hid, kg, kv);
+  };
+  // first item's ids and rows go out before the staging loads
+  typename I::raw_t cr0, hr0, cr1, hr1;
+  item_ids(w, cr0, hr0);
+  item_ids(w + DF_NW, cr1, hr1);
+
+  // ---- stage every position's alphas and the W2^T image: every load of a
+  // round is issued before its LDS stores (a load -> store loop pays one L2
+  // round trip per iteration: 7.7k cycles of staging in the first version)
+  {
+    const float* pa1 = a.prep + g.a1;
+    const float* pa2 = a.prep + g.a2;
+    const floatx4* pw2 = reinterpret_cast<const floatx4*>(a.prep + g.w2);
+    const int n1 = NTT * 16 * HT1 * 16, n2 = NTT * 16 * HT2 * 16, nw2 = HT2 * HT1 * 64;
+    constexpr int R1 = 12, R2 = 8, NTH = DF_NW * 64;
+    for (int b1 = 0, b2 = 0, bw = 0; b1 < n1 || b2 < n2 || bw < nw2; b1 += R1 * NTH, b2 += R2 * NTH, bw += NTH) {
+      float v1[R1], v2[R2];
+      floatx4 vw;
+#pragma unroll
+      for (int u = 0; u < R1; ++u) v1[u] = pa1[min(b1 + u * NTH + (int)threadIdx.x, n1 - 1)];  // clamped: unconditional
+#pragma unroll
+      for (int u = 0; u < R2; ++u) v2[u] = pa2[min(b2 + u * NTH + (int)threadIdx.x, n2 - 1)];
+      vw = pw2[min(bw + (int)threadIdx.x, nw2 - 1)];
+#pragma unroll
+      for (int u = 0; u < R1; ++u) {
+        const int i = b1 + u * NTH + threadIdx.x;
+        if (i < n1) a1s[(i / (HT1 * 16)) * A1W + i % (HT1 * 16)] = v1[u];
+      }
+#pragma unroll
+      for (int u = 0; u < R2; ++u) {
+        const int i = b2 + u * NTH + threadIdx.x;
+        if (i < n2) a2s[(i / (HT2 * 16)) * A2W + i % (HT2 * 16)] = v2[u];
+      }
+      if (bw + (int)threadIdx.x < nw2) w2s[bw + threadIdx.x] = vw;
+    }
+    if (threadIdx.x < HT1 * 16) reinterpret_cast<float*>(b1s)[threadIdx.x] = a.prep[g.b1 + threadIdx.x];
+    if (threadIdx.x < HT2 * 16) {
+      reinterpret_cast<float*>(b2s)[threadIdx.x] = a.prep[g.b2 + threadIdx.x];
+      reinterpret_cast<float*>(w3s)[threadIdx.x] = a.prep[g.w3 + threadIdx.x];
+    }
+  }
+  float wkd[HT1][KS], wpv[HT1][KS], wqd[HT1][KS];
+#pragma unroll
+  for (int ht = 0; ht < HT1; ++ht) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int64_t o = (int64_t)(ht * KS + s) * 64 + lane;
+      wkd[ht][s] = a.prep[g.wkd + o];
+      wpv[ht][s] = a.prep[g.wp + o];
+      wqd[ht][s] = a.prep[g.wqd + o];
+    }
+  }
+  const float b3 = a.prep[g.b3];
+  float q[KS], kv[KS];
+  item_rows(cr0, hr0, q, kv);
+  __syncthreads();
+  DF_STAMP(1);
+
+  bool bad = false;
+  int cnt = 0;
+  for (int it = w; it < nitems; it += DF_NW) {
+    const int si = it / NTT, j = it - si * NTT;
+    const int t = 16 * j + col;
+    const bool tv = t < T;
+    int64_t cid, hid;
+    const bool cok = I::decode(cr0, a.vocab, cid);
+    const bool hok = I::decode(hr0, a.vocab, hid);
+    bad |= !cok || (tv && !hok);
+    const bool masked = static_cast<float>(hr0) == 0.f;  // din.py: mask = hist != 0
+    float qc[KS], kc[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      qc[s] = cok ? q[s] : 0.f;
+      kc[s] = hok ? kv[s] : 0.f;
+    }
+    // the next item's rows (its ids arrived long ago) and the one after's ids
+    cr0 = cr1;
+    hr0 = hr1;
+    item_rows(cr0, hr0, q, kv);
+    item_ids(it + 2 * DF_NW, cr1, hr1);
+
+    // layer 1 (lane holds h = 16ht + 4kg + r of position t)
+    float y1[HT1][4];
+#pragma unroll
+    for (int ht = 0; ht < HT1; ++ht) {
+      floatx4 acc = b1s[ht * 4 + kg];  // bias as the C input
+#pragma unroll
+      for (int s = 0; s < KS; ++s) acc = mfma16x16x4(fmaf(qc[s], wpv[ht][s], wkd[ht][s]), kc[s], acc);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) acc = mfma16x16x4(wqd[ht][s], qc[s], acc);
+      const floatx4 al = *reinterpret_cast<const floatx4*>(&a1s[t * A1W + 16 * ht + 4 * kg]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) y1[ht][r] = prelu(acc[r], al[r]);
+    }
+    // layer 2 + score: the HT2 accumulators advance together (independent chains)
+    floatx4 acc2[HT2];
+#pragma unroll
+    for (int h2 = 0; h2 < HT2; ++h2) acc2[h2] = b2s[h2 * 4 + kg];
+#pragma unroll
+    for (int ht = 0; ht < HT1; ++ht) {
+      floatx4 wa[HT2];
+#pragma unroll
+      for (int h2 = 0; h2 < HT2; ++h2) wa[h2] = w2s[(h2 * HT1 + ht) * 64 + lane];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int h2 = 0; h2 < HT2; ++h2) acc2[h2] = mfma16x16x4(wa[h2][r], y1[ht][r], acc2[h2]);
+    }
+    float sc = 0.f;
+#pragma unroll
+    for (int h2 = 0; h2 < HT2; ++h2) {
+      const floatx4 al = *reinterpret_cast<const floatx4*>(&a2s[t * A2W + 16 * h2 + 4 * kg]);
+      const floatx4 w3v = w3s[h2 * 4 + kg];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sc = fmaf(prelu(acc2[h2][r], al[r]), w3v[r], sc);
+    }
+    sc += __shfl_xor(sc, 16);
+    sc += __shfl_xor(sc, 32);
+    sc = masked ? -4294967296.0f : sc + b3;
+    // the tile's online-softmax partial (positions past T excluded)
+    float mj = tv ? sc : -INFINITY;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) mj = fmaxf(mj, __shfl_xor(mj, o));
+    const float e = tv ? __expf(sc - mj) : 0.f;
+    const float lj = row16_sum(e);
+    float* pp = part + (size_t)it * (2 + DF_MAXK);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const float os = row16_sum(e * kc[s]);
+      if (col == 0) pp[2 + kg * KS + s] = os;
+    }
+    if (lane == 0) {
+      pp[0] = mj;
+      pp[1] = lj;
+    }
+    if (cnt < 4) DF_STAMP(2 + cnt);
+    ++cnt;
+  }
+  if (__any(bad) && lane == 0) flag_error(a.err);
+  __syncthreads();
+  // merge the tiles of sample w (one wave per sample, lane c < k = channel)
+  if (w < nsmp && lane < K) {
+    const float* pp = part + (size_t)w * NTT * (2 + DF_MAXK);
+    float m = -INFINITY;
+    for (int jj = 0; jj < NTT; ++jj) m = fmaxf(m, pp[jj * (2 + DF_MAXK)]);
+    float l = 0.f, o = 0.f;
+    for (int jj = 0; jj < NTT; ++jj) {
+      const float sj = __expf(pp[jj * (2 + DF_MAXK)] - m);
+      l = fmaf(pp[jj * (2 + DF_MAXK) + 1], sj, l);
+      o = fmaf(pp[jj * (2 + DF_MAXK) + 2 + lane], sj, o);
+    }
+    a.out[(s0 + w) * a.ldo + lane] = o / l;
+  }
+  DF_STAMP(7);
+}
+
 template <int KS, int HT1M, int HT2M, int KIND, bool EXACT>
 static void launch_din(const DinArgs& a, hipStream_t st) {
   // One resident round: 4 workgroups per CU (4 waves/SIMD), the batch split
@@ -420,10 +659,26 @@ static void launch_din(const DinArgs& a, hipStream_t st) {
   din_pool<KIND><<<(unsigned)((a.batch + 3) / 4), 256, 0, st>>>(b);
 }
 
+// din_fused's dynamic LDS for this shape, or 0 when it does not fit
+static size_t df_lds(const DinGeom& g) {
+  const size_t b = (size_t)df_layout(g.NTT, g.HT1, g.HT2).total * sizeof(float);
+  return b + 1024 <= 160 * 1024 ? b : 0;  // (+ the static bias / w3 tiles)
+}
+
 template <int KS, int KIND>
 static void launch_din_h(const DinArgs& a, hipStream_t st) {
-  if (a.g.HT1 == 5 && a.g.HT2 == 3) launch_din<KS, 5, 3, KIND, true>(a, st);  // reference (80, 40)
-  else launch_din<KS, 8, 4, KIND, false>(a, st);
+  if (a.g.HT1 == 5 && a.g.HT2 == 3) {  // reference (80, 40)
+    const size_t lds = df_lds(a.g);
+    if (opt(RS_OPT_DIN_KERNEL) == 0 && lds) {
+      static LdsAttr set;
+      lds_attr(set, (const void*)din_fused<KS, 5, 3, KIND>, lds);
+      din_fused<KS, 5, 3, KIND><<<(unsigned)((a.batch + DF_SPW - 1) / DF_SPW), DF_NW * 64, lds, st>>>(a);
+      return;
+    }
+    launch_din<KS, 5, 3, KIND, true>(a, st);
+  } else {
+    launch_din<KS, 8, 4, KIND, false>(a, st);
+  }
 }
 
 }  // namespace rs

@@ -694,9 +694,16 @@ __global__ __launch_bounds__(16 * 64) void deepfm_fused_ka(EmbedFmArgs a, MlpArg
 // 1.. run as mlp_tower_tile on all 16 waves.  Every spin is bounded.
 constexpr int WS_NL = 8;
 
-__device__ __forceinline__ void lds_wait_ge(int* p, int v) {
+// A logic error must neither hang the kernel nor pass silently: a wait that
+// gives up raises RS_FLAG_TIMEOUT in the launch's error flag (the host layer
+// then raises RSError instead of returning the outputs) and the kernel runs
+// on to its end, so every wave still reaches every barrier and the grid drains.
+__device__ __forceinline__ void lds_wait_ge(int* p, int v, int* err) {
   for (int spins = 0; __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v; ++spins) {
-    if (spins > (1 << 22)) break;  // a logic error must end the kernel, never hang it
+    if (spins > (1 << 22)) {
+      if ((threadIdx.x & 63) == 0) flag_error(err, RS_FLAG_TIMEOUT);
+      break;
+    }
     __builtin_amdgcn_s_sleep(1);
   }
 }
@@ -801,6 +808,9 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
           }
         }
       }
+#ifdef RS_DIAG_STAMPS
+      if (!(burst == 1 && (a.ablate & 32)))  // diagnostic knob: burst 1 never signalled (the timeout test)
+#endif
       lds_signal(&cnt[1 + burst]);
       {
         const MlpArgs& a = t;
@@ -860,7 +870,7 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     const float* ap = tsm + s * RS + 4 * kk;
     // two output tiles, two chains each (MFMA j of a group into chain j & 1)
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc0b = acc0, acc1b = acc0;
-    lds_wait_ge(&cnt[0], a.DB);
+    lds_wait_ge(&cnt[0], a.DB, a.err);
     // one k-group: MFMAs of ring slot U, then the slot refilled 3 groups ahead
     auto step = [&](int i, auto U) {
       constexpr int u = decltype(U)::value;
@@ -882,7 +892,7 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     using U1 = std::integral_constant<int, 1>;
     using U2 = std::integral_constant<int, 2>;
     auto wait_burst = [&](int which) {
-      lds_wait_ge(&cnt[1 + which], WS_NL);  // fields 0..15 / 16.. in the tile
+      lds_wait_ge(&cnt[1 + which], WS_NL, a.err);  // fields 0..15 / 16.. in the tile
       const MlpArgs& a = t;
       MLP_STAMP(2 + which);  // diagnostic hook: burst seen
     };
@@ -952,6 +962,239 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     }
   }
   mlp_tower_tile<NW>(t, tsm, (int64_t)blockIdx.x * 16, ring, fmlog, 1);
+}
+
+// ---- Fused DeepFM, every wave on layer 0 (deepfm_all; RS_OPT_DEEPFM_KERNEL 2)
+// at the Criteo shape (k 16, 26 fields, 1..16 dense features, a 256-unit first
+// layer).  deepfm_ws ran layer 0 on 8 of the 16 waves (2 per SIMD, ~48 cycles
+// per MFMA per SIMD) while the other 8 gathered; here all 16 waves both gather
+// and compute, one 16-column output tile of layer 0 each (4 waves per SIMD
+// share the matrix pipe), and nothing waits on a spin:
+//   * prologue (no id dependence): each wave's own layer-0 weights (ring of
+//     3 k-groups: the dense group, fields 0, 1), its FM B fragments, and the
+//     dense block as its own A fragment of the dense k-group — so the dense
+//     group's MFMAs run inside the row trip, before any row has landed;
+//   * ids of the wave's fields c0 = w and c1 = w + 16 (< 26), decoded against
+//     the kernarg metadata, both rows requested (non-temporal) at once;
+//   * row c0 -> LDS tile + its FM partial (MFMA against the packed [v | w1]
+//     image, q = sum x^2 |v|^2 on the VALU) -> barrier A -> row c1 the same,
+//     layer 0 over the dense group and fields 0..15 -> barrier B -> fields
+//     16..25 (every load unconditional, every wait the compiler's counted one);
+//   * the 16 FM partial tiles meet in LDS (fixed wave order) after barrier B;
+//     waves 8..11, idle in the 8-tile layer 1, finish the FM logit while waves
+//     0..7 start layer 1; layers 1.. run as mlp_tower_tile.
+// Reference: model/deepFM.py:23-31, layer/interaction.py:40-46 (DNN),
+// :106-114 (FM), layer/core.py:273-280 (lookup).
+template <int KIND, int G, bool RF, int GWA = 0, int GWB = 0>
+__global__ __launch_bounds__(16 * 64) void deepfm_all(EmbedFmArgs a, MlpArgs t, FieldMeta m) {
+  typedef Ids<KIND> I;
+  constexpr int NW = 16, F = G - 1;
+  static_assert(F > 16 && F <= 32, "deepfm_all: 17..32 fields (two per wave at most)");
+  extern __shared__ float tsm[];
+  __shared__ floatx4 fm_acc[NW][64];  // FM partial tile of each wave
+  __shared__ float fm_q[NW][16];      // sum_i x_i^2 |v_i|^2 partial of each wave, per sample
+  __shared__ float fmlog[16];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int s = lane & 15, kk = lane >> 4;
+  const int64_t bt = (int64_t)blockIdx.x * 16 + s;
+  const bool valid = bt < a.batch;
+  const int64_t b = valid ? bt : a.batch - 1;  // padded lanes recompute the last sample
+  const int RS = t.rs;
+  float* par = tsm + 32 * RS + NW * 256;
+  {
+    const MlpArgs& a = t;
+    MLP_STAMP(0);
+  }
+  // ---- prologue.  RF (lean front end, the headline kernel's recipe): only
+  // the ids (and the dense features of waves 12..15) go out before the rows;
+  // weights, FM fragments and the bias block follow the rows, and the dense
+  // k-group is read from the LDS tile like the fields.  !RF: the first
+  // weights and every wave's dense A fragment go out with the ids, so the
+  // dense group's MFMAs run inside the row trip.
+  const int c0 = w, c1 = w + 16 < F ? w + 16 : w;  // (waves past F-16: c1 re-reads c0, unused)
+  const bool two = w + 16 < F;                     // wave-uniform
+  const typename I::raw_t rid0 = I::load(a.ids, b * a.id_stride + c0);
+  const typename I::raw_t rid1 = I::load(a.ids, b * a.id_stride + c1);
+  // FM dense k-step dw (waves 12..15; the same waves write the tile's dense group)
+  const int dw = w - (NW - 4);
+  const bool has_dense = dw >= 0 && dw < a.DB;  // wave-uniform
+  const int dwc = dw < 0 ? 0 : (dw < a.DB ? dw : 0);
+  const int de = 4 * dwc + kk;
+  const float dxv = a.dense[b * a.dense_stride + (de < a.nd ? de : 0)];
+  // layer-0 weights of output tile w: k-groups in the order dense (G-1), 0, 1, ..
+  const floatx4* W0 = reinterpret_cast<const floatx4*>(t.prep + t.off[0]) + lane + (int64_t)w * G * 64;
+  auto grp = [](int i) { return i == 0 ? G - 1 : i - 1; };
+  floatx4 ring[3];
+  auto prefill = [&]() {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) ring[u] = W0[(int64_t)grp(u) * 64];
+  };
+  float dA[4];  // !RF: this lane's A values of the dense k-group, dense[b][4kk + j]
+  if constexpr (!RF) {
+    prefill();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = 4 * kk + j;
+      dA[j] = a.dense[b * a.dense_stride + (e < a.nd ? e : 0)];
+    }
+  }
+  // ---- ids -> rows (both fields of the wave at once)
+  int64_t id0, id1;
+  const bool ok0 = I::decode(rid0, m.voc[c0], id0);
+  const bool ok1 = I::decode(rid1, m.voc[c1], id1);
+  const floatx4 x0 = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(a.table + (m.off[c0] + id0) * 16) + kk);
+  const floatx4 x1 = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(a.table + (m.off[c1] + id1) * 16) + kk);
+  if constexpr (RF) prefill();
+  const float* drec = a.prep + (int64_t)dwc * a.dense_rec;
+  const float drv = drec[lane], dnv = drec[64 + kk];
+  const floatx4 bw0 = *reinterpret_cast<const floatx4*>(a.prep + a.field_base + (int64_t)c0 * a.field_rec + lane * 4);
+  const floatx4 bw1 = *reinterpret_cast<const floatx4*>(a.prep + a.field_base + (int64_t)c1 * a.field_rec + lane * 4);
+  const float w0v = a.w0[0];
+  // bias / alpha of every layer -> LDS (visible after barrier A)
+  const int npar = t.ptot;
+  const int pi = threadIdx.x < npar ? threadIdx.x : 0;
+  const float pv = t.prep[t.wtot + pi];
+  bool bad = !ok0 || (two && !ok1);
+  // ---- layer 0, four chains (MFMA j of a k-group into chain j)
+  MacAcc<4> L0;
+  const float* ap = tsm + s * RS + 4 * kk;
+  auto step = [&](int i, auto U) {
+    constexpr int u = decltype(U)::value;
+    floatx4 av;
+    if (!RF && i == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) av[j] = 4 * kk + j < a.nd ? dA[j] : 0.f;
+    } else {
+      av = *reinterpret_cast<const floatx4*>(ap + 16 * grp(i));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    L0.mac4(av, ring[u]);
+    if (i + 3 < G) ring[u] = W0[(int64_t)grp(i + 3) * 64];
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using U0 = std::integral_constant<int, 0>;
+  using U1 = std::integral_constant<int, 1>;
+  using U2 = std::integral_constant<int, 2>;
+  if constexpr (!RF) step(0, U0{});  // the dense group: its A fragment is in registers already
+  // ---- FM partials: the dense k-step, then each field as its row lands
+  floatx4 fa = {0.f, 0.f, 0.f, 0.f};
+  float qn = 0.f;
+  if (dw >= 0) {
+    // the tile's dense group (columns F*16 .. F*16+15, zero past nd), and the FM's dense k-step
+    const int e = 4 * dw + kk;
+    const float x = e < a.nd ? dxv : 0.f;
+    if constexpr (RF) tsm[s * RS + F * 16 + e] = x;
+    if (has_dense) {
+      fa = mfma16x16x4(x, drv, fa);
+      qn = fmaf(x * x, dnv, qn);
+    }
+  }
+  float n0[4], n1[4];
+#pragma unroll
+  for (int tp = 0; tp < 4; ++tp) {
+    n0[tp] = row16_sum(s < a.kfm ? bw0[tp] * bw0[tp] : 0.f);
+    n1[tp] = row16_sum(s < a.kfm ? bw1[tp] * bw1[tp] : 0.f);
+  }
+  if (threadIdx.x < npar) par[pi] = pv;
+  auto put_row = [&](int c, const floatx4& xr, bool ok, const floatx4& bw, const float (&nr)[4]) {
+    const floatx4 x = ok ? xr : floatx4{0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<floatx4*>(tsm + s * RS + c * 16 + 4 * kk) = x;
+#pragma unroll
+    for (int tp = 0; tp < 4; ++tp) {
+      fa = mfma16x16x4(x[tp], bw[tp], fa);
+      qn = fmaf(x[tp] * x[tp], nr[tp], qn);
+    }
+  };
+  put_row(c0, x0, ok0, bw0, n0);
+  __syncthreads();  // A: fields 0..15 (one per wave), the dense group, the bias / alpha block in LDS
+  {
+    const MlpArgs& a = t;
+    MLP_STAMP(2);
+  }
+  if (two) put_row(c1, x1, ok1, bw1, n1);
+  // the wave's FM partial tile (its fields + dense k-step) for the combine
+  fm_acc[w][lane] = fa;
+  qn += __shfl_xor(qn, 16);
+  qn += __shfl_xor(qn, 32);
+  if (lane < 16) fm_q[w][lane] = qn;
+  if (__any(bad && valid) && lane == 0) flag_error(a.err);
+  if constexpr (RF) step(0, U0{});  // the dense group, from the tile
+  // fields 0..15: k-groups 1..16 (ring slots continue 1, 2, 0, ..)
+#pragma unroll
+  for (int i = 1; i <= 16; ++i) {
+    if (i % 3 == 0) step(i, U0{});
+    else if (i % 3 == 1) step(i, U1{});
+    else step(i, U2{});
+  }
+  __syncthreads();  // B: fields 16..F-1 in the tile, the FM partials in LDS
+  {
+    const MlpArgs& a = t;
+    MLP_STAMP(3);
+  }
+  // FM logit of sample w (wave = sample, lane = column < 16): its 16 wave
+  // partials added in wave order — the reads go out before the last layer-0
+  // groups and are summed after them; wave index ww doubles as the q column.
+  float fmv[NW];
+  {
+    const int ln = (w >> 2) * 16 + s, r = w & 3;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) fmv[ww] = fm_acc[ww][ln][r];
+  }
+  const float fq = fm_q[s][w];
+#pragma unroll
+  for (int i = 17; i < G; ++i) {
+    if (i % 3 == 0) step(i, U0{});
+    else if (i % 3 == 1) step(i, U1{});
+    else step(i, U2{});
+  }
+  const floatx4 acc0 = L0.sum();
+  // layer 1's weights: the split-K tail's whole slice, or the ring's first groups
+  constexpr bool TAIL = GWA > 0;
+  floatx4 wr[TAIL ? GWA : 1];
+  floatx4 tring[MLP_R];
+  if constexpr (TAIL) {
+    mlp_tail_fetch<GWA>(t, 1, wr);
+  } else {
+    const int T1 = t.Np[1] >> 4, G1 = t.Kp[1] >> 4;
+    const int S1 = mlp_slices(T1, G1, NW);
+    if (w < T1 * S1) {
+      const MlpItem it = mlp_item(w, T1, G1, S1);
+      mlp_ring_fill(tring, reinterpret_cast<const floatx4*>(t.prep + t.off[1]) + lane + (int64_t)it.t * G1 * 64,
+                    it.g0, it.g1);
+    }
+  }
+  {
+    const float* bias = par + t.poff[0];
+    const float* alpha = bias + t.Np[0];
+    float* out = tsm + 16 * RS;  // layer 0 -> buf1
+    const int col = 16 * w + s;
+    with_act(t.act[0], [&](auto A) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(4 * kk + r) * RS + col] = mlp_act_c<decltype(A)::value>(acc0[r] + bias[col], alpha[col]);
+    });
+  }
+  {
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) v += fmv[ww];
+    float tq = (s < a.kfm ? v * v : 0.f) - fq;
+    float lin = s == a.kfm ? v : 0.f;
+    tq = row16_sum(tq);
+    lin = row16_sum(lin);
+    const float fm = (lin + w0v) + 0.5f * tq;
+    if (lane == 0) {
+      fmlog[w] = fm;
+      const int64_t bb = (int64_t)blockIdx.x * 16 + w;
+      if (bb < a.batch && a.logit) a.logit[bb] = fm;
+    }
+  }
+  {
+    const MlpArgs& a = t;
+    MLP_STAMP(1);
+  }
+  if constexpr (TAIL) mlp_tail_splitk<NW, GWA, GWB>(t, tsm, (int64_t)blockIdx.x * 16, wr, fmlog, 1);
+  else mlp_tower_tile<NW>(t, tsm, (int64_t)blockIdx.x * 16, tring, fmlog, 1);
 }
 
 // Generic fallback (any k / kfm): one 256-thread workgroup per sample.
@@ -1797,11 +2040,39 @@ static bool deepfm_ws_ok(const EmbedFmArgs& a, const MlpArgs& t, const FieldMeta
          opt(RS_OPT_DEEPFM_KERNEL) == 0;
 }
 
+// deepfm_all covers the same shapes as deepfm_ws (every wave owns one of the
+// 16 output tiles of the 256-unit first layer and at most two of the fields)
+static bool deepfm_all_ok(const EmbedFmArgs& a, const MlpArgs& t, const FieldMeta* hm, int KV) {
+  return hm && KV == 4 && a.F == 26 && a.nd >= 1 && a.nd <= 16 && a.DB <= 4 && t.L >= 2 && t.Np[0] == 256 &&
+         t.Kp[0] == 16 * (a.F + 1) && t.ptot <= 1024 && opt(RS_OPT_DEEPFM_KERNEL) >= 2;
+}
+
 template <int KV, int KIND>
 static void launch_deepfm(const EmbedFmArgs& a, const MlpArgs& t, size_t lds, hipStream_t st,
                           const FieldMeta* hm) {
   const unsigned grid = (unsigned)((a.batch + 15) / 16);
   if constexpr (KV == 4) {
+    if (deepfm_all_ok(a, t, hm, KV)) {
+      // the split-K tail at the DeepFM widths (256 -> 128 -> 64 -> 1: 8 + 2
+      // k-groups per wave), the one-role tail for other towers
+      int gwa = 0, gwb = 0;
+      const bool tail = mlp_tail_ok(t.Np, t.Kp, t.N, t.L, 1, gwa, gwb) && gwa == 8 && gwb == 2;
+      static LdsAttr all_set[3];
+      auto go = [&](const void* k, LdsAttr& set, auto launch) {
+        lds_attr(set, k, lds);
+        launch();
+      };
+      if (tail && opt(RS_OPT_DEEPFM_KERNEL) == 2)
+        go((const void*)deepfm_all<KIND, 27, true, 8, 2>, all_set[0],
+           [&] { deepfm_all<KIND, 27, true, 8, 2><<<grid, 16 * 64, lds, st>>>(a, t, *hm); });
+      else if (tail)
+        go((const void*)deepfm_all<KIND, 27, false, 8, 2>, all_set[1],
+           [&] { deepfm_all<KIND, 27, false, 8, 2><<<grid, 16 * 64, lds, st>>>(a, t, *hm); });
+      else
+        go((const void*)deepfm_all<KIND, 27, false>, all_set[2],
+           [&] { deepfm_all<KIND, 27, false><<<grid, 16 * 64, lds, st>>>(a, t, *hm); });
+      return;
+    }
     if (deepfm_ws_ok(a, t, hm, KV)) {
       static LdsAttr ws_set;
       lds_attr(ws_set, (const void*)deepfm_ws<KIND, 27>, lds);
@@ -1810,7 +2081,9 @@ static void launch_deepfm(const EmbedFmArgs& a, const MlpArgs& t, size_t lds, hi
     }
   }
   static LdsAttr lds_set[2];  // opt in to exactly what is needed beyond the default
-  const int ka = hm && a.F <= 32 ? 1 : 0;
+  // the kernarg body is built lean for at most 16 dense k-steps (nd <= 64):
+  // its dense loop is compiled out (embed_fm_body: dense_small = KA || ...)
+  const int ka = hm && a.F <= 32 && a.DB <= 16 ? 1 : 0;
   lds_attr(lds_set[ka], ka ? (const void*)deepfm_fused_ka<KV, KIND> : (const void*)deepfm_fused<KV, KIND>, lds);
   if (ka) deepfm_fused_ka<KV, KIND><<<grid, 16 * 64, lds, st>>>(a, t, *hm);
   else deepfm_fused<KV, KIND><<<grid, 16 * 64, lds, st>>>(a, t);
@@ -1870,6 +2143,9 @@ static int deepfm_run(const void* ids, int id_kind, int64_t id_stride, const flo
   a.dense_rec = fg.dense_rec;
   a.field_rec = fg.field_rec;
   a.field_base = fg.field_base;
+#ifdef RS_DIAG_STAMPS
+  a.ablate = getenv("RS_ABLATE") ? atoi(getenv("RS_ABLATE")) : 0;  // 32: deepfm_ws never signals burst 1
+#endif
   hipStream_t st = as_stream(stream);
   with_id_kind(id_kind, [&](auto K) {
     constexpr int KIND = decltype(K)::value;

@@ -390,6 +390,141 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
   MLP_STAMP(15);
 }
 
+// ---- Split-K tail: the tower after its first layer at the DeepFM / DCN
+// widths (256 -> 128 -> 64 -> 1), every layer on all 16 waves.  The one-role
+// tail (mlp_tower_tile) runs the 8- and 4-tile layers on 8 / 4 waves with a
+// 2-deep weight ring, and its narrow layers stall on the L2 latency of every
+// weight refill (stamps: ~450 cycles per k-group per wave, layer 2 at ~110
+// cycles per MFMA).  Here layer l (T output tiles, G k-groups) is cut into
+// 16 items of one tile and G*T/16 <= 8 k-groups: a wave's whole weight slice
+// (<= 8 KB) is requested at the end of the previous layer, so the MFMAs of a
+// layer wait on nothing but the barrier; the 16 partial tiles meet in LDS and
+// are reduced in part order (+ bias, activation) by all 1024 threads; the
+// one-unit head is folded into the last reduction (wave = sample row, lane =
+// column, a wave sum).  Host side: mlp_tail_ok.
+inline bool mlp_tail_ok(const int* Np, const int* Kp, const int* N, int L, int l0, int& gwa, int& gwb) {
+  // exactly two split layers after l0's caller-run layer, then a one-unit head
+  if (L != l0 + 3 || N[L - 1] != 1 || Np[L - 2] > 64) return false;
+  int gw[2];
+  for (int q = 0; q < 2; ++q) {
+    const int l = l0 + q, T = Np[l] >> 4, G = Kp[l] >> 4;
+    if (T < 1 || T > 16 || 16 % T || G % (16 / T)) return false;
+    gw[q] = G / (16 / T);
+  }
+  gwa = gw[0];
+  gwb = gw[1];
+  return (gwa == 8 && gwb == 2) || (gwa == 4 && gwb == 2) || (gwa == 8 && gwb == 4) || (gwa == 4 && gwb == 1);
+}
+// this wave's weight slice of layer l (item w: tile w % T, k-groups part w / T)
+template <int GW>
+__device__ __forceinline__ void mlp_tail_fetch(const MlpArgs& a, int l, floatx4 (&wr)[GW]) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int T = a.Np[l] >> 4, G = a.Kp[l] >> 4;
+  const int t = w % T, g0 = (w / T) * GW;
+  const floatx4* W = reinterpret_cast<const floatx4*>(a.prep + a.off[l]) + lane + ((int64_t)t * G + g0) * 64;
+#pragma unroll
+  for (int u = 0; u < GW; ++u) wr[u] = W[(int64_t)u * 64];
+}
+// layer l's contraction of this wave's slice -> its partial tile in red
+template <int GW>
+__device__ __forceinline__ void mlp_tail_mac(const MlpArgs& a, int l, const floatx4 (&wr)[GW], const float* in,
+                                             float* red) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int T = a.Np[l] >> 4;
+  const int g0 = (w / T) * GW;
+  const float* ap = in + (lane & 15) * a.rs + 4 * (lane >> 4);
+  floatx4 an[GW];
+#pragma unroll
+  for (int u = 0; u < GW; ++u) an[u] = *reinterpret_cast<const floatx4*>(ap + 16 * (g0 + u));
+  MacAcc<4> acc;
+#pragma unroll
+  for (int u = 0; u < GW; ++u) acc.mac4(an[u], wr[u]);
+  *reinterpret_cast<floatx4*>(red + w * 256 + lane * 4) = acc.sum();
+}
+// sum of the S = 16 / T partial tiles of output (row, col) of layer l, in part order
+__device__ __forceinline__ float mlp_tail_red(const float* red, int T, int row, int col) {
+  const int tt = col >> 4, ln = (row >> 2) * 16 + (col & 15), r = row & 3, S = 16 / T;
+  float v = 0.f;
+  for (int p = 0; p < S; ++p) v += red[(p * T + tt) * 256 + ln * 4 + r];
+  return v;
+}
+// Layers l0, l0+1 (split K over the 16 waves) and the one-unit head l0+2.
+// On entry: layer l0's input is in buf (l0 & 1) (written, barrier not yet
+// taken), wa holds this wave's slice of layer l0 (mlp_tail_fetch), the bias /
+// alpha block is in LDS (par).
+template <int NW, int GWA, int GWB>
+__device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, int64_t m0, const floatx4 (&wa)[GWA],
+                                                const float* extra_lds, int l0) {
+  static_assert(NW == 16, "split-K tail: 16 waves");
+  const int RS = a.rs;
+  float* red = smem + 32 * RS;
+  float* par = red + NW * 256;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float* in = (l0 & 1) ? smem + 16 * RS : smem;
+  float* out = (l0 & 1) ? smem : smem + 16 * RS;
+  const int l1 = l0 + 1, LH = l0 + 2;
+  // ---- layer l0
+  __syncthreads();  // its input complete
+  MLP_STAMP(2 + 2 * l0);
+  mlp_tail_mac<GWA>(a, l0, wa, in, red);
+  MLP_STAMP(3 + 2 * l0);
+  floatx4 wb[GWB];
+  mlp_tail_fetch<GWB>(a, l1, wb);  // the next layer's slice, in flight over the reduction
+  __syncthreads();                 // the 16 partial tiles in red
+  {
+    const float* bias = par + a.poff[l0];
+    const float* alpha = bias + a.Np[l0];
+    const int T = a.Np[l0] >> 4, Np = a.Np[l0];
+    with_act(a.act[l0], [&](auto A) {
+      for (int e = threadIdx.x; e < 16 * Np; e += NW * 64) {
+        const int row = e / Np, col = e - row * Np;
+        out[row * RS + col] = mlp_act_c<decltype(A)::value>(mlp_tail_red(red, T, row, col) + bias[col], alpha[col]);
+      }
+    });
+  }
+  // ---- layer l1
+  __syncthreads();  // its input complete; red free
+  MLP_STAMP(2 + 2 * l1);
+  mlp_tail_mac<GWB>(a, l1, wb, out, red);
+  MLP_STAMP(3 + 2 * l1);
+  // the head's weight of this lane's column (packed head layer: W[k][0] at
+  // lane 16 ((k & 15) >> 2), element k & 3, of k-group k >> 4)
+  const int Np = a.Np[l1];
+  const float hw = lane < a.N[l1] ? a.prep[a.off[LH] + ((int64_t)(lane >> 4) * 64 + 16 * ((lane & 15) >> 2)) * 4 +
+                                           (lane & 3)]
+                                  : 0.f;
+  __syncthreads();  // the 16 partial tiles in red
+  // ---- layer l1's reduction folded with the head: wave = sample row, lane = column
+  float h = 0.f;
+  if (lane < Np) {
+    const float* bias = par + a.poff[l1];
+    const float* alpha = bias + Np;
+    h = mlp_act(mlp_tail_red(red, Np >> 4, w, lane) + bias[lane], a.act[l1], alpha[lane]) * hw;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
+  MLP_STAMP(2 + 2 * LH);
+  if (lane == 0) {
+    const float* hb = par + a.poff[LH];
+    const float v = mlp_act(h + hb[0], a.act[LH], hb[a.Np[LH]]);
+    const int64_t m = m0 + w;
+    if (m < a.M) {
+      if (a.head == 0) {
+        a.y[m * a.ys] = v;
+      } else {
+        float zz = a.c0 * v;
+        if (extra_lds) zz = zz + a.c1 * extra_lds[w];
+        else if (a.extra) zz = zz + a.c1 * a.extra[m];
+        a.y[m * a.ys] = 1.0f / (1.0f + expf(-zz));
+      }
+    }
+  }
+  MLP_STAMP(15);
+}
+
 // Layer-0 ring fill for the wave's first item (issue before anything else).
 template <int NW>
 __device__ __forceinline__ void mlp_first_fill(const MlpArgs& a, floatx4 (&ring)[MLP_R]) {

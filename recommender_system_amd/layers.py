@@ -77,7 +77,7 @@ class _ErrFlag:
         if v != 0:
             self.t.zero_()
             if v & ~_lib.FLAG_BAD_ID:
-                raise _lib.RSError(f"{what}: kernel error flag {v:#x}")
+                raise _lib.RSError(f"{what}: kernel error flag {v:#x} ({_lib.flag_names(v)})")
             raise IndexError(f"{what}: embedding id out of range (indices must be in [0, vocab))")
 
 

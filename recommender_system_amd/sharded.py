@@ -42,17 +42,23 @@ from . import _lib
 from ._lib import call, ptr
 
 
+_FLAG_BITS = 8  # rs_flag bits carried across ranks
+
+
 def raise_flag(f, what, group=None, world=1):
-    """Raise for the rs_flag bits in the device flag `f` (reduced by MAX over
-    the group first when world > 1, so every rank takes the same branch):
-    RS_FLAG_LAYOUT (or any unknown bit) -> RSError, RS_FLAG_BAD_ID ->
-    IndexError (TF's InvalidArgumentError on an out-of-range Embedding id)."""
+    """Raise for the rs_flag bits in the device flag `f` (OR-ed over the group
+    first when world > 1 — one 0/1 word per bit reduced by MAX, since MAX of
+    the masks is not their OR — so every rank sees every bit and takes the
+    same branch): RS_FLAG_LAYOUT / RS_FLAG_TIMEOUT (or any unknown bit) ->
+    RSError, RS_FLAG_BAD_ID alone -> IndexError (TF's InvalidArgumentError on
+    an out-of-range Embedding id)."""
     if world > 1:
-        dist.all_reduce(f, op=dist.ReduceOp.MAX, group=group)
+        per_bit = torch.stack([(f.reshape(-1)[0] >> i) & 1 for i in range(_FLAG_BITS)])
+        dist.all_reduce(per_bit, op=dist.ReduceOp.MAX, group=group)
+        f = (per_bit << torch.arange(_FLAG_BITS, device=per_bit.device, dtype=per_bit.dtype)).sum()
     bits = int(f.item())
     if bits & ~_lib.FLAG_BAD_ID:
-        raise _lib.RSError(f"{what}: device error flag {bits:#x} (RS_FLAG_LAYOUT: the table's field row ranges "
-                           "overlap or decrease)")
+        raise _lib.RSError(f"{what}: device error flag {bits:#x} ({_lib.flag_names(bits)})")
     if bits:
         raise IndexError(f"{what}: embedding id out of range")
 

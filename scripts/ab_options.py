@@ -19,14 +19,14 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-OPTS = {"embed_fm_kernel": 0, "mlp_unroll": 1, "deepfm_kernel": 2}
+OPTS = {"embed_fm_kernel": 0, "mlp_unroll": 1, "deepfm_kernel": 2, "din_kernel": 3}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--option", default="embed_fm_kernel", choices=sorted(OPTS))
     ap.add_argument("--values", default="0,1")
-    ap.add_argument("--workload", default="deepfm", choices=["deepfm", "dcn", "cross", "embed_fm"])
+    ap.add_argument("--workload", default="deepfm", choices=["deepfm", "dcn", "cross", "embed_fm", "din"])
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--vocab", type=float, default=1e7)
     ap.add_argument("--rounds", type=int, default=8)
@@ -50,7 +50,19 @@ def main():
     NP = args.pool
     ids = torch.randint(0, V, (NP, B, F), generator=g, device=dev, dtype=torch.int32)
     dense = torch.rand(NP, B, nd, generator=g, device=dev)
-    if args.workload in ("dcn", "cross"):
+    if args.workload == "din":  # config 4: the attention unit from ids, B 2048, T 100, k 8, (80, 40)
+        Bd, T, kd, Vd = 2048 if args.batch == 4096 else args.batch, 100, 8, 63001
+        B = Bd
+        layer = rs.Attention((80, 40), "prelu", seed=1)
+        layer.build(T, kd)
+        table = torch.randn(Vd, kd, device=dev, generator=g)
+        hist_p = torch.randint(1, Vd, (NP, Bd, T), generator=g, device=dev)
+        hist_p[:, :, 80:] = 0  # padded tails, as Amazon-Electronics histories
+        cand_p = torch.randint(1, Vd, (NP, Bd, 1), generator=g, device=dev)
+
+        def fn(i):
+            outs[i % NP] = layer.forward_ids(table, Vd, hist_p[i % NP], cand_p[i % NP])
+    elif args.workload in ("dcn", "cross"):
         m = rs.DCN(cols, [256, 128, 64], 1, "relu", layer_num=3, embed_dim=k, seed=3, device=dev)
 
         def fn(i):

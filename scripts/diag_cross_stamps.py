@@ -15,6 +15,10 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import recommender_system_amd as rs  # noqa: E402
 from recommender_system_amd import _lib  # noqa: E402
+from pathlib import Path  # noqa: E402
+
+# the CrossNet stamps exist only in the diagnostic build (scripts/build_diag.sh)
+_lib._LIB_PATH = Path(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))) / "recommender_system_amd" / "librs_hip_diag.so"
 
 B, F, V, k = 4096, 26, 1_000_000, 16
 cols = [[{"feat": f"I{i}"} for i in range(13)],

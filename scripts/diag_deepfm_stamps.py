@@ -56,6 +56,8 @@ def main():
         names[3 + 2 * l] = f"l{l}_mac_done"
     if int(os.environ.get("DIAG_DEEPFM_OPT", "1")) == 0:  # split roles: slots 2 / 3 = burst 0 / 1 in
         names[2], names[3] = "burst0_in", "burst1_in"
+    elif int(os.environ.get("DIAG_DEEPFM_OPT", "1")) == 2:  # every wave on layer 0: after barriers A / B
+        names[2], names[3] = "after_A", "after_B"
     names[15] = "end"
     out = {"B": B, "V": V, "deepfm_kernel_option": int(os.environ.get("DIAG_DEEPFM_OPT", "1")), "phases_cycles": {}}
     for j, n in names.items():

@@ -614,13 +614,26 @@ def test_embed_cross_fused(gpu, k, L, B, id_dtype):
 
 
 # ------------------------------------- DIN attention from ids (rs_din_attention_ids_fwd)
+@pytest.mark.parametrize("form", [0, 1])
 @pytest.mark.parametrize("T,k,h,B,id_dtype", [(100, 8, (80, 40), 2048, np.int64), (10, 8, (80, 40), 5, np.int32),
                                               (1, 4, (16, 16), 3, np.int64), (33, 16, (128, 64), 21, np.int32),
-                                              (17, 8, (20, 7), 40, np.int32)])
-def test_din_attention_ids(gpu, T, k, h, B, id_dtype):
+                                              (17, 8, (20, 7), 40, np.int32), (37, 4, (80, 40), 13, np.int32),
+                                              (150, 16, (80, 40), 9, np.int64), (100, 8, (80, 40), 2045, np.int32)])
+def test_din_attention_ids(gpu, form, T, k, h, B, id_dtype):
     """keys = values = table[hist], query = table[cand], mask = hist != 0;
     padded positions keep their (id 0) rows in the pooled values, a fully
-    padded row averages them uniformly — as the reference."""
+    padded row averages them uniformly — as the reference.  form 0 = the
+    one-launch kernel (din_fused, the reference's (80, 40) widths), 1 = the
+    two-launch scores + pool path (RS_OPT_DIN_KERNEL)."""
+    from recommender_system_amd import Attention, _lib
+    prev = _lib.set_option(_lib.OPT_DIN_KERNEL, form)
+    try:
+        _din_ids_case(T, k, h, B, id_dtype)
+    finally:
+        _lib.set_option(_lib.OPT_DIN_KERNEL, prev)
+
+
+def _din_ids_case(T, k, h, B, id_dtype):
     from recommender_system_amd import Attention
     rng = np.random.default_rng(T * k + B)
     V = 5000
@@ -917,14 +930,16 @@ def test_hm_front_end_bit_identical(gpu, F, B, id_dtype):
 
 
 # --------------------------- fused DeepFM kernel forms (RS_OPT_DEEPFM_KERNEL)
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("B,id_dtype,hidden,nd", [(4096, np.int32, [256, 128, 64], 13), (4093, np.int64, [248, 160, 8], 13),
                                                   (33, np.float32, [256, 128], 16), (1, np.int32, [256, 128, 64], 13),
                                                   (300, np.int32, [256, 128, 64], 9)])
 def test_deepfm_kernel_forms(gpu, mlp_unroll, variant, B, id_dtype, hidden, nd):
     """rs_deepfm_fwd_hm in its forms — 0: split wave roles (loader waves
     gather the rows and the FM while compute waves run the first layer as the
-    fields land; the Criteo shape), 1: one role per wave — == the fp64
+    fields land; the Criteo shape), 1: one role per wave, 2: every wave
+    gathers two fields and computes one layer-0 output tile (deepfm_all, the
+    Criteo shape) — == the fp64
     oracle (post-sigmoid 1e-5 relative), the FM logit output too, and an
     out-of-range id raises.  Shapes outside the split form's (nd 9 here) run
     the one-role kernel under both values."""
@@ -987,7 +1002,7 @@ def test_mfma_chain_kernels_match_oracle(gpu, B, hidden):
     lib = _lib.lib()
     prev_k = lib.rs_get_option(_lib.OPT_DEEPFM_KERNEL)
     try:
-        for form in (0, 1):
+        for form in (0, 1, 2):
             _lib.set_option(_lib.OPT_DEEPFM_KERNEL, form)
             fm = torch.empty(B, 1, device=gpu)
             outs[("deepfm", form)] = dfm.forward_fused((dense, ids), fm_logit=fm).clone()
@@ -1000,7 +1015,43 @@ def test_mfma_chain_kernels_match_oracle(gpu, B, hidden):
     p = {"tables": tables_of(dfm.embed_layer), "w0": dfm.fm.w0.cpu().numpy(), "w1": dfm.fm.w1.cpu().numpy(),
          "v": dfm.fm.v.cpu().numpy(), "dnn_hidden": hidden_p, "dnn_out": out_p}
     ref, ref_fm, _ = O.deepfm(None, p, nd=13, inputs=(dense_np, ids_np))
-    for form in (0, 1):
+    for form in (0, 1, 2):
         assert_rel_close(outs[("deepfm", form)], ref, what=f"deepfm form {form}")
         assert_scaled_close(outs[("fm", form)], ref_fm, what=f"deepfm form {form} fm logit")
     assert_scaled_close(outs["fm_logit"], ref_fm, what="fm logit kernel")
+
+
+# --------------------------- wide dense blocks in the fused DeepFM
+@pytest.mark.parametrize("nd,F,B", [(70, 26, 300), (65, 9, 64), (64, 26, 33)])
+def test_deepfm_fused_wide_dense(gpu, nd, F, B):
+    """rs_deepfm_fwd_hm with more than 16 dense k-steps (nd > 64) and F <= 32:
+    the kernarg-metadata body is built for <= 16 dense k-steps, so such shapes
+    must take the streaming-dense body — before the fix the dense columns past
+    64 were dropped from the FM logit and left stale in the tower's tile."""
+    from recommender_system_amd import DeepFM, _lib
+    from tests.helpers import criteo_columns, dnn_params, tables_of
+    rng = np.random.default_rng(nd * 31 + F)
+    vocabs = rng.integers(2, 3000, size=F)
+    m = DeepFM(criteo_columns(vocabs, n_dense=nd, embed_dim=16), 10, 1e-4, 1e-4, [128, 64], 1, "relu",
+               embed_dim=16, seed=5)
+    with torch.no_grad():
+        for l in m.dnn._layers():
+            l.bias.uniform_(-0.1, 0.1)
+        m.embed_layer.table.mul_(10.0)
+    assert m.fused_ok()
+    ids = random_ids(rng, B, vocabs, np.int32)
+    dense = (rng.random((B, nd)) * 2 - 1).astype(np.float32)
+    for form in (0, 1, 2):
+        prev = _lib.set_option(_lib.OPT_DEEPFM_KERNEL, form)
+        try:
+            fm = torch.empty(B, 1, device=gpu)
+            y = m.forward_fused((torch.as_tensor(dense, device=gpu), torch.as_tensor(ids, device=gpu)), fm_logit=fm)
+            torch.cuda.synchronize()
+        finally:
+            _lib.set_option(_lib.OPT_DEEPFM_KERNEL, prev)
+        hidden_p, out_p = dnn_params(m.dnn)
+        p = {"tables": tables_of(m.embed_layer), "w0": m.fm.w0.cpu().numpy(), "w1": m.fm.w1.cpu().numpy(),
+             "v": m.fm.v.cpu().numpy(), "dnn_hidden": hidden_p, "dnn_out": out_p}
+        ref, ref_fm, _ = O.deepfm(None, p, nd=nd, inputs=(dense, ids))
+        assert_rel_close(y, ref, what=f"DeepFM nd={nd} F={F} form {form}")
+        assert_scaled_close(fm, ref_fm, what=f"DeepFM nd={nd} F={F} form {form} fm logit")

@@ -1362,6 +1362,43 @@ def test_raise_flag_keeps_the_flag_bits():
             raise_flag(torch.tensor([bits]), "t")
 
 
+def _flag_or_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from recommender_system_amd import _lib
+    from recommender_system_amd.sharded import raise_flag
+    try:
+        # rank 0 saw a bad id, rank 1 a layout error: every rank must see both
+        f = torch.tensor([_lib.FLAG_BAD_ID if rank == 0 else _lib.FLAG_LAYOUT], dtype=torch.int32)
+        try:
+            raise_flag(f, "t", group=None, world=world)
+            q.put((rank, "no raise"))
+        except _lib.RSError as e:
+            q.put((rank, str(e)))
+        except IndexError as e:
+            q.put((rank, "IndexError " + str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_raise_flag_ors_the_bits_across_ranks():
+    """the ranks' flag masks were reduced by MAX (BAD_ID 1 + LAYOUT
+    2 -> 2, the bad id lost); they are OR-ed now — every rank raises RSError
+    naming both bits (gloo, world 2)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_flag_or_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p_ in procs:
+        p_.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p_ in procs:
+        p_.join(timeout=60)
+        assert p_.exitcode == 0
+    for rank, msg in res:
+        assert "RS_FLAG_BAD_ID" in msg and "RS_FLAG_LAYOUT" in msg, (rank, msg)
+
+
 @pytest.mark.gpu
 def test_gpu_sharded_deepfm_pipelined(gpu):
     """ShardedDeepFM.forward_stream / pipe_step (batch t+1's route + owner
