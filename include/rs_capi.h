@@ -75,8 +75,9 @@ enum rs_flag {
 enum rs_option {
   RS_OPT_EMBED_FM_KERNEL = 0, /* rs_embed_fm_fwd kernel (id inputs, no x_out): 0 = MFMA K-split,
                                  1 = VALU/DPP persistent 8-sample tiles, 2 / 3 = MFMA persistent
-                                 16-sample tiles (2 / 1 resident per CU); shapes a kernel does
-                                 not cover run the K-split one.  See DESIGN.md 4.1                */
+                                 16-sample tiles (2 / 1 resident per CU), 4 = the K-split kernel of
+                                 rs_embed_fm_fwd_hm with its ids through scalar loads; shapes a
+                                 kernel does not cover run the K-split one.  See DESIGN.md 4.1    */
   RS_OPT_MLP_UNROLL = 1,      /* fused MLP towers (rs_mlp_fwd, rs_deepfm_fwd, rs_dcn_fwd): 1 (the
                                  default) = the k-group loop of the common layer widths fully
                                  unrolled (no loop-head wait on the weight ring), 0 = the looped
@@ -92,6 +93,35 @@ enum rs_option {
                                  1 = two launches (din_scores, din_pool).  See DESIGN.md 4.4     */
   RS_OPT_COUNT = 4
 };
+
+/* ------------------------------------------- peer-mapped exchange (§8(e))
+ * An equal-split all-to-all for the sharded lookup's fixed-size record
+ * exchanges without RCCL (csrc/peer.hip, sharded.py PeerExchange): every rank
+ * owns one mailbox (rs_peer_alloc: uncached device memory, zeroed) of
+ * rs_peer_mailbox_bytes(world, block_bytes) bytes = [world][block_bytes] data
+ * + step flags, exports it (rs_peer_ipc_handle: a 64-byte hipIpcMemHandle_t)
+ * and maps every peer's (rs_peer_ipc_open).  rs_peer_a2a is ONE launch per
+ * exchange: rank `rank` writes block p of `send` into rank p's mailbox at
+ * data[rank] once p has flagged its mailbox free for the step, flags it, and
+ * the launch ends when every rank's block of the step is in its own mailbox.
+ * mailboxes: device array [world] of every rank's mailbox base as seen by
+ * this process (its own at [rank]); state: rs_peer_state_bytes() of zeroed
+ * device memory, private to this rank and exchange (the step counter lives
+ * there: graph-capturable).  Kernels that read the received data must run on
+ * `stream` after the call and before the next rs_peer_a2a of the same
+ * mailbox.  Bounded waits (spin_limit polls): a timeout sets RS_FLAG_TIMEOUT
+ * in *err_flag.  block_bytes % 16 == 0, world <= 64, chunks * world <= 1024.
+ * No reference counterpart (the reference has no distributed code).     */
+int64_t rs_peer_state_bytes(void);
+int64_t rs_peer_mailbox_bytes(int world, int64_t block_bytes);
+int rs_peer_alloc(int64_t bytes, void** ptr);
+int rs_peer_free(void* ptr);
+int rs_peer_ipc_handle(void* ptr, void* handle64);
+int rs_peer_ipc_open(const void* handle64, void** ptr);
+int rs_peer_ipc_close(void* ptr);
+int rs_peer_a2a(const void* send, int64_t block_bytes, void* const* mailboxes,
+                int rank, int world, void* state, int chunks,
+                int64_t spin_limit, int* err_flag, rs_stream_t stream);
 
 /* ------------------------------------------------------------------ meta */
 const char* rs_version(void);

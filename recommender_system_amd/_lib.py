@@ -27,6 +27,14 @@ SIGNATURES = {
     "rs_version": (C.c_char_p, []),
     "rs_last_error_string": (C.c_char_p, []),
     "rs_set_option": (I, [I, I]),
+    "rs_peer_state_bytes": (L, []),
+    "rs_peer_mailbox_bytes": (L, [I, L]),
+    "rs_peer_alloc": (I, [L, P]),
+    "rs_peer_free": (I, [P]),
+    "rs_peer_ipc_handle": (I, [P, P]),
+    "rs_peer_ipc_open": (I, [P, P]),
+    "rs_peer_ipc_close": (I, [P]),
+    "rs_peer_a2a": (I, [P, L, P, I, I, P, I, L, P, P]),
     "rs_get_option": (I, [I]),
     "rs_diag_empty": (I, [I, I, P]),
     "rs_diag_wave_slots": (I, [I, I, I, P, P]),

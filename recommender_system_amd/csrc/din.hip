@@ -486,10 +486,13 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
     din_row<KS>(a.table, cid, kg, q);
     din_row<KS>(a.table, hid, kg, kv);
   };
-  // first item's ids and rows go out before the staging loads
+  // the first item's ids and rows go out before the staging loads
   typename I::raw_t cr0, hr0, cr1, hr1;
   item_ids(w, cr0, hr0);
   item_ids(w + DF_NW, cr1, hr1);
+  float q[KS], kv[KS];
+  item_rows(cr0, hr0, q, kv);
+  __builtin_amdgcn_sched_barrier(0);
 
   // ---- stage every position's alphas and the W2^T image: every load of a
   // round is issued before its LDS stores (a load -> store loop pays one L2
@@ -538,8 +541,6 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
     }
   }
   const float b3 = a.prep[g.b3];
-  float q[KS], kv[KS];
-  item_rows(cr0, hr0, q, kv);
   __syncthreads();
   DF_STAMP(1);
 
@@ -565,6 +566,9 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
     hr0 = hr1;
     item_rows(cr0, hr0, q, kv);
     item_ids(it + 2 * DF_NW, cr1, hr1);
+    // pinned here: left alone the scheduler sinks these loads to the end of
+    // the item, and the next item's loop-head vmcnt(0) then pays their trip
+    __builtin_amdgcn_sched_barrier(0);
 
     // layer 1 (lane holds h = 16ht + 4kg + r of position t)
     float y1[HT1][4];

@@ -131,7 +131,27 @@ __global__ void fm_prepare_generic(const float* __restrict__ w1, const float* __
 // row stride tw->rs) instead of x_out, and the DNN tower of mlp_tower.hpp runs
 // on it, closed by sigmoid(c0*dnn + c1*fm) (model/deepFM.py:24-30).
 // A workgroup owns one 16-sample MFMA row tile.
-template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, bool PF = false, bool KA = false>
+// SID (kernarg kernel, RS_OPT_EMBED_FM_KERNEL 4; an A/B of VERDICT r4 item 4):
+// a wave's 16 ids of its field come through the SCALAR unit (16 s_load_dword
+// from the constant address space, wave-uniform addresses) and are moved into
+// the lanes by a select chain — the id trip leaves the vector memory queue
+// that the other workgroups' row traffic fills.
+template <class I>
+__device__ __forceinline__ typename I::raw_t ids_scalar(const EmbedFmArgs& a, int tile, int c, int s) {
+  typedef typename I::raw_t R;
+  const __attribute__((address_space(4))) R* p = (const __attribute__((address_space(4))) R*)a.ids;
+  R v = R(0);
+#pragma unroll
+  for (int si = 0; si < 16; ++si) {
+    int64_t row = (int64_t)tile * 16 + si;
+    row = row < a.batch ? row : a.batch - 1;
+    const R x = p[row * a.id_stride + c];
+    v = s == si ? x : v;
+  }
+  return v;
+}
+
+template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, bool PF = false, bool KA = false, bool SID = false>
 __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArgs* tw, const int tile,
                                               const FieldMeta* km = nullptr) {
   // MC > 0: field slots per wave and pass (owner kernels with few fields)
@@ -323,7 +343,8 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
         } else if constexpr (KA) {  // kernarg metadata: scalar loads, wave-uniform field
           offc[j] = km->off[P.cj[j]];
           vocc[j] = km->voc[P.cj[j]];
-          P.rid[j] = I::load(a.ids, b * a.id_stride + P.cj[j]);
+          if constexpr (SID) P.rid[j] = ids_scalar<I>(a, tile, P.cj[j], s);
+          else P.rid[j] = I::load(a.ids, b * a.id_stride + P.cj[j]);
         } else {
           const int cv = min(cg + j * NW + wv, a.F - 1);
           offc[j] = a.offs[cv];
@@ -576,9 +597,9 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
 // the field metadata by value (rs_embed_fm_fwd_hm): each wave loads its own
 // fields' ids and reads (offset, vocab) through scalar kernarg loads — no LDS
 // id tile, no barrier, no per-wave metadata loads from one hot L2 line
-template <int KV, int NT, int NW, int KIND, bool PF>
+template <int KV, int NT, int NW, int KIND, bool PF, bool SID = false>
 __global__ __launch_bounds__(NW * 64) void embed_fm_mfma_ka(EmbedFmArgs a, FieldMeta m) {
-  embed_fm_body<KV, NT, NW, KIND, false, 1, PF, true>(a, nullptr, blockIdx.x, &m);
+  embed_fm_body<KV, NT, NW, KIND, false, 1, PF, true, SID>(a, nullptr, blockIdx.x, &m);
 }
 
 // ---- sharded FM, partial protocol: combine (requester side) as a block part
@@ -1401,7 +1422,10 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st, const FieldMe
   // (the kernarg kernel is built lean: at most 2 x 16 fields, 16 dense k-steps,
   // no x output — its straight-line code runs from a cold instruction cache)
   if (hm && a.F <= 32 && KIND != 3 && grid <= 512 && a.DB <= 16 && !a.x_out) {
-    embed_fm_mfma_ka<KV, NT, 16, KIND, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
+    if (opt(RS_OPT_EMBED_FM_KERNEL) == 4 && KV == 4 && NT == 1)
+      embed_fm_mfma_ka<KV, NT, 16, KIND, true, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
+    else
+      embed_fm_mfma_ka<KV, NT, 16, KIND, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
     return;
   }
   if (a.F <= 32 && grid > 1024) embed_fm_mfma<KV, NT, 4, KIND, 1, true><<<grid, 4 * 64, 0, st>>>(a);

@@ -63,6 +63,132 @@ def raise_flag(f, what, group=None, world=1):
         raise IndexError(f"{what}: embedding id out of range")
 
 
+class _DevBuf:
+    """A device allocation as a torch tensor view (__cuda_array_interface__)."""
+
+    def __init__(self, ptr_, nbytes):
+        self.__cuda_array_interface__ = {"shape": (int(nbytes),), "typestr": "|u1", "data": (int(ptr_), False),
+                                         "version": 3, "strides": None}
+
+
+class PeerExchange:
+    """Equal-split all-to-all over hipIpc-mapped mailboxes (rs_peer_a2a,
+    csrc/peer.hip) — the RCCL all-to-all's drop-in for the sharded lookup's
+    fixed-size record exchanges.  Every rank allocates one uncached mailbox
+    ([world][block_bytes] data + ready / full step flags), exports its IPC
+    handle, and opens every peer's (handles all-gathered over the group once,
+    before any timed step).  ``all_to_all(send)`` is ONE launch: each rank
+    writes its block for peer p straight into p's mailbox (xGMI stores on an
+    8-GPU node) once p has said its mailbox is free for the step, flags it, and
+    the launch ends when every block of the step is in its own mailbox — the
+    returned tensor (a view of the mailbox) is then valid until the next
+    ``all_to_all`` on this exchange.  Step numbers live on the device, so the
+    call is graph-capturable.  Every wait is bounded: a timeout raises
+    RS_FLAG_TIMEOUT in ``err`` (check with ``check()``).
+
+    Requires every rank's process to see every peer's device (one node) and
+    the HIP dmabuf IPC path (HSA_ENABLE_IPC_MODE_LEGACY=0).  Tested with two
+    processes on one device (tests/test_peer_exchange.py); RCCL stays the
+    default exchange."""
+
+    def __init__(self, block_bytes, group=None, world=None, rank=None, device=None, chunks=None,
+                 spin_limit=1 << 22):
+        self.group = group
+        self.world = int(world) if world is not None else dist.get_world_size(group)
+        self.rank = int(rank) if rank is not None else dist.get_rank(group)
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.block_bytes = int(block_bytes)
+        if self.block_bytes % 16:
+            raise ValueError("PeerExchange: block_bytes must be a multiple of 16")
+        lib = _lib.lib()
+        self.mbox_bytes = int(lib.rs_peer_mailbox_bytes(self.world, self.block_bytes))
+        if self.mbox_bytes < 0:
+            raise ValueError("PeerExchange: bad world / block size")
+        # Setup is collective and fails collectively: a rank whose allocation,
+        # export or mapping fails still takes part in every collective below,
+        # and then every rank raises (no rank is left waiting in a collective).
+        self._mine, self._opened = None, []
+        h = (C.c_uint8 * 64)()
+        err = ""
+        try:
+            mine = C.c_void_p()
+            call("rs_peer_alloc", self.mbox_bytes, C.addressof(mine))
+            self._mine = mine.value
+            call("rs_peer_ipc_handle", self._mine, C.addressof(h))
+        except Exception as e:  # noqa: BLE001 — reported collectively below
+            err = f"rank {self.rank}: {e}"
+        # every rank's [ok | handle (64 B)] — over the group's backend (gloo: CPU tensors)
+        cpu = dist.get_backend(group) == "gloo"
+        ht = torch.tensor([0 if err else 1] + list(bytes(h)), dtype=torch.uint8, device="cpu" if cpu else self.device)
+        allh = [torch.empty_like(ht) for _ in range(self.world)]
+        dist.all_gather(allh, ht, group=group)
+        allh = [a.cpu() for a in allh]
+        ptrs = []
+        if all(int(a[0]) == 1 for a in allh):
+            try:
+                for r in range(self.world):
+                    if r == self.rank:
+                        ptrs.append(self._mine)
+                        continue
+                    hr = (C.c_uint8 * 64)(*allh[r][1:].tolist())
+                    pr = C.c_void_p()
+                    call("rs_peer_ipc_open", C.addressof(hr), C.addressof(pr))
+                    self._opened.append(pr.value)
+                    ptrs.append(pr.value)
+            except Exception as e:  # noqa: BLE001
+                err = err or f"rank {self.rank}: {e}"
+        else:
+            err = err or "a peer failed to allocate / export its mailbox"
+        okt = torch.tensor([0 if err else 1], dtype=torch.int32, device="cpu" if cpu else self.device)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN, group=group)
+        if int(okt.item()) != 1:
+            for p_ in self._opened:
+                _lib.lib().rs_peer_ipc_close(p_)
+            self._opened = []
+            dist.barrier(group=group)
+            if self._mine:
+                _lib.lib().rs_peer_free(self._mine)
+                self._mine = None
+            raise _lib.RSError(f"PeerExchange setup failed ({err or 'on another rank'})")
+        self.mailboxes = torch.tensor(ptrs, dtype=torch.int64, device=self.device)
+        self.state = torch.zeros(int(lib.rs_peer_state_bytes()), dtype=torch.uint8, device=self.device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.recv = torch.as_tensor(_DevBuf(self._mine, self.world * self.block_bytes), device=self.device)
+        if chunks is None:  # ~256 workgroups in all, at least 1 per destination
+            chunks = max(1, min(1024 // self.world, 256 // self.world, -(-self.block_bytes // 16384)))
+        self.chunks = int(chunks)
+        self.spin_limit = int(spin_limit)
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=group)  # every mailbox opened before any rank writes
+
+    def all_to_all(self, send):
+        """send: contiguous device tensor of world * block_bytes bytes (block p
+        for rank p); returns the mailbox view (uint8, world * block_bytes)."""
+        if send.numel() * send.element_size() != self.world * self.block_bytes or not send.is_contiguous():
+            raise ValueError("PeerExchange.all_to_all: send must be contiguous, world * block_bytes bytes")
+        call("rs_peer_a2a", ptr(send), self.block_bytes, ptr(self.mailboxes), self.rank, self.world, ptr(self.state),
+             self.chunks, self.spin_limit, ptr(self.err), _lib.stream())
+        return self.recv
+
+    def check(self, what="PeerExchange"):
+        v = int(self.err.item())
+        if v:
+            self.err.zero_()
+            raise _lib.RSError(f"{what}: device error flag {v:#x} ({_lib.flag_names(v)})")
+
+    def close(self):
+        """Collective: every rank stops writing before any mailbox is unmapped or freed."""
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=self.group)
+        for p_ in self._opened:
+            _lib.lib().rs_peer_ipc_close(p_)
+        self._opened = []
+        dist.barrier(group=self.group)
+        if self._mine:
+            _lib.lib().rs_peer_free(self._mine)
+            self._mine = None
+
+
 class HipShardOps:
     """Local per-rank steps on librs_hip.so kernels."""
 
@@ -556,6 +682,37 @@ class ShardedEmbeddingFM:
         bench forces the RCCL self-exchange)."""
         return self.world > 1 or self._force_exchange
 
+    # -- peer-mapped exchange (PeerExchange) in place of the RCCL all-to-all
+    def use_peer_exchange(self, on=True):
+        """Route the pipelined step's all-to-all (pipe_step / forward_stream)
+        through PeerExchange mailboxes instead of RCCL.  Collective: every
+        rank switches together (the mailboxes are created on first use, in
+        the same order on every rank)."""
+        self._peer_on = bool(on)
+        if not hasattr(self, "_peers"):
+            self._peers = {}
+
+    def _peer(self, name, nbytes):
+        ex = self._peers.get(name)
+        if ex is None or ex.world * ex.block_bytes != nbytes:
+            if ex is not None:
+                ex.close()
+            ex = PeerExchange(nbytes // self.world, group=self.group, world=self.world, rank=self.rank,
+                              device=self.device)
+            self._peers[name] = ex
+        return ex
+
+    def close_peer_exchange(self):
+        """Collective: unmap and free every mailbox (after the last step)."""
+        for ex in getattr(self, "_peers", {}).values():
+            ex.close()
+        self._peers = {}
+        self._peer_on = False
+
+    def _peer_check(self):
+        for ex in getattr(self, "_peers", {}).values():
+            ex.check("sharded lookup (peer exchange)")
+
     def pipe_step(self, prev=None, cur=None, nxt=None):
         """One step of the pipelined partial protocol, for batch t = cur:
           all_to_all                  -> ONE collective: [row ids of t | partials of t-1]
@@ -568,8 +725,13 @@ class ShardedEmbeddingFM:
         B = next(x for x in (cur, prev and prev[0], nxt and nxt[1]) if x is not None).shape[0]
         sb = self._sbufs(B)
         if self.exchanges:
-            dist.all_to_all_single(sb["recv"], sb["send"], group=self.group)
-            self.ops.pipe(self, sb["recv"], sb["send"], prev=prev, cur=cur, nxt=nxt)
+            if getattr(self, "_peer_on", False):
+                # the records land in this rank's mailbox (valid until the next exchange)
+                recv = self._peer("pipe", sb["send"].numel() * 4).all_to_all(sb["send"]).view(torch.int32)
+            else:
+                dist.all_to_all_single(sb["recv"], sb["send"], group=self.group)
+                recv = sb["recv"]
+            self.ops.pipe(self, recv, sb["send"], prev=prev, cur=cur, nxt=nxt)
         else:
             # no exchange: the launch must not write the records it reads, so
             # the two buffers alternate (read "send", write "recv", swap)
@@ -595,6 +757,8 @@ class ShardedEmbeddingFM:
             self.pipe_step(prev, cur, nxt)
         if check:
             raise_flag(self.ops.bad_flag(), "sharded lookup", self.group, self.world)
+            if getattr(self, "_peer_on", False):
+                self._peer_check()
         return outs
 
     # -- the fixed-capacity row exchange (returns rows; forward_slots)
