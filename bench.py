@@ -846,6 +846,53 @@ def _world1_group():
     dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
 
 
+def _peer_leg_deepfm(args, world, model, dense_pool, ids_pool, out, step, rccl_dt):
+    """Config 5's per-batch forward with both exchanges peer-mapped
+    (ShardedDeepFM.use_peer_exchange: row ids through rs_peer_a2a, the
+    owner's rows gathered straight into the requesters' mailboxes by
+    rs_peer_gather_a2a — no rs_gather_rows launch, no row all-to-all).  The
+    same 3 batches through RCCL and through the mailboxes must give
+    bit-identical outputs on every rank; then the timed steps (graph-replayed).
+    Failures are collective and reported; the RCCL value stands."""
+    import torch.distributed as dist
+    npool = ids_pool.shape[0]
+    B = ids_pool.shape[1]
+    try:
+        ref = [model.forward((dense_pool[j], ids_pool[j]), check=True).clone() for j in range(3)]
+        model.use_peer_exchange()
+        got = [model.forward((dense_pool[j], ids_pool[j]), check=True) for j in range(3)]
+        same = torch.tensor([int(all(torch.equal(a, b) for a, b in zip(ref, got)))], dtype=torch.int32,
+                            device=ids_pool.device)
+        dist.all_reduce(same, op=dist.ReduceOp.MIN)
+        identical = bool(same.item())
+        for i in range(args.warmup):
+            step(i)
+        torch.cuda.synchronize()
+        _barrier(world)
+        dt, slot_ms = _timed_graph(step, args.steps, 0, world, chunk=16)
+        fl = model.ops.bad_flag().clone()
+        for ex in model.emb._peers.values():
+            fl |= ex.err
+        dist.all_reduce(fl, op=dist.ReduceOp.MAX)
+        if int(fl.item()):
+            raise RuntimeError(f"peer exchange: device error flag {int(fl.item()):#x}")
+        res = {"samples_per_s": world * args.steps * B / dt, "ms_per_step": dt / args.steps * 1e3,
+               "slot_ms": _max_over_ranks(slot_ms, world), "timing": "HIP graph replay (peer exchange captured)",
+               "bit_identical_to_rccl": identical, "faster_and_identical": identical and dt < rccl_dt,
+               "rccl_ms_per_step": rccl_dt / args.steps * 1e3,
+               "protocol": "rs_shard_row_route, rs_peer_a2a of the row ids (one launch), rs_peer_gather_a2a (the "
+                           "owner's rows straight into the requesters' mailboxes, one launch), rs_deepfm_fwd from "
+                           "the mailbox"}
+    except Exception as e:  # noqa: BLE001 — reported, the RCCL value stands
+        res = {"error": repr(e)[:400]}
+    finally:
+        try:
+            model.close_peer_exchange()
+        except Exception as e:  # noqa: BLE001
+            res = dict(res, close_error=repr(e)[:200])
+    return res
+
+
 def bench_sharded_deepfm(args, world, rank, lite=False):
     """BASELINE config 5 (nested as `config5` in the N > 1 line and as
     `config5_n1` at N = 1): DeepFM forward with ONE 1e8-row table (26 fields x 3,846,154 rows x 16 fp32 = 6.4 GB)
@@ -920,6 +967,8 @@ def bench_sharded_deepfm(args, world, rank, lite=False):
     dist.all_reduce(f, op=dist.ReduceOp.MAX)
     if bool(f.item()):
         raise RuntimeError("sharded DeepFM bench: bad ids during timing")
+    peer = _peer_leg_deepfm(args, world, model, dense_pool, ids_pool, out, step, dt) \
+        if os.environ.get("RS_BENCH_PEER", "1") != "0" else {"skipped": "RS_BENCH_PEER=0"}
     # the fused DeepFM kernel alone, from the exchange buffer of the last step
     rb = model._rbufs(B)
 
@@ -951,7 +1000,13 @@ def bench_sharded_deepfm(args, world, rank, lite=False):
                          "rs_deepfm_fwd in sequence (the comparison for the pipelined value)"}
     cpu = _cpu_leg_config5(args, world, rank, model, dense_pool, ids_pool, out, B)
     res = {"samples_per_s": world * args.steps * B / dt, "ms_per_step": ms, "value_kind": kind,
-           "per_batch": per_batch, "roofline": roof, "exchange": exch, "cpu_baseline": cpu}
+           "per_batch": per_batch, "roofline": roof, "exchange": exch, "cpu_baseline": cpu, "peer_exchange": peer}
+    if peer.get("faster_and_identical"):
+        # the same forward with both exchanges peer-mapped (ids by rs_peer_a2a,
+        # rows gathered into the requesters' mailboxes by rs_peer_gather_a2a):
+        # bit-identical outputs, faster — the value; the RCCL per-batch numbers stay in per_batch
+        res["samples_per_s"], res["ms_per_step"] = peer["samples_per_s"], peer["ms_per_step"]
+        res["value_kind"] = "per_batch_peer_exchange"
     if pipe is not None:
         res["pipelined"] = pipe
     if lite:

@@ -90,7 +90,8 @@ enum rs_option {
                                  requested before / after the first weights).  See DESIGN.md 4.5 */
   RS_OPT_DIN_KERNEL = 3,      /* rs_din_attention_ids_fwd at the reference's (80, 40) widths: 0
                                  (the default) = one launch (scores + softmax + pool, din_fused),
-                                 1 = two launches (din_scores, din_pool).  See DESIGN.md 4.4     */
+                                 1 = two launches (din_scores, din_pool), 2 = one launch with the
+                                 waves 8..15 started late (a stagger A/B).  See DESIGN.md 4.4    */
   RS_OPT_COUNT = 4
 };
 
@@ -122,6 +123,17 @@ int rs_peer_ipc_close(void* ptr);
 int rs_peer_a2a(const void* send, int64_t block_bytes, void* const* mailboxes,
                 int rank, int world, void* state, int chunks,
                 int64_t spin_limit, int* err_flag, rs_stream_t stream);
+/* The owner's row service fused with the row exchange (config 5): block p
+ * for rank p is gathered on the fly — for every word i of ids[p][0..nw) the
+ * 64-B row table[ids[p][i]] of the local shard (k = 16; -1 = a zero row, any
+ * other id outside [0, n_rows) a zero row + RS_FLAG_BAD_ID) — and written
+ * straight into rank p's mailbox (block_bytes = nw * 64); the same flags,
+ * waits and state as rs_peer_a2a.  Replaces rs_gather_rows + the row
+ * all-to-all of sharded.py ShardedDeepFM.                                 */
+int rs_peer_gather_a2a(const int32_t* ids, int64_t nw, const float* table,
+                       int64_t n_rows, int k, void* const* mailboxes, int rank,
+                       int world, void* state, int chunks, int64_t spin_limit,
+                       int* err_flag, rs_stream_t stream);
 
 /* ------------------------------------------------------------------ meta */
 const char* rs_version(void);

@@ -35,6 +35,7 @@ SIGNATURES = {
     "rs_peer_ipc_open": (I, [P, P]),
     "rs_peer_ipc_close": (I, [P]),
     "rs_peer_a2a": (I, [P, L, P, I, I, P, I, L, P, P]),
+    "rs_peer_gather_a2a": (I, [P, L, P, L, I, P, I, I, P, I, L, P, P]),
     "rs_get_option": (I, [I]),
     "rs_diag_empty": (I, [I, I, P]),
     "rs_diag_wave_slots": (I, [I, I, I, P, P]),

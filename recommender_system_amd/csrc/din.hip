@@ -133,6 +133,7 @@ struct DinArgs {
   int64_t batch;
   int* err;
   unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_din_set_dbg)
+  int stagger;              // din_fused: waves 8..15 start ~stagger x 2k cycles late (RS_OPT_DIN_KERNEL 2)
 };
 // (phase stamps only in the diagnostic build, scripts/build_diag.sh)
 #ifdef RS_DIAG_STAMPS
@@ -544,6 +545,11 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
   __syncthreads();
   DF_STAMP(1);
 
+  // stagger (A/B, RS_OPT_DIN_KERNEL 2): the 4 waves of a SIMD (w, w+4, w+8,
+  // w+12) run the same item code in lockstep and reach their VALU phases
+  // together; the waves with one item fewer (8..15) start late instead
+  if (w >= 8)
+    for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(32);
   bool bad = false;
   int cnt = 0;
   for (int it = w; it < nitems; it += DF_NW) {
@@ -673,10 +679,12 @@ template <int KS, int KIND>
 static void launch_din_h(const DinArgs& a, hipStream_t st) {
   if (a.g.HT1 == 5 && a.g.HT2 == 3) {  // reference (80, 40)
     const size_t lds = df_lds(a.g);
-    if (opt(RS_OPT_DIN_KERNEL) == 0 && lds) {
+    if ((opt(RS_OPT_DIN_KERNEL) == 0 || opt(RS_OPT_DIN_KERNEL) == 2) && lds) {
       static LdsAttr set;
       lds_attr(set, (const void*)din_fused<KS, 5, 3, KIND>, lds);
-      din_fused<KS, 5, 3, KIND><<<(unsigned)((a.batch + DF_SPW - 1) / DF_SPW), DF_NW * 64, lds, st>>>(a);
+      DinArgs b = a;
+      b.stagger = opt(RS_OPT_DIN_KERNEL) == 2 ? 2 : 0;
+      din_fused<KS, 5, 3, KIND><<<(unsigned)((a.batch + DF_SPW - 1) / DF_SPW), DF_NW * 64, lds, st>>>(b);
       return;
     }
     launch_din<KS, 5, 3, KIND, true>(a, st);

@@ -1065,7 +1065,13 @@ __global__ __launch_bounds__(16 * 64) void deepfm_all(EmbedFmArgs a, MlpArgs t, 
   const bool ok0 = I::decode(rid0, m.voc[c0], id0);
   const bool ok1 = I::decode(rid1, m.voc[c1], id1);
   const floatx4 x0 = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(a.table + (m.off[c0] + id0) * 16) + kk);
-  const floatx4 x1 = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(a.table + (m.off[c1] + id1) * 16) + kk);
+  // RF: the second field's rows go out only after barrier A, so the first
+  // burst (one row per wave: fields 0..15) does not share the memory system
+  // with it — barrier A waits for 8.4 MB of row lines, not 13.6; the second
+  // burst lands under the first nine k-groups' MFMAs
+  const floatx4* x1p = reinterpret_cast<const floatx4*>(a.table + (m.off[c1] + id1) * 16) + kk;
+  floatx4 x1 = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (!RF) x1 = __builtin_nontemporal_load(x1p);
   if constexpr (RF) prefill();
   const float* drec = a.prep + (int64_t)dwc * a.dense_rec;
   const float drv = drec[lane], dnv = drec[64 + kk];
@@ -1133,20 +1139,31 @@ __global__ __launch_bounds__(16 * 64) void deepfm_all(EmbedFmArgs a, MlpArgs t, 
     const MlpArgs& a = t;
     MLP_STAMP(2);
   }
-  if (two) put_row(c1, x1, ok1, bw1, n1);
-  // the wave's FM partial tile (its fields + dense k-step) for the combine
-  fm_acc[w][lane] = fa;
-  qn += __shfl_xor(qn, 16);
-  qn += __shfl_xor(qn, 32);
-  if (lane < 16) fm_q[w][lane] = qn;
-  if (__any(bad && valid) && lane == 0) flag_error(a.err);
-  if constexpr (RF) step(0, U0{});  // the dense group, from the tile
+  auto fm_publish = [&]() {  // the wave's FM partial tile (its fields + dense k-step) for the combine
+    fm_acc[w][lane] = fa;
+    qn += __shfl_xor(qn, 16);
+    qn += __shfl_xor(qn, 32);
+    if (lane < 16) fm_q[w][lane] = qn;
+    if (__any(bad && valid) && lane == 0) flag_error(a.err);
+  };
+  if constexpr (RF) {
+    x1 = __builtin_nontemporal_load(x1p);  // (unconditional: waves past F-16 re-read their first row)
+    __builtin_amdgcn_sched_barrier(0);
+    step(0, U0{});  // the dense group, from the tile
+  } else {
+    if (two) put_row(c1, x1, ok1, bw1, n1);
+    fm_publish();
+  }
   // fields 0..15: k-groups 1..16 (ring slots continue 1, 2, 0, ..)
 #pragma unroll
   for (int i = 1; i <= 16; ++i) {
     if (i % 3 == 0) step(i, U0{});
     else if (i % 3 == 1) step(i, U1{});
     else step(i, U2{});
+    if (RF && i == 8) {  // the second burst, nine groups after it was requested
+      if (two) put_row(c1, x1, ok1, bw1, n1);
+      fm_publish();
+    }
   }
   __syncthreads();  // B: fields 16..F-1 in the tile, the FM partials in LDS
   {

@@ -49,7 +49,7 @@ constexpr int PEER_MAXW = 64;
 constexpr int PEER_FLAG_STRIDE = 128;  // bytes: each flag on its own line
 
 struct PeerArgs {
-  const char* send;      // [world][block_bytes], local
+  const char* send;      // [world][block_bytes], local (GATHER: unused)
   int64_t block_bytes;   // multiple of 16
   char* const* mbox;     // device array [world]: every rank's mailbox base (mine at [rank])
   int64_t data_bytes;    // world * block_bytes, rounded up to 256 (offset of the flags)
@@ -57,6 +57,12 @@ struct PeerArgs {
   int rank, world, chunks;  // chunks per destination (grid = chunks x world)
   int64_t spin_limit;
   int* err;
+  // GATHER (rs_peer_gather_a2a): block p is gathered on the fly — row ids[p][i]
+  // of the local table shard (k = 16 floats, -1 = a zero row) for every word i
+  const int32_t* ids;  // [world][nw] local row ids (the requests each peer sent me)
+  int64_t nw;
+  const float* table;
+  int64_t n_rows;
 };
 
 __device__ __forceinline__ unsigned long long* peer_flag(char* mbox, int64_t data_bytes, int which, int world,
@@ -74,6 +80,7 @@ __device__ __forceinline__ bool peer_wait_ge(unsigned long long* f, unsigned lon
   return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= v;
 }
 
+template <bool GATHER>
 __global__ __launch_bounds__(256) void peer_a2a_kernel(PeerArgs a) {
   const int c = blockIdx.x, p = blockIdx.y;
   const unsigned long long seq = a.st->seq + 1;
@@ -90,9 +97,23 @@ __global__ __launch_bounds__(256) void peer_a2a_kernel(PeerArgs a) {
   if (ok) {
     const int64_t per = (a.block_bytes / 16 + a.chunks - 1) / a.chunks;  // 16-B words per chunk
     const int64_t w0 = (int64_t)c * per, w1 = min<int64_t>(w0 + per, a.block_bytes / 16);
-    const floatx4* src = reinterpret_cast<const floatx4*>(a.send + (int64_t)p * a.block_bytes);
     floatx4* dst = reinterpret_cast<floatx4*>(a.mbox[p] + (int64_t)a.rank * a.block_bytes);
-    for (int64_t i = w0 + threadIdx.x; i < w1; i += blockDim.x) dst[i] = src[i];
+    if constexpr (GATHER) {
+      // 4 lanes per 64-B row: row ids[p][i >> 2], quarter i & 3 (non-temporal: read once)
+      const int32_t* rid = a.ids + (int64_t)p * a.nw;
+      bool bad = false;
+      for (int64_t i = w0 + threadIdx.x; i < w1; i += blockDim.x) {
+        const int64_t r = rid[i >> 2];
+        floatx4 x = {0.f, 0.f, 0.f, 0.f};
+        if (r >= 0 && r < a.n_rows) x = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(a.table + r * 16) + (i & 3));
+        else bad |= r != -1;
+        dst[i] = x;
+      }
+      if (__any(bad) && (threadIdx.x & 63) == 0) flag_error(a.err);
+    } else {
+      const floatx4* src = reinterpret_cast<const floatx4*>(a.send + (int64_t)p * a.block_bytes);
+      for (int64_t i = w0 + threadIdx.x; i < w1; i += blockDim.x) dst[i] = src[i];
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -216,7 +237,24 @@ extern "C" int rs_peer_a2a(const void* send, int64_t block_bytes, void* const* m
   RS_REQUIRE(chunks >= 1 && (int64_t)chunks * world <= 1024 && spin_limit >= 1, "rs_peer_a2a: bad chunks / limit");
   PeerArgs a{static_cast<const char*>(send), block_bytes, reinterpret_cast<char* const*>(mailboxes),
              ((int64_t)world * block_bytes + 255) / 256 * 256, static_cast<PeerState*>(state), rank, world, chunks,
-             spin_limit, err_flag};
-  peer_a2a_kernel<<<dim3(chunks, world), 256, 0, as_stream(stream)>>>(a);
+             spin_limit, err_flag, nullptr, 0, nullptr, 0};
+  peer_a2a_kernel<false><<<dim3(chunks, world), 256, 0, as_stream(stream)>>>(a);
   return launch_status("rs_peer_a2a");
+}
+
+extern "C" int rs_peer_gather_a2a(const int32_t* ids, int64_t nw, const float* table, int64_t n_rows, int k,
+                                  void* const* mailboxes, int rank, int world, void* state, int chunks,
+                                  int64_t spin_limit, int* err_flag, rs_stream_t stream) {
+  RS_REQUIRE(world >= 1 && world <= PEER_MAXW && rank >= 0 && rank < world, "rs_peer_gather_a2a: bad rank / world");
+  RS_REQUIRE(k == 16, "rs_peer_gather_a2a: k must be 16");
+  RS_REQUIRE(nw >= 0 && n_rows >= 0 && (uintptr_t)table % 16 == 0, "rs_peer_gather_a2a: bad shape / alignment");
+  RS_REQUIRE(mailboxes && state && (nw == 0 || ids) && (n_rows == 0 || table), "rs_peer_gather_a2a: null pointer");
+  RS_REQUIRE(chunks >= 1 && (int64_t)chunks * world <= 1024 && spin_limit >= 1,
+             "rs_peer_gather_a2a: bad chunks / limit");
+  const int64_t block_bytes = nw * 64;
+  PeerArgs a{nullptr, block_bytes, reinterpret_cast<char* const*>(mailboxes),
+             ((int64_t)world * block_bytes + 255) / 256 * 256, static_cast<PeerState*>(state), rank, world, chunks,
+             spin_limit, err_flag, ids, nw, table, n_rows};
+  peer_a2a_kernel<true><<<dim3(chunks, world), 256, 0, as_stream(stream)>>>(a);
+  return launch_status("rs_peer_gather_a2a");
 }

@@ -170,6 +170,18 @@ class PeerExchange:
              self.chunks, self.spin_limit, ptr(self.err), _lib.stream())
         return self.recv
 
+    def gather_all_to_all(self, ids, nw, table, err=None):
+        """The owner's row service fused with the exchange: block p = the
+        64-B rows table[ids[p][i]] (i < nw; -1 = zero row) of this rank's
+        shard, written straight into peer p's mailbox (rs_peer_gather_a2a;
+        block_bytes must be nw * 64).  Returns the mailbox view."""
+        if self.block_bytes != nw * 64 or table.shape[1] != 16 or ids.numel() < self.world * nw:
+            raise ValueError("PeerExchange.gather_all_to_all: block_bytes != nw * 64 or k != 16")
+        call("rs_peer_gather_a2a", ptr(ids), nw, ptr(table), table.shape[0], 16, ptr(self.mailboxes), self.rank,
+             self.world, ptr(self.state), self.chunks, self.spin_limit, ptr(err if err is not None else self.err),
+             _lib.stream())
+        return self.recv
+
     def check(self, what="PeerExchange"):
         v = int(self.err.item())
         if v:
@@ -1091,6 +1103,31 @@ class ShardedDeepFM:
             raise_flag(self.ops.bad_flag(), "sharded DeepFM", self.group, self.world)
         return outs
 
+    # -- peer-mapped exchange (PeerExchange) in place of the two RCCL all-to-alls
+    def use_peer_exchange(self, on=True):
+        """forward's exchanges through PeerExchange mailboxes: the row-id
+        records (rs_peer_a2a), then the owner's rows gathered straight into
+        the requesters' mailboxes (rs_peer_gather_a2a: rs_gather_rows and the
+        row all-to-all become one launch).  Collective; k = 16 only."""
+        if on and self.k != 16:
+            raise ValueError("ShardedDeepFM.use_peer_exchange: k must be 16")
+        self.emb.use_peer_exchange(on)
+
+    def close_peer_exchange(self):
+        self.emb.close_peer_exchange()
+
+    def _peer_rows(self, rb):
+        """Steps 2-4 over the mailboxes; None when this exchange cannot use
+        them (record blocks not 16-B multiples)."""
+        sh = self.emb
+        n = rb["n"]
+        nw = n // self.world
+        if nw % 4 or not isinstance(self.ops, HipShardOps):
+            return None
+        recv = sh._peer("row_ids", n * 4).all_to_all(rb["send"]).view(torch.int32)
+        got = sh._peer("rows", n * 64).gather_all_to_all(recv, nw, sh.table_shard, err=self.ops.err)
+        return got.view(torch.float32).view(n, self.k)
+
     def serve(self, recv, reply):
         """Step 3 (owner): rows of the received record words (-1 -> zero row)."""
         return self.ops.gather_rows_into(self.emb.table_shard, recv, reply)
@@ -1229,17 +1266,21 @@ class ShardedDeepFM:
             self.ops.deepfm_table(self, ids, dense, out)  # world 1: the shard is the whole table
         else:
             rb = self._routed(ids, check)
-            recv = rb["send"]
-            if sh.exchanges:
-                recv = rb["recv"]
-                dist.all_to_all_single(recv, rb["send"], group=self.group)
-            reply = got = self.serve(recv, rb["reply"])
-            if sh.exchanges:
-                got = rb["got"]
-                dist.all_to_all_single(got, reply, group=self.group)
+            got = self._peer_rows(rb) if sh.exchanges and getattr(sh, "_peer_on", False) else None
+            if got is None:
+                recv = rb["send"]
+                if sh.exchanges:
+                    recv = rb["recv"]
+                    dist.all_to_all_single(recv, rb["send"], group=self.group)
+                reply = got = self.serve(recv, rb["reply"])
+                if sh.exchanges:
+                    got = rb["got"]
+                    dist.all_to_all_single(got, reply, group=self.group)
             self.finish(dense, got, rb, out)
         if check:
             raise_flag(self.ops.bad_flag(), "sharded DeepFM", self.group, self.world)
+            if getattr(sh, "_peer_on", False):
+                sh._peer_check()
         return out
 
     __call__ = forward
