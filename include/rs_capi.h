@@ -75,9 +75,8 @@ enum rs_flag {
 enum rs_option {
   RS_OPT_EMBED_FM_KERNEL = 0, /* rs_embed_fm_fwd kernel (id inputs, no x_out): 0 = MFMA K-split,
                                  1 = VALU/DPP persistent 8-sample tiles, 2 / 3 = MFMA persistent
-                                 16-sample tiles (2 / 1 resident per CU), 4 = the K-split kernel of
-                                 rs_embed_fm_fwd_hm with its ids through scalar loads; shapes a
-                                 kernel does not cover run the K-split one.  See DESIGN.md 4.1    */
+                                 16-sample tiles (2 / 1 resident per CU); shapes a kernel does
+                                 not cover run the K-split one.  See DESIGN.md 4.1                */
   RS_OPT_MLP_UNROLL = 1,      /* fused MLP towers (rs_mlp_fwd, rs_deepfm_fwd, rs_dcn_fwd): 1 (the
                                  default) = the k-group loop of the common layer widths fully
                                  unrolled (no loop-head wait on the weight ring), 0 = the looped
@@ -86,8 +85,8 @@ enum rs_option {
                                  first layer): 0 (the default) = split wave roles (loaders +
                                  layer-0 compute waves, deepfm_ws), 1 = one role per wave (gather
                                  + FM, then the tower), 2 / 3 = every wave gathers two fields and
-                                 computes one layer-0 tile, split-K tower tail (deepfm_all; rows
-                                 requested before / after the first weights).  See DESIGN.md 4.5 */
+                                 computes one layer-0 tile, split-K tower tail (deepfm_all; a
+                                 weight ring 3 / 4 k-groups deep).  See DESIGN.md 4.5            */
   RS_OPT_DIN_KERNEL = 3,      /* rs_din_attention_ids_fwd at the reference's (80, 40) widths: 0
                                  (the default) = one launch (scores + softmax + pool, din_fused),
                                  1 = two launches (din_scores, din_pool), 2 = one launch with the

@@ -131,27 +131,7 @@ __global__ void fm_prepare_generic(const float* __restrict__ w1, const float* __
 // row stride tw->rs) instead of x_out, and the DNN tower of mlp_tower.hpp runs
 // on it, closed by sigmoid(c0*dnn + c1*fm) (model/deepFM.py:24-30).
 // A workgroup owns one 16-sample MFMA row tile.
-// SID (kernarg kernel, RS_OPT_EMBED_FM_KERNEL 4; an A/B of VERDICT r4 item 4):
-// a wave's 16 ids of its field come through the SCALAR unit (16 s_load_dword
-// from the constant address space, wave-uniform addresses) and are moved into
-// the lanes by a select chain — the id trip leaves the vector memory queue
-// that the other workgroups' row traffic fills.
-template <class I>
-__device__ __forceinline__ typename I::raw_t ids_scalar(const EmbedFmArgs& a, int tile, int c, int s) {
-  typedef typename I::raw_t R;
-  const __attribute__((address_space(4))) R* p = (const __attribute__((address_space(4))) R*)a.ids;
-  R v = R(0);
-#pragma unroll
-  for (int si = 0; si < 16; ++si) {
-    int64_t row = (int64_t)tile * 16 + si;
-    row = row < a.batch ? row : a.batch - 1;
-    const R x = p[row * a.id_stride + c];
-    v = s == si ? x : v;
-  }
-  return v;
-}
-
-template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, bool PF = false, bool KA = false, bool SID = false>
+template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, bool PF = false, bool KA = false>
 __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArgs* tw, const int tile,
                                               const FieldMeta* km = nullptr) {
   // MC > 0: field slots per wave and pass (owner kernels with few fields)
@@ -343,8 +323,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
         } else if constexpr (KA) {  // kernarg metadata: scalar loads, wave-uniform field
           offc[j] = km->off[P.cj[j]];
           vocc[j] = km->voc[P.cj[j]];
-          if constexpr (SID) P.rid[j] = ids_scalar<I>(a, tile, P.cj[j], s);
-          else P.rid[j] = I::load(a.ids, b * a.id_stride + P.cj[j]);
+          P.rid[j] = I::load(a.ids, b * a.id_stride + P.cj[j]);
         } else {
           const int cv = min(cg + j * NW + wv, a.F - 1);
           offc[j] = a.offs[cv];
@@ -597,9 +576,9 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
 // the field metadata by value (rs_embed_fm_fwd_hm): each wave loads its own
 // fields' ids and reads (offset, vocab) through scalar kernarg loads — no LDS
 // id tile, no barrier, no per-wave metadata loads from one hot L2 line
-template <int KV, int NT, int NW, int KIND, bool PF, bool SID = false>
+template <int KV, int NT, int NW, int KIND, bool PF>
 __global__ __launch_bounds__(NW * 64) void embed_fm_mfma_ka(EmbedFmArgs a, FieldMeta m) {
-  embed_fm_body<KV, NT, NW, KIND, false, 1, PF, true, SID>(a, nullptr, blockIdx.x, &m);
+  embed_fm_body<KV, NT, NW, KIND, false, 1, PF, true>(a, nullptr, blockIdx.x, &m);
 }
 
 // ---- sharded FM, partial protocol: combine (requester side) as a block part
@@ -732,7 +711,7 @@ __device__ __forceinline__ void lds_signal(int* p) {
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int KIND, int G>
+template <int KIND, int G, int GWA = 0, int GWB = 0>
 __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, FieldMeta m) {
   typedef Ids<KIND> I;
   constexpr int NW = 16, F = G - 1, MF = (F + WS_NL - 1) / WS_NL;
@@ -973,44 +952,54 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     const MlpArgs& a = t;
     MLP_STAMP(1);  // loader: rows + FM done; compute wave: layer 0 done
   }
-  {  // layer 1's first weights (this wave's first item of it, if any)
-    const int T1 = t.Np[1] >> 4, G1 = t.Kp[1] >> 4;
-    const int S1 = mlp_slices(T1, G1, NW);
-    if (w < T1 * S1) {
-      const MlpItem it = mlp_item(w, T1, G1, S1);
-      mlp_ring_fill(ring, reinterpret_cast<const floatx4*>(t.prep + t.off[1]) + lane + (int64_t)it.t * G1 * 64,
-                    it.g0, it.g1);
+  if constexpr (GWA > 0) {
+    // the split-K tail (mlp_tail_splitk) at the DeepFM widths: layer 1's whole slice of this wave
+    floatx4 wr[GWA];
+    mlp_tail_fetch<GWA>(t, 1, wr);
+    mlp_tail_splitk<NW, GWA, GWB>(t, tsm, (int64_t)blockIdx.x * 16, wr, fmlog, 1);
+  } else {
+    {  // layer 1's first weights (this wave's first item of it, if any)
+      const int T1 = t.Np[1] >> 4, G1 = t.Kp[1] >> 4;
+      const int S1 = mlp_slices(T1, G1, NW);
+      if (w < T1 * S1) {
+        const MlpItem it = mlp_item(w, T1, G1, S1);
+        mlp_ring_fill(ring, reinterpret_cast<const floatx4*>(t.prep + t.off[1]) + lane + (int64_t)it.t * G1 * 64,
+                      it.g0, it.g1);
+      }
     }
+    mlp_tower_tile<NW>(t, tsm, (int64_t)blockIdx.x * 16, ring, fmlog, 1);
   }
-  mlp_tower_tile<NW>(t, tsm, (int64_t)blockIdx.x * 16, ring, fmlog, 1);
 }
 
-// ---- Fused DeepFM, every wave on layer 0 (deepfm_all; RS_OPT_DEEPFM_KERNEL 2)
-// at the Criteo shape (k 16, 26 fields, 1..16 dense features, a 256-unit first
-// layer).  deepfm_ws ran layer 0 on 8 of the 16 waves (2 per SIMD, ~48 cycles
-// per MFMA per SIMD) while the other 8 gathered; here all 16 waves both gather
-// and compute, one 16-column output tile of layer 0 each (4 waves per SIMD
-// share the matrix pipe), and nothing waits on a spin:
-//   * prologue (no id dependence): each wave's own layer-0 weights (ring of
-//     3 k-groups: the dense group, fields 0, 1), its FM B fragments, and the
-//     dense block as its own A fragment of the dense k-group — so the dense
-//     group's MFMAs run inside the row trip, before any row has landed;
-//   * ids of the wave's fields c0 = w and c1 = w + 16 (< 26), decoded against
-//     the kernarg metadata, both rows requested (non-temporal) at once;
+// ---- Fused DeepFM, every wave on layer 0 (deepfm_all; RS_OPT_DEEPFM_KERNEL 2
+// / 3 = weight ring 3 / 4 k-groups deep) at the Criteo shape (k 16, 26 fields,
+// 1..16 dense features, a 256-unit first layer).  deepfm_ws ran layer 0 on 8
+// of the 16 waves (2 per SIMD, ~48 cycles per MFMA per SIMD) while the other
+// 8 gathered; here all 16 waves both gather and compute, one 16-column output
+// tile of layer 0 each (4 waves per SIMD share the matrix pipe), and nothing
+// spins (two workgroup barriers publish the two row bursts):
+//   * front end (the headline kernel's recipe): only the ids of the wave's
+//     fields c0 = w, c1 = w + 16 (< 26) and the dense features of waves
+//     12..15 go out before the first burst (row c0 of every wave); weights,
+//     FM fragments and the bias block follow it;
 //   * row c0 -> LDS tile + its FM partial (MFMA against the packed [v | w1]
-//     image, q = sum x^2 |v|^2 on the VALU) -> barrier A -> row c1 the same,
-//     layer 0 over the dense group and fields 0..15 -> barrier B -> fields
-//     16..25 (every load unconditional, every wait the compiler's counted one);
-//   * the 16 FM partial tiles meet in LDS (fixed wave order) after barrier B;
-//     waves 8..11, idle in the 8-tile layer 1, finish the FM logit while waves
-//     0..7 start layer 1; layers 1.. run as mlp_tower_tile.
+//     image, q = sum x^2 |v|^2 on the VALU), the dense group written by waves
+//     12..15 -> barrier A -> the second burst (row c1) requested, layer 0
+//     over the dense group and fields 0..15 with row c1 stored under them ->
+//     barrier B -> fields 16..25 (every load unconditional, every wait the
+//     compiler's counted one).  Requesting c1 only after barrier A: barrier A
+//     waits for 8.4 MB of row lines instead of 13.6 (7.5k vs 11.4k cycles);
+//   * the 16 FM partial tiles meet in LDS (fixed wave order); every wave then
+//     finishes one sample's FM logit; layers 1.. run as the split-K tail
+//     (mlp_tail_splitk) at the DeepFM widths, else as mlp_tower_tile.
 // Reference: model/deepFM.py:23-31, layer/interaction.py:40-46 (DNN),
 // :106-114 (FM), layer/core.py:273-280 (lookup).
-template <int KIND, int G, bool RF, int GWA = 0, int GWB = 0>
+template <int KIND, int G, int RD, int GWA = 0, int GWB = 0>
 __global__ __launch_bounds__(16 * 64) void deepfm_all(EmbedFmArgs a, MlpArgs t, FieldMeta m) {
   typedef Ids<KIND> I;
   constexpr int NW = 16, F = G - 1;
   static_assert(F > 16 && F <= 32, "deepfm_all: 17..32 fields (two per wave at most)");
+  static_assert(RD == 3 || RD == 4, "deepfm_all: weight ring 3 or 4 k-groups deep");
   extern __shared__ float tsm[];
   __shared__ floatx4 fm_acc[NW][64];  // FM partial tile of each wave
   __shared__ float fm_q[NW][16];      // sum_i x_i^2 |v_i|^2 partial of each wave, per sample
@@ -1027,83 +1016,62 @@ __global__ __launch_bounds__(16 * 64) void deepfm_all(EmbedFmArgs a, MlpArgs t, 
     const MlpArgs& a = t;
     MLP_STAMP(0);
   }
-  // ---- prologue.  RF (lean front end, the headline kernel's recipe): only
-  // the ids (and the dense features of waves 12..15) go out before the rows;
-  // weights, FM fragments and the bias block follow the rows, and the dense
-  // k-group is read from the LDS tile like the fields.  !RF: the first
-  // weights and every wave's dense A fragment go out with the ids, so the
-  // dense group's MFMAs run inside the row trip.
+  // ---- front end: ids (+ the dense features of waves 12..15), then row c0
   const int c0 = w, c1 = w + 16 < F ? w + 16 : w;  // (waves past F-16: c1 re-reads c0, unused)
   const bool two = w + 16 < F;                     // wave-uniform
   const typename I::raw_t rid0 = I::load(a.ids, b * a.id_stride + c0);
   const typename I::raw_t rid1 = I::load(a.ids, b * a.id_stride + c1);
-  // FM dense k-step dw (waves 12..15; the same waves write the tile's dense group)
-  const int dw = w - (NW - 4);
+  const int dw = w - (NW - 4);                  // FM dense k-step of waves 12..15 (they also write the dense group)
   const bool has_dense = dw >= 0 && dw < a.DB;  // wave-uniform
   const int dwc = dw < 0 ? 0 : (dw < a.DB ? dw : 0);
   const int de = 4 * dwc + kk;
   const float dxv = a.dense[b * a.dense_stride + (de < a.nd ? de : 0)];
-  // layer-0 weights of output tile w: k-groups in the order dense (G-1), 0, 1, ..
-  const floatx4* W0 = reinterpret_cast<const floatx4*>(t.prep + t.off[0]) + lane + (int64_t)w * G * 64;
-  auto grp = [](int i) { return i == 0 ? G - 1 : i - 1; };
-  floatx4 ring[3];
-  auto prefill = [&]() {
-#pragma unroll
-    for (int u = 0; u < 3; ++u) ring[u] = W0[(int64_t)grp(u) * 64];
-  };
-  float dA[4];  // !RF: this lane's A values of the dense k-group, dense[b][4kk + j]
-  if constexpr (!RF) {
-    prefill();
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int e = 4 * kk + j;
-      dA[j] = a.dense[b * a.dense_stride + (e < a.nd ? e : 0)];
-    }
-  }
-  // ---- ids -> rows (both fields of the wave at once)
   int64_t id0, id1;
   const bool ok0 = I::decode(rid0, m.voc[c0], id0);
   const bool ok1 = I::decode(rid1, m.voc[c1], id1);
   const floatx4 x0 = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(a.table + (m.off[c0] + id0) * 16) + kk);
-  // RF: the second field's rows go out only after barrier A, so the first
-  // burst (one row per wave: fields 0..15) does not share the memory system
-  // with it — barrier A waits for 8.4 MB of row lines, not 13.6; the second
-  // burst lands under the first nine k-groups' MFMAs
   const floatx4* x1p = reinterpret_cast<const floatx4*>(a.table + (m.off[c1] + id1) * 16) + kk;
-  floatx4 x1 = {0.f, 0.f, 0.f, 0.f};
-  if constexpr (!RF) x1 = __builtin_nontemporal_load(x1p);
-  if constexpr (RF) prefill();
+  // ---- behind the first burst: layer-0 weights of output tile w (k-groups in
+  // the order dense (G-1), 0, 1, ..), the FM fragments, the bias / alpha block
+  const floatx4* W0 = reinterpret_cast<const floatx4*>(t.prep + t.off[0]) + lane + (int64_t)w * G * 64;
+  auto grp = [](int i) { return i == 0 ? G - 1 : i - 1; };
+  floatx4 ring[RD];
+#pragma unroll
+  for (int u = 0; u < RD; ++u) ring[u] = W0[(int64_t)grp(u) * 64];
   const float* drec = a.prep + (int64_t)dwc * a.dense_rec;
   const float drv = drec[lane], dnv = drec[64 + kk];
   const floatx4 bw0 = *reinterpret_cast<const floatx4*>(a.prep + a.field_base + (int64_t)c0 * a.field_rec + lane * 4);
   const floatx4 bw1 = *reinterpret_cast<const floatx4*>(a.prep + a.field_base + (int64_t)c1 * a.field_rec + lane * 4);
   const float w0v = a.w0[0];
-  // bias / alpha of every layer -> LDS (visible after barrier A)
   const int npar = t.ptot;
   const int pi = threadIdx.x < npar ? threadIdx.x : 0;
   const float pv = t.prep[t.wtot + pi];
   bool bad = !ok0 || (two && !ok1);
-  // ---- layer 0, four chains (MFMA j of a k-group into chain j)
+  // ---- layer 0, four chains (MFMA j of a k-group into chain j), ring slot i % RD
   MacAcc<4> L0;
   const float* ap = tsm + s * RS + 4 * kk;
+  // A fragments one k-group ahead inside a segment (the LDS latency hides
+  // behind the previous group's MFMAs); a segment's first read is issued
+  // after its barrier (seg_start)
+  floatx4 an = {0.f, 0.f, 0.f, 0.f};
+  auto seg_start = [&](int i) { an = *reinterpret_cast<const floatx4*>(ap + 16 * grp(i)); };
   auto step = [&](int i, auto U) {
     constexpr int u = decltype(U)::value;
-    floatx4 av;
-    if (!RF && i == 0) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) av[j] = 4 * kk + j < a.nd ? dA[j] : 0.f;
-    } else {
-      av = *reinterpret_cast<const floatx4*>(ap + 16 * grp(i));
-    }
+    const floatx4 av = an;
+    if (i != 16 && i + 1 < G) an = *reinterpret_cast<const floatx4*>(ap + 16 * grp(i + 1));  // 16: last before barrier B
     __builtin_amdgcn_sched_barrier(0);
     L0.mac4(av, ring[u]);
-    if (i + 3 < G) ring[u] = W0[(int64_t)grp(i + 3) * 64];
+    if (i + RD < G) ring[u] = W0[(int64_t)grp(i + RD) * 64];
     __builtin_amdgcn_sched_barrier(0);
   };
-  using U0 = std::integral_constant<int, 0>;
-  using U1 = std::integral_constant<int, 1>;
-  using U2 = std::integral_constant<int, 2>;
-  if constexpr (!RF) step(0, U0{});  // the dense group: its A fragment is in registers already
+  auto step_i = [&](int i) {
+    switch (i % RD) {
+      case 0: step(i, std::integral_constant<int, 0>{}); break;
+      case 1: step(i, std::integral_constant<int, 1>{}); break;
+      case 2: step(i, std::integral_constant<int, 2>{}); break;
+      default: step(i, std::integral_constant<int, (RD > 3 ? 3 : 0)>{}); break;
+    }
+  };
   // ---- FM partials: the dense k-step, then each field as its row lands
   floatx4 fa = {0.f, 0.f, 0.f, 0.f};
   float qn = 0.f;
@@ -1111,7 +1079,7 @@ __global__ __launch_bounds__(16 * 64) void deepfm_all(EmbedFmArgs a, MlpArgs t, 
     // the tile's dense group (columns F*16 .. F*16+15, zero past nd), and the FM's dense k-step
     const int e = 4 * dw + kk;
     const float x = e < a.nd ? dxv : 0.f;
-    if constexpr (RF) tsm[s * RS + F * 16 + e] = x;
+    tsm[s * RS + F * 16 + e] = x;
     if (has_dense) {
       fa = mfma16x16x4(x, drv, fa);
       qn = fmaf(x * x, dnv, qn);
@@ -1139,30 +1107,22 @@ __global__ __launch_bounds__(16 * 64) void deepfm_all(EmbedFmArgs a, MlpArgs t, 
     const MlpArgs& a = t;
     MLP_STAMP(2);
   }
-  auto fm_publish = [&]() {  // the wave's FM partial tile (its fields + dense k-step) for the combine
-    fm_acc[w][lane] = fa;
-    qn += __shfl_xor(qn, 16);
-    qn += __shfl_xor(qn, 32);
-    if (lane < 16) fm_q[w][lane] = qn;
-    if (__any(bad && valid) && lane == 0) flag_error(a.err);
-  };
-  if constexpr (RF) {
-    x1 = __builtin_nontemporal_load(x1p);  // (unconditional: waves past F-16 re-read their first row)
-    __builtin_amdgcn_sched_barrier(0);
-    step(0, U0{});  // the dense group, from the tile
-  } else {
-    if (two) put_row(c1, x1, ok1, bw1, n1);
-    fm_publish();
-  }
-  // fields 0..15: k-groups 1..16 (ring slots continue 1, 2, 0, ..)
+  // the second burst (unconditional: waves past F-16 re-read their first row)
+  const floatx4 x1 = __builtin_nontemporal_load(x1p);
+  __builtin_amdgcn_sched_barrier(0);
+  // the dense group and fields 0..15: k-groups 0..16; row c1 lands under the first nine
+  seg_start(0);
 #pragma unroll
-  for (int i = 1; i <= 16; ++i) {
-    if (i % 3 == 0) step(i, U0{});
-    else if (i % 3 == 1) step(i, U1{});
-    else step(i, U2{});
-    if (RF && i == 8) {  // the second burst, nine groups after it was requested
+  for (int i = 0; i <= 16; ++i) {
+    step_i(i);
+    if (i == 8) {
       if (two) put_row(c1, x1, ok1, bw1, n1);
-      fm_publish();
+      // the wave's FM partial tile (its fields + dense k-step) for the combine
+      fm_acc[w][lane] = fa;
+      qn += __shfl_xor(qn, 16);
+      qn += __shfl_xor(qn, 32);
+      if (lane < 16) fm_q[w][lane] = qn;
+      if (__any(bad && valid) && lane == 0) flag_error(a.err);
     }
   }
   __syncthreads();  // B: fields 16..F-1 in the tile, the FM partials in LDS
@@ -1180,12 +1140,9 @@ __global__ __launch_bounds__(16 * 64) void deepfm_all(EmbedFmArgs a, MlpArgs t, 
     for (int ww = 0; ww < NW; ++ww) fmv[ww] = fm_acc[ww][ln][r];
   }
   const float fq = fm_q[s][w];
+  seg_start(17);
 #pragma unroll
-  for (int i = 17; i < G; ++i) {
-    if (i % 3 == 0) step(i, U0{});
-    else if (i % 3 == 1) step(i, U1{});
-    else step(i, U2{});
-  }
+  for (int i = 17; i < G; ++i) step_i(i);
   const floatx4 acc0 = L0.sum();
   // layer 1's weights: the split-K tail's whole slice, or the ring's first groups
   constexpr bool TAIL = GWA > 0;
@@ -1439,10 +1396,10 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st, const FieldMe
   // (the kernarg kernel is built lean: at most 2 x 16 fields, 16 dense k-steps,
   // no x output — its straight-line code runs from a cold instruction cache)
   if (hm && a.F <= 32 && KIND != 3 && grid <= 512 && a.DB <= 16 && !a.x_out) {
-    if (opt(RS_OPT_EMBED_FM_KERNEL) == 4 && KV == 4 && NT == 1)
-      embed_fm_mfma_ka<KV, NT, 16, KIND, true, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
-    else
-      embed_fm_mfma_ka<KV, NT, 16, KIND, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
+    // (round 5: the ids through 16 scalar loads per wave and a lane select
+    // chain, off the vector memory queue, ran 7.08 vs 6.12 us per launch,
+    // bit-identical — profiles/r5_ab_scalar_ids.json; not kept)
+    embed_fm_mfma_ka<KV, NT, 16, KIND, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
     return;
   }
   if (a.F <= 32 && grid > 1024) embed_fm_mfma<KV, NT, 4, KIND, 1, true><<<grid, 4 * 64, 0, st>>>(a);
@@ -2098,26 +2055,34 @@ static void launch_deepfm(const EmbedFmArgs& a, const MlpArgs& t, size_t lds, hi
       // k-groups per wave), the one-role tail for other towers
       int gwa = 0, gwb = 0;
       const bool tail = mlp_tail_ok(t.Np, t.Kp, t.N, t.L, 1, gwa, gwb) && gwa == 8 && gwb == 2;
+      const bool ring4 = opt(RS_OPT_DEEPFM_KERNEL) == 3;
       static LdsAttr all_set[3];
       auto go = [&](const void* k, LdsAttr& set, auto launch) {
         lds_attr(set, k, lds);
         launch();
       };
-      if (tail && opt(RS_OPT_DEEPFM_KERNEL) == 2)
-        go((const void*)deepfm_all<KIND, 27, true, 8, 2>, all_set[0],
-           [&] { deepfm_all<KIND, 27, true, 8, 2><<<grid, 16 * 64, lds, st>>>(a, t, *hm); });
+      if (tail && ring4)
+        go((const void*)deepfm_all<KIND, 27, 4, 8, 2>, all_set[0],
+           [&] { deepfm_all<KIND, 27, 4, 8, 2><<<grid, 16 * 64, lds, st>>>(a, t, *hm); });
       else if (tail)
-        go((const void*)deepfm_all<KIND, 27, false, 8, 2>, all_set[1],
-           [&] { deepfm_all<KIND, 27, false, 8, 2><<<grid, 16 * 64, lds, st>>>(a, t, *hm); });
+        go((const void*)deepfm_all<KIND, 27, 3, 8, 2>, all_set[1],
+           [&] { deepfm_all<KIND, 27, 3, 8, 2><<<grid, 16 * 64, lds, st>>>(a, t, *hm); });
       else
-        go((const void*)deepfm_all<KIND, 27, false>, all_set[2],
-           [&] { deepfm_all<KIND, 27, false><<<grid, 16 * 64, lds, st>>>(a, t, *hm); });
+        go((const void*)deepfm_all<KIND, 27, 3>, all_set[2],
+           [&] { deepfm_all<KIND, 27, 3><<<grid, 16 * 64, lds, st>>>(a, t, *hm); });
       return;
     }
     if (deepfm_ws_ok(a, t, hm, KV)) {
-      static LdsAttr ws_set;
-      lds_attr(ws_set, (const void*)deepfm_ws<KIND, 27>, lds);
-      deepfm_ws<KIND, 27><<<grid, 16 * 64, lds, st>>>(a, t, *hm);
+      // layers 1.. as the split-K tail at the DeepFM widths (256 -> 128 -> 64 -> 1), else mlp_tower_tile
+      int gwa = 0, gwb = 0;
+      static LdsAttr ws_set[2];
+      if (mlp_tail_ok(t.Np, t.Kp, t.N, t.L, 1, gwa, gwb) && gwa == 8 && gwb == 2) {
+        lds_attr(ws_set[0], (const void*)deepfm_ws<KIND, 27, 8, 2>, lds);
+        deepfm_ws<KIND, 27, 8, 2><<<grid, 16 * 64, lds, st>>>(a, t, *hm);
+      } else {
+        lds_attr(ws_set[1], (const void*)deepfm_ws<KIND, 27>, lds);
+        deepfm_ws<KIND, 27><<<grid, 16 * 64, lds, st>>>(a, t, *hm);
+      }
       return;
     }
   }

@@ -404,7 +404,7 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
 // column, a wave sum).  Host side: mlp_tail_ok.
 inline bool mlp_tail_ok(const int* Np, const int* Kp, const int* N, int L, int l0, int& gwa, int& gwb) {
   // exactly two split layers after l0's caller-run layer, then a one-unit head
-  if (L != l0 + 3 || N[L - 1] != 1 || Np[L - 2] > 64) return false;
+  if (L != l0 + 3 || N[L - 1] != 1) return false;
   int gw[2];
   for (int q = 0; q < 2; ++q) {
     const int l = l0 + q, T = Np[l] >> 4, G = Kp[l] >> 4;
@@ -426,10 +426,9 @@ __device__ __forceinline__ void mlp_tail_fetch(const MlpArgs& a, int l, floatx4 
 #pragma unroll
   for (int u = 0; u < GW; ++u) wr[u] = W[(int64_t)u * 64];
 }
-// layer l's contraction of this wave's slice -> its partial tile in red
+// layer l's contraction of this wave's slice (its partial tile)
 template <int GW>
-__device__ __forceinline__ void mlp_tail_mac(const MlpArgs& a, int l, const floatx4 (&wr)[GW], const float* in,
-                                             float* red) {
+__device__ __forceinline__ floatx4 mlp_tail_mac(const MlpArgs& a, int l, const floatx4 (&wr)[GW], const float* in) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int T = a.Np[l] >> 4;
@@ -441,19 +440,16 @@ __device__ __forceinline__ void mlp_tail_mac(const MlpArgs& a, int l, const floa
   MacAcc<4> acc;
 #pragma unroll
   for (int u = 0; u < GW; ++u) acc.mac4(an[u], wr[u]);
-  *reinterpret_cast<floatx4*>(red + w * 256 + lane * 4) = acc.sum();
-}
-// sum of the S = 16 / T partial tiles of output (row, col) of layer l, in part order
-__device__ __forceinline__ float mlp_tail_red(const float* red, int T, int row, int col) {
-  const int tt = col >> 4, ln = (row >> 2) * 16 + (col & 15), r = row & 3, S = 16 / T;
-  float v = 0.f;
-  for (int p = 0; p < S; ++p) v += red[(p * T + tt) * 256 + ln * 4 + r];
-  return v;
+  return acc.sum();
 }
 // Layers l0, l0+1 (split K over the 16 waves) and the one-unit head l0+2.
 // On entry: layer l0's input is in buf (l0 & 1) (written, barrier not yet
 // taken), wa holds this wave's slice of layer l0 (mlp_tail_fetch), the bias /
-// alpha block is in LDS (par).
+// alpha block is in LDS (par).  Wave w of a layer with T tiles owns tile
+// w % T, k-part w / T; the waves of parts >= 1 leave their partial tile in
+// LDS and the part-0 wave of each tile adds them in part order (one
+// ds_read_b128 per partial, conflict-free) and runs the tile's epilogue —
+// no all-thread reduction pass.
 template <int NW, int GWA, int GWB>
 __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, int64_t m0, const floatx4 (&wa)[GWA],
                                                 const float* extra_lds, int l0) {
@@ -463,60 +459,83 @@ __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, i
   float* par = red + NW * 256;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int s = lane & 15, kk = lane >> 4;
   float* in = (l0 & 1) ? smem + 16 * RS : smem;
   float* out = (l0 & 1) ? smem : smem + 16 * RS;
   const int l1 = l0 + 1, LH = l0 + 2;
+  // the part-0 wave of tile t: its accumulator + the other parts' partial tiles
+  auto gather_parts = [&](floatx4 acc, int T) {
+    const int S = 16 / T;
+    for (int p = 1; p < S; ++p) {
+      const floatx4 q = *reinterpret_cast<const floatx4*>(red + (w + p * T) * 256 + lane * 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] += q[r];
+    }
+    return acc;
+  };
   // ---- layer l0
+  const int TA = a.Np[l0] >> 4;
   __syncthreads();  // its input complete
   MLP_STAMP(2 + 2 * l0);
-  mlp_tail_mac<GWA>(a, l0, wa, in, red);
+  floatx4 acc = mlp_tail_mac<GWA>(a, l0, wa, in);
   MLP_STAMP(3 + 2 * l0);
+  if (w >= TA) *reinterpret_cast<floatx4*>(red + w * 256 + lane * 4) = acc;
   floatx4 wb[GWB];
-  mlp_tail_fetch<GWB>(a, l1, wb);  // the next layer's slice, in flight over the reduction
-  __syncthreads();                 // the 16 partial tiles in red
-  {
+  mlp_tail_fetch<GWB>(a, l1, wb);  // the next layer's slice, in flight over the hand-off
+  __syncthreads();                 // the partial tiles in red
+  if (w < TA) {
+    acc = gather_parts(acc, TA);
     const float* bias = par + a.poff[l0];
     const float* alpha = bias + a.Np[l0];
-    const int T = a.Np[l0] >> 4, Np = a.Np[l0];
+    const int col = 16 * w + s;
     with_act(a.act[l0], [&](auto A) {
-      for (int e = threadIdx.x; e < 16 * Np; e += NW * 64) {
-        const int row = e / Np, col = e - row * Np;
-        out[row * RS + col] = mlp_act_c<decltype(A)::value>(mlp_tail_red(red, T, row, col) + bias[col], alpha[col]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(4 * kk + r) * RS + col] = mlp_act_c<decltype(A)::value>(acc[r] + bias[col], alpha[col]);
+    });
+  }
+  // ---- layer l1, its epilogue folded with the head
+  const int TB = a.Np[l1] >> 4;
+  __syncthreads();  // its input complete; red free
+  MLP_STAMP(2 + 2 * l1);
+  acc = mlp_tail_mac<GWB>(a, l1, wb, out);
+  MLP_STAMP(3 + 2 * l1);
+  if (w >= TB) *reinterpret_cast<floatx4*>(red + w * 256 + lane * 4) = acc;
+  // the head's weight of this lane's column (packed head layer: W[k][0] at
+  // lane 16 ((k & 15) >> 2), element k & 3, of k-group k >> 4)
+  const int colh = 16 * (w % TB) + s;
+  const float hw = colh < a.N[l1] ? a.prep[a.off[LH] + ((int64_t)(colh >> 4) * 64 + 16 * ((colh & 15) >> 2)) * 4 +
+                                           (colh & 3)]
+                                  : 0.f;
+  __syncthreads();  // the partial tiles in red
+  float* redh = red;  // [TB][16] head partials (red[0 .. 256 TB) is never a partial: parts >= 1 are waves >= TB)
+  if (w < TB) {
+    acc = gather_parts(acc, TB);
+    const float* bias = par + a.poff[l1];
+    const float* alpha = bias + a.Np[l1];
+    with_act(a.act[l1], [&](auto A) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float h = colh < a.N[l1] ? mlp_act_c<decltype(A)::value>(acc[r] + bias[colh], alpha[colh]) * hw : 0.f;
+        h = row16_sum(h);
+        if (s == 0) redh[w * 16 + 4 * kk + r] = h;
       }
     });
   }
-  // ---- layer l1
-  __syncthreads();  // its input complete; red free
-  MLP_STAMP(2 + 2 * l1);
-  mlp_tail_mac<GWB>(a, l1, wb, out, red);
-  MLP_STAMP(3 + 2 * l1);
-  // the head's weight of this lane's column (packed head layer: W[k][0] at
-  // lane 16 ((k & 15) >> 2), element k & 3, of k-group k >> 4)
-  const int Np = a.Np[l1];
-  const float hw = lane < a.N[l1] ? a.prep[a.off[LH] + ((int64_t)(lane >> 4) * 64 + 16 * ((lane & 15) >> 2)) * 4 +
-                                           (lane & 3)]
-                                  : 0.f;
-  __syncthreads();  // the 16 partial tiles in red
-  // ---- layer l1's reduction folded with the head: wave = sample row, lane = column
-  float h = 0.f;
-  if (lane < Np) {
-    const float* bias = par + a.poff[l1];
-    const float* alpha = bias + Np;
-    h = mlp_act(mlp_tail_red(red, Np >> 4, w, lane) + bias[lane], a.act[l1], alpha[lane]) * hw;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
+  __syncthreads();  // the tiles' head partials
   MLP_STAMP(2 + 2 * LH);
-  if (lane == 0) {
+  if (threadIdx.x < 16) {
+    const int row = threadIdx.x;
+    float z = 0.f;
+    for (int t = 0; t < TB; ++t) z += redh[t * 16 + row];  // tile order
     const float* hb = par + a.poff[LH];
-    const float v = mlp_act(h + hb[0], a.act[LH], hb[a.Np[LH]]);
-    const int64_t m = m0 + w;
+    const float v = mlp_act(z + hb[0], a.act[LH], hb[a.Np[LH]]);
+    const int64_t m = m0 + row;
     if (m < a.M) {
       if (a.head == 0) {
         a.y[m * a.ys] = v;
       } else {
         float zz = a.c0 * v;
-        if (extra_lds) zz = zz + a.c1 * extra_lds[w];
+        if (extra_lds) zz = zz + a.c1 * extra_lds[row];
         else if (a.extra) zz = zz + a.c1 * a.extra[m];
         a.y[m * a.ys] = 1.0f / (1.0f + expf(-zz));
       }

@@ -92,7 +92,7 @@ class PeerExchange:
     default exchange."""
 
     def __init__(self, block_bytes, group=None, world=None, rank=None, device=None, chunks=None,
-                 spin_limit=1 << 22):
+                 spin_limit=1 << 24):
         self.group = group
         self.world = int(world) if world is not None else dist.get_world_size(group)
         self.rank = int(rank) if rank is not None else dist.get_rank(group)

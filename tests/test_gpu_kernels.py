@@ -232,19 +232,6 @@ def test_embed_fm_host_meta(gpu, k, kfm, F, nd, B, idt, with_x):
     assert torch.equal(got_logit, ref_logit)
     if with_x:
         assert torch.equal(got_x, ref_x)
-    # the scalar-id form of the kernarg kernel (RS_OPT_EMBED_FM_KERNEL 4): same bits
-    prev = _lib.set_option(_lib.OPT_EMBED_FM_KERNEL, 4)
-    try:
-        sid_logit, _ = run(ids, True)
-        assert err.item() == 0
-        assert torch.equal(sid_logit, ref_logit)
-        bad = ids.copy()
-        bad[B - 1, F - 1] = vocabs[F - 1]
-        run(bad, True)
-        assert err.item() != 0
-        err.zero_()
-    finally:
-        _lib.set_option(_lib.OPT_EMBED_FM_KERNEL, prev)
     tables = [table[o:o + vv] for o, vv in zip(offs, vocabs)]
     x64 = np.concatenate([dense, O.embed_layer(ids, tables, np.float64)], 1)
     assert_scaled_close(got_logit, O.fm_layer(x64, w0, w1, v)[:, 0], what="embed_fm host meta")
@@ -831,7 +818,7 @@ def test_full_size_table_addressing(gpu):
     assert_scaled_close(xin, pref, what="PNN both @16.6 GB")
 
 
-@pytest.mark.parametrize("embed_fm_variant", [0, 1, 2, 3, 4], indirect=True)
+@pytest.mark.parametrize("embed_fm_variant", [0, 1, 2, 3], indirect=True)
 def test_headline_shape_full_size(gpu, embed_fm_variant):
     """The headline configuration itself (BASELINE metric: batch 4096, 26 x
     1e7 x 16 fp32 table = 16.6 GB, uniform int32 ids over the full range):
