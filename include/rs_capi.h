@@ -89,8 +89,7 @@ enum rs_option {
                                  weight ring 3 / 4 k-groups deep).  See DESIGN.md 4.5            */
   RS_OPT_DIN_KERNEL = 3,      /* rs_din_attention_ids_fwd at the reference's (80, 40) widths: 0
                                  (the default) = one launch (scores + softmax + pool, din_fused),
-                                 1 = two launches (din_scores, din_pool), 2 = one launch with the
-                                 waves 8..15 started late (a stagger A/B).  See DESIGN.md 4.4    */
+                                 1 = two launches (din_scores, din_pool).  See DESIGN.md 4.4     */
   RS_OPT_COUNT = 4
 };
 

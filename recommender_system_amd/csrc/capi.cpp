@@ -28,7 +28,7 @@ int launch_status(const char* what) {
 // that thread makes, so concurrent callers never see each other's choices.
 // defaults: K-split headline kernel, unrolled towers, split-role DeepFM, one-launch DIN attention
 static thread_local int g_opt[RS_OPT_COUNT] = {0, 1, 0, 0};
-static const int g_opt_hi[RS_OPT_COUNT] = {3, 1, 3, 2};
+static const int g_opt_hi[RS_OPT_COUNT] = {3, 1, 3, 1};
 int opt(int option) { return (option >= 0 && option < RS_OPT_COUNT) ? g_opt[option] : 0; }
 }  // namespace rs
 

@@ -133,7 +133,6 @@ struct DinArgs {
   int64_t batch;
   int* err;
   unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_din_set_dbg)
-  int stagger;              // din_fused: waves 8..15 start ~stagger x 2k cycles late (RS_OPT_DIN_KERNEL 2)
 };
 // (phase stamps only in the diagnostic build, scripts/build_diag.sh)
 #ifdef RS_DIAG_STAMPS
@@ -425,7 +424,7 @@ __global__ __launch_bounds__(256) void din_pool(DinArgs a) {
 #define DF_STAMP(i)                                                                                            \
   do {                                                                                                         \
     if (a.dbg && (threadIdx.x & 63) == 0)                                                                      \
-      a.dbg[((int64_t)blockIdx.x * DF_NW + (threadIdx.x >> 6)) * 8 + (i)] = __builtin_amdgcn_s_memtime();      \
+      a.dbg[((int64_t)blockIdx.x * DF_NW + (threadIdx.x >> 6)) * 16 + (i)] = __builtin_amdgcn_s_memtime();     \
   } while (0)
 #else
 #define DF_STAMP(i) \
@@ -436,15 +435,16 @@ constexpr int DF_SPW = 8;     // samples per workgroup
 constexpr int DF_NW = 16;     // waves per workgroup
 constexpr int DF_MAXK = 16;   // embedding width (k) at most
 
-struct DfLayout {  // dynamic LDS (floats): a1s | a2s | w2s | part
-  int a1, a2, w2, part, total;
+struct DfLayout {  // dynamic LDS (floats): a1s | a2s | w2s | w1s (layer-1 lane images) | part
+  int a1, a2, w2, w1, part, total;
 };
-__host__ __device__ inline DfLayout df_layout(int NTT, int HT1, int HT2) {
+__host__ __device__ inline DfLayout df_layout(int NTT, int HT1, int HT2, int KS) {
   DfLayout L;
   L.a1 = 0;
   L.a2 = L.a1 + NTT * 16 * (HT1 * 16 + 4);
   L.w2 = L.a2 + NTT * 16 * (HT2 * 16 + 4);
-  L.part = L.w2 + HT2 * HT1 * 64 * 4;
+  L.w1 = L.w2 + HT2 * HT1 * 64 * 4;
+  L.part = L.w1 + 3 * HT1 * KS * 64;
   L.total = L.part + DF_SPW * NTT * (2 + DF_MAXK);
   return L;
 }
@@ -455,7 +455,7 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
   constexpr int K = 4 * KS;
   const DinGeom& g = a.g;
   const int NTT = g.NTT, T = g.T;
-  const DfLayout L = df_layout(NTT, HT1, HT2);
+  const DfLayout L = df_layout(NTT, HT1, HT2, KS);
   extern __shared__ float dsm[];
   float* a1s = dsm + L.a1;  // [NTT*16][HT1*16 + 4]
   float* a2s = dsm + L.a2;  // [NTT*16][HT2*16 + 4]
@@ -487,42 +487,57 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
     din_row<KS>(a.table, cid, kg, q);
     din_row<KS>(a.table, hid, kg, kv);
   };
-  // the first item's ids and rows go out before the staging loads
+  // the first items' ids go out first; the first rows are requested right
+  // after the first staging round's loads (their id trip overlaps it)
   typename I::raw_t cr0, hr0, cr1, hr1;
   item_ids(w, cr0, hr0);
   item_ids(w + DF_NW, cr1, hr1);
   float q[KS], kv[KS];
-  item_rows(cr0, hr0, q, kv);
   __builtin_amdgcn_sched_barrier(0);
 
   // ---- stage every position's alphas and the W2^T image: every load of a
   // round is issued before its LDS stores (a load -> store loop pays one L2
   // round trip per iteration: 7.7k cycles of staging in the first version)
   {
-    const float* pa1 = a.prep + g.a1;
-    const float* pa2 = a.prep + g.a2;
+    // 16-B loads and stores (round 5: 4-B ones issued 4x the vector memory
+    // instructions — 51 per wave with the per-lane constants — and the
+    // staging took 5.8k-7.7k cycles); rows of HT*16 floats never straddle a float4
+    const floatx4* pa1 = reinterpret_cast<const floatx4*>(a.prep + g.a1);
+    const floatx4* pa2 = reinterpret_cast<const floatx4*>(a.prep + g.a2);
     const floatx4* pw2 = reinterpret_cast<const floatx4*>(a.prep + g.w2);
-    const int n1 = NTT * 16 * HT1 * 16, n2 = NTT * 16 * HT2 * 16, nw2 = HT2 * HT1 * 64;
-    constexpr int R1 = 12, R2 = 8, NTH = DF_NW * 64;
+    const int n1 = NTT * 16 * HT1 * 4, n2 = NTT * 16 * HT2 * 4, nw2 = HT2 * HT1 * 64;  // float4s
+    constexpr int R1 = 3, R2 = 2, NTH = DF_NW * 64, W1 = HT1 * 4, W2 = HT2 * 4;
     for (int b1 = 0, b2 = 0, bw = 0; b1 < n1 || b2 < n2 || bw < nw2; b1 += R1 * NTH, b2 += R2 * NTH, bw += NTH) {
-      float v1[R1], v2[R2];
-      floatx4 vw;
+      floatx4 v1[R1], v2[R2], vw;
 #pragma unroll
       for (int u = 0; u < R1; ++u) v1[u] = pa1[min(b1 + u * NTH + (int)threadIdx.x, n1 - 1)];  // clamped: unconditional
 #pragma unroll
       for (int u = 0; u < R2; ++u) v2[u] = pa2[min(b2 + u * NTH + (int)threadIdx.x, n2 - 1)];
       vw = pw2[min(bw + (int)threadIdx.x, nw2 - 1)];
+      if (b1 == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        item_rows(cr0, hr0, q, kv);
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int u = 0; u < R1; ++u) {
         const int i = b1 + u * NTH + threadIdx.x;
-        if (i < n1) a1s[(i / (HT1 * 16)) * A1W + i % (HT1 * 16)] = v1[u];
+        if (i < n1) *reinterpret_cast<floatx4*>(a1s + (i / W1) * A1W + 4 * (i % W1)) = v1[u];
       }
 #pragma unroll
       for (int u = 0; u < R2; ++u) {
         const int i = b2 + u * NTH + threadIdx.x;
-        if (i < n2) a2s[(i / (HT2 * 16)) * A2W + i % (HT2 * 16)] = v2[u];
+        if (i < n2) *reinterpret_cast<floatx4*>(a2s + (i / W2) * A2W + 4 * (i % W2)) = v2[u];
       }
       if (bw + (int)threadIdx.x < nw2) w2s[bw + threadIdx.x] = vw;
+    }
+    // the layer-1 lane images (wkd | wp | wqd, contiguous in prep) once per
+    // workgroup: each wave reads its 3 x HT1 x KS values from LDS after the
+    // barrier instead of 30 4-B global loads per wave
+    {
+      const int nl = 3 * HT1 * KS * 16;  // float4s
+      const floatx4* pl = reinterpret_cast<const floatx4*>(a.prep + g.wkd);
+      for (int i = threadIdx.x; i < nl; i += NTH) reinterpret_cast<floatx4*>(dsm + L.w1)[i] = pl[i];
     }
     if (threadIdx.x < HT1 * 16) reinterpret_cast<float*>(b1s)[threadIdx.x] = a.prep[g.b1 + threadIdx.x];
     if (threadIdx.x < HT2 * 16) {
@@ -530,26 +545,26 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
       reinterpret_cast<float*>(w3s)[threadIdx.x] = a.prep[g.w3 + threadIdx.x];
     }
   }
-  float wkd[HT1][KS], wpv[HT1][KS], wqd[HT1][KS];
-#pragma unroll
-  for (int ht = 0; ht < HT1; ++ht) {
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int64_t o = (int64_t)(ht * KS + s) * 64 + lane;
-      wkd[ht][s] = a.prep[g.wkd + o];
-      wpv[ht][s] = a.prep[g.wp + o];
-      wqd[ht][s] = a.prep[g.wqd + o];
-    }
-  }
   const float b3 = a.prep[g.b3];
+  DF_STAMP(6);  // staging stores issued (before the barrier)
   __syncthreads();
   DF_STAMP(1);
+  float wkd[HT1][KS], wpv[HT1][KS], wqd[HT1][KS];
+  {
+    const float* w1s = dsm + L.w1;  // [wkd | wp | wqd], each [HT1][KS][64]
+    const int img = HT1 * KS * 64;
+#pragma unroll
+    for (int ht = 0; ht < HT1; ++ht) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int o = (ht * KS + s) * 64 + lane;
+        wkd[ht][s] = w1s[o];
+        wpv[ht][s] = w1s[img + o];
+        wqd[ht][s] = w1s[2 * img + o];
+      }
+    }
+  }
 
-  // stagger (A/B, RS_OPT_DIN_KERNEL 2): the 4 waves of a SIMD (w, w+4, w+8,
-  // w+12) run the same item code in lockstep and reach their VALU phases
-  // together; the waves with one item fewer (8..15) start late instead
-  if (w >= 8)
-    for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(32);
   bool bad = false;
   int cnt = 0;
   for (int it = w; it < nitems; it += DF_NW) {
@@ -576,6 +591,7 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
     // the item, and the next item's loop-head vmcnt(0) then pays their trip
     __builtin_amdgcn_sched_barrier(0);
 
+    if (cnt == 0) DF_STAMP(8);  // item 0: its operands in registers, MFMAs start
     // layer 1 (lane holds h = 16ht + 4kg + r of position t)
     float y1[HT1][4];
 #pragma unroll
@@ -589,6 +605,7 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) y1[ht][r] = prelu(acc[r], al[r]);
     }
+    if (cnt == 0) DF_STAMP(9);  // item 0: layer 1 done
     // layer 2 + score: the HT2 accumulators advance together (independent chains)
     floatx4 acc2[HT2];
 #pragma unroll
@@ -603,6 +620,7 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
 #pragma unroll
         for (int h2 = 0; h2 < HT2; ++h2) acc2[h2] = mfma16x16x4(wa[h2][r], y1[ht][r], acc2[h2]);
     }
+    if (cnt == 0) DF_STAMP(10);  // item 0: layer 2 issued
     float sc = 0.f;
 #pragma unroll
     for (int h2 = 0; h2 < HT2; ++h2) {
@@ -671,7 +689,7 @@ static void launch_din(const DinArgs& a, hipStream_t st) {
 
 // din_fused's dynamic LDS for this shape, or 0 when it does not fit
 static size_t df_lds(const DinGeom& g) {
-  const size_t b = (size_t)df_layout(g.NTT, g.HT1, g.HT2).total * sizeof(float);
+  const size_t b = (size_t)df_layout(g.NTT, g.HT1, g.HT2, g.KS).total * sizeof(float);
   return b + 1024 <= 160 * 1024 ? b : 0;  // (+ the static bias / w3 tiles)
 }
 
@@ -679,11 +697,10 @@ template <int KS, int KIND>
 static void launch_din_h(const DinArgs& a, hipStream_t st) {
   if (a.g.HT1 == 5 && a.g.HT2 == 3) {  // reference (80, 40)
     const size_t lds = df_lds(a.g);
-    if ((opt(RS_OPT_DIN_KERNEL) == 0 || opt(RS_OPT_DIN_KERNEL) == 2) && lds) {
+    if (opt(RS_OPT_DIN_KERNEL) == 0 && lds) {
       static LdsAttr set;
       lds_attr(set, (const void*)din_fused<KS, 5, 3, KIND>, lds);
       DinArgs b = a;
-      b.stagger = opt(RS_OPT_DIN_KERNEL) == 2 ? 2 : 0;
       din_fused<KS, 5, 3, KIND><<<(unsigned)((a.batch + DF_SPW - 1) / DF_SPW), DF_NW * 64, lds, st>>>(b);
       return;
     }

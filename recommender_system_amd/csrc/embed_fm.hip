@@ -760,7 +760,21 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
         if (s <= a.kfm) bw[p] = *reinterpret_cast<const floatx4*>(a.prep + a.field_base + (int64_t)c * a.field_rec + lane * 4);
       }
     }
-    for (int i = threadIdx.x; i < t.ptot; i += WS_NL * 64) par[i] = t.prep[t.wtot + i];
+    // burst 0's rows go out before the barrier (round 5: the bias-block copy
+    // that used to sit here — two dependent L2 trips — moved to the compute
+    // waves, which wait for the rows anyway)
+    floatx4 xs0[2];
+    bool ok0[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = l + WS_NL * q;
+      ok0[q] = false;
+      if (q < MF && c < F) {
+        int64_t id;
+        ok0[q] = I::decode(rid[q], m.voc[c], id);
+        xs0[q] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(a.table + (m.off[c] + id) * 16) + kk);
+      }
+    }
     __syncthreads();  // the counters start at 0 (the compute waves pass the same barrier)
     floatx4 ac[4];  // four accumulation chains (MFMA tp into chain tp)
 #pragma unroll
@@ -787,6 +801,11 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int p = 2 * burst + q, c = l + WS_NL * p;
+        if (burst == 0) {
+          xs[q] = xs0[q];
+          ok[q] = ok0[q];
+          continue;
+        }
         ok[q] = false;
         if (p < MF && c < F) {
           int64_t id;
@@ -867,6 +886,13 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
       r1[u] = W1[(int64_t)grp(u) * 64];
     }
     __syncthreads();  // the counters start at 0
+    // the bias / alpha block -> LDS for the layers after the first (visible
+    // at the tail's first barrier); this layer's epilogue reads its 4 values
+    // per lane from global memory, so no hand-off among the compute waves
+    for (int i = threadIdx.x - WS_NL * 64; i < t.ptot; i += (NW - WS_NL) * 64) par[i] = t.prep[t.wtot + i];
+    const int ecol0 = 16 * c8 + s, ecol1 = ecol0 + 16 * WS_NL;
+    const float* pb = t.prep + t.wtot + t.poff[0];
+    const float eb0 = pb[ecol0], eb1 = pb[ecol1], ea0 = pb[t.Np[0] + ecol0], ea1 = pb[t.Np[0] + ecol1];
     const float* ap = tsm + s * RS + 4 * kk;
     // two output tiles, two chains each (MFMA j of a group into chain j & 1)
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc0b = acc0, acc1b = acc0;
@@ -936,15 +962,13 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
       acc0[i] += acc0b[i];
       acc1[i] += acc1b[i];
     }
-    const float* bias = par + t.poff[0];
-    const float* alpha = bias + t.Np[0];
     float* out = tsm + 16 * RS;  // layer 0 -> buf1
     with_act(t.act[0], [&](auto A) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = 4 * kk + r, col0 = 16 * c8 + s, col1 = col0 + 16 * WS_NL;
-        out[row * RS + col0] = mlp_act_c<decltype(A)::value>(acc0[r] + bias[col0], alpha[col0]);
-        out[row * RS + col1] = mlp_act_c<decltype(A)::value>(acc1[r] + bias[col1], alpha[col1]);
+        const int row = 4 * kk + r;
+        out[row * RS + ecol0] = mlp_act_c<decltype(A)::value>(acc0[r] + eb0, ea0);
+        out[row * RS + ecol1] = mlp_act_c<decltype(A)::value>(acc1[r] + eb1, ea1);
       }
     });
   }

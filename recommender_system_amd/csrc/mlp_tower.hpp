@@ -495,17 +495,17 @@ __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, i
   }
   // ---- layer l1, its epilogue folded with the head
   const int TB = a.Np[l1] >> 4;
+  // the head's weight of this lane's column (packed head layer: W[k][0] at
+  // lane 16 ((k & 15) >> 2), element k & 3, of k-group k >> 4), requested
+  // before the barrier (an L2 trip the part-0 epilogue would otherwise wait for)
+  const int colh = 16 * (w % TB) + s;
+  const float hw = a.prep[a.off[LH] + ((int64_t)(min(colh, a.Np[l1] - 1) >> 4) * 64 +
+                                       16 * ((colh & 15) >> 2)) * 4 + (colh & 3)];
   __syncthreads();  // its input complete; red free
   MLP_STAMP(2 + 2 * l1);
   acc = mlp_tail_mac<GWB>(a, l1, wb, out);
   MLP_STAMP(3 + 2 * l1);
   if (w >= TB) *reinterpret_cast<floatx4*>(red + w * 256 + lane * 4) = acc;
-  // the head's weight of this lane's column (packed head layer: W[k][0] at
-  // lane 16 ((k & 15) >> 2), element k & 3, of k-group k >> 4)
-  const int colh = 16 * (w % TB) + s;
-  const float hw = colh < a.N[l1] ? a.prep[a.off[LH] + ((int64_t)(colh >> 4) * 64 + 16 * ((colh & 15) >> 2)) * 4 +
-                                           (colh & 3)]
-                                  : 0.f;
   __syncthreads();  // the partial tiles in red
   float* redh = red;  // [TB][16] head partials (red[0 .. 256 TB) is never a partial: parts >= 1 are waves >= TB)
   if (w < TB) {
@@ -515,7 +515,7 @@ __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, i
     with_act(a.act[l1], [&](auto A) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float h = colh < a.N[l1] ? mlp_act_c<decltype(A)::value>(acc[r] + bias[colh], alpha[colh]) * hw : 0.f;
+        float h = colh < a.N[l1] ? mlp_act_c<decltype(A)::value>(acc[r] + bias[colh], alpha[colh]) * hw : 0.f;  // (padded columns: 0)
         h = row16_sum(h);
         if (s == 0) redh[w * 16 + 4 * kk + r] = h;
       }

@@ -1,8 +1,9 @@
 """Per-wave s_memtime stamps of the one-launch DIN attention unit (din_fused)
 at the config-4 shape (B 2048, T 100, k 8, (80, 40)): cycles from the
 workgroup's first stamp, median over workgroups of the median wave and the
-slowest wave.  Slots: 0 start, 1 staged (alphas + W2 in LDS, first rows
-in), 2..5 the wave's items 0..3 done, 7 end (tiles merged, output written).
+slowest wave.  Slots: 0 start, 6 staging stores issued, 1 staged (after the
+barrier), 8 / 9 / 10 item 0's MFMAs start / layer 1 done / layer 2 issued,
+2..5 the wave's items 0..3 done, 7 end (tiles merged, output written).
 Needs the diagnostic build (scripts/build_diag.sh)."""
 import ctypes as C
 import json
@@ -33,15 +34,16 @@ for _ in range(20):
     layer.forward_ids(table, V, hist, cand)
 torch.cuda.synchronize()
 nwg = (B + 7) // 8
-dbg = torch.zeros(nwg * 16 * 8, dtype=torch.int64, device="cuda")
+dbg = torch.zeros(nwg * 16 * 16, dtype=torch.int64, device="cuda")
 lib.rs_diag_din_set_dbg(dbg.data_ptr())
 layer.forward_ids(table, V, hist, cand)
 torch.cuda.synchronize()
 lib.rs_diag_din_set_dbg(None)
-d = dbg.cpu().numpy().reshape(nwg, 16, 8).astype(np.int64)
+d = dbg.cpu().numpy().reshape(nwg, 16, 16).astype(np.int64)
 t0 = d[:, :, 0].min(axis=1, keepdims=True)
 out = {"B": B, "T": T, "phases_cycles": {}}
-for j, n in {0: "start", 1: "staged", 2: "item0", 3: "item1", 4: "item2", 5: "item3", 7: "end"}.items():
+for j, n in {0: "start", 6: "staging_stored", 1: "staged", 8: "item0_mfma_start", 9: "item0_l1_done",
+             10: "item0_l2_issued", 2: "item0", 3: "item1", 4: "item2", 5: "item3", 7: "end"}.items():
     ok = d[:, :, j] > 0
     if not ok.any():
         continue
