@@ -428,6 +428,19 @@ int rs_din_attention_ids_fwd(const void* hist, int id_kind, int64_t hist_stride,
                              int H2, const float* prepared, float* scores,
                              float* out, int64_t out_stride, int64_t batch,
                              int* err_flag, rs_stream_t stream);
+/* ... and the candidate rows table[cand] into cand_out [B, k] (rows
+ * cand_out_stride floats apart; an out-of-range id writes a zero row and sets
+ * *err_flag), the copy DIN.call concatenates beside the pooled rows
+ * (model/din.py:73,83-84): the same launch, no separate candidate gather.   */
+int rs_din_attention_ids_cand_fwd(const void* hist, int id_kind,
+                                  int64_t hist_stride, const void* cand,
+                                  int64_t cand_stride, int T, int k,
+                                  const float* table, int64_t vocab, int H1,
+                                  int H2, const float* prepared, float* scores,
+                                  float* out, int64_t out_stride,
+                                  float* cand_out, int64_t cand_out_stride,
+                                  int64_t batch, int* err_flag,
+                                  rs_stream_t stream);
 
 /* --------------------------------------------------- dense tower (a7, a15)
  * Keras Dense: y = act(x @ W + bias), W:[K,N] (Keras (in,out) orientation),

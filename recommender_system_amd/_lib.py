@@ -69,6 +69,7 @@ SIGNATURES = {
     "rs_din_prepared_size": (L, [I, I, I, I]),
     "rs_din_prepare": (I, [P, P, P, I, P, P, P, I, P, P, I, I, P, P]),
     "rs_din_attention_ids_fwd": (I, [P, I, L, P, L, I, I, P, L, I, I, P, P, P, L, L, P, P]),
+    "rs_din_attention_ids_cand_fwd": (I, [P, I, L, P, L, I, I, P, L, I, I, P, P, P, L, P, L, L, P, P]),
     "rs_dense_fwd": (I, [P, L, P, P, P, I, P, L, L, I, I, P]),
     "rs_dense_prelu_rows_fwd": (I, [P, L, P, P, P, I, P, L, L, I, I, P]),
     "rs_din_attention_gen_workspace_size": (L, [L, I, I, I, P]),
@@ -187,6 +188,9 @@ class RSError(RuntimeError):
     pass
 
 
+_ALLOW_MISSING = False  # scripts only: bind an older build that lacks newer entries
+
+
 def lib():
     """Load (once) and return the bound library; raises if it is missing."""
     global _lib
@@ -200,6 +204,8 @@ def lib():
                     "(python -c 'import __graft_entry__ as g; g.build()')")
             h = C.CDLL(str(_LIB_PATH))
             for name, (res, args) in SIGNATURES.items():
+                if _ALLOW_MISSING and not hasattr(h, name):
+                    continue  # an older build under A/B (scripts/ab_options.py --lib)
                 fn = getattr(h, name)
                 fn.restype = res
                 fn.argtypes = args

@@ -133,6 +133,8 @@ struct DinArgs {
   int64_t batch;
   int* err;
   unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_din_set_dbg)
+  float* cand_out;          // optional [B, k] copy of the candidate rows (table[cand]), rows ldc floats apart
+  int64_t ldc;
 };
 // (phase stamps only in the diagnostic build, scripts/build_diag.sh)
 #ifdef RS_DIAG_STAMPS
@@ -400,6 +402,11 @@ __global__ __launch_bounds__(256) void din_pool(DinArgs a) {
   float v = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   for (int o = k; o < 64; o <<= 1) v += __shfl_xor(v, o);
   if (lane < k) a.out[b * a.ldo + lane] = v / sum;
+  if (a.cand_out && lane < k) {  // the candidate row (an OOR id: a zero row, flagged by din_scores)
+    int64_t cid;
+    const bool ok = I::decode(I::load(a.cand, b * a.cand_stride), a.vocab, cid);
+    a.cand_out[b * a.ldc + lane] = ok ? a.table[cid * k + lane] : 0.f;
+  }
 }
 
 // ---- One-launch DIN attention unit (din_fused; RS_OPT_DIN_KERNEL 0, the
@@ -410,13 +417,16 @@ __global__ __launch_bounds__(256) void din_pool(DinArgs a) {
 // slice of each layer) and the W2^T image are staged in LDS once per
 // workgroup; item (sample, tile) = one 16-position MFMA tile exactly as in
 // din_scores (layer 1 regrouped per sample, layer 1's accumulators are layer
-// 2's B operand), the wave's next item's ids and rows requested while the
-// current one computes.  Each item ends with its tile's online-softmax
-// partial {m_j = max s_t, l_j = sum e^(s_t - m_j), o_j = sum e^(s_t - m_j)
-// key_t} in LDS; after one barrier a wave per sample merges its tiles
-// (m = max m_j, weights e^(m_j - m)) and writes out[b] = o / l.  Items are
-// dealt round-robin to the waves (w, w + 16, ..): at 8 samples x 7 tiles
-// every SIMD runs 14 items.  Masking as the reference (din.py: hist != 0 ->
+// 2's B operand), the wave's next item's rows requested while the current
+// one computes (the ids are read once per workgroup into LDS).  Only LIVE
+// tiles (>= 1 unmasked position) are items: a fully masked tile's scores
+// are the mask value whatever the MLP gives, and its merge weight is exactly
+// 0.  Each item ends with its tile's online-softmax partial {m_j = max s_t,
+// l_j = sum e^(s_t - m_j), o_j = sum e^(s_t - m_j) key_t} in LDS; after one
+// barrier a wave per sample merges its live tiles (m = max m_j, weights
+// e^(m_j - m)) and writes out[b] = o / l.  Live items are dealt round-robin
+// to the waves (w, w + 16, ..): with no masking, 8 samples x 7 tiles put 14
+// items on every SIMD.  Masking as the reference (din.py: hist != 0 ->
 // score -2^32 + 1 in fp32 = -4294967296): a fully masked row averages its
 // keys; an out-of-range id reads a zero row and sets the flag (din_pool's
 // rule).  Reference: layer/interaction.py:369-406, model/din.py:56-80.
@@ -434,6 +444,7 @@ __global__ __launch_bounds__(256) void din_pool(DinArgs a) {
 constexpr int DF_SPW = 8;     // samples per workgroup
 constexpr int DF_NW = 16;     // waves per workgroup
 constexpr int DF_MAXK = 16;   // embedding width (k) at most
+constexpr int DF_TMAX = 128;  // history length at most (8 position tiles)
 
 struct DfLayout {  // dynamic LDS (floats): a1s | a2s | w2s | w1s (layer-1 lane images) | part
   int a1, a2, w2, w1, part, total;
@@ -468,30 +479,53 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
   const int col = lane & 15, kg = lane >> 4;
   const int64_t s0 = (int64_t)blockIdx.x * DF_SPW;
   const int nsmp = (int)min<int64_t>(DF_SPW, a.batch - s0);
-  const int nitems = nsmp * NTT;
   DF_STAMP(0);
 
-  // the wave's items: it = w + 16 m  ->  (sample it / NTT, tile it % NTT)
-  auto item_ids = [&](int it, typename I::raw_t& craw, typename I::raw_t& hraw) {
-    const int itc = it < nitems ? it : nitems - 1;  // clamped: loads stay in bounds, results unused
-    const int si = itc / NTT, j = itc - si * NTT;
-    const int64_t b = s0 + si;
-    const int t = 16 * j + col;
-    craw = I::load(a.cand, b * a.cand_stride);
-    hraw = I::load(a.hist, b * a.hist_stride + (t < T ? t : 0));
+  // ---- the workgroup's ids: wave s < nsmp loads sample s's history ids
+  // (positions lane, lane + 64) and its candidate id into LDS and marks its
+  // LIVE tiles, the 16-position tiles holding at least one unmasked position.
+  // A tile whose valid positions are all masked adds exactly nothing to its
+  // sample's pool when the sample has a live tile: its scores are the mask
+  // value -2^32 whatever the MLP computes, so its merge weight
+  // e^(-2^32 - m) is 0 in fp32 and the merge adds l_j x 0 and o_j x 0.  So
+  // only live tiles run the MLP (bit-identical output); a sample with no live
+  // tile runs all its tiles (the fully-masked average of din.py's softmax).
+  __shared__ typename I::raw_t hs[DF_SPW][DF_TMAX];
+  __shared__ typename I::raw_t cs[DF_SPW];
+  __shared__ unsigned tmask[DF_SPW];
+  typename I::raw_t h0 = 0, h1 = 0, c0 = 0;
+  float cq = 0.f;
+  if (w < nsmp) {
+    const int64_t b = s0 + w;
+    if (lane < T) h0 = I::load(a.hist, b * a.hist_stride + lane);
+    if (lane + 64 < T) h1 = I::load(a.hist, b * a.hist_stride + lane + 64);
+    c0 = I::load(a.cand, b * a.cand_stride);
+  }
+  auto ids_to_lds = [&]() {
+    if (w < nsmp) {
+      hs[w][lane] = h0;
+      hs[w][lane + 64] = h1;
+      if (lane == 0) cs[w] = c0;
+      if (a.cand_out) {  // the candidate row for the caller's concat, written at the merge
+        int64_t cid;
+        const bool ok = I::decode(c0, a.vocab, cid);
+        cq = ok && lane < K ? a.table[cid * K + lane] : 0.f;
+      }
+      const uint64_t l0 = __ballot(lane < T && static_cast<float>(h0) != 0.f);  // din.py: mask = hist != 0
+      const uint64_t l1 = __ballot(lane + 64 < T && static_cast<float>(h1) != 0.f);
+      unsigned m = 0;
+      for (int j = 0; j < NTT; ++j) m |= (((j < 4 ? l0 >> (16 * j) : l1 >> (16 * (j - 4))) & 0xffffu) != 0) << j;
+      if (lane == 0) tmask[w] = m ? m : (1u << NTT) - 1;
+    }
   };
-  auto item_rows = [&](typename I::raw_t craw, typename I::raw_t hraw, float (&q)[KS], float (&kv)[KS]) {
+  auto item_rows = [&](int code, float (&q)[KS], float (&kv)[KS]) {  // code = sample * NTT + tile
+    const int si = code / NTT, j = code - si * NTT;
     int64_t cid, hid;
-    I::decode(craw, a.vocab, cid);
-    I::decode(hraw, a.vocab, hid);
+    I::decode(cs[si], a.vocab, cid);
+    I::decode(hs[si][16 * j + col], a.vocab, hid);
     din_row<KS>(a.table, cid, kg, q);
     din_row<KS>(a.table, hid, kg, kv);
   };
-  // the first items' ids go out first; the first rows are requested right
-  // after the first staging round's loads (their id trip overlaps it)
-  typename I::raw_t cr0, hr0, cr1, hr1;
-  item_ids(w, cr0, hr0);
-  item_ids(w + DF_NW, cr1, hr1);
   float q[KS], kv[KS];
   __builtin_amdgcn_sched_barrier(0);
 
@@ -516,7 +550,7 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
       vw = pw2[min(bw + (int)threadIdx.x, nw2 - 1)];
       if (b1 == 0) {
         __builtin_amdgcn_sched_barrier(0);
-        item_rows(cr0, hr0, q, kv);
+        ids_to_lds();
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
@@ -549,6 +583,26 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
   DF_STAMP(6);  // staging stores issued (before the barrier)
   __syncthreads();
   DF_STAMP(1);
+  // the wave's live items, built once: lane L < nsmp * NTT stands for
+  // (sample L / NTT, tile L % NTT); the live ones are numbered in lane order
+  // (sample-major) and dealt round-robin (w, w + 16, ..): at most 4 per wave,
+  // kept as 6-bit lane codes in one register
+  unsigned items = 0;
+  int nmine = 0;
+  {
+    const int si = lane / NTT, j = lane - si * NTT;
+    const bool live = lane < nsmp * NTT && (tmask[si < DF_SPW ? si : 0] >> j & 1);
+    const uint64_t lv = __ballot(live);
+    const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(lv >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)lv, 0));
+    for (int m = 0; m < 4; ++m) {
+      const uint64_t hit = __ballot(live && rank == w + DF_NW * m);
+      if (!hit) break;
+      items |= (unsigned)__builtin_ctzll(hit) << (6 * m);
+      ++nmine;
+    }
+  }
+  // the first item's rows now: their trip overlaps the lane-image reads
+  if (nmine > 0) item_rows(items & 63, q, kv);
   float wkd[HT1][KS], wpv[HT1][KS], wqd[HT1][KS];
   {
     const float* w1s = dsm + L.w1;  // [wkd | wp | wqd], each [HT1][KS][64]
@@ -567,10 +621,12 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
 
   bool bad = false;
   int cnt = 0;
-  for (int it = w; it < nitems; it += DF_NW) {
-    const int si = it / NTT, j = it - si * NTT;
+  for (int m = 0; m < nmine; ++m) {
+    const int code = __builtin_amdgcn_readfirstlane((items >> (6 * m)) & 63);
+    const int si = code / NTT, j = code - si * NTT;
     const int t = 16 * j + col;
     const bool tv = t < T;
+    const typename I::raw_t cr0 = cs[si], hr0 = hs[si][t];
     int64_t cid, hid;
     const bool cok = I::decode(cr0, a.vocab, cid);
     const bool hok = I::decode(hr0, a.vocab, hid);
@@ -582,11 +638,8 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
       qc[s] = cok ? q[s] : 0.f;
       kc[s] = hok ? kv[s] : 0.f;
     }
-    // the next item's rows (its ids arrived long ago) and the one after's ids
-    cr0 = cr1;
-    hr0 = hr1;
-    item_rows(cr0, hr0, q, kv);
-    item_ids(it + 2 * DF_NW, cr1, hr1);
+    // the next item's rows (ids in LDS), requested under this item's MFMAs
+    if (m + 1 < nmine) item_rows((items >> (6 * (m + 1))) & 63, q, kv);
     // pinned here: left alone the scheduler sinks these loads to the end of
     // the item, and the next item's loop-head vmcnt(0) then pays their trip
     __builtin_amdgcn_sched_barrier(0);
@@ -638,7 +691,7 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
     for (int o = 1; o < 16; o <<= 1) mj = fmaxf(mj, __shfl_xor(mj, o));
     const float e = tv ? __expf(sc - mj) : 0.f;
     const float lj = row16_sum(e);
-    float* pp = part + (size_t)it * (2 + DF_MAXK);
+    float* pp = part + (size_t)code * (2 + DF_MAXK);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const float os = row16_sum(e * kc[s]);
@@ -656,15 +709,19 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
   // merge the tiles of sample w (one wave per sample, lane c < k = channel)
   if (w < nsmp && lane < K) {
     const float* pp = part + (size_t)w * NTT * (2 + DF_MAXK);
+    const unsigned mk = tmask[w];  // live tiles only (the others would add exact zeros)
     float m = -INFINITY;
-    for (int jj = 0; jj < NTT; ++jj) m = fmaxf(m, pp[jj * (2 + DF_MAXK)]);
+    for (int jj = 0; jj < NTT; ++jj)
+      if (mk >> jj & 1) m = fmaxf(m, pp[jj * (2 + DF_MAXK)]);
     float l = 0.f, o = 0.f;
     for (int jj = 0; jj < NTT; ++jj) {
+      if (!(mk >> jj & 1)) continue;
       const float sj = __expf(pp[jj * (2 + DF_MAXK)] - m);
       l = fmaf(pp[jj * (2 + DF_MAXK) + 1], sj, l);
       o = fmaf(pp[jj * (2 + DF_MAXK) + 2 + lane], sj, o);
     }
     a.out[(s0 + w) * a.ldo + lane] = o / l;
+    if (a.cand_out) a.cand_out[(s0 + w) * a.ldc + lane] = cq;
   }
   DF_STAMP(7);
 }
@@ -690,7 +747,8 @@ static void launch_din(const DinArgs& a, hipStream_t st) {
 // din_fused's dynamic LDS for this shape, or 0 when it does not fit
 static size_t df_lds(const DinGeom& g) {
   const size_t b = (size_t)df_layout(g.NTT, g.HT1, g.HT2, g.KS).total * sizeof(float);
-  return b + 1024 <= 160 * 1024 ? b : 0;  // (+ the static bias / w3 tiles)
+  // (+ the static bias / w3 tiles and the id tile: <= 8 B per id)
+  return g.NTT * 16 <= DF_TMAX && b + 1024 + DF_SPW * (DF_TMAX + 2) * 8 <= 160 * 1024 ? b : 0;
 }
 
 template <int KS, int KIND>
@@ -732,10 +790,11 @@ extern "C" int rs_din_prepare(const float* W1, const float* b1, const float* alp
   return launch_status("rs_din_prepare");
 }
 
-extern "C" int rs_din_attention_ids_fwd(const void* hist, int id_kind, int64_t hist_stride, const void* cand,
+static int din_ids_run(const void* hist, int id_kind, int64_t hist_stride, const void* cand,
                                         int64_t cand_stride, int T, int k, const float* table, int64_t vocab,
                                         int H1, int H2, const float* prepared, float* scores, float* out,
-                                        int64_t out_stride, int64_t batch, int* err_flag, rs_stream_t stream) {
+                                        int64_t out_stride, float* cand_out, int64_t cand_out_stride, int64_t batch,
+                      int* err_flag, rs_stream_t stream) {
   if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   RS_REQUIRE(rs_din_prepared_size(T, k, H1, H2) > 0,
              "rs_din_attention_ids_fwd: need k in {4,8,16}, H1 <= 128, H2 <= 64");
@@ -745,9 +804,10 @@ extern "C" int rs_din_attention_ids_fwd(const void* hist, int id_kind, int64_t h
              "rs_din_attention_ids_fwd: bad ids / shape");
   RS_REQUIRE((uintptr_t)table % 16 == 0, "rs_din_attention_ids_fwd: table must be 16-B aligned");
   RS_REQUIRE(out_stride >= k, "rs_din_attention_ids_fwd: out_stride < k");
+  RS_REQUIRE(!cand_out || cand_out_stride >= k, "rs_din_attention_ids_cand_fwd: cand_out_stride < k");
   if (batch == 0) return RS_OK;
   DinArgs a{hist, hist_stride, cand, cand_stride, table, vocab, prepared, din_geom(T, k, H1, H2),
-            0, scores, out, out_stride, batch, err_flag, g_din_dbg};
+            0, scores, out, out_stride, batch, err_flag, g_din_dbg, cand_out, cand_out_stride};
   hipStream_t st = as_stream(stream);
   with_id_kind(id_kind, [&](auto K) {
     constexpr int KIND = decltype(K)::value;
@@ -755,5 +815,23 @@ extern "C" int rs_din_attention_ids_fwd(const void* hist, int id_kind, int64_t h
     else if (k == 8) launch_din_h<2, KIND>(a, st);
     else launch_din_h<4, KIND>(a, st);
   });
-  return launch_status("rs_din_attention_ids_fwd");
+  return launch_status(cand_out ? "rs_din_attention_ids_cand_fwd" : "rs_din_attention_ids_fwd");
+}
+
+extern "C" int rs_din_attention_ids_fwd(const void* hist, int id_kind, int64_t hist_stride, const void* cand,
+                                        int64_t cand_stride, int T, int k, const float* table, int64_t vocab,
+                                        int H1, int H2, const float* prepared, float* scores, float* out,
+                                        int64_t out_stride, int64_t batch, int* err_flag, rs_stream_t stream) {
+  return din_ids_run(hist, id_kind, hist_stride, cand, cand_stride, T, k, table, vocab, H1, H2, prepared, scores,
+                     out, out_stride, nullptr, 0, batch, err_flag, stream);
+}
+
+extern "C" int rs_din_attention_ids_cand_fwd(const void* hist, int id_kind, int64_t hist_stride, const void* cand,
+                                             int64_t cand_stride, int T, int k, const float* table, int64_t vocab,
+                                             int H1, int H2, const float* prepared, float* scores, float* out,
+                                             int64_t out_stride, float* cand_out, int64_t cand_out_stride,
+                                             int64_t batch, int* err_flag, rs_stream_t stream) {
+  RS_REQUIRE(batch == 0 || cand_out, "rs_din_attention_ids_cand_fwd: null cand_out");
+  return din_ids_run(hist, id_kind, hist_stride, cand, cand_stride, T, k, table, vocab, H1, H2, prepared, scores,
+                     out, out_stride, cand_out, cand_out_stride, batch, err_flag, stream);
 }

@@ -742,9 +742,11 @@ class Attention(KerasModule):
             self._ids_prep, self._ids_key = prep, key
         return self._ids_prep
 
-    def forward_ids(self, table, vocab, hist, cand, err=None, out=None, scores=None):
+    def forward_ids(self, table, vocab, hist, cand, err=None, out=None, scores=None, cand_out=None):
         """Attention over key = value = table[hist], query = table[cand],
-        mask = hist != 0 (model/din.py:56-80) without materialising [B,T,k]."""
+        mask = hist != 0 (model/din.py:56-80) without materialising [B,T,k].
+        ``cand_out`` [B, k] (any row stride): also write the candidate rows
+        table[cand] there, in the same launch (DIN.call's concat)."""
         B, T = hist.shape
         k = table.shape[1]
         if self.out_kernel is None:
@@ -758,6 +760,13 @@ class Attention(KerasModule):
         if scores.numel() < B * T:
             raise ValueError("forward_ids: scores workspace needs B*T elements")
         h1, h2 = self.hidden_units
+        if cand_out is not None:
+            if cand_out.shape != (B, k) or cand_out.stride(1) != 1 or cand_out.dtype != torch.float32:
+                raise ValueError("forward_ids: cand_out must be a float32 [B, k] view with unit column stride")
+            call("rs_din_attention_ids_cand_fwd", ptr(hist), _lib.id_kind(hist), hist.stride(0), ptr(cand),
+                 cand.stride(0), T, k, ptr(table), vocab, h1, h2, ptr(self.prepared_ids(k)), ptr(scores), ptr(out),
+                 out.stride(0), ptr(cand_out), cand_out.stride(0), B, ptr(err), _stream())
+            return out
         call("rs_din_attention_ids_fwd", ptr(hist), _lib.id_kind(hist), hist.stride(0), ptr(cand),
              cand.stride(0), T, k, ptr(table), vocab, h1, h2, ptr(self.prepared_ids(k)), ptr(scores), ptr(out),
              out.stride(0), B, ptr(err), _stream())

@@ -817,11 +817,11 @@ class DIN(TowerMixin, KerasModule):
             self.att_layer.build(T, K)
         if nb == 1 and self.att_layer.ids_ok(K):
             # keys/values read through the ids from the (L2-resident) table; the
-            # candidate rows go straight into emb (the attention reads the ids)
+            # pooled rows and the candidate rows go straight into emb, in the
+            # attention's one launch (rs_din_attention_ids_cand_fwd)
             seq_layer = self.embed_seq_layers[0]
-            seq_layer.gather(cand, out=emb[:, K:2 * K], check_ids=check_ids)
             self.att_layer.forward_ids(seq_layer.table, int(seq_layer.vocab_sizes[0]), hists[0], cand,
-                                       err=self._err.t, out=emb[:, :K])  # pooled rows straight into emb
+                                       err=self._err.t, out=emb[:, :K], cand_out=emb[:, K:2 * K])
             if check_ids:
                 self._err.check("DIN")
         else:

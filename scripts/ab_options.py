@@ -32,6 +32,10 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--chunk", type=int, default=64)
     ap.add_argument("--pool", type=int, default=64)
+    ap.add_argument("--save", default=None, help="save the first value's outputs here (.pt)")
+    ap.add_argument("--compare", default=None, help="compare the first value's outputs with a saved .pt")
+    ap.add_argument("--hist", default="pad80", choices=["pad80", "random", "full"],
+                    help="din: history padding (from position 80 / random lengths 1..T as bench.py / none)")
     ap.add_argument("--lib", default=None, help="another build of librs_hip.so (build A/B: one process per build)")
     args = ap.parse_args()
     import recommender_system_amd as rs
@@ -39,6 +43,7 @@ def main():
     if args.lib:
         from pathlib import Path
         _lib._LIB_PATH = Path(args.lib).resolve()
+        _lib._ALLOW_MISSING = True
 
     dev = torch.device("cuda")
     B, F, k, nd = args.batch, 26, 16, 13
@@ -57,7 +62,11 @@ def main():
         layer.build(T, kd)
         table = torch.randn(Vd, kd, device=dev, generator=g)
         hist_p = torch.randint(1, Vd, (NP, Bd, T), generator=g, device=dev)
-        hist_p[:, :, 80:] = 0  # padded tails, as Amazon-Electronics histories
+        if args.hist == "pad80":
+            hist_p[:, :, 80:] = 0  # padded tails, as Amazon-Electronics histories
+        elif args.hist == "random":  # bench.py's config-4 lengths
+            lens = torch.randint(1, T + 1, (NP, Bd, 1), generator=g, device=dev)
+            hist_p = torch.where(torch.arange(T, device=dev)[None, None, :] < lens, hist_p, torch.zeros_like(hist_p))
         cand_p = torch.randint(1, Vd, (NP, Bd, 1), generator=g, device=dev)
 
         def fn(i):
@@ -120,6 +129,14 @@ def main():
             "us_per_launch_all": {v: [round(x, 3) for x in res[v]["us"]] for v in values},
             "max_scaled_diff_vs_first": {v: float(((res[v]["out"] - base).abs() / base.abs().clamp_min(rms)).max())
                                          for v in values}}
+    if args.save:
+        torch.save(base.cpu(), args.save)
+    if args.compare:
+        ref = torch.load(args.compare, weights_only=True)
+        cur = base.cpu()
+        line["vs_saved"] = {"bit_identical": bool(torch.equal(ref, cur)),
+                            "max_abs_diff": float((ref - cur).abs().max())}
+    line["hist"] = args.hist if args.workload == "din" else None
     print(json.dumps(line))
 
 

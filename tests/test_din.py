@@ -133,16 +133,18 @@ def test_din_model(gpu, dnn_act, att_act, att_hidden, nb, k, B, T):
 
 
 @pytest.mark.gpu
-def test_din_model_bad_ids(gpu):
+@pytest.mark.parametrize("nb", [1, 2])
+def test_din_model_bad_ids(gpu, nb):
     """An out-of-range behaviour / candidate id raises IndexError (Keras
-    Embedding's InvalidArgumentError on CPU)."""
+    Embedding's InvalidArgumentError on CPU) — nb = 1 is the id-driven path
+    whose one launch also copies the candidate rows."""
     from recommender_system_amd import DIN
     rng = np.random.default_rng(5)
-    cols, behaviour = din_columns(2, 8)
+    cols, behaviour = din_columns(nb, 8)
     model = DIN(cols, behaviour, seed=1)
     inputs = din_inputs(rng, cols, behaviour, 64, 20)
     model(inputs)
-    for key, val in (("cate_seq", 801), ("movie_id", 63001)):
+    for key, val in ((behaviour[-1], 801 if nb == 2 else 63001), ("movie_id", 63001)):
         bad = {k_: v.copy() for k_, v in inputs.items()}
         if key == "movie_id":
             bad[key][3, 0] = val

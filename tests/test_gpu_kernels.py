@@ -661,6 +661,22 @@ def _din_ids_case(T, k, h, B, id_dtype):
     ref = O.attention(q, key, key, mask, _att_params(layer), "prelu")
     assert_scaled_close(y, ref, what="DIN attention from ids")
     assert err.item() == 0
+    # the same launch also copies the candidate rows (DIN.call's concat: a
+    # strided [B, k] view): the pool unchanged bit for bit, the copy exact
+    emb = torch.full((B, 3 * k + 1), 7.0, device="cuda")
+    y2 = layer.forward_ids(table, V, torch.tensor(hist, device="cuda"), torch.tensor(cand, device="cuda"), err=err,
+                           out=emb[:, :k], cand_out=emb[:, k:2 * k])
+    torch.cuda.synchronize()
+    assert torch.equal(y2, y)
+    assert np.array_equal(emb[:, k:2 * k].cpu().numpy(), q)
+    assert bool((emb[:, 2 * k:] == 7.0).all())
+    bad_c = cand.copy()
+    bad_c[B // 2, 0] = V
+    layer.forward_ids(table, V, torch.tensor(hist, device="cuda"), torch.tensor(bad_c, device="cuda"), err=err,
+                      out=emb[:, :k], cand_out=emb[:, k:2 * k])
+    torch.cuda.synchronize()
+    assert err.item() != 0 and bool((emb[B // 2, k:2 * k] == 0).all())
+    err.zero_()
     bad = hist.copy()
     bad[B - 1, 0] = V
     layer.forward_ids(table, V, torch.tensor(bad, device="cuda"), torch.tensor(cand, device="cuda"), err=err)
