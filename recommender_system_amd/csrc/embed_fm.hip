@@ -1184,13 +1184,12 @@ __global__ __launch_bounds__(16 * 64) void deepfm_all(EmbedFmArgs a, MlpArgs t, 
     }
   }
   {
-    const float* bias = par + t.poff[0];
-    const float* alpha = bias + t.Np[0];
     float* out = tsm + 16 * RS;  // layer 0 -> buf1
     const int col = 16 * w + s;
+    const float bc = par[t.poff[0] + col], ac = par[t.poff[0] + t.Np[0] + col];  // registers before the stores
     with_act(t.act[0], [&](auto A) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) out[(4 * kk + r) * RS + col] = mlp_act_c<decltype(A)::value>(acc0[r] + bias[col], alpha[col]);
+      for (int r = 0; r < 4; ++r) out[(4 * kk + r) * RS + col] = mlp_act_c<decltype(A)::value>(acc0[r] + bc, ac);
     });
   }
   {

@@ -287,8 +287,10 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
     const bool last = l == a.L - 1;
     const int Nl = a.N[l];
 
-    auto finish = [&](auto A, int row, int col, float v) {
-      v = mlp_act_c<decltype(A)::value>(v + bias[col], alpha[col]);
+    // bias / alpha come in as values: read between LDS stores they would be
+    // re-read after every store (the compiler cannot prove out != par)
+    auto finish = [&](auto A, int row, int col, float v, float bc, float ac) {
+      v = mlp_act_c<decltype(A)::value>(v + bc, ac);
       if (!last) {
         out[row * RS + col] = v;
       } else {
@@ -321,18 +323,21 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
         const float hw = col < Nl ? a.prep[a.off[LH] + ((int64_t)(col >> 4) * 64 + 16 * ((col & 15) >> 2)) * 4 +
                                            (col & 3)]
                                   : 0.f;
+        const float bc = bias[col], ac = alpha[col];
         with_act(act, [&](auto A) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float p = col < Nl ? mlp_act_c<decltype(A)::value>(acc[r] + bias[col], alpha[col]) * hw : 0.f;
+            float p = col < Nl ? mlp_act_c<decltype(A)::value>(acc[r] + bc, ac) * hw : 0.f;
             p = row16_sum(p);
             if ((lane & 15) == 0) red[it.t * 16 + 4 * (lane >> 4) + r] = p;
           }
         });
       } else if (S == 1) {
+        const int col = 16 * it.t + (lane & 15);
+        const float bc = bias[col], ac = alpha[col];
         with_act(act, [&](auto A) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) finish(A, 4 * (lane >> 4) + r, 16 * it.t + (lane & 15), acc[r]);
+          for (int r = 0; r < 4; ++r) finish(A, 4 * (lane >> 4) + r, col, acc[r], bc, ac);
         });
       } else {
         *reinterpret_cast<floatx4*>(red + item * 256 + lane * 4) = acc;
@@ -357,7 +362,8 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
           const int t = e >> 8, q = e & 255, ln = q >> 2, r = q & 3;
           float v = 0.f;
           for (int p = 0; p < S; ++p) v += red[(p * T + t) * 256 + q];
-          finish(A, 4 * (ln >> 4) + r, 16 * t + (ln & 15), v);
+          const int col = 16 * t + (ln & 15);
+          finish(A, 4 * (ln >> 4) + r, col, v, bias[col], alpha[col]);
         }
       });
     }
@@ -485,12 +491,13 @@ __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, i
   __syncthreads();                 // the partial tiles in red
   if (w < TA) {
     acc = gather_parts(acc, TA);
-    const float* bias = par + a.poff[l0];
-    const float* alpha = bias + a.Np[l0];
     const int col = 16 * w + s;
+    // bias / alpha in registers first: read between the LDS stores below they
+    // are re-read after every store (the compiler cannot prove out != par)
+    const float bc = par[a.poff[l0] + col], ac = par[a.poff[l0] + a.Np[l0] + col];
     with_act(a.act[l0], [&](auto A) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) out[(4 * kk + r) * RS + col] = mlp_act_c<decltype(A)::value>(acc[r] + bias[col], alpha[col]);
+      for (int r = 0; r < 4; ++r) out[(4 * kk + r) * RS + col] = mlp_act_c<decltype(A)::value>(acc[r] + bc, ac);
     });
   }
   // ---- layer l1, its epilogue folded with the head
@@ -510,12 +517,12 @@ __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, i
   float* redh = red;  // [TB][16] head partials (red[0 .. 256 TB) is never a partial: parts >= 1 are waves >= TB)
   if (w < TB) {
     acc = gather_parts(acc, TB);
-    const float* bias = par + a.poff[l1];
-    const float* alpha = bias + a.Np[l1];
+    const float bc = par[a.poff[l1] + colh], ac = par[a.poff[l1] + a.Np[l1] + colh];  // (registers: see l0)
+    const bool live = colh < a.N[l1];
     with_act(a.act[l1], [&](auto A) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float h = colh < a.N[l1] ? mlp_act_c<decltype(A)::value>(acc[r] + bias[colh], alpha[colh]) * hw : 0.f;  // (padded columns: 0)
+        float h = live ? mlp_act_c<decltype(A)::value>(acc[r] + bc, ac) * hw : 0.f;  // (padded columns: 0)
         h = row16_sum(h);
         if (s == 0) redh[w * 16 + 4 * kk + r] = h;
       }
