@@ -470,6 +470,15 @@ int rs_mlp_fwd(const float* x, int64_t x_stride, int n_layers, const int* dims,
                const int* acts, const float* prepared, float* y,
                int64_t y_stride, int head, const float* extra, float c0,
                float c1, int64_t batch, rs_stream_t stream);
+/* ... with an inference BatchNormalization on the input folded into the
+ * tile staging: column c enters the tower as x[m, c] * in_scale[c] +
+ * in_shift[c] (rs_affine_act's arithmetic; DIN.call's bn_layer before the
+ * DNN, model/din.py:89), so the normalised concat never reaches HBM.        */
+int rs_mlp_affine_fwd(const float* x, int64_t x_stride, const float* in_scale,
+                      const float* in_shift, int n_layers, const int* dims,
+                      const int* acts, const float* prepared, float* y,
+                      int64_t y_stride, int head, const float* extra, float c0,
+                      float c1, int64_t batch, rs_stream_t stream);
 
 /* --------------------------------------------- fused DeepFM forward (a8)
  * DeepFM.call (model/deepFM.py:23-31) in ONE launch: ids -> rows -> x (kept

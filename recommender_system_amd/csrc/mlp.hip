@@ -86,6 +86,16 @@ __global__ __launch_bounds__(NW * 64) void mlp_tower(MlpArgs a) {
       const int c = lane + 64 * i;
       xv[i] = c < a.K0 ? xr[c] : 0.f;
     }
+    if (a.in_scale) {  // the BatchNormalization affine, as rs_affine_act computes it
+#pragma unroll
+      for (int i = 0; i < XU; ++i) {
+        const int c = lane + 64 * i;
+        if (c < a.K0) {
+#pragma clang fp contract(off)  // two roundings, as rs_affine_act (no fma)
+          xv[i] = xv[i] * a.in_scale[c] + a.in_shift[c];
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < XU; ++i) {
       const int c = lane + 64 * i;
@@ -139,9 +149,9 @@ extern "C" int rs_mlp_prepare(int n_layers, const int* dims, const float* const*
   return launch_status("rs_mlp_prepare");
 }
 
-extern "C" int rs_mlp_fwd(const float* x, int64_t x_stride, int n_layers, const int* dims, const int* acts,
-                          const float* prepared, float* y, int64_t y_stride, int head, const float* extra, float c0,
-                          float c1, int64_t batch, rs_stream_t stream) {
+static int mlp_run(const float* x, int64_t x_stride, const float* in_scale, const float* in_shift, int n_layers,
+                   const int* dims, const int* acts, const float* prepared, float* y, int64_t y_stride, int head,
+                   const float* extra, float c0, float c1, int64_t batch, rs_stream_t stream) {
   if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   MlpGeom g;
   RS_REQUIRE(mlp_geom(n_layers, dims, g), "rs_mlp_fwd: need 1..%d layers with widths 1..%d", MLP_MAXL, MLP_MAXD);
@@ -163,6 +173,8 @@ extern "C" int rs_mlp_fwd(const float* x, int64_t x_stride, int n_layers, const 
   a.c1 = c1;
   a.M = batch;
   a.dbg = g_mlp_dbg;
+  a.in_scale = in_scale;
+  a.in_shift = in_shift;
   const size_t lds = g.lds;
   static LdsAttr lds_set;  // opt in to exactly what is needed beyond the default
   lds_attr(lds_set, (const void*)mlp_tower<MLP_NW>, lds);
@@ -170,4 +182,20 @@ extern "C" int rs_mlp_fwd(const float* x, int64_t x_stride, int n_layers, const 
   RS_REQUIRE(grid < (1ll << 31), "rs_mlp_fwd: batch too large");
   mlp_tower<MLP_NW><<<(unsigned)grid, MLP_NW * 64, lds, as_stream(stream)>>>(a);
   return launch_status("rs_mlp_fwd");
+}
+
+extern "C" int rs_mlp_fwd(const float* x, int64_t x_stride, int n_layers, const int* dims, const int* acts,
+                          const float* prepared, float* y, int64_t y_stride, int head, const float* extra, float c0,
+                          float c1, int64_t batch, rs_stream_t stream) {
+  return mlp_run(x, x_stride, nullptr, nullptr, n_layers, dims, acts, prepared, y, y_stride, head, extra, c0, c1,
+                 batch, stream);
+}
+
+extern "C" int rs_mlp_affine_fwd(const float* x, int64_t x_stride, const float* in_scale, const float* in_shift,
+                                 int n_layers, const int* dims, const int* acts, const float* prepared, float* y,
+                                 int64_t y_stride, int head, const float* extra, float c0, float c1, int64_t batch,
+                                 rs_stream_t stream) {
+  RS_REQUIRE(batch == 0 || (in_scale && in_shift), "rs_mlp_affine_fwd: null in_scale / in_shift");
+  return mlp_run(x, x_stride, in_scale, in_shift, n_layers, dims, acts, prepared, y, y_stride, head, extra, c0, c1,
+                 batch, stream);
 }

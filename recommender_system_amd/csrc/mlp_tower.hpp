@@ -69,6 +69,8 @@ struct MlpArgs {
   int64_t M;
   unsigned long long* dbg;  // diagnostics only: per-wave phase stamps (rs_diag_mlp_set_dbg)
   int unroll;               // RS_OPT_MLP_UNROLL at launch
+  const float* in_scale;    // rs_mlp_affine_fwd: input column c staged as x * in_scale[c] + in_shift[c]
+  const float* in_shift;    //   (an inference BatchNormalization folded into the staging; null = none)
 };
 // Per-wave phase stamps (rs_diag_mlp_set_dbg) exist only in the diagnostic
 // build (scripts/build_diag.sh, -DRS_DIAG_STAMPS): the product's runtime

@@ -515,9 +515,11 @@ class TowerMixin:
             ent = cache[slot] = (key, prep, in_rows)  # in_rows kept alive with its packing
         return ent[1]
 
-    def tower(self, x, extra=None, c0=1.0, c1=1.0, head=False, out=None):
+    def tower(self, x, extra=None, c0=1.0, c1=1.0, head=False, out=None, in_affine=None):
         """rs_mlp_fwd on x:[M, K] (device, row stride x.stride(0)).  head=True:
-        sigmoid(c0*dnn + c1*extra) (output_dim 1)."""
+        sigmoid(c0*dnn + c1*extra) (output_dim 1).  in_affine=(scale, shift):
+        the tower runs on x * scale + shift (an inference BatchNormalization
+        folded into the launch: rs_mlp_affine_fwd)."""
         ls = self._layers()
         n = len(ls)
         dims = self._dims()
@@ -525,6 +527,14 @@ class TowerMixin:
         if out is None:
             out = torch.empty(M, 1 if head else dims[-1], dtype=torch.float32, device=self._dev)
         acts = [_lib.ACT[l.activation] for l in ls]
+        if in_affine is not None:
+            sc, sh = in_affine
+            if sc.numel() != dims[0] or sh.numel() != dims[0]:
+                raise ValueError(f"tower: in_affine needs {dims[0]} scales and shifts")
+            call("rs_mlp_affine_fwd", ptr(x), x.stride(0), ptr(sc), ptr(sh), n, (C.c_int * (n + 1))(*dims),
+                 (C.c_int * n)(*acts), ptr(self.prepared()), ptr(out), out.stride(0), 1 if head else 0, ptr(extra),
+                 float(c0), float(c1), M, _stream())
+            return out
         call("rs_mlp_fwd", ptr(x), x.stride(0), n, (C.c_int * (n + 1))(*dims), (C.c_int * n)(*acts),
              ptr(self.prepared()), ptr(out), out.stride(0), 1 if head else 0, ptr(extra), float(c0), float(c1), M,
              _stream())

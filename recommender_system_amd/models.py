@@ -840,9 +840,12 @@ class DIN(TowerMixin, KerasModule):
         for f in self.dense_feature_columns:
             emb[:, col:col + 1] = _to_device_f32(inputs[f["feat"]], dev).reshape(B, 1)
             col += 1
-        x = self.bn_layer(emb)
         if self.out_layer.kernel is not None and self.tower_ok():
-            return self.tower(x)  # PReLU MLP + Dense(1, sigmoid) in one launch
+            # BatchNormalization + PReLU MLP + Dense(1, sigmoid) in one launch
+            if self.bn_layer.gamma is None:
+                self.bn_layer.build(emb.shape[-1])
+            return self.tower(emb, in_affine=self.bn_layer.affine())
+        x = self.bn_layer(emb)
         for layer in self.dense_layer:
             x = layer(x)
         return self.out_layer(x)

@@ -1071,3 +1071,38 @@ def test_deepfm_fused_wide_dense(gpu, nd, F, B):
         ref, ref_fm, _ = O.deepfm(None, p, nd=nd, inputs=(dense, ids))
         assert_rel_close(y, ref, what=f"DeepFM nd={nd} F={F} form {form}")
         assert_scaled_close(fm, ref_fm, what=f"DeepFM nd={nd} F={F} form {form} fm logit")
+
+
+# ------------------------------------------- tower with a folded input affine
+@pytest.mark.gpu
+@pytest.mark.parametrize("act", ["relu", "prelu"])
+def test_tower_input_affine_equals_bn_then_tower(gpu, act):
+    """rs_mlp_affine_fwd (DIN.call's BatchNormalization folded into the tower
+    launch) is bit-identical to rs_affine_act followed by rs_mlp_fwd, on a
+    strided input view."""
+    from recommender_system_amd import DNNLayer
+    from recommender_system_amd.layers import BatchNormalization
+    torch.manual_seed(3)
+    buf = torch.randn(1000, 31, device="cuda")
+    x = buf[:, 3:28]  # [1000, 25], row stride 31
+    dnn = DNNLayer((256, 128, 64), 1, act, seed=2)
+    dnn.build(25)
+    with torch.no_grad():
+        for L in dnn._layers():
+            L.bias.uniform_(-0.1, 0.1)
+            if L.alpha is not None:
+                L.alpha.uniform_(-0.5, 0.5)
+    bn = BatchNormalization()
+    bn.build(25)
+    with torch.no_grad():
+        bn.gamma.uniform_(0.5, 1.5)
+        bn.beta.uniform_(-0.1, 0.1)
+        bn.moving_mean.uniform_(-0.05, 0.05)
+        bn.moving_variance.uniform_(0.5, 2.0)
+    xa = bn(x)
+    inv, shift = bn.affine()
+    assert torch.equal(xa, (x * inv) + shift), "rs_affine_act is x * scale, then + shift"
+    ref = dnn.tower(xa.contiguous())
+    got = dnn.tower(x, in_affine=(inv, shift))
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), float((got - ref).abs().max())
