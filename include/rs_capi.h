@@ -442,6 +442,21 @@ int rs_din_attention_ids_cand_fwd(const void* hist, int id_kind,
                                   int64_t batch, int* err_flag,
                                   rs_stream_t stream);
 
+/* ------------------------------------------------ concat pieces (a15, a3)
+ * One launch for the concat pieces that live in different tables: piece p
+ * writes widths[p] columns of out [B, *] (rows out_stride floats apart)
+ * starting at out_cols[p].  kinds[p] = RS_ID_* : a sparse feature, one id
+ * per sample (srcs[p], src_strides[p] elements apart) looked up in
+ * tables[p] [vocabs[p], widths[p]] (Keras Embedding; an out-of-range id
+ * writes a zero row and sets *err_flag); kinds[p] = -1: dense fp32 values
+ * [B, widths[p]] copied as they are.  DIN.call's other sparse embeddings and
+ * dense features (model/din.py:81-86).  1..16 pieces.                      */
+int rs_concat_pieces(int n_pieces, const int* widths, const int* out_cols,
+                     const int* kinds, const void* const* srcs,
+                     const int64_t* src_strides, const float* const* tables,
+                     const int64_t* vocabs, float* out, int64_t out_stride,
+                     int64_t batch, int* err_flag, rs_stream_t stream);
+
 /* --------------------------------------------------- dense tower (a7, a15)
  * Keras Dense: y = act(x @ W + bias), W:[K,N] (Keras (in,out) orientation),
  * fp32 MFMA.  alpha: per-column PReLU slope (RS_ACT_PRELU only).            */

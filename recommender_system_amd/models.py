@@ -832,14 +832,7 @@ class DIN(TowerMixin, KerasModule):
             att_emb = self.att_layer([item_embed, seq_embed, seq_embed, mask])
             emb[:, K:2 * K] = item_embed
             emb[:, :K] = att_emb
-        col = 2 * K
-        for f, layer in zip(self.other_sparse, self.embed_sparse_layers):
-            ids = _ids_tensor(inputs[f["feat"]], dev).reshape(B, 1)
-            layer.gather(ids, out=emb[:, col:col + layer.k], check_ids=check_ids)
-            col += layer.k
-        for f in self.dense_feature_columns:
-            emb[:, col:col + 1] = _to_device_f32(inputs[f["feat"]], dev).reshape(B, 1)
-            col += 1
+        self._concat_rest(inputs, emb, 2 * K, B, check_ids)
         if self.out_layer.kernel is not None and self.tower_ok():
             # BatchNormalization + PReLU MLP + Dense(1, sigmoid) in one launch
             if self.bn_layer.gamma is None:
@@ -849,6 +842,32 @@ class DIN(TowerMixin, KerasModule):
         for layer in self.dense_layer:
             x = layer(x)
         return self.out_layer(x)
+
+    def _concat_rest(self, inputs, emb, col, B, check_ids):
+        """The other sparse embeddings and the dense features into emb[:, col:]
+        (model/din.py:81-86): ONE rs_concat_pieces launch for up to 16
+        pieces, one launch per piece beyond."""
+        dev = self._dev
+        pieces = []  # (width, out col, kind, source tensor, table, vocab)
+        for f, layer in zip(self.other_sparse, self.embed_sparse_layers):
+            ids = _ids_tensor(inputs[f["feat"]], dev).reshape(B, 1)
+            pieces.append((layer.k, col, _lib.id_kind(ids), ids, layer.table, int(layer.vocab_sizes[0])))
+            col += layer.k
+        for f in self.dense_feature_columns:
+            x = _to_device_f32(inputs[f["feat"]], dev).reshape(B, 1)
+            pieces.append((1, col, -1, x, None, 0))
+            col += 1
+        for i in range(0, len(pieces), 16):
+            part = pieces[i:i + 16]
+            n = len(part)
+            arr = lambda ctype, vals: (ctype * n)(*vals)
+            call("rs_concat_pieces", n, arr(C.c_int, [p[0] for p in part]), arr(C.c_int, [p[1] for p in part]),
+                 arr(C.c_int, [p[2] for p in part]), arr(C.c_void_p, [ptr(p[3]) for p in part]),
+                 arr(C.c_int64, [p[3].stride(0) for p in part]),
+                 arr(C.c_void_p, [ptr(p[4]) if p[4] is not None else None for p in part]),
+                 arr(C.c_int64, [p[5] for p in part]), ptr(emb), emb.stride(0), B, ptr(self._err.t), _lib.stream())
+        if check_ids and pieces:
+            self._err.check("DIN")
 
     def _layers(self):
         return list(self.dense_layer) + [self.out_layer]

@@ -144,7 +144,7 @@ def test_din_model_bad_ids(gpu, nb):
     model = DIN(cols, behaviour, seed=1)
     inputs = din_inputs(rng, cols, behaviour, 64, 20)
     model(inputs)
-    for key, val in ((behaviour[-1], 801 if nb == 2 else 63001), ("movie_id", 63001)):
+    for key, val in ((behaviour[-1], 801 if nb == 2 else 63001), ("movie_id", 63001), ("user_id", 192404)):
         bad = {k_: v.copy() for k_, v in inputs.items()}
         if key == "movie_id":
             bad[key][3, 0] = val
