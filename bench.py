@@ -1847,12 +1847,15 @@ def main():
                 "parallelism": f"dp{world}+rowshard{world}",
                 "table_rows_per_rank": res["rows_per_rank"],
                 "value_kind": "embed + FM logit of the same workload with the 26 x 1e7 table row-sharded over the "
-                              "ranks: per batch ONE RCCL all-to-all of [row ids t | FM partials t-1] + ONE "
-                              "rs_shard_fm_pipe launch (sharded.py pipe_step); config 5 (the DeepFM forward on the "
-                              "1e8-row table) is nested as config5"})
+                              "ranks: per batch ONE all-to-all of [row ids t | FM partials t-1] (" +
+                              res.get("exchange", "RCCL all_to_all") + ": the faster of RCCL and the peer-mapped "
+                              "exchange when their logits are bit-identical, both nested) + ONE rs_shard_fm_pipe "
+                              "launch (sharded.py pipe_step); config 5 (the DeepFM forward on the 1e8-row table) is "
+                              "nested as config5"})
         for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "config5_n1", "fm_hotpath_sharded_n1",
                     "config5", "protocol", "timing", "slot_ms", "unpipelined", "rows_protocol", "train_step",
-                    "owner_field_ranges", "bytes_per_rank_each_way", "world1_no_exchange"):
+                    "owner_field_ranges", "bytes_per_rank_each_way", "world1_no_exchange", "exchange",
+                    "peer_exchange", "rccl_pipelined"):
             if key in res:
                 line[key] = res[key]
         _emit(line)
