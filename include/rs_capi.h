@@ -431,7 +431,7 @@ int rs_din_attention_ids_fwd(const void* hist, int id_kind, int64_t hist_stride,
 /* ... and the candidate rows table[cand] into cand_out [B, k] (rows
  * cand_out_stride floats apart; an out-of-range id writes a zero row and sets
  * *err_flag), the copy DIN.call concatenates beside the pooled rows
- * (model/din.py:73,83-84): the same launch, no separate candidate gather.   */
+ * (model/din.py:78-79,84-85): the same launch, no separate candidate gather.   */
 int rs_din_attention_ids_cand_fwd(const void* hist, int id_kind,
                                   int64_t hist_stride, const void* cand,
                                   int64_t cand_stride, int T, int k,
@@ -450,7 +450,7 @@ int rs_din_attention_ids_cand_fwd(const void* hist, int id_kind,
  * tables[p] [vocabs[p], widths[p]] (Keras Embedding; an out-of-range id
  * writes a zero row and sets *err_flag); kinds[p] = -1: dense fp32 values
  * [B, widths[p]] copied as they are.  DIN.call's other sparse embeddings and
- * dense features (model/din.py:81-86).  1..16 pieces.                      */
+ * dense features (model/din.py:64-69,84-85).  1..16 pieces.                      */
 int rs_concat_pieces(int n_pieces, const int* widths, const int* out_cols,
                      const int* kinds, const void* const* srcs,
                      const int64_t* src_strides, const float* const* tables,

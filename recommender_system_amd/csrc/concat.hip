@@ -1,5 +1,5 @@
 // concat.hip — one launch for the per-feature pieces of a model's concat that
-// live in DIFFERENT tables: DIN.call (model/din.py:81-86) concatenates the
+// live in DIFFERENT tables: DIN.call (model/din.py:64-69,84-85) concatenates the
 // embeddings of every non-behaviour sparse feature (one EmbedLayer, i.e. one
 // table, each) and the raw dense features beside the pooled attention; the
 // reference runs one Embedding lookup per feature and a concat.  Here every

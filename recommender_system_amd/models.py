@@ -845,7 +845,7 @@ class DIN(TowerMixin, KerasModule):
 
     def _concat_rest(self, inputs, emb, col, B, check_ids):
         """The other sparse embeddings and the dense features into emb[:, col:]
-        (model/din.py:81-86): ONE rs_concat_pieces launch for up to 16
+        (model/din.py:64-69,84-85): ONE rs_concat_pieces launch for up to 16
         pieces, one launch per piece beyond."""
         dev = self._dev
         pieces = []  # (width, out col, kind, source tensor, table, vocab)
