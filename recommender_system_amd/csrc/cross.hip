@@ -419,7 +419,7 @@ __global__ __launch_bounds__(16 * 64) void embed_cross_ka(CrossArgs a, EmbedCros
 // branch's logit is alpha_L (x0.w_o) + beta_L.w_o = alpha_L g_L + h_L, x_L is
 // never formed); the DNN tower on the same tile with its last layer folded
 // with the output Dense's DNN half; head sigmoid(dnn + cross).
-template <int NT, int KIND, bool KA>
+template <int NT, int KIND, bool KA, bool TAIL = false>
 __device__ __forceinline__ void dcn_fused_body(const CrossArgs& a, const EmbedCrossArgs& e, const MlpArgs& t,
                                                const FieldMeta* km) {
   constexpr int NW = 16;
@@ -536,16 +536,25 @@ __device__ __forceinline__ void dcn_fused_body(const CrossArgs& a, const EmbedCr
     xlog[tid] = fmaf(al, go, a.h[L]);
   }
   // (the tower's first barrier publishes xlog and the tile)
-  mlp_tower_tile<NW>(t, tsm, b0, ring, xlog);
+  if constexpr (TAIL) {
+    // layer 0 as usual, layers 1.. as the split-K tail at the DeepFM / DCN
+    // widths (256 -> 128 -> 64 -> 1: all 16 waves per layer, mlp_tail_splitk)
+    mlp_tower_tile<NW>(t, tsm, b0, ring, xlog, 0, 1);
+    floatx4 wr[8];
+    mlp_tail_fetch<8>(t, 1, wr);
+    mlp_tail_splitk<NW, 8, 2>(t, tsm, b0, wr, xlog, 1);
+  } else {
+    mlp_tower_tile<NW>(t, tsm, b0, ring, xlog);
+  }
 }
 
 template <int NT, int KIND>
 __global__ __launch_bounds__(16 * 64) void dcn_fused(CrossArgs a, EmbedCrossArgs e, MlpArgs t) {
   dcn_fused_body<NT, KIND, false>(a, e, t, nullptr);
 }
-template <int NT, int KIND>
+template <int NT, int KIND, bool TAIL = false>
 __global__ __launch_bounds__(16 * 64) void dcn_fused_ka(CrossArgs a, EmbedCrossArgs e, MlpArgs t, FieldMeta m) {
-  dcn_fused_body<NT, KIND, true>(a, e, t, &m);
+  dcn_fused_body<NT, KIND, true, TAIL>(a, e, t, &m);
 }
 
 }  // namespace rs
@@ -734,7 +743,12 @@ static int dcn_run(const void* ids, int id_kind, int64_t id_stride, const float*
   hipStream_t st = as_stream(stream);
   with_id_kind(id_kind, [&](auto K) {
     constexpr int KIND = decltype(K)::value;
-    if (hm && g.NT == 1) {
+    int gwa = 0, gwb = 0;
+    if (hm && g.NT == 1 && mlp_tail_ok(t.Np, t.Kp, t.N, t.L, 1, gwa, gwb) && gwa == 8 && gwb == 2) {
+      static LdsAttr setkt;  // the split-K tail at the reference's 256-128-64 tower
+      lds_attr(setkt, (const void*)dcn_fused_ka<1, KIND, true>, lds);
+      dcn_fused_ka<1, KIND, true><<<grid, 16 * 64, lds, st>>>(a, e, t, *hm);
+    } else if (hm && g.NT == 1) {
       static LdsAttr setk1;
       lds_attr(setk1, (const void*)dcn_fused_ka<1, KIND>, lds);
       dcn_fused_ka<1, KIND><<<grid, 16 * 64, lds, st>>>(a, e, t, *hm);

@@ -260,7 +260,8 @@ __device__ __forceinline__ void mlp_mac(floatx4 (&ring)[MLP_R], const float* ap,
 // in buf (l0 & 1), its ring filled).
 template <int NW>
 __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, int64_t m0, floatx4 (&ring)[MLP_R],
-                                               const float* extra_lds = nullptr, int l0 = 0) {
+                                               const float* extra_lds = nullptr, int l0 = 0, int lstop = MLP_MAXL) {
+  // layers l0 .. min(a.L, lstop) - 1 (lstop < a.L: a caller's split-K tail runs the rest)
   const int RS = a.rs;
   float* red = smem + 32 * RS;
   float* par = red + NW * 256;
@@ -275,8 +276,9 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
   // 16 threads add the tiles' partials in tile order — no head layer of its
   // own (ring fill, barrier, K-split reduction).
   const int LH = a.L - 1;
-  const bool fhead = LH - 1 >= l0 && a.N[LH] == 1 && mlp_slices(a.Np[LH - 1] >> 4, a.Kp[LH - 1] >> 4, NW) == 1;
-  const int Lrun = fhead ? LH : a.L;
+  const bool fhead = lstop >= a.L && LH - 1 >= l0 && a.N[LH] == 1 &&
+                     mlp_slices(a.Np[LH - 1] >> 4, a.Kp[LH - 1] >> 4, NW) == 1;
+  const int Lrun = fhead ? LH : (lstop < a.L ? lstop : a.L);
   for (int l = l0; l < Lrun; ++l) {
     const int T = a.Np[l] >> 4, G = a.Kp[l] >> 4;
     const int S = mlp_slices(T, G, NW);
@@ -348,7 +350,7 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
     MLP_STAMP(3 + 2 * l);
     // next layer's first weights do not depend on this layer: request them
     // now, so they arrive during the barrier / reduction below
-    if (l + 1 < a.L) {
+    if (l + 1 < Lrun || (fhead && l + 1 < a.L)) {
       const int T2 = a.Np[l + 1] >> 4, G2 = a.Kp[l + 1] >> 4;
       const int S2 = mlp_slices(T2, G2, NW);
       if (w < T2 * S2) {
