@@ -62,7 +62,7 @@ __global__ void mlp_prepare_kernel(MlpPrepArgs a) {
   a.out[i] = v;
 }
 
-template <int NW>
+template <int NW, bool TAIL = false>
 __global__ __launch_bounds__(NW * 64) void mlp_tower(MlpArgs a) {
   extern __shared__ float smem[];
   const int RS = a.rs;
@@ -105,7 +105,16 @@ __global__ __launch_bounds__(NW * 64) void mlp_tower(MlpArgs a) {
   float* par = smem + 32 * RS + NW * 256;
   for (int i = threadIdx.x; i < a.ptot; i += NW * 64) par[i] = a.prep[a.wtot + i];
   MLP_STAMP(1);
-  mlp_tower_tile<NW>(a, smem, m0, ring);
+  if constexpr (TAIL) {
+    // a 256 -> 128 -> 64 -> 1 tail (the reference's DNN widths): layer 0 as
+    // usual, the rest as the split-K tail on all 16 waves (mlp_tail_splitk)
+    mlp_tower_tile<NW>(a, smem, m0, ring, nullptr, 0, 1);
+    floatx4 wr[8];
+    mlp_tail_fetch<8>(a, 1, wr);
+    mlp_tail_splitk<NW, 8, 2>(a, smem, m0, wr, nullptr, 1);
+  } else {
+    mlp_tower_tile<NW>(a, smem, m0, ring);
+  }
 }
 
 }  // namespace rs
@@ -176,10 +185,17 @@ static int mlp_run(const float* x, int64_t x_stride, const float* in_scale, cons
   a.in_scale = in_scale;
   a.in_shift = in_shift;
   const size_t lds = g.lds;
-  static LdsAttr lds_set;  // opt in to exactly what is needed beyond the default
-  lds_attr(lds_set, (const void*)mlp_tower<MLP_NW>, lds);
   const int64_t grid = (batch + 15) / 16;
   RS_REQUIRE(grid < (1ll << 31), "rs_mlp_fwd: batch too large");
+  int gwa = 0, gwb = 0;
+  if (MLP_NW == 16 && mlp_tail_ok(a.Np, a.Kp, a.N, a.L, 1, gwa, gwb) && gwa == 8 && gwb == 2) {
+    static LdsAttr lds_tail;
+    lds_attr(lds_tail, (const void*)mlp_tower<MLP_NW, true>, lds);
+    mlp_tower<MLP_NW, true><<<(unsigned)grid, MLP_NW * 64, lds, as_stream(stream)>>>(a);
+    return launch_status("rs_mlp_fwd");
+  }
+  static LdsAttr lds_set;  // opt in to exactly what is needed beyond the default
+  lds_attr(lds_set, (const void*)mlp_tower<MLP_NW>, lds);
   mlp_tower<MLP_NW><<<(unsigned)grid, MLP_NW * 64, lds, as_stream(stream)>>>(a);
   return launch_status("rs_mlp_fwd");
 }
