@@ -1154,10 +1154,13 @@ class NFM(TowerMixin, KerasModule):
         return x
 
     def forward(self, inputs, check_ids=True):
-        x = self.bn_layer(self.bi_interaction_input(inputs, check_ids))
+        x = self.bi_interaction_input(inputs, check_ids)
         if self.tower_ok():
-            return self.tower(x)  # DNNLayer + Dense(1, sigmoid) in one launch
-        return self.output_layer(self.dnn_layers(x))
+            # BatchNormalization + DNNLayer + Dense(1, sigmoid) in one launch
+            if self.bn_layer.gamma is None:
+                self.bn_layer.build(x.shape[-1])
+            return self.tower(x, in_affine=self.bn_layer.affine())
+        return self.output_layer(self.dnn_layers(self.bn_layer(x)))
 
     def train_step(self, inputs, labels, lr=0.01, return_loss=False, check_ids=True, dropout=None):
         """One step of compile_fit on NFM (utils/compile_fit.py:9-15; the
