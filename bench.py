@@ -1323,8 +1323,10 @@ def bench_din(args, world, rank):
                  {"materialised_keys_path": {"samples_per_s": args.steps * B / dt_old,
                                              "ms_per_step": dt_old / args.steps * 1e3},
                   "din_forward": {"samples_per_s": n2 * B / dt2, "ms_per_step": dt2 / n2 * 1e3,
-                                  "note": "graph-replayed full DIN.call (id checks off): gathers, attention "
-                                          "from ids, BN, PReLU MLP + sigmoid head"},
+                                  "note": "graph-replayed full DIN.call (id checks off), three launches: the "
+                                          "other sparse rows + dense (rs_concat_pieces), the attention from ids "
+                                          "with the candidate rows (rs_din_attention_ids_cand_fwd), BN + PReLU "
+                                          "MLP + sigmoid head (rs_mlp_affine_fwd)"},
                   "train_step": {"samples_per_s": nt * B / tdt, "ms_per_step": tdt / nt * 1e3,
                                  "timing": ttiming,
                                  "note": "DIN.train_step: gathers, attention Dense+PReLU layers over [B*T] rows, "
@@ -1463,7 +1465,7 @@ def bench_nfm(args, world, rank):
     return _hbm_line("NFM bi-interaction input samples/sec @ batch 4096, 26 sparse x 1e6 vocab, dim 16", args,
                      world, B, dt, slot, alg, "nfm_embed_bi_interaction_fused", V, "pair_pool_ksplit (sum)",
                      {"nfm_forward": {"samples_per_s": n2 * B / dtf, "ms_per_step": dtf / n2 * 1e3,
-                                      "note": "bi-interaction launch + BN + DNN 29-256-128-64-1 + Dense(1) tower"},
+                                      "note": "bi-interaction launch + one tower launch (BN folded into the staging, DNN 29-256-128-64-1, Dense(1))"},
                       "cpu_baseline": cpu})
 
 

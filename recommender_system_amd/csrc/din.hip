@@ -603,7 +603,11 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
   }
   // the first item's rows now: their trip overlaps the lane-image reads
   if (nmine > 0) item_rows(items & 63, q, kv);
-  float wkd[HT1][KS], wpv[HT1][KS], wqd[HT1][KS];
+  // layer 1's lane images in registers; at k = 16 the q image stays in LDS
+  // and is read at its MFMA (all three in registers spill at 128 VGPRs)
+  constexpr bool QREG = KS < 4;
+  float wkd[HT1][KS], wpv[HT1][KS], wqd[HT1][QREG ? KS : 1];
+  const float* w1q = dsm + L.w1 + 2 * HT1 * KS * 64 + lane;  // the q image, [HT1][KS][64]
   {
     const float* w1s = dsm + L.w1;  // [wkd | wp | wqd], each [HT1][KS][64]
     const int img = HT1 * KS * 64;
@@ -614,7 +618,7 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
         const int o = (ht * KS + s) * 64 + lane;
         wkd[ht][s] = w1s[o];
         wpv[ht][s] = w1s[img + o];
-        wqd[ht][s] = w1s[2 * img + o];
+        if constexpr (QREG) wqd[ht][s] = w1s[2 * img + o];
       }
     }
   }
@@ -653,7 +657,10 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
 #pragma unroll
       for (int s = 0; s < KS; ++s) acc = mfma16x16x4(fmaf(qc[s], wpv[ht][s], wkd[ht][s]), kc[s], acc);
 #pragma unroll
-      for (int s = 0; s < KS; ++s) acc = mfma16x16x4(wqd[ht][s], qc[s], acc);
+      for (int s = 0; s < KS; ++s) {
+        if constexpr (QREG) acc = mfma16x16x4(wqd[ht][s], qc[s], acc);
+        else acc = mfma16x16x4(w1q[(ht * KS + s) * 64], qc[s], acc);
+      }
       const floatx4 al = *reinterpret_cast<const floatx4*>(&a1s[t * A1W + 16 * ht + 4 * kg]);
 #pragma unroll
       for (int r = 0; r < 4; ++r) y1[ht][r] = prelu(acc[r], al[r]);

@@ -618,7 +618,8 @@ def test_embed_cross_fused(gpu, k, L, B, id_dtype):
 @pytest.mark.parametrize("T,k,h,B,id_dtype", [(100, 8, (80, 40), 2048, np.int64), (10, 8, (80, 40), 5, np.int32),
                                               (1, 4, (16, 16), 3, np.int64), (33, 16, (128, 64), 21, np.int32),
                                               (17, 8, (20, 7), 40, np.int32), (37, 4, (80, 40), 13, np.int32),
-                                              (150, 16, (80, 40), 9, np.int64), (100, 8, (80, 40), 2045, np.int32)])
+                                              (150, 16, (80, 40), 9, np.int64), (100, 8, (80, 40), 2045, np.int32),
+                                              (100, 16, (80, 40), 70, np.int64), (128, 4, (80, 40), 17, np.int32)])
 def test_din_attention_ids(gpu, form, T, k, h, B, id_dtype):
     """keys = values = table[hist], query = table[cand], mask = hist != 0;
     padded positions keep their (id 0) rows in the pooled values, a fully
