@@ -393,7 +393,7 @@ def bench_hotpath(args, world, rank):
                                                  "this shape: TCC_EA0_RDREQ x 128 B + WRITE_SIZE per launch)"
                                                  if int(args.vocab) == int(1e7) else
                                                  "none: no PMC pass at this vocabulary"),
-                              "kernel": "embed_fm_mfma", "kernel_ms": kern_ms,
+                              "kernel": "embed_fm_mfma_ka", "kernel_ms": kern_ms,
                               "kernel_ms_source": "HIP events around the graph-replayed timed region / steps "
                                                   "(kernel + back-to-back dispatch boundary)",
                               "eager_launch_event_ms_median": float(np.median(ms)),
@@ -985,7 +985,7 @@ def bench_sharded_deepfm(args, world, rank, lite=False):
     S = model.emb.slot_stride
     roof = {"bound": "mfma", "achieved": flops / (fin_ms * 1e-3) / 1e12, "peak": PEAK_F32 / 1e12,
             "unit": "TFLOP/s", "frac": flops / (fin_ms * 1e-3) / PEAK_F32, "traffic": None,
-            "kernel": "deepfm_fused (rs_deepfm_fwd from the row-exchange buffer)",
+            "kernel": "deepfm_ws (rs_deepfm_fwd_hm from the row-exchange buffer)",
             "kernel_ms": fin_ms, "dnn_flop_per_launch": flops,
             "kernel_ms_source": "HIP events around graph-replayed launches of the fused kernel alone"}
     exch = {"protocol": "field-range row records: rs_shard_row_route, RCCL all-to-all of row ids, "
@@ -1207,7 +1207,7 @@ def bench_dcn(args, world, rank):
                  {"workload": "dcn_embed+crossnet_depth3_fused", "global_batch": B, "d": d, "layer_num": 3,
                   "vocab_per_field": V, "parallelism": "dp1"},
                  {"bound": "hbm", "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                  "frac": ach / PEAK_HBM, "traffic": _pmc_cfg("dcn"), "kernel": "embed_cross", "kernel_ms": kern_ms,
+                  "frac": ach / PEAK_HBM, "traffic": _pmc_cfg("dcn"), "kernel": "embed_cross_ka", "kernel_ms": kern_ms,
                   "kernel_ms_source": "graph-replayed slot time per launch",
                   "algorithmic_bytes_per_launch": alg, "mfma_useful_flop_per_launch": useful,
                   "mfma_issued_flop_per_launch": issued, "mfma_useful_fraction_by_construction": useful / issued},
@@ -1314,8 +1314,8 @@ def bench_din(args, world, rank):
                  {"workload": "din_attention_unit_from_ids", "global_batch": B, "seq_len": T, "embed_dim": k,
                   "att_hidden": [80, 40], "behaviour_vocab": 63001, "parallelism": "dp1"},
                  {"bound": "mfma", "achieved": ach / 1e12, "peak": PEAK_F32 / 1e12, "unit": "TFLOP/s",
-                  "frac": ach / PEAK_F32, "traffic": _pmc_cfg("din"), "kernel": "din_scores (+din_pool)", "kernel_ms": att_ms,
-                  "kernel_ms_source": "graph-replayed step (both launches) / steps",
+                  "frac": ach / PEAK_F32, "traffic": _pmc_cfg("din"), "kernel": "din_fused", "kernel_ms": att_ms,
+                  "kernel_ms_source": "graph-replayed step (one launch: scores, masked softmax, pool) / steps",
                   "useful_flop_per_launch": flop,
                   "useful_flop_note": "reference formulation T*2*(4k*80+80*40+40); the kernel regroups layer 1 "
                                       "per sample (q(Wq+Wd) + key(Wk-Wd+diag(q)Wp)) and issues fewer",
@@ -1393,7 +1393,7 @@ def bench_pnn(args, world, rank):
                  args.steps * B / dt, "samples/s", args, world, dt / args.steps * 1e3,
                  {"workload": "pnn_embed_inner_fused", "global_batch": B, "vocab_per_field": V, "parallelism": "dp1"},
                  {"bound": "hbm", "achieved": ach / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                  "frac": ach / PEAK_HBM, "traffic": _pmc_cfg("pnn"), "kernel": "inner_fast", "kernel_ms": slot,
+                  "frac": ach / PEAK_HBM, "traffic": _pmc_cfg("pnn"), "kernel": "inner_fast_ka", "kernel_ms": slot,
                   "algorithmic_bytes_per_launch": alg},
                  {"mode_both": {"samples_per_s": n2 * B / dtb, "kernel_ms": slotb,
                                 "outer_mfma_tflops": B * P * k * k * 2 / (slotb * 1e-3) / 1e12,

@@ -10,9 +10,9 @@ import statistics as st
 import sys
 
 # config -> (bench line's roofline "kernel" key, kernel-name substring)
-KERNELS = {"dcn": ("embed_cross", "rs::embed_cross<"), "pnn": ("inner_fast", "rs::inner_fast<"),
+KERNELS = {"dcn": ("embed_cross_ka", "rs::embed_cross_ka<"), "pnn": ("inner_fast_ka", "rs::inner_fast_ka<"),
            "nfm": ("pair_pool_ksplit", "rs::pair_pool_ksplit<"), "afm": ("pair_pool_ksplit", "rs::pair_pool_ksplit<"),
-           "ffm": ("ffm4_kernel", "rs::ffm4_kernel<"), "din": ("din_scores", "rs::din_scores<")}
+           "ffm": ("ffm4_kernel", "rs::ffm4_kernel<"), "din": ("din_fused", "rs::din_fused<")}
 
 
 def main():
