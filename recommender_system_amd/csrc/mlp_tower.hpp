@@ -414,7 +414,9 @@ __device__ __forceinline__ void mlp_tower_tile(const MlpArgs& a, float* smem, in
 // column, a wave sum).  Host side: mlp_tail_ok.
 inline bool mlp_tail_ok(const int* Np, const int* Kp, const int* N, int L, int l0, int& gwa, int& gwb) {
   // exactly two split layers after l0's caller-run layer, then a one-unit head
-  if (L != l0 + 3 || N[L - 1] != 1) return false;
+  // (+ at most one more 1 -> 1 layer: NFM's Dense(1) after its DNNLayer)
+  const bool extra = L == l0 + 4 && N[L - 2] == 1 && N[L - 1] == 1 && Kp[L - 1] == 16;
+  if ((L != l0 + 3 && !extra) || N[l0 + 2] != 1) return false;
   int gw[2];
   for (int q = 0; q < 2; ++q) {
     const int l = l0 + q, T = Np[l] >> 4, G = Kp[l] >> 4;
@@ -539,7 +541,17 @@ __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, i
     float z = 0.f;
     for (int t = 0; t < TB; ++t) z += redh[t * 16 + row];  // tile order
     const float* hb = par + a.poff[LH];
-    const float v = mlp_act(z + hb[0], a.act[LH], hb[a.Np[LH]]);
+    float v = mlp_act(z + hb[0], a.act[LH], hb[a.Np[LH]]);
+    if (a.L == LH + 2) {  // a trailing 1 -> 1 layer: v * W[0][0] + b, then its activation
+      const int L2 = LH + 1;
+      const float* hb2 = par + a.poff[L2];
+      float u;
+      {
+#pragma clang fp contract(off)  // product, then bias: as its MFMA epilogue would round
+        u = v * a.prep[a.off[L2]] + hb2[0];
+      }
+      v = mlp_act(u, a.act[L2], hb2[a.Np[L2]]);
+    }
     const int64_t m = m0 + row;
     if (m < a.M) {
       if (a.head == 0) {
