@@ -656,15 +656,19 @@ struct PipeArgs {
 
 template <int KV, int NT, int NW, int MC>
 __global__ __launch_bounds__(NW * 64) void shard_fm_pipe(EmbedFmArgs a, PipeArgs p) {
+  // the short route / combine blocks come first in dispatch order, the owner
+  // blocks (the headline kernel's body) after them: dispatched last, the
+  // owner tiles spread over the CUs the short blocks leave instead of
+  // doubling up behind them
   const int bid = blockIdx.x;
-  if (bid < p.owner_blocks) {
+  if (bid < p.route_blocks) {
+    field_route_part<NW * 64>(p.r, bid, p.route_blocks);
+  } else if (bid < p.route_blocks + p.combine_blocks) {
+    fm_combine_part<NW * 64>(p.c, bid - p.route_blocks, p.combine_blocks);
+  } else {
     // the headline kernel's schedule: B fragments of the first two passes and
     // both passes' ids issued before the first rows (PF)
-    embed_fm_body<KV, NT, NW, 4, false, MC, true>(a, nullptr, bid);
-  } else if (bid < p.owner_blocks + p.route_blocks) {
-    field_route_part<NW * 64>(p.r, bid - p.owner_blocks, p.route_blocks);
-  } else {
-    fm_combine_part<NW * 64>(p.c, bid - p.owner_blocks - p.route_blocks, p.combine_blocks);
+    embed_fm_body<KV, NT, NW, 4, false, MC, true>(a, nullptr, bid - p.route_blocks - p.combine_blocks);
   }
 }
 
