@@ -312,19 +312,28 @@ __global__ __launch_bounds__(256) void ffm_kernel(FfmArgs a) {
   for (int t = 0; t < NS; ++t) acc[t] = 0.f;
   // sparse rows first (the HBM gathers), then the dense rows (L2-resident)
   float lin = 0.f;
-  bool bad = false;
-  // CH fields per step: ids first, then CH * NS row loads in flight
+  // every field's id and table row up front (lane c = field c, F <= 64), as
+  // in ffm4_kernel; then CH fields per step with CH * NS row loads in flight
+  int64_t frow = 0;
+  bool fok = false;
+  if (lane < a.F) {
+    int64_t id;
+    fok = I::decode(I::load(a.ids, b * a.id_stride + lane), a.vocab[lane], id);
+    frow = a.nd + a.offs[lane] + id;
+  }
+  const bool bad = lane < a.F && !fok;
+  const uint64_t okm = __ballot(fok);
+  const int frow_lo = (int)(uint32_t)frow, frow_hi = (int)(uint32_t)((uint64_t)frow >> 32);
   constexpr int CH = NS >= 8 ? 4 : 8;
   for (int c0 = 0; c0 < a.F; c0 += CH) {
     int64_t row[CH];
     bool okc[CH];
 #pragma unroll
     for (int u = 0; u < CH; ++u) {
-      const int c = c0 + u < a.F ? c0 + u : a.F - 1;
-      int64_t id;
-      okc[u] = I::decode(I::load(a.ids, b * a.id_stride + c), a.vocab[c], id) && c0 + u < a.F;
-      bad |= c0 + u < a.F && !okc[u];
-      row[u] = a.nd + a.offs[c] + id;
+      const int c = c0 + u < a.F ? c0 + u : a.F - 1;  // wave-uniform
+      okc[u] = ((okm >> c) & 1) && c0 + u < a.F;
+      row[u] = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(frow_hi, c) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane(frow_lo, c));
     }
     float x[CH][NS];
 #pragma unroll
@@ -389,18 +398,29 @@ __global__ __launch_bounds__(256) void ffm4_kernel(FfmArgs a) {
 #pragma unroll
   for (int t = 0; t < NS; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
   float lin = 0.f;
-  bool bad = false;
+  // every field's id, validity and table row up front, lane c = field c (F <=
+  // 64): one id trip for the sample instead of one per chunk of fields (the
+  // chunks' row loads then wait on nothing but their own trip)
+  int64_t frow = 0;
+  bool fok = false;
+  if (lane < a.F) {
+    int64_t id;
+    fok = I::decode(I::load(a.ids, b * a.id_stride + lane), a.vocab[lane], id);
+    frow = a.nd + a.offs[lane] + id;
+  }
+  const bool bad = lane < a.F && !fok;
+  const uint64_t okm = __ballot(fok);
+  const int frow_lo = (int)(uint32_t)frow, frow_hi = (int)(uint32_t)((uint64_t)frow >> 32);
   constexpr int CH = NS >= 4 ? 4 : 8;  // 13 at NS = 2 ran 37 % slower (occupancy), 4 the same as 8
   for (int c0 = 0; c0 < a.F; c0 += CH) {
     int64_t row[CH];
     bool okc[CH];
 #pragma unroll
     for (int u = 0; u < CH; ++u) {
-      const int c = c0 + u < a.F ? c0 + u : a.F - 1;
-      int64_t id;
-      okc[u] = I::decode(I::load(a.ids, b * a.id_stride + c), a.vocab[c], id) && c0 + u < a.F;
-      bad |= c0 + u < a.F && !okc[u];
-      row[u] = a.nd + a.offs[c] + id;
+      const int c = c0 + u < a.F ? c0 + u : a.F - 1;  // wave-uniform
+      okc[u] = ((okm >> c) & 1) && c0 + u < a.F;
+      row[u] = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(frow_hi, c) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane(frow_lo, c));
     }
     floatx4 x[CH][NS];
 #pragma unroll

@@ -144,7 +144,7 @@ def test_nfm(gpu, k, B, id_dtype, hidden):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,B,nvoc,id_dtype", [(8, 200, 300, np.int32), (4, 31, 1000, np.int64),
-                                               (16, 7, 50, np.float32)])
+                                               (16, 7, 50, np.float32), (2, 33, 200, np.int32)])
 def test_ffm(gpu, k, B, nvoc, id_dtype):
     from recommender_system_amd import FFM
     rng = np.random.default_rng(k + B)
