@@ -170,6 +170,11 @@ def _capture(fn, first, count, begin=None, end=None):
 # driver's --steps 20 a 10-step leg carried ~2-4 us per step of graph-launch
 # and sync overhead (r4: deepfm_forward 24.1 us on the driver vs 22.0 at 200)
 NESTED_MIN_STEPS = 128
+# the peer legs' device waits: a working exchange waits microseconds; a broken
+# one (e.g. mailbox visibility across GPUs of a node this code never ran on)
+# gives up after ~1 s per wait instead of PeerExchange's default ~20 s, and
+# the RCCL value stands
+BENCH_PEER_SPIN = 1 << 20
 
 
 def _timed_graph(fn, steps, warmup, world, chunk=64, begin=None, end=None):
@@ -550,7 +555,8 @@ def _peer_exchange_leg(args, world, sh, ids_pool, dense_pool, outs, rccl_step_ms
     seq = [(dense_pool[j % npool], ids_pool[j % npool]) for j in range(T)]
     try:
         ref = [o.clone() for o in sh.forward_stream(seq, check=True)]
-        sh.use_peer_exchange()
+        sh.use_peer_exchange(spin_limit=BENCH_PEER_SPIN)
+        sh.forward_stream(seq[:1], check=True)  # one step first: a broken exchange fails after one bounded wait
         got = sh.forward_stream(seq, check=True)
         same = torch.tensor([int(all(torch.equal(a, b) for a, b in zip(ref, got)))], dtype=torch.int32,
                             device=ids_pool.device)
@@ -874,7 +880,7 @@ def _peer_leg_deepfm(args, world, model, dense_pool, ids_pool, out, step, rccl_d
     B = ids_pool.shape[1]
     try:
         ref = [model.forward((dense_pool[j], ids_pool[j]), check=True).clone() for j in range(3)]
-        model.use_peer_exchange()
+        model.use_peer_exchange(spin_limit=BENCH_PEER_SPIN)
         got = [model.forward((dense_pool[j], ids_pool[j]), check=True) for j in range(3)]
         same = torch.tensor([int(all(torch.equal(a, b) for a, b in zip(ref, got)))], dtype=torch.int32,
                             device=ids_pool.device)

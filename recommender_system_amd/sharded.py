@@ -695,22 +695,26 @@ class ShardedEmbeddingFM:
         return self.world > 1 or self._force_exchange
 
     # -- peer-mapped exchange (PeerExchange) in place of the RCCL all-to-all
-    def use_peer_exchange(self, on=True):
+    def use_peer_exchange(self, on=True, spin_limit=None):
         """Route the pipelined step's all-to-all (pipe_step / forward_stream)
         through PeerExchange mailboxes instead of RCCL.  Collective: every
         rank switches together (the mailboxes are created on first use, in
-        the same order on every rank)."""
+        the same order on every rank).  spin_limit: the mailboxes' bounded
+        device waits (PeerExchange's default when None)."""
         self._peer_on = bool(on)
         if not hasattr(self, "_peers"):
             self._peers = {}
+        if spin_limit is not None:
+            self._peer_spin = int(spin_limit)
 
     def _peer(self, name, nbytes):
         ex = self._peers.get(name)
         if ex is None or ex.world * ex.block_bytes != nbytes:
             if ex is not None:
                 ex.close()
+            kw = {"spin_limit": self._peer_spin} if getattr(self, "_peer_spin", None) else {}
             ex = PeerExchange(nbytes // self.world, group=self.group, world=self.world, rank=self.rank,
-                              device=self.device)
+                              device=self.device, **kw)
             self._peers[name] = ex
         return ex
 
@@ -1104,14 +1108,14 @@ class ShardedDeepFM:
         return outs
 
     # -- peer-mapped exchange (PeerExchange) in place of the two RCCL all-to-alls
-    def use_peer_exchange(self, on=True):
+    def use_peer_exchange(self, on=True, spin_limit=None):
         """forward's exchanges through PeerExchange mailboxes: the row-id
         records (rs_peer_a2a), then the owner's rows gathered straight into
         the requesters' mailboxes (rs_peer_gather_a2a: rs_gather_rows and the
         row all-to-all become one launch).  Collective; k = 16 only."""
         if on and self.k != 16:
             raise ValueError("ShardedDeepFM.use_peer_exchange: k must be 16")
-        self.emb.use_peer_exchange(on)
+        self.emb.use_peer_exchange(on, spin_limit=spin_limit)
 
     def close_peer_exchange(self):
         self.emb.close_peer_exchange()
