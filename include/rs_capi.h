@@ -90,7 +90,12 @@ enum rs_option {
   RS_OPT_DIN_KERNEL = 3,      /* rs_din_attention_ids_fwd at the reference's (80, 40) widths: 0
                                  (the default) = one launch (scores + softmax + pool, din_fused),
                                  1 = two launches (din_scores, din_pool).  See DESIGN.md 4.4     */
-  RS_OPT_COUNT = 4
+  RS_OPT_PEER_FENCES = 4,     /* the peer-mapped exchange's ordering (rs_peer_a2a, rs_peer_gather_a2a,
+                                 rs_shard_fm_pipe_peer): 0 (the default) = lean — write-through
+                                 data stores, relaxed counts, write-through flags, no L2
+                                 maintenance; 1 = a system-scope release / acquire fence around
+                                 every count and flag.  See DESIGN.md 4.6                        */
+  RS_OPT_COUNT = 5
 };
 
 /* ------------------------------------------- peer-mapped exchange (§8(e))
@@ -1132,6 +1137,37 @@ int rs_shard_fm_pipe(const int32_t* recv, int field_lo, int n_owned,
                      int n_fields, int k, const float* prepared,
                      const float* w0, int kfm, int* err_flag,
                      rs_stream_t stream);
+
+/* The TWO-DEEP pipelined step with the peer-mapped exchange inside the
+ * launch (sharded.py pipe2_step; replaces, for the step, the all-to-all
+ * torch.distributed would run before rs_shard_fm_pipe — the lookup sharded is
+ * EmbedLayer.call, layer/core.py:273-280).  Launch t = exchange of batch t+1
+ * (if `exchange`: this rank's send slot `xsend` = [world][batch] records of
+ * [row ids of t+1 | partials of t-1] copied into slot `xslot` of every
+ * peer's two-slot mailbox, rs_peer_a2a's ready / full protocol, one step of
+ * `peer_state`) | combine of batch t-2 (logit_prev) | owner partials of batch
+ * t | field route of batch t+2 (ids_next), the three pipe parts reading
+ * `recv` (= this rank's mailbox slot t % 2) and writing `send` (= send slot
+ * t % 2).  mailboxes: device array [world] of two-slot mailboxes
+ * (rs_peer_mailbox_bytes(world, 2 * batch * R * 4), R = slot_stride +
+ * rs_fm_partial_width(kfm)); the launch ends when every peer's block of this
+ * step is in this rank's mailbox.  A bounded wait that gives up sets
+ * RS_FLAG_TIMEOUT in xerr.  kfm <= 15, <= 32 owned fields, batch * R * 4 a
+ * multiple of 16 (else RS_ERR_UNSUPPORTED / RS_ERR_ARG).                    */
+int rs_shard_fm_pipe_peer(const int32_t* recv, int32_t* send,
+                          const int32_t* xsend, int xslot, int exchange,
+                          int field_lo, int n_owned, const float* shard,
+                          int64_t shard_rows, const float* dense_prev,
+                          int64_t dense_stride, float* logit_prev,
+                          const void* ids_next, int id_kind, int64_t id_stride,
+                          const int64_t* field_offsets,
+                          const int64_t* field_vocab, int64_t rows_per_rank,
+                          const int32_t* owner_fields, int slot_stride,
+                          int world, int64_t batch, int nd, int n_fields,
+                          int k, const float* prepared, const float* w0,
+                          int kfm, int* err_flag, void* const* mailboxes,
+                          int rank, void* peer_state, int chunks,
+                          int64_t spin_limit, int* xerr, rs_stream_t stream);
 
 /* FM over pre-gathered rows (sharded path): emb is [B, F*k] in x order.     */
 int rs_rows_fm_fwd(const float* emb, const float* dense, int64_t dense_stride,

@@ -160,6 +160,8 @@ SIGNATURES = {
     "rs_shard_owner_fm": (I, [P, L, I, I, P, L, I, I, I, P, I, P, L, L, P, P]),
     "rs_shard_fm_combine": (I, [P, L, I, L, P, L, I, I, I, P, P, I, P, P]),
     "rs_shard_fm_pipe": (I, [P, I, I, P, L, P, L, P, P, I, L, P, P, L, P, I, P, I, L, I, I, I, P, P, I, P, P]),
+    "rs_shard_fm_pipe_peer": (I, [P, P, P, I, I, I, I, P, L, P, L, P, P, I, L, P, P, L, P, I, I, L, I, I, I, P, P, I,
+                                  P, P, I, P, I, L, P, P]),
 }
 
 ID_I32, ID_I64, ID_F32 = 0, 1, 2
@@ -180,6 +182,7 @@ OPT_EMBED_FM_KERNEL = 0  # rs_option
 OPT_MLP_UNROLL = 1
 OPT_DEEPFM_KERNEL = 2
 OPT_DIN_KERNEL = 3
+OPT_PEER_FENCES = 4
 ACT = {None: 0, "linear": 0, "relu": 1, "prelu": 2, "sigmoid": 3}
 
 _lock = threading.Lock()

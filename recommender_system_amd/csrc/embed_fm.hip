@@ -27,6 +27,7 @@
 
 #include "embed_fm.hpp"
 #include "mlp_tower.hpp"
+#include "peer.hpp"
 #include "rs_common.hpp"
 #include "shard_route.hpp"
 
@@ -652,15 +653,30 @@ struct PipeArgs {
   int owner_blocks, route_blocks, combine_blocks;
   RouteArgs r;
   CombineArgs c;
+  // two-deep peer step (rs_shard_fm_pipe_peer, XCHG): the exchange of the
+  // NEXT batch's records (x.chunks x x.world workgroups, first in dispatch
+  // order) rides in this launch beside the pipe parts of this batch
+  int xchg_blocks;
+  PeerArgs x;
 };
 
-template <int KV, int NT, int NW, int MC>
+template <int KV, int NT, int NW, int MC, bool XCHG = false>
 __global__ __launch_bounds__(NW * 64) void shard_fm_pipe(EmbedFmArgs a, PipeArgs p) {
   // the short route / combine blocks come first in dispatch order, the owner
   // blocks (the headline kernel's body) after them: dispatched last, the
   // owner tiles spread over the CUs the short blocks leave instead of
-  // doubling up behind them
-  const int bid = blockIdx.x;
+  // doubling up behind them.  XCHG: the exchange workgroups before all of
+  // them (workgroup 0 publishes this rank's mailbox readiness at once; they
+  // wait on peers, never on the other parts of this launch, and those never
+  // wait, so the launch drains whatever the dispatch order)
+  int bid = blockIdx.x;
+  if constexpr (XCHG) {
+    if (bid < p.xchg_blocks) {
+      peer_a2a_part<false>(p.x, bid / p.x.world, bid % p.x.world);
+      return;
+    }
+    bid -= p.xchg_blocks;
+  }
   if (bid < p.route_blocks) {
     field_route_part<NW * 64>(p.r, bid, p.route_blocks);
   } else if (bid < p.route_blocks + p.combine_blocks) {
@@ -1742,14 +1758,32 @@ extern "C" int rs_diag_embed_fm_fwd(const void* ids, int id_kind, int64_t id_str
 // (layer/interaction.py:106-114 regrouped; same reassociation as the headline).
 namespace rs {
 
-template <int KV, int NT, int NW, int MC>
+template <int KV, int NT, int NW, int MC, bool XCHG = false>
 static void launch_pipe4(const EmbedFmArgs& a, PipeArgs p, hipStream_t st) {
   const int T = NW * 64;
   p.owner_blocks = a.F > 0 ? (int)((a.batch + 15) / 16) : 0;
   if (p.route_blocks) p.route_blocks = (int)std::min<int64_t>((p.r.total + T - 1) / T, 4096);
   if (p.combine_blocks) p.combine_blocks = (int)std::min<int64_t>((p.c.batch * 16 + T - 1) / T, 4096);
-  const int grid = p.owner_blocks + p.route_blocks + p.combine_blocks;
-  if (grid) shard_fm_pipe<KV, NT, NW, MC><<<grid, T, 0, st>>>(a, p);
+  if (!XCHG) p.xchg_blocks = 0;
+  const int grid = p.xchg_blocks + p.owner_blocks + p.route_blocks + p.combine_blocks;
+  if (grid) shard_fm_pipe<KV, NT, NW, MC, XCHG><<<grid, T, 0, st>>>(a, p);
+}
+
+// the two-deep peer step: 1-tile (kfm <= 15) owner part with <= 32 fields
+template <int KV>
+static void launch_pipe_xchg_kv(const EmbedFmArgs& a, const PipeArgs& p, hipStream_t st) {
+  if (a.F <= 4) launch_pipe4<KV, 1, 4, 1, true>(a, p, st);
+  else if (a.F <= 8) launch_pipe4<KV, 1, 8, 1, true>(a, p, st);
+  else launch_pipe4<KV, 1, 16, 1, true>(a, p, st);
+}
+static void launch_pipe_xchg(const EmbedFmArgs& a, const PipeArgs& p, const FmGeom& g, hipStream_t st) {
+  switch (g.KV) {
+    case 1: launch_pipe_xchg_kv<1>(a, p, st); break;
+    case 2: launch_pipe_xchg_kv<2>(a, p, st); break;
+    case 4: launch_pipe_xchg_kv<4>(a, p, st); break;
+    case 8: launch_pipe_xchg_kv<8>(a, p, st); break;
+    default: launch_pipe_xchg_kv<16>(a, p, st); break;
+  }
 }
 
 // NW / MC by the owner's field count: 4 waves x 1 slot for <= 4 fields (the
@@ -1926,6 +1960,82 @@ extern "C" int rs_shard_fm_pipe(const int32_t* recv, int field_lo, int n_owned, 
   }
   launch_pipe(a, p, g, st);
   return launch_status("rs_shard_fm_pipe");
+}
+
+// The two-deep pipelined step with the peer exchange inside the launch:
+// launch t = exchange of batch t+1's records [row ids of t+1 | partials of
+// t-1] (send slot xslot -> every peer's mailbox slot xslot) | combine of t-2 |
+// owner partials of t | route of t+2, the pipe parts reading this rank's
+// mailbox slot (recv) and writing send slot t % 2 (send).  Host contract in
+// sharded.py (ShardedEmbeddingFM.pipe2_step); protocol in peer.hip.
+extern "C" int rs_shard_fm_pipe_peer(const int32_t* recv, int32_t* send, const int32_t* xsend, int xslot,
+                                     int exchange, int field_lo, int n_owned, const float* shard, int64_t shard_rows,
+                                     const float* dense_prev, int64_t dense_stride, float* logit_prev,
+                                     const void* ids_next, int id_kind, int64_t id_stride,
+                                     const int64_t* field_offsets, const int64_t* field_vocab, int64_t rows_per_rank,
+                                     const int32_t* owner_fields, int slot_stride, int world, int64_t batch, int nd,
+                                     int n_fields, int k, const float* prepared, const float* w0, int kfm,
+                                     int* err_flag, void* const* mailboxes, int rank, void* peer_state, int chunks,
+                                     int64_t spin_limit, int* xerr, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(batch > 0 && world >= 1 && world <= PEER_MAXW && rank >= 0 && rank < world && nd >= 0 &&
+                 n_fields >= 1 && k >= 1 && kfm >= 1 && slot_stride >= 1 && slot_stride <= n_fields &&
+                 field_lo >= 0 && n_owned >= 0 && field_lo + n_owned <= n_fields && n_owned <= slot_stride &&
+                 shard_rows >= 0 && rows_per_rank >= 1 && (xslot == 0 || xslot == 1),
+             "rs_shard_fm_pipe_peer: bad shape");
+  RS_REQUIRE(recv && send && prepared && w0 && (n_owned == 0 || shard || shard_rows == 0),
+             "rs_shard_fm_pipe_peer: null pointer");
+  RS_REQUIRE(!exchange || (xsend && mailboxes && peer_state && xerr), "rs_shard_fm_pipe_peer: exchange inputs missing");
+  RS_REQUIRE(!exchange || (chunks >= 1 && (int64_t)chunks * world <= 1024 && spin_limit >= 1),
+             "rs_shard_fm_pipe_peer: bad chunks / limit");
+  RS_REQUIRE(!ids_next || (field_offsets && field_vocab && owner_fields),
+             "rs_shard_fm_pipe_peer: route inputs missing");
+  RS_REQUIRE(!logit_prev || nd == 0 || dense_prev, "rs_shard_fm_pipe_peer: dense_prev is null");
+  RS_REQUIRE((uintptr_t)shard % 16 == 0, "rs_shard_fm_pipe_peer: shard must be 16-B aligned");
+  RS_REQUIRE((int64_t)world * batch * (slot_stride + 32) < ((int64_t)1 << 31) && rows_per_rank < ((int64_t)1 << 31),
+             "rs_shard_fm_pipe_peer: too many slots / shard rows must fit int32");
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32, "rs_shard_fm_pipe_peer: bad id_kind");
+  RS_PIPE_GEOM("rs_shard_fm_pipe_peer");
+  if (g.NT != 1 || n_owned > 32) {
+    set_error("rs_shard_fm_pipe_peer: needs kfm <= 15 and <= 32 owned fields");
+    return RS_ERR_UNSUPPORTED;
+  }
+  const int64_t R = slot_stride + pw;
+  hipStream_t st = as_stream(stream);
+  const int64_t n_pairs = (int64_t)world * batch;
+  float* pout = reinterpret_cast<float*>(send + slot_stride);
+  const float* pin = reinterpret_cast<const float*>(recv + slot_stride);
+  EmbedFmArgs a{};
+  if (n_owned > 0) {
+    a = owner_args(g, recv, R, field_lo, n_owned, shard, shard_rows, k, prepared, kfm, pout, R, n_pairs, err_flag);
+  } else {
+    (void)hipMemset2DAsync(pout, R * sizeof(float), 0, pw * sizeof(float), n_pairs, st);
+  }
+  PipeArgs p{};
+  if (ids_next) {
+    p.route_blocks = 1;
+    p.r = RouteArgs{ids_next, id_kind, id_stride, field_offsets, field_vocab, rows_per_rank, owner_fields,
+                    slot_stride, (int)batch, R, send, err_flag, (int64_t)world * batch * slot_stride};
+  }
+  if (logit_prev) {
+    p.combine_blocks = 1;
+    p.c = CombineArgs{pin, R, world, batch, dense_prev, dense_stride, nd, prepared, g.dense_rec, g.NT, w0, kfm,
+                      logit_prev};
+  }
+  if (exchange) {
+    const int64_t blk = batch * R * 4;  // bytes of one rank's records for one peer
+    if (blk % 16) {
+      set_error("rs_shard_fm_pipe_peer: batch * record bytes must be a multiple of 16");
+      return RS_ERR_ARG;
+    }
+    p.xchg_blocks = chunks * world;
+    p.x = PeerArgs{reinterpret_cast<const char*>(xsend), blk, reinterpret_cast<char* const*>(mailboxes),
+                   (2 * (int64_t)world * blk + 255) / 256 * 256, static_cast<PeerState*>(peer_state), rank, world,
+                   chunks, spin_limit, xerr, nullptr, 0, nullptr, 0, (int64_t)xslot * world * blk,
+                   opt(RS_OPT_PEER_FENCES) == 0};
+  }
+  launch_pipe_xchg(a, p, g, st);
+  return launch_status("rs_shard_fm_pipe_peer");
 }
 
 extern "C" int rs_rows_fm_fwd(const float* emb, const float* dense, int64_t dense_stride, int nd, int n_fields,

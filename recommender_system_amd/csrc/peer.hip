@@ -35,122 +35,13 @@
 // can be read after a peer's writes.
 #include <string.h>
 
-#include "rs_common.hpp"
+#include "peer.hpp"
 
 namespace rs {
 
-struct PeerState {  // per-rank local state, rs_peer_state_bytes() bytes, zeroed by the caller once
-  unsigned long long seq;
-  unsigned int total;
-  unsigned int pad[29];
-  unsigned int cnt[64];  // per destination: chunks written this step
-};
-constexpr int PEER_MAXW = 64;
-constexpr int PEER_FLAG_STRIDE = 128;  // bytes: each flag on its own line
-
-struct PeerArgs {
-  const char* send;      // [world][block_bytes], local (GATHER: unused)
-  int64_t block_bytes;   // multiple of 16
-  char* const* mbox;     // device array [world]: every rank's mailbox base (mine at [rank])
-  int64_t data_bytes;    // world * block_bytes, rounded up to 256 (offset of the flags)
-  PeerState* st;
-  int rank, world, chunks;  // chunks per destination (grid = chunks x world)
-  int64_t spin_limit;
-  int* err;
-  // GATHER (rs_peer_gather_a2a): block p is gathered on the fly — row ids[p][i]
-  // of the local table shard (k = 16 floats, -1 = a zero row) for every word i
-  const int32_t* ids;  // [world][nw] local row ids (the requests each peer sent me)
-  int64_t nw;
-  const float* table;
-  int64_t n_rows;
-};
-
-__device__ __forceinline__ unsigned long long* peer_flag(char* mbox, int64_t data_bytes, int which, int world,
-                                                         int r) {
-  return reinterpret_cast<unsigned long long*>(mbox + data_bytes +
-                                               ((int64_t)which * world + r) * PEER_FLAG_STRIDE);
-}
-
-// bounded wait until *f >= v (one lane); false on timeout
-__device__ __forceinline__ bool peer_wait_ge(unsigned long long* f, unsigned long long v, int64_t limit) {
-  for (int64_t i = 0; i < limit; ++i) {
-    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= v) return true;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= v;
-}
-
 template <bool GATHER>
 __global__ __launch_bounds__(256) void peer_a2a_kernel(PeerArgs a) {
-  const int c = blockIdx.x, p = blockIdx.y;
-  const unsigned long long seq = a.st->seq + 1;
-  __shared__ int ok_s;
-  bool ok = true;
-  // 1. my mailbox is free for this step: tell every peer
-  if (c == 0 && p == 0 && threadIdx.x < (unsigned)a.world)
-    __hip_atomic_store(peer_flag(a.mbox[threadIdx.x], a.data_bytes, 0, a.world, a.rank), seq, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-  // 2. peer p's mailbox free for this step? (p's step 1 wrote ready[p] in MY mailbox: a local poll)
-  if (threadIdx.x == 0) ok_s = peer_wait_ge(peer_flag(a.mbox[a.rank], a.data_bytes, 0, a.world, p), seq, a.spin_limit);
-  __syncthreads();
-  ok = ok_s != 0;
-  if (ok) {
-    const int64_t per = (a.block_bytes / 16 + a.chunks - 1) / a.chunks;  // 16-B words per chunk
-    const int64_t w0 = (int64_t)c * per, w1 = min<int64_t>(w0 + per, a.block_bytes / 16);
-    floatx4* dst = reinterpret_cast<floatx4*>(a.mbox[p] + (int64_t)a.rank * a.block_bytes);
-    if constexpr (GATHER) {
-      // 4 lanes per 64-B row: row ids[p][i >> 2], quarter i & 3 (non-temporal: read once)
-      const int32_t* rid = a.ids + (int64_t)p * a.nw;
-      bool bad = false;
-      for (int64_t i = w0 + threadIdx.x; i < w1; i += blockDim.x) {
-        const int64_t r = rid[i >> 2];
-        floatx4 x = {0.f, 0.f, 0.f, 0.f};
-        if (r >= 0 && r < a.n_rows) x = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(a.table + r * 16) + (i & 3));
-        else bad |= r != -1;
-        dst[i] = x;
-      }
-      if (__any(bad) && (threadIdx.x & 63) == 0) flag_error(a.err);
-    } else {
-      const floatx4* src = reinterpret_cast<const floatx4*>(a.send + (int64_t)p * a.block_bytes);
-      for (int64_t i = w0 + threadIdx.x; i < w1; i += blockDim.x) dst[i] = src[i];
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (!ok) flag_error(a.err, RS_FLAG_TIMEOUT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: my chunk before the count / flag
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(&a.st->cnt[p], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == (unsigned)a.chunks - 1) {
-      a.st->cnt[p] = 0;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-      __hip_atomic_store(peer_flag(a.mbox[p], a.data_bytes, 1, a.world, a.rank), seq, __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    __hip_atomic_fetch_add(&a.st->total, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // 3. workgroup 0: the whole step in my mailbox, every workgroup counted
-  if (c == 0 && p == 0) {
-    bool done = true;
-    if (threadIdx.x < (unsigned)a.world)
-      done = peer_wait_ge(peer_flag(a.mbox[a.rank], a.data_bytes, 1, a.world, threadIdx.x), seq, a.spin_limit);
-    if (threadIdx.x == 0) {
-      const unsigned nblk = (unsigned)a.chunks * (unsigned)a.world;
-      int64_t i = 0;
-      for (; i < a.spin_limit && __hip_atomic_load(&a.st->total, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < nblk;
-           ++i)
-        __builtin_amdgcn_s_sleep(2);
-      done = done && i < a.spin_limit;
-    }
-    if (!done) flag_error(a.err, RS_FLAG_TIMEOUT);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-      a.st->total = 0;
-      a.st->seq = seq;
-    }
-  }
+  peer_a2a_part<GATHER>(a, blockIdx.x, blockIdx.y);
 }
 
 }  // namespace rs
@@ -237,7 +128,7 @@ extern "C" int rs_peer_a2a(const void* send, int64_t block_bytes, void* const* m
   RS_REQUIRE(chunks >= 1 && (int64_t)chunks * world <= 1024 && spin_limit >= 1, "rs_peer_a2a: bad chunks / limit");
   PeerArgs a{static_cast<const char*>(send), block_bytes, reinterpret_cast<char* const*>(mailboxes),
              ((int64_t)world * block_bytes + 255) / 256 * 256, static_cast<PeerState*>(state), rank, world, chunks,
-             spin_limit, err_flag, nullptr, 0, nullptr, 0};
+             spin_limit, err_flag, nullptr, 0, nullptr, 0, 0, opt(RS_OPT_PEER_FENCES) == 0};
   peer_a2a_kernel<false><<<dim3(chunks, world), 256, 0, as_stream(stream)>>>(a);
   return launch_status("rs_peer_a2a");
 }
@@ -254,7 +145,7 @@ extern "C" int rs_peer_gather_a2a(const int32_t* ids, int64_t nw, const float* t
   const int64_t block_bytes = nw * 64;
   PeerArgs a{nullptr, block_bytes, reinterpret_cast<char* const*>(mailboxes),
              ((int64_t)world * block_bytes + 255) / 256 * 256, static_cast<PeerState*>(state), rank, world, chunks,
-             spin_limit, err_flag, ids, nw, table, n_rows};
+             spin_limit, err_flag, ids, nw, table, n_rows, 0, opt(RS_OPT_PEER_FENCES) == 0};
   peer_a2a_kernel<true><<<dim3(chunks, world), 256, 0, as_stream(stream)>>>(a);
   return launch_status("rs_peer_gather_a2a");
 }

@@ -317,6 +317,21 @@ class HipShardOps:
              ptr(sh.owner_fields), sh.slot_stride, ptr(send), sh.world, B, sh.nd, sh.F, sh.k, ptr(sh.prepared),
              ptr(sh.w0), sh.kfm, ptr(self.err), _lib.stream())
 
+    def pipe_peer(self, sh, recv, send, xsend, xslot, exchange, ex, prev=None, cur=None, nxt=None, B=None):
+        """rs_shard_fm_pipe_peer: E(t+1) (send slot xslot -> the peers'
+        mailbox slot xslot, if ``exchange``) | combine(prev) | owner(cur) |
+        route(nxt = ids) in ONE launch (sharded.py pipe2_step)."""
+        lo, n_own = sh.owner_field_ranges[sh.rank]
+        if cur is None:
+            n_own = 0  # no owner part this step (its partial words are never read)
+        call("rs_shard_fm_pipe_peer", ptr(recv), ptr(send), ptr(xsend), int(xslot), int(bool(exchange)), lo, n_own,
+             ptr(sh.table_shard), sh.table_shard.shape[0], ptr(prev[0]) if prev is not None else None,
+             prev[0].stride(0) if prev is not None else 0, ptr(prev[1]) if prev is not None else None, ptr(nxt),
+             _lib.id_kind(nxt) if nxt is not None else 0, nxt.stride(0) if nxt is not None else 0, ptr(sh.offsets),
+             ptr(sh.vocab), sh.rows_per_rank, ptr(sh.owner_fields), sh.slot_stride, sh.world, B, sh.nd, sh.F, sh.k,
+             ptr(sh.prepared), ptr(sh.w0), sh.kfm, ptr(self.err), ptr(ex.mailboxes), sh.rank, ptr(ex.state),
+             ex.chunks, ex.spin_limit, ptr(ex.err), _lib.stream())
+
     # -- training (ShardedEmbeddingFM.train_step)
     def combine_grad(self, sh, partials, dense, labels, scale, logit, gs, loss=None):
         B = dense.shape[0]
@@ -771,6 +786,147 @@ class ShardedEmbeddingFM:
             cur = batches[t][1] if t < n else None
             nxt = batches[t + 1] if t + 1 < n else None
             self.pipe_step(prev, cur, nxt)
+        if check:
+            raise_flag(self.ops.bad_flag(), "sharded lookup", self.group, self.world)
+            if getattr(self, "_peer_on", False):
+                self._peer_check()
+        return outs
+
+    # -- the TWO-DEEP pipelined partial protocol: the exchange off the critical path
+    # Step t runs the exchange of batch t+1 BESIDE the pipe parts of batch t:
+    #   E(t+1): [row ids of t+1 | partials of t-1]  (send slot (t+1) % 2 -> recv slot (t+1) % 2)
+    #   P(t)  : combine(t-2) | owner partials of t | field route of t+2
+    #           (reads recv slot t % 2, writes send slot t % 2)
+    # E(t+1) needs only P(t-1)'s records and P(t) only E(t)'s, so the two
+    # overlap: a step costs max(pipe, exchange) instead of pipe + exchange.
+    # Peer exchange: ONE launch per step (rs_shard_fm_pipe_peer: the exchange
+    # workgroups ride in the pipe launch; two-slot mailboxes).  RCCL: the
+    # all-to-all stays on the caller's stream, the pipe launch goes to a side
+    # stream; events order E(t+1) after P(t-1) and P(t) after E(t).  The
+    # per-batch arithmetic is the one-deep step's, so the logits are
+    # bit-identical to ``forward_stream``.
+    def _s2bufs(self, B):
+        sb = getattr(self, "_stream2_bufs", None)
+        if sb is None or sb["B"] != B:
+            R = self.slot_stride + self.partial_width
+            n = self.world * B * R
+            sb = {"B": B, "R": R, "n": n,
+                  "send": torch.zeros(2, n, dtype=torch.int32, device=self.device),
+                  "recv": torch.zeros(2, n, dtype=torch.int32, device=self.device)}
+            self._stream2_bufs = sb
+            self._p2_slot = 0
+        return sb
+
+    def _peer2(self, sb):
+        """The two-slot mailboxes of the two-deep peer step (one PeerExchange
+        of block 2 * B * R * 4 bytes: its data region is read as [2][world][B*R])."""
+        blk = sb["B"] * sb["R"] * 4
+        chunks = max(1, min(1024 // self.world, -(-blk // 16384)))
+        ex = self._peers.get("pipe2")
+        if ex is None or ex.block_bytes != 2 * blk:
+            if ex is not None:
+                ex.close()
+            kw = {"spin_limit": self._peer_spin} if getattr(self, "_peer_spin", None) else {}
+            ex = PeerExchange(2 * blk, group=self.group, world=self.world, rank=self.rank, device=self.device,
+                              chunks=chunks, **kw)
+            self._peers["pipe2"] = ex
+        return ex
+
+    def pipe2_prologue(self, ids0, ids1=None):
+        """Prologue of a two-deep stream: route batches 0 and 1 into the send
+        slots and run E(0) (launch t = -1).  Resets the slot parity."""
+        sb = self._s2bufs(ids0.shape[0])
+        self._p2_slot = 0
+        self.ops.field_route(self, ids0, sb["send"][0], rec=sb["R"])
+        if ids1 is not None:
+            self.ops.field_route(self, ids1, sb["send"][1], rec=sb["R"])
+        self._p2_slot = 1  # launch t = -1 has slot (-1) % 2 = 1: its exchange carries send slot 0
+        self.pipe2_step(exchange=True, B=ids0.shape[0])
+
+    def pipe2_step(self, prev=None, cur=None, nxt=None, exchange=True, B=None):
+        """One two-deep step t (slot parity kept here, flipped every call):
+        exchange E(t+1) of send slot (t+1) % 2 if ``exchange``, combine of
+        prev = (dense, out) of batch t-2, owner partials of cur = ids of batch
+        t, field route of nxt = ids of batch t+2 (any may be None)."""
+        if B is None:
+            B = next(x for x in (cur, prev and prev[0], nxt) if x is not None).shape[0]
+        sb = self._s2bufs(B)
+        if not self.exchanges:
+            raise RuntimeError("pipe2_step: the two-deep step needs the exchange (world > 1 or a forced one)")
+        slot = self._p2_slot
+        xs = 1 - slot
+        self._p2_slot = xs
+        pipe = prev is not None or cur is not None or nxt is not None
+        if getattr(self, "_peer_on", False):
+            ex = self._peer2(sb)
+            mbox = ex.recv.view(torch.int32).view(2, sb["n"])
+            self.ops.pipe_peer(self, mbox[slot], sb["send"][slot], sb["send"][xs], xs, exchange, ex,
+                               prev=prev, cur=cur, nxt=nxt, B=B)
+            return
+        on_gpu = self.device.type == "cuda"
+        nx = (None, nxt) if nxt is not None else None  # ops.pipe takes (dense, ids)
+        if exchange:
+            if on_gpu and getattr(self, "_p2_evp", None) is not None:
+                torch.cuda.current_stream(self.device).wait_event(self._p2_evp)
+            dist.all_to_all_single(sb["recv"][xs], sb["send"][xs], group=self.group)
+            if on_gpu:
+                self._p2_eve_next = torch.cuda.Event()
+                self._p2_eve_next.record(torch.cuda.current_stream(self.device))
+        if pipe:
+            if on_gpu:
+                side = self._p2_side_stream()
+                if getattr(self, "_p2_eve", None) is not None:
+                    side.wait_event(self._p2_eve)
+                with torch.cuda.stream(side):
+                    self.ops.pipe(self, sb["recv"][slot], sb["send"][slot], prev=prev, cur=cur, nxt=nx)
+                self._p2_evp = torch.cuda.Event()
+                self._p2_evp.record(side)
+            else:
+                self.ops.pipe(self, sb["recv"][slot], sb["send"][slot], prev=prev, cur=cur, nxt=nx)
+        if on_gpu:
+            self._p2_eve = self._p2_eve_next if exchange else None
+
+    def _p2_side_stream(self):
+        s = getattr(self, "_p2_side", None)
+        if s is None:
+            s = self._p2_side = torch.cuda.Stream(self.device)
+        return s
+
+    def pipe2_begin(self):
+        """Fork the side stream off the caller's stream and forget earlier
+        events (the start of a captured / timed run of RCCL two-deep steps)."""
+        self._p2_evp = self._p2_eve = None
+        if self.device.type == "cuda" and not getattr(self, "_peer_on", False):
+            self._p2_side_stream().wait_stream(torch.cuda.current_stream(self.device))
+
+    def pipe2_join(self):
+        """The caller's stream waits for the side stream's pipe launches (RCCL
+        two-deep step; a no-op for the peer step, which has no side stream)."""
+        if self.device.type == "cuda" and getattr(self, "_p2_side", None) is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._p2_side)
+
+    def forward_stream2(self, batches, check=True):
+        """FM logits of a sequence of local batches [(dense, ids), ...] with the
+        two-deep pipelined protocol (``pipe2_step``); bit-identical to
+        ``forward_stream``.  n batches cost n + 3 launches (peer exchange: each
+        carries the next batch's exchange) or n + 1 all-to-alls beside n + 2
+        pipe launches (RCCL).  Every rank passes the same number of batches."""
+        n = len(batches)
+        outs = [torch.empty(ids.shape[0], 1, dtype=torch.float32, device=self.device) for _, ids in batches]
+        if not n:
+            return outs
+        if check:
+            self.ops.clear_flags()
+        self._p2_evp = self._p2_eve = None
+        self.pipe2_prologue(batches[0][1], batches[1][1] if n > 1 else None)
+        for t in range(0, n + 2):
+            exchange = t + 1 < n or 1 <= t <= n
+            prev = (batches[t - 2][0], outs[t - 2]) if 0 <= t - 2 < n else None
+            cur = batches[t][1] if t < n else None
+            nxt = batches[t + 2][1] if t + 2 < n else None
+            self.pipe2_step(prev, cur, nxt, exchange=exchange, B=batches[0][1].shape[0])
+        self.pipe2_join()
+        self._p2_evp = self._p2_eve = None
         if check:
             raise_flag(self.ops.bad_flag(), "sharded lookup", self.group, self.world)
             if getattr(self, "_peer_on", False):

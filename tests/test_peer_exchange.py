@@ -10,7 +10,12 @@ exported and mapped through hipIpc handles, the step flags crossing processes.
   peer exchange gives bit-identical logits to the same step with the gloo
   all-to-all, and both equal the fp64 oracle on the global table;
 * graph capture: the exchange and the pipe kernel captured once and
-  replayed give the eager results (the step number lives on the device).
+  replayed give the eager results (the step number lives on the device);
+* the TWO-DEEP step (ShardedEmbeddingFM.forward_stream2: the exchange of
+  batch t+1 beside the pipe launch of batch t — inside it for the peer
+  exchange, rs_shard_fm_pipe_peer; on a side stream for the collective) gives
+  the one-deep logits bit for bit, for streams of 1, 2 and 5 batches, eager
+  and graph-replayed.
 
 GPU-marked; two processes on cuda:0, gloo for the host-side collectives."""
 import os
@@ -40,11 +45,15 @@ def _init(rank, world, port):
 def _a2a_worker(rank, world, port, q):
     try:
         _init(rank, world, port)
+        from recommender_system_amd import _lib
         from recommender_system_amd.sharded import PeerExchange
         blk = 40 * 1024 + 16  # not a multiple of the chunking
         ex = PeerExchange(blk, world=world, rank=rank, device="cuda")
         ok = True
-        for step in range(6):
+        for step in range(8):
+            # both orderings (RS_OPT_PEER_FENCES: lean write-through / full
+            # fences), switching between steps on the same mailboxes
+            _lib.set_option(_lib.OPT_PEER_FENCES, (step // 2) % 2)
             g = torch.Generator(device="cpu")
             g.manual_seed(1000 * step + rank)
             send = torch.randint(0, 256, (world * blk,), generator=g, dtype=torch.uint8)
@@ -73,15 +82,36 @@ def _pipe_worker(rank, world, port, q):
         vocabs = [5000, 17, 3000, 1, 700, 2500, 40, 900, 1200, 8]
         k, nd, kfm, B, T = 16, 3, 10, 96, 5
         res = {}
-        for mode in ("gloo", "peer"):
+        for mode in ("gloo", "gloo2", "peer2", "peer"):
             sh = ShardedEmbeddingFM(vocabs, k, nd, kfm, device="cuda", seed=3)
-            if mode == "peer":
+            if mode.startswith("peer"):
                 sh.use_peer_exchange()
             g = torch.Generator(device="cpu")
             g.manual_seed(77 + rank)
             batches = [(torch.rand(B, nd, generator=g).cuda(),
                         torch.stack([torch.randint(0, v, (B,), generator=g) for v in vocabs], 1).int().cuda())
                        for _ in range(T)]
+            if mode.endswith("2"):
+                # two-deep: exchange of t+1 beside the pipe of t (the peer
+                # exchange inside the pipe launch; gloo: a side stream)
+                outs = sh.forward_stream2(batches, check=True)
+                res[mode] = torch.cat([o.cpu() for o in outs])
+                res[mode + "_short"] = [torch.cat([o.cpu() for o in sh.forward_stream2(batches[:n_], check=True)])
+                                        for n_ in (1, 2)]
+                if mode == "peer2":
+                    torch.cuda.synchronize()
+                    side = torch.cuda.Stream()
+                    side.wait_stream(torch.cuda.current_stream())
+                    graph = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(graph, stream=side):
+                        gouts = sh.forward_stream2(batches, check=False)
+                    graph.replay()
+                    graph.replay()
+                    torch.cuda.synchronize()
+                    sh._peer_check()
+                    res["graph2"] = torch.cat([o.cpu() for o in gouts])
+                    sh.close_peer_exchange()
+                continue
             outs = sh.forward_stream(batches, check=True)
             res[mode] = torch.cat([o.cpu() for o in outs])
             if mode == "peer":
@@ -112,6 +142,10 @@ def _pipe_worker(rank, world, port, q):
                 sh.close_peer_exchange()
         ok = torch.equal(res["gloo"], res["peer"]) and torch.equal(res["peer"], res["graph"]) and \
             res["oracle_err"] <= 1e-5
+        for m2 in ("gloo2", "peer2"):
+            ok = ok and torch.equal(res[m2], res["gloo"]) and \
+                all(torch.equal(s_, res["gloo"][:s_.shape[0]]) for s_ in res[m2 + "_short"])
+        ok = ok and torch.equal(res["graph2"], res["gloo"])
         q.put((rank, ok, f"oracle_err={res['oracle_err']:.2e}"))
     except Exception as e:
         import traceback

@@ -394,6 +394,12 @@ def _worker(rank, world, port, vocabs, k, B, q):
         outs = sh.forward_stream(list(zip(d2, i2)))
         for d_, i_, o_ in zip(d2, i2, outs):
             ok_part = ok_part and np.allclose(o_.numpy(), sh.forward(d_, i_).numpy(), rtol=1e-6, atol=1e-7)
+        # two-deep (exchange of t+1 beside the pipe of t): the same logits, bit
+        # for bit, for every stream length (prologue / drain edge cases)
+        for n_ in (1, 2, 3):
+            o2 = sh.forward_stream2(list(zip(d2, i2))[:n_])
+            ok_part = ok_part and all(torch.equal(a, b) for a, b in zip(o2, outs[:n_] if n_ == 3 else
+                                                                       sh.forward_stream(list(zip(d2, i2))[:n_])))
         q.put((rank, ok_rows and ok_part, float(np.max(np.abs(fm_sh - fm_ref))), sh.row_range))
     finally:
         dist.destroy_process_group()
