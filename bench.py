@@ -355,6 +355,48 @@ def cpu_baseline_hotpath(model, ids_pool, dense_pool, budget_s, max_batches=64):
                       f"table host copy {t_copy:.1f}s excluded"}, gpu_check
 
 
+def _streamed_leg(args, world, model, ids_pool, dense_pool, step, logit, alg_bytes):
+    """The hot path over S consecutive batch-B requests in ONE launch
+    (DeepFM.fm_logit_stream / rs_embed_fm_fwd_hm_stream: tile g % tpb of batch
+    g / tpb, the per-batch kernel's body): µs per batch, its HBM roofline
+    fraction, and the check that every batch's logits are bit-identical to
+    the single-launch step's.  min_blocks 1 / 2 (resident workgroups per CU)
+    both timed; the faster is reported first."""
+    B = ids_pool.shape[1]
+    out = {}
+    for S in (8, 32):
+        sout = torch.empty(S, B, 1, device=ids_pool.device)
+        ref = []
+        for j in range(S):
+            step(j)
+            ref.append(logit.clone())
+        legs = {}
+        for mb in (1, 2):
+            model.fm_logit_stream(dense_pool[:S], ids_pool[:S], min_blocks=mb, out=sout, check_ids=True)
+            same = all(torch.equal(sout[j], ref[j]) for j in range(S))
+            npool = ids_pool.shape[0] // S
+
+            def stream_step(i, mb=mb):
+                j0 = (i % npool) * S
+                model.fm_logit_stream(dense_pool[j0:j0 + S], ids_pool[j0:j0 + S], min_blocks=mb, out=sout,
+                                      check_ids=False)
+
+            n = max(NESTED_MIN_STEPS // 4, args.steps // S)
+            dt, slot = _timed_graph(stream_step, n, 5, world, chunk=8)
+            us = slot * 1e3 / S
+            legs[f"min_blocks_{mb}"] = {"us_per_batch": us, "launch_us": slot * 1e3,
+                                        "samples_per_s": n * S * B / dt,
+                                        "frac": alg_bytes / (us * 1e-6) / PEAK_HBM,
+                                        "frac_of_random_row_ceiling": alg_bytes / (us * 1e-6) / 3.31e12,
+                                        "bit_identical_to_single_launch": bool(same)}
+        best = min(legs, key=lambda kk: legs[kk]["us_per_batch"])
+        out[f"S{S}"] = dict(legs[best], best=best, **{"all": legs})
+    out["note"] = ("one launch serves S consecutive batch-%d requests (ids/dense of batch s read from device memory "
+                   "inside the kernel); us_per_batch = HIP-event slot of the graph-replayed launch / S; frac = the "
+                   "headline's algorithmic bytes per batch / us_per_batch / 8 TB/s" % B)
+    return out
+
+
 def bench_hotpath(args, world, rank):
     import recommender_system_amd as rs
     from recommender_system_amd import _lib
@@ -433,6 +475,10 @@ def bench_hotpath(args, world, rank):
             t = _timed_graph_streams(step_s, n, ns, world)
             conc[f"{ns}_streams"] = {"samples_per_s": n * B / t, "us_per_batch": t / n * 1e6}
         result["concurrent_batches"] = conc
+        # S consecutive batch requests served by ONE launch
+        # (rs_embed_fm_fwd_hm_stream): the multi-batch floor of the same hot
+        # path, nested (the value above stays one launch per batch)
+        result["streamed"] = _streamed_leg(args, world, model, ids_pool, dense_pool, step, logit, alg_bytes)
         # secondary: Zipf(a=1.05) ids per field — repeated hot rows
         # hit L2 / the Infinity Cache, so this is cache-assisted, not the HBM line
         zrng = np.random.default_rng(SEED + 7)
@@ -507,6 +553,11 @@ def bench_hotpath(args, world, rank):
                            "RCCL self-exchange forced - not what a world-1 job runs (it calls the unsharded "
                            "kernel, the value above)")
             result["fm_hotpath_sharded_n1"] = sfm
+        # BASELINE configs 3 (DCN CrossNet) and 4 (DIN attention) under the
+        # same clock: each its own line, nested (roofline + cpu_baseline)
+        if not args.no_configs34:
+            result["config3_n1"] = bench_dcn(args, 1, 0, nested=True)
+            result["config4_n1"] = bench_din(args, 1, 0, nested=True)
     else:
         # N > 1 (and --sharded at N = 1): the metric's own workload, the
         # 26 x 1e7 table row-sharded over the ranks, B local samples per rank
@@ -1241,11 +1292,24 @@ def _line(metric, value, unit, args, world, ms_per_step, config, roofline, extra
     return out
 
 
-def bench_dcn(args, world, rank):
+def _nested_args(args):
+    """A config line nested in the N = 1 headline line (config3_n1 /
+    config4_n1): at least NESTED_MIN_STEPS steps, a shorter CPU sample."""
+    a = copy.copy(args)
+    a.steps = max(args.steps, NESTED_MIN_STEPS)
+    a.cpu_budget = min(args.cpu_budget, 5.0)
+    return a
+
+
+def bench_dcn(args, world, rank, nested=False):
     """Config 3: DCN CrossNet depth 3 on the DeepFM feature shape (26 x 1e6 x 16,
     13 dense, d = 429), B = 4096: step = rs_embed_cross_fwd (gather assembled in LDS + CrossNet, one
-    launch); the two-launch path (rs_embed_gather + rs_cross_fwd) is reported beside it."""
+    launch); the two-launch path (rs_embed_gather + rs_cross_fwd) is reported beside it.
+    nested: the config3_n1 leg of the N = 1 headline line (B 4096 whatever --batch)."""
     import recommender_system_amd as rs
+    if nested:
+        args = _nested_args(args)
+        args.batch = 4096
     B, F, V, k, nd = args.batch, 26, int(args.vocab if args.vocab != 1e7 else 1e6), 16, 13
     dev = torch.device("cuda")
     cols = [[{"feat": f"I{i + 1}"} for i in range(nd)],
@@ -1322,11 +1386,15 @@ def bench_dcn(args, world, rank):
                   "cpu_baseline": cpu})
 
 
-def bench_din(args, world, rank):
+def bench_din(args, world, rank, nested=False):
     """Config 4: DIN, Amazon-Electronics-shaped: B = 2048, T = 100, behaviour
     vocab 63,001, k = 8, 1 dense + user_id (192,404); step = behaviour-seq +
-    candidate gathers + the attention-unit kernel."""
+    candidate gathers + the attention-unit kernel.  nested: the config4_n1
+    leg of the N = 1 headline line (no training step)."""
     import recommender_system_amd as rs
+    if nested:
+        args = _nested_args(args)
+        args.batch = 4096
     B, T, k = 2048 if args.batch == 4096 else args.batch, 100, 8
     dev = torch.device("cuda")
     cols = [[{"feat": "age"}],
@@ -1376,7 +1444,23 @@ def bench_din(args, world, rank):
     dt_old, _ = _timed_graph(two_launch_materialised, args.steps, 5, world)
     flop = B * T * 2 * (4 * k * 80 + 80 * 40 + 40)  # reference formulation
     ach = flop / (att_ms * 1e-3)
-    issued = B * ((T + 15) // 16) * 16 * 2 * (5 * 16 * 4 * (k // 4) * 2 + 3 * 16 * 80)
+    # issued MFMA flops: din_fused runs the MLP only on LIVE 16-position tiles
+    # (>= 1 unmasked position; din.hip) - per position of a live tile the
+    # regrouped layers issue 2 * (5*16*4*(k/4)*2 + 3*16*80) flops; with
+    # U[1, T] lengths about half the positions are padding
+    per_pos = 2 * (5 * 16 * 4 * (k // 4) * 2 + 3 * 16 * 80)
+    live_pos = float(np.mean([float(((((m.sum(1) + 15) // 16) * 16).clamp(min=16)).sum()) for m in masks]))
+    issued = live_pos * per_pos
+    issued_all = B * ((T + 15) // 16) * 16 * per_pos
+    # the same step on full-length histories (no padding: every tile live)
+    full_pool = [dict(p, movies_seq=torch.randint(1, 63001, (B, T), generator=g, device=dev)) for p in pool[:2]]
+
+    def step_full(i):
+        p = full_pool[i % 2]
+        att.forward_ids(table, V, p["movies_seq"], p["movie_id"], err=err, out=out, scores=ws)
+
+    dtf_, _ = _timed_graph(step_full, args.steps, 5, world)
+    full_ms = dtf_ / args.steps * 1e3
     n2 = max(NESTED_MIN_STEPS, args.steps // 5)
 
     def full(i):
@@ -1412,7 +1496,7 @@ def bench_din(args, world, rank):
         model.train_step(pool[i % 8], labels[i % 8], lr=0.01, check_ids=False)
 
     nt = max(10, args.steps // 10)
-    tdt, ttiming = _train_timed(train, nt, world)
+    tdt, ttiming = _train_timed(train, nt, world) if not nested else (None, None)
     return _line("DIN forward samples/sec @ batch 2048, behaviour seq len 100 (attention unit)",
                  args.steps * B / dt, "samples/s", args, world, att_ms,
                  {"workload": "din_attention_unit_from_ids", "global_batch": B, "seq_len": T, "embed_dim": k,
@@ -1421,9 +1505,22 @@ def bench_din(args, world, rank):
                   "frac": ach / PEAK_F32, "traffic": _pmc_cfg("din"), "kernel": "din_fused", "kernel_ms": att_ms,
                   "kernel_ms_source": "graph-replayed step (one launch: scores, masked softmax, pool) / steps",
                   "useful_flop_per_launch": flop,
-                  "useful_flop_note": "reference formulation T*2*(4k*80+80*40+40); the kernel regroups layer 1 "
-                                      "per sample (q(Wq+Wd) + key(Wk-Wd+diag(q)Wp)) and issues fewer",
-                  "issued_mfma_flop_per_launch": issued},
+                  "useful_flop_note": "reference formulation B*T*2*(4k*80+80*40+40) over ALL T positions "
+                                      "(SURVEY 8(d)); the kernel regroups layer 1 per sample (q(Wq+Wd) + "
+                                      "key(Wk-Wd+diag(q)Wp)) and skips fully masked 16-position tiles, so it "
+                                      "issues fewer",
+                  "issued_mfma_flop_per_launch": issued,
+                  "issued_note": "live tiles only: sum over samples of ceil(len/16)*16 positions (mean over the "
+                                 "8-batch pool: %.0f of B*T = %d) x %d flops per position; check: PMC "
+                                 "SQ_VALU_MFMA_BUSY_CYCLES x 64 (profiles/r6_pmc_din.json)" % (live_pos, B * T,
+                                                                                               per_pos),
+                  "issued_mfma_flop_if_every_tile_ran": issued_all,
+                  "issued_mfma_tflops": issued / (att_ms * 1e-3) / 1e12,
+                  "issued_frac_of_mfma_peak": issued / (att_ms * 1e-3) / PEAK_F32,
+                  "no_padding": {"kernel_ms": full_ms, "frac": flop / (full_ms * 1e-3) / PEAK_F32,
+                                 "issued_frac": issued_all / (full_ms * 1e-3) / PEAK_F32,
+                                 "note": "every history full length (T valid positions, every tile live): the "
+                                         "reference formulation's frac without padding"}},
                  {"materialised_keys_path": {"samples_per_s": args.steps * B / dt_old,
                                              "ms_per_step": dt_old / args.steps * 1e3},
                   "din_forward": {"samples_per_s": n2 * B / dt2, "ms_per_step": dt2 / n2 * 1e3,
@@ -1435,7 +1532,7 @@ def bench_din(args, world, rank):
                                  "timing": ttiming,
                                  "note": "DIN.train_step: gathers, attention Dense+PReLU layers over [B*T] rows, "
                                          "masked softmax pool, training-mode BN, PReLU DNN, full backward, SGD + "
-                                         "row-sparse embedding SGD"},
+                                         "row-sparse embedding SGD"} if not nested else None,
                   "cpu_baseline": cpu})
 
 
@@ -1907,6 +2004,8 @@ def main():
                     help="also time config 5's pipelined stream (slower than the per-batch forward on one GPU)")
     ap.add_argument("--no-config5", dest="no_config5", action="store_true",
                     help="skip the nested config-5 line (config5_n1 at N = 1, config5 at N > 1)")
+    ap.add_argument("--no-configs34", dest="no_configs34", action="store_true",
+                    help="skip the nested config-3 / config-4 lines of the N = 1 line")
     ap.add_argument("--sharded", action="store_true",
                     help="time the N > 1 line's row-sharded protocol even at world 1 (RCCL self-exchange)")
     args = ap.parse_args()
@@ -1963,6 +2062,7 @@ def main():
                               "beside the pipe of t) whose logits are bit-identical to the one-deep RCCL step's, "
                               "all nested; config 5 (the DeepFM forward on the 1e8-row table) is nested as config5"})
         for key in ("concurrent_batches", "zipf_ids", "deepfm_forward", "config5_n1", "fm_hotpath_sharded_n1",
+                    "config3_n1", "config4_n1", "streamed",
                     "config5", "protocol", "timing", "slot_ms", "unpipelined", "rows_protocol", "train_step",
                     "owner_field_ranges", "bytes_per_rank_each_way", "world1_no_exchange", "exchange",
                     "peer_exchange", "rccl_pipelined", "rccl_two_deep", "exchange_candidates_ms_per_step"):

@@ -1169,6 +1169,30 @@ int rs_shard_fm_pipe_peer(const int32_t* recv, int32_t* send,
                           int rank, void* peer_state, int chunks,
                           int64_t spin_limit, int* xerr, rs_stream_t stream);
 
+/* S consecutive batch requests in ONE launch (the headline hot path served
+ * back to back: EmbedLayer + concat + FMLayer, layer/core.py:273-280,
+ * layer/interaction.py:106-114, per batch as rs_embed_fm_fwd_hm computes it):
+ * batch s (s < n_batches) has `batch` samples (the last one last_batch), its
+ * ids at ids + s * ids_batch_stride elements (rows id_stride apart), dense at
+ * dense + s * dense_batch_stride floats, logits written at logit + s *
+ * logit_batch_stride.  Every batch's logits are bit-identical to
+ * rs_embed_fm_fwd_hm on that batch alone (same kernel body and tiles).
+ * Shapes of the kernarg-metadata kernel only: k in {4, 8, 16}, kfm <= 15,
+ * 1..32 fields (host metadata), nd <= 64, int32 / int64 ids, batch <= 8192;
+ * min_blocks = 1 or 2 resident workgroups per CU (RS_ERR_ARG otherwise).    */
+int rs_embed_fm_fwd_hm_stream(const void* ids, int id_kind, int64_t id_stride,
+                              int64_t ids_batch_stride, const float* dense,
+                              int64_t dense_stride, int64_t dense_batch_stride,
+                              int nd, const float* table,
+                              const int64_t* field_offsets_host,
+                              const int64_t* field_vocab_host, int n_fields,
+                              int k, const float* prepared, const float* w0,
+                              int kfm, float* logit,
+                              int64_t logit_batch_stride, int64_t batch,
+                              int n_batches, int64_t last_batch,
+                              int min_blocks, int* err_flag,
+                              rs_stream_t stream);
+
 /* FM over pre-gathered rows (sharded path): emb is [B, F*k] in x order.     */
 int rs_rows_fm_fwd(const float* emb, const float* dense, int64_t dense_stride,
                    int nd, int n_fields, int k, const float* prepared,

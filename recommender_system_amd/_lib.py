@@ -46,6 +46,7 @@ SIGNATURES = {
     "rs_fm_prepare": (I, [P, P, I, I, I, I, P, P]),
     "rs_embed_fm_fwd": (I, [P, I, L, P, L, I, P, P, P, I, I, P, P, I, P, P, L, P, P]),
     "rs_embed_fm_fwd_hm": (I, [P, I, L, P, L, I, P, P, P, P, P, I, I, P, P, I, P, P, L, P, P]),
+    "rs_embed_fm_fwd_hm_stream": (I, [P, I, L, L, P, L, L, I, P, P, P, I, I, P, P, I, P, L, L, I, L, I, P, P]),
     "rs_fm_fwd": (I, [P, L, I, P, P, I, P, L, P]),
     "rs_fm_onehot_fwd": (I, [P, I, L, P, L, I, P, P, I, P, P, P, I, P, L, P, P]),
     "rs_cross_prepared_size": (L, [I, I]),

@@ -582,6 +582,30 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma_ka(EmbedFmArgs a, Field
   embed_fm_body<KV, NT, NW, KIND, false, 1, PF, true>(a, nullptr, blockIdx.x, &m);
 }
 
+// S consecutive batches in ONE launch (rs_embed_fm_fwd_hm_stream): workgroup
+// g runs the kernarg kernel's body on tile g % tpb of batch g / tpb (batch-
+// major dispatch order) — the same instantiation and tile arithmetic as the
+// per-batch launch, so every batch's logits are bit-identical to
+// rs_embed_fm_fwd_hm's; batch s's ids / dense / logit start at the given
+// per-batch strides; the last batch may be shorter (its own tile count).
+// MINB = 2 asks for two resident workgroups per CU (<= 64 VGPRs), so one
+// tile's id trip runs under another's rows and combine.
+struct StreamArgs {
+  int tpb, S;
+  int64_t ids_bstride_bytes, dense_bstride, logit_bstride, last_batch;
+};
+template <int KV, int NT, int KIND, int MINB>
+__global__ __launch_bounds__(16 * 64, MINB) void embed_fm_stream_ka(EmbedFmArgs a, FieldMeta m, StreamArgs sa) {
+  const int s = blockIdx.x / sa.tpb, tile = blockIdx.x - s * sa.tpb;
+  EmbedFmArgs b = a;
+  b.ids = static_cast<const char*>(a.ids) + s * sa.ids_bstride_bytes;
+  b.dense = a.dense + s * sa.dense_bstride;
+  b.logit = a.logit + s * sa.logit_bstride;
+  if (s == sa.S - 1) b.batch = sa.last_batch;
+  if ((int64_t)tile * 16 >= b.batch) return;  // a shorter last batch: fewer tiles (uniform exit)
+  embed_fm_body<KV, NT, 16, KIND, false, 1, true, true>(b, nullptr, tile, &m);
+}
+
 // ---- sharded FM, partial protocol: combine (requester side) as a block part
 struct CombineArgs {
   const float* part;  // partial records [world][batch], pst floats apart
@@ -1610,6 +1634,79 @@ extern "C" int rs_embed_fm_fwd_hm(const void* ids, int id_kind, int64_t id_strid
   a.batch = batch;
   a.err = err_flag;
   return run_embed_fm(a, g, id_kind, as_stream(stream), "rs_embed_fm_fwd_hm", &m);
+}
+
+// S consecutive batch requests of `batch` samples each (the last one
+// `last_batch`), batch s's ids at ids + s * ids_batch_stride elements, dense
+// at dense + s * dense_batch_stride, logits at logit + s * logit_batch_stride:
+// one launch, each batch's logits bit-identical to rs_embed_fm_fwd_hm's on
+// that batch alone.  The kernarg-metadata kernel's shapes only (k 16 / 8 / 4,
+// kfm <= 15, <= 32 fields, <= 16 dense k-steps, int32 / int64 ids, batch <=
+// 8192, no x output); min_blocks: 1 or 2 resident workgroups per CU.
+extern "C" int rs_embed_fm_fwd_hm_stream(const void* ids, int id_kind, int64_t id_stride, int64_t ids_batch_stride,
+                                         const float* dense, int64_t dense_stride, int64_t dense_batch_stride,
+                                         int nd, const float* table, const int64_t* field_offsets_host,
+                                         const int64_t* field_vocab_host, int n_fields, int k,
+                                         const float* prepared, const float* w0, int kfm, float* logit,
+                                         int64_t logit_batch_stride, int64_t batch, int n_batches,
+                                         int64_t last_batch, int min_blocks, int* err_flag, rs_stream_t stream) {
+  if (n_batches == 0 || batch == 0) return RS_OK;
+  RS_REQUIRE(n_batches > 0 && batch > 0 && last_batch > 0 && last_batch <= batch && batch <= 8192 && nd >= 0 &&
+                 nd <= 64 && n_fields >= 1 && n_fields <= 32 && kfm >= 1 && kfm <= 15 &&
+                 (k == 4 || k == 8 || k == 16) && (min_blocks == 1 || min_blocks == 2),
+             "rs_embed_fm_fwd_hm_stream: unsupported shape");
+  RS_REQUIRE(id_kind == RS_ID_I32 || id_kind == RS_ID_I64, "rs_embed_fm_fwd_hm_stream: int32 / int64 ids only");
+  RS_REQUIRE(ids && table && prepared && w0 && logit && (nd == 0 || dense) && field_offsets_host &&
+                 field_vocab_host,
+             "rs_embed_fm_fwd_hm_stream: null pointer");
+  RS_REQUIRE((uintptr_t)table % 16 == 0, "rs_embed_fm_fwd_hm_stream: table must be 16-B aligned");
+  RS_REQUIRE(ids_batch_stride >= batch * id_stride && dense_batch_stride >= (nd ? batch * dense_stride : 0) &&
+                 logit_batch_stride >= batch,
+             "rs_embed_fm_fwd_hm_stream: batches overlap");
+  const int64_t tpb = (batch + 15) / 16;
+  RS_REQUIRE(tpb * n_batches < (1ll << 31), "rs_embed_fm_fwd_hm_stream: too many tiles");
+  FieldMeta m{};
+  for (int c = 0; c < n_fields; ++c) {
+    m.off[c] = field_offsets_host[c];
+    m.voc[c] = field_vocab_host[c];
+  }
+  const FmGeom g = fm_geom(nd, n_fields, k, kfm);
+  EmbedFmArgs a{};
+  a.ids = ids;
+  a.id_stride = id_stride;
+  a.dense = dense;
+  a.dense_stride = dense_stride;
+  a.nd = nd;
+  a.table = table;
+  a.F = n_fields;
+  a.k = k;
+  a.prep = prepared;
+  a.w0 = w0;
+  a.kfm = kfm;
+  a.logit = logit;
+  a.batch = batch;
+  a.err = err_flag;
+  a.DB = g.DB;
+  a.dense_rec = g.dense_rec;
+  a.field_rec = g.field_rec;
+  a.field_base = g.field_base;
+  StreamArgs sa{(int)tpb, n_batches, ids_batch_stride * (id_kind == RS_ID_I64 ? 8 : 4), dense_batch_stride,
+                logit_batch_stride, last_batch};
+  const unsigned grid = (unsigned)(tpb * n_batches);
+  hipStream_t st = as_stream(stream);
+  auto go = [&](auto kv, auto kind) {
+    constexpr int KV = decltype(kv)::value, KIND = decltype(kind)::value;
+    if (min_blocks == 2) embed_fm_stream_ka<KV, 1, KIND, 2><<<grid, 16 * 64, 0, st>>>(a, m, sa);
+    else embed_fm_stream_ka<KV, 1, KIND, 1><<<grid, 16 * 64, 0, st>>>(a, m, sa);
+  };
+  auto by_kind = [&](auto kv) {
+    if (id_kind == RS_ID_I64) go(kv, std::integral_constant<int, 1>());
+    else go(kv, std::integral_constant<int, 0>());
+  };
+  if (k == 16) by_kind(std::integral_constant<int, 4>());
+  else if (k == 8) by_kind(std::integral_constant<int, 2>());
+  else by_kind(std::integral_constant<int, 1>());
+  return launch_status("rs_embed_fm_fwd_hm_stream");
 }
 
 #ifdef RS_DIAG_STAMPS

@@ -310,6 +310,30 @@ class DeepFM(KerasModule):
             self._err.check("DeepFM")
         return logit
 
+    def fm_logit_stream(self, dense, ids, last_batch=None, min_blocks=1, out=None, check_ids=True):
+        """The hot path over S consecutive batch requests in ONE launch
+        (rs_embed_fm_fwd_hm_stream): dense [S, B, nd] f32, ids [S, B, F]
+        int32 / int64 (contiguous per batch); the last batch may hold only
+        ``last_batch`` samples.  Returns logits [S, B, 1] (rows past
+        last_batch of the last batch untouched), each batch bit-identical to
+        ``fm_logit`` on it alone."""
+        S, B, F = ids.shape
+        e = self.embed_layer
+        if F != e.n_fields or dense.shape[:2] != (S, B) or dense.shape[2] != self.nd:
+            raise ValueError("fm_logit_stream: dense [S, B, nd] and ids [S, B, F] expected")
+        if ids.stride(2) != 1 or dense.stride(2) != 1:
+            raise ValueError("fm_logit_stream: the last axis must be contiguous")
+        prep = self.fm.prepared(self.nd, e.n_fields, e.k)
+        logit = out if out is not None else torch.empty(S, B, 1, dtype=torch.float32, device=self._dev)
+        hoff, hvoc = e.host_meta()
+        call("rs_embed_fm_fwd_hm_stream", ptr(ids), _lib.id_kind(ids), ids.stride(1), ids.stride(0), ptr(dense),
+             dense.stride(1), dense.stride(0), self.nd, ptr(e.table), hoff, hvoc, e.n_fields, e.k, ptr(prep),
+             ptr(self.fm.w0), self.fm.k, ptr(logit), logit.stride(0), B, S, B if last_batch is None else last_batch,
+             min_blocks, ptr(self._err.t), _lib.stream())
+        if check_ids:
+            self._err.check("DeepFM")
+        return logit
+
     def train_step(self, inputs, labels, lr=0.01, return_loss=False, check_ids=True, dropout=None):
         """One step of compile_fit (utils/compile_fit.py:9-15: SGD(lr),
         binary cross-entropy on sigmoid(0.5 (FM + DNN)), FMLayer's l2

@@ -1107,3 +1107,41 @@ def test_tower_input_affine_equals_bn_then_tower(gpu, act):
     got = dnn.tower(x, in_affine=(inv, shift))
     torch.cuda.synchronize()
     assert torch.equal(got, ref), float((got - ref).abs().max())
+
+
+@pytest.mark.parametrize("S,B,last,id_dtype,min_blocks", [
+    (1, 4096, 4096, torch.int32, 1),
+    (2, 4096, 4093, torch.int32, 2),    # ragged last batch (a partial last tile)
+    (8, 4096, 1000, torch.int32, 1),
+    (8, 2048, 2048, torch.int64, 2),
+    (3, 37, 5, torch.int32, 1),          # batches smaller than a tile
+])
+def test_embed_fm_stream_bit_identical(gpu, S, B, last, id_dtype, min_blocks):
+    """rs_embed_fm_fwd_hm_stream (S consecutive batch requests, one launch):
+    every batch's logits == rs_embed_fm_fwd_hm on that batch alone, bit for
+    bit, and == the fp64 oracle; rows past the last batch's length untouched;
+    an out-of-range id in the last batch sets the flag (IndexError)."""
+    from recommender_system_amd import DeepFM
+    from tests.helpers import criteo_columns, tables_of
+    rng = np.random.default_rng(S * 1000 + B + last)
+    vocabs = rng.integers(2, 50000, size=26).tolist()
+    m = DeepFM(criteo_columns(vocabs, embed_dim=16), 10, 1e-4, 1e-4, [64, 32], 1, "relu", embed_dim=16, seed=6)
+    ids = torch.as_tensor(np.stack([random_ids(rng, B, vocabs) for _ in range(S)]), device=gpu).to(id_dtype)
+    dense = torch.as_tensor(rng.random((S, B, 13)).astype(np.float32), device=gpu)
+    out = torch.full((S, B, 1), 77.0, device=gpu)
+    got = m.fm_logit_stream(dense, ids, last_batch=last, min_blocks=min_blocks, out=out)
+    tables = tables_of(m.embed_layer)
+    c = lambda t: t.detach().cpu().numpy()
+    for s in range(S):
+        n = B if s < S - 1 else last
+        ref = m.fm_logit((dense[s, :n], ids[s, :n]))
+        assert torch.equal(got[s, :n], ref), f"batch {s}"
+        x64 = np.concatenate([c(dense[s, :n]).astype(np.float64),
+                              O.embed_layer(c(ids[s, :n]), tables, np.float64)], 1)
+        assert_scaled_close(got[s, :n, 0], O.fm_layer(x64, c(m.fm.w0), c(m.fm.w1), c(m.fm.v))[:, 0],
+                            what=f"stream batch {s}")
+    assert bool((got[S - 1, last:] == 77.0).all())
+    bad = ids.clone()
+    bad[S - 1, last - 1, 25] = vocabs[25]
+    with pytest.raises(IndexError):
+        m.fm_logit_stream(dense, bad, last_batch=last, min_blocks=min_blocks)
