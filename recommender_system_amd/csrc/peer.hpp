@@ -41,7 +41,11 @@ struct PeerArgs {
   // times per workgroup; 1 (lean): the data stores themselves write through
   // (sc0 sc1: nothing of the step can sit dirty in any L2), so s_waitcnt
   // vmcnt(0) orders them before relaxed counts and write-through flags, and
-  // no cache maintenance runs beside the launch's other work
+  // no cache maintenance runs beside the launch's other work.  At world 1
+  // (lean) the mailbox is ordinary device memory (sharded.PeerExchange: no
+  // peer, nothing crosses a device) and the data stores are plain: only the
+  // next kernels on this stream read them (kernel-boundary coherence); the
+  // flags stay write-through
   int lean;
 };
 
@@ -97,7 +101,7 @@ __device__ __forceinline__ void peer_a2a_part(const PeerArgs& a, int c, int p) {
         floatx4 x = {0.f, 0.f, 0.f, 0.f};
         if (r >= 0 && r < a.n_rows) x = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(a.table + r * 16) + (i & 3));
         else bad |= r != -1;
-        if (a.lean) {  // write-through (see PeerArgs::lean)
+        if (a.lean && a.world > 1) {  // write-through (see PeerArgs::lean; world 1: ordinary memory, plain stores)
           unsigned long long* d8 = reinterpret_cast<unsigned long long*>(dst + i);
           __hip_atomic_store(d8, __builtin_bit_cast(unsigned long long, floatx2{x[0], x[1]}), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_SYSTEM);
@@ -110,7 +114,7 @@ __device__ __forceinline__ void peer_a2a_part(const PeerArgs& a, int c, int p) {
       if (__any(bad) && (threadIdx.x & 63) == 0) flag_error(a.err);
     } else {
       const floatx4* src = reinterpret_cast<const floatx4*>(a.send + (int64_t)p * a.block_bytes);
-      if (a.lean) {
+      if (a.lean && a.world > 1) {
         // write-through stores (system scope, relaxed: sc0 sc1), 8 B each
         unsigned long long* d8 = reinterpret_cast<unsigned long long*>(dst);
         const unsigned long long* s8 = reinterpret_cast<const unsigned long long*>(src);

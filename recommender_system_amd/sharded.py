@@ -89,7 +89,8 @@ class PeerExchange:
     Requires every rank's process to see every peer's device (one node) and
     the HIP dmabuf IPC path (HSA_ENABLE_IPC_MODE_LEGACY=0).  Tested with two
     processes on one device (tests/test_peer_exchange.py); RCCL stays the
-    default exchange."""
+    default exchange.  At world 1 with the lean ordering the mailbox is
+    ordinary device memory (no peer maps it)."""
 
     def __init__(self, block_bytes, group=None, world=None, rank=None, device=None, chunks=None,
                  spin_limit=1 << 24):
@@ -107,14 +108,22 @@ class PeerExchange:
         # Setup is collective and fails collectively: a rank whose allocation,
         # export or mapping fails still takes part in every collective below,
         # and then every rank raises (no rank is left waiting in a collective).
-        self._mine, self._opened = None, []
+        self._mine, self._opened, self._local = None, [], None
         h = (C.c_uint8 * 64)()
         err = ""
+        # world 1 (the bench's forced self-exchange): no peer maps the mailbox
+        # and nothing crosses a device, so it is ordinary (cached) device
+        # memory written with plain stores under the lean ordering
+        # (RS_OPT_PEER_FENCES 0; peer.hpp) instead of uncached memory
+        local = self.world == 1 and _lib.lib().rs_get_option(_lib.OPT_PEER_FENCES) == 0
         try:
-            mine = C.c_void_p()
-            call("rs_peer_alloc", self.mbox_bytes, C.addressof(mine))
-            self._mine = mine.value
-            call("rs_peer_ipc_handle", self._mine, C.addressof(h))
+            if local:
+                self._local = torch.zeros(self.mbox_bytes, dtype=torch.uint8, device=self.device)
+            else:
+                mine = C.c_void_p()
+                call("rs_peer_alloc", self.mbox_bytes, C.addressof(mine))
+                self._mine = mine.value
+                call("rs_peer_ipc_handle", self._mine, C.addressof(h))
         except Exception as e:  # noqa: BLE001 — reported collectively below
             err = f"rank {self.rank}: {e}"
         # every rank's [ok | handle (64 B)] — over the group's backend (gloo: CPU tensors)
@@ -128,7 +137,7 @@ class PeerExchange:
             try:
                 for r in range(self.world):
                     if r == self.rank:
-                        ptrs.append(self._mine)
+                        ptrs.append(self._mine if self._local is None else self._local.data_ptr())
                         continue
                     hr = (C.c_uint8 * 64)(*allh[r][1:].tolist())
                     pr = C.c_void_p()
@@ -153,7 +162,8 @@ class PeerExchange:
         self.mailboxes = torch.tensor(ptrs, dtype=torch.int64, device=self.device)
         self.state = torch.zeros(int(lib.rs_peer_state_bytes()), dtype=torch.uint8, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self.recv = torch.as_tensor(_DevBuf(self._mine, self.world * self.block_bytes), device=self.device)
+        self.recv = (self._local[:self.world * self.block_bytes] if self._local is not None else
+                     torch.as_tensor(_DevBuf(self._mine, self.world * self.block_bytes), device=self.device))
         if chunks is None:  # ~256 workgroups in all, at least 1 per destination
             chunks = max(1, min(1024 // self.world, 256 // self.world, -(-self.block_bytes // 16384)))
         self.chunks = int(chunks)
@@ -199,6 +209,7 @@ class PeerExchange:
         if self._mine:
             _lib.lib().rs_peer_free(self._mine)
             self._mine = None
+        self._local = None
 
 
 class HipShardOps:

@@ -223,3 +223,49 @@ def test_peer_sharded_deepfm_two_processes_one_device(gpu):
     the same forward over the gloo all-to-alls, bit for bit; a bad id raises."""
     for rank, ok, msg in _run(_deepfm_worker):
         assert ok, f"rank {rank}: {msg}"
+
+
+def test_peer_world1_local_mailbox(gpu):
+    """World 1 with the exchange forced (the bench's N = 1 anchors): the
+    mailbox is ordinary device memory written with plain stores (lean
+    ordering), for the one-deep and two-deep FM steps and config 5's fused
+    gather — logits bit-identical to the same world-1 models without an
+    exchange; with RS_OPT_PEER_FENCES 1 the uncached mailbox gives the same."""
+    from recommender_system_amd import _lib
+    from recommender_system_amd.sharded import ShardedDeepFM, ShardedEmbeddingFM
+    port = _free_port()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        vocabs = [5000, 17, 3000, 1, 700, 2500, 40, 900, 1200, 8, 300, 77, 4000, 12, 9, 600, 31, 2, 150, 2222,
+                  45, 8000, 3, 1000, 64, 500]
+        g = torch.Generator(device="cpu")
+        g.manual_seed(11)
+        B = 128
+        batches = [(torch.rand(B, 13, generator=g).cuda(),
+                    torch.stack([torch.randint(0, v, (B,), generator=g) for v in vocabs], 1).int().cuda())
+                   for _ in range(4)]
+        for fences in (0, 1):
+            _lib.set_option(_lib.OPT_PEER_FENCES, fences)
+            sh = ShardedEmbeddingFM(vocabs, 16, 13, 10, device="cuda", seed=3)
+            ref = torch.cat(sh.forward_stream(batches))  # world 1, no exchange
+            sh._force_exchange = True
+            sh.use_peer_exchange()
+            one = torch.cat(sh.forward_stream(batches))
+            two = torch.cat(sh.forward_stream2(batches))
+            local = sh._peers["pipe"]._local is not None
+            sh.close_peer_exchange()
+            assert local == (fences == 0)
+            assert torch.equal(one, ref) and torch.equal(two, ref), f"fences={fences}"
+            cols = [[{"feat": f"I{i}"} for i in range(13)],
+                    [{"feat": f"C{i}", "feat_onehot_dim": v, "embed_dim": 16} for i, v in enumerate(vocabs)]]
+            m = ShardedDeepFM(cols, 10, 1e-4, 1e-4, [256, 128, 64], 1, "relu", embed_dim=16, device="cuda", seed=4)
+            dref = torch.cat([m.forward(b) for b in batches])
+            m.emb._force_exchange = True
+            m.use_peer_exchange()
+            dgot = torch.cat([m.forward(b) for b in batches])
+            m.close_peer_exchange()
+            assert torch.equal(dgot, dref), f"config 5 fences={fences}"
+    finally:
+        _lib.set_option(_lib.OPT_PEER_FENCES, 0)
+        dist.destroy_process_group()
