@@ -1524,10 +1524,11 @@ def bench_din(args, world, rank, nested=False):
                  {"materialised_keys_path": {"samples_per_s": args.steps * B / dt_old,
                                              "ms_per_step": dt_old / args.steps * 1e3},
                   "din_forward": {"samples_per_s": n2 * B / dt2, "ms_per_step": dt2 / n2 * 1e3,
-                                  "note": "graph-replayed full DIN.call (id checks off), three launches: the "
-                                          "other sparse rows + dense (rs_concat_pieces), the attention from ids "
-                                          "with the candidate rows (rs_din_attention_ids_cand_fwd), BN + PReLU "
-                                          "MLP + sigmoid head (rs_mlp_affine_fwd)"},
+                                  "note": "graph-replayed full DIN.call (id checks off), two launches: the "
+                                          "attention from ids with the candidate rows "
+                                          "(rs_din_attention_ids_cand_fwd), then BN + PReLU MLP + sigmoid head "
+                                          "reading the other sparse rows and the dense features straight into "
+                                          "its input tile (rs_mlp_affine_pieces_fwd)"},
                   "train_step": {"samples_per_s": nt * B / tdt, "ms_per_step": tdt / nt * 1e3,
                                  "timing": ttiming,
                                  "note": "DIN.train_step: gathers, attention Dense+PReLU layers over [B*T] rows, "

@@ -499,6 +499,25 @@ int rs_mlp_affine_fwd(const float* x, int64_t x_stride, const float* in_scale,
                       const int* acts, const float* prepared, float* y,
                       int64_t y_stride, int head, const float* extra, float c0,
                       float c1, int64_t batch, rs_stream_t stream);
+/* ... and some input columns read straight from their sources instead of x:
+ * the concat pieces of rs_concat_pieces (widths / kinds / srcs / strides /
+ * tables / vocabs as there; in_cols = the input column of each piece's first
+ * column), e.g. DIN.call's other sparse embeddings and dense features
+ * (model/din.py:64-69,84-85) beside the pooled attention — the concat is
+ * never written and needs no launch of its own.  x (rows x_stride apart)
+ * provides every other column (NULL if the pieces cover them all).  At most
+ * 64 input columns; an out-of-range id reads a zero row and sets err_flag. */
+int rs_mlp_affine_pieces_fwd(const float* x, int64_t x_stride,
+                             const float* in_scale, const float* in_shift,
+                             int n_layers, const int* dims, const int* acts,
+                             const float* prepared, float* y, int64_t y_stride,
+                             int head, const float* extra, float c0, float c1,
+                             int64_t batch, int n_pieces, const int* widths,
+                             const int* in_cols, const int* kinds,
+                             const void* const* srcs,
+                             const int64_t* src_strides,
+                             const float* const* tables, const int64_t* vocabs,
+                             int* err_flag, rs_stream_t stream);
 
 /* --------------------------------------------- fused DeepFM forward (a8)
  * DeepFM.call (model/deepFM.py:23-31) in ONE launch: ids -> rows -> x (kept

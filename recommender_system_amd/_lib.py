@@ -79,6 +79,7 @@ SIGNATURES = {
     "rs_mlp_prepare": (I, [I, P, P, P, P, P, P, P]),
     "rs_mlp_fwd": (I, [P, L, I, P, P, P, P, L, I, P, F, F, L, P]),
     "rs_mlp_affine_fwd": (I, [P, L, P, P, I, P, P, P, P, L, I, P, F, F, L, P]),
+    "rs_mlp_affine_pieces_fwd": (I, [P, L, P, P, I, P, P, P, P, L, I, P, F, F, L, I, P, P, P, P, P, P, P, P, P]),
     "rs_concat_pieces": (I, [I, P, P, P, P, P, P, P, P, L, L, P, P]),
     "rs_deepfm_fused_ok": (I, [I, I, I, I, I, P]),
     "rs_deepfm_fwd": (I, [P, I, L, P, L, I, P, P, P, I, I, P, P, I, I, P, P, P, F, F, P, P, L, P, P]),

@@ -21,6 +21,7 @@
 //     workgroup and stay L2-resident; per 4 MFMAs a wave reads 1 KB of
 //     weights from L2 and 1 KB of activations from LDS, both under the
 //     per-CU rates at MFMA peak.
+#include "concat.hpp"
 #include "mlp_tower.hpp"
 
 namespace rs {
@@ -62,8 +63,12 @@ __global__ void mlp_prepare_kernel(MlpPrepArgs a) {
   a.out[i] = v;
 }
 
-template <int NW, bool TAIL = false>
-__global__ __launch_bounds__(NW * 64) void mlp_tower(MlpArgs a) {
+// PC: some input columns are concat pieces (rs_mlp_affine_pieces_fwd: DIN's
+// other sparse embeddings + dense features, model/din.py:64-69,84-85) read
+// straight into the input tile — id, then table row — instead of from x;
+// at most 64 input columns (one per lane)
+template <int NW, bool TAIL, bool PC>
+__device__ __forceinline__ void mlp_tower_body(const MlpArgs& a, const ConcatArgs* pc) {
   extern __shared__ float smem[];
   const int RS = a.rs;
   const int lane = threadIdx.x & 63;
@@ -79,12 +84,23 @@ __global__ __launch_bounds__(NW * 64) void mlp_tower(MlpArgs a) {
   for (int r = w; r < 16; r += NW) {
     const int64_t m = m0 + r < a.M ? m0 + r : a.M - 1;
     const float* xr = a.x + m * a.xs;
-    constexpr int XU = MLP_MAXD / 64;
+    constexpr int XU = PC ? 1 : MLP_MAXD / 64;
     float xv[XU];
+    if constexpr (PC) {
+      // the lane's column: a piece column (its piece found in the kernarg
+      // table) or a column of x
+      int p = -1;
+      for (int q = 0; q < pc->np; ++q)
+        if (lane >= pc->out_col[q] && lane < pc->out_col[q] + (pc->col0[q + 1] - pc->col0[q])) p = q;
+      bool bad = false;
+      xv[0] = lane >= a.K0 ? 0.f : (p >= 0 ? concat_value(*pc, p, lane - pc->out_col[p], m, bad) : xr[lane]);
+      if (__any(bad && m0 + r < a.M) && lane == 0) flag_error(pc->err);
+    } else {
 #pragma unroll
-    for (int i = 0; i < XU; ++i) {
-      const int c = lane + 64 * i;
-      xv[i] = c < a.K0 ? xr[c] : 0.f;
+      for (int i = 0; i < XU; ++i) {
+        const int c = lane + 64 * i;
+        xv[i] = c < a.K0 ? xr[c] : 0.f;
+      }
     }
     if (a.in_scale) {  // the BatchNormalization affine, as rs_affine_act computes it
 #pragma unroll
@@ -115,6 +131,15 @@ __global__ __launch_bounds__(NW * 64) void mlp_tower(MlpArgs a) {
   } else {
     mlp_tower_tile<NW>(a, smem, m0, ring);
   }
+}
+
+template <int NW, bool TAIL = false>
+__global__ __launch_bounds__(NW * 64) void mlp_tower(MlpArgs a) {
+  mlp_tower_body<NW, TAIL, false>(a, nullptr);
+}
+template <int NW, bool TAIL = false>
+__global__ __launch_bounds__(NW * 64) void mlp_tower_pc(MlpArgs a, ConcatArgs pc) {
+  mlp_tower_body<NW, TAIL, true>(a, &pc);
 }
 
 }  // namespace rs
@@ -160,7 +185,8 @@ extern "C" int rs_mlp_prepare(int n_layers, const int* dims, const float* const*
 
 static int mlp_run(const float* x, int64_t x_stride, const float* in_scale, const float* in_shift, int n_layers,
                    const int* dims, const int* acts, const float* prepared, float* y, int64_t y_stride, int head,
-                   const float* extra, float c0, float c1, int64_t batch, rs_stream_t stream) {
+                   const float* extra, float c0, float c1, int64_t batch, rs_stream_t stream,
+                   const ConcatArgs* pc = nullptr) {
   if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
   MlpGeom g;
   RS_REQUIRE(mlp_geom(n_layers, dims, g), "rs_mlp_fwd: need 1..%d layers with widths 1..%d", MLP_MAXL, MLP_MAXD);
@@ -188,7 +214,20 @@ static int mlp_run(const float* x, int64_t x_stride, const float* in_scale, cons
   const int64_t grid = (batch + 15) / 16;
   RS_REQUIRE(grid < (1ll << 31), "rs_mlp_fwd: batch too large");
   int gwa = 0, gwb = 0;
-  if (MLP_NW == 16 && mlp_tail_ok(a.Np, a.Kp, a.N, a.L, 1, gwa, gwb) && gwa == 8 && gwb == 2) {
+  const bool tail = MLP_NW == 16 && mlp_tail_ok(a.Np, a.Kp, a.N, a.L, 1, gwa, gwb) && gwa == 8 && gwb == 2;
+  if (pc) {
+    if (tail) {
+      static LdsAttr lds_pt;
+      lds_attr(lds_pt, (const void*)mlp_tower_pc<MLP_NW, true>, lds);
+      mlp_tower_pc<MLP_NW, true><<<(unsigned)grid, MLP_NW * 64, lds, as_stream(stream)>>>(a, *pc);
+    } else {
+      static LdsAttr lds_p;
+      lds_attr(lds_p, (const void*)mlp_tower_pc<MLP_NW>, lds);
+      mlp_tower_pc<MLP_NW><<<(unsigned)grid, MLP_NW * 64, lds, as_stream(stream)>>>(a, *pc);
+    }
+    return launch_status("rs_mlp_affine_pieces_fwd");
+  }
+  if (tail) {
     static LdsAttr lds_tail;
     lds_attr(lds_tail, (const void*)mlp_tower<MLP_NW, true>, lds);
     mlp_tower<MLP_NW, true><<<(unsigned)grid, MLP_NW * 64, lds, as_stream(stream)>>>(a);
@@ -214,4 +253,27 @@ extern "C" int rs_mlp_affine_fwd(const float* x, int64_t x_stride, const float* 
   RS_REQUIRE(batch == 0 || (in_scale && in_shift), "rs_mlp_affine_fwd: null in_scale / in_shift");
   return mlp_run(x, x_stride, in_scale, in_shift, n_layers, dims, acts, prepared, y, y_stride, head, extra, c0, c1,
                  batch, stream);
+}
+
+extern "C" int rs_mlp_affine_pieces_fwd(const float* x, int64_t x_stride, const float* in_scale,
+                                        const float* in_shift, int n_layers, const int* dims, const int* acts,
+                                        const float* prepared, float* y, int64_t y_stride, int head, const float* extra,
+                                        float c0, float c1, int64_t batch, int n_pieces, const int* widths,
+                                        const int* in_cols, const int* kinds, const void* const* srcs,
+                                        const int64_t* src_strides, const float* const* tables,
+                                        const int64_t* vocabs, int* err_flag, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;
+  RS_REQUIRE(in_scale && in_shift, "rs_mlp_affine_pieces_fwd: null in_scale / in_shift");
+  RS_REQUIRE(n_layers >= 1 && dims && dims[0] >= 1 && dims[0] <= 64,
+             "rs_mlp_affine_pieces_fwd: at most 64 input columns");
+  RS_REQUIRE(err_flag, "rs_mlp_affine_pieces_fwd: null error flag");
+  ConcatArgs pc{};
+  const int st = concat_fill(n_pieces, widths, in_cols, kinds, srcs, src_strides, tables, vocabs, dims[0],
+                             "rs_mlp_affine_pieces_fwd", pc);
+  if (st != RS_OK) return st;
+  pc.err = err_flag;
+  // x provides every column no piece covers (rows x_stride apart)
+  RS_REQUIRE(x || pc.ncol == dims[0], "rs_mlp_affine_pieces_fwd: x is null");
+  return mlp_run(x ? x : in_scale, x ? x_stride : dims[0], in_scale, in_shift, n_layers, dims, acts, prepared, y,
+                 y_stride, head, extra, c0, c1, batch, stream, &pc);
 }

@@ -856,23 +856,37 @@ class DIN(TowerMixin, KerasModule):
             att_emb = self.att_layer([item_embed, seq_embed, seq_embed, mask])
             emb[:, K:2 * K] = item_embed
             emb[:, :K] = att_emb
-        self._concat_rest(inputs, emb, 2 * K, B, check_ids)
         if self.out_layer.kernel is not None and self.tower_ok():
-            # BatchNormalization + PReLU MLP + Dense(1, sigmoid) in one launch
+            # BatchNormalization + PReLU MLP + Dense(1, sigmoid) in one launch,
+            # the other sparse embeddings and the dense features read
+            # straight into its input tile (no concat launch, no buffer)
             if self.bn_layer.gamma is None:
                 self.bn_layer.build(emb.shape[-1])
+            pieces = self._rest_pieces(inputs, 2 * K, B)
+            if self.pieces_in_tower and 0 < len(pieces) <= 16 and width <= 64:
+                y = self._tower_pieces(emb, pieces, self.bn_layer.affine())
+                if check_ids:
+                    self._err.check("DIN")
+                return y
+            self._concat_rest(inputs, emb, 2 * K, B, check_ids)
             return self.tower(emb, in_affine=self.bn_layer.affine())
+        self._concat_rest(inputs, emb, 2 * K, B, check_ids)
         x = self.bn_layer(emb)
         for layer in self.dense_layer:
             x = layer(x)
         return self.out_layer(x)
 
-    def _concat_rest(self, inputs, emb, col, B, check_ids):
-        """The other sparse embeddings and the dense features into emb[:, col:]
-        (model/din.py:64-69,84-85): ONE rs_concat_pieces launch for up to 16
-        pieces, one launch per piece beyond."""
+    # DIN.call's tower reads the other sparse embeddings and the dense
+    # features itself (rs_mlp_affine_pieces_fwd); False: one rs_concat_pieces
+    # launch writes them into the concat first (both tested)
+    pieces_in_tower = True
+
+    def _rest_pieces(self, inputs, col, B):
+        """(width, column, kind, source, table, vocab) of the other sparse
+        embeddings and the dense features, from column `col` on
+        (model/din.py:64-69,84-85)."""
         dev = self._dev
-        pieces = []  # (width, out col, kind, source tensor, table, vocab)
+        pieces = []
         for f, layer in zip(self.other_sparse, self.embed_sparse_layers):
             ids = _ids_tensor(inputs[f["feat"]], dev).reshape(B, 1)
             pieces.append((layer.k, col, _lib.id_kind(ids), ids, layer.table, int(layer.vocab_sizes[0])))
@@ -881,6 +895,32 @@ class DIN(TowerMixin, KerasModule):
             x = _to_device_f32(inputs[f["feat"]], dev).reshape(B, 1)
             pieces.append((1, col, -1, x, None, 0))
             col += 1
+        return pieces
+
+    def _tower_pieces(self, emb, pieces, affine):
+        """BN + PReLU MLP + head over [emb[:, :2K] | pieces] in one launch."""
+        ls = self._layers()
+        n = len(ls)
+        dims = self._dims()
+        B = emb.shape[0]
+        out = torch.empty(B, dims[-1], dtype=torch.float32, device=self._dev)
+        sc, sh = affine
+        k = len(pieces)
+        arr = lambda ctype, vals: (ctype * k)(*vals)
+        call("rs_mlp_affine_pieces_fwd", ptr(emb), emb.stride(0), ptr(sc), ptr(sh), n, (C.c_int * (n + 1))(*dims),
+             (C.c_int * n)(*[_lib.ACT[l.activation] for l in ls]), ptr(self.prepared()), ptr(out), out.stride(0), 0,
+             None, 1.0, 1.0, B, k, arr(C.c_int, [p[0] for p in pieces]), arr(C.c_int, [p[1] for p in pieces]),
+             arr(C.c_int, [p[2] for p in pieces]), arr(C.c_void_p, [ptr(p[3]) for p in pieces]),
+             arr(C.c_int64, [p[3].stride(0) for p in pieces]),
+             arr(C.c_void_p, [ptr(p[4]) if p[4] is not None else None for p in pieces]),
+             arr(C.c_int64, [p[5] for p in pieces]), ptr(self._err.t), _lib.stream())
+        return out
+
+    def _concat_rest(self, inputs, emb, col, B, check_ids):
+        """The other sparse embeddings and the dense features into emb[:, col:]
+        (model/din.py:64-69,84-85): ONE rs_concat_pieces launch for up to 16
+        pieces, one launch per piece beyond."""
+        pieces = self._rest_pieces(inputs, col, B)
         for i in range(0, len(pieces), 16):
             part = pieces[i:i + 16]
             n = len(part)

@@ -26,7 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--option", default="embed_fm_kernel", choices=sorted(OPTS))
     ap.add_argument("--values", default="0,1")
-    ap.add_argument("--workload", default="deepfm", choices=["deepfm", "dcn", "cross", "embed_fm", "din", "mlp"])
+    ap.add_argument("--workload", default="deepfm",
+                    choices=["deepfm", "dcn", "cross", "embed_fm", "din", "mlp", "din_tower"])
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--vocab", type=float, default=1e7)
     ap.add_argument("--rounds", type=int, default=8)
@@ -71,6 +72,15 @@ def main():
 
         def fn(i):
             outs[i % NP] = layer.forward_ids(table, Vd, hist_p[i % NP], cand_p[i % NP])
+    elif args.workload == "din_tower":  # DIN's tower shape: PReLU 25 -> 256 -> 128 -> 64 -> 1 at B 2048
+        Bt = 2048 if args.batch == 4096 else args.batch
+        B = Bt
+        dnn = rs.DNNLayer((256, 128, 64), 1, "prelu", seed=2, device=dev)
+        dnn.build(25)
+        xs = torch.randn(NP, Bt, 25, generator=g, device=dev)
+
+        def fn(i):
+            outs[i % NP] = dnn.tower(xs[i % NP])
     elif args.workload == "mlp":  # rs_mlp_fwd: DNNLayer((256, 128, 64), 1) on [B, 429] (the DeepFM tower alone)
         dnn = rs.DNNLayer((256, 128, 64), 1, "relu", seed=2, device=dev)
         dnn.build(429)

@@ -154,6 +154,26 @@ def test_din_model_bad_ids(gpu, nb):
             model(bad)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("nb,B,T", [(1, 2048, 100), (2, 37, 20)])
+def test_din_tower_reads_pieces(gpu, nb, B, T):
+    """DIN.call's tower reading the other sparse embeddings and the dense
+    features itself (rs_mlp_affine_pieces_fwd: no rs_concat_pieces launch, no
+    concat buffer) == the two-launch form (concat, then the tower), bit for
+    bit — the staged values and the arithmetic are the same."""
+    from recommender_system_amd import DIN
+    rng = np.random.default_rng(B + nb)
+    cols, behaviour = din_columns(nb, 8)
+    model = DIN(cols, behaviour, seed=3)
+    inputs = din_inputs(rng, cols, behaviour, B, T)
+    model(inputs)
+    randomize(model, rng)
+    y1 = model(inputs)
+    model.pieces_in_tower = False
+    y0 = model(inputs)
+    assert torch.equal(y1, y0)
+
+
 def test_oracle_din_two_behaviours_is_concat():
     """CPU: O.din with two behaviour features equals the attention over the
     k-concatenated embeddings with the mask of the first feature."""
