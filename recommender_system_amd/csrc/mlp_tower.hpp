@@ -494,7 +494,9 @@ __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, i
   if (w >= TA) *reinterpret_cast<floatx4*>(red + w * 256 + lane * 4) = acc;
   floatx4 wb[GWB];
   mlp_tail_fetch<GWB>(a, l1, wb);  // the next layer's slice, in flight over the hand-off
+  MLP_STAMP(10);                   // (diagnostic stamps 10..14: the layer hand-offs)
   __syncthreads();                 // the partial tiles in red
+  MLP_STAMP(11);
   if (w < TA) {
     acc = gather_parts(acc, TA);
     const int col = 16 * w + s;
@@ -514,12 +516,15 @@ __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, i
   const int colh = 16 * (w % TB) + s;
   const float hw = a.prep[a.off[LH] + ((int64_t)(min(colh, a.Np[l1] - 1) >> 4) * 64 +
                                        16 * ((colh & 15) >> 2)) * 4 + (colh & 3)];
+  MLP_STAMP(12);
   __syncthreads();  // its input complete; red free
   MLP_STAMP(2 + 2 * l1);
   acc = mlp_tail_mac<GWB>(a, l1, wb, out);
   MLP_STAMP(3 + 2 * l1);
   if (w >= TB) *reinterpret_cast<floatx4*>(red + w * 256 + lane * 4) = acc;
+  MLP_STAMP(13);
   __syncthreads();  // the partial tiles in red
+  MLP_STAMP(14);
   float* redh = red;  // [TB][16] head partials (red[0 .. 256 TB) is never a partial: parts >= 1 are waves >= TB)
   if (w < TB) {
     acc = gather_parts(acc, TB);
