@@ -542,7 +542,7 @@ __device__ __forceinline__ void dcn_fused_body(const CrossArgs& a, const EmbedCr
     mlp_tower_tile<NW>(t, tsm, b0, ring, xlog, 0, 1);
     floatx4 wr[8];
     mlp_tail_fetch<8>(t, 1, wr);
-    mlp_tail_splitk<NW, 8, 2>(t, tsm, b0, wr, xlog, 1);
+    mlp_tail_dispatch<NW>(t, tsm, b0, wr, xlog, 1);
   } else {
     mlp_tower_tile<NW>(t, tsm, b0, ring, xlog);
   }

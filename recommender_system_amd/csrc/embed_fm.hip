@@ -1024,7 +1024,8 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
     // the split-K tail (mlp_tail_splitk) at the DeepFM widths: layer 1's whole slice of this wave
     floatx4 wr[GWA];
     mlp_tail_fetch<GWA>(t, 1, wr);
-    mlp_tail_splitk<NW, GWA, GWB>(t, tsm, (int64_t)blockIdx.x * 16, wr, fmlog, 1);
+    if constexpr (GWA == 8 && GWB == 2) mlp_tail_dispatch<NW>(t, tsm, (int64_t)blockIdx.x * 16, wr, fmlog, 1);
+    else mlp_tail_splitk<NW, GWA, GWB>(t, tsm, (int64_t)blockIdx.x * 16, wr, fmlog, 1);
   } else {
     {  // layer 1's first weights (this wave's first item of it, if any)
       const int T1 = t.Np[1] >> 4, G1 = t.Kp[1] >> 4;
@@ -1255,7 +1256,10 @@ __global__ __launch_bounds__(16 * 64) void deepfm_all(EmbedFmArgs a, MlpArgs t, 
     const MlpArgs& a = t;
     MLP_STAMP(1);
   }
-  if constexpr (TAIL) mlp_tail_splitk<NW, GWA, GWB>(t, tsm, (int64_t)blockIdx.x * 16, wr, fmlog, 1);
+  if constexpr (TAIL) {
+    if constexpr (GWA == 8 && GWB == 2) mlp_tail_dispatch<NW>(t, tsm, (int64_t)blockIdx.x * 16, wr, fmlog, 1);
+    else mlp_tail_splitk<NW, GWA, GWB>(t, tsm, (int64_t)blockIdx.x * 16, wr, fmlog, 1);
+  }
   else mlp_tower_tile<NW>(t, tsm, (int64_t)blockIdx.x * 16, tring, fmlog, 1);
 }
 

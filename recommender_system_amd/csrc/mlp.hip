@@ -127,7 +127,7 @@ __device__ __forceinline__ void mlp_tower_body(const MlpArgs& a, const ConcatArg
     mlp_tower_tile<NW>(a, smem, m0, ring, nullptr, 0, 1);
     floatx4 wr[8];
     mlp_tail_fetch<8>(a, 1, wr);
-    mlp_tail_splitk<NW, 8, 2>(a, smem, m0, wr, nullptr, 1);
+    mlp_tail_dispatch<NW>(a, smem, m0, wr, nullptr, 1);
   } else {
     mlp_tower_tile<NW>(a, smem, m0, ring);
   }

@@ -427,23 +427,24 @@ inline bool mlp_tail_ok(const int* Np, const int* Kp, const int* N, int L, int l
   gwb = gw[1];
   return (gwa == 8 && gwb == 2) || (gwa == 4 && gwb == 2) || (gwa == 8 && gwb == 4) || (gwa == 4 && gwb == 1);
 }
-// this wave's weight slice of layer l (item w: tile w % T, k-groups part w / T)
-template <int GW>
+// this wave's weight slice of layer l (item w: tile w % T, k-groups part w / T);
+// TC > 0: the layer's tile count T known at compile time (no integer division)
+template <int GW, int TC = 0>
 __device__ __forceinline__ void mlp_tail_fetch(const MlpArgs& a, int l, floatx4 (&wr)[GW]) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int T = a.Np[l] >> 4, G = a.Kp[l] >> 4;
+  const int T = TC > 0 ? TC : a.Np[l] >> 4, G = a.Kp[l] >> 4;
   const int t = w % T, g0 = (w / T) * GW;
   const floatx4* W = reinterpret_cast<const floatx4*>(a.prep + a.off[l]) + lane + ((int64_t)t * G + g0) * 64;
 #pragma unroll
   for (int u = 0; u < GW; ++u) wr[u] = W[(int64_t)u * 64];
 }
 // layer l's contraction of this wave's slice (its partial tile)
-template <int GW>
+template <int GW, int TC = 0>
 __device__ __forceinline__ floatx4 mlp_tail_mac(const MlpArgs& a, int l, const floatx4 (&wr)[GW], const float* in) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int T = a.Np[l] >> 4;
+  const int T = TC > 0 ? TC : a.Np[l] >> 4;
   const int g0 = (w / T) * GW;
   const float* ap = in + (lane & 15) * a.rs + 4 * (lane >> 4);
   floatx4 an[GW];
@@ -462,7 +463,12 @@ __device__ __forceinline__ floatx4 mlp_tail_mac(const MlpArgs& a, int l, const f
 // LDS and the part-0 wave of each tile adds them in part order (one
 // ds_read_b128 per partial, conflict-free) and runs the tile's epilogue —
 // no all-thread reduction pass.
-template <int NW, int GWA, int GWB>
+// TAC / TBC > 0: the two split layers' tile counts known at compile time
+// (mlp_tail_dispatch: the DeepFM / DCN / DIN widths 256 -> 128 -> 64, T = 8 /
+// 4): part counts, item indices and the partial / head loops fold to
+// constants — the generic form spends its hand-offs in integer division and
+// loop control (profiles/r6_tail_stamps.jsonl)
+template <int NW, int GWA, int GWB, int TAC = 0, int TBC = 0>
 __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, int64_t m0, const floatx4 (&wa)[GWA],
                                                 const float* extra_lds, int l0) {
   static_assert(NW == 16, "split-K tail: 16 waves");
@@ -478,6 +484,7 @@ __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, i
   // the part-0 wave of tile t: its accumulator + the other parts' partial tiles
   auto gather_parts = [&](floatx4 acc, int T) {
     const int S = 16 / T;
+#pragma unroll
     for (int p = 1; p < S; ++p) {
       const floatx4 q = *reinterpret_cast<const floatx4*>(red + (w + p * T) * 256 + lane * 4);
 #pragma unroll
@@ -486,14 +493,14 @@ __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, i
     return acc;
   };
   // ---- layer l0
-  const int TA = a.Np[l0] >> 4;
+  const int TA = TAC > 0 ? TAC : a.Np[l0] >> 4;
   __syncthreads();  // its input complete
   MLP_STAMP(2 + 2 * l0);
-  floatx4 acc = mlp_tail_mac<GWA>(a, l0, wa, in);
+  floatx4 acc = mlp_tail_mac<GWA, TAC>(a, l0, wa, in);
   MLP_STAMP(3 + 2 * l0);
   if (w >= TA) *reinterpret_cast<floatx4*>(red + w * 256 + lane * 4) = acc;
   floatx4 wb[GWB];
-  mlp_tail_fetch<GWB>(a, l1, wb);  // the next layer's slice, in flight over the hand-off
+  mlp_tail_fetch<GWB, TBC>(a, l1, wb);  // the next layer's slice, in flight over the hand-off
   MLP_STAMP(10);                   // (diagnostic stamps 10..14: the layer hand-offs)
   __syncthreads();                 // the partial tiles in red
   MLP_STAMP(11);
@@ -509,7 +516,7 @@ __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, i
     });
   }
   // ---- layer l1, its epilogue folded with the head
-  const int TB = a.Np[l1] >> 4;
+  const int TB = TBC > 0 ? TBC : a.Np[l1] >> 4;
   // the head's weight of this lane's column (packed head layer: W[k][0] at
   // lane 16 ((k & 15) >> 2), element k & 3, of k-group k >> 4), requested
   // before the barrier (an L2 trip the part-0 epilogue would otherwise wait for)
@@ -519,7 +526,7 @@ __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, i
   MLP_STAMP(12);
   __syncthreads();  // its input complete; red free
   MLP_STAMP(2 + 2 * l1);
-  acc = mlp_tail_mac<GWB>(a, l1, wb, out);
+  acc = mlp_tail_mac<GWB, TBC>(a, l1, wb, out);
   MLP_STAMP(3 + 2 * l1);
   if (w >= TB) *reinterpret_cast<floatx4*>(red + w * 256 + lane * 4) = acc;
   MLP_STAMP(13);
@@ -544,6 +551,7 @@ __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, i
   if (threadIdx.x < 16) {
     const int row = threadIdx.x;
     float z = 0.f;
+#pragma unroll
     for (int t = 0; t < TB; ++t) z += redh[t * 16 + row];  // tile order
     const float* hb = par + a.poff[LH];
     float v = mlp_act(z + hb[0], a.act[LH], hb[a.Np[LH]]);
@@ -570,6 +578,17 @@ __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, i
     }
   }
   MLP_STAMP(15);
+}
+
+// The split-K tail at GWA = 8 / GWB = 2 with its tile counts as constants
+// when the widths are the DeepFM / DCN / DIN ones (a uniform branch on the
+// kernel arguments), the generic form otherwise.  wa: layer l0's slice,
+// fetched by the caller (mlp_tail_fetch<8> — the same values either way).
+template <int NW>
+__device__ __forceinline__ void mlp_tail_dispatch(const MlpArgs& a, float* smem, int64_t m0, const floatx4 (&wa)[8],
+                                                  const float* extra_lds, int l0) {
+  if (a.Np[l0] == 128 && a.Np[l0 + 1] == 64) mlp_tail_splitk<NW, 8, 2, 8, 4>(a, smem, m0, wa, extra_lds, l0);
+  else mlp_tail_splitk<NW, 8, 2>(a, smem, m0, wa, extra_lds, l0);
 }
 
 // Layer-0 ring fill for the wave's first item (issue before anything else).
