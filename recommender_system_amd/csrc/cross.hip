@@ -539,10 +539,9 @@ __device__ __forceinline__ void dcn_fused_body(const CrossArgs& a, const EmbedCr
   if constexpr (TAIL) {
     // layer 0 as usual, layers 1.. as the split-K tail at the DeepFM / DCN
     // widths (256 -> 128 -> 64 -> 1: all 16 waves per layer, mlp_tail_splitk)
-    mlp_tower_tile<NW>(t, tsm, b0, ring, xlog, 0, 1);
-    floatx4 wr[8];
-    mlp_tail_fetch<8>(t, 1, wr);
-    mlp_tail_dispatch<NW>(t, tsm, b0, wr, xlog, 1);
+    if (t.Np[0] == NW * 16) mlp_layer0_tiles<NW>(t, tsm, ring);
+    else mlp_tower_tile<NW>(t, tsm, b0, ring, xlog, 0, 1);
+    mlp_tail_run<NW>(t, tsm, b0, xlog);
   } else {
     mlp_tower_tile<NW>(t, tsm, b0, ring, xlog);
   }

@@ -1022,10 +1022,13 @@ __global__ __launch_bounds__(16 * 64) void deepfm_ws(EmbedFmArgs a, MlpArgs t, F
   }
   if constexpr (GWA > 0) {
     // the split-K tail (mlp_tail_splitk) at the DeepFM widths: layer 1's whole slice of this wave
-    floatx4 wr[GWA];
-    mlp_tail_fetch<GWA>(t, 1, wr);
-    if constexpr (GWA == 8 && GWB == 2) mlp_tail_dispatch<NW>(t, tsm, (int64_t)blockIdx.x * 16, wr, fmlog, 1);
-    else mlp_tail_splitk<NW, GWA, GWB>(t, tsm, (int64_t)blockIdx.x * 16, wr, fmlog, 1);
+    if constexpr (GWA == 8 && GWB == 2) {
+      mlp_tail_run<NW>(t, tsm, (int64_t)blockIdx.x * 16, fmlog);
+    } else {
+      floatx4 wr[GWA];
+      mlp_tail_fetch<GWA>(t, 1, wr);
+      mlp_tail_splitk<NW, GWA, GWB>(t, tsm, (int64_t)blockIdx.x * 16, wr, fmlog, 1);
+    }
   } else {
     {  // layer 1's first weights (this wave's first item of it, if any)
       const int T1 = t.Np[1] >> 4, G1 = t.Kp[1] >> 4;

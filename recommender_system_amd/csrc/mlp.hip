@@ -124,10 +124,9 @@ __device__ __forceinline__ void mlp_tower_body(const MlpArgs& a, const ConcatArg
   if constexpr (TAIL) {
     // a 256 -> 128 -> 64 -> 1 tail (the reference's DNN widths): layer 0 as
     // usual, the rest as the split-K tail on all 16 waves (mlp_tail_splitk)
-    mlp_tower_tile<NW>(a, smem, m0, ring, nullptr, 0, 1);
-    floatx4 wr[8];
-    mlp_tail_fetch<8>(a, 1, wr);
-    mlp_tail_dispatch<NW>(a, smem, m0, wr, nullptr, 1);
+    if (a.Np[0] == NW * 16) mlp_layer0_tiles<NW>(a, smem, ring);
+    else mlp_tower_tile<NW>(a, smem, m0, ring, nullptr, 0, 1);
+    mlp_tail_run<NW>(a, smem, m0, nullptr);
   } else {
     mlp_tower_tile<NW>(a, smem, m0, ring);
   }

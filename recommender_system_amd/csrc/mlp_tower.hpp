@@ -580,6 +580,38 @@ __device__ __forceinline__ void mlp_tail_splitk(const MlpArgs& a, float* smem, i
   MLP_STAMP(15);
 }
 
+// Layer 0 of a tower whose first layer has NW 16-unit output tiles (256
+// units: the DeepFM / DCN / DIN widths) before the split-K tail: wave w owns
+// output tile w over every k-group (its ring filled by mlp_first_fill), the
+// epilogue (bias, activation) writes buf1.  The generic mlp_tower_tile does
+// the same work through run-time item / part arithmetic and a per-layer
+// loop; here only G (the k-groups) is a run-time value.  Input in buf0
+// (written, barrier not yet taken).
+template <int NW>
+__device__ __forceinline__ void mlp_layer0_tiles(const MlpArgs& a, float* smem, floatx4 (&ring)[MLP_R],
+                                                 const float* extra_lds = nullptr) {
+  const int RS = a.rs;
+  float* par = smem + 32 * RS + NW * 256;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int G = a.Kp[0] >> 4;
+  __syncthreads();
+  MLP_STAMP(2);
+  const floatx4* bp = reinterpret_cast<const floatx4*>(a.prep + a.off[0]) + lane + (int64_t)w * G * 64;
+  const float* ap = smem + (lane & 15) * RS + 4 * (lane >> 4);
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  mlp_mac(ring, ap, bp, 0, G, acc, a.unroll);
+  const int col = 16 * w + (lane & 15);
+  const float bc = par[a.poff[0] + col], ac = par[a.poff[0] + a.Np[0] + col];
+  float* out = smem + 16 * RS;
+  with_act(a.act[0], [&](auto A) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[(4 * (lane >> 4) + r) * RS + col] = mlp_act_c<decltype(A)::value>(acc[r] + bc, ac);
+  });
+  MLP_STAMP(3);
+  (void)extra_lds;
+}
+
 // The split-K tail at GWA = 8 / GWB = 2 with its tile counts as constants
 // when the widths are the DeepFM / DCN / DIN ones (a uniform branch on the
 // kernel arguments), the generic form otherwise.  wa: layer l0's slice,
@@ -589,6 +621,19 @@ __device__ __forceinline__ void mlp_tail_dispatch(const MlpArgs& a, float* smem,
                                                   const float* extra_lds, int l0) {
   if (a.Np[l0] == 128 && a.Np[l0 + 1] == 64) mlp_tail_splitk<NW, 8, 2, 8, 4>(a, smem, m0, wa, extra_lds, l0);
   else mlp_tail_splitk<NW, 8, 2>(a, smem, m0, wa, extra_lds, l0);
+}
+// ... fetching layer 1's slice itself (wave w: tile w % T, part w / T — with T
+// a constant in the specialised form)
+template <int NW>
+__device__ __forceinline__ void mlp_tail_run(const MlpArgs& a, float* smem, int64_t m0, const float* extra_lds) {
+  floatx4 wa[8];
+  if (a.Np[1] == 128 && a.Np[2] == 64) {
+    mlp_tail_fetch<8, 8>(a, 1, wa);
+    mlp_tail_splitk<NW, 8, 2, 8, 4>(a, smem, m0, wa, extra_lds, 1);
+  } else {
+    mlp_tail_fetch<8>(a, 1, wa);
+    mlp_tail_splitk<NW, 8, 2>(a, smem, m0, wa, extra_lds, 1);
+  }
 }
 
 // Layer-0 ring fill for the wave's first item (issue before anything else).
