@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--option", default="embed_fm_kernel", choices=sorted(OPTS))
     ap.add_argument("--values", default="0,1")
     ap.add_argument("--workload", default="deepfm",
-                    choices=["deepfm", "dcn", "cross", "embed_fm", "din", "mlp", "din_tower"])
+                    choices=["deepfm", "dcn", "cross", "embed_fm", "din", "mlp", "din_tower", "shard_pipe"])
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--vocab", type=float, default=1e7)
     ap.add_argument("--rounds", type=int, default=8)
@@ -72,6 +72,18 @@ def main():
 
         def fn(i):
             outs[i % NP] = layer.forward_ids(table, Vd, hist_p[i % NP], cand_p[i % NP])
+    elif args.workload == "shard_pipe":  # the sharded FM's pipe launch at world 1 (no exchange), 26 x 1e7
+        from recommender_system_amd.sharded import ShardedEmbeddingFM
+        V = int(args.vocab)
+        sh = ShardedEmbeddingFM([V] * F, k, nd, 10, device=dev, seed=3, world=1, rank=0)
+        idsv = torch.randint(0, V, (NP, B, F), generator=g, device=dev, dtype=torch.int32)
+        souts = [torch.empty(B, 1, device=dev) for _ in range(NP)]
+        sh.pipe_route(idsv[0])
+
+        def fn(i):
+            j, jp, jn = i % NP, (i - 1) % NP, (i + 1) % NP
+            sh.pipe_step(prev=(dense[jp], souts[jp]), cur=idsv[j], nxt=(dense[jn], idsv[jn]))
+            outs[i % NP] = souts[jp]
     elif args.workload == "din_tower":  # DIN's tower shape: PReLU 25 -> 256 -> 128 -> 64 -> 1 at B 2048
         Bt = 2048 if args.batch == 4096 else args.batch
         B = Bt
