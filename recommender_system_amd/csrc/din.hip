@@ -460,12 +460,15 @@ __host__ __device__ inline DfLayout df_layout(int NTT, int HT1, int HT2, int KS)
   return L;
 }
 
-template <int KS, int HT1, int HT2, int KIND>
+// NTTC > 0: the position-tile count known at compile time (config 4: T =
+// 100 -> 7 tiles): the (sample, tile) item codes, the live-tile scan and the
+// merge loops fold to constants instead of run-time division / loop control
+template <int KS, int HT1, int HT2, int KIND, int NTTC = 0>
 __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
   typedef Ids<KIND> I;
   constexpr int K = 4 * KS;
   const DinGeom& g = a.g;
-  const int NTT = g.NTT, T = g.T;
+  const int NTT = NTTC > 0 ? NTTC : g.NTT, T = g.T;
   const DfLayout L = df_layout(NTT, HT1, HT2, KS);
   extern __shared__ float dsm[];
   float* a1s = dsm + L.a1;  // [NTT*16][HT1*16 + 4]
@@ -763,10 +766,17 @@ static void launch_din_h(const DinArgs& a, hipStream_t st) {
   if (a.g.HT1 == 5 && a.g.HT2 == 3) {  // reference (80, 40)
     const size_t lds = df_lds(a.g);
     if (opt(RS_OPT_DIN_KERNEL) == 0 && lds) {
+      DinArgs b = a;
+      const unsigned grid = (unsigned)((a.batch + DF_SPW - 1) / DF_SPW);
+      if (KS == 2 && a.g.NTT == 7) {  // config 4 (k 8, T 97..112)
+        static LdsAttr set7;
+        lds_attr(set7, (const void*)din_fused<KS, 5, 3, KIND, 7>, lds);
+        din_fused<KS, 5, 3, KIND, 7><<<grid, DF_NW * 64, lds, st>>>(b);
+        return;
+      }
       static LdsAttr set;
       lds_attr(set, (const void*)din_fused<KS, 5, 3, KIND>, lds);
-      DinArgs b = a;
-      din_fused<KS, 5, 3, KIND><<<(unsigned)((a.batch + DF_SPW - 1) / DF_SPW), DF_NW * 64, lds, st>>>(b);
+      din_fused<KS, 5, 3, KIND><<<grid, DF_NW * 64, lds, st>>>(b);
       return;
     }
     launch_din<KS, 5, 3, KIND, true>(a, st);
