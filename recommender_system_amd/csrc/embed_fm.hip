@@ -132,9 +132,16 @@ __global__ void fm_prepare_generic(const float* __restrict__ w1, const float* __
 // row stride tw->rs) instead of x_out, and the DNN tower of mlp_tower.hpp runs
 // on it, closed by sigmoid(c0*dnn + c1*fm) (model/deepFM.py:24-30).
 // A workgroup owns one 16-sample MFMA row tile.
-template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, bool PF = false, bool KA = false>
+// FC / KFMC / NDC: the field count, FM width and dense width as compile-time
+// constants (0 / 0 / -1: the kernel arguments' run-time values) — the
+// headline shape's kernarg and streamed kernels take 26 / 10 / 13
+template <int KV, int NT, int NW, int KIND, bool TW, int MC = 0, bool PF = false, bool KA = false, int FC = 0,
+          int KFMC = 0, int NDC = -1>
 __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArgs* tw, const int tile,
                                               const FieldMeta* km = nullptr) {
+  const int aF = FC > 0 ? FC : a.F;        // (compile-time at the specialised shapes)
+  const int akfm = KFMC > 0 ? KFMC : a.kfm;
+  const int and_ = NDC >= 0 ? NDC : a.nd;
   // MC > 0: field slots per wave and pass (owner kernels with few fields)
   constexpr int MAXC0 = MC > 0 ? MC : 128 / (NW * KV);
   constexpr int MAXC = MAXC0 < 1 ? 1 : (MAXC0 > 8 ? 8 : MAXC0);
@@ -152,7 +159,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   // Padded lanes of the last tile recompute the last sample: an MFMA output
   // row depends only on its own A row, so they never touch valid outputs.
   const int64_t b = bt < a.batch ? bt : a.batch - 1;
-  const int d = a.nd + a.F * a.k;
+  const int d = and_ + aF * a.k;
   // w0 is requested now, not behind the rows (a dependent load at the end)
   const float w0v = OWNER ? 0.f : a.w0[0];
 
@@ -176,7 +183,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   // Materialise every kernel argument at entry: one batched s_load instead
   // of lazy per-use kernarg loads (each a dependent K$ round trip).
   asm volatile("" ::"s"(a.ids), "s"(a.id_stride), "s"(a.dense), "s"(a.dense_stride), "s"(a.nd), "s"(a.table),
-               "s"(a.offs), "s"(a.vocab), "s"(a.F), "s"(a.k), "s"(a.prep), "s"(a.kfm));
+               "s"(a.offs), "s"(a.vocab), "s"(aF), "s"(a.k), "s"(a.prep), "s"(akfm));
   asm volatile("" ::"s"(a.batch), "s"(a.DB), "s"(a.dense_rec), "s"(a.field_rec), "s"(a.field_base), "s"(a.x_out),
                "s"(a.logit), "s"(a.w0), "s"(a.err));
   RS_STAMP(0);
@@ -196,7 +203,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     mlp_first_fill<NW>(*tw, ring);
     float* par = tsm + 32 * tw->rs + NW * 256;
     for (int i = threadIdx.x; i < tw->ptot; i += NW * 64) par[i] = tw->prep[tw->wtot + i];
-    const int d0 = a.F * a.k + a.nd, padw = tw->Kp[0] - d0;
+    const int d0 = aF * a.k + and_, padw = tw->Kp[0] - d0;
     for (int i = threadIdx.x; i < 16 * padw; i += NW * 64) {
       const int r = i / padw;
       tsm[r * xrs + d0 + (i - r * padw)] = 0.f;
@@ -213,7 +220,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   auto load_dense = [&]() {
     if (has_dense) {
       const int e = 4 * dw + kk;
-      dx = a.dense[b * a.dense_stride + (e < a.nd ? e : 0)];  // masked at use
+      dx = a.dense[b * a.dense_stride + (e < and_ ? e : 0)];  // masked at use
       const float* rec = a.prep + (int64_t)dw * a.dense_rec;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) drec[nt] = rec[nt * 64 + lane];
@@ -230,14 +237,14 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   // (owner side, KIND 4: the local rows need no field metadata, so every
   // wave loads its own ids — no id tile, no barrier before the rows)
 #ifdef RS_DIAG_STAMPS
-  const bool coop = !KA && !OWNER && (KIND != 3) && a.F <= FMAX && !(a.ablate & 16);  // bit 16: per-wave id loads
+  const bool coop = !KA && !OWNER && (KIND != 3) && aF <= FMAX && !(a.ablate & 16);  // bit 16: per-wave id loads
 #else
-  const bool coop = !KA && !OWNER && (KIND != 3) && a.F <= FMAX;
+  const bool coop = !KA && !OWNER && (KIND != 3) && aF <= FMAX;
 #endif
   if (coop) {
     const int64_t b0 = (int64_t)tile * 16;
-    for (int t = threadIdx.x; t < 16 * a.F; t += NW * 64) {
-      const int ss = t / a.F, c = t - ss * a.F;
+    for (int t = threadIdx.x; t < 16 * aF; t += NW * 64) {
+      const int ss = t / aF, c = t - ss * aF;
       const int64_t bb = b0 + ss < a.batch ? b0 + ss : a.batch - 1;
       const auto idv = I::load(a.ids, bb * a.id_stride + c);
 #ifdef RS_DIAG_STAMPS
@@ -247,9 +254,9 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       lid[ss][c] = idv;
     }
     if constexpr (!OWNER) {
-      for (int t = threadIdx.x; t < 2 * a.F; t += NW * 64) {
-        const int c = t < a.F ? t : t - a.F;
-        lmeta[t < a.F ? 0 : 1][c] = t < a.F ? a.offs[c] : a.vocab[c];
+      for (int t = threadIdx.x; t < 2 * aF; t += NW * 64) {
+        const int c = t < aF ? t : t - aF;
+        lmeta[t < aF ? 0 : 1][c] = t < aF ? a.offs[c] : a.vocab[c];
       }
     }
   }
@@ -273,7 +280,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
       const int c = cg + j * NW + w;
-      P.cj[j] = c < a.F ? c : a.F - 1;
+      P.cj[j] = c < aF ? c : aF - 1;
       const float* rec = a.prep + a.field_base + (int64_t)P.cj[j] * a.field_rec;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
@@ -281,7 +288,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
         if (a.ablate & 2) { P.bw[j][nt].zero(); P.bw[j][nt].v[0] = (float)P.cj[j]; continue; }
 #endif
         // lanes of the zero-padded columns (> kfm) load nothing
-        if (nt * 16 + s <= a.kfm) P.bw[j][nt].load(rec + (int64_t)(nt * 64 + lane) * KV);
+        if (nt * 16 + s <= akfm) P.bw[j][nt].load(rec + (int64_t)(nt * 64 + lane) * KV);
         else P.bw[j][nt].zero();
       }
     }
@@ -296,7 +303,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
         float sq = 0.f;
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
-          const float bv = nt * 16 + s < a.kfm ? P.bw[j][nt].v[tp] : 0.f;
+          const float bv = nt * 16 + s < akfm ? P.bw[j][nt].v[tp] : 0.f;
           sq = fmaf(bv, bv, sq);
         }
         P.nrm[j][tp] = row16_sum(sq);
@@ -326,14 +333,14 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
           vocc[j] = km->voc[P.cj[j]];
           P.rid[j] = I::load(a.ids, b * a.id_stride + P.cj[j]);
         } else {
-          const int cv = min(cg + j * NW + wv, a.F - 1);
+          const int cv = min(cg + j * NW + wv, aF - 1);
           offc[j] = a.offs[cv];
           vocc[j] = a.vocab[cv];
           P.rid[j] = I::load(a.ids, b * a.id_stride + P.cj[j]);
         }
       }
     }
-    if (cg == 0 && !coop && a.F > 0) load_dense();
+    if (cg == 0 && !coop && aF > 0) load_dense();
   };
   // id -> table row (the ids must have arrived)
   auto decode_rows = [&](int cg, Pass& P) {
@@ -342,7 +349,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
       if constexpr (KIND == 3) {
-        P.row[j] = b * a.F + P.cj[j];
+        P.row[j] = b * aF + P.cj[j];
         P.ok[j] = true;
       } else {
         int64_t id;
@@ -359,7 +366,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
 #ifdef RS_DIAG_STAMPS
-      if ((a.ablate & 8) && cg + j * NW + w >= a.F) { P.xs[j].zero(); continue; }
+      if ((a.ablate & 8) && cg + j * NW + w >= aF) { P.xs[j].zero(); continue; }
 #endif
       P.xs[j].load_nt(a.table + P.row[j] * a.k + KV * kk);
     }
@@ -376,7 +383,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     else RS_STAMP(12);
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
-      const bool live = cg + j * NW + w < a.F;
+      const bool live = cg + j * NW + w < aF;
       if constexpr (OWNER) bad |= live && !P.ok[j] && P.rid[j] != -1;
       else bad |= live && !P.ok[j];
       const bool use = live && P.ok[j];
@@ -399,7 +406,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
           for (int tp = 0; tp < KV; ++tp) xo[tp] = P.ok[j] ? P.xs[j].v[tp] : 0.f;
         }
       } else if (!KA && a.x_out && live && valid) {  // (the kernarg kernel never emits x)
-        float* xo = a.x_out + b * d + a.nd + P.cj[j] * a.k + KV * kk;
+        float* xo = a.x_out + b * d + and_ + P.cj[j] * a.k + KV * kk;
 #pragma unroll
         for (int tp = 0; tp < KV; ++tp) xo[tp] = P.ok[j] ? P.xs[j].v[tp] : 0.f;
       }
@@ -410,7 +417,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   };
   // one slot per wave: a wave with no field left in a pass stops there (a
   // wave-uniform exit; nothing after the loop needs its slot)
-  auto has_pass = [&](int cg) { return cg < a.F && !(MAXC == 1 && cg + w >= a.F); };
+  auto has_pass = [&](int cg) { return cg < aF && !(MAXC == 1 && cg + w >= aF); };
   constexpr int PS = NW * MAXC;  // fields per pass
   // PF: B fragments of the first two passes ride the id trip (registers: two
   // passes only where they are few; larger rows load theirs per pass).
@@ -422,7 +429,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     if (has_pass(0)) issue_b(0, P0);
     if (has_pass(PS)) issue_b(PS, P1);
   }
-  if (a.F == 0 || coop) load_dense();
+  if (aF == 0 || coop) load_dense();
   if (coop) __syncthreads();
   RS_STAMP(9);
   if (PRE) {
@@ -433,7 +440,7 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       // fragments: ids first was slower, 5.95 vs 5.75 us at 4096)
       fetch_ids(0, P0);
       if (two) fetch_ids(PS, P1);
-    } else if (!coop && a.F > 0) {
+    } else if (!coop && aF > 0) {
       load_dense();  // a wave with no field (F < NW) may still own a dense k-step
     }
     if (one) {
@@ -472,28 +479,28 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
   // ---- dense MFMAs (their loads were issued in the prologue)
   if (has_dense) {
     const int e = 4 * dw + kk;
-    dx = e < a.nd ? dx : 0.f;
+    dx = e < and_ ? dx : 0.f;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) ac[nt][0] = mfma16x16x4(dx, drec[nt], ac[nt][0]);
     qn = fmaf(dx * dx, dn, qn);
     if constexpr (TW) {
-      if (e < a.nd) tsm[s * xrs + a.F * a.k + e] = dx;
-    } else if (!KA && a.x_out && valid && e < a.nd) {
+      if (e < and_) tsm[s * xrs + aF * a.k + e] = dx;
+    } else if (!KA && a.x_out && valid && e < and_) {
       a.x_out[b * d + e] = dx;
     }
   }
   if (!dense_small) {
     for (int t = w; t < a.DB; t += NW) {
       const int e = 4 * t + kk;
-      const float xv = a.dense[b * a.dense_stride + (e < a.nd ? e : 0)];
-      const float x = e < a.nd ? xv : 0.f;
+      const float xv = a.dense[b * a.dense_stride + (e < and_ ? e : 0)];
+      const float x = e < and_ ? xv : 0.f;
       const float* rec = a.prep + (int64_t)t * a.dense_rec;
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) ac[nt][0] = mfma16x16x4(x, rec[nt * 64 + lane], ac[nt][0]);
       qn = fmaf(x * x, rec[NT * 64 + kk], qn);
       if constexpr (TW) {
-        if (e < a.nd) tsm[s * xrs + a.F * a.k + e] = x;
-      } else if (a.x_out && valid && e < a.nd) {
+        if (e < and_) tsm[s * xrs + aF * a.k + e] = x;
+      } else if (a.x_out && valid && e < and_) {
         a.x_out[b * d + e] = x;
       }
     }
@@ -530,9 +537,9 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
     float v = 0.f;
 #pragma unroll
     for (int ww = 0; ww < NW; ++ww) v += cs[ww][smp][col];
-    float t = col < a.kfm ? v * v : 0.f;       // s_f^2
+    float t = col < akfm ? v * v : 0.f;       // s_f^2
     if (col < NW) t -= qs[col][smp];           // - sum_i x_i^2 |v_i|^2 (wave partials)
-    float lin = col == a.kfm ? v : 0.f;        // x@w1
+    float lin = col == akfm ? v : 0.f;        // x@w1
     t = row16_sum(t);
     lin = row16_sum(lin);
     if constexpr (NT == 2) {
@@ -547,9 +554,9 @@ __device__ __forceinline__ void embed_fm_body(const EmbedFmArgs& a, const MlpArg
       if constexpr (NT == 2) q += __shfl_xor(q, 16);
       if (bb < a.batch) {
         float* rec = a.logit + bb * a.pstride;
-        if (col <= a.kfm) rec[col] = v;
-        if (col == 0) rec[a.kfm + 1] = q;
-        else if (a.kfm + 1 + col < a.pw) rec[a.kfm + 1 + col] = 0.f;
+        if (col <= akfm) rec[col] = v;
+        if (col == 0) rec[akfm + 1] = q;
+        else if (akfm + 1 + col < a.pw) rec[akfm + 1 + col] = 0.f;
       }
       return;
     }
@@ -577,9 +584,9 @@ __global__ __launch_bounds__(NW * 64) void embed_fm_mfma(EmbedFmArgs a) {
 // the field metadata by value (rs_embed_fm_fwd_hm): each wave loads its own
 // fields' ids and reads (offset, vocab) through scalar kernarg loads — no LDS
 // id tile, no barrier, no per-wave metadata loads from one hot L2 line
-template <int KV, int NT, int NW, int KIND, bool PF>
+template <int KV, int NT, int NW, int KIND, bool PF, int FC = 0, int KFMC = 0, int NDC = -1>
 __global__ __launch_bounds__(NW * 64) void embed_fm_mfma_ka(EmbedFmArgs a, FieldMeta m) {
-  embed_fm_body<KV, NT, NW, KIND, false, 1, PF, true>(a, nullptr, blockIdx.x, &m);
+  embed_fm_body<KV, NT, NW, KIND, false, 1, PF, true, FC, KFMC, NDC>(a, nullptr, blockIdx.x, &m);
 }
 
 // S consecutive batches in ONE launch (rs_embed_fm_fwd_hm_stream): workgroup
@@ -594,7 +601,7 @@ struct StreamArgs {
   int tpb, S;
   int64_t ids_bstride_bytes, dense_bstride, logit_bstride, last_batch;
 };
-template <int KV, int NT, int KIND, int MINB>
+template <int KV, int NT, int KIND, int MINB, int FC = 0, int KFMC = 0, int NDC = -1>
 __global__ __launch_bounds__(16 * 64, MINB) void embed_fm_stream_ka(EmbedFmArgs a, FieldMeta m, StreamArgs sa) {
   const int s = blockIdx.x / sa.tpb, tile = blockIdx.x - s * sa.tpb;
   EmbedFmArgs b = a;
@@ -603,7 +610,7 @@ __global__ __launch_bounds__(16 * 64, MINB) void embed_fm_stream_ka(EmbedFmArgs 
   b.logit = a.logit + s * sa.logit_bstride;
   if (s == sa.S - 1) b.batch = sa.last_batch;
   if ((int64_t)tile * 16 >= b.batch) return;  // a shorter last batch: fewer tiles (uniform exit)
-  embed_fm_body<KV, NT, 16, KIND, false, 1, true, true>(b, nullptr, tile, &m);
+  embed_fm_body<KV, NT, 16, KIND, false, 1, true, true, FC, KFMC, NDC>(b, nullptr, tile, &m);
 }
 
 // ---- sharded FM, partial protocol: combine (requester side) as a block part
@@ -684,7 +691,7 @@ struct PipeArgs {
   PeerArgs x;
 };
 
-template <int KV, int NT, int NW, int MC, bool XCHG = false>
+template <int KV, int NT, int NW, int MC, bool XCHG = false, int FC = 0, int KFMC = 0>
 __global__ __launch_bounds__(NW * 64) void shard_fm_pipe(EmbedFmArgs a, PipeArgs p) {
   // the short route / combine blocks come first in dispatch order, the owner
   // blocks (the headline kernel's body) after them: dispatched last, the
@@ -708,7 +715,8 @@ __global__ __launch_bounds__(NW * 64) void shard_fm_pipe(EmbedFmArgs a, PipeArgs
   } else {
     // the headline kernel's schedule: B fragments of the first two passes and
     // both passes' ids issued before the first rows (PF)
-    embed_fm_body<KV, NT, NW, 4, false, MC, true>(a, nullptr, bid - p.route_blocks - p.combine_blocks);
+    embed_fm_body<KV, NT, NW, 4, false, MC, true, false, FC, KFMC, (FC > 0 ? 0 : -1)>(
+        a, nullptr, bid - p.route_blocks - p.combine_blocks);
   }
 }
 
@@ -1473,6 +1481,12 @@ static void launch_embed_fm3(const EmbedFmArgs& a, hipStream_t st, const FieldMe
     // (round 5: the ids through 16 scalar loads per wave and a lane select
     // chain, off the vector memory queue, ran 7.08 vs 6.12 us per launch,
     // bit-identical — profiles/r5_ab_scalar_ids.json; not kept)
+    if constexpr (KV == 4 && NT == 1 && KIND != 2) {
+      if (a.F == 26 && a.kfm == 10 && a.nd == 13) {  // the Criteo / headline shape
+        embed_fm_mfma_ka<KV, NT, 16, KIND, true, 26, 10, 13><<<grid, 16 * 64, 0, st>>>(a, *hm);
+        return;
+      }
+    }
     embed_fm_mfma_ka<KV, NT, 16, KIND, true><<<grid, 16 * 64, 0, st>>>(a, *hm);
     return;
   }
@@ -1703,6 +1717,13 @@ extern "C" int rs_embed_fm_fwd_hm_stream(const void* ids, int id_kind, int64_t i
   hipStream_t st = as_stream(stream);
   auto go = [&](auto kv, auto kind) {
     constexpr int KV = decltype(kv)::value, KIND = decltype(kind)::value;
+    if constexpr (KV == 4) {
+      if (n_fields == 26 && kfm == 10 && nd == 13) {  // the headline shape, as the single launch
+        if (min_blocks == 2) embed_fm_stream_ka<KV, 1, KIND, 2, 26, 10, 13><<<grid, 16 * 64, 0, st>>>(a, m, sa);
+        else embed_fm_stream_ka<KV, 1, KIND, 1, 26, 10, 13><<<grid, 16 * 64, 0, st>>>(a, m, sa);
+        return;
+      }
+    }
     if (min_blocks == 2) embed_fm_stream_ka<KV, 1, KIND, 2><<<grid, 16 * 64, 0, st>>>(a, m, sa);
     else embed_fm_stream_ka<KV, 1, KIND, 1><<<grid, 16 * 64, 0, st>>>(a, m, sa);
   };
@@ -1870,7 +1891,16 @@ static void launch_pipe4(const EmbedFmArgs& a, PipeArgs p, hipStream_t st) {
   if (p.combine_blocks) p.combine_blocks = (int)std::min<int64_t>((p.c.batch * 16 + T - 1) / T, 4096);
   if (!XCHG) p.xchg_blocks = 0;
   const int grid = p.xchg_blocks + p.owner_blocks + p.route_blocks + p.combine_blocks;
-  if (grid) shard_fm_pipe<KV, NT, NW, MC, XCHG><<<grid, T, 0, st>>>(a, p);
+  if (!grid) return;
+  if constexpr (KV == 4 && NT == 1 && NW == 16 && MC == 1) {
+    // the world-1 owner of the Criteo table (all 26 fields, kfm 10, no dense
+    // block): field count and FM width as constants (as the headline kernel)
+    if (a.F == 26 && a.kfm == 10 && a.nd == 0) {
+      shard_fm_pipe<KV, NT, NW, MC, XCHG, 26, 10><<<grid, T, 0, st>>>(a, p);
+      return;
+    }
+  }
+  shard_fm_pipe<KV, NT, NW, MC, XCHG><<<grid, T, 0, st>>>(a, p);
 }
 
 // the two-deep peer step: 1-tile (kfm <= 15) owner part with <= 32 fields
