@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--option", default="embed_fm_kernel", choices=sorted(OPTS))
     ap.add_argument("--values", default="0,1")
     ap.add_argument("--workload", default="deepfm",
-                    choices=["deepfm", "dcn", "cross", "embed_fm", "din", "mlp", "din_tower", "shard_pipe"])
+                    choices=["deepfm", "dcn", "cross", "embed_fm", "din", "mlp", "din_tower", "shard_pipe", "peer_gather"])
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--vocab", type=float, default=1e7)
     ap.add_argument("--rounds", type=int, default=8)
@@ -84,6 +84,19 @@ def main():
             j, jp, jn = i % NP, (i - 1) % NP, (i + 1) % NP
             sh.pipe_step(prev=(dense[jp], souts[jp]), cur=idsv[j], nxt=(dense[jn], idsv[jn]))
             outs[i % NP] = souts[jp]
+    elif args.workload == "peer_gather":  # config 5's owner row service at world 1: rs_peer_gather_a2a, B x F rows
+        import torch.distributed as dist
+        from recommender_system_amd.sharded import PeerExchange
+        if not dist.is_initialized():
+            dist.init_process_group("gloo", init_method="tcp://127.0.0.1:29533", rank=0, world_size=1)
+        V = int(args.vocab)
+        table = torch.randn(V, k, device=dev, generator=g)
+        nw = B * F
+        idsp = torch.randint(0, V, (NP, nw), generator=g, device=dev, dtype=torch.int32)
+        ex = PeerExchange(nw * 64, world=1, rank=0, device=dev)
+
+        def fn(i):
+            outs[i % NP] = ex.gather_all_to_all(idsp[i % NP], nw, table).view(torch.float32)
     elif args.workload == "din_tower":  # DIN's tower shape: PReLU 25 -> 256 -> 128 -> 64 -> 1 at B 2048
         Bt = 2048 if args.batch == 4096 else args.batch
         B = Bt
