@@ -10,7 +10,10 @@
 //   ready [world] x 128 B        ready[r] = the last step for which rank r's
 //                                mailbox is free (written by rank r at every peer)
 //   full  [world] x 128 B        full[r]  = the last step whose block from rank r
-//                                is in my data (written by rank r)
+//                                is in my data (written by rank r; full-fence mode)
+//   chunk [world][chunks] x 8 B  lean mode: [r][c] = the last step whose chunk c
+//                                from rank r is in my data (written by that
+//                                workgroup of rank r)
 // Per-rank local state (ordinary device memory): seq (steps done), a
 // per-destination chunk counter, and a completed-workgroup counter.
 //
@@ -19,14 +22,18 @@
 //   1. workgroup 0 tells every peer that my mailbox is free for step seq
 //      (ready[me] = seq at each peer): the kernels that read the previous
 //      step's data ran before this one on my stream;
-//   2. workgroup (c, p) waits until peer p's mailbox is free for seq (p's
-//      ready word in MY mailbox: a local poll), copies
-//      chunk c of my block for p into p's data[me] (16-B stores), drains its
-//      stores, releases at system scope and counts itself on p's chunk
-//      counter; the last chunk writer of destination p sets full[me] = seq
-//      at p (release store, system scope);
-//   3. workgroup 0 waits for full[r] == seq from every rank r (acquire) and
-//      for every workgroup of this launch to have counted itself, then
+//   2. workgroup (c, p) requests its first words of chunk c of my block for
+//      p (local sources), waits until peer p's mailbox is free for seq (p's
+//      ready word in MY mailbox: a local poll), stores the chunk into p's
+//      data[me] (16-B stores) and drains them; then
+//      - lean mode: sets its own chunk flag [me][c] = seq at p and its done
+//        word in my state (plain write-through stores, no shared counter);
+//      - full-fence mode: releases at system scope and counts itself on p's
+//        chunk counter; the last chunk writer of destination p sets
+//        full[me] = seq at p (release store, system scope);
+//   3. workgroup 0 waits for every chunk of step seq to be in my mailbox
+//      (lean: all [r][c] chunk flags; full-fence: full[r] from every rank r,
+//      acquire) and for every workgroup of this launch to be done, then
 //      advances state.seq — so the launch completes only when my mailbox
 //      holds the whole step, and the next kernel on the stream reads it.
 // Every spin is bounded: a wait that gives up sets RS_FLAG_TIMEOUT in the
@@ -53,7 +60,7 @@ extern "C" int64_t rs_peer_state_bytes(void) { return (int64_t)sizeof(PeerState)
 extern "C" int64_t rs_peer_mailbox_bytes(int world, int64_t block_bytes) {
   if (world < 1 || world > PEER_MAXW || block_bytes < 0 || block_bytes % 16) return -1;
   const int64_t data = ((int64_t)world * block_bytes + 255) / 256 * 256;
-  return data + 2 * (int64_t)world * PEER_FLAG_STRIDE;
+  return data + 2 * (int64_t)world * PEER_FLAG_STRIDE + PEER_MAXBLK * 8;
 }
 
 extern "C" int rs_peer_alloc(int64_t bytes, void** ptr) {
