@@ -1467,6 +1467,9 @@ def bench_din(args, world, rank, nested=False):
         model(pool[i % 8], check_ids=False)
 
     dt2, _ = _timed_graph(full, n2, args.warmup, world, chunk=8)
+    model.fused_call = False  # the two-launch DIN.call, for comparison
+    dt2b, _ = _timed_graph(full, n2, args.warmup, world, chunk=8)
+    model.fused_call = True
     cpu = None
     if args.cpu_baseline and rank == 0:
         from oracle import ctr_oracle as O
@@ -1524,11 +1527,13 @@ def bench_din(args, world, rank, nested=False):
                  {"materialised_keys_path": {"samples_per_s": args.steps * B / dt_old,
                                              "ms_per_step": dt_old / args.steps * 1e3},
                   "din_forward": {"samples_per_s": n2 * B / dt2, "ms_per_step": dt2 / n2 * 1e3,
-                                  "note": "graph-replayed full DIN.call (id checks off), two launches: the "
-                                          "attention from ids with the candidate rows "
-                                          "(rs_din_attention_ids_cand_fwd), then BN + PReLU MLP + sigmoid head "
-                                          "reading the other sparse rows and the dense features straight into "
-                                          "its input tile (rs_mlp_affine_pieces_fwd)"},
+                                  "two_launch_ms_per_step": dt2b / n2 * 1e3,
+                                  "note": "graph-replayed full DIN.call (id checks off) as ONE launch "
+                                          "(rs_din_forward_ids: the attention from ids, then BN + PReLU MLP + "
+                                          "sigmoid head in the same workgroups, the other sparse rows and the "
+                                          "dense features read into the tower tile); two_launch = the attention "
+                                          "with the candidate rows (rs_din_attention_ids_cand_fwd), then the "
+                                          "tower reading the pieces (rs_mlp_affine_pieces_fwd), bit-identical"},
                   "train_step": {"samples_per_s": nt * B / tdt, "ms_per_step": tdt / nt * 1e3,
                                  "timing": ttiming,
                                  "note": "DIN.train_step: gathers, attention Dense+PReLU layers over [B*T] rows, "

@@ -447,6 +447,32 @@ int rs_din_attention_ids_cand_fwd(const void* hist, int id_kind,
                                   int64_t batch, int* err_flag,
                                   rs_stream_t stream);
 
+/* DIN.call (model/din.py:56-95) in ONE launch: the attention unit of
+ * rs_din_attention_ids_cand_fwd, then BatchNormalization (in_scale / in_shift,
+ * as rs_mlp_affine_fwd) + the PReLU tower + Dense(1, sigmoid) of
+ * rs_mlp_affine_pieces_fwd over the input [pooled (k) | cand rows (k) |
+ * pieces] — the pieces must cover columns 2k .. dims[0]-1 (in_cols >= 2k) —
+ * writing y [B] (rows y_stride apart).  Bit-identical to those two launches.
+ * pooled (optional, rows pooled_stride apart) also receives the attention
+ * output.  rs_din_forward_ids_supported: 1 when the shape takes the fused
+ * launch (the reference's (80, 40) attention, a 256-unit first layer and the
+ * 128 -> 64 -> 1 tail, dims[0] <= 64), else 0 (the caller keeps two launches).
+ * Replaces DIN.call's attention + concat + bn + dense_layer + out_layer. */
+int rs_din_forward_ids_supported(int T, int k, int H1, int H2, int n_layers,
+                                 const int* dims);
+int rs_din_forward_ids(const void* hist, int id_kind, int64_t hist_stride,
+                       const void* cand, int64_t cand_stride, int T, int k,
+                       const float* table, int64_t vocab, int H1, int H2,
+                       const float* att_prepared, float* pooled,
+                       int64_t pooled_stride, const float* in_scale,
+                       const float* in_shift, int n_layers, const int* dims,
+                       const int* acts, const float* tower_prepared, float* y,
+                       int64_t y_stride, int n_pieces, const int* widths,
+                       const int* in_cols, const int* kinds,
+                       const void* const* srcs, const int64_t* src_strides,
+                       const float* const* tables, const int64_t* vocabs,
+                       int64_t batch, int* err_flag, rs_stream_t stream);
+
 /* ------------------------------------------------ concat pieces (a15, a3)
  * One launch for the concat pieces that live in different tables: piece p
  * writes widths[p] columns of out [B, *] (rows out_stride floats apart)

@@ -71,6 +71,9 @@ SIGNATURES = {
     "rs_din_prepare": (I, [P, P, P, I, P, P, P, I, P, P, I, I, P, P]),
     "rs_din_attention_ids_fwd": (I, [P, I, L, P, L, I, I, P, L, I, I, P, P, P, L, L, P, P]),
     "rs_din_attention_ids_cand_fwd": (I, [P, I, L, P, L, I, I, P, L, I, I, P, P, P, L, P, L, L, P, P]),
+    "rs_din_forward_ids_supported": (I, [I, I, I, I, I, P]),
+    "rs_din_forward_ids": (I, [P, I, L, P, L, I, I, P, L, I, I, P, P, L, P, P, I, P, P, P, P, L, I, P, P, P, P, P,
+                               P, P, L, P, P]),
     "rs_dense_fwd": (I, [P, L, P, P, P, I, P, L, L, I, I, P]),
     "rs_dense_prelu_rows_fwd": (I, [P, L, P, P, P, I, P, L, L, I, I, P]),
     "rs_din_attention_gen_workspace_size": (L, [L, I, I, I, P]),

@@ -24,6 +24,8 @@
 //    layer 2's B operand in registers (k order permuted to match).
 //  * din_pool: one wave per sample — masked softmax over the T scores and
 //    the weighted sum of the value rows (gathered through the ids again).
+#include "concat.hpp"
+#include "mlp_tower.hpp"
 #include "rs_common.hpp"
 
 namespace rs {
@@ -463,8 +465,24 @@ __host__ __device__ inline DfLayout df_layout(int NTT, int HT1, int HT2, int KS)
 // NTTC > 0: the position-tile count known at compile time (config 4: T =
 // 100 -> 7 tiles): the (sample, tile) item codes, the live-tile scan and the
 // merge loops fold to constants instead of run-time division / loop control
-template <int KS, int HT1, int HT2, int KIND, int NTTC = 0>
-__global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
+// TW (rs_din_forward_ids: DIN.call from the attention to the logit in ONE
+// launch): after the merge the workgroup's tower input rows [pooled | cand |
+// pieces] (model/din.py:84-85) are staged in LDS — BatchNormalization's affine
+// applied as rs_mlp_affine_pieces_fwd stages it, the pieces' ids and rows
+// requested at kernel start — over the dead alpha images, and the PReLU tower
+// + Dense(1, sigmoid) runs on the 16-row MFMA tile (rows >= the workgroup's
+// samples are zero and never stored) with the DIN tower's own code
+// (mlp_layer0_tiles + mlp_tail_run): every valid row's arithmetic is the
+// separate tower launch's, so the logits are bit-identical to
+// rs_din_attention_ids_cand_fwd + rs_mlp_affine_pieces_fwd.
+struct DinTower {
+  MlpArgs t;       // the tower (y, head = 0, M = batch)
+  ConcatArgs pc;   // the pieces at tower columns >= 2k
+  int tbase;       // floats: the tower's LDS region in the dynamic LDS (0: over the alpha images)
+};
+
+template <int KS, int HT1, int HT2, int KIND, int NTTC, bool TW>
+__device__ __forceinline__ void din_fused_body(const DinArgs& a, const DinTower* tw) {
   typedef Ids<KIND> I;
   constexpr int K = 4 * KS;
   const DinGeom& g = a.g;
@@ -504,15 +522,57 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
     if (lane + 64 < T) h1 = I::load(a.hist, b * a.hist_stride + lane + 64);
     c0 = I::load(a.cand, b * a.cand_stride);
   }
+  // TW: lane c of wave s < nsmp holds tower input column c of sample s; a
+  // piece column's raw id (or dense value) is requested now, its row after
+  // the ids reach LDS
+  int tp = -1;
+  int64_t traw = 0;
+  float tval = 0.f;
+  if constexpr (TW) {
+    const ConcatArgs& pc = tw->pc;
+    if (w < nsmp && lane >= 2 * K && lane < tw->t.K0) {
+      for (int q = 0; q < pc.np; ++q)
+        if (lane >= pc.out_col[q] && lane < pc.out_col[q] + (pc.col0[q + 1] - pc.col0[q])) tp = q;
+      if (tp >= 0) {
+        const int64_t off = (s0 + w) * pc.src_stride[tp];
+        switch (pc.kind[tp]) {
+          case RS_ID_I32: traw = static_cast<const int32_t*>(pc.src[tp])[off]; break;
+          case RS_ID_I64: traw = static_cast<const int64_t*>(pc.src[tp])[off]; break;
+          case RS_ID_F32: traw = (int64_t)__float_as_uint(static_cast<const float*>(pc.src[tp])[off]); break;
+          default: tval = static_cast<const float*>(pc.src[tp])[off + (lane - pc.out_col[tp])]; break;
+        }
+      }
+    }
+  }
+  bool tbad = false;
   auto ids_to_lds = [&]() {
     if (w < nsmp) {
       hs[w][lane] = h0;
       hs[w][lane + 64] = h1;
       if (lane == 0) cs[w] = c0;
-      if (a.cand_out) {  // the candidate row for the caller's concat, written at the merge
+      if (TW || a.cand_out) {  // the candidate row for the caller's concat, written at the merge
         int64_t cid;
         const bool ok = I::decode(c0, a.vocab, cid);
-        cq = ok && lane < K ? a.table[cid * K + lane] : 0.f;
+        const int cl = TW ? lane - K : lane;  // TW: lanes K..2K-1 hold the tower's cand columns
+        cq = ok && cl >= 0 && cl < K ? a.table[cid * K + cl] : 0.f;
+      }
+      if constexpr (TW) {  // the piece's row (its id arrived with the history ids)
+        const ConcatArgs& pc = tw->pc;
+        if (tp >= 0 && pc.kind[tp] >= 0) {
+          int64_t id = 0;
+          bool ok;
+          if (pc.kind[tp] == RS_ID_F32) {
+            const float f = __uint_as_float((unsigned)traw);
+            ok = f > -1.0f && static_cast<double>(f) < static_cast<double>(pc.vocab[tp]);
+            id = ok ? static_cast<int64_t>(f) : 0;
+          } else {
+            id = traw;
+            ok = id >= 0 && id < pc.vocab[tp];
+          }
+          tbad = !ok;
+          const int kw = pc.col0[tp + 1] - pc.col0[tp];
+          tval = ok ? pc.table[tp][id * kw + (lane - pc.out_col[tp])] : 0.f;
+        }
       }
       const uint64_t l0 = __ballot(lane < T && static_cast<float>(h0) != 0.f);  // din.py: mask = hist != 0
       const uint64_t l1 = __ballot(lane + 64 < T && static_cast<float>(h1) != 0.f);
@@ -716,7 +776,31 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
   }
   if (__any(bad) && lane == 0) flag_error(a.err);
   __syncthreads();
+  floatx4 ring[MLP_R];
+  // TW: the tower's buf0 | buf1 | red | par — over the alpha / weight images
+  // (dead now) when they fit below the partials the merge reads, else past them
+  float* tsm = TW ? dsm + tw->tbase : dsm;
+  if constexpr (TW) {
+    const MlpArgs& t = tw->t;
+    if (__any(tbad) && lane == 0) flag_error(tw->pc.err);
+    mlp_first_fill<DF_NW>(t, ring);  // layer 0's weights under the merge
+    float* par = tsm + 32 * t.rs + DF_NW * 256;
+    for (int i = threadIdx.x; i < t.ptot; i += DF_NW * 64) par[i] = t.prep[t.wtot + i];
+  }
   // merge the tiles of sample w (one wave per sample, lane c < k = channel)
+  if (TW && w < 16) {
+    // tower input row w: [pooled (merge below) | cand | pieces | 0 padding];
+    // rows >= nsmp are zero
+    const MlpArgs& t = tw->t;
+    float v = 0.f;
+    if (w < nsmp && lane >= K && lane < t.K0) v = lane < 2 * K ? cq : tval;
+    if (w < nsmp && lane >= K && lane < t.K0) {
+#pragma clang fp contract(off)  // two roundings, as rs_affine_act (no fma)
+      v = v * t.in_scale[lane] + t.in_shift[lane];
+    }
+    if (lane >= K || w >= nsmp)
+      if (lane < t.Kp[0]) tsm[w * t.rs + lane] = v;
+  }
   if (w < nsmp && lane < K) {
     const float* pp = part + (size_t)w * NTT * (2 + DF_MAXK);
     const unsigned mk = tmask[w];  // live tiles only (the others would add exact zeros)
@@ -730,10 +814,38 @@ __global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
       l = fmaf(pp[jj * (2 + DF_MAXK) + 1], sj, l);
       o = fmaf(pp[jj * (2 + DF_MAXK) + 2 + lane], sj, o);
     }
-    a.out[(s0 + w) * a.ldo + lane] = o / l;
-    if (a.cand_out) a.cand_out[(s0 + w) * a.ldc + lane] = cq;
+    const float pooled = o / l;
+    if constexpr (TW) {
+      const MlpArgs& t = tw->t;
+      float v;
+      {
+#pragma clang fp contract(off)  // two roundings, as rs_affine_act (no fma)
+        v = pooled * t.in_scale[lane] + t.in_shift[lane];
+      }
+      tsm[w * t.rs + lane] = v;
+      if (a.out) a.out[(s0 + w) * a.ldo + lane] = pooled;
+    } else {
+      a.out[(s0 + w) * a.ldo + lane] = pooled;
+      if (a.cand_out) a.cand_out[(s0 + w) * a.ldc + lane] = cq;
+    }
   }
   DF_STAMP(7);
+  if constexpr (TW) {
+    // rows s0 .. s0 + nsmp - 1 are this workgroup's (M: the others are never stored)
+    MlpArgs t = tw->t;
+    t.M = s0 + nsmp;
+    mlp_layer0_tiles<DF_NW>(t, tsm, ring);
+    mlp_tail_run<DF_NW>(t, tsm, s0, nullptr);
+  }
+}
+
+template <int KS, int HT1, int HT2, int KIND, int NTTC = 0>
+__global__ __launch_bounds__(DF_NW * 64) void din_fused(DinArgs a) {
+  din_fused_body<KS, HT1, HT2, KIND, NTTC, false>(a, nullptr);
+}
+template <int KS, int HT1, int HT2, int KIND, int NTTC = 0>
+__global__ __launch_bounds__(DF_NW * 64) void din_fused_tower(DinArgs a, DinTower tw) {
+  din_fused_body<KS, HT1, HT2, KIND, NTTC, true>(a, &tw);
 }
 
 template <int KS, int HT1M, int HT2M, int KIND, bool EXACT>
@@ -851,4 +963,106 @@ extern "C" int rs_din_attention_ids_cand_fwd(const void* hist, int id_kind, int6
   RS_REQUIRE(batch == 0 || cand_out, "rs_din_attention_ids_cand_fwd: null cand_out");
   return din_ids_run(hist, id_kind, hist_stride, cand, cand_stride, T, k, table, vocab, H1, H2, prepared, scores,
                      out, out_stride, cand_out, cand_out_stride, batch, err_flag, stream);
+}
+
+// ---- DIN.call in ONE launch (din_fused_tower): the attention unit from the
+// behaviour ids, then BatchNormalization + the PReLU tower + Dense(1,
+// sigmoid) over [pooled | cand | pieces] (model/din.py:56-95) — the
+// two-launch path is rs_din_attention_ids_cand_fwd + rs_mlp_affine_pieces_fwd.
+namespace rs {
+// the shapes the fused launch takes (else the caller keeps the two launches);
+// tbase / lds: where the tower's LDS region starts (floats) and the launch's
+// dynamic LDS bytes
+static bool din_tower_ok(const DinGeom& g, int n_layers, const int* dims, MlpGeom& mg, int& tbase, size_t& lds) {
+  if (opt(RS_OPT_DIN_KERNEL) != 0 || g.HT1 != 5 || g.HT2 != 3 || !df_lds(g)) return false;
+  if (!mlp_geom(n_layers, dims, mg) || dims[0] > 64 || dims[0] < 2 * g.k || mg.Np[0] != DF_NW * 16) return false;
+  int gwa = 0, gwb = 0;
+  if (!mlp_tail_ok(mg.Np, mg.Kp, mg.N, mg.L, 1, gwa, gwb) || gwa != 8 || gwb != 2) return false;
+  // the tower's LDS (buf0 | buf1 | red | par) lies over the alpha / weight
+  // images when it fits below the online-softmax partials the merge still
+  // reads (config 4), else after everything (short histories)
+  const DfLayout L = df_layout(g.NTT, g.HT1, g.HT2, g.KS);
+  const int tfl = 32 * mg.rs + DF_NW * 256 + mg.ptot;
+  tbase = tfl <= L.part ? 0 : L.total;
+  lds = std::max(df_lds(g), (size_t)(tbase + tfl) * sizeof(float));
+  return lds + 1024 + DF_SPW * (DF_TMAX + 2) * 8 <= 160 * 1024;
+}
+
+template <int KS, int KIND>
+static void launch_din_tower(const DinArgs& a, const DinTower& tw, size_t lds, hipStream_t st) {
+  const unsigned grid = (unsigned)((a.batch + DF_SPW - 1) / DF_SPW);
+  if (KS == 2 && a.g.NTT == 7) {  // config 4 (k 8, T 97..112)
+    static LdsAttr set7;
+    lds_attr(set7, (const void*)din_fused_tower<KS, 5, 3, KIND, 7>, lds);
+    din_fused_tower<KS, 5, 3, KIND, 7><<<grid, DF_NW * 64, lds, st>>>(a, tw);
+    return;
+  }
+  static LdsAttr set;
+  lds_attr(set, (const void*)din_fused_tower<KS, 5, 3, KIND>, lds);
+  din_fused_tower<KS, 5, 3, KIND><<<grid, DF_NW * 64, lds, st>>>(a, tw);
+}
+}  // namespace rs
+
+extern "C" int rs_din_forward_ids_supported(int T, int k, int H1, int H2, int n_layers, const int* dims) {
+  if (rs_din_prepared_size(T, k, H1, H2) <= 0 || T > ATT_POOL_TMAX || !dims) return 0;
+  MlpGeom mg;
+  int tbase = 0;
+  size_t lds = 0;
+  return din_tower_ok(din_geom(T, k, H1, H2), n_layers, dims, mg, tbase, lds) ? 1 : 0;
+}
+
+extern "C" int rs_din_forward_ids(const void* hist, int id_kind, int64_t hist_stride, const void* cand,
+                                  int64_t cand_stride, int T, int k, const float* table, int64_t vocab, int H1,
+                                  int H2, const float* att_prepared, float* pooled, int64_t pooled_stride,
+                                  const float* in_scale, const float* in_shift, int n_layers, const int* dims,
+                                  const int* acts, const float* tower_prepared, float* y, int64_t y_stride,
+                                  int n_pieces, const int* widths, const int* in_cols, const int* kinds,
+                                  const void* const* srcs, const int64_t* src_strides, const float* const* tables,
+                                  const int64_t* vocabs, int64_t batch, int* err_flag, rs_stream_t stream) {
+  if (batch == 0) return RS_OK;  // empty batch: nothing to launch (null data pointers allowed)
+  RS_REQUIRE(rs_din_prepared_size(T, k, H1, H2) > 0, "rs_din_forward_ids: need k in {4,8,16}, H1 <= 128, H2 <= 64");
+  RS_REQUIRE(hist && cand && table && att_prepared && tower_prepared && y && acts && in_scale && in_shift &&
+                 err_flag,
+             "rs_din_forward_ids: null pointer");
+  RS_REQUIRE(T <= ATT_POOL_TMAX && vocab < (1ll << 31), "rs_din_forward_ids: T > %d or vocab >= 2^31", ATT_POOL_TMAX);
+  RS_REQUIRE(id_kind >= RS_ID_I32 && id_kind <= RS_ID_F32 && vocab >= 1 && batch >= 0 && hist_stride >= T,
+             "rs_din_forward_ids: bad ids / shape");
+  RS_REQUIRE((uintptr_t)table % 16 == 0, "rs_din_forward_ids: table must be 16-B aligned");
+  RS_REQUIRE(!pooled || pooled_stride >= k, "rs_din_forward_ids: pooled_stride < k");
+  const DinGeom g = din_geom(T, k, H1, H2);
+  MlpGeom mg;
+  int tbase = 0;
+  size_t lds = 0;
+  RS_REQUIRE(n_layers >= 1 && dims && din_tower_ok(g, n_layers, dims, mg, tbase, lds),
+             "rs_din_forward_ids: shape not supported by the fused launch (rs_din_forward_ids_supported)");
+  RS_REQUIRE(dims[n_layers] == 1 && y_stride >= 1, "rs_din_forward_ids: the tower must end in one unit");
+  DinTower tw{};
+  int st = concat_fill(n_pieces, widths, in_cols, kinds, srcs, src_strides, tables, vocabs, dims[0],
+                       "rs_din_forward_ids", tw.pc);
+  if (st != RS_OK) return st;
+  for (int p = 0; p < n_pieces; ++p)
+    RS_REQUIRE(in_cols[p] >= 2 * k, "rs_din_forward_ids: piece %d overlaps the pooled / candidate columns", p);
+  RS_REQUIRE(tw.pc.ncol == dims[0] - 2 * k, "rs_din_forward_ids: the pieces must cover columns 2k .. %d", dims[0] - 1);
+  tw.pc.err = err_flag;
+  tw.tbase = tbase;
+  RS_REQUIRE(mlp_fill_args(mg, acts, tower_prepared, tw.t), "rs_din_forward_ids: bad activation");
+  tw.t.y = y;
+  tw.t.ys = y_stride;
+  tw.t.head = 0;  // the output Dense(1, sigmoid) is the tower's last layer
+  tw.t.c0 = 1.f;
+  tw.t.c1 = 1.f;
+  tw.t.M = batch;
+  tw.t.dbg = mlp_diag_dbg();
+  tw.t.in_scale = in_scale;
+  tw.t.in_shift = in_shift;
+  DinArgs a{hist, hist_stride, cand, cand_stride, table, vocab, att_prepared, g,
+            0, nullptr, pooled, pooled_stride, batch, err_flag, g_din_dbg, nullptr, 0};
+  hipStream_t hs = as_stream(stream);
+  with_id_kind(id_kind, [&](auto K) {
+    constexpr int KIND = decltype(K)::value;
+    if (k == 4) launch_din_tower<1, KIND>(a, tw, lds, hs);
+    else if (k == 8) launch_din_tower<2, KIND>(a, tw, lds, hs);
+    else launch_din_tower<4, KIND>(a, tw, lds, hs);
+  });
+  return launch_status("rs_din_forward_ids");
 }

@@ -839,6 +839,10 @@ class DIN(TowerMixin, KerasModule):
         emb = torch.empty(B, width, dtype=torch.float32, device=dev)
         if self.att_layer.out_kernel is None:
             self.att_layer.build(T, K)
+        if nb == 1 and self.att_layer.ids_ok(K) and self.fused_call:
+            y = self._forward_one_launch(inputs, hists[0], cand, K, width, check_ids)
+            if y is not None:
+                return y
         if nb == 1 and self.att_layer.ids_ok(K):
             # keys/values read through the ids from the (L2-resident) table; the
             # pooled rows and the candidate rows go straight into emb, in the
@@ -875,6 +879,48 @@ class DIN(TowerMixin, KerasModule):
         for layer in self.dense_layer:
             x = layer(x)
         return self.out_layer(x)
+
+    # DIN.call from the ids to the logit as ONE launch (rs_din_forward_ids:
+    # the attention unit, then bn + the PReLU tower + Dense(1, sigmoid) in the
+    # same workgroups; bit-identical to the two launches below, which stay the
+    # path for shapes it does not take and for fused_call = False)
+    fused_call = True
+
+    def _forward_one_launch(self, inputs, hist, cand, K, width, check_ids):
+        if self.out_layer.kernel is None or not self.tower_ok() or not self.pieces_in_tower or width > 64:
+            return None
+        B, T = hist.shape
+        pieces = self._rest_pieces(inputs, 2 * K, B)
+        if not 0 < len(pieces) <= 16:
+            return None
+        att = self.att_layer
+        if att.out_kernel is None:
+            att.build(T, K)
+        h1, h2 = att.hidden_units
+        ls = self._layers()
+        n = len(ls)
+        dims = self._dims()
+        cdims = (C.c_int * (n + 1))(*dims)
+        if T != att.T or not _lib.lib().rs_din_forward_ids_supported(T, K, h1, h2, n, cdims):
+            return None
+        if self.bn_layer.gamma is None:
+            self.bn_layer.build(width)
+        sc, sh = self.bn_layer.affine()
+        seq_layer = self.embed_seq_layers[0]
+        y = torch.empty(B, 1, dtype=torch.float32, device=self._dev)
+        k = len(pieces)
+        arr = lambda ctype, vals: (ctype * k)(*vals)
+        call("rs_din_forward_ids", ptr(hist), _lib.id_kind(hist), hist.stride(0), ptr(cand), cand.stride(0), T, K,
+             ptr(seq_layer.table), int(seq_layer.vocab_sizes[0]), h1, h2, ptr(att.prepared_ids(K)), None, 0,
+             ptr(sc), ptr(sh), n, cdims, (C.c_int * n)(*[_lib.ACT[l.activation] for l in ls]),
+             ptr(self.prepared()), ptr(y), y.stride(0), k, arr(C.c_int, [p[0] for p in pieces]),
+             arr(C.c_int, [p[1] for p in pieces]), arr(C.c_int, [p[2] for p in pieces]),
+             arr(C.c_void_p, [ptr(p[3]) for p in pieces]), arr(C.c_int64, [p[3].stride(0) for p in pieces]),
+             arr(C.c_void_p, [ptr(p[4]) if p[4] is not None else None for p in pieces]),
+             arr(C.c_int64, [p[5] for p in pieces]), B, ptr(self._err.t), _lib.stream())
+        if check_ids:
+            self._err.check("DIN")
+        return y
 
     # DIN.call's tower reads the other sparse embeddings and the dense
     # features itself (rs_mlp_affine_pieces_fwd); False: one rs_concat_pieces

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--compare", default=None, help="compare the first value's outputs with a saved .pt")
     ap.add_argument("--hist", default="pad80", choices=["pad80", "random", "full"],
                     help="din: history padding (from position 80 / random lengths 1..T as bench.py / none)")
+    ap.add_argument("--vocab-all", action="store_true", help="use --vocab for every workload (default: embed_fm only)")
     ap.add_argument("--lib", default=None, help="another build of librs_hip.so (build A/B: one process per build)")
     args = ap.parse_args()
     import recommender_system_amd as rs
@@ -48,7 +49,7 @@ def main():
 
     dev = torch.device("cuda")
     B, F, k, nd = args.batch, 26, 16, 13
-    V = int(args.vocab) if args.workload == "embed_fm" else int(1e6)
+    V = int(args.vocab) if args.workload == "embed_fm" or args.vocab_all else int(1e6)
     cols = [[{"feat": f"I{i + 1}"} for i in range(nd)],
             [{"feat": f"C{i + 1}", "feat_onehot_dim": V, "embed_dim": k} for i in range(F)]]
     g = torch.Generator(device=dev)

@@ -9,6 +9,8 @@ moving statistics, random PReLU / Dice parameters; dnn_activation 'prelu' and
 'dice'; two behaviour features (item + category ids concatenated along k,
 model/din.py:73,77-79); attention depths other than the reference's two
 hidden layers.  Post-sigmoid outputs at 1e-5 relative."""
+import ctypes as ct
+
 import numpy as np
 import pytest
 import torch
@@ -172,6 +174,39 @@ def test_din_tower_reads_pieces(gpu, nb, B, T):
     model.pieces_in_tower = False
     y0 = model(inputs)
     assert torch.equal(y1, y0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,B,T,idt", [(8, 2048, 100, np.int64), (8, 1003, 100, np.int32), (4, 37, 20, np.int64),
+                                       (16, 203, 128, np.int32), (8, 5, 7, np.float32)])
+def test_din_one_launch_matches_two(gpu, k, B, T, idt):
+    """DIN.call as ONE launch (rs_din_forward_ids: the attention unit, then bn
+    + the PReLU tower + Dense(1, sigmoid) in the same workgroups, 8 samples
+    each on a 16-row tile) == the attention launch + the tower launch, bit for
+    bit: ragged batches, k 4 / 8 / 16, 1..8 position tiles, int32 / int64 /
+    float ids; and an out-of-range id of a piece (the user_id embedding read
+    inside the tower staging) raises."""
+    from recommender_system_amd import DIN, _lib
+    rng = np.random.default_rng(B + k)
+    cols, behaviour = din_columns(1, k)
+    model = DIN(cols, behaviour, seed=5)
+    inputs = din_inputs(rng, cols, behaviour, B, T)
+    model(inputs)
+    randomize(model, rng)
+    inputs = {f: (v.astype(idt) if f != "price" else v) for f, v in inputs.items()}
+    dims = model._dims()
+    assert _lib.lib().rs_din_forward_ids_supported(T, k, 80, 40, len(dims) - 1, (ct.c_int * len(dims))(*dims)) == 1
+    y1 = model(inputs)
+    model.fused_call = False
+    y0 = model(inputs)
+    assert torch.equal(y1, y0)
+    model.fused_call = True
+    bad = dict(inputs)
+    bad["user_id"] = inputs["user_id"].copy()
+    bad["user_id"][B // 2] = 192404
+    with pytest.raises(IndexError):
+        model(bad)
+    assert torch.equal(model(inputs), y1)  # the flag was cleared by the raise
 
 
 def test_oracle_din_two_behaviours_is_concat():
