@@ -527,9 +527,18 @@ __device__ __forceinline__ void din_fused_body(const DinArgs& a, const DinTower*
   // the ids reach LDS
   int tp = -1;
   int64_t traw = 0;
-  float tval = 0.f;
+  float tval = 0.f, tpar = 0.f, tsc = 0.f, tsh = 0.f;
   if constexpr (TW) {
     const ConcatArgs& pc = tw->pc;
+    // the BatchNormalization affine of this lane's tower column (read at the merge)
+    if (lane < tw->t.K0) {
+      tsc = tw->t.in_scale[lane];
+      tsh = tw->t.in_shift[lane];
+    }
+    // the tower's bias / alpha block (its first 1024 floats; the DIN tower's
+    // is 928): requested now, stored to LDS after the items — its trip stays
+    // off the merge
+    if (threadIdx.x < (unsigned)tw->t.ptot) tpar = tw->t.prep[tw->t.wtot + threadIdx.x];
     if (w < nsmp && lane >= 2 * K && lane < tw->t.K0) {
       for (int q = 0; q < pc.np; ++q)
         if (lane >= pc.out_col[q] && lane < pc.out_col[q] + (pc.col0[q + 1] - pc.col0[q])) tp = q;
@@ -777,6 +786,8 @@ __device__ __forceinline__ void din_fused_body(const DinArgs& a, const DinTower*
   if (__any(bad) && lane == 0) flag_error(a.err);
   __syncthreads();
   floatx4 ring[MLP_R];
+  floatx4 wa[8];
+  const bool tspec = TW && tw->t.Np[1] == 128 && tw->t.Np[2] == 64;  // mlp_tail_run's specialised widths
   // TW: the tower's buf0 | buf1 | red | par — over the alpha / weight images
   // (dead now) when they fit below the partials the merge reads, else past them
   float* tsm = TW ? dsm + tw->tbase : dsm;
@@ -784,8 +795,13 @@ __device__ __forceinline__ void din_fused_body(const DinArgs& a, const DinTower*
     const MlpArgs& t = tw->t;
     if (__any(tbad) && lane == 0) flag_error(tw->pc.err);
     mlp_first_fill<DF_NW>(t, ring);  // layer 0's weights under the merge
+    // ... and layer 1's slice of this wave (its 128 KB per workgroup through
+    // the CU's L2 port would otherwise sit between layer 0 and layer 1)
+    if (tspec) mlp_tail_fetch<8, 8>(t, 1, wa);
+    else mlp_tail_fetch<8>(t, 1, wa);
     float* par = tsm + 32 * t.rs + DF_NW * 256;
-    for (int i = threadIdx.x; i < t.ptot; i += DF_NW * 64) par[i] = t.prep[t.wtot + i];
+    if (threadIdx.x < (unsigned)t.ptot) par[threadIdx.x] = tpar;
+    for (int i = threadIdx.x + DF_NW * 64; i < t.ptot; i += DF_NW * 64) par[i] = t.prep[t.wtot + i];
   }
   // merge the tiles of sample w (one wave per sample, lane c < k = channel)
   if (TW && w < 16) {
@@ -796,7 +812,7 @@ __device__ __forceinline__ void din_fused_body(const DinArgs& a, const DinTower*
     if (w < nsmp && lane >= K && lane < t.K0) v = lane < 2 * K ? cq : tval;
     if (w < nsmp && lane >= K && lane < t.K0) {
 #pragma clang fp contract(off)  // two roundings, as rs_affine_act (no fma)
-      v = v * t.in_scale[lane] + t.in_shift[lane];
+      v = v * tsc + tsh;
     }
     if (lane >= K || w >= nsmp)
       if (lane < t.Kp[0]) tsm[w * t.rs + lane] = v;
@@ -820,7 +836,7 @@ __device__ __forceinline__ void din_fused_body(const DinArgs& a, const DinTower*
       float v;
       {
 #pragma clang fp contract(off)  // two roundings, as rs_affine_act (no fma)
-        v = pooled * t.in_scale[lane] + t.in_shift[lane];
+        v = pooled * tsc + tsh;
       }
       tsm[w * t.rs + lane] = v;
       if (a.out) a.out[(s0 + w) * a.ldo + lane] = pooled;
@@ -835,7 +851,8 @@ __device__ __forceinline__ void din_fused_body(const DinArgs& a, const DinTower*
     MlpArgs t = tw->t;
     t.M = s0 + nsmp;
     mlp_layer0_tiles<DF_NW>(t, tsm, ring);
-    mlp_tail_run<DF_NW>(t, tsm, s0, nullptr);
+    if (tspec) mlp_tail_splitk<DF_NW, 8, 2, 8, 4>(t, tsm, s0, wa, nullptr, 1);  // = mlp_tail_run, slice fetched above
+    else mlp_tail_splitk<DF_NW, 8, 2>(t, tsm, s0, wa, nullptr, 1);
   }
 }
 

@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--option", default="embed_fm_kernel", choices=sorted(OPTS))
     ap.add_argument("--values", default="0,1")
     ap.add_argument("--workload", default="deepfm",
-                    choices=["deepfm", "dcn", "cross", "embed_fm", "din", "mlp", "din_tower", "shard_pipe", "peer_gather"])
+                    choices=["deepfm", "dcn", "cross", "embed_fm", "din", "mlp", "din_tower", "shard_pipe", "peer_gather", "din_forward"])
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--vocab", type=float, default=1e7)
     ap.add_argument("--rounds", type=int, default=8)
@@ -85,6 +85,22 @@ def main():
             j, jp, jn = i % NP, (i - 1) % NP, (i + 1) % NP
             sh.pipe_step(prev=(dense[jp], souts[jp]), cur=idsv[j], nxt=(dense[jn], idsv[jn]))
             outs[i % NP] = souts[jp]
+    elif args.workload == "din_forward":  # config 4's DIN.call (random history lengths as bench.py)
+        Bd, T, kd = 2048 if args.batch == 4096 else args.batch, 100, 8
+        B = Bd
+        dcols = [[{"feat": "price"}], [{"feat": "user_id", "feat_onehot_dim": 192404, "embed_dim": kd},
+                                       {"feat": "movies_seq", "feat_onehot_dim": 63001, "embed_dim": kd}]]
+        dm = rs.DIN(dcols, ["movies_seq"], seed=1, device=dev)
+        lens = torch.randint(1, T + 1, (NP, Bd, 1), generator=g, device=dev)
+        hs = torch.randint(1, 63001, (NP, Bd, T), generator=g, device=dev)
+        hs = torch.where(torch.arange(T, device=dev)[None, None, :] < lens, hs, torch.zeros_like(hs))
+        dpool = [{"price": torch.rand(Bd, 1, generator=g, device=dev),
+                  "user_id": torch.randint(0, 192404, (Bd, 1), generator=g, device=dev),
+                  "movies_seq": hs[j], "movie_id": torch.randint(1, 63001, (Bd, 1), generator=g, device=dev)}
+                 for j in range(NP)]
+
+        def fn(i):
+            outs[i % NP] = dm(dpool[i % NP], check_ids=False)
     elif args.workload == "peer_gather":  # config 5's owner row service at world 1: rs_peer_gather_a2a, B x F rows
         import torch.distributed as dist
         from recommender_system_amd.sharded import PeerExchange
