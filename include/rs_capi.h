@@ -95,7 +95,12 @@ enum rs_option {
                                  data stores, relaxed counts, write-through flags, no L2
                                  maintenance; 1 = a system-scope release / acquire fence around
                                  every count and flag.  See DESIGN.md 4.6                        */
-  RS_OPT_COUNT = 5
+  RS_OPT_CROSS_KERNEL = 5,    /* rs_embed_cross_fwd_hm / rs_dcn_fwd_hm (k 16, <= 32 fields, <= 16
+                                 CrossNet B columns): 0
+                                 (the default) = the contraction from the gathered registers as
+                                 the rows land; 1 = the staged-tile contraction after the gather
+                                 (bit-identical to rs_embed_cross_fwd).  See DESIGN.md 4.2       */
+  RS_OPT_COUNT = 6
 };
 
 /* ------------------------------------------- peer-mapped exchange (§8(e))

@@ -188,6 +188,7 @@ OPT_MLP_UNROLL = 1
 OPT_DEEPFM_KERNEL = 2
 OPT_DIN_KERNEL = 3
 OPT_PEER_FENCES = 4
+OPT_CROSS_KERNEL = 5
 ACT = {None: 0, "linear": 0, "relu": 1, "prelu": 2, "sigmoid": 3}
 
 _lock = threading.Lock()

@@ -27,9 +27,9 @@ int launch_status(const char* what) {
 // Per host thread (rs_capi.h): a thread's setting changes only the launches
 // that thread makes, so concurrent callers never see each other's choices.
 // defaults: K-split headline kernel, unrolled towers, split-role DeepFM, one-launch DIN attention,
-// lean peer-exchange ordering
-static thread_local int g_opt[RS_OPT_COUNT] = {0, 1, 0, 0, 0};
-static const int g_opt_hi[RS_OPT_COUNT] = {3, 1, 3, 1, 1};
+// lean peer-exchange ordering, register contraction in embed_cross
+static thread_local int g_opt[RS_OPT_COUNT] = {0, 1, 0, 0, 0, 0};
+static const int g_opt_hi[RS_OPT_COUNT] = {3, 1, 3, 1, 1, 1};
 int opt(int option) { return (option >= 0 && option < RS_OPT_COUNT) ? g_opt[option] : 0; }
 }  // namespace rs
 

@@ -170,17 +170,30 @@ __device__ __forceinline__ void cross_contract(const CrossArgs& a, const float* 
 // Phases (2)-(4) on a staged 16 x d tile of x0 (rows >= `rows` zero).
 // beta: beta_L (a.beta, or its LDS copy when the caller staged one).
 template <int NT, int NW>
+__device__ __forceinline__ void cross_finish(const CrossArgs& a, float* tile, float* cs, float* alpha, int64_t b0,
+                                             int rows, const floatx4 (&acc)[NT], const float* beta);
+
+template <int NT, int NW>
 __device__ __forceinline__ void cross_tile(const CrossArgs& a, float* tile, float* cs, float* alpha, int64_t b0,
                                            int rows, const CrossB<NT, NW>* pre = nullptr,
                                            const float* beta = nullptr) {
+  // (2) G = X0 @ W on MFMA
+  floatx4 acc[NT];
+  cross_contract<NT, NW>(a, tile, a.d, pre, acc);
+  cross_finish<NT, NW>(a, tile, cs, alpha, b0, rows, acc, beta);
+}
+
+// Phases (3)-(4) from each wave's partial G tile `acc` (its share of the
+// contraction): partials to LDS, the recurrence, the output pass.  The tile
+// must be complete in LDS by the barrier below.
+template <int NT, int NW>
+__device__ __forceinline__ void cross_finish(const CrossArgs& a, float* tile, float* cs, float* alpha, int64_t b0,
+                                             int rows, const floatx4 (&acc)[NT], const float* beta) {
   if (!beta) beta = a.beta;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int s = lane & 15, kk = lane >> 4;
   const int n = rows * a.d;
-  // (2) G = X0 @ W on MFMA
-  floatx4 acc[NT];
-  cross_contract<NT, NW>(a, tile, a.d, pre, acc);
   constexpr int CW = NT * 16 + 1;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
@@ -302,7 +315,94 @@ constexpr int EC_FMAX = 128;
 // KA: the field metadata by value (rs_embed_cross_fwd_hm, k = 16, <= 32
 // fields): the headline kernel's front end (tile_gather.hpp) instead of the
 // cooperative id tile.
-template <int NT, int KIND, bool KA>
+// The kernarg front end with the CrossNet contraction done from registers
+// (k 16, <= 2 NW fields, <= 16 B columns): wave w gathers fields w and w + NW
+// with lane (s = l & 15, q = l >> 4) loading chunk q of sample s's row — the
+// MFMA A layout, so the float4 is four MFMAs' A operands (k-slot q of columns
+// nd + 16c + 4q + j, j = 0..3) — and contracts them against B fragments read
+// per lane from the prepared image (record col / 4, k-slot col % 4) while
+// storing them into the tile (row pitch ld, columns [dense nd | fields]); wave
+// NW-1-g also contracts dense k-group g (the dense tile columns are the
+// caller's).  Rows in two bursts as the headline kernel: the second
+// requested once the first is in.  Returns the lane's bad-id flag; `acc` =
+// this wave's partial G tile (rows = samples, columns = B columns).
+template <int NW, int KIND>
+__device__ __forceinline__ bool gather_contract_reg(const CrossArgs& a, const EmbedCrossArgs& e, const FieldMeta* km,
+                                                    int64_t b0, int rows, float* tile, int ld, floatx4& acc) {
+  typedef Ids<KIND> I;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int s = lane & 15, q = lane >> 4, F = e.F;
+  const int64_t bb = b0 + (s < rows ? s : rows - 1);
+  const int c0 = w, c1 = w + NW;
+  typename I::raw_t r0{}, r1{};
+  if (c0 < F) r0 = I::load(e.ids, bb * e.id_stride + c0);
+  if (c1 < F) r1 = I::load(e.ids, bb * e.id_stride + c1);
+  auto bimg = [&](int col) -> float { return a.img[(int64_t)(col >> 2) * 64 + (col & 3) * 16 + s]; };
+  float bf0[4] = {0.f, 0.f, 0.f, 0.f}, bf1[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (c0 < F) bf0[j] = bimg(e.nd + 16 * c0 + 4 * q + j);
+    if (c1 < F) bf1[j] = bimg(e.nd + 16 * c1 + 4 * q + j);
+  }
+  floatx4 ac[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ac[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int g = NW - 1 - w; 16 * g < e.nd; g += NW) {  // dense k-groups (nd = 13: wave NW-1 only)
+    float xd[4], bd[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = 16 * g + 4 * q + j;
+      const bool ok = col < e.nd;
+      xd[j] = ok && s < rows ? e.dense[bb * e.dense_stride + col] : 0.f;
+      bd[j] = ok ? bimg(col) : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ac[j] = mfma16x16x4(xd[j], bd[j], ac[j]);
+  }
+  bool bad = false;
+  auto row = [&](int c, typename I::raw_t r) -> floatx4 {
+    int64_t id;
+    const bool ok = I::decode(r, km->voc[c], id);
+    bad |= !ok && s < rows;
+    floatx4 x = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(e.table + (km->off[c] + id) * 16) + q);
+    if (!ok || s >= rows) x = floatx4{0.f, 0.f, 0.f, 0.f};
+    return x;
+  };
+  auto put = [&](int c, floatx4 x) {
+    float* p = tile + s * ld + e.nd + c * 16 + 4 * q;
+    p[0] = x[0];
+    p[1] = x[1];
+    p[2] = x[2];
+    p[3] = x[3];
+  };
+  floatx4 x0v{0.f, 0.f, 0.f, 0.f}, x1v{0.f, 0.f, 0.f, 0.f};
+  if (c0 < F) {
+    x0v = row(c0, r0);
+    put(c0, x0v);
+  }
+  if (c1 < F) x1v = row(c1, r1);
+  if (c0 < F) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ac[j] = mfma16x16x4(x0v[j], bf0[j], ac[j]);
+  }
+  if (c1 < F) {
+    put(c1, x1v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ac[j] = mfma16x16x4(x1v[j], bf1[j], ac[j]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = (ac[0][i] + ac[1][i]) + (ac[2][i] + ac[3][i]);
+  return bad;
+}
+
+// REG (RS_OPT_CROSS_KERNEL 0, the default on the kernarg front end, L <= 16):
+// gather_contract_reg — each wave's partial G tile goes straight to the
+// cross-wave sums: no post-gather tile reads, no contraction phase, one
+// barrier fewer.  G's summation order differs from the staged-tile
+// contraction (REG false: bit-identical to the cooperative-id-tile kernel),
+// so the two forms agree to rounding.
+template <int NT, int KIND, bool KA, bool REG = false>
 __device__ __forceinline__ void embed_cross_body(const CrossArgs& a, const EmbedCrossArgs& e, const FieldMeta* km) {
   constexpr int NW = 16;
   typedef Ids<KIND> I;
@@ -315,7 +415,26 @@ __device__ __forceinline__ void embed_cross_body(const CrossArgs& a, const Embed
   const int64_t b0 = (int64_t)blockIdx.x * 16;
   const int rows = (int)((a.batch - b0) < 16 ? (a.batch - b0) : 16);
   const int F = e.F;
-  if constexpr (KA) {
+  if constexpr (KA && REG) {
+    static_assert(NT == 1, "register contraction: at most 16 cross layers");
+    CR_STAMP(0);
+    float* betal = alpha + 16;
+    const float bv0 = tid < a.d ? a.beta[tid] : 0.f;
+    const float bv1 = tid + NW * 64 < a.d ? a.beta[tid + NW * 64] : 0.f;
+    {  // dense columns into the tile (wave w: sample w)
+      const int64_t bw = b0 + (w < rows ? w : rows - 1);
+      for (int j = lane; j < e.nd; j += 64) tile[w * a.d + j] = w < rows ? e.dense[bw * e.dense_stride + j] : 0.f;
+    }
+    floatx4 acc[1];
+    const bool bad = gather_contract_reg<NW, KIND>(a, e, km, b0, rows, tile, a.d, acc[0]);
+    if (__any(bad) && lane == 0) flag_error(e.err);
+    if (tid < a.d) betal[tid] = bv0;
+    if (tid + NW * 64 < a.d) betal[tid + NW * 64] = bv1;
+    CR_STAMP(1);
+    CR_STAMP(2);
+    cross_finish<1, NW>(a, tile, cs, alpha, b0, rows, acc, a.d <= 2 * NW * 64 ? betal : a.beta);
+    return;
+  } else if constexpr (KA) {
     CR_STAMP(0);
     CrossB<NT, NW> pre;  // the contraction's first B fragments ride the gather's trips
     pre.load(a, w);
@@ -407,9 +526,9 @@ template <int NT, int KIND>
 __global__ __launch_bounds__(16 * 64) void embed_cross(CrossArgs a, EmbedCrossArgs e) {
   embed_cross_body<NT, KIND, false>(a, e, nullptr);
 }
-template <int NT, int KIND>
+template <int NT, int KIND, bool REG = false>
 __global__ __launch_bounds__(16 * 64) void embed_cross_ka(CrossArgs a, EmbedCrossArgs e, FieldMeta m) {
-  embed_cross_body<NT, KIND, true>(a, e, &m);
+  embed_cross_body<NT, KIND, true, REG>(a, e, &m);
 }
 
 // Fused DCN forward (model/dcn.py:24-34) in ONE launch: x0 = [dense |
@@ -419,7 +538,7 @@ __global__ __launch_bounds__(16 * 64) void embed_cross_ka(CrossArgs a, EmbedCros
 // branch's logit is alpha_L (x0.w_o) + beta_L.w_o = alpha_L g_L + h_L, x_L is
 // never formed); the DNN tower on the same tile with its last layer folded
 // with the output Dense's DNN half; head sigmoid(dnn + cross).
-template <int NT, int KIND, bool KA, bool TAIL = false>
+template <int NT, int KIND, bool KA, bool TAIL = false, bool REG = false>
 __device__ __forceinline__ void dcn_fused_body(const CrossArgs& a, const EmbedCrossArgs& e, const MlpArgs& t,
                                                const FieldMeta* km) {
   constexpr int NW = 16;
@@ -440,6 +559,17 @@ __device__ __forceinline__ void dcn_fused_body(const CrossArgs& a, const EmbedCr
   mlp_first_fill<NW>(t, ring);
   float* par = tsm + 32 * RS + NW * 256;
   for (int i = tid; i < t.ptot; i += NW * 64) par[i] = t.prep[t.wtot + i];
+  floatx4 acc[NT];
+  if constexpr (KA && REG) {  // RS_OPT_CROSS_KERNEL 0: the contraction from the gathered registers
+    static_assert(NT == 1, "register contraction: at most 15 cross layers");
+    {  // dense columns + zero padding of the tile row (wave w: sample w)
+      const int64_t bb = b0 + (w < rows ? w : rows - 1);
+      for (int j = lane; j < e.nd; j += 64) tsm[w * RS + j] = w < rows ? e.dense[bb * e.dense_stride + j] : 0.f;
+      for (int j = d + lane; j < t.Kp[0]; j += 64) tsm[w * RS + j] = 0.f;
+    }
+    const bool bad = gather_contract_reg<NW, KIND>(a, e, km, b0, rows, tsm, RS, acc[0]);
+    if (__any(bad) && lane == 0) flag_error(e.err);
+  } else {
   CrossB<NT, NW> pre;  // KA: the contraction's first B fragments ride the gather's trips
   if constexpr (KA) pre.load(a, w);
   if constexpr (KA) {
@@ -514,8 +644,8 @@ __device__ __forceinline__ void dcn_fused_body(const CrossArgs& a, const EmbedCr
   }
 
   // CrossNet contraction G = X0 @ [w_0 .. w_{L-1}, w_o[:d]] (a.L = L + 1 columns)
-  floatx4 acc[NT];
   cross_contract<NT, NW>(a, tsm, RS, KA ? &pre : nullptr, acc);
+  }
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -551,9 +681,9 @@ template <int NT, int KIND>
 __global__ __launch_bounds__(16 * 64) void dcn_fused(CrossArgs a, EmbedCrossArgs e, MlpArgs t) {
   dcn_fused_body<NT, KIND, false>(a, e, t, nullptr);
 }
-template <int NT, int KIND, bool TAIL = false>
+template <int NT, int KIND, bool TAIL = false, bool REG = false>
 __global__ __launch_bounds__(16 * 64) void dcn_fused_ka(CrossArgs a, EmbedCrossArgs e, MlpArgs t, FieldMeta m) {
-  dcn_fused_body<NT, KIND, true, TAIL>(a, e, t, &m);
+  dcn_fused_body<NT, KIND, true, TAIL, REG>(a, e, t, &m);
 }
 
 }  // namespace rs
@@ -649,7 +779,11 @@ static int embed_cross_run(const void* ids, int id_kind, int64_t id_stride, cons
   hipStream_t st = as_stream(stream);
   with_id_kind(id_kind, [&](auto K) {
     constexpr int KIND = decltype(K)::value;
-    if (hm && g.NT == 1) {
+    if (hm && g.NT == 1 && opt(RS_OPT_CROSS_KERNEL) == 0) {
+      static LdsAttr setr;
+      lds_attr(setr, (const void*)embed_cross_ka<1, KIND, true>, lds);
+      embed_cross_ka<1, KIND, true><<<grid, NW * 64, lds, st>>>(a, e, *hm);
+    } else if (hm && g.NT == 1) {
       static LdsAttr setk1;
       lds_attr(setk1, (const void*)embed_cross_ka<1, KIND>, lds);
       embed_cross_ka<1, KIND><<<grid, NW * 64, lds, st>>>(a, e, *hm);
@@ -743,10 +877,22 @@ static int dcn_run(const void* ids, int id_kind, int64_t id_stride, const float*
   with_id_kind(id_kind, [&](auto K) {
     constexpr int KIND = decltype(K)::value;
     int gwa = 0, gwb = 0;
+    const bool reg = opt(RS_OPT_CROSS_KERNEL) == 0;
     if (hm && g.NT == 1 && mlp_tail_ok(t.Np, t.Kp, t.N, t.L, 1, gwa, gwb) && gwa == 8 && gwb == 2) {
-      static LdsAttr setkt;  // the split-K tail at the reference's 256-128-64 tower
-      lds_attr(setkt, (const void*)dcn_fused_ka<1, KIND, true>, lds);
-      dcn_fused_ka<1, KIND, true><<<grid, 16 * 64, lds, st>>>(a, e, t, *hm);
+      // the split-K tail at the reference's 256-128-64 tower
+      if (reg) {
+        static LdsAttr setktr;
+        lds_attr(setktr, (const void*)dcn_fused_ka<1, KIND, true, true>, lds);
+        dcn_fused_ka<1, KIND, true, true><<<grid, 16 * 64, lds, st>>>(a, e, t, *hm);
+      } else {
+        static LdsAttr setkt;
+        lds_attr(setkt, (const void*)dcn_fused_ka<1, KIND, true>, lds);
+        dcn_fused_ka<1, KIND, true><<<grid, 16 * 64, lds, st>>>(a, e, t, *hm);
+      }
+    } else if (hm && g.NT == 1 && reg) {
+      static LdsAttr setk1r;
+      lds_attr(setk1r, (const void*)dcn_fused_ka<1, KIND, false, true>, lds);
+      dcn_fused_ka<1, KIND, false, true><<<grid, 16 * 64, lds, st>>>(a, e, t, *hm);
     } else if (hm && g.NT == 1) {
       static LdsAttr setk1;
       lds_attr(setk1, (const void*)dcn_fused_ka<1, KIND>, lds);

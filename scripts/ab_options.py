@@ -19,7 +19,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-OPTS = {"embed_fm_kernel": 0, "mlp_unroll": 1, "deepfm_kernel": 2, "din_kernel": 3}
+OPTS = {"embed_fm_kernel": 0, "mlp_unroll": 1, "deepfm_kernel": 2, "din_kernel": 3, "cross_kernel": 5}
 
 
 def main():

@@ -586,9 +586,24 @@ def test_deepfm_fused_oor_and_float_ids(gpu):
 
 
 # ------------------------------------------- fused DCN input + CrossNet
+@pytest.mark.parametrize("form", [0, 1])
 @pytest.mark.parametrize("k,L,B,id_dtype", [(16, 3, 4096, np.int32), (8, 2, 37, np.int64), (4, 1, 5, np.int32),
-                                            (16, 20, 100, np.int64), (8, 0, 9, np.int32)])
-def test_embed_cross_fused(gpu, k, L, B, id_dtype):
+                                            (16, 20, 100, np.int64), (8, 0, 9, np.int32), (16, 3, 4093, np.int64),
+                                            (16, 16, 33, np.float32), (16, 1, 1, np.int32)])
+def test_embed_cross_fused(gpu, form, k, L, B, id_dtype):
+    """embed + CrossNet (rs_embed_cross_fwd[_hm]) vs the fp64 oracle; at k 16
+    both RS_OPT_CROSS_KERNEL forms of the kernarg front end (0: contraction
+    from the gathered registers, 1: staged-tile contraction)."""
+    from recommender_system_amd import DCN, _lib
+    from tests.helpers import criteo_columns, tables_of
+    prev = _lib.set_option(_lib.OPT_CROSS_KERNEL, form)
+    try:
+        _embed_cross_case(k, L, B, id_dtype)
+    finally:
+        _lib.set_option(_lib.OPT_CROSS_KERNEL, prev)
+
+
+def _embed_cross_case(k, L, B, id_dtype):
     from recommender_system_amd import DCN
     from tests.helpers import criteo_columns, tables_of
     rng = np.random.default_rng(k * 7 + L)
@@ -754,7 +769,9 @@ def test_pnn_modes_fused(gpu, mode, k, B, id_dtype):
 @pytest.mark.parametrize("k,L,hidden,out_dim,B,id_dtype", [(16, 3, [256, 128, 64], 1, 4096, np.int32),
                                                            (8, 2, [40, 24], 3, 37, np.int64),
                                                            (4, 0, [16], 1, 5, np.int32),
-                                                           (16, 20, [32], 2, 100, np.int64)])
+                                                           (16, 20, [32], 2, 100, np.int64),
+                                                           (16, 3, [48], 1, 333, np.int64),
+                                                           (16, 15, [256, 128, 64], 1, 61, np.float32)])
 def test_dcn_fused(gpu, mlp_unroll, k, L, hidden, out_dim, B, id_dtype):
     """One-launch DCN == the layer-by-layer path == the fp64 oracle."""
     from recommender_system_amd import DCN
@@ -902,18 +919,42 @@ def test_hm_front_end_bit_identical(gpu, F, B, id_dtype):
     d = m.d
     xl = torch.empty(B, d, device=gpu)
     prep = m.cross_layer.prepared(d)
-    a, b = both("rs_embed_cross_fwd", (ids.data_ptr(), kind, ids.stride(0), dense.data_ptr(), 13, 13, e.table.data_ptr(),
-                                       e.field_offsets.data_ptr(), e.field_vocab.data_ptr()),
-                (F, 16, 3, prep.data_ptr(), xl.data_ptr(), d, B, err.data_ptr(), st), xl)
+    cross_args = ((ids.data_ptr(), kind, ids.stride(0), dense.data_ptr(), 13, 13, e.table.data_ptr(),
+                   e.field_offsets.data_ptr(), e.field_vocab.data_ptr()),
+                  (F, 16, 3, prep.data_ptr(), xl.data_ptr(), d, B, err.data_ptr(), st), xl)
+    prev = _lib.set_option(_lib.OPT_CROSS_KERNEL, 1)  # the staged-tile form: bit-identical
+    try:
+        a, b = both("rs_embed_cross_fwd", *cross_args)
+    finally:
+        _lib.set_option(_lib.OPT_CROSS_KERNEL, prev)
     assert torch.equal(a, b) and int(err.item()) == 0
+    _lib.set_option(_lib.OPT_CROSS_KERNEL, 0)  # the register form: the same up to G's summation order
+    try:
+        _, c = both("rs_embed_cross_fwd", *cross_args)
+    finally:
+        _lib.set_option(_lib.OPT_CROSS_KERNEL, prev)
+    assert_scaled_close(c, a.double().cpu().numpy(), rtol=1e-6, what="cross register form vs staged tile")
+    assert int(err.item()) == 0
     cross, mlp, dims, acts, _ = m._fused_params()
     n = len(dims) - 1
     y = torch.empty(B, 1, device=gpu)
-    a, b = both("rs_dcn_fwd", (ids.data_ptr(), kind, ids.stride(0), dense.data_ptr(), 13, 13, e.table.data_ptr(),
-                               e.field_offsets.data_ptr(), e.field_vocab.data_ptr()),
+    dcn_args = ((ids.data_ptr(), kind, ids.stride(0), dense.data_ptr(), 13, 13, e.table.data_ptr(),
+                 e.field_offsets.data_ptr(), e.field_vocab.data_ptr()),
                 (F, 16, 3, cross.data_ptr(), n, (C.c_int * (n + 1))(*dims), (C.c_int * n)(*acts), mlp.data_ptr(),
                  y.data_ptr(), B, err.data_ptr(), st), y)
+    prev = _lib.set_option(_lib.OPT_CROSS_KERNEL, 1)
+    try:
+        a, b = both("rs_dcn_fwd", *dcn_args)
+    finally:
+        _lib.set_option(_lib.OPT_CROSS_KERNEL, prev)
     assert torch.equal(a, b) and int(err.item()) == 0
+    _lib.set_option(_lib.OPT_CROSS_KERNEL, 0)
+    try:
+        _, c = both("rs_dcn_fwd", *dcn_args)
+    finally:
+        _lib.set_option(_lib.OPT_CROSS_KERNEL, prev)
+    assert_scaled_close(c, a.double().cpu().numpy(), rtol=1e-6, what="DCN register form vs staged tile")
+    assert int(err.item()) == 0
     pe = p.embed_layer
     hoff, hvoc = pe.host_meta()
     args_hm = (hoff, hvoc)
