@@ -27,7 +27,8 @@ def main():
     ap.add_argument("--option", default="embed_fm_kernel", choices=sorted(OPTS))
     ap.add_argument("--values", default="0,1")
     ap.add_argument("--workload", default="deepfm",
-                    choices=["deepfm", "dcn", "cross", "embed_fm", "din", "mlp", "din_tower", "shard_pipe", "peer_gather", "din_forward"])
+                    choices=["deepfm", "dcn", "cross", "embed_fm", "din", "mlp", "din_tower", "shard_pipe", "peer_gather", "din_forward",
+                             "gather_rows", "pnn", "embed_x"])
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--vocab", type=float, default=1e7)
     ap.add_argument("--rounds", type=int, default=8)
@@ -114,6 +115,30 @@ def main():
 
         def fn(i):
             outs[i % NP] = ex.gather_all_to_all(idsp[i % NP], nw, table).view(torch.float32)
+    elif args.workload == "gather_rows":  # config 5's owner gather (rs_gather_rows, k 16) on the 1e8-row shard
+        from recommender_system_amd.sharded import ShardedEmbeddingFM  # noqa: F401  (library handle only)
+        from recommender_system_amd._lib import call, ptr
+        V = int(1e8)
+        table = torch.empty(V, k, device=dev).uniform_(-1, 1, generator=g)
+        nw = B * F
+        rowsp = torch.randint(0, V, (NP, nw), generator=g, device=dev, dtype=torch.int32)
+        gouts = [torch.empty(nw, k, device=dev) for _ in range(NP)]
+        errf = torch.zeros(1, dtype=torch.int32, device=dev)
+
+        def fn(i):
+            call("rs_gather_rows", ptr(table), V, k, ptr(rowsp[i % NP]), nw, ptr(gouts[i % NP]), ptr(errf),
+                 _lib.stream())
+            outs[i % NP] = gouts[i % NP]
+    elif args.workload == "pnn":  # PNN's product inputs [flat_emb | inner] (rs_embed_inner_fwd_hm), 26 x 1e6
+        pm = rs.PNN(cols, "inner", [256, 128, 64], 1, embed_dim=k, seed=3, device=dev)
+
+        def fn(i):
+            outs[i % NP] = pm.product_inputs((dense[i % NP], ids[i % NP]), check_ids=False)
+    elif args.workload == "embed_x":  # x = [dense | EmbedLayer(ids)] (rs_embed_gather), 26 x 1e6
+        dm = rs.DeepFM(cols, 10, 1e-4, 1e-4, [256, 128, 64], 1, "relu", embed_dim=k, seed=3, device=dev)
+
+        def fn(i):
+            outs[i % NP] = dm.embed_layer.gather(ids[i % NP], dense[i % NP], check_ids=False)
     elif args.workload == "din_tower":  # DIN's tower shape: PReLU 25 -> 256 -> 128 -> 64 -> 1 at B 2048
         Bt = 2048 if args.batch == 4096 else args.batch
         B = Bt

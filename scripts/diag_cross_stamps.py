@@ -27,6 +27,7 @@ model = rs.DCN(cols, [256, 128, 64], 1, "relu", 3, embed_dim=k, seed=1, device=t
 ids = torch.randint(0, V, (B, F), dtype=torch.int32, device="cuda")
 dense = torch.rand(B, 13, device="cuda")
 lib = _lib.lib()
+_lib.set_option(_lib.OPT_CROSS_KERNEL, int(os.environ.get("RS_CROSS_KERNEL", "0")))  # 0 register / 1 staged tile
 lib.rs_diag_cross_set_dbg.argtypes = [C.c_void_p]
 for _ in range(5):
     model.cross_fused((dense, ids), check_ids=False)
