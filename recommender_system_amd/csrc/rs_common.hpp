@@ -53,7 +53,7 @@ struct Ids {
   typedef typename std::conditional<KIND == 1, int64_t,
                                     typename std::conditional<KIND == 2, float, int32_t>::type>::type raw_t;
   static __device__ __forceinline__ raw_t load(const void* p, int64_t off) {
-    return static_cast<const raw_t*>(p)[off];
+    return static_cast<const raw_t*>(p)[off];  // a non-temporal id load: +0.05 / +0.1 us (profiles/r6_ab_nt_ids_rejected.jsonl)
   }
   static __device__ __forceinline__ bool decode(raw_t r, int64_t vocab, int64_t& id) {
     if constexpr (KIND == 2) {
